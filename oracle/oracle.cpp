@@ -1,0 +1,1335 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of Siddhi's pattern/sequence state engine, used by tests/, by
+// __graft_entry__.smoke() and by bench.py's cpu_baseline leg as the CHECKER. It is never
+// linked into or called by the product path (siddhi_amd/csrc, libsiddhi_gpu.so).
+//
+// It transliterates the reference's object graph rule by rule: partial matches are mutable,
+// reference-counted StateEvent objects shared (aliased) between per-state lists, slots hold
+// StreamEvent chains whose `next` links are shared by shallow clones, exactly as in Java.
+// It is built from the *AST* (serialized by siddhi_amd/lowering.py::oracle_image) with its own
+// transliteration of StateInputStreamParser, independent of the flat NFA tables the GPU uses.
+//
+// Reference files followed (C/ = modules/siddhi-core/src/main/java/io/siddhi/core/):
+//   C/util/parser/StateInputStreamParser.java:76-404          -> build_runtime()/parse()
+//   C/util/parser/ExpressionParser.java:1250-1404 (parseVariable) -> resolve_var()
+//   C/query/input/stream/state/StreamPreStateProcessor.java    -> StreamPre
+//   C/query/input/stream/state/StreamPostStateProcessor.java   -> StreamPost
+//   C/query/input/stream/state/CountPre/PostStateProcessor.java -> CountPre/CountPost
+//   C/query/input/stream/state/LogicalPre/PostStateProcessor.java -> LogicalPre/LogicalPost
+//   C/query/input/stream/state/AbsentStreamPre/PostStateProcessor.java -> AbsentPre/AbsentPost
+//   C/query/input/stream/state/runtime/*InnerStateRuntime.java -> RtNode
+//   C/query/input/{Multi,Single,StateMulti}ProcessStreamReceiver.java, receiver/*.java -> Receiver
+//   C/event/state/StateEvent.java:138-236, StateEventCloner.java:48-60 -> StateEvent, chain ops
+//   C/executor/condition/**  (compare/and/or/not/isnull)       -> eval()
+//   C/util/Scheduler.java:74-214, C/util/timestamp/TimestampGeneratorImpl.java:106-125 -> Clock
+//   C/partition/PartitionRuntime.java:255-308, StreamPreStateProcessor.java:190-200 (clone drops
+//     withinEvery) -> per-key runtimes with is_clone
+//   C/query/selector/QuerySelector.java:125-163, SelectorParser.java:199-233 -> project()
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <cstdio>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+#include <deque>
+#include <algorithm>
+
+namespace orc {
+
+enum AttrType { T_STRING = 0, T_INT = 1, T_LONG = 2, T_FLOAT = 3, T_DOUBLE = 4, T_BOOL = 5 };
+static const int64_t UNKNOWN = -1;
+static const int CURRENT = -1, LAST = -2, ANY = -1;
+enum StateType { PATTERN = 0, SEQUENCE = 1 };
+
+struct Err { std::string msg; };
+[[noreturn]] static void fail(const std::string& m) { throw Err{m}; }
+
+// ------------------------------------------------------------------ values
+struct Val { int type; bool null; int64_t i; double d; };  // i: INT/LONG/STRING id/BOOL ; d: FLOAT/DOUBLE
+static inline Val vnull(int t) { Val v; v.type = t; v.null = true; v.i = 0; v.d = 0; return v; }
+
+// ------------------------------------------------------------------ intrusive refcount
+template <class T> struct Ref {
+  T* p = nullptr;
+  Ref() {}
+  Ref(T* q) : p(q) { if (p) p->rc++; }
+  Ref(const Ref& o) : p(o.p) { if (p) p->rc++; }
+  Ref(Ref&& o) noexcept : p(o.p) { o.p = nullptr; }
+  ~Ref() { release(); }
+  void release() { if (p && --p->rc == 0) T::destroy(p); p = nullptr; }
+  Ref& operator=(const Ref& o) { if (o.p) o.p->rc++; release(); p = o.p; return *this; }
+  Ref& operator=(Ref&& o) noexcept { if (this != &o) { release(); p = o.p; o.p = nullptr; } return *this; }
+  T* operator->() const { return p; }
+  T* get() const { return p; }
+  explicit operator bool() const { return p != nullptr; }
+  bool operator==(const Ref& o) const { return p == o.p; }
+};
+
+// Immutable per-input-event attribute data (the Object[] a StreamEvent copy carries).
+struct EventData {
+  int rc = 0;
+  int64_t ts; uint64_t index; int stream;
+  std::vector<Val> vals;
+  static void destroy(EventData* e) { delete e; }
+};
+
+// StreamEvent: copies share EventData (values are immutable) but each copy has its own
+// `next` (StreamEventCloner.copyStreamEvent creates a fresh event with next == null).
+struct StreamEvent {
+  int rc = 0;
+  Ref<EventData> data;
+  Ref<StreamEvent> next;
+  static void destroy(StreamEvent* e);
+};
+static std::vector<StreamEvent*> g_se_free;
+void StreamEvent::destroy(StreamEvent* e) {
+  // iterative chain release to avoid deep recursion on long chains
+  while (e) {
+    StreamEvent* nx = e->next.p;
+    e->next.p = nullptr;
+    e->data.release();
+    g_se_free.push_back(e);
+    if (nx && --nx->rc == 0) e = nx; else e = nullptr;
+  }
+}
+static StreamEvent* new_se(const Ref<EventData>& d) {
+  StreamEvent* e;
+  if (!g_se_free.empty()) { e = g_se_free.back(); g_se_free.pop_back(); e->rc = 0; }
+  else e = new StreamEvent();
+  e->data = d;
+  return e;
+}
+
+struct StateEvent {
+  int rc = 0;
+  std::vector<Ref<StreamEvent>> slots;
+  int64_t ts = -1;
+  int64_t id = 0;
+  static void destroy(StateEvent* s) { delete s; }
+};
+using SE = Ref<StateEvent>;
+
+// StateEvent.addEvent (StateEvent.java:212-222)
+static void add_event(StateEvent* s, int pos, const Ref<StreamEvent>& e) {
+  if (!s->slots[pos]) { s->slots[pos] = e; return; }
+  StreamEvent* a = s->slots[pos].get();
+  while (a->next) a = a->next.get();
+  a->next = e;
+}
+// StateEvent.removeLastEvent (StateEvent.java:224-236)
+static void remove_last_event(StateEvent* s, int pos) {
+  StreamEvent* a = s->slots[pos].get();
+  if (!a) return;
+  while (a->next) {
+    if (!a->next->next) { a->next = Ref<StreamEvent>(); return; }
+    a = a->next.get();
+  }
+  s->slots[pos] = Ref<StreamEvent>();
+}
+// StateEvent.getStreamEvent(int[] position) (StateEvent.java:138-182)
+static StreamEvent* get_stream_event(StateEvent* s, int chain, int idx) {
+  StreamEvent* e = s->slots[chain].get();
+  if (!e) return nullptr;
+  if (idx >= 0) {
+    for (int i = 1; i <= idx; i++) { e = e->next.get(); if (!e) return nullptr; }
+  } else if (idx == CURRENT) {
+    while (e->next) e = e->next.get();
+  } else if (idx == LAST) {
+    if (!e->next) return nullptr;
+    while (e->next->next) e = e->next.get();
+  } else {
+    std::vector<StreamEvent*> v;
+    while (e) { v.push_back(e); e = e->next.get(); }
+    long index = (long)v.size() + idx;
+    if (index < 0) return nullptr;
+    e = v[index];
+  }
+  return e;
+}
+
+// ------------------------------------------------------------------ app description (from image)
+struct StreamDef { std::vector<int> types; std::vector<int> names; int name_id; };
+
+enum ElemKind { E_STREAM = 1, E_ABSENT = 2, E_NEXT = 3, E_EVERY = 4, E_LOGICAL = 5, E_COUNT = 6 };
+enum ExprKind { X_CONST = 10, X_VAR = 11, X_CMP = 12, X_AND = 13, X_OR = 14, X_NOT = 15, X_ISNULL = 16, X_MATH = 17 };
+
+struct Expr {
+  int kind = 0;
+  int op = 0;
+  Val cval;
+  int ref = -1, has_index = 0, index = 0, attr = -1;  // VAR (unresolved)
+  // resolved variable position
+  int chain = -1, in_chain = 0, attr_idx = -1, vtype = 0;
+  std::unique_ptr<Expr> l, r;
+};
+
+struct Elem {
+  int kind = 0;
+  int stream = -1, ref = -1;
+  std::vector<std::unique_ptr<Expr>> filters;
+  int64_t waiting = -1;
+  int logical = 0;  // 0 AND 1 OR
+  int min = 0, max = 0;
+  std::unique_ptr<Elem> a, b;
+};
+
+struct App {
+  int type = PATTERN;
+  int64_t within = -1;
+  bool playback = false, partitioned = false;
+  std::vector<StreamDef> streams;
+  std::vector<int> key_attr;  // per stream
+  std::unique_ptr<Elem> root;
+  std::vector<std::unique_ptr<Expr>> select;
+};
+
+struct Reader {
+  const int64_t* p; int64_t n; int64_t i = 0;
+  int64_t next() { if (i >= n) fail("image truncated"); return p[i++]; }
+};
+
+static std::unique_ptr<Expr> read_expr(Reader& r) {
+  auto e = std::make_unique<Expr>();
+  e->kind = (int)r.next();
+  switch (e->kind) {
+    case X_CONST: {
+      int t = (int)r.next(); int64_t bits = r.next();
+      e->cval.type = t; e->cval.null = false; e->cval.i = 0; e->cval.d = 0;
+      if (t == T_FLOAT) { float f; uint32_t u = (uint32_t)bits; memcpy(&f, &u, 4); e->cval.d = f; }
+      else if (t == T_DOUBLE) { double d; memcpy(&d, &bits, 8); e->cval.d = d; }
+      else e->cval.i = bits;
+      break;
+    }
+    case X_VAR:
+      e->ref = (int)r.next(); e->has_index = (int)r.next(); e->index = (int)r.next(); e->attr = (int)r.next();
+      break;
+    case X_CMP: e->op = (int)r.next(); e->l = read_expr(r); e->r = read_expr(r); break;
+    case X_AND: case X_OR: e->l = read_expr(r); e->r = read_expr(r); break;
+    case X_NOT: case X_ISNULL: e->l = read_expr(r); break;
+    case X_MATH: fail("arithmetic expressions are not supported by the oracle");
+    default: fail("bad expr kind");
+  }
+  return e;
+}
+
+static std::unique_ptr<Elem> read_elem(Reader& r) {
+  auto e = std::make_unique<Elem>();
+  e->kind = (int)r.next();
+  switch (e->kind) {
+    case E_STREAM: case E_ABSENT: {
+      e->stream = (int)r.next(); e->ref = (int)r.next();
+      int nf = (int)r.next();
+      for (int i = 0; i < nf; i++) e->filters.push_back(read_expr(r));
+      if (e->kind == E_ABSENT) e->waiting = r.next();
+      break;
+    }
+    case E_NEXT: e->a = read_elem(r); e->b = read_elem(r); break;
+    case E_EVERY: e->a = read_elem(r); break;
+    case E_LOGICAL: e->logical = (int)r.next(); e->a = read_elem(r); e->b = read_elem(r); break;
+    case E_COUNT: e->min = (int)r.next(); e->max = (int)r.next(); e->a = read_elem(r); break;
+    default: fail("bad element kind");
+  }
+  return e;
+}
+
+static App read_app(const int64_t* img, int64_t n) {
+  Reader r{img, n};
+  App a;
+  if (r.next() != 0x5344484931LL) fail("bad image magic");
+  a.type = (int)r.next();
+  a.within = r.next();
+  a.playback = r.next() != 0;
+  a.partitioned = r.next() != 0;
+  int ns = (int)r.next();
+  a.streams.resize(ns);
+  for (int s = 0; s < ns; s++) {
+    a.streams[s].name_id = (int)r.next();
+    int na = (int)r.next();
+    for (int k = 0; k < na; k++) { a.streams[s].types.push_back((int)r.next()); a.streams[s].names.push_back((int)r.next()); }
+  }
+  for (int s = 0; s < ns; s++) a.key_attr.push_back((int)r.next());
+  a.root = read_elem(r);
+  int nsel = (int)r.next();
+  for (int i = 0; i < nsel; i++) a.select.push_back(read_expr(r));
+  return a;
+}
+
+// ------------------------------------------------------------------ engine-wide context
+struct Output {
+  uint64_t trigger; int64_t ts; int32_t key; uint32_t group;
+  std::vector<Val> vals;
+};
+
+struct Engine;
+struct KeyRuntime;
+struct PostBase;
+
+// Meta state per state index (MetaStateEvent: stream + reference id)
+struct MetaState { int stream; int ref; };
+
+// ------------------------------------------------------------------ predicate evaluation
+// CompareConditionExpressionExecutor.java:39-43 (null -> false), NotEqual...java:37 (null -> true),
+// typed compare executors (Java numeric promotion; == / != on Float-Long via double).
+static int promote_order(int a, int b) {  // binary numeric promotion for > >= < <=
+  if (a == T_DOUBLE || b == T_DOUBLE) return T_DOUBLE;
+  if (a == T_FLOAT || b == T_FLOAT) return T_FLOAT;
+  if (a == T_LONG || b == T_LONG) return T_LONG;
+  return T_INT;
+}
+static int promote_eq(int a, int b) {     // Equal/NotEqual executors (equal/*.java)
+  if (a == T_DOUBLE || b == T_DOUBLE) return T_DOUBLE;
+  if ((a == T_FLOAT && b == T_LONG) || (a == T_LONG && b == T_FLOAT)) return T_DOUBLE;
+  if (a == T_FLOAT || b == T_FLOAT) return T_FLOAT;
+  if (a == T_LONG || b == T_LONG) return T_LONG;
+  return T_INT;
+}
+static bool cmp_num(int op, const Val& l, const Val& r, int pt) {
+  if (pt == T_DOUBLE || pt == T_FLOAT) {
+    double a, b;
+    auto cv = [&](const Val& v) -> double {
+      if (v.type == T_FLOAT || v.type == T_DOUBLE) return v.d;
+      return (double)v.i;
+    };
+    if (pt == T_FLOAT) {
+      float fa = (l.type == T_FLOAT) ? (float)l.d : (float)l.i;
+      float fb = (r.type == T_FLOAT) ? (float)r.d : (float)r.i;
+      a = fa; b = fb;
+    } else { a = cv(l); b = cv(r); }
+    switch (op) {
+      case 0: return a == b; case 1: return a != b; case 2: return a > b;
+      case 3: return a >= b; case 4: return a < b; default: return a <= b;
+    }
+  }
+  int64_t a = l.i, b = r.i;
+  switch (op) {
+    case 0: return a == b; case 1: return a != b; case 2: return a > b;
+    case 3: return a >= b; case 4: return a < b; default: return a <= b;
+  }
+}
+
+static Val eval(const Expr* x, StateEvent* s);
+
+static Val read_var(const Expr* x, StateEvent* s) {
+  StreamEvent* e = get_stream_event(s, x->chain, x->in_chain);
+  if (!e) return vnull(x->vtype);
+  return e->data->vals[x->attr_idx];
+}
+
+// tri-state boolean: 0 false, 1 true, 2 null
+static int truth(const Val& v) { if (v.null) return 2; return v.i ? 1 : 0; }
+static Val vbool(bool b) { Val v; v.type = T_BOOL; v.null = false; v.i = b; v.d = 0; return v; }
+
+static Val eval(const Expr* x, StateEvent* s) {
+  switch (x->kind) {
+    case X_CONST: return x->cval;
+    case X_VAR: return read_var(x, s);
+    case X_CMP: {
+      Val l = eval(x->l.get(), s), r = eval(x->r.get(), s);
+      if (x->op == 1) {  // !=
+        if (l.null || r.null) return vbool(true);
+      } else if (l.null || r.null) return vbool(false);
+      if (l.type == T_STRING || l.type == T_BOOL) return vbool(x->op == 0 ? l.i == r.i : l.i != r.i);
+      int pt = (x->op <= 1) ? promote_eq(l.type, r.type) : promote_order(l.type, r.type);
+      return vbool(cmp_num(x->op, l, r, pt));
+    }
+    case X_AND: {  // AndConditionExpressionExecutor.java:66-75
+      if (truth(eval(x->l.get(), s)) != 1) return vbool(false);
+      return vbool(truth(eval(x->r.get(), s)) == 1);
+    }
+    case X_OR: {   // OrConditionExpressionExecutor.java:65-75
+      if (truth(eval(x->l.get(), s)) == 1) return vbool(true);
+      return vbool(truth(eval(x->r.get(), s)) == 1);
+    }
+    case X_NOT: return vbool(truth(eval(x->l.get(), s)) != 1);  // NotCondition...java:43-49
+    case X_ISNULL: return vbool(eval(x->l.get(), s).null);
+  }
+  fail("eval: bad expr");
+}
+
+// ------------------------------------------------------------------ processors
+struct PreBase;
+struct List {
+  std::vector<SE> v;
+  int iterating = 0;   // CME detection (Java LinkedList iterators throw on concurrent modification)
+  void add(const SE& s) { v.push_back(s); if (iterating) fail("ConcurrentModification of a pending list"); }
+  void clear() { v.clear(); }
+  bool empty() const { return v.empty(); }
+  size_t size() const { return v.size(); }
+};
+
+struct Scheduler;
+
+struct PostBase {
+  int stateId = 0;
+  PreBase* nextStatePre = nullptr;
+  PreBase* nextEveryStatePre = nullptr;
+  PreBase* thisStatePre = nullptr;
+  bool hasSelector = false;          // nextProcessor != null (QuerySelector)
+  PreBase* callbackPre = nullptr;    // CountPreStateProcessor
+  bool isEventReturned = false;
+  virtual ~PostBase() {}
+  virtual void process(const SE& s);
+  virtual void setNextStatePre(PreBase* p) { nextStatePre = p; }
+  virtual void setNextEveryStatePre(PreBase* p) { nextEveryStatePre = p; }
+};
+
+enum PreKind { P_STREAM, P_COUNT, P_LOGICAL, P_ABSENT };
+
+struct PreBase {
+  KeyRuntime* rt = nullptr;
+  PreKind kind = P_STREAM;
+  int stateId = 0;
+  bool isStartState = false;
+  bool stateChanged = false;
+  int stateType = PATTERN;
+  int64_t withinTime = UNKNOWN;
+  std::vector<int> startStateIds;
+  PreBase* withinEvery = nullptr;
+  PostBase* thisStatePost = nullptr;
+  PostBase* thisLastPost = nullptr;
+  const std::vector<std::unique_ptr<Expr>>* filters = nullptr;
+  List pending, newAndEvery;
+  bool initialized = false;
+  virtual ~PreBase() {}
+
+  bool isExpired(StateEvent* s, int64_t ts) {   // StreamPreStateProcessor.java:102-113
+    if (!isStartState && withinTime != UNKNOWN) {
+      for (int id : startStateIds) {
+        StreamEvent* e = s->slots[id].get();
+        if (e && std::llabs(e->data->ts - ts) > withinTime) return true;
+      }
+    }
+    return false;
+  }
+  // process(StateEvent) :115-121 -> FilterProcessor chain -> Post
+  void process(const SE& s) {
+    stateChanged = false;
+    for (auto& f : *filters) {
+      if (truth(eval(f.get(), s.get())) != 1) return;
+    }
+    thisStatePost->process(s);
+  }
+  virtual void init();
+  virtual void addState(const SE& s) {           // :203-216
+    if (stateType == SEQUENCE) { if (newAndEvery.empty()) newAndEvery.add(s); }
+    else newAndEvery.add(s);
+  }
+  virtual void addEveryState(const SE& s);       // :219-227
+  virtual void resetState();                     // :262-278
+  virtual void updateState() {                   // :281-289
+    for (auto& x : newAndEvery.v) pending.add(x);
+    newAndEvery.clear();
+  }
+  virtual void processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret);
+  virtual bool removeOnNoStateChange() { return stateType == SEQUENCE; }
+};
+
+struct CountPre : PreBase {
+  int minCount = 0, maxCount = 0;
+  bool successCondition = false;
+  bool startStateResetFlag = false;
+  struct CountPost* countPost = nullptr;
+  int depth = 0;
+  void processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) override;
+  void addState(const SE& s) override;
+  void startStateReset();
+  void updateState() override {
+    if (startStateResetFlag) { startStateResetFlag = false; init(); }
+    PreBase::updateState();
+  }
+};
+
+struct CountPost : PostBase {
+  int minCount = 0, maxCount = 0;
+  void process(const SE& s) override;
+  void processMinCountReached(const SE& s);
+  void setNextStatePre(PreBase* p) override;
+};
+
+struct LogicalPre : PreBase {
+  int logicalType = 0;  // 0 AND 1 OR
+  LogicalPre* partner = nullptr;
+  void addState(const SE& s) override;
+  void addEveryState(const SE& s) override;
+  void resetState() override;
+  void updateState() override;
+  void processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) override;
+};
+
+struct LogicalPost : PostBase {
+  int type = 0;
+  LogicalPre* partnerPre = nullptr;
+  LogicalPost* partnerPost = nullptr;
+  void process(const SE& s) override;
+  void setNextStatePre(PreBase* p) override { nextStatePre = p; partnerPost->nextStatePre = p; }
+  void setNextEveryStatePre(PreBase* p) override { nextEveryStatePre = p; partnerPost->nextEveryStatePre = p; }
+};
+
+struct AbsentPre : PreBase {
+  Scheduler* scheduler = nullptr;
+  int64_t waitingTime = -1;
+  int64_t lastScheduledTime = 0;
+  bool active = true;
+  void updateLastArrivalTime(int64_t ts);
+  void addState(const SE& s) override;
+  void addEveryState(const SE& s) override;
+  void resetState() override;
+  void processTimer(int64_t currentTime);
+  void sendEvent(const SE& s);
+  void processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) override;
+  bool removeOnNoStateChange() override { return false; }
+  void start();
+};
+
+struct AbsentPost : PostBase {
+  void process(const SE& s) override;
+};
+
+// Inner state runtimes (runtime/*InnerStateRuntime.java)
+struct Receiver;
+struct RtNode {
+  int kind;                  // E_STREAM/E_NEXT/E_EVERY/E_LOGICAL/E_COUNT (absent is E_STREAM here)
+  PreBase* first = nullptr;
+  PostBase* last = nullptr;
+  RtNode* a = nullptr; RtNode* b = nullptr;
+  int stream = -1;           // Stream node
+};
+
+struct Receiver {
+  int stream = -1;
+  bool multi = false;
+  int stateType = PATTERN;
+  std::vector<PreBase*> nextProcessors;   // filled in setNext order (init order)
+  std::vector<PreBase*> stateProcessors;  // addStatefulProcessor order
+  std::vector<int> eventSequence;
+  bool selector = false;                  // querySelector != null
+};
+
+// Scheduler (C/util/Scheduler.java): FIFO toNotifyQueue, listener on the app clock
+struct Scheduler {
+  std::deque<int64_t> q;
+  AbsentPre* target = nullptr;
+  KeyRuntime* rt = nullptr;
+  uint32_t order = 0;
+};
+
+struct KeyRuntime {
+  Engine* eng = nullptr;
+  int32_t key = 0;
+  bool is_clone = false;
+  std::vector<std::unique_ptr<PreBase>> pres;     // by stateId
+  std::vector<std::unique_ptr<PostBase>> posts;   // by stateId
+  std::vector<std::unique_ptr<RtNode>> nodes;
+  RtNode* root = nullptr;
+  std::vector<Receiver> receivers;                // by stream index (multi/single or none)
+  std::vector<int8_t> has_receiver;
+  std::vector<std::unique_ptr<Scheduler>> schedulers;
+  // output context while processing an input event
+  uint64_t cur_trigger = 0;
+  int cur_phase = 1;
+  uint32_t cur_group = 0;
+  void emit(const SE& s);
+  void resetAndUpdate() { reset(root); update(root); }
+  void reset(RtNode* n);
+  void update(RtNode* n);
+};
+
+struct Engine {
+  App app;
+  std::vector<MetaState> meta;     // per state index
+  int nstates = 0;
+  std::unordered_map<int32_t, std::unique_ptr<KeyRuntime>> keys;
+  std::vector<KeyRuntime*> key_order;
+  std::unique_ptr<KeyRuntime> single;
+  // clock: TimestampGeneratorImpl (listeners in registration order)
+  int64_t lastEventTimestamp = 0;
+  std::vector<Scheduler*> listeners;
+  std::vector<Output> out;
+  int64_t next_id = 0;
+  std::string error;
+  // select resolution
+  std::vector<int> sel_chain, sel_idx, sel_attr, sel_type;
+  uint64_t stats_partials = 0;
+  void setCurrentTimestamp(int64_t ts, uint64_t trigger);
+};
+
+// ---- PostBase::process  (StreamPostStateProcessor.java:53-72)
+void PostBase::process(const SE& s) {
+  thisStatePre->stateChanged = true;
+  StreamEvent* e = s->slots[stateId].get();
+  s->ts = e->data->ts;
+  if (hasSelector) isEventReturned = true;
+  if (nextStatePre) nextStatePre->addState(s);
+  if (nextEveryStatePre) nextEveryStatePre->addEveryState(s);
+  if (callbackPre) static_cast<CountPre*>(callbackPre)->startStateReset();
+}
+
+// ---- StreamPre
+static SE clone_state(const SE& s) {  // StateEventCloner.copyStateEvent
+  StateEvent* c = new StateEvent();
+  c->slots = s->slots;
+  c->ts = s->ts;
+  c->id = s->id;
+  return SE(c);
+}
+
+void PreBase::addEveryState(const SE& s) { newAndEvery.add(clone_state(s)); }
+
+void PreBase::init() {  // StreamPreStateProcessor.java:157-166
+  if (isStartState && (!initialized || thisStatePost->nextEveryStatePre != nullptr ||
+                       (stateType == SEQUENCE && thisStatePost->nextStatePre &&
+                        thisStatePost->nextStatePre->kind == P_ABSENT))) {
+    StateEvent* s = new StateEvent();
+    s->slots.resize(rt->eng->nstates);
+    s->id = ++rt->eng->next_id;
+    addState(SE(s));
+    initialized = true;
+  }
+}
+
+void PreBase::resetState() {  // :262-278
+  pending.clear();
+  if (isStartState && newAndEvery.empty()) {
+    if (stateType == SEQUENCE && thisStatePost->nextEveryStatePre == nullptr) {
+      PreBase* n = thisStatePost->nextStatePre;
+      if (!n) fail("NullPointerException in resetState (reference behaviour)");
+      if (!n->pending.empty()) return;
+    }
+    init();
+  }
+}
+
+void PreBase::processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) {  // :292-337
+  auto& v = pending.v;
+  pending.iterating++;
+  size_t w = 0;
+  for (size_t r = 0; r < v.size(); r++) {
+    SE s = v[r];
+    bool remove = false;
+    if (isExpired(s.get(), ev->ts)) {
+      remove = true;
+      if (withinEvery) {
+        pending.iterating--;
+        withinEvery->addEveryState(s);
+        withinEvery->updateState();
+        pending.iterating++;
+      }
+    } else {
+      s->slots[stateId] = Ref<StreamEvent>(new_se(ev));
+      process(s);
+      if (thisLastPost->isEventReturned) { thisLastPost->isEventReturned = false; ret.push_back(s); }
+      if (stateChanged) remove = true;
+      else {
+        s->slots[stateId] = Ref<StreamEvent>();
+        if (stateType == SEQUENCE) {
+          if (removeOnNoStateChange()) remove = true;
+          if (thisStatePost->callbackPre) static_cast<CountPre*>(thisStatePost->callbackPre)->startStateReset();
+        }
+      }
+    }
+    if (!remove) v[w++] = s;
+  }
+  v.resize(w);
+  pending.iterating--;
+}
+
+// ---- CountPre (CountPreStateProcessor.java:53-156)
+void CountPre::processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) {
+  auto& v = pending.v;
+  pending.iterating++;
+  size_t w = 0;
+  int ns = rt->eng->nstates;
+  for (size_t r = 0; r < v.size(); r++) {
+    SE s = v[r];
+    bool remove = false;
+    // removeIfNextStateProcessed(stateId + 1), (stateId + 2)
+    if ((ns > stateId + 1 && s->slots[stateId + 1]) || (ns > stateId + 2 && s->slots[stateId + 2])) {
+      continue;  // removed
+    }
+    add_event(s.get(), stateId, Ref<StreamEvent>(new_se(ev)));
+    successCondition = false;
+    process(s);
+    if (thisLastPost->isEventReturned) { thisLastPost->isEventReturned = false; ret.push_back(s); }
+    if (stateChanged) remove = true;
+    if (!successCondition) {
+      remove_last_event(s.get(), stateId);
+      if (stateType == SEQUENCE) remove = true;
+    }
+    if (!remove) v[w++] = s;
+  }
+  v.resize(w);
+  pending.iterating--;
+}
+
+void CountPre::addState(const SE& s) {  // :109-132
+  if (stateType == SEQUENCE) { if (newAndEvery.empty()) newAndEvery.add(s); }
+  else newAndEvery.add(s);
+  if (minCount == 0 && !s->slots[stateId]) countPost->processMinCountReached(s);
+}
+
+void CountPre::startStateReset() {  // :142-147
+  if (++depth > 64) fail("StackOverflowError in CountPreStateProcessor.startStateReset (reference behaviour)");
+  startStateResetFlag = true;
+  if (thisStatePost->callbackPre) static_cast<CountPre*>(countPost->thisStatePre)->startStateReset();
+  depth--;
+}
+
+// ---- CountPost (CountPostStateProcessor.java:45-95)
+void CountPost::process(const SE& s) {
+  StreamEvent* e = s->slots[stateId].get();
+  int n = 1;
+  while (e->next) { n++; e = e->next.get(); }
+  static_cast<CountPre*>(thisStatePre)->successCondition = true;
+  s->ts = e->data->ts;
+  if (n >= minCount) {
+    if (thisStatePre->stateType == SEQUENCE) {
+      if (nextStatePre) nextStatePre->addState(s);
+      if (n != maxCount) thisStatePre->addState(s);
+    } else if (n == minCount) {
+      processMinCountReached(s);
+    }
+    if (n == maxCount) thisStatePre->stateChanged = true;
+  }
+}
+void CountPost::processMinCountReached(const SE& s) {
+  if (hasSelector) { thisStatePre->stateChanged = true; isEventReturned = true; }
+  if (nextStatePre) nextStatePre->addState(s);
+  if (nextEveryStatePre) nextEveryStatePre->addEveryState(s);
+}
+void CountPost::setNextStatePre(PreBase* p) {
+  nextStatePre = p;
+  if (thisStatePre->isStartState && thisStatePre->stateType == SEQUENCE && minCount == 0)
+    p->thisStatePost->callbackPre = thisStatePre;
+}
+
+// ---- LogicalPre (LogicalPreStateProcessor.java:56-183)
+void LogicalPre::addState(const SE& s) {
+  if (isStartState || stateType == SEQUENCE) {
+    if (newAndEvery.empty()) newAndEvery.add(s);
+    if (partner && partner->newAndEvery.empty()) partner->newAndEvery.add(s);
+  } else {
+    newAndEvery.add(s);
+    if (partner) partner->newAndEvery.add(s);
+  }
+}
+void LogicalPre::addEveryState(const SE& s) {
+  SE c = clone_state(s);
+  c->slots[stateId] = Ref<StreamEvent>();
+  newAndEvery.add(c);
+  if (partner) { c->slots[partner->stateId] = Ref<StreamEvent>(); partner->newAndEvery.add(c); }
+}
+void LogicalPre::resetState() {
+  if (logicalType == 1 || pending.size() == partner->pending.size()) {
+    pending.clear();
+    partner->pending.clear();
+    if (isStartState && newAndEvery.empty()) {
+      if (stateType == SEQUENCE && thisStatePost->nextEveryStatePre == nullptr) {
+        PreBase* n = thisStatePost->nextStatePre;
+        if (!n) fail("NullPointerException in resetState (reference behaviour)");
+        if (!n->pending.empty()) return;
+      }
+      init();
+    }
+  }
+}
+void LogicalPre::updateState() {
+  for (auto& x : newAndEvery.v) pending.add(x);
+  newAndEvery.clear();
+  for (auto& x : partner->newAndEvery.v) partner->pending.add(x);
+  partner->newAndEvery.clear();
+}
+void LogicalPre::processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) {
+  auto& v = pending.v;
+  pending.iterating++;
+  size_t w = 0;
+  for (size_t r = 0; r < v.size(); r++) {
+    SE s = v[r];
+    bool remove = false;
+    if (isExpired(s.get(), ev->ts)) {
+      remove = true;
+      if (withinEvery) {
+        pending.iterating--;
+        withinEvery->addEveryState(s);
+        withinEvery->updateState();
+        pending.iterating++;
+      }
+    } else if (logicalType == 1 && s->slots[partner->stateId]) {
+      remove = true;
+    } else {
+      s->slots[stateId] = Ref<StreamEvent>(new_se(ev));
+      process(s);
+      if (thisLastPost->isEventReturned) { thisLastPost->isEventReturned = false; ret.push_back(s); }
+      if (stateChanged) remove = true;
+      else {
+        s->slots[stateId] = Ref<StreamEvent>();
+        if (stateType == SEQUENCE) remove = true;
+      }
+    }
+    if (!remove) v[w++] = s;
+  }
+  v.resize(w);
+  pending.iterating--;
+}
+
+// ---- LogicalPost (LogicalPostStateProcessor.java:59-87)
+void LogicalPost::process(const SE& s) {
+  if (type == 0) {  // AND
+    if (partnerPre->kind == P_ABSENT) fail("logical absent patterns are not supported");
+    if (s->slots[partnerPre->stateId]) PostBase::process(s);
+    else thisStatePre->stateChanged = true;
+  } else {          // OR
+    PostBase::process(s);
+    if (partnerPost->hasSelector && thisStatePre->thisLastPost == partnerPost) partnerPost->isEventReturned = true;
+  }
+}
+
+// ---- Absent (AbsentStreamPreStateProcessor.java:69-294, AbsentStreamPostStateProcessor.java:36-56)
+static void notify_at(Scheduler* sc, int64_t t) { sc->q.push_back(t); }
+
+void AbsentPre::updateLastArrivalTime(int64_t ts) {
+  lastScheduledTime = ts + waitingTime;
+  notify_at(scheduler, lastScheduledTime);
+}
+void AbsentPre::addState(const SE& s) {
+  if (!active) return;
+  if (stateType == SEQUENCE) { newAndEvery.clear(); newAndEvery.add(s); }
+  else newAndEvery.add(s);
+  if (!isStartState) {
+    lastScheduledTime = s->ts + waitingTime;
+    notify_at(scheduler, lastScheduledTime);
+  }
+}
+void AbsentPre::addEveryState(const SE& s) {
+  newAndEvery.add(clone_state(s));
+  lastScheduledTime = s->ts + waitingTime;
+  notify_at(scheduler, lastScheduledTime);
+}
+void AbsentPre::resetState() {
+  pending.clear();
+  if (isStartState) {
+    if (stateType == SEQUENCE && thisStatePost->nextEveryStatePre == nullptr) {
+      PreBase* n = thisStatePost->nextStatePre;
+      if (!n) fail("NullPointerException in resetState (reference behaviour)");
+      if (!n->pending.empty()) return;
+    }
+    init();
+  }
+}
+void AbsentPre::processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) {
+  if (!active) return;
+  std::vector<SE> tmp;
+  PreBase::processAndReturn(ev, tmp);  // always returns an empty chunk
+}
+void AbsentPre::sendEvent(const SE& s) {
+  if (thisStatePost->hasSelector) rt->emit(s);
+  if (thisStatePost->nextStatePre) thisStatePost->nextStatePre->addState(s);
+  if (thisStatePost->nextEveryStatePre) thisStatePost->nextEveryStatePre->addEveryState(s);
+  else if (isStartState) active = false;
+  if (thisStatePost->callbackPre) static_cast<CountPre*>(thisStatePost->callbackPre)->startStateReset();
+}
+void AbsentPre::processTimer(int64_t currentTime) {  // process(ComplexEventChunk) :140-210
+  if (!active) return;
+  std::vector<SE> retl;
+  bool initialize = isStartState && newAndEvery.empty() && pending.empty();
+  if (initialize && stateType == SEQUENCE && thisStatePost->nextEveryStatePre == nullptr && lastScheduledTime > 0)
+    initialize = false;
+  if (initialize) {
+    StateEvent* s = new StateEvent();
+    s->slots.resize(rt->eng->nstates);
+    s->id = ++rt->eng->next_id;
+    addState(SE(s));
+  } else if (stateType == SEQUENCE && !newAndEvery.empty()) {
+    resetState();
+  }
+  updateState();
+  auto& v = pending.v;
+  size_t w = 0;
+  std::vector<SE> re_every;
+  for (size_t r = 0; r < v.size(); r++) {
+    SE s = v[r];
+    if (isExpired(s.get(), currentTime)) {
+      if (withinEvery && thisStatePost->nextEveryStatePre != this) re_every.push_back(s);
+      continue;
+    }
+    if ((s->ts == -1 && currentTime >= lastScheduledTime) || (s->ts != -1 && currentTime >= s->ts + waitingTime)) {
+      s->ts = currentTime;
+      retl.push_back(s);
+      continue;
+    }
+    v[w++] = s;
+  }
+  v.resize(w);
+  for (auto& s : re_every) thisStatePost->nextEveryStatePre->addEveryState(s);
+  if (withinEvery) withinEvery->updateState();
+  bool notProcessed = retl.empty();
+  for (auto& s : retl) sendEvent(s);
+  int64_t actual = rt->eng->lastEventTimestamp;
+  if (actual > waitingTime + currentTime) lastScheduledTime = actual + waitingTime;
+  if (notProcessed && lastScheduledTime < currentTime) {
+    lastScheduledTime = currentTime + waitingTime;
+    notify_at(scheduler, lastScheduledTime);
+  }
+}
+void AbsentPre::start() {
+  if (isStartState && waitingTime != -1 && active) {
+    lastScheduledTime = rt->eng->lastEventTimestamp + waitingTime;
+    notify_at(scheduler, lastScheduledTime);
+  }
+}
+void AbsentPost::process(const SE& s) {
+  thisStatePre->stateChanged = true;
+  StreamEvent* e = s->slots[stateId].get();
+  s->ts = e->data->ts;
+  isEventReturned = true;
+  if (thisStatePre->isStartState && nextEveryStatePre && nextEveryStatePre == thisStatePre)
+    nextEveryStatePre->addEveryState(s);
+  static_cast<AbsentPre*>(thisStatePre)->updateLastArrivalTime(e->data->ts);
+}
+
+// ---- runtime reset/update (InnerStateRuntime implementations)
+void KeyRuntime::reset(RtNode* n) {
+  switch (n->kind) {
+    case E_NEXT: reset(n->b); reset(n->a); break;          // NextInnerStateRuntime.java:53-57
+    case E_LOGICAL: reset(n->b); break;                     // LogicalInnerStateRuntime.java:56-59
+    default: n->first->resetState(); break;                 // Stream/Count/Every: firstProcessor.resetState()
+  }
+}
+void KeyRuntime::update(RtNode* n) {
+  switch (n->kind) {
+    case E_NEXT: update(n->a); update(n->b); break;
+    case E_LOGICAL: update(n->b); break;
+    default: n->first->updateState(); break;
+  }
+}
+
+// ---- selector / output (QuerySelector.processNoGroupBy + SelectiveStateEventPopulator)
+void KeyRuntime::emit(const SE& s) {
+  Engine* e = eng;
+  Output o;
+  o.trigger = cur_trigger;
+  o.ts = s->ts;
+  o.key = key;
+  o.group = ((uint32_t)cur_phase << 24) | (cur_group & 0xFFFFFF);
+  for (size_t i = 0; i < e->sel_chain.size(); i++) {
+    StreamEvent* se = get_stream_event(s.get(), e->sel_chain[i], e->sel_idx[i]);
+    if (!se) o.vals.push_back(vnull(e->sel_type[i]));
+    else o.vals.push_back(se->data->vals[e->sel_attr[i]]);
+  }
+  e->out.push_back(std::move(o));
+}
+
+// ------------------------------------------------------------------ build (StateInputStreamParser)
+struct Builder {
+  Engine* eng;
+  KeyRuntime* rt;
+  int counter = 0;                 // stream elements parsed so far (MetaStateEvent size)
+  std::vector<int> stream_count;   // getStreamCount per stream
+  std::vector<PreBase*> allPres;   // preStateProcessors (for within)
+
+  // parseVariable for a filter inside state `cur` (ExpressionParser.java:1250-1404)
+  void resolve(Expr* x, int cur, bool in_select) {
+    if (!x) return;
+    if (x->kind == X_VAR) {
+      int idx_in_chain = in_select ? 0 : CURRENT;
+      if (x->has_index) idx_in_chain = (x->index <= LAST) ? x->index + 1 : x->index;
+      int chain = -1;
+      int limit = in_select ? eng->nstates : cur + 1;
+      if (x->ref < 0) {
+        if (!in_select) chain = cur;
+        else {
+          for (int i = 0; i < limit; i++) {
+            const StreamDef& d = eng->app.streams[eng->meta[i].stream];
+            for (size_t k = 0; k < d.names.size(); k++)
+              if (d.names[k] == x->attr) {
+                if (chain >= 0) fail("ambiguous attribute in select");
+                chain = i;
+              }
+          }
+        }
+      } else {
+        for (int i = 0; i < limit; i++) {
+          const MetaState& m = eng->meta[i];
+          if (m.ref < 0) {
+            if (eng->app.streams[m.stream].name_id == x->ref) { chain = i; break; }
+          } else if (m.ref == x->ref) {
+            chain = i;
+            if (!in_select && cur > -1 && eng->meta[cur].ref >= 0 && x->has_index && x->index <= LAST &&
+                x->ref == eng->meta[cur].ref)
+              idx_in_chain = x->index;
+            break;
+          }
+        }
+      }
+      if (chain < 0) fail("stream reference not found");
+      const StreamDef& d = eng->app.streams[eng->meta[chain].stream];
+      int ai = -1;
+      for (size_t k = 0; k < d.names.size(); k++) if (d.names[k] == x->attr) ai = (int)k;
+      if (ai < 0) fail("attribute not found");
+      x->chain = chain; x->in_chain = idx_in_chain; x->attr_idx = ai; x->vtype = d.types[ai];
+      return;
+    }
+    resolve(x->l.get(), cur, in_select);
+    resolve(x->r.get(), cur, in_select);
+  }
+
+  void count_streams(const Elem* e) {
+    if (!e) return;
+    if (e->kind == E_STREAM || e->kind == E_ABSENT) { stream_count[e->stream]++; return; }
+    count_streams(e->a.get()); count_streams(e->b.get());
+  }
+
+  RtNode* node(int kind) { rt->nodes.emplace_back(new RtNode()); rt->nodes.back()->kind = kind; return rt->nodes.back().get(); }
+
+  Scheduler* new_scheduler(AbsentPre* p) {
+    rt->schedulers.emplace_back(new Scheduler());
+    Scheduler* s = rt->schedulers.back().get();
+    s->target = p; s->rt = rt;
+    eng->listeners.push_back(s);
+    return s;
+  }
+
+  RtNode* parse(Elem* e, PreBase* pre, PostBase* post, std::vector<PreBase*>& pres, bool isStart) {
+    int type = eng->app.type;
+    switch (e->kind) {
+      case E_STREAM: case E_ABSENT: {
+        int stateIndex = counter++;
+        eng->meta[stateIndex] = MetaState{e->stream, e->ref};
+        if (!pre) {
+          if (e->kind == E_ABSENT) {
+            auto* ap = new AbsentPre(); ap->kind = P_ABSENT; ap->waitingTime = e->waiting;
+            if (!rt->is_clone) ap->scheduler = new_scheduler(ap);
+            pre = ap;
+          } else { pre = new PreBase(); pre->kind = P_STREAM; }
+          pre->stateType = type;
+        }
+        pre->rt = rt;
+        pre->stateId = stateIndex;
+        pre->isStartState = isStart;
+        for (auto& f : e->filters) resolve(f.get(), stateIndex, false);
+        pre->filters = &e->filters;
+        if (!post) post = (e->kind == E_ABSENT) ? (PostBase*)new AbsentPost() : new PostBase();
+        post->stateId = stateIndex;
+        post->thisStatePre = pre;
+        pre->thisStatePost = post;
+        pre->thisLastPost = post;
+        rt->pres[stateIndex].reset(pre);
+        rt->posts[stateIndex].reset(post);
+        RtNode* n = node(E_STREAM);
+        n->first = pre; n->last = post; n->stream = e->stream;
+        pres.push_back(pre);
+        return n;
+      }
+      case E_NEXT: {
+        RtNode* cur = parse(e->a.get(), nullptr, nullptr, pres, isStart);
+        RtNode* nxt = parse(e->b.get(), nullptr, nullptr, pres, false);
+        cur->last->setNextStatePre(nxt->first);
+        RtNode* n = node(E_NEXT);
+        n->a = cur; n->b = nxt; n->first = cur->first; n->last = nxt->last;
+        return n;
+      }
+      case E_EVERY: {
+        std::vector<PreBase*> inner;
+        RtNode* in = parse(e->a.get(), nullptr, nullptr, inner, isStart);
+        RtNode* n = node(E_EVERY);
+        n->a = in; n->first = in->first; n->last = in->last;
+        n->last->setNextEveryStatePre(n->first);
+        // withinEveryPreStateProcessor is set by the parser only; clones never get it
+        // (StreamPreStateProcessor.cloneProperties :190-200)
+        if (!rt->is_clone) for (PreBase* p : inner) p->withinEvery = n->first;
+        for (PreBase* p : inner) pres.push_back(p);
+        return n;
+      }
+      case E_LOGICAL: {
+        if (e->a->kind != E_STREAM || e->b->kind != E_STREAM) fail("logical absent patterns are not supported");
+        auto* pre1 = new LogicalPre(); pre1->kind = P_LOGICAL; pre1->logicalType = e->logical; pre1->stateType = type;
+        auto* post1 = new LogicalPost(); post1->type = e->logical;
+        auto* pre2 = new LogicalPre(); pre2->kind = P_LOGICAL; pre2->logicalType = e->logical; pre2->stateType = type;
+        auto* post2 = new LogicalPost(); post2->type = e->logical;
+        post1->partnerPre = pre2; post2->partnerPre = pre1;
+        post1->partnerPost = post2; post2->partnerPost = post1;
+        pre1->partner = pre2; pre2->partner = pre1;
+        RtNode* r2 = parse(e->b.get(), pre2, post2, pres, isStart);   // element2 parsed first (:345-357)
+        RtNode* r1 = parse(e->a.get(), pre1, post1, pres, isStart);
+        RtNode* n = node(E_LOGICAL);
+        n->a = r1; n->b = r2; n->first = r1->first; n->last = r2->last;
+        return n;
+      }
+      case E_COUNT: {
+        int mn = e->min == ANY ? 0 : e->min;
+        int mx = e->max == ANY ? 0x7fffffff : e->max;
+        auto* cp = new CountPre(); cp->kind = P_COUNT; cp->minCount = mn; cp->maxCount = mx; cp->stateType = type;
+        auto* cpost = new CountPost(); cpost->minCount = mn; cpost->maxCount = mx;
+        cp->countPost = cpost;
+        RtNode* in = parse(e->a.get(), cp, cpost, pres, isStart);
+        in->kind = E_COUNT;
+        return in;
+      }
+    }
+    fail("bad element");
+  }
+
+  // setQuerySelector (InnerStateRuntime.setQuerySelector implementations)
+  void set_selector(RtNode* n) {
+    switch (n->kind) {
+      case E_NEXT: set_selector(n->b); break;
+      case E_LOGICAL: set_selector(n->b); set_selector(n->a); break;
+      case E_EVERY: set_selector(n->a); break;
+      default: n->last->hasSelector = true; break;
+    }
+  }
+  // init (StreamInnerStateRuntime.init etc.)
+  void init(RtNode* n) {
+    switch (n->kind) {
+      case E_NEXT: init(n->a); init(n->b); break;
+      case E_LOGICAL: init(n->b); init(n->a); break;
+      case E_EVERY: init(n->a); break;
+      default: {
+        Receiver& r = rt->receivers[n->stream];
+        // receiver.setNext(firstProcessor)
+        r.nextProcessors.push_back(n->first);
+        if (r.multi) r.selector = n->first->thisStatePost->hasSelector;          // StateMulti...:40-44
+        else r.selector = n->first->thisLastPost->hasSelector;                    // SingleProcess...:45-48
+        r.stateProcessors.push_back(n->first);
+        n->first->init();
+        break;
+      }
+    }
+  }
+
+  void build() {
+    Engine* E = eng;
+    int ns = (int)E->app.streams.size();
+    stream_count.assign(ns, 0);
+    count_streams(E->app.root.get());
+    rt->receivers.assign(ns, Receiver());
+    rt->has_receiver.assign(ns, 0);
+    for (int s = 0; s < ns; s++) {
+      if (!stream_count[s]) continue;
+      rt->has_receiver[s] = 1;
+      Receiver& r = rt->receivers[s];
+      r.stream = s; r.multi = stream_count[s] > 1; r.stateType = E->app.type;
+      for (int i = stream_count[s] - 1; i >= 0; i--) r.eventSequence.push_back(i);  // PatternMulti...:38-43
+    }
+    rt->pres.resize(E->nstates);
+    rt->posts.resize(E->nstates);
+    std::vector<PreBase*> pres;
+    RtNode* root = parse(E->app.root.get(), nullptr, nullptr, pres, true);
+    rt->root = root;
+    if (E->app.within != -1) {  // :124-136
+      std::vector<int> ids;
+      for (PreBase* p : pres) if (p->isStartState) ids.push_back(p->stateId);
+      for (PreBase* p : pres) { p->startStateIds = ids; p->withinTime = E->app.within; }
+    }
+    root->first->thisLastPost = root->last;   // :137-138
+    set_selector(root);
+    init(root);
+    if (rt->is_clone) {
+      // clones create their schedulers in runtime clone order (Next: current,next; Logical: 1,2)
+      clone_schedulers(root);
+    }
+  }
+  void clone_schedulers(RtNode* n) {
+    switch (n->kind) {
+      case E_NEXT: clone_schedulers(n->a); clone_schedulers(n->b); break;
+      case E_LOGICAL: clone_schedulers(n->a); clone_schedulers(n->b); break;
+      case E_EVERY: clone_schedulers(n->a); break;
+      default:
+        if (n->first->kind == P_ABSENT) static_cast<AbsentPre*>(n->first)->scheduler = new_scheduler(static_cast<AbsentPre*>(n->first));
+        break;
+    }
+  }
+};
+
+static int count_states(const Elem* e) {
+  if (!e) return 0;
+  if (e->kind == E_STREAM || e->kind == E_ABSENT) return 1;
+  return count_states(e->a.get()) + count_states(e->b.get());
+}
+
+static KeyRuntime* make_runtime(Engine* E, int32_t key, bool clone) {
+  auto* rt = new KeyRuntime();
+  rt->eng = E; rt->key = key; rt->is_clone = clone;
+  Builder b{E, rt};
+  b.build();
+  return rt;
+}
+
+// ------------------------------------------------------------------ clock (playback)
+void Engine::setCurrentTimestamp(int64_t ts, uint64_t trigger) {  // TimestampGeneratorImpl.java:106-125
+  if (ts < lastEventTimestamp) return;
+  lastEventTimestamp = ts;
+  for (size_t li = 0; li < listeners.size(); li++) {
+    Scheduler* sc = listeners[li];
+    if (sc->q.empty() || sc->q.front() > ts) continue;     // Scheduler listener :74-86
+    KeyRuntime* rt = sc->rt;
+    while (!sc->q.empty() && sc->q.front() - lastEventTimestamp <= 0) {   // sendTimerEvents :179-214
+      int64_t t = sc->q.front(); sc->q.pop_front();
+      rt->cur_trigger = trigger; rt->cur_phase = 0; rt->cur_group = (uint32_t)li;
+      sc->target->processTimer(t);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ receivers (per event)
+static void receive(KeyRuntime* rt, int stream, const Ref<EventData>& ev, uint64_t trigger) {
+  Receiver& r = rt->receivers[stream];
+  rt->cur_trigger = trigger; rt->cur_phase = 1;
+  if (r.multi) {
+    // stabilizeStates: PatternMulti -> updateState on every registered pre; SequenceMulti -> resetAndUpdate
+    if (r.stateType == PATTERN) { for (PreBase* p : r.stateProcessors) p->updateState(); }
+    else rt->resetAndUpdate();
+    for (size_t k = 0; k < r.eventSequence.size(); k++) {
+      int idx = r.eventSequence[k];
+      std::vector<SE> ret;
+      r.nextProcessors[idx]->processAndReturn(ev, ret);
+      if (r.selector) {
+        rt->cur_group = (uint32_t)k;
+        for (auto& s : ret) rt->emit(s);
+      }
+    }
+  } else {
+    if (r.stateType == PATTERN) { if (!r.stateProcessors.empty()) r.stateProcessors[0]->updateState(); }
+    else rt->resetAndUpdate();
+    std::vector<SE> ret;
+    r.nextProcessors[0]->processAndReturn(ev, ret);
+    uint32_t g = 0;
+    for (auto& s : ret) { rt->cur_group = 0x800000u | g++; rt->emit(s); }
+  }
+}
+
+}  // namespace orc
+
+// ================================================================== C API (test-only)
+using namespace orc;
+
+struct OrcHandle {
+  Engine eng;
+  bool started = false;
+};
+
+extern "C" {
+
+OrcHandle* orc_create(const int64_t* image, int64_t n, char* err, int errlen) {
+  try {
+    auto* h = new OrcHandle();
+    h->eng.app = read_app(image, n);
+    h->eng.nstates = count_states(h->eng.app.root.get());
+    h->eng.meta.resize(h->eng.nstates);
+    if (!h->eng.app.partitioned) {
+      h->eng.single.reset(make_runtime(&h->eng, 0, false));
+      // SiddhiAppRuntime.start(): AbsentStreamPreStateProcessor.start() for start-state absence
+      for (auto& p : h->eng.single->pres)
+        if (p->kind == P_ABSENT) static_cast<AbsentPre*>(p.get())->start();
+    } else {
+      // resolve select against a template runtime (metadata only)
+      std::unique_ptr<KeyRuntime> tmpl(make_runtime(&h->eng, -1, true));
+      h->eng.listeners.clear();
+    }
+    // select resolution (SelectorParser: default chain index 0, UNKNOWN_STATE scope)
+    Builder b{&h->eng, nullptr};
+    for (auto& x : h->eng.app.select) {
+      if (x->kind != X_VAR) throw Err{"only attribute projections are supported in select"};
+      b.resolve(x.get(), -1, true);
+      h->eng.sel_chain.push_back(x->chain); h->eng.sel_idx.push_back(x->in_chain);
+      h->eng.sel_attr.push_back(x->attr_idx); h->eng.sel_type.push_back(x->vtype);
+    }
+    return h;
+  } catch (Err& e) {
+    if (err) snprintf(err, errlen, "%s", e.msg.c_str());
+    return nullptr;
+  }
+}
+
+void orc_destroy(OrcHandle* h) { delete h; }
+
+// cols[c] for c in [0, total attrs): column of (stream, attr) flattened in stream order; rows of other
+// streams are ignored. nulls[c] may be NULL. key: dense partition key id (-1 = null key -> dropped).
+int orc_push(OrcHandle* h, int64_t n, uint64_t base_index, const int64_t* ts, const int32_t* stream,
+             const int32_t* key, const void* const* cols, const uint8_t* const* nulls, char* err, int errlen) {
+  Engine& E = h->eng;
+  try {
+    std::vector<int> col_base(E.app.streams.size());
+    int c = 0;
+    for (size_t s = 0; s < E.app.streams.size(); s++) { col_base[s] = c; c += (int)E.app.streams[s].types.size(); }
+    for (int64_t i = 0; i < n; i++) {
+      uint64_t trig = base_index + (uint64_t)i;
+      int s = stream[i];
+      if (E.app.playback) E.setCurrentTimestamp(ts[i], trig);
+      if (s < 0) continue;  // pure clock advance / unrelated stream
+      const StreamDef& d = E.app.streams[s];
+      KeyRuntime* rt = nullptr;
+      if (!E.app.partitioned) rt = E.single.get();
+      else {
+        int32_t k = key ? key[i] : 0;
+        if (k < 0) continue;
+        auto it = E.keys.find(k);
+        if (it == E.keys.end()) {
+          KeyRuntime* nrt = make_runtime(&E, k, true);
+          E.keys[k].reset(nrt);
+          E.key_order.push_back(nrt);
+          rt = nrt;
+        } else rt = it->second.get();
+      }
+      if (!rt->has_receiver[s]) continue;
+      EventData* ed = new EventData();
+      ed->ts = ts[i]; ed->index = trig; ed->stream = s;
+      ed->vals.resize(d.types.size());
+      for (size_t a = 0; a < d.types.size(); a++) {
+        int cc = col_base[s] + (int)a;
+        Val v; v.type = d.types[a]; v.null = false; v.i = 0; v.d = 0;
+        if (nulls && nulls[cc] && nulls[cc][i]) v.null = true;
+        else switch (d.types[a]) {
+          case T_INT: case T_STRING: case T_BOOL: v.i = ((const int32_t*)cols[cc])[i]; break;
+          case T_LONG: v.i = ((const int64_t*)cols[cc])[i]; break;
+          case T_FLOAT: v.d = ((const float*)cols[cc])[i]; break;
+          case T_DOUBLE: v.d = ((const double*)cols[cc])[i]; break;
+        }
+        ed->vals[a] = v;
+      }
+      Ref<EventData> ev(ed);
+      receive(rt, s, ev, trig);
+    }
+    return 0;
+  } catch (Err& e) {
+    if (err) snprintf(err, errlen, "%s", e.msg.c_str());
+    return -1;
+  }
+}
+
+int orc_advance_time(OrcHandle* h, int64_t now, uint64_t trigger) {
+  if (h->eng.app.playback) h->eng.setCurrentTimestamp(now, trigger);
+  return 0;
+}
+
+int64_t orc_output_count(OrcHandle* h) { return (int64_t)h->eng.out.size(); }
+
+// Copies and clears the pending outputs. vals: n x nsel int64 bit patterns (float as f32 bits,
+// double as f64 bits); vnull: n x nsel bytes.
+int64_t orc_fetch(OrcHandle* h, int64_t cap, uint64_t* trigger, int64_t* ts, int32_t* key, uint32_t* group,
+                  int64_t* vals, uint8_t* vnull) {
+  Engine& E = h->eng;
+  int64_t n = std::min<int64_t>(cap, (int64_t)E.out.size());
+  size_t ns = E.sel_chain.size();
+  for (int64_t i = 0; i < n; i++) {
+    const Output& o = E.out[i];
+    trigger[i] = o.trigger; ts[i] = o.ts; key[i] = o.key; group[i] = o.group;
+    for (size_t k = 0; k < ns; k++) {
+      const Val& v = o.vals[k];
+      int64_t bits = 0;
+      if (!v.null) {
+        if (v.type == T_FLOAT) { float f = (float)v.d; uint32_t u; memcpy(&u, &f, 4); bits = u; }
+        else if (v.type == T_DOUBLE) memcpy(&bits, &v.d, 8);
+        else bits = v.i;
+      }
+      vals[i * ns + k] = bits;
+      vnull[i * ns + k] = v.null ? 1 : 0;
+    }
+  }
+  E.out.erase(E.out.begin(), E.out.begin() + n);
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,8 @@
+"""siddhi_amd — MI355X-native pattern/sequence matcher for Siddhi's CEP state engine.
+
+The product path is the HIP engine in siddhi_amd/csrc behind the C-ABI declared in
+include/siddhi_gpu.h; siddhi_amd.runtime mirrors Siddhi's host API (SiddhiManager,
+SiddhiAppRuntime, InputHandler, QueryCallback, StreamCallback) on top of it.
+"""
+from .runtime import (Event, InputHandler, QueryCallback, SiddhiAppCreationException,  # noqa: F401
+                      SiddhiAppRuntime, SiddhiManager, StreamCallback)

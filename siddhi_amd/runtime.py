@@ -1,0 +1,341 @@
+"""Host-side mirror of Siddhi's app API for the pattern/sequence path.
+
+Mirrors the reference's public surface so parity tests read like the reference's own tests
+(e.g. T/query/pattern/WithinPatternTestCase.java:48-98):
+
+  SiddhiManager.createSiddhiAppRuntime(String)       C/SiddhiManager.java:74-76
+  SiddhiAppRuntime.addCallback / getInputHandler     C/SiddhiAppRuntime.java
+  InputHandler.send(ts, Object[]) / send(Object[])   C/stream/input/InputHandler.java:51-86
+  QueryCallback.receive(ts, inEvents, removeEvents)  C/query/output/callback/QueryCallback.java:52-85
+  StreamCallback.receive(Event[])                    C/stream/output/StreamCallback.java:93
+
+Events are accumulated into columnar (SoA) batches and handed to the matching engine behind the
+C-ABI (include/siddhi_gpu.h) on flush(); matches come back in the reference's delivery order
+(trigger event index, then timer passes before the event's own states, then state visit order).
+Documented semantic change: callbacks fire when a batch is flushed, not inside send().
+
+Partition routing (`partition with (attr of S)`) is done here the way PartitionStreamReceiver does it
+(C/partition/PartitionStreamReceiver.java:162-174,270-275; ValuePartitionExecutor.java:34-40): the key is
+String.valueOf(attr) (null -> event dropped), dictionary-encoded to a dense id in first-seen order, which is
+also the order the reference registers per-key schedulers in (PartitionRuntime.java:255-308).
+"""
+from __future__ import annotations
+
+import math
+import struct
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+from . import compiler as C
+from . import lowering as L
+
+_NP = {"STRING": np.int32, "INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64,
+       "BOOL": np.int32}
+
+
+@dataclass
+class Event:
+    timestamp: int
+    data: list
+
+    def getTimestamp(self):
+        return self.timestamp
+
+    def getData(self, i=None):
+        return self.data if i is None else self.data[i]
+
+    def __repr__(self):
+        return f"Event{{timestamp={self.timestamp}, data={self.data}}}"
+
+
+class QueryCallback:
+    def receive(self, timestamp, inEvents, removeEvents):  # pragma: no cover - user override
+        pass
+
+
+class StreamCallback:
+    def receive(self, events):  # pragma: no cover - user override
+        pass
+
+
+class SiddhiAppCreationException(Exception):
+    pass
+
+
+@dataclass
+class Batch:
+    """One SoA batch in the C-ABI layout (see include/siddhi_gpu.h, sg_batch)."""
+    n: int
+    base_index: int
+    ts: np.ndarray       # int64[n]
+    stream: np.ndarray   # int32[n]   (-1: clock-only event of a stream no query reads)
+    key: np.ndarray      # int32[n]   dense partition key, -1 = null key / not partitioned stream
+    cols: List[np.ndarray]
+    nulls: List[Optional[np.ndarray]]
+
+
+@dataclass
+class Outputs:
+    trigger: np.ndarray
+    ts: np.ndarray
+    key: np.ndarray
+    group: np.ndarray
+    vals: np.ndarray     # int64 [n, nsel] bit patterns
+    vnull: np.ndarray    # uint8 [n, nsel]
+
+    def __len__(self):
+        return len(self.trigger)
+
+
+def _key_string(v, t):
+    """String.valueOf(value) identity for partition keys."""
+    if v is None:
+        return None
+    if t == "FLOAT" or t == "DOUBLE":
+        f = float(v)
+        if math.isnan(f):
+            return "NaN"
+        return ("f" if t == "FLOAT" else "d") + repr(np.float32(f) if t == "FLOAT" else f)
+    if t == "BOOL":
+        return "true" if v else "false"
+    return str(v)
+
+
+class _QueryRuntime:
+    def __init__(self, app_rt: "SiddhiAppRuntime", query: C.Query, partition: Optional[C.Partition],
+                 engine_factory):
+        self.app_rt = app_rt
+        self.query = query
+        self.partition = partition
+        self.ctx = L.make_context(app_rt.app, query, partition, app_rt.strings)
+        self.sel_types = [self._select_type(oa.expr) for oa in query.select]
+        self.engine = engine_factory(self.ctx)
+        self.query_callbacks: List[QueryCallback] = []
+
+    def _select_type(self, e):
+        if not isinstance(e, C.Var):
+            raise SiddhiAppCreationException("only attribute projections are supported in select")
+        # resolve type by reference or attribute name (SelectorParser / parseVariable)
+        elems = []
+
+        def walk(el):
+            if isinstance(el, (C.StreamStateElement, C.AbsentStreamStateElement)):
+                elems.append(el)
+            elif isinstance(el, C.NextStateElement):
+                walk(el.current); walk(el.next)
+            elif isinstance(el, C.EveryStateElement):
+                walk(el.inner)
+            elif isinstance(el, C.LogicalStateElement):
+                walk(el.e2); walk(el.e1)
+            elif isinstance(el, C.CountStateElement):
+                walk(el.inner)
+        walk(self.query.input.element)
+        for el in elems:
+            d = self.app_rt.app.streams[el.stream_id]
+            if e.stream_ref is None or e.stream_ref == el.ref or (el.ref is None and e.stream_ref == el.stream_id):
+                if d.attr_index(e.attr) >= 0:
+                    return d.attr_type(e.attr)
+        raise SiddhiAppCreationException(f"cannot resolve select attribute {e}")
+
+
+class InputHandler:
+    def __init__(self, app_rt: "SiddhiAppRuntime", stream_id: str):
+        self.app_rt = app_rt
+        self.stream_id = stream_id
+        self.stream_index = app_rt.stream_ids.index(stream_id)
+
+    def getStreamId(self):
+        return self.stream_id
+
+    def send(self, a, b=None):
+        """send(Object[]) | send(long ts, Object[]) | send(Event) | send(Event[])."""
+        if b is not None:
+            self.app_rt._append(self.stream_index, int(a), list(b))
+        elif isinstance(a, Event):
+            self.app_rt._append(self.stream_index, int(a.timestamp), list(a.data))
+        elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
+            for ev in a:
+                self.app_rt._append(self.stream_index, int(ev.timestamp), list(ev.data))
+        else:
+            self.app_rt._append(self.stream_index, int(time.time() * 1000), list(a))
+
+
+class SiddhiAppRuntime:
+    def __init__(self, text: str, engine_factory, batch_size: int = 1 << 20):
+        try:
+            self.app = C.parse(text)
+        except C.SiddhiParserException as e:
+            raise SiddhiAppCreationException(str(e)) from e
+        self.stream_ids = list(self.app.streams.keys())
+        self.strings: Dict[str, int] = {}
+        self.string_list: List[str] = []
+        self.queries: List[_QueryRuntime] = []
+        for q in self.app.queries:
+            self.queries.append(_QueryRuntime(self, q, None, engine_factory))
+        for p in self.app.partitions:
+            for q in p.queries:
+                self.queries.append(_QueryRuntime(self, q, p, engine_factory))
+        self.stream_callbacks: Dict[str, List[StreamCallback]] = {}
+        self.key_dicts = [dict() for _ in self.queries]
+        self.batch_size = batch_size
+        self._rows: List[tuple] = []
+        self.next_index = 0
+        self.started = False
+
+    # -- API
+    def getInputHandler(self, stream_id: str) -> InputHandler:
+        if stream_id not in self.app.streams:
+            raise SiddhiAppCreationException(f"stream {stream_id} not defined")
+        return InputHandler(self, stream_id)
+
+    def addCallback(self, name: str, cb):
+        if isinstance(cb, QueryCallback):
+            for q in self.queries:
+                if q.query.name == name:
+                    q.query_callbacks.append(cb)
+                    return
+            raise SiddhiAppCreationException(f"no query named {name}")
+        self.stream_callbacks.setdefault(name, []).append(cb)
+
+    def start(self):
+        self.started = True
+
+    def shutdown(self):
+        self.flush()
+        for q in self.queries:
+            q.engine.close()
+
+    # -- ingestion
+    def _string_id(self, s: str) -> int:
+        i = self.strings.get(s)
+        if i is None:
+            i = len(self.strings)
+            self.strings[s] = i
+        return i
+
+    def _append(self, stream: int, ts: int, data: list):
+        self._rows.append((stream, ts, data))
+        if len(self._rows) >= self.batch_size:
+            self.flush()
+
+    def advance_time(self, now: int):
+        """Playback clock advance without an event (heartbeat)."""
+        self._rows.append((-1, int(now), None))
+
+    def flush(self):
+        rows, self._rows = self._rows, []
+        if not rows:
+            return
+        n = len(rows)
+        base = self.next_index
+        self.next_index += n
+        ts = np.fromiter((r[1] for r in rows), dtype=np.int64, count=n)
+        stream = np.fromiter((r[0] for r in rows), dtype=np.int32, count=n)
+        cols, nulls = [], []
+        for s, sid in enumerate(self.stream_ids):
+            d = self.app.streams[sid]
+            for a, (_, t) in enumerate(d.attrs):
+                col = np.zeros(n, dtype=_NP[t])
+                nul = None
+                for i, r in enumerate(rows):
+                    if r[0] != s:
+                        continue
+                    v = r[2][a]
+                    if v is None:
+                        if nul is None:
+                            nul = np.zeros(n, dtype=np.uint8)
+                        nul[i] = 1
+                        continue
+                    if t == "STRING":
+                        v = self._string_id(v)
+                    elif t == "BOOL":
+                        v = 1 if v else 0
+                    col[i] = v
+                cols.append(col)
+                nulls.append(nul)
+        for qi, q in enumerate(self.queries):
+            key = np.full(n, -1, dtype=np.int32)
+            if q.ctx.partitioned:
+                kd = self.key_dicts[qi]
+                for i, r in enumerate(rows):
+                    s = r[0]
+                    if s < 0 or q.ctx.key_attr[s] < 0:
+                        continue
+                    ai = q.ctx.key_attr[s]
+                    t = self.app.streams[self.stream_ids[s]].attrs[ai][1]
+                    ks = _key_string(r[2][ai], t)
+                    if ks is None:
+                        continue
+                    k = kd.get(ks)
+                    if k is None:
+                        k = len(kd)
+                        kd[ks] = k
+                    key[i] = k
+            else:
+                key[:] = 0
+            b = Batch(n, base, ts, stream, key, cols, nulls)
+            q.engine.push(b)
+            self._deliver(q, q.engine.fetch())
+
+    # -- output
+    def _decode(self, q: _QueryRuntime, vals: np.ndarray, vnull: np.ndarray) -> list:
+        out = []
+        for k, t in enumerate(q.sel_types):
+            if vnull[k]:
+                out.append(None)
+                continue
+            bits = int(vals[k])
+            if t == "FLOAT":
+                out.append(float(np.float32(struct.unpack("<f", struct.pack("<I", bits & 0xFFFFFFFF))[0])))
+            elif t == "DOUBLE":
+                out.append(struct.unpack("<d", struct.pack("<q", bits))[0])
+            elif t == "STRING":
+                if not self.string_list or len(self.string_list) != len(self.strings):
+                    self.string_list = [None] * len(self.strings)
+                    for s, i in self.strings.items():
+                        self.string_list[i] = s
+                out.append(self.string_list[bits])
+            elif t == "BOOL":
+                out.append(bool(bits))
+            else:
+                out.append(bits)
+        return out
+
+    def _deliver(self, q: _QueryRuntime, o: Outputs):
+        if len(o) == 0:
+            return
+        # group consecutive outputs of one (trigger, group) into one callback batch
+        # (MultiProcessStreamReceiver ReturnEventHolder per visited state, :284-307)
+        i = 0
+        n = len(o)
+        while i < n:
+            j = i + 1
+            while j < n and o.trigger[j] == o.trigger[i] and o.group[j] == o.group[i] and o.key[j] == o.key[i]:
+                j += 1
+            events = [Event(int(o.ts[k]), self._decode(q, o.vals[k], o.vnull[k])) for k in range(i, j)]
+            for cb in q.query_callbacks:
+                cb.receive(events[0].timestamp, events, None)
+            for cb in self.stream_callbacks.get(q.query.output_stream, []):
+                cb.receive(events)
+            i = j
+
+
+class SiddhiManager:
+    """C/SiddhiManager.java:61-76.  `engine` selects the matching engine factory; the default is the
+    MI355X engine behind the C-ABI (siddhi_amd._native.GpuEngine)."""
+
+    def __init__(self, engine=None):
+        self.engine = engine
+
+    def createSiddhiAppRuntime(self, text: str) -> SiddhiAppRuntime:
+        factory = self.engine
+        if factory is None:
+            from ._native import GpuEngine
+            factory = GpuEngine
+        return SiddhiAppRuntime(text, factory)
+
+    def shutdown(self):
+        pass
