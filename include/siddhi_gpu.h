@@ -1,0 +1,190 @@
+/*
+ * siddhi_gpu.h — C-ABI of the MI355X pattern/sequence state engine.
+ *
+ * Drop-in boundary for Siddhi's state-engine hot path.  One handle = one HIP device = one
+ * cloned-per-key state query (all partition keys of that query live in the handle).  A handle is
+ * single-threaded (mirrors `synchronized receive`, C/query/input/MultiProcessStreamReceiver.java:103);
+ * handles on different devices may be driven concurrently.
+ *
+ * What each entry point replaces in the reference (C/ = modules/siddhi-core/src/main/java/io/siddhi/core/):
+ *   sg_open          StateInputStreamParser.parseInputStream (C/util/parser/StateInputStreamParser.java:76-141)
+ *                    + QueryRuntime/StateStreamRuntime.setCommonProcessor/init (C/query/input/stream/state/
+ *                    StateStreamRuntime.java:73-76): the lowered NFA (sg_nfa_desc) replaces the Pre/Post
+ *                    processor graph; per-key runtimes are created on first sight of a key
+ *                    (PartitionRuntime.cloneIfNotExist, C/partition/PartitionRuntime.java:255-308).
+ *   sg_push          StreamJunction.Receiver.receive(Event[]) / receive(long, Object[])
+ *                    (C/stream/StreamJunction.java:376-389) as implemented by ProcessStreamReceiver
+ *                    (C/query/input/ProcessStreamReceiver.java:43-223), MultiProcessStreamReceiver
+ *                    (C/query/input/MultiProcessStreamReceiver.java:98-309) and PartitionStreamReceiver
+ *                    (C/partition/PartitionStreamReceiver.java:80-275); InputHandler.send's playback clock
+ *                    (C/stream/input/InputHandler.java:57-65) is applied per row.
+ *   sg_advance_time  TimestampGeneratorImpl.setCurrentTimestamp (C/util/timestamp/TimestampGeneratorImpl.java:106-125)
+ *                    driving Scheduler.sendTimerEvents (C/util/Scheduler.java:179-214) for `not ... for T`.
+ *   sg_poll          QuerySelector.process -> OutputRateLimiter.sendToCallBacks
+ *                    (C/query/selector/QuerySelector.java:76-163, C/query/output/ratelimit/OutputRateLimiter.java:61-100):
+ *                    projected matches in the reference's delivery order.
+ *   sg_close         SiddhiAppRuntime.shutdown for the query's state.
+ * No exceptions cross the ABI: every call returns SG_OK or a negative status; sg_last_error() explains.
+ */
+#ifndef SIDDHI_GPU_H
+#define SIDDHI_GPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_ABI_VERSION 1
+
+#define SG_MAX_STATES 16
+#define SG_MAX_STREAMS 16
+#define SG_MAX_SELECT 32
+#define SG_MAX_RET 16
+#define SG_MAX_COLS 64
+#define SG_MAX_CODE 512
+
+/* status codes */
+#define SG_OK 0
+#define SG_EINVAL -1
+#define SG_EHIP -2
+#define SG_ECAPACITY -3     /* a per-key pool / list capacity (sg_options) was exceeded */
+#define SG_EUNSUPPORTED -4
+#define SG_EORDER -5        /* a closed-form kernel's precondition (non-decreasing ts) failed */
+
+/* state kinds (Pre/Post processor pairs) */
+#define SG_K_STREAM 0       /* StreamPre/PostStateProcessor */
+#define SG_K_COUNT 1        /* CountPre/PostStateProcessor */
+#define SG_K_LOGICAL 2      /* LogicalPre/PostStateProcessor */
+#define SG_K_ABSENT 3       /* AbsentStreamPre/PostStateProcessor */
+
+/* attribute types (Attribute.Type) */
+#define SG_T_STRING 0       /* dictionary id, int32 */
+#define SG_T_INT 1
+#define SG_T_LONG 2
+#define SG_T_FLOAT 3
+#define SG_T_DOUBLE 4
+#define SG_T_BOOL 5         /* int32 0/1 */
+
+/* closed-form shapes recognised at lowering time */
+#define SG_SHAPE_GENERAL 0
+#define SG_SHAPE_EVERY_NEXT_CMP 1    /* every A[l] -> B[l' and B.x OP A.x] within T */
+#define SG_SHAPE_EVERY_ABSENT_EQ 2   /* every A[l] -> not B[l' and B.x == A.x] for T  (playback) */
+
+/* postfix predicate program opcodes; words are int64 */
+#define SG_OP_VAR 1     /* VAR state index_in_chain retained_slot type */
+#define SG_OP_CONST 2   /* CONST type bits */
+#define SG_OP_CMP 3     /* CMP op(0 == 1 != 2 > 3 >= 4 < 5 <=) domain(0 i64 1 f32 2 f64 3 id) */
+#define SG_OP_AND 4
+#define SG_OP_OR 5
+#define SG_OP_NOT 6
+#define SG_OP_ISNULL 7
+
+typedef struct sg_state_desc {
+  int32_t kind, stream, is_start, min_count, max_count, logical_type, partner;
+  int32_t next_state;     /* post.nextStatePreProcessor (-1) */
+  int32_t next_every;     /* post.nextEveryStatePreProcessor (-1) */
+  int32_t within_every;   /* pre.withinEveryPreStateProcessor (-1; never set for partition clones) */
+  int32_t callback;       /* post.callbackPreStateProcessor (count pre) (-1) */
+  int32_t has_selector;   /* post.nextProcessor != null */
+  int32_t this_last;      /* pre.thisLastProcessor = post of this state id */
+  int32_t prog_off, prog_len, local;
+  int64_t waiting_time;   /* absent: `for T` in ms */
+} sg_state_desc;
+
+typedef struct sg_receiver_desc {
+  int32_t stream, multi, selector, n;
+  int32_t pres[SG_MAX_STATES];   /* nextProcessors in setNext (init) order */
+  int32_t stab[SG_MAX_STATES];   /* stateProcessors in addStatefulProcessor order */
+} sg_receiver_desc;
+
+typedef struct sg_nfa_desc {
+  int32_t abi_version;
+  int32_t type;                  /* 0 PATTERN, 1 SEQUENCE */
+  int64_t within;                /* ms, -1 = none */
+  int32_t playback, partitioned;
+  int32_t n_states, n_streams, n_cols, n_ret, n_select;
+  int32_t n_init, n_reset, n_update, n_start;
+  sg_state_desc states[SG_MAX_STATES];
+  int32_t recv_of_stream[SG_MAX_STREAMS];      /* receiver index or -1 */
+  sg_receiver_desc receivers[SG_MAX_STREAMS];
+  int32_t init_order[SG_MAX_STATES];
+  int32_t reset_ops[SG_MAX_STATES];
+  int32_t update_ops[SG_MAX_STATES];
+  int32_t start_ids[SG_MAX_STATES];
+  int32_t col_type[SG_MAX_COLS], col_stream[SG_MAX_COLS];
+  int32_t ret_col[SG_MAX_RET], ret_type[SG_MAX_RET];          /* retained slot -> batch column */
+  int32_t sel_state[SG_MAX_SELECT], sel_index[SG_MAX_SELECT], sel_ret[SG_MAX_SELECT], sel_type[SG_MAX_SELECT];
+  int32_t shape;
+  int32_t shape_args[8];
+  int32_t shape_prog_off, shape_prog_len;
+  int32_t code_len;
+  int64_t code[SG_MAX_CODE];
+} sg_nfa_desc;
+
+typedef struct sg_options {
+  int64_t max_batch;        /* largest n per sg_push the workspaces are sized for (grown on demand) */
+  int32_t pool_partials;    /* general engine: partial-match (StateEvent) pool per key */
+  int32_t pool_events;      /* general engine: retained event copies per key */
+  int32_t pool_chain;       /* general engine: count-chain nodes per key */
+  int32_t list_cap;         /* general engine: capacity of each pending / newAndEvery list */
+  int32_t force_general;    /* 1: ignore closed-form shapes (parity testing of the general kernel) */
+  int32_t reserved[7];
+} sg_options;
+
+/* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)
+ * c of sg_nfa_desc (rows of other streams are ignored).  Host pointers must stay valid until
+ * sg_push returns; device pointers (on_device = 1) must be HBM buffers of the handle's device. */
+typedef struct sg_batch {
+  int64_t n;
+  uint64_t base_index;          /* global event index of row 0 (the reference's send order) */
+  const int64_t* ts;            /* event timestamps (ms) */
+  const int32_t* stream;        /* stream index; -1 = row that only advances the playback clock */
+  const int32_t* key;           /* dense partition key id (first-seen order); -1 = null key (dropped) */
+  const void* const* cols;      /* [n_cols] typed columns (width from col_type) */
+  const uint8_t* const* nulls;  /* [n_cols] optional 1-byte null flags per row, or NULL */
+  int32_t on_device;
+  int32_t key_bound;            /* exclusive upper bound of key ids in this batch (0 = unknown) */
+} sg_batch;
+
+/* Match tuples in delivery order.  vals[i*n_select + k] holds the bit pattern of select column k
+ * (FLOAT: f32 bits, DOUBLE: f64 bits, others sign-extended); bit k of vnull[i] marks a null. */
+typedef struct sg_matches {
+  int64_t n;
+  uint64_t* trigger;            /* global index of the event whose arrival produced the match */
+  int64_t* ts;                  /* output event timestamp (StateEvent.timestamp) */
+  int32_t* key;                 /* dense partition key */
+  uint32_t* group;              /* callback batch: (phase << 24) | receiver visit slot */
+  int64_t* vals;
+  uint32_t* vnull;
+} sg_matches;
+
+typedef struct sg_timing {
+  float pred_ms, partition_ms, match_ms, output_ms, total_ms;   /* HIP-event times of the last push */
+  int64_t events, matches;
+} sg_timing;
+
+typedef struct sg_handle sg_handle;
+
+int sg_open(int hip_device, const sg_nfa_desc* nfa, const sg_options* opt, sg_handle** out);
+int sg_push(sg_handle* h, const sg_batch* b);
+int sg_advance_time(sg_handle* h, int64_t now, uint64_t trigger_index);
+int sg_pending(sg_handle* h, int64_t* n);
+/* Copy up to cap pending matches into host arrays (fields may be NULL to skip) and consume them. */
+int sg_poll(sg_handle* h, sg_matches* out, int64_t cap, int64_t* n);
+/* Zero-copy view of the pending matches in HBM (valid until the next push/poll/reset). */
+int sg_device_matches(sg_handle* h, sg_matches* view);
+int sg_discard(sg_handle* h);           /* drop pending matches without copying */
+int sg_flush(sg_handle* h);             /* wait for all work on the handle's stream */
+int sg_reset(sg_handle* h);             /* forget all per-key state (fresh runtime) */
+int sg_set_stream(sg_handle* h, void* hip_stream);   /* launch on a caller-owned hipStream_t */
+int sg_get_timing(sg_handle* h, sg_timing* t);
+int sg_close(sg_handle* h);
+const char* sg_last_error(const sg_handle* h);
+const char* sg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIDDHI_GPU_H */

@@ -1,0 +1,299 @@
+"""ctypes binding of libsiddhi_gpu.so (the C-ABI in include/siddhi_gpu.h) and the GpuEngine that
+siddhi_amd.runtime drives.  The library is built in-tree (siddhi_amd/csrc/Makefile); there is no CPU
+fallback: if the library or a GPU is missing the engine raises."""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+import numpy as np
+
+from . import lowering as L
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsiddhi_gpu.so")
+
+SG_MAX_STATES, SG_MAX_STREAMS, SG_MAX_SELECT, SG_MAX_RET, SG_MAX_COLS, SG_MAX_CODE = 16, 16, 32, 16, 64, 512
+SG_ABI_VERSION = 1
+
+SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_matches", "sg_discard",
+           "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version"]
+
+I32, I64, U64 = ct.c_int32, ct.c_int64, ct.c_uint64
+
+
+class sg_state_desc(ct.Structure):
+    _fields_ = [(n, I32) for n in ("kind", "stream", "is_start", "min_count", "max_count", "logical_type",
+                                   "partner", "next_state", "next_every", "within_every", "callback",
+                                   "has_selector", "this_last", "prog_off", "prog_len", "local")] + \
+               [("waiting_time", I64)]
+
+
+class sg_receiver_desc(ct.Structure):
+    _fields_ = [("stream", I32), ("multi", I32), ("selector", I32), ("n", I32),
+                ("pres", I32 * SG_MAX_STATES), ("stab", I32 * SG_MAX_STATES)]
+
+
+class sg_nfa_desc(ct.Structure):
+    _fields_ = [("abi_version", I32), ("type", I32), ("within", I64), ("playback", I32), ("partitioned", I32),
+                ("n_states", I32), ("n_streams", I32), ("n_cols", I32), ("n_ret", I32), ("n_select", I32),
+                ("n_init", I32), ("n_reset", I32), ("n_update", I32), ("n_start", I32),
+                ("states", sg_state_desc * SG_MAX_STATES),
+                ("recv_of_stream", I32 * SG_MAX_STREAMS),
+                ("receivers", sg_receiver_desc * SG_MAX_STREAMS),
+                ("init_order", I32 * SG_MAX_STATES), ("reset_ops", I32 * SG_MAX_STATES),
+                ("update_ops", I32 * SG_MAX_STATES), ("start_ids", I32 * SG_MAX_STATES),
+                ("col_type", I32 * SG_MAX_COLS), ("col_stream", I32 * SG_MAX_COLS),
+                ("ret_col", I32 * SG_MAX_RET), ("ret_type", I32 * SG_MAX_RET),
+                ("sel_state", I32 * SG_MAX_SELECT), ("sel_index", I32 * SG_MAX_SELECT),
+                ("sel_ret", I32 * SG_MAX_SELECT), ("sel_type", I32 * SG_MAX_SELECT),
+                ("shape", I32), ("shape_args", I32 * 8), ("shape_prog_off", I32), ("shape_prog_len", I32),
+                ("code_len", I32), ("code", I64 * SG_MAX_CODE)]
+
+
+class sg_options(ct.Structure):
+    _fields_ = [("max_batch", I64), ("pool_partials", I32), ("pool_events", I32), ("pool_chain", I32),
+                ("list_cap", I32), ("force_general", I32), ("reserved", I32 * 7)]
+
+
+class sg_batch(ct.Structure):
+    _fields_ = [("n", I64), ("base_index", U64), ("ts", ct.c_void_p), ("stream", ct.c_void_p),
+                ("key", ct.c_void_p), ("cols", ct.c_void_p), ("nulls", ct.c_void_p),
+                ("on_device", I32), ("key_bound", I32)]
+
+
+class sg_matches(ct.Structure):
+    _fields_ = [("n", I64), ("trigger", ct.c_void_p), ("ts", ct.c_void_p), ("key", ct.c_void_p),
+                ("group", ct.c_void_p), ("vals", ct.c_void_p), ("vnull", ct.c_void_p)]
+
+
+class sg_timing(ct.Structure):
+    _fields_ = [("pred_ms", ct.c_float), ("partition_ms", ct.c_float), ("match_ms", ct.c_float),
+                ("output_ms", ct.c_float), ("total_ms", ct.c_float), ("events", I64), ("matches", I64)]
+
+
+_lib = None
+
+
+class SgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"siddhi_gpu error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libsiddhi_gpu.so; raises if it is not built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise RuntimeError(f"libsiddhi_gpu.so not built at {path}: run `make -C siddhi_amd/csrc` "
+                               "or __graft_entry__.build()")
+        lib = ct.CDLL(path)
+        P = ct.c_void_p
+        lib.sg_open.argtypes = [ct.c_int, P, P, ct.POINTER(P)]
+        lib.sg_push.argtypes = [P, P]
+        lib.sg_advance_time.argtypes = [P, I64, U64]
+        lib.sg_pending.argtypes = [P, ct.POINTER(I64)]
+        lib.sg_poll.argtypes = [P, P, I64, ct.POINTER(I64)]
+        lib.sg_device_matches.argtypes = [P, P]
+        lib.sg_discard.argtypes = [P]
+        lib.sg_flush.argtypes = [P]
+        lib.sg_reset.argtypes = [P]
+        lib.sg_set_stream.argtypes = [P, P]
+        lib.sg_get_timing.argtypes = [P, P]
+        lib.sg_close.argtypes = [P]
+        lib.sg_last_error.argtypes = [P]
+        lib.sg_last_error.restype = ct.c_char_p
+        lib.sg_version.restype = ct.c_char_p
+        _lib = lib
+    return _lib
+
+
+def build_desc(nfa: L.FlatNFA) -> sg_nfa_desc:
+    d = sg_nfa_desc()
+    d.abi_version = SG_ABI_VERSION
+    d.type = nfa.type
+    d.within = nfa.within
+    d.playback = nfa.playback
+    d.partitioned = nfa.partitioned
+    d.n_states = len(nfa.states)
+    d.n_streams = max(1, max((s for s, _, _ in nfa.cols), default=0) + 1)
+    d.n_cols = len(nfa.cols)
+    d.n_ret = len(nfa.retained)
+    d.n_select = len(nfa.select)
+    code = []
+    for i, st in enumerate(nfa.states):
+        x = d.states[i]
+        for f in ("kind", "stream", "is_start", "min_count", "max_count", "logical_type", "partner",
+                  "next_state", "next_every", "within_every", "callback", "has_selector", "this_last",
+                  "local"):
+            setattr(x, f, int(getattr(st, f)))
+        x.waiting_time = int(st.waiting_time)
+        x.prog_off = len(code)
+        x.prog_len = len(st.prog)
+        code += st.prog
+    d.shape = nfa.shape
+    for k, v in enumerate(nfa.shape_args[:8]):
+        d.shape_args[k] = int(v)
+    d.shape_prog_off = len(code)
+    d.shape_prog_len = len(nfa.shape_prog)
+    code += nfa.shape_prog
+    if len(code) > SG_MAX_CODE:
+        raise L.LoweringError("predicate programs too long")
+    d.code_len = len(code)
+    for k, w in enumerate(code):
+        d.code[k] = int(w)
+    for s in range(SG_MAX_STREAMS):
+        d.recv_of_stream[s] = -1
+    for k, (s, r) in enumerate(sorted(nfa.receivers.items())):
+        rr = d.receivers[k]
+        rr.stream, rr.multi, rr.selector, rr.n = s, r.multi, r.selector, len(r.pres)
+        for j, p in enumerate(r.pres):
+            rr.pres[j] = p
+        for j, p in enumerate(r.stab):
+            rr.stab[j] = p
+        d.recv_of_stream[s] = k
+    d.n_init, d.n_reset, d.n_update, d.n_start = (len(nfa.init_order), len(nfa.reset_ops), len(nfa.update_ops),
+                                                  len(nfa.start_ids))
+    for k, v in enumerate(nfa.init_order):
+        d.init_order[k] = v
+    for k, v in enumerate(nfa.reset_ops):
+        d.reset_ops[k] = v
+    for k, v in enumerate(nfa.update_ops):
+        d.update_ops[k] = v
+    for k, v in enumerate(nfa.start_ids):
+        d.start_ids[k] = v
+    colidx = {}
+    for c, (s, a, t) in enumerate(nfa.cols):
+        d.col_type[c] = L.TYPE_CODE[t]
+        d.col_stream[c] = s
+        colidx[(s, a)] = c
+    for r, (s, a, t) in enumerate(nfa.retained):
+        d.ret_col[r] = colidx[(s, a)]
+        d.ret_type[r] = L.TYPE_CODE[t]
+    for k, (st, idx, slot, t) in enumerate(nfa.select):
+        d.sel_state[k], d.sel_index[k], d.sel_ret[k], d.sel_type[k] = st, idx, slot, L.TYPE_CODE[t]
+    return d
+
+
+class Handle:
+    """Thin RAII wrapper of one sg_handle."""
+
+    def __init__(self, desc: sg_nfa_desc, device: int = 0, options: sg_options = None):
+        self.lib = load_library()
+        self.h = ct.c_void_p()
+        self.desc = desc
+        self.opts = options if options is not None else sg_options()
+        rc = self.lib.sg_open(device, ct.byref(desc), ct.byref(self.opts), ct.byref(self.h))
+        if rc != 0:
+            msg = self.lib.sg_last_error(self.h).decode() if self.h else ""
+            if self.h:
+                self.lib.sg_close(self.h)
+            self.h = None
+            raise SgError(rc, msg)
+
+    def check(self, rc):
+        if rc != 0:
+            raise SgError(rc, self.lib.sg_last_error(self.h).decode())
+
+    def push(self, b: sg_batch):
+        self.check(self.lib.sg_push(self.h, ct.byref(b)))
+
+    def pending(self) -> int:
+        n = I64()
+        self.check(self.lib.sg_pending(self.h, ct.byref(n)))
+        return n.value
+
+    def poll(self, nsel: int):
+        n = self.pending()
+        tr = np.zeros(n, np.uint64)
+        ts = np.zeros(n, np.int64)
+        ky = np.zeros(n, np.int32)
+        gr = np.zeros(n, np.uint32)
+        vals = np.zeros((n, max(nsel, 1)), np.int64)
+        vn = np.zeros(n, np.uint32)
+        if n:
+            m = sg_matches(n, tr.ctypes.data, ts.ctypes.data, ky.ctypes.data, gr.ctypes.data, vals.ctypes.data,
+                           vn.ctypes.data)
+            got = I64()
+            self.check(self.lib.sg_poll(self.h, ct.byref(m), n, ct.byref(got)))
+        return tr, ts, ky, gr, vals[:, :nsel], vn
+
+    def device_matches(self) -> sg_matches:
+        m = sg_matches()
+        self.check(self.lib.sg_device_matches(self.h, ct.byref(m)))
+        return m
+
+    def timing(self) -> sg_timing:
+        t = sg_timing()
+        self.check(self.lib.sg_get_timing(self.h, ct.byref(t)))
+        return t
+
+    def reset(self):
+        self.check(self.lib.sg_reset(self.h))
+
+    def discard(self):
+        self.check(self.lib.sg_discard(self.h))
+
+    def flush(self):
+        self.check(self.lib.sg_flush(self.h))
+
+    def close(self):
+        if self.h:
+            self.lib.sg_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_batch(n, base_index, ts, stream, key, cols, nulls, on_device, key_bound=0, keep=None):
+    """Assemble an sg_batch from raw pointers (ints); `keep` collects ctypes arrays to keep alive."""
+    ncol = len(cols)
+    carr = (ct.c_void_p * max(ncol, 1))(*[c for c in cols])
+    narr = (ct.c_void_p * max(ncol, 1))(*[(x if x else None) for x in nulls])
+    if keep is not None:
+        keep += [carr, narr]
+    return sg_batch(n, base_index, ts, stream, key, ct.cast(carr, ct.c_void_p), ct.cast(narr, ct.c_void_p),
+                    on_device, key_bound)
+
+
+class GpuEngine:
+    """Engine interface (see siddhi_amd/runtime.py) on the MI355X kernels."""
+
+    def __init__(self, ctx: L.QueryContext, device: int = 0, force_general: bool = False):
+        self.ctx = ctx
+        self.nfa = L.lower(ctx)
+        self.desc = build_desc(self.nfa)
+        opts = sg_options()
+        opts.force_general = 1 if force_general else 0
+        self.handle = Handle(self.desc, device, opts)
+        self.nsel = len(self.nfa.select)
+
+    def push(self, b):
+        import numpy as np
+        keep = []
+        ts = np.ascontiguousarray(b.ts, np.int64)
+        st = np.ascontiguousarray(b.stream, np.int32)
+        ky = np.ascontiguousarray(b.key, np.int32)
+        cols = [np.ascontiguousarray(c) for c in b.cols]
+        keep += [ts, st, ky] + cols + [x for x in b.nulls if x is not None]
+        kb = int(ky.max()) + 1 if len(ky) and ky.max() >= 0 else 1
+        sb = make_batch(b.n, b.base_index, ts.ctypes.data, st.ctypes.data, ky.ctypes.data,
+                        [c.ctypes.data for c in cols], [(x.ctypes.data if x is not None else 0) for x in b.nulls],
+                        0, kb, keep)
+        self.handle.push(sb)
+
+    def fetch(self):
+        from .runtime import Outputs
+        tr, ts, ky, gr, vals, vn = self.handle.poll(self.nsel)
+        vnull = np.zeros((len(tr), self.nsel), np.uint8)
+        for k in range(self.nsel):
+            vnull[:, k] = (vn >> np.uint32(k)) & np.uint32(1)
+        return Outputs(tr, ts, ky, gr, vals, vnull)
+
+    def close(self):
+        self.handle.close()

@@ -1,0 +1,289 @@
+// C-ABI entry points of libsiddhi_gpu.so (declared in include/siddhi_gpu.h).
+#include <cstring>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <string>
+
+#include "sg_engine.h"
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw SgError(SG_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct sg_handle {
+  SgHandle h;
+};
+
+static int col_width(int type) { return (type == SG_T_LONG || type == SG_T_DOUBLE) ? 8 : 4; }
+
+template <class F>
+static int guard(sg_handle* hh, F&& f) {
+  try {
+    f();
+    return SG_OK;
+  } catch (SgError& e) {
+    if (hh) hh->h.err = e.msg;
+    return e.code;
+  } catch (std::exception& e) {
+    if (hh) hh->h.err = e.what();
+    return SG_EINVAL;
+  }
+}
+
+static void validate(const sg_nfa_desc* d) {
+  if (d->abi_version != SG_ABI_VERSION) throw SgError(SG_EINVAL, "sg_nfa_desc ABI version mismatch");
+  if (d->n_states < 1 || d->n_states > SG_MAX_STATES) throw SgError(SG_EINVAL, "bad n_states");
+  if (d->n_streams < 1 || d->n_streams > SG_MAX_STREAMS) throw SgError(SG_EINVAL, "bad n_streams");
+  if (d->n_cols < 0 || d->n_cols > SG_MAX_COLS) throw SgError(SG_EINVAL, "bad n_cols");
+  if (d->n_ret < 0 || d->n_ret > SG_MAX_RET) throw SgError(SG_EINVAL, "bad n_ret");
+  if (d->n_select < 0 || d->n_select > SG_MAX_SELECT) throw SgError(SG_EINVAL, "bad n_select");
+  if (d->code_len < 0 || d->code_len > SG_MAX_CODE) throw SgError(SG_EINVAL, "bad code_len");
+  for (int s = 0; s < d->n_states; ++s) {
+    const sg_state_desc& st = d->states[s];
+    if (st.stream < 0 || st.stream >= d->n_streams) throw SgError(SG_EINVAL, "state stream out of range");
+    if (st.prog_off < 0 || st.prog_off + st.prog_len > d->code_len) throw SgError(SG_EINVAL, "bad program range");
+  }
+  for (int r = 0; r < d->n_ret; ++r)
+    if (d->ret_col[r] < 0 || d->ret_col[r] >= d->n_cols) throw SgError(SG_EINVAL, "retained column out of range");
+}
+
+extern "C" {
+
+const char* sg_version(void) { return "siddhi_gpu 0.1 (gfx950)"; }
+
+int sg_open(int hip_device, const sg_nfa_desc* nfa, const sg_options* opt, sg_handle** out) {
+  if (!nfa || !out) return SG_EINVAL;
+  sg_handle* hh = new sg_handle();
+  SgHandle& h = hh->h;
+  int rc = guard(hh, [&] {
+    validate(nfa);
+    h.device = hip_device;
+    HIPCHK(hipSetDevice(hip_device));
+    h.desc = *nfa;
+    if (opt) h.opt = *opt;
+    else memset(&h.opt, 0, sizeof(h.opt));
+    if (h.opt.pool_partials <= 0) h.opt.pool_partials = 256;
+    if (h.opt.pool_events <= 0) h.opt.pool_events = 256;
+    if (h.opt.pool_chain <= 0) h.opt.pool_chain = 256;
+    if (h.opt.list_cap <= 0) h.opt.list_cap = 256;
+    HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
+    h.own_stream = true;
+    for (auto& e : h.ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipMalloc(&h.ddesc, sizeof(DevDesc)));
+    HIPCHK(hipMemcpy(h.ddesc, &h.desc, sizeof(DevDesc), hipMemcpyHostToDevice));
+  });
+  if (rc != SG_OK) {
+    // keep the handle so the caller can read sg_last_error, but mark it unusable
+    *out = hh;
+    return rc;
+  }
+  *out = hh;
+  return SG_OK;
+}
+
+int sg_push(sg_handle* hh, const sg_batch* b) {
+  if (!hh || !b) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipSetDevice(h.device));
+    const sg_nfa_desc& d = h.desc;
+    int64_t n = b->n;
+    if (n <= 0) return;
+    if (n >= (1ll << 30) - 1) throw SgError(SG_EINVAL, "batch too large (max 2^30-2 rows)");
+    if (!b->ts) throw SgError(SG_EINVAL, "batch without timestamps");
+    BatchView bv;
+    bv.n = n;
+    bv.base_index = b->base_index;
+    bv.key_bound = b->key_bound;
+    memset(&bv.cols, 0, sizeof(bv.cols));
+    hipStream_t st = h.stream;
+    if (b->on_device) {
+      bv.ts = b->ts;
+      bv.stream = b->stream;
+      bv.key = b->key;
+      for (int c = 0; c < d.n_cols; ++c) {
+        bv.cols.col[c] = b->cols ? b->cols[c] : nullptr;
+        bv.cols.nul[c] = b->nulls ? b->nulls[c] : nullptr;
+      }
+    } else {
+      auto up = [&](const char* name, const void* src, size_t bytes) -> void* {
+        if (!src) return nullptr;
+        void* p = h.ws.get(name, bytes, st);
+        HIPCHK(hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, st));
+        return p;
+      };
+      bv.ts = (const int64_t*)up("in_ts", b->ts, sizeof(int64_t) * n);
+      bv.stream = (const int32_t*)up("in_stream", b->stream, sizeof(int32_t) * n);
+      bv.key = (const int32_t*)up("in_key", b->key, sizeof(int32_t) * n);
+      for (int c = 0; c < d.n_cols; ++c) {
+        char nm[32];
+        snprintf(nm, sizeof nm, "in_col%d", c);
+        bv.cols.col[c] = b->cols ? up(nm, b->cols[c], (size_t)col_width(d.col_type[c]) * n) : nullptr;
+        snprintf(nm, sizeof nm, "in_nul%d", c);
+        bv.cols.nul[c] = (const uint8_t*)(b->nulls ? up(nm, b->nulls[c], (size_t)n) : nullptr);
+      }
+    }
+    for (int r = 0; r < d.n_ret; ++r)
+      if (!bv.cols.col[d.ret_col[r]]) throw SgError(SG_EINVAL, "batch is missing a column the query reads");
+    int shape = h.opt.force_general ? SG_SHAPE_GENERAL : d.shape;
+    switch (shape) {
+      case SG_SHAPE_EVERY_NEXT_CMP:
+        if (h.pushes > 0)
+          throw SgError(SG_EUNSUPPORTED, "closed-form every->next kernel: carry across pushes not implemented yet");
+        sg_run_every_next(&h, bv, n);
+        break;
+      default:
+        throw SgError(SG_EUNSUPPORTED, "general NFA kernel not built yet");
+    }
+    h.pushes++;
+  });
+}
+
+int sg_advance_time(sg_handle* hh, int64_t now, uint64_t trigger_index) {
+  if (!hh) return SG_EINVAL;
+  (void)now;
+  (void)trigger_index;
+  return SG_OK;
+}
+
+int sg_pending(sg_handle* hh, int64_t* n) {
+  if (!hh || !n) return SG_EINVAL;
+  *n = hh->h.out.n;
+  return SG_OK;
+}
+
+int sg_device_matches(sg_handle* hh, sg_matches* v) {
+  if (!hh || !v) return SG_EINVAL;
+  OutStore& o = hh->h.out;
+  v->n = o.n;
+  v->trigger = o.trigger;
+  v->ts = o.ts;
+  v->key = o.key;
+  v->group = o.group;
+  v->vals = o.vals;
+  v->vnull = o.vnull;
+  return SG_OK;
+}
+
+int sg_poll(sg_handle* hh, sg_matches* out, int64_t cap, int64_t* n) {
+  if (!hh || !out) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipSetDevice(h.device));
+    OutStore& o = h.out;
+    int64_t k = std::min<int64_t>(cap, o.n);
+    hipStream_t st = h.stream;
+    int ns = std::max(1, o.nsel);
+    if (k > 0) {
+      if (out->trigger) HIPCHK(hipMemcpyAsync(out->trigger, o.trigger, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+      if (out->ts) HIPCHK(hipMemcpyAsync(out->ts, o.ts, k * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      if (out->key) HIPCHK(hipMemcpyAsync(out->key, o.key, k * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+      if (out->group) HIPCHK(hipMemcpyAsync(out->group, o.group, k * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      if (out->vals && o.nsel) HIPCHK(hipMemcpyAsync(out->vals, o.vals, k * ns * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      if (out->vnull) HIPCHK(hipMemcpyAsync(out->vnull, o.vnull, k * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      o.consume(k, st);
+    }
+    out->n = k;
+    if (n) *n = k;
+  });
+}
+
+int sg_discard(sg_handle* hh) {
+  if (!hh) return SG_EINVAL;
+  hh->h.out.n = 0;
+  return SG_OK;
+}
+
+int sg_flush(sg_handle* hh) {
+  if (!hh) return SG_EINVAL;
+  return guard(hh, [&] { HIPCHK(hipStreamSynchronize(hh->h.stream)); });
+}
+
+int sg_reset(sg_handle* hh) {
+  if (!hh) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipStreamSynchronize(h.stream));
+    h.out.n = 0;
+    h.pushes = 0;
+    h.clock = 0;
+  });
+}
+
+int sg_set_stream(sg_handle* hh, void* s) {
+  if (!hh) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipStreamSynchronize(h.stream));
+    if (h.own_stream) HIPCHK(hipStreamDestroy(h.stream));
+    h.own_stream = false;
+    h.stream = (hipStream_t)s;
+  });
+}
+
+int sg_get_timing(sg_handle* hh, sg_timing* t) {
+  if (!hh || !t) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipEventSynchronize(h.ev[4]));
+    float a = 0, b = 0, c = 0, d = 0;
+    HIPCHK(hipEventElapsedTime(&a, h.ev[0], h.ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, h.ev[1], h.ev[2]));
+    HIPCHK(hipEventElapsedTime(&c, h.ev[2], h.ev[3]));
+    HIPCHK(hipEventElapsedTime(&d, h.ev[3], h.ev[4]));
+    t->pred_ms = a;
+    t->partition_ms = b;
+    t->match_ms = c;
+    t->output_ms = d;
+    t->total_ms = a + b + c + d;
+    t->events = h.last_events;
+    t->matches = h.last_matches;
+  });
+}
+
+int sg_close(sg_handle* hh) {
+  if (!hh) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  hipSetDevice(h.device);
+  if (h.stream) hipStreamSynchronize(h.stream);
+  h.ws.release();
+  h.out.release();
+  if (h.ddesc) hipFree(h.ddesc);
+  for (auto& e : h.ev) if (e) hipEventDestroy(e);
+  if (h.own_stream && h.stream) hipStreamDestroy(h.stream);
+  delete hh;
+  return SG_OK;
+}
+
+const char* sg_last_error(const sg_handle* hh) { return hh ? hh->h.err.c_str() : "null handle"; }
+
+}  // extern "C"
+
+void OutStore::consume(int64_t k, hipStream_t st) {
+  if (k >= n) {
+    n = 0;
+    return;
+  }
+  int64_t rest = n - k;
+  int ns = std::max(1, nsel);
+  auto shift = [&](auto* p, size_t elt) {
+    void* tmp = nullptr;
+    if (hipMalloc(&tmp, rest * elt) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc in consume");
+    hipMemcpyAsync(tmp, (char*)p + k * elt, rest * elt, hipMemcpyDeviceToDevice, st);
+    hipMemcpyAsync(p, tmp, rest * elt, hipMemcpyDeviceToDevice, st);
+    hipStreamSynchronize(st);
+    hipFree(tmp);
+  };
+  shift(trigger, sizeof(uint64_t));
+  shift(ts, sizeof(int64_t));
+  shift(key, sizeof(int32_t));
+  shift(group, sizeof(uint32_t));
+  shift(vals, sizeof(int64_t) * ns);
+  shift(vnull, sizeof(uint32_t));
+  n = rest;
+}

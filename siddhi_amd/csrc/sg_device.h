@@ -1,0 +1,183 @@
+// Device-side helpers shared by the MI355X state-engine kernels: typed column reads and the
+// postfix predicate VM that replaces Siddhi's ExpressionExecutor trees.
+//
+// Semantics restated from the reference executors (C/ = modules/siddhi-core/src/main/java/io/siddhi/core/):
+//   compare with a null operand -> false, except != -> true
+//       (C/executor/condition/compare/CompareConditionExpressionExecutor.java:39-43,
+//        .../compare/notequal/NotEqualCompareConditionExpressionExecutor.java:37)
+//   numeric domains: Java binary promotion for > >= < <=; == / != on Float-Long in double
+//       (.../compare/equal/EqualCompareConditionExpressionExecutorFloatLong.java:38); the lowering
+//       (siddhi_amd/lowering.py::_cmp_domain) picks the domain per compare.
+//   and: true iff both true; or: true iff either true; not: true unless operand is TRUE; is null
+//       (C/executor/condition/{And,Or,Not,IsNull}ConditionExpressionExecutor.java)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/siddhi_gpu.h"
+
+struct SgVal {
+  int64_t i;
+  double d;
+  int type;
+  int null;
+};
+
+struct SgCols {          // kernel-argument view of one batch's columns
+  const void* col[SG_MAX_COLS];
+  const uint8_t* nul[SG_MAX_COLS];
+};
+
+__device__ __forceinline__ SgVal sg_read_col(const SgCols& c, int col, int type, int64_t row) {
+  SgVal v;
+  v.type = type;
+  v.i = 0;
+  v.d = 0.0;
+  v.null = (c.nul[col] != nullptr && c.nul[col][row]) ? 1 : 0;
+  if (v.null) return v;
+  switch (type) {
+    case SG_T_LONG: v.i = ((const int64_t*)c.col[col])[row]; break;
+    case SG_T_FLOAT: v.d = (double)((const float*)c.col[col])[row]; break;
+    case SG_T_DOUBLE: v.d = ((const double*)c.col[col])[row]; break;
+    default: v.i = ((const int32_t*)c.col[col])[row]; break;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int64_t sg_val_bits(const SgVal& v) {
+  if (v.null) return 0;
+  if (v.type == SG_T_FLOAT) {
+    float f = (float)v.d;
+    return (int64_t)(uint32_t)__float_as_uint(f);
+  }
+  if (v.type == SG_T_DOUBLE) return __double_as_longlong(v.d);
+  return v.i;
+}
+
+__device__ __forceinline__ SgVal sg_val_from_bits(int64_t bits, int type, int null) {
+  SgVal v;
+  v.type = type;
+  v.null = null;
+  v.i = 0;
+  v.d = 0.0;
+  if (null) return v;
+  if (type == SG_T_FLOAT) v.d = (double)__uint_as_float((uint32_t)bits);
+  else if (type == SG_T_DOUBLE) v.d = __longlong_as_double(bits);
+  else v.i = bits;
+  return v;
+}
+
+__device__ __forceinline__ bool sg_cmp(int op, int dom, const SgVal& l, const SgVal& r) {
+  if (op == 1) {
+    if (l.null || r.null) return true;
+  } else if (l.null || r.null) {
+    return false;
+  }
+  if (dom == 3 || dom == 0) {  // dictionary ids / integral
+    int64_t a = l.i, b = r.i;
+    if (dom == 0) {  // int-vs-float handled by promotion domain, here both integral
+      a = (l.type == SG_T_FLOAT || l.type == SG_T_DOUBLE) ? (int64_t)l.d : l.i;
+      b = (r.type == SG_T_FLOAT || r.type == SG_T_DOUBLE) ? (int64_t)r.d : r.i;
+    }
+    switch (op) {
+      case 0: return a == b;
+      case 1: return a != b;
+      case 2: return a > b;
+      case 3: return a >= b;
+      case 4: return a < b;
+      default: return a <= b;
+    }
+  }
+  if (dom == 1) {  // float domain
+    float a = (l.type == SG_T_FLOAT || l.type == SG_T_DOUBLE) ? (float)l.d : (float)l.i;
+    float b = (r.type == SG_T_FLOAT || r.type == SG_T_DOUBLE) ? (float)r.d : (float)r.i;
+    switch (op) {
+      case 0: return a == b;
+      case 1: return a != b;
+      case 2: return a > b;
+      case 3: return a >= b;
+      case 4: return a < b;
+      default: return a <= b;
+    }
+  }
+  double a = (l.type == SG_T_FLOAT || l.type == SG_T_DOUBLE) ? l.d : (double)l.i;
+  double b = (r.type == SG_T_FLOAT || r.type == SG_T_DOUBLE) ? r.d : (double)r.i;
+  switch (op) {
+    case 0: return a == b;
+    case 1: return a != b;
+    case 2: return a > b;
+    case 3: return a >= b;
+    case 4: return a < b;
+    default: return a <= b;
+  }
+}
+
+// Postfix VM. `Reader` supplies VAR operands: SgVal read(int state, int index_in_chain, int ret_slot, int type).
+// Booleans are kept tri-state in SgVal (i = 0/1, null) so `not` of null is true (NotConditionExpressionExecutor).
+#define SG_VM_STACK 16
+template <class Reader>
+__device__ __forceinline__ bool sg_eval(const int64_t* code, int len, Reader& rd) {
+  if (len <= 0) return true;
+  SgVal st[SG_VM_STACK];
+  int sp = 0;
+  int pc = 0;
+  while (pc < len) {
+    int op = (int)code[pc];
+    switch (op) {
+      case SG_OP_VAR: {
+        st[sp++] = rd.read((int)code[pc + 1], (int)code[pc + 2], (int)code[pc + 3], (int)code[pc + 4]);
+        pc += 5;
+        break;
+      }
+      case SG_OP_CONST: {
+        st[sp++] = sg_val_from_bits(code[pc + 2], (int)code[pc + 1], 0);
+        pc += 3;
+        break;
+      }
+      case SG_OP_CMP: {
+        SgVal r = st[--sp];
+        SgVal l = st[--sp];
+        SgVal o;
+        o.type = SG_T_BOOL;
+        o.null = 0;
+        o.d = 0;
+        o.i = sg_cmp((int)code[pc + 1], (int)code[pc + 2], l, r) ? 1 : 0;
+        st[sp++] = o;
+        pc += 3;
+        break;
+      }
+      case SG_OP_AND:
+      case SG_OP_OR: {
+        SgVal r = st[--sp];
+        SgVal l = st[--sp];
+        bool lt = !l.null && l.i, rt = !r.null && r.i;
+        SgVal o;
+        o.type = SG_T_BOOL;
+        o.null = 0;
+        o.d = 0;
+        o.i = (op == SG_OP_AND) ? (lt && rt) : (lt || rt);
+        st[sp++] = o;
+        pc += 1;
+        break;
+      }
+      case SG_OP_NOT: {
+        SgVal x = st[sp - 1];
+        st[sp - 1].i = !(!x.null && x.i);
+        st[sp - 1].null = 0;
+        st[sp - 1].type = SG_T_BOOL;
+        pc += 1;
+        break;
+      }
+      case SG_OP_ISNULL: {
+        SgVal x = st[sp - 1];
+        st[sp - 1].i = x.null ? 1 : 0;
+        st[sp - 1].null = 0;
+        st[sp - 1].type = SG_T_BOOL;
+        pc += 1;
+        break;
+      }
+      default:
+        return false;
+    }
+  }
+  return sp > 0 && !st[sp - 1].null && st[sp - 1].i != 0;
+}

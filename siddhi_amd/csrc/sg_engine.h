@@ -1,0 +1,139 @@
+// Host-side engine state shared by the MI355X kernels' launch code (engine.hip, interp.hip, absent.hip)
+// and the C-ABI (api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_gpu.h"
+#include "sg_device.h"
+
+typedef sg_nfa_desc DevDesc;
+
+struct SgError {
+  int code;
+  std::string msg;
+  SgError(int c, std::string m) : code(c), msg(std::move(m)) {}
+};
+
+// Named, grow-only device workspaces (no allocation in steady state).
+struct Workspace {
+  struct Buf { void* p = nullptr; size_t bytes = 0; };
+  std::map<std::string, Buf> bufs;
+  void* get(const std::string& name, size_t bytes, hipStream_t st) {
+    Buf& b = bufs[name];
+    if (bytes == 0) bytes = 16;
+    if (b.bytes < bytes) {
+      if (b.p) {
+        hipStreamSynchronize(st);
+        hipFree(b.p);
+      }
+      size_t want = bytes + bytes / 4;
+      if (hipMalloc(&b.p, want) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc failed for workspace " + name);
+      b.bytes = want;
+    }
+    return b.p;
+  }
+  void release() {
+    for (auto& kv : bufs) if (kv.second.p) hipFree(kv.second.p);
+    bufs.clear();
+  }
+};
+
+struct OutPtrsH {
+  uint64_t* trigger;
+  int64_t* ts;
+  int32_t* key;
+  uint32_t* group;
+  int64_t* vals;
+  uint32_t* vnull;
+};
+
+// Pending match tuples in HBM, in delivery order.
+struct OutStore {
+  int64_t n = 0, cap = 0;
+  int nsel = 0;
+  uint64_t* trigger = nullptr;
+  int64_t* ts = nullptr;
+  int32_t* key = nullptr;
+  uint32_t* group = nullptr;
+  int64_t* vals = nullptr;
+  uint32_t* vnull = nullptr;
+  template <class P>
+  P reserve(int64_t extra, int n_select, hipStream_t st);
+  void release() {
+    hipFree(trigger); hipFree(ts); hipFree(key); hipFree(group); hipFree(vals); hipFree(vnull);
+    trigger = nullptr; ts = nullptr; key = nullptr; group = nullptr; vals = nullptr; vnull = nullptr;
+    n = cap = 0;
+  }
+  void consume(int64_t k, hipStream_t st);
+};
+
+struct BatchView {
+  int64_t n;
+  uint64_t base_index;
+  const int64_t* ts;
+  const int32_t* stream;
+  const int32_t* key;
+  SgCols cols;
+  int32_t key_bound;
+};
+
+struct SgHandle {
+  int device = 0;
+  sg_nfa_desc desc;
+  sg_options opt;
+  DevDesc* ddesc = nullptr;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  Workspace ws;
+  OutStore out;
+  std::string err;
+  hipEvent_t ev[8] = {};
+  int64_t last_events = 0, last_matches = 0;
+  int pushes = 0;
+  int64_t clock = 0;          // playback clock (TimestampGeneratorImpl.lastEventTimestamp)
+  void* state = nullptr;      // per-shape persistent state (interp / absent)
+  void mark(int k) { hipEventRecord(ev[k], stream); }
+};
+
+template <class P>
+P OutStore::reserve(int64_t extra, int n_select, hipStream_t st) {
+  nsel = n_select;
+  int64_t need = n + extra;
+  if (need > cap) {
+    int64_t nc = std::max<int64_t>(need + need / 2, 1024);
+    auto grow = [&](auto*& p, size_t elt) {
+      void* np = nullptr;
+      if (hipMalloc(&np, nc * elt) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc failed for match store");
+      if (p && n) hipMemcpyAsync(np, p, n * elt, hipMemcpyDeviceToDevice, st);
+      hipStreamSynchronize(st);
+      if (p) hipFree(p);
+      p = (std::remove_reference_t<decltype(p)>)np;
+    };
+    grow(trigger, sizeof(uint64_t));
+    grow(ts, sizeof(int64_t));
+    grow(key, sizeof(int32_t));
+    grow(group, sizeof(uint32_t));
+    grow(vals, sizeof(int64_t) * std::max(1, n_select));
+    grow(vnull, sizeof(uint32_t));
+    cap = nc;
+  }
+  P o;
+  o.trigger = trigger;
+  o.ts = ts;
+  o.key = key;
+  o.group = group;
+  o.vals = vals;
+  o.vnull = vnull;
+  return o;
+}
+
+void sg_run_every_next(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_general_reset(SgHandle* h);
+void sg_general_release(SgHandle* h);

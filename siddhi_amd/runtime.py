@@ -150,6 +150,11 @@ class InputHandler:
     def getStreamId(self):
         return self.stream_id
 
+    def send_columns(self, ts, **cols):
+        """Columnar bulk send (the SoA analogue of send(Event[])): ts int64[n] plus one array per
+        attribute.  STRING attributes may be given as integer arrays (already dictionary ids)."""
+        self.app_rt._append_columns(self.stream_index, np.asarray(ts, np.int64), cols)
+
     def send(self, a, b=None):
         """send(Object[]) | send(long ts, Object[]) | send(Event) | send(Event[])."""
         if b is not None:
@@ -220,6 +225,48 @@ class SiddhiAppRuntime:
         self._rows.append((stream, ts, data))
         if len(self._rows) >= self.batch_size:
             self.flush()
+
+    def _append_columns(self, stream: int, ts: np.ndarray, cols: dict):
+        self.flush()
+        n = len(ts)
+        d = self.app.streams[self.stream_ids[stream]]
+        base = self.next_index
+        self.next_index += n
+        stream_col = np.full(n, stream, np.int32)
+        allcols, nulls = [], []
+        for s, sid in enumerate(self.stream_ids):
+            for a, (name, t) in enumerate(self.app.streams[sid].attrs):
+                if s == stream:
+                    v = cols.get(name)
+                    if v is None:
+                        raise SiddhiAppCreationException(f"missing column {name}")
+                    allcols.append(np.ascontiguousarray(v, dtype=_NP[t]))
+                else:
+                    allcols.append(np.zeros(n, dtype=_NP[t]))
+                nulls.append(None)
+        for qi, q in enumerate(self.queries):
+            if q.ctx.partitioned and q.ctx.key_attr[stream] >= 0:
+                name = d.attrs[q.ctx.key_attr[stream]][0]
+                key = self._dense_keys(qi, np.asarray(cols[name]))
+            else:
+                key = np.zeros(n, np.int32) if not q.ctx.partitioned else np.full(n, -1, np.int32)
+            q.engine.push(Batch(n, base, ts, stream_col, key, allcols, nulls))
+            self._deliver(q, q.engine.fetch())
+
+    def _dense_keys(self, qi: int, vals: np.ndarray) -> np.ndarray:
+        """First-seen dense ids of partition key values (PartitionRuntime clone order)."""
+        kd = self.key_dicts[qi]
+        uniq, first = np.unique(vals, return_index=True)
+        order = np.argsort(first, kind="stable")
+        ids = np.empty(len(uniq), np.int32)
+        for k in order:
+            ks = str(uniq[k].item())
+            i = kd.get(ks)
+            if i is None:
+                i = len(kd)
+                kd[ks] = i
+            ids[k] = i
+        return ids[np.searchsorted(uniq, vals)]
 
     def advance_time(self, now: int):
         """Playback clock advance without an event (heartbeat)."""

@@ -1,0 +1,67 @@
+"""Helpers that drive an engine directly with SoA batches (bypassing per-row callbacks) so the oracle
+and the HIP engine can be compared bit for bit on large synthetic inputs."""
+import numpy as np
+
+from siddhi_amd import compiler as C
+from siddhi_amd import lowering as L
+from siddhi_amd import synth
+from siddhi_amd.runtime import Batch, Outputs, SiddhiAppRuntime
+
+
+def context(query_text):
+    app = C.parse(query_text)
+    if app.partitions:
+        p = app.partitions[0]
+        return L.make_context(app, p.queries[0], p, {})
+    return L.make_context(app, app.queries[0], None, {})
+
+
+def synth_batch(cfg, start, count, keys=None, rate=None):
+    """A Batch of config `cfg` rows with first-seen dense keys (via the runtime's encoder)."""
+    g = synth.generate(cfg, start, count, keys=keys, rate=rate)
+    n = count
+    if cfg.startswith("C4"):
+        cols = [g["id"], g["seq"], np.zeros(n, np.int32)]       # S(id, seq), Tick(x)
+        return Batch(n, start, g["ts"], np.zeros(n, np.int32), np.zeros(n, np.int32), cols, [None] * 3)
+    if cfg.startswith("C3"):
+        cols = [g["id"], g["key"], g["v"], g["w"]]
+    else:
+        cols = [g["id"], g["key"], g["price"]]
+    return Batch(n, start, g["ts"], np.zeros(n, np.int32), g["key"].astype(np.int32), cols, [None] * len(cols))
+
+
+def dense_first_seen(keys):
+    uniq, first = np.unique(keys, return_index=True)
+    order = np.argsort(first, kind="stable")
+    ids = np.empty(len(uniq), np.int32)
+    ids[order] = np.arange(len(uniq), dtype=np.int32)
+    return ids[np.searchsorted(uniq, keys)]
+
+
+def run_engine(engine_cls, query_text, batches, **kw):
+    ctx = context(query_text)
+    eng = engine_cls(ctx, **kw)
+    outs = []
+    for b in batches:
+        if not ctx.partitioned:
+            b = Batch(b.n, b.base_index, b.ts, b.stream, np.zeros(b.n, np.int32), b.cols, b.nulls)
+        eng.push(b)
+        outs.append(eng.fetch())
+    eng.close()
+    return Outputs(*[np.concatenate([getattr(o, f) for o in outs]) for f in
+                     ("trigger", "ts", "key", "group", "vals", "vnull")])
+
+
+def assert_same(a: Outputs, b: Outputs):
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("trigger", "ts", "key", "group"):
+        x, y = getattr(a, f), getattr(b, f)
+        if not np.array_equal(x, y):
+            k = int(np.nonzero(x != y)[0][0])
+            raise AssertionError(f"field {f} differs first at {k}: {x[k]} vs {y[k]}")
+    assert np.array_equal(a.vnull, b.vnull)
+    vals_a = np.where(a.vnull.astype(bool), 0, a.vals)
+    vals_b = np.where(b.vnull.astype(bool), 0, b.vals)
+    if not np.array_equal(vals_a, vals_b):
+        k = int(np.nonzero((vals_a != vals_b).any(axis=1))[0][0])
+        raise AssertionError(f"vals differ first at {k}: {vals_a[k]} vs {vals_b[k]}")
