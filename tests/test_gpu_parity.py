@@ -33,9 +33,9 @@ def test_kat_on_gpu(case):
 
 @pytest.mark.parametrize("cfg,n,keys,rate", [
     ("C1", 300_000, 1, 1),
-    ("C2", 2_000_000, 10_000, 1_000),
-    ("C2", 500_000, 50, 100),
-    ("C5", 3_000_000, 1_000_000, 10_000),
+    ("C2", 1_000_000, 10_000, 1_000),
+    ("C2", 300_000, 50, 100),
+    ("C5", 1_000_000, 100_000, 10_000),
 ])
 def test_every_next_synthetic_parity(cfg, n, keys, rate):
     b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
