@@ -130,7 +130,8 @@ typedef struct sg_options {
   int32_t pool_chain;       /* general engine: count-chain nodes per key */
   int32_t list_cap;         /* general engine: capacity of each pending / newAndEvery list */
   int32_t force_general;    /* 1: ignore closed-form shapes (parity testing of the general kernel) */
-  int32_t reserved[7];
+  int32_t no_carry;         /* 1: pushes are independent streams (no state carried between them) */
+  int32_t reserved[6];
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)
@@ -147,6 +148,15 @@ typedef struct sg_batch {
   int32_t on_device;
   int32_t key_bound;            /* exclusive upper bound of key ids in this batch (0 = unknown) */
 } sg_batch;
+
+/* Pending matches as they sit in HBM: n AoS records of record_bytes = 32 + 8*n_select bytes,
+ * {u64 trigger; i64 ts; i32 key; u32 group; u32 vnull; u32 pad; i64 vals[n_select]} (see sg_matches). */
+typedef struct sg_match_records {
+  int64_t n;
+  int32_t record_bytes;
+  int32_t n_select;
+  void* base;
+} sg_match_records;
 
 /* Match tuples in delivery order.  vals[i*n_select + k] holds the bit pattern of select column k
  * (FLOAT: f32 bits, DOUBLE: f64 bits, others sign-extended); bit k of vnull[i] marks a null. */
@@ -173,8 +183,8 @@ int sg_advance_time(sg_handle* h, int64_t now, uint64_t trigger_index);
 int sg_pending(sg_handle* h, int64_t* n);
 /* Copy up to cap pending matches into host arrays (fields may be NULL to skip) and consume them. */
 int sg_poll(sg_handle* h, sg_matches* out, int64_t cap, int64_t* n);
-/* Zero-copy view of the pending matches in HBM (valid until the next push/poll/reset). */
-int sg_device_matches(sg_handle* h, sg_matches* view);
+/* Zero-copy view of the pending match records in HBM (valid until the next push/poll/reset). */
+int sg_device_records(sg_handle* h, sg_match_records* view);
 int sg_discard(sg_handle* h);           /* drop pending matches without copying */
 int sg_flush(sg_handle* h);             /* wait for all work on the handle's stream */
 int sg_reset(sg_handle* h);             /* forget all per-key state (fresh runtime) */

@@ -919,6 +919,7 @@ void KeyRuntime::emit(const SE& s) {
     else o.vals.push_back(se->data->vals[e->sel_attr[i]]);
   }
   e->out.push_back(std::move(o));
+  if (cur_phase == 0) cur_group++;   // every timer emission is its own callback (sendEvent per partial)
 }
 
 // ------------------------------------------------------------------ build (StateInputStreamParser)
@@ -987,6 +988,7 @@ struct Builder {
     rt->schedulers.emplace_back(new Scheduler());
     Scheduler* s = rt->schedulers.back().get();
     s->target = p; s->rt = rt;
+    s->order = (uint32_t)(rt->schedulers.size() - 1);
     eng->listeners.push_back(s);
     return s;
   }
@@ -1165,9 +1167,10 @@ void Engine::setCurrentTimestamp(int64_t ts, uint64_t trigger) {  // TimestampGe
     Scheduler* sc = listeners[li];
     if (sc->q.empty() || sc->q.front() > ts) continue;     // Scheduler listener :74-86
     KeyRuntime* rt = sc->rt;
+    rt->cur_group = sc->order << 16;
     while (!sc->q.empty() && sc->q.front() - lastEventTimestamp <= 0) {   // sendTimerEvents :179-214
       int64_t t = sc->q.front(); sc->q.pop_front();
-      rt->cur_trigger = trigger; rt->cur_phase = 0; rt->cur_group = (uint32_t)li;
+      rt->cur_trigger = trigger; rt->cur_phase = 0;
       sc->target->processTimer(t);
     }
   }

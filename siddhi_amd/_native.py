@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libsiddhi_gpu.so")
 SG_MAX_STATES, SG_MAX_STREAMS, SG_MAX_SELECT, SG_MAX_RET, SG_MAX_COLS, SG_MAX_CODE = 16, 16, 32, 16, 64, 512
 SG_ABI_VERSION = 1
 
-SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_matches", "sg_discard",
+SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
            "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version"]
 
 I32, I64, U64 = ct.c_int32, ct.c_int64, ct.c_uint64
@@ -53,7 +53,7 @@ class sg_nfa_desc(ct.Structure):
 
 class sg_options(ct.Structure):
     _fields_ = [("max_batch", I64), ("pool_partials", I32), ("pool_events", I32), ("pool_chain", I32),
-                ("list_cap", I32), ("force_general", I32), ("reserved", I32 * 7)]
+                ("list_cap", I32), ("force_general", I32), ("no_carry", I32), ("reserved", I32 * 6)]
 
 
 class sg_batch(ct.Structure):
@@ -65,6 +65,10 @@ class sg_batch(ct.Structure):
 class sg_matches(ct.Structure):
     _fields_ = [("n", I64), ("trigger", ct.c_void_p), ("ts", ct.c_void_p), ("key", ct.c_void_p),
                 ("group", ct.c_void_p), ("vals", ct.c_void_p), ("vnull", ct.c_void_p)]
+
+
+class sg_match_records(ct.Structure):
+    _fields_ = [("n", I64), ("record_bytes", I32), ("n_select", I32), ("base", ct.c_void_p)]
 
 
 class sg_timing(ct.Structure):
@@ -95,7 +99,7 @@ def load_library(path: str = LIB_PATH):
         lib.sg_advance_time.argtypes = [P, I64, U64]
         lib.sg_pending.argtypes = [P, ct.POINTER(I64)]
         lib.sg_poll.argtypes = [P, P, I64, ct.POINTER(I64)]
-        lib.sg_device_matches.argtypes = [P, P]
+        lib.sg_device_records.argtypes = [P, P]
         lib.sg_discard.argtypes = [P]
         lib.sg_flush.argtypes = [P]
         lib.sg_reset.argtypes = [P]
@@ -219,9 +223,9 @@ class Handle:
             self.check(self.lib.sg_poll(self.h, ct.byref(m), n, ct.byref(got)))
         return tr, ts, ky, gr, vals[:, :nsel], vn
 
-    def device_matches(self) -> sg_matches:
-        m = sg_matches()
-        self.check(self.lib.sg_device_matches(self.h, ct.byref(m)))
+    def device_records(self) -> sg_match_records:
+        m = sg_match_records()
+        self.check(self.lib.sg_device_records(self.h, ct.byref(m)))
         return m
 
     def timing(self) -> sg_timing:
@@ -264,12 +268,16 @@ def make_batch(n, base_index, ts, stream, key, cols, nulls, on_device, key_bound
 class GpuEngine:
     """Engine interface (see siddhi_amd/runtime.py) on the MI355X kernels."""
 
-    def __init__(self, ctx: L.QueryContext, device: int = 0, force_general: bool = False):
+    def __init__(self, ctx: L.QueryContext, device: int = 0, force_general: bool = False, pool: int = 0,
+                 no_carry: bool = False):
         self.ctx = ctx
         self.nfa = L.lower(ctx)
         self.desc = build_desc(self.nfa)
         opts = sg_options()
         opts.force_general = 1 if force_general else 0
+        opts.no_carry = 1 if no_carry else 0
+        if pool:
+            opts.pool_partials = opts.pool_events = opts.pool_chain = opts.list_cap = pool
         self.handle = Handle(self.desc, device, opts)
         self.nsel = len(self.nfa.select)
 

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "sg_engine.h"
 
@@ -132,12 +133,13 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
     int shape = h.opt.force_general ? SG_SHAPE_GENERAL : d.shape;
     switch (shape) {
       case SG_SHAPE_EVERY_NEXT_CMP:
-        if (h.pushes > 0)
-          throw SgError(SG_EUNSUPPORTED, "closed-form every->next kernel: carry across pushes not implemented yet");
         sg_run_every_next(&h, bv, n);
         break;
+      case SG_SHAPE_EVERY_ABSENT_EQ:
+        sg_run_every_absent(&h, bv, n);
+        break;
       default:
-        throw SgError(SG_EUNSUPPORTED, "general NFA kernel not built yet");
+        sg_run_general(&h, bv, n);
     }
     h.pushes++;
   });
@@ -156,16 +158,13 @@ int sg_pending(sg_handle* hh, int64_t* n) {
   return SG_OK;
 }
 
-int sg_device_matches(sg_handle* hh, sg_matches* v) {
+int sg_device_records(sg_handle* hh, sg_match_records* v) {
   if (!hh || !v) return SG_EINVAL;
   OutStore& o = hh->h.out;
   v->n = o.n;
-  v->trigger = o.trigger;
-  v->ts = o.ts;
-  v->key = o.key;
-  v->group = o.group;
-  v->vals = o.vals;
-  v->vnull = o.vnull;
+  v->record_bytes = 32 + 8 * hh->h.desc.n_select;
+  v->n_select = hh->h.desc.n_select;
+  v->base = o.rec;
   return SG_OK;
 }
 
@@ -177,15 +176,21 @@ int sg_poll(sg_handle* hh, sg_matches* out, int64_t cap, int64_t* n) {
     OutStore& o = h.out;
     int64_t k = std::min<int64_t>(cap, o.n);
     hipStream_t st = h.stream;
-    int ns = std::max(1, o.nsel);
+    int ns = h.desc.n_select;
+    size_t stride = 32 + 8 * (size_t)ns;
     if (k > 0) {
-      if (out->trigger) HIPCHK(hipMemcpyAsync(out->trigger, o.trigger, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-      if (out->ts) HIPCHK(hipMemcpyAsync(out->ts, o.ts, k * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      if (out->key) HIPCHK(hipMemcpyAsync(out->key, o.key, k * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-      if (out->group) HIPCHK(hipMemcpyAsync(out->group, o.group, k * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      if (out->vals && o.nsel) HIPCHK(hipMemcpyAsync(out->vals, o.vals, k * ns * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      if (out->vnull) HIPCHK(hipMemcpyAsync(out->vnull, o.vnull, k * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      std::vector<char> tmp((size_t)k * stride);
+      HIPCHK(hipMemcpyAsync(tmp.data(), o.rec, (size_t)k * stride, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
+      for (int64_t i = 0; i < k; ++i) {
+        const char* r = tmp.data() + (size_t)i * stride;
+        if (out->trigger) memcpy(out->trigger + i, r, 8);
+        if (out->ts) memcpy(out->ts + i, r + 8, 8);
+        if (out->key) memcpy(out->key + i, r + 16, 4);
+        if (out->group) memcpy(out->group + i, r + 20, 4);
+        if (out->vnull) memcpy(out->vnull + i, r + 24, 4);
+        if (out->vals && ns) memcpy(out->vals + i * ns, r + 32, 8 * (size_t)ns);
+      }
       o.consume(k, st);
     }
     out->n = k;
@@ -212,6 +217,8 @@ int sg_reset(sg_handle* hh) {
     h.out.n = 0;
     h.pushes = 0;
     h.clock = 0;
+    sg_every_next_reset(&h);
+    sg_general_reset(&h);
   });
 }
 
@@ -251,6 +258,8 @@ int sg_close(sg_handle* hh) {
   SgHandle& h = hh->h;
   hipSetDevice(h.device);
   if (h.stream) hipStreamSynchronize(h.stream);
+  sg_every_next_release(&h);
+  sg_general_release(&h);
   h.ws.release();
   h.out.release();
   if (h.ddesc) hipFree(h.ddesc);
@@ -270,20 +279,11 @@ void OutStore::consume(int64_t k, hipStream_t st) {
     return;
   }
   int64_t rest = n - k;
-  int ns = std::max(1, nsel);
-  auto shift = [&](auto* p, size_t elt) {
-    void* tmp = nullptr;
-    if (hipMalloc(&tmp, rest * elt) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc in consume");
-    hipMemcpyAsync(tmp, (char*)p + k * elt, rest * elt, hipMemcpyDeviceToDevice, st);
-    hipMemcpyAsync(p, tmp, rest * elt, hipMemcpyDeviceToDevice, st);
-    hipStreamSynchronize(st);
-    hipFree(tmp);
-  };
-  shift(trigger, sizeof(uint64_t));
-  shift(ts, sizeof(int64_t));
-  shift(key, sizeof(int32_t));
-  shift(group, sizeof(uint32_t));
-  shift(vals, sizeof(int64_t) * ns);
-  shift(vnull, sizeof(uint32_t));
+  void* tmp = nullptr;
+  if (hipMalloc(&tmp, (size_t)rest * stride) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc in consume");
+  hipMemcpyAsync(tmp, rec + (size_t)k * stride, (size_t)rest * stride, hipMemcpyDeviceToDevice, st);
+  hipMemcpyAsync(rec, tmp, (size_t)rest * stride, hipMemcpyDeviceToDevice, st);
+  hipStreamSynchronize(st);
+  hipFree(tmp);
   n = rest;
 }

@@ -1,0 +1,352 @@
+// General NFA pass on MI355X (SG_SHAPE_GENERAL): one thread advances one partition key's runtime
+// (interp.h KeyMachine, the flat restatement of the Pre/Post processor chain) over that key's rows.
+//
+// Per sg_push:
+//   1. k_route      rows -> partition key (sentinel for rows no receiver reads / null keys);
+//                   for playback queries with `not ... for T` also checks that timestamps never decrease
+//   2. key partition stable radix sort of (key, row) (rocPRIM) + k_segments: each key's rows contiguous,
+//                   in arrival order (PartitionStreamReceiver routing)
+//   3. k_nfa        one thread per key that ever appeared: runs the key machine over its rows and the
+//                   absence timers its schedulers fire on the global playback clock; every match is
+//                   appended (atomic bump) with a sort key (trigger row, timer-before-event, key)
+//   4. radix sort of the sort keys (stable: per-key emission order is kept) + k_gather into the
+//                   pending match store in the reference's delivery order.
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <string>
+
+#include "sg_device.h"
+#include "sg_engine.h"
+#include "interp.h"
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw SgError(SG_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct GeneralState {
+  SgGeo geo;
+  int32_t* arena = nullptr;
+  int64_t keys_alloc = 0;     // arenas allocated
+  SgGeo* dgeo = nullptr;
+  int32_t* dfail = nullptr;
+};
+
+__global__ void k_route(int64_t n, const int32_t* __restrict__ stream, const int32_t* __restrict__ key,
+                        const int64_t* __restrict__ ts, const DevDesc* __restrict__ dd, int partitioned,
+                        uint32_t sentinel, int check_order, uint32_t* __restrict__ okey, uint32_t* __restrict__ orow,
+                        int32_t* __restrict__ order_err) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int s = stream ? stream[i] : 0;
+  bool own = s >= 0 && s < SG_MAX_STREAMS && dd->recv_of_stream[s] >= 0;
+  uint32_t k = sentinel;
+  if (own) {
+    if (!partitioned) k = 0;
+    else {
+      int32_t kk = key ? key[i] : -1;
+      if (kk >= 0) k = (uint32_t)kk;
+    }
+  }
+  okey[i] = k;
+  orow[i] = (uint32_t)i;
+  if (check_order && i > 0 && ts[i - 1] > ts[i]) atomicOr(order_err, 1);
+}
+
+__global__ void k_segments(int64_t n, const uint32_t* __restrict__ skey, uint32_t sentinel, uint32_t* __restrict__ beg,
+                           uint32_t* __restrict__ end) {
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  uint32_t k = skey[p];
+  if (k == sentinel) return;
+  if (p == 0 || skey[p - 1] != k) beg[k] = (uint32_t)p;
+  if (p == n - 1 || skey[p + 1] != k) end[k] = (uint32_t)p + 1;
+}
+
+struct DevRows {
+  const uint32_t* rows;   // sorted row indices of this key: rows[0..nown)
+  int64_t nown;
+  int64_t n;
+  const int64_t* ts;
+  const int32_t* stream;
+  const SgCols* cols;
+  const DevDesc* d;
+  uint64_t base;
+  __device__ int64_t n_own() { return nown; }
+  __device__ int64_t own_local(int64_t i) { return (int64_t)rows[i]; }
+  __device__ int64_t n_rows() { return n; }
+  __device__ int64_t ts_at(int64_t r) { return ts[r]; }
+  __device__ int64_t ts_(int64_t r) { return ts[r]; }
+  __device__ int64_t find_ge(int64_t from, int64_t v) {
+    int64_t lo = from, hi = n;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (ts[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  }
+  __device__ void fill(int64_t r, SgRow& row) {
+    row.ts = ts[r];
+    row.index = base + (uint64_t)r;
+    row.stream = stream ? stream[r] : 0;
+    row.nullmask = 0;
+    for (int k = 0; k < d->n_ret; ++k) {
+      SgVal v = sg_read_col(*cols, d->ret_col[k], d->ret_type[k], r);
+      if (v.null) row.nullmask |= 1 << k;
+      row.vals[k] = sg_val_bits(v);
+    }
+  }
+};
+// sg_run_key calls rows.ts(r)
+struct DevRowsTs : DevRows {
+  __device__ int64_t ts(int64_t r) { return DevRows::ts[r]; }
+};
+
+struct NfaArgs {
+  int64_t n;
+  uint64_t base_index;
+  int64_t nkeys;
+  int32_t partitioned;
+  int32_t clone;
+  const uint32_t* rows;
+  const uint32_t* beg;
+  const uint32_t* end;
+  const int64_t* ts;
+  const int32_t* stream;
+};
+
+__global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDesc* __restrict__ dd,
+                                            const SgGeo* __restrict__ geo, int32_t* __restrict__ arena,
+                                            SgEmitSink sink, int32_t* __restrict__ fail_code) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.nkeys) return;
+  int32_t* ar = arena + k * geo->key_words;
+  uint32_t b = a.beg[k], e = a.end[k];
+  if (!a.partitioned || true) {
+    // keys that never received a row have no runtime yet (and no timers)
+    if (ar[K_CREATED] == 0 && e <= b && a.partitioned) return;
+  }
+  KeyMachine m;
+  m.d = dd;
+  m.g = geo;
+  m.a = ar;
+  m.key = (int32_t)k;
+  m.clone = a.clone;
+  m.sink = sink;
+  m.base_index = a.base_index;
+  m.trigger = a.base_index;
+  m.phase = 1;
+  m.group = 0;
+  m.now = 0;
+  m.failed = ar[K_OVERFLOW];
+  if (m.failed) { atomicCAS(fail_code, 0, m.failed); return; }
+  DevRowsTs rows;
+  rows.rows = a.rows + b;
+  rows.nown = (e > b) ? (int64_t)(e - b) : 0;
+  rows.n = a.n;
+  rows.DevRows::ts = a.ts;
+  rows.stream = a.stream;
+  rows.cols = &cols;
+  rows.d = dd;
+  rows.base = a.base_index;
+  sg_run_key(m, rows, !a.partitioned);
+  if (m.failed) atomicCAS(fail_code, 0, m.failed);
+}
+
+__global__ void k_sortkeys(int64_t n, const char* __restrict__ buf, int32_t stride, uint64_t* __restrict__ sk,
+                           uint32_t* __restrict__ idx) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  sk[i] = *(const uint64_t*)(buf + (size_t)i * stride);
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void k_gather(int64_t n, const char* __restrict__ buf, int32_t stride, const uint32_t* __restrict__ idx,
+                         char* __restrict__ out, int32_t ostride) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t* src = (const uint64_t*)(buf + (size_t)idx[i] * stride + 8);
+  uint64_t* dst = (uint64_t*)(out + (size_t)i * ostride);
+  for (int w = 0; w < ostride / 8; ++w) dst[w] = src[w];
+}
+
+static GeneralState* gstate(SgHandle* h) {
+  if (!h->state) {
+    GeneralState* g = new GeneralState();
+    int q = h->opt.list_cap;
+    g->geo = sg_make_geo(h->desc, h->opt.pool_partials, h->opt.pool_events, h->opt.pool_chain, h->opt.list_cap, q);
+    if (hipMalloc(&g->dgeo, sizeof(SgGeo)) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc geo");
+    hipMemcpy(g->dgeo, &g->geo, sizeof(SgGeo), hipMemcpyHostToDevice);
+    if (hipMalloc(&g->dfail, sizeof(int32_t)) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc fail");
+    h->state = g;
+    h->state_kind = 2;
+  }
+  return (GeneralState*)h->state;
+}
+
+void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  GeneralState* gs = gstate(h);
+  bool has_absent = gs->geo.A > 0;
+  // ---- key bound
+  uint32_t kb = 1;
+  if (d.partitioned) {
+    kb = bv.key_bound > 0 ? (uint32_t)bv.key_bound : 0;
+    if (kb == 0) {
+      int32_t* dmax = (int32_t*)h->ws.get("kmax", sizeof(int32_t), st);
+      size_t tb = 0;
+      HIPCHK(rocprim::reduce(nullptr, tb, bv.key, dmax, (int32_t)-1, (size_t)n, rocprim::maximum<int32_t>(), st));
+      void* tmp = h->ws.get("kmax_tmp", tb, st);
+      HIPCHK(rocprim::reduce(tmp, tb, bv.key, dmax, (int32_t)-1, (size_t)n, rocprim::maximum<int32_t>(), st));
+      int32_t hm = 0;
+      HIPCHK(hipMemcpyAsync(&hm, dmax, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      kb = (uint32_t)(hm + 1);
+    }
+  }
+  if (kb < h->key_bound_seen) kb = h->key_bound_seen;
+  h->key_bound_seen = kb;
+  // ---- grow arenas (new ones zeroed: runtime not created yet)
+  if ((int64_t)kb > gs->keys_alloc) {
+    int64_t nk = std::max<int64_t>((int64_t)kb, gs->keys_alloc * 3 / 2);
+    size_t bytes = (size_t)nk * (size_t)gs->geo.key_words * 4;
+    int32_t* na = nullptr;
+    if (hipMalloc(&na, bytes) != hipSuccess)
+      throw SgError(SG_ECAPACITY, "cannot allocate per-key NFA arenas (" + std::to_string(bytes >> 20) + " MiB)");
+    HIPCHK(hipMemsetAsync(na, 0, bytes, st));
+    if (gs->arena) {
+      HIPCHK(hipMemcpyAsync(na, gs->arena, (size_t)gs->keys_alloc * gs->geo.key_words * 4, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+      hipFree(gs->arena);
+    }
+    gs->arena = na;
+    gs->keys_alloc = nk;
+  }
+  int kbits = 1;
+  while ((1ull << kbits) <= (uint64_t)kb) ++kbits;
+  uint32_t sentinel = kb;
+  int end_bit = 1;
+  while ((1ull << end_bit) <= (uint64_t)sentinel) ++end_bit;
+  dim3 blk(256), grd((unsigned)((n + 255) / 256));
+  // ---- route + partition
+  uint32_t* keys = (uint32_t*)h->ws.get("g_keys", sizeof(uint32_t) * n, st);
+  uint32_t* rows = (uint32_t*)h->ws.get("g_rows", sizeof(uint32_t) * n, st);
+  uint32_t* skeys = (uint32_t*)h->ws.get("g_skeys", sizeof(uint32_t) * n, st);
+  uint32_t* srows = (uint32_t*)h->ws.get("g_srows", sizeof(uint32_t) * n, st);
+  int32_t* order_err = (int32_t*)h->ws.get("order_err", sizeof(int32_t), st);
+  HIPCHK(hipMemsetAsync(order_err, 0, sizeof(int32_t), st));
+  h->mark(0);
+  hipLaunchKernelGGL(k_route, grd, blk, 0, st, n, bv.stream, bv.key, bv.ts, h->ddesc, d.partitioned, sentinel,
+                     has_absent ? 1 : 0, keys, rows, order_err);
+  HIPCHK(hipGetLastError());
+  h->mark(1);
+  {
+    size_t tb = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, rows, srows, (size_t)n, 0, end_bit, st));
+    void* tmp = h->ws.get("g_sort_tmp", tb, st);
+    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, rows, srows, (size_t)n, 0, end_bit, st));
+  }
+  uint32_t* beg = (uint32_t*)h->ws.get("g_beg", sizeof(uint32_t) * kb, st);
+  uint32_t* end = (uint32_t*)h->ws.get("g_end", sizeof(uint32_t) * kb, st);
+  HIPCHK(hipMemsetAsync(beg, 0, sizeof(uint32_t) * kb, st));
+  HIPCHK(hipMemsetAsync(end, 0, sizeof(uint32_t) * kb, st));
+  hipLaunchKernelGGL(k_segments, grd, blk, 0, st, n, skeys, sentinel, beg, end);
+  HIPCHK(hipGetLastError());
+  h->mark(2);
+  // ---- per-key machines
+  int32_t stride = sg_emit_stride(d.n_select);
+  int64_t cap = n + 65536;
+  char* ebuf = (char*)h->ws.get("g_emit", (size_t)cap * stride, st);
+  unsigned long long* ecount = (unsigned long long*)h->ws.get("g_ecount", 16, st);
+  int32_t* eover = (int32_t*)h->ws.get("g_eover", 4, st);
+  HIPCHK(hipMemsetAsync(ecount, 0, 8, st));
+  HIPCHK(hipMemsetAsync(eover, 0, 4, st));
+  HIPCHK(hipMemsetAsync(gs->dfail, 0, 4, st));
+  int32_t oerr = 0;
+  if (has_absent) {
+    HIPCHK(hipMemcpyAsync(&oerr, order_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (oerr) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps within a push");
+  }
+  NfaArgs na;
+  na.n = n;
+  na.base_index = bv.base_index;
+  na.nkeys = kb;
+  na.partitioned = d.partitioned;
+  na.clone = d.partitioned;
+  na.rows = srows;
+  na.beg = beg;
+  na.end = end;
+  na.ts = bv.ts;
+  na.stream = bv.stream;
+  SgEmitSink sink;
+  sink.buf = ebuf;
+  sink.cap = cap;
+  sink.count = ecount;
+  sink.overflow = eover;
+  sink.stride = stride;
+  sink.key_bits = kbits;
+  hipLaunchKernelGGL(k_nfa, dim3((unsigned)((kb + 63) / 64)), dim3(64), 0, st, na, bv.cols, h->ddesc, gs->dgeo,
+                     gs->arena, sink, gs->dfail);
+  HIPCHK(hipGetLastError());
+  h->mark(3);
+  unsigned long long total = 0;
+  int32_t over = 0, fcode = 0;
+  HIPCHK(hipMemcpyAsync(&total, ecount, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&over, eover, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&fcode, gs->dfail, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (fcode) throw SgError(fcode, fcode == SG_ECAPACITY
+                                      ? "per-key pool/list capacity exceeded (raise sg_options pool_* / list_cap)"
+                                      : "query shape hits a reference failure path (see DESIGN.md)");
+  if (over) throw SgError(SG_ECAPACITY, "match buffer overflow: push smaller batches");
+  // ---- order matches by (trigger, timer-before-event, key) keeping per-key emission order
+  if (total) {
+    uint64_t* sk = (uint64_t*)h->ws.get("g_sk", 8 * total, st);
+    uint64_t* sk2 = (uint64_t*)h->ws.get("g_sk2", 8 * total, st);
+    uint32_t* ix = (uint32_t*)h->ws.get("g_ix", 4 * total, st);
+    uint32_t* ix2 = (uint32_t*)h->ws.get("g_ix2", 4 * total, st);
+    dim3 g2((unsigned)((total + 255) / 256));
+    hipLaunchKernelGGL(k_sortkeys, g2, blk, 0, st, (int64_t)total, ebuf, stride, sk, ix);
+    HIPCHK(hipGetLastError());
+    int sbits = 31 + 1 + kbits;
+    if (sbits > 64) sbits = 64;
+    size_t tb = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, sk, sk2, ix, ix2, (size_t)total, 0, sbits, st));
+    void* tmp = h->ws.get("g_sort2_tmp", tb, st);
+    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, sk, sk2, ix, ix2, (size_t)total, 0, sbits, st));
+    char* out = h->out.reserve((int64_t)total, d.n_select, st);
+    int32_t ostride = 32 + 8 * d.n_select;
+    hipLaunchKernelGGL(k_gather, g2, blk, 0, st, (int64_t)total, ebuf, stride, ix2, out + (size_t)h->out.n * ostride,
+                       ostride);
+    HIPCHK(hipGetLastError());
+    h->out.n += (int64_t)total;
+  }
+  h->mark(4);
+  h->last_events = n;
+  h->last_matches = (int64_t)total;
+}
+
+void sg_general_reset(SgHandle* h) {
+  if (!h->state || h->state_kind != 2) return;
+  GeneralState* gs = (GeneralState*)h->state;
+  if (gs->arena) hipMemset(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4);
+  h->key_bound_seen = 0;
+}
+
+void sg_general_release(SgHandle* h) {
+  if (!h->state || h->state_kind != 2) return;
+  GeneralState* gs = (GeneralState*)h->state;
+  if (gs->arena) hipFree(gs->arena);
+  if (gs->dgeo) hipFree(gs->dgeo);
+  if (gs->dfail) hipFree(gs->dfail);
+  delete gs;
+  h->state = nullptr;
+  h->state_kind = 0;
+}

@@ -11,7 +11,11 @@
 //   and: true iff both true; or: true iff either true; not: true unless operand is TRUE; is null
 //       (C/executor/condition/{And,Or,Not,IsNull}ConditionExpressionExecutor.java)
 #pragma once
+#ifdef SG_HOST_ONLY
+#include "sg_host_shim.h"
+#else
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 #include "../../include/siddhi_gpu.h"
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -43,30 +44,31 @@ struct Workspace {
   }
 };
 
-struct OutPtrsH {
-  uint64_t* trigger;
-  int64_t* ts;
-  int32_t* key;
-  uint32_t* group;
-  int64_t* vals;
-  uint32_t* vnull;
-};
-
-// Pending match tuples in HBM, in delivery order.
+// Pending match records in HBM, AoS, in delivery order (layout: sg_match_records).
 struct OutStore {
   int64_t n = 0, cap = 0;
   int nsel = 0;
-  uint64_t* trigger = nullptr;
-  int64_t* ts = nullptr;
-  int32_t* key = nullptr;
-  uint32_t* group = nullptr;
-  int64_t* vals = nullptr;
-  uint32_t* vnull = nullptr;
-  template <class P>
-  P reserve(int64_t extra, int n_select, hipStream_t st);
+  int stride = 32;
+  char* rec = nullptr;
+  char* reserve(int64_t extra, int n_select, hipStream_t st) {
+    nsel = n_select;
+    stride = 32 + 8 * n_select;
+    int64_t need = n + extra;
+    if (need > cap) {
+      int64_t nc = std::max<int64_t>(need + need / 4, 1024);
+      void* np = nullptr;
+      if (hipMalloc(&np, (size_t)nc * stride) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc failed for match store");
+      if (rec && n) hipMemcpyAsync(np, rec, (size_t)n * stride, hipMemcpyDeviceToDevice, st);
+      hipStreamSynchronize(st);
+      if (rec) hipFree(rec);
+      rec = (char*)np;
+      cap = nc;
+    }
+    return rec;
+  }
   void release() {
-    hipFree(trigger); hipFree(ts); hipFree(key); hipFree(group); hipFree(vals); hipFree(vnull);
-    trigger = nullptr; ts = nullptr; key = nullptr; group = nullptr; vals = nullptr; vnull = nullptr;
+    if (rec) hipFree(rec);
+    rec = nullptr;
     n = cap = 0;
   }
   void consume(int64_t k, hipStream_t st);
@@ -96,43 +98,17 @@ struct SgHandle {
   int64_t last_events = 0, last_matches = 0;
   int pushes = 0;
   int64_t clock = 0;          // playback clock (TimestampGeneratorImpl.lastEventTimestamp)
+  uint32_t key_bound_seen = 0;
   void* state = nullptr;      // per-shape persistent state (interp / absent)
+  int state_kind = 0;         // 1 every->next closed form, 2 general machine, 3 absence closed form
   void mark(int k) { hipEventRecord(ev[k], stream); }
 };
 
-template <class P>
-P OutStore::reserve(int64_t extra, int n_select, hipStream_t st) {
-  nsel = n_select;
-  int64_t need = n + extra;
-  if (need > cap) {
-    int64_t nc = std::max<int64_t>(need + need / 2, 1024);
-    auto grow = [&](auto*& p, size_t elt) {
-      void* np = nullptr;
-      if (hipMalloc(&np, nc * elt) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc failed for match store");
-      if (p && n) hipMemcpyAsync(np, p, n * elt, hipMemcpyDeviceToDevice, st);
-      hipStreamSynchronize(st);
-      if (p) hipFree(p);
-      p = (std::remove_reference_t<decltype(p)>)np;
-    };
-    grow(trigger, sizeof(uint64_t));
-    grow(ts, sizeof(int64_t));
-    grow(key, sizeof(int32_t));
-    grow(group, sizeof(uint32_t));
-    grow(vals, sizeof(int64_t) * std::max(1, n_select));
-    grow(vnull, sizeof(uint32_t));
-    cap = nc;
-  }
-  P o;
-  o.trigger = trigger;
-  o.ts = ts;
-  o.key = key;
-  o.group = group;
-  o.vals = vals;
-  o.vnull = vnull;
-  return o;
-}
+
 
 void sg_run_every_next(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_every_next_reset(SgHandle* h);
+void sg_every_next_release(SgHandle* h);
 void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_general_reset(SgHandle* h);

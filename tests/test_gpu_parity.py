@@ -16,19 +16,73 @@ def gpu_engine():
     return GpuEngine
 
 
-def _supported(case):
-    from siddhi_amd import compiler as C, lowering as L
-    from parity_util import context
-    nfa = L.lower(context(case["app"]))
-    return nfa.shape == L.SHAPE_EVERY_NEXT_CMP
-
-
-@pytest.mark.parametrize("case", [k for k in KATS if _supported(k)], ids=lambda k: k["name"])
+@pytest.mark.parametrize("case", KATS, ids=lambda k: k["name"])
 def test_kat_on_gpu(case):
     rows, tss = run_kat(case, gpu_engine())
     assert rows == case["expect"]
     rows_o, tss_o = run_kat(case, OracleEngine)
     assert tss == tss_o
+
+
+@pytest.mark.parametrize("case", KATS, ids=lambda k: k["name"])
+def test_kat_on_gpu_general_kernel(case):
+    """Every KAT through the general per-key NFA kernel (closed forms disabled)."""
+    from siddhi_amd._native import GpuEngine
+    rows, tss = run_kat(case, lambda ctx: GpuEngine(ctx, force_general=True))
+    assert rows == case["expect"]
+
+
+def _c4_batch(n, ids):
+    from siddhi_amd.runtime import Batch
+    b = synth_batch("C4", 0, n, keys=ids, rate=1)
+    ts = np.append(b.ts, b.ts[-1] + 5001)
+    st = np.append(b.stream, np.int32(1)).astype(np.int32)
+    cols = [np.append(b.cols[0], 0), np.append(b.cols[1], 0), np.append(b.cols[2], 0).astype(np.int32)]
+    return Batch(n + 1, 0, ts, st, np.zeros(n + 1, np.int32), cols, [None] * 3)
+
+
+@pytest.mark.parametrize("cfg,n,keys,rate", [
+    ("C3", 300_000, 1_000, 1_000),     # literal: the reference emits nothing (SURVEY.md A.5)
+    ("C3b", 300_000, 1_000, 1_000),
+    ("C3c", 300_000, 1_000, 100),
+    ("C2", 200_000, 1_000, 100),       # closed-form shape forced through the general kernel below
+])
+def test_general_kernel_synthetic_parity(cfg, n, keys, rate):
+    from siddhi_amd._native import GpuEngine
+    b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
+    b.key = dense_first_seen(b.key)
+    q = synth.QUERIES[cfg]
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, [b])
+    assert_same(got, want)
+    if cfg == "C3":
+        assert len(want) == 0
+
+
+def test_general_kernel_absence_parity():
+    from siddhi_amd._native import GpuEngine
+    b = _c4_batch(30_000, 2_000)
+    q = synth.QUERIES["C4"]
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True, pool=16384), q, [b])
+    assert len(want) > 0
+    assert_same(got, want)
+
+
+def test_general_kernel_multi_push():
+    from siddhi_amd._native import GpuEngine
+    from siddhi_amd.runtime import Batch
+    b = synth_batch("C3b", 0, 200_000, keys=500, rate=1_000)
+    b.key = dense_first_seen(b.key)
+    q = synth.QUERIES["C3b"]
+    want = run_engine(OracleEngine, q, [b])
+    parts, lo = [], 0
+    for hi in (70_000, 70_001, 150_000, 200_000):
+        parts.append(Batch(hi - lo, lo, b.ts[lo:hi], b.stream[lo:hi], b.key[lo:hi],
+                           [c[lo:hi] for c in b.cols], [None] * len(b.cols)))
+        lo = hi
+    got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, parts)
+    assert_same(got, want)
 
 
 @pytest.mark.parametrize("cfg,n,keys,rate", [
@@ -58,4 +112,24 @@ def test_every_next_edge_cases():
               [ids, np.zeros(10, np.int32), price], [None] * 3)
     want = run_engine(OracleEngine, q, [b])
     got = run_engine(gpu_engine(), q, [b])
+    assert_same(got, want)
+
+
+@pytest.mark.parametrize("cfg,n,keys,rate,splits", [
+    ("C1", 200_000, 1, 1, [50_000, 120_001]),
+    ("C2", 600_000, 5_000, 1_000, [100_000, 100_001, 350_000]),
+])
+def test_every_next_multi_push_carry(cfg, n, keys, rate, splits):
+    """Matches spanning pushes: the carried window must reproduce the single-stream result."""
+    b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
+    b.key = dense_first_seen(b.key)
+    q = synth.QUERIES[cfg]
+    want = run_engine(OracleEngine, q, [b])
+    from siddhi_amd.runtime import Batch
+    parts, lo = [], 0
+    for hi in splits + [n]:
+        parts.append(Batch(hi - lo, lo, b.ts[lo:hi], b.stream[lo:hi], b.key[lo:hi],
+                           [c[lo:hi] for c in b.cols], [None] * len(b.cols)))
+        lo = hi
+    got = run_engine(gpu_engine(), q, parts)
     assert_same(got, want)
