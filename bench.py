@@ -49,7 +49,9 @@ def make_handle(cfg):
     else:
         ctx = L.make_context(app, app.queries[0], None, {})
     nfa = L.lower(ctx)
-    return N.Handle(N.build_desc(nfa), device=torch.cuda.current_device()), nfa
+    opts = N.sg_options()
+    opts.no_carry = 1
+    return N.Handle(N.build_desc(nfa), device=torch.cuda.current_device(), options=opts), nfa
 
 
 def cpu_baseline(cfg, n_sample, keys, rate):
@@ -93,7 +95,7 @@ def main():
     cols = [g["id"], sym, g["price"]]
     torch.cuda.synchronize()
 
-    h, nfa = make_handle(cfg)
+    h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
     stream = torch.cuda.current_stream()
     h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
     keep = []

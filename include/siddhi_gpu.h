@@ -143,6 +143,8 @@ typedef struct sg_batch {
   const int64_t* ts;            /* event timestamps (ms) */
   const int32_t* stream;        /* stream index; -1 = row that only advances the playback clock */
   const int32_t* key;           /* dense partition key id (first-seen order); -1 = null key (dropped) */
+  const uint64_t* index;        /* optional global event index per row (key-sharded sub-batches); NULL =
+                                   base_index + row.  Must be increasing. */
   const void* const* cols;      /* [n_cols] typed columns (width from col_type) */
   const uint8_t* const* nulls;  /* [n_cols] optional 1-byte null flags per row, or NULL */
   int32_t on_device;

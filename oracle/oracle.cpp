@@ -1251,14 +1251,15 @@ void orc_destroy(OrcHandle* h) { delete h; }
 // cols[c] for c in [0, total attrs): column of (stream, attr) flattened in stream order; rows of other
 // streams are ignored. nulls[c] may be NULL. key: dense partition key id (-1 = null key -> dropped).
 int orc_push(OrcHandle* h, int64_t n, uint64_t base_index, const int64_t* ts, const int32_t* stream,
-             const int32_t* key, const void* const* cols, const uint8_t* const* nulls, char* err, int errlen) {
+             const int32_t* key, const uint64_t* index, const void* const* cols, const uint8_t* const* nulls,
+             char* err, int errlen) {
   Engine& E = h->eng;
   try {
     std::vector<int> col_base(E.app.streams.size());
     int c = 0;
     for (size_t s = 0; s < E.app.streams.size(); s++) { col_base[s] = c; c += (int)E.app.streams[s].types.size(); }
     for (int64_t i = 0; i < n; i++) {
-      uint64_t trig = base_index + (uint64_t)i;
+      uint64_t trig = index ? index[i] : base_index + (uint64_t)i;
       int s = stream[i];
       if (E.app.playback) E.setCurrentTimestamp(ts[i], trig);
       if (s < 0) continue;  // pure clock advance / unrelated stream

@@ -31,7 +31,7 @@ def _load():
         lib.orc_create.argtypes = [P, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int]
         lib.orc_destroy.argtypes = [P]
         lib.orc_push.restype = ctypes.c_int
-        lib.orc_push.argtypes = [P, ctypes.c_int64, ctypes.c_uint64, P, P, P, P, P, ctypes.c_char_p, ctypes.c_int]
+        lib.orc_push.argtypes = [P, ctypes.c_int64, ctypes.c_uint64, P, P, P, P, P, P, ctypes.c_char_p, ctypes.c_int]
         lib.orc_output_count.restype = ctypes.c_int64
         lib.orc_output_count.argtypes = [P]
         lib.orc_fetch.restype = ctypes.c_int64
@@ -65,7 +65,11 @@ class OracleEngine:
         ts = np.ascontiguousarray(b.ts, dtype=np.int64)
         st = np.ascontiguousarray(b.stream, dtype=np.int32)
         ky = np.ascontiguousarray(b.key, dtype=np.int32)
-        rc = lib.orc_push(self.h, b.n, b.base_index, ts.ctypes.data, st.ctypes.data, ky.ctypes.data,
+        ix = None
+        if getattr(b, "index", None) is not None:
+            ixa = np.ascontiguousarray(b.index, np.uint64)
+            ix = ixa.ctypes.data
+        rc = lib.orc_push(self.h, b.n, b.base_index, ts.ctypes.data, st.ctypes.data, ky.ctypes.data, ix,
                           ctypes.cast(cols, ctypes.c_void_p), ctypes.cast(nul, ctypes.c_void_p), err, 512)
         if rc != 0:
             raise RuntimeError("oracle: " + err.value.decode())

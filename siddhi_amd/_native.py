@@ -58,7 +58,7 @@ class sg_options(ct.Structure):
 
 class sg_batch(ct.Structure):
     _fields_ = [("n", I64), ("base_index", U64), ("ts", ct.c_void_p), ("stream", ct.c_void_p),
-                ("key", ct.c_void_p), ("cols", ct.c_void_p), ("nulls", ct.c_void_p),
+                ("key", ct.c_void_p), ("index", ct.c_void_p), ("cols", ct.c_void_p), ("nulls", ct.c_void_p),
                 ("on_device", I32), ("key_bound", I32)]
 
 
@@ -254,15 +254,15 @@ class Handle:
             pass
 
 
-def make_batch(n, base_index, ts, stream, key, cols, nulls, on_device, key_bound=0, keep=None):
+def make_batch(n, base_index, ts, stream, key, cols, nulls, on_device, key_bound=0, keep=None, index=0):
     """Assemble an sg_batch from raw pointers (ints); `keep` collects ctypes arrays to keep alive."""
     ncol = len(cols)
     carr = (ct.c_void_p * max(ncol, 1))(*[c for c in cols])
     narr = (ct.c_void_p * max(ncol, 1))(*[(x if x else None) for x in nulls])
     if keep is not None:
         keep += [carr, narr]
-    return sg_batch(n, base_index, ts, stream, key, ct.cast(carr, ct.c_void_p), ct.cast(narr, ct.c_void_p),
-                    on_device, key_bound)
+    return sg_batch(n, base_index, ts, stream, key, index or None, ct.cast(carr, ct.c_void_p),
+                    ct.cast(narr, ct.c_void_p), on_device, key_bound)
 
 
 class GpuEngine:
@@ -290,9 +290,14 @@ class GpuEngine:
         cols = [np.ascontiguousarray(c) for c in b.cols]
         keep += [ts, st, ky] + cols + [x for x in b.nulls if x is not None]
         kb = int(ky.max()) + 1 if len(ky) and ky.max() >= 0 else 1
+        ix = 0
+        if getattr(b, "index", None) is not None:
+            ixa = np.ascontiguousarray(b.index, np.uint64)
+            keep.append(ixa)
+            ix = ixa.ctypes.data
         sb = make_batch(b.n, b.base_index, ts.ctypes.data, st.ctypes.data, ky.ctypes.data,
                         [c.ctypes.data for c in cols], [(x.ctypes.data if x is not None else 0) for x in b.nulls],
-                        0, kb, keep)
+                        0, kb, keep, index=ix)
         self.handle.push(sb)
 
     def fetch(self):

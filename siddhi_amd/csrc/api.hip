@@ -106,6 +106,7 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
       bv.ts = b->ts;
       bv.stream = b->stream;
       bv.key = b->key;
+      bv.index = b->index;
       for (int c = 0; c < d.n_cols; ++c) {
         bv.cols.col[c] = b->cols ? b->cols[c] : nullptr;
         bv.cols.nul[c] = b->nulls ? b->nulls[c] : nullptr;
@@ -120,6 +121,7 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
       bv.ts = (const int64_t*)up("in_ts", b->ts, sizeof(int64_t) * n);
       bv.stream = (const int32_t*)up("in_stream", b->stream, sizeof(int32_t) * n);
       bv.key = (const int32_t*)up("in_key", b->key, sizeof(int32_t) * n);
+      bv.index = (const uint64_t*)up("in_index", b->index, sizeof(uint64_t) * n);
       for (int c = 0; c < d.n_cols; ++c) {
         char nm[32];
         snprintf(nm, sizeof nm, "in_col%d", c);

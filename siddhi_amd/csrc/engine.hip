@@ -182,6 +182,7 @@ struct MatchArgs {
   int32_t n_select;
   int32_t stride;        // output record bytes
   int64_t out_base;
+  const uint64_t* index; // optional global index per batch row
 };
 
 template <class T>
@@ -244,7 +245,7 @@ __global__ void __launch_bounds__(256) k_match(MatchArgs a, const Rec<T, NP>* __
           vals[s] = bits;
         }
         uint64_t* h64 = (uint64_t*)o;
-        h64[0] = a.base_index + q.row;
+        h64[0] = a.index ? a.index[q.row] : a.base_index + q.row;
         h64[1] = (uint64_t)q.ts;
         uint32_t* h32 = (uint32_t*)(o + 16);
         h32[0] = k;
@@ -419,6 +420,7 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, ProjPlan
   ma.n_select = d.n_select;
   ma.stride = 32 + 8 * d.n_select;
   ma.out_base = 0;
+  ma.index = bv.index;
   auto launch = [&](bool write, char* out) {
     switch (op) {
       case 2: launch_match<T, NP, 2>(write, grdt, blk, st, ma, srec, skeys, cnt, off, pp, bv.cols, h->ddesc, out); break;
@@ -451,21 +453,52 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, ProjPlan
     h->out.n += total;
   }
   h->mark(4);
-  // ---- carry rows still inside the window into the next push
+  // ---- carry rows still inside the window into the next push: the surviving old carry plus the
+  // time-ordered tail of this batch (pre-sort records [nc + lo, nt) with ts >= last_ts - T)
   if (h->opt.no_carry == 0) {
     int64_t min_ts = last_ts - d.within;
-    uint8_t* fl = (uint8_t*)h->ws.get("carry_fl", nt, st);
-    hipLaunchKernelGGL((k_carry_flags<T, NP>), grdt, blk, 0, st, srec, skeys, nt, min_ts, kb, d.partitioned, fl);
-    HIPCHK(hipGetLastError());
-    int64_t* cnt_sel = (int64_t*)h->ws.get("carry_cnt", sizeof(int64_t), st);
-    R* crec = (R*)h->ws.get("carry_rec_tmp", sizeof(R) * nt, st);
-    size_t tb = 0;
-    HIPCHK(rocprim::select(nullptr, tb, srec, fl, crec, cnt_sel, (size_t)nt, st));
-    void* tmp = h->ws.get("carry_tmp", tb, st);
-    HIPCHK(rocprim::select(tmp, tb, srec, fl, crec, cnt_sel, (size_t)nt, st));
-    int64_t ncar = 0;
-    HIPCHK(hipMemcpyAsync(&ncar, cnt_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    int64_t lo = 0;
+    {
+      // first batch row with ts >= min_ts (timestamps are non-decreasing; checked above)
+      std::vector<int64_t> probe(1);
+      int64_t a0 = 0, a1 = n;
+      while (a0 < a1) {
+        int64_t mid = (a0 + a1) / 2;
+        HIPCHK(hipMemcpy(probe.data(), bv.ts + mid, 8, hipMemcpyDeviceToHost));
+        if (probe[0] < min_ts) a0 = mid + 1; else a1 = mid;
+      }
+      lo = a0;
+    }
+    int64_t tail = n - lo;
+    int64_t keep_old = 0;
+    R* crec = (R*)h->ws.get("carry_rec_tmp", sizeof(R) * (nc + tail + 1), st);
+    uint32_t* ck = (uint32_t*)h->ws.get("carry_keys_tmp", sizeof(uint32_t) * (nc + tail + 1), st);
+    if (nc) {
+      // old carry sits unsorted at rec[0, nc) (copied before k_pack)
+      uint8_t* fl = (uint8_t*)h->ws.get("carry_fl", nc, st);
+      hipLaunchKernelGGL((k_carry_flags<T, NP>), dim3((unsigned)((nc + 255) / 256)), blk, 0, st, rec, keys, nc, min_ts,
+                         kb, d.partitioned, fl);
+      HIPCHK(hipGetLastError());
+      int64_t* cnt_sel = (int64_t*)h->ws.get("carry_cnt", sizeof(int64_t), st);
+      size_t tb = 0;
+      HIPCHK(rocprim::select(nullptr, tb, rec, fl, crec, cnt_sel, (size_t)nc, st));
+      void* tmp = h->ws.get("carry_tmp", tb, st);
+      HIPCHK(rocprim::select(tmp, tb, rec, fl, crec, cnt_sel, (size_t)nc, st));
+      if (d.partitioned) {
+        size_t tb2 = 0;
+        HIPCHK(rocprim::select(nullptr, tb2, keys, fl, ck, cnt_sel, (size_t)nc, st));
+        void* tmp2 = h->ws.get("carry_tmp2", tb2, st);
+        HIPCHK(rocprim::select(tmp2, tb2, keys, fl, ck, cnt_sel, (size_t)nc, st));
+      }
+      HIPCHK(hipMemcpyAsync(&keep_old, cnt_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    if (tail) {
+      HIPCHK(hipMemcpyAsync(crec + keep_old, rec + nc + lo, sizeof(R) * tail, hipMemcpyDeviceToDevice, st));
+      if (d.partitioned)
+        HIPCHK(hipMemcpyAsync(ck + keep_old, keys + nc + lo, sizeof(uint32_t) * tail, hipMemcpyDeviceToDevice, st));
+    }
+    int64_t ncar = keep_old + tail;
     if (ncar && pp.np == 0) {
       for (int s = 0; s < d.n_select; ++s)
         if (pp.kind[s] == 3 && pp.src[s] == 0)
@@ -476,15 +509,10 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, ProjPlan
       HIPCHK(hipMemcpyAsync(keep, crec, sizeof(R) * ncar, hipMemcpyDeviceToDevice, st));
       hipLaunchKernelGGL((k_mark_carry<T, NP>), dim3((unsigned)((ncar + 255) / 256)), blk, 0, st, keep, ncar);
       HIPCHK(hipGetLastError());
-    }
-    if (d.partitioned && ncar) {
-      uint32_t* ck = (uint32_t*)h->ws.get("carry_keys_tmp", sizeof(uint32_t) * nt, st);
-      size_t tb2 = 0;
-      HIPCHK(rocprim::select(nullptr, tb2, skeys, fl, ck, cnt_sel, (size_t)nt, st));
-      void* tmp2 = h->ws.get("carry_tmp2", tb2, st);
-      HIPCHK(rocprim::select(tmp2, tb2, skeys, fl, ck, cnt_sel, (size_t)nt, st));
-      uint32_t* keepk = (uint32_t*)h->ws.get("carry_keys", sizeof(uint32_t) * ncar, st);
-      HIPCHK(hipMemcpyAsync(keepk, ck, sizeof(uint32_t) * ncar, hipMemcpyDeviceToDevice, st));
+      if (d.partitioned) {
+        uint32_t* keepk = (uint32_t*)h->ws.get("carry_keys", sizeof(uint32_t) * ncar, st);
+        HIPCHK(hipMemcpyAsync(keepk, ck, sizeof(uint32_t) * ncar, hipMemcpyDeviceToDevice, st));
+      }
     }
     es->n_carry = ncar;
   } else {

@@ -72,6 +72,7 @@ struct KeyMachine {
   uint64_t base_index;
   // current step
   uint64_t trigger;
+  int64_t trig_local;   // batch row of the trigger (ordering key)
   int phase;
   uint32_t group;
   int64_t now;          // playback clock value (TimestampGeneratorImpl.currentTime)
@@ -300,7 +301,7 @@ struct KeyMachine {
     unsigned long long o = atomic_bump(sink.count);
     if ((int64_t)o >= sink.cap) { *sink.overflow = 1; return; }
     char* r = sink.buf + (size_t)o * (size_t)sink.stride;
-    uint64_t tl = trigger - base_index;
+    uint64_t tl = (uint64_t)trig_local;
     uint64_t* h64 = (uint64_t*)r;
     h64[0] = (tl << (sink.key_bits + 1)) | ((uint64_t)(phase & 1) << sink.key_bits) | (uint32_t)key;
     h64[1] = trigger;
@@ -746,8 +747,7 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start) {
     // earliest timer trigger of this key's schedulers
     int64_t ltim = nrows;
     if (A > 0 && m.hdr()[K_CREATED]) {
-      int64_t p = m.pos() - (int64_t)m.base_index;   // last processed local row (may be < 0)
-      int64_t from = p + 1 < 0 ? 0 : p + 1;
+      int64_t from = rows.first_after(m.pos());   // first local row with global index > pos
       for (int ai = 0; ai < A; ++ai) {
         if (m.tq_empty(ai)) continue;
         int64_t r = rows.find_ge(from, m.tq_head(ai));
@@ -756,7 +756,8 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start) {
     }
     if (ltim < nrows && ltim <= lev) {
       m.now = rows.ts(ltim);
-      m.trigger = m.base_index + (uint64_t)ltim;
+      m.trigger = rows.index_of(ltim);
+      m.trig_local = ltim;
       m.phase = 0;
       for (int ai = 0; ai < A && !m.failed; ++ai) {
         m.group = (uint32_t)ai << 16;
@@ -768,7 +769,7 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start) {
           m.absent_timer(abs_state[ai], t);
         }
       }
-      m.set_pos((int64_t)m.base_index + ltim);
+      m.set_pos((int64_t)rows.index_of(ltim));
       if (ltim < lev) continue;
     }
     if (i >= nown) break;
@@ -776,6 +777,7 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start) {
     rows.fill(lev, row);
     m.now = row.ts;
     m.trigger = row.index;
+    m.trig_local = lev;
     if (!m.hdr()[K_CREATED]) m.create_runtime();
     if (m.failed) break;
     m.maybe_gc();

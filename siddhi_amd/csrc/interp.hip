@@ -76,6 +76,21 @@ struct DevRows {
   const SgCols* cols;
   const DevDesc* d;
   uint64_t base;
+  const uint64_t* index;
+  __device__ uint64_t index_of(int64_t r) { return index ? index[r] : base + (uint64_t)r; }
+  __device__ int64_t first_after(int64_t pos) {
+    if (!index) {
+      int64_t p = pos - (int64_t)base + 1;
+      return p < 0 ? 0 : (p > n ? n : p);
+    }
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)index[mid] <= pos) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  }
   __device__ int64_t n_own() { return nown; }
   __device__ int64_t own_local(int64_t i) { return (int64_t)rows[i]; }
   __device__ int64_t n_rows() { return n; }
@@ -92,7 +107,7 @@ struct DevRows {
   }
   __device__ void fill(int64_t r, SgRow& row) {
     row.ts = ts[r];
-    row.index = base + (uint64_t)r;
+    row.index = index_of(r);
     row.stream = stream ? stream[r] : 0;
     row.nullmask = 0;
     for (int k = 0; k < d->n_ret; ++k) {
@@ -118,6 +133,7 @@ struct NfaArgs {
   const uint32_t* end;
   const int64_t* ts;
   const int32_t* stream;
+  const uint64_t* index;
 };
 
 __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDesc* __restrict__ dd,
@@ -154,6 +170,7 @@ __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDes
   rows.cols = &cols;
   rows.d = dd;
   rows.base = a.base_index;
+  rows.index = a.index;
   sg_run_key(m, rows, !a.partitioned);
   if (m.failed) atomicCAS(fail_code, 0, m.failed);
 }
@@ -285,6 +302,7 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   na.end = end;
   na.ts = bv.ts;
   na.stream = bv.stream;
+  na.index = bv.index;
   SgEmitSink sink;
   sink.buf = ebuf;
   sink.cap = cap;

@@ -80,6 +80,7 @@ struct BatchView {
   const int64_t* ts;
   const int32_t* stream;
   const int32_t* key;
+  const uint64_t* index;
   SgCols cols;
   int32_t key_bound;
 };

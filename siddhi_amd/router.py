@@ -1,0 +1,52 @@
+"""Multi-GPU routing for partitioned queries.
+
+Keys are fully isolated (one cloned runtime per key, C/partition/PartitionRuntime.java:261-308), so the
+node shards by key with no data-path collective: key k belongs to rank mix64(k) % G.  Each rank runs its
+own engine on its rows (global event indices preserved) and the per-rank match streams are merged by
+(trigger index, timer-before-event, key) — the reference's delivery order, since timer emissions of one
+clock advance follow key registration (first-seen) order and an event's own matches come from its key.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+
+def mix64(k: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = k.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+        return z ^ (z >> np.uint64(31))
+
+
+def shard_of(keys: np.ndarray, world: int) -> np.ndarray:
+    """Owning rank of each dense key id (rows with key < 0 go to rank 0, which drops them)."""
+    r = (mix64(np.maximum(keys, 0)) % np.uint64(world)).astype(np.int32)
+    return r
+
+
+def shard_batch(batch, rank: int, world: int):
+    """Rows of `batch` owned by `rank` (arrival order and global indices kept)."""
+    from .runtime import Batch
+    own = shard_of(batch.key, world) == rank
+    idx = np.nonzero(own)[0]
+    # rows keep their global index: engines see a sparse batch through an explicit index column
+    gidx = (batch.index[idx] if batch.index is not None else batch.base_index + idx).astype(np.uint64)
+    return idx, Batch(len(idx), int(gidx[0]) if len(idx) else batch.base_index, batch.ts[idx], batch.stream[idx],
+                      batch.key[idx], [c[idx] for c in batch.cols], [None if x is None else x[idx] for x in batch.nulls],
+                      gidx)
+
+
+def merge(parts):
+    """Merge per-rank Outputs (each already in delivery order) into the node's delivery order."""
+    from .runtime import Outputs
+    if not parts:
+        raise ValueError("nothing to merge")
+    cat = Outputs(*[np.concatenate([getattr(p, f) for p in parts]) for f in
+                    ("trigger", "ts", "key", "group", "vals", "vnull")])
+    phase = (cat.group >> np.uint32(24)).astype(np.uint64)
+    order = np.lexsort((np.arange(len(cat)), cat.key.astype(np.int64), phase, cat.trigger))
+    return Outputs(*[getattr(cat, f)[order] for f in ("trigger", "ts", "key", "group", "vals", "vnull")])

@@ -75,6 +75,7 @@ class Batch:
     key: np.ndarray      # int32[n]   dense partition key, -1 = null key / not partitioned stream
     cols: List[np.ndarray]
     nulls: List[Optional[np.ndarray]]
+    index: Optional[np.ndarray] = None   # global event index per row (key-sharded sub-batches)
 
 
 @dataclass

@@ -23,6 +23,11 @@ struct HostRows {
   const sg_batch* b;
   const sg_nfa_desc* d;
   const std::vector<int64_t>* own;
+  uint64_t index_of(int64_t r) { return b->index ? b->index[r] : b->base_index + (uint64_t)r; }
+  int64_t first_after(int64_t pos) {
+    if (!b->index) { int64_t p = pos - (int64_t)b->base_index + 1; return p < 0 ? 0 : (p > b->n ? b->n : p); }
+    return std::upper_bound(b->index, b->index + b->n, (uint64_t)pos, [](uint64_t v, uint64_t x) { return v < x; }) - b->index;
+  }
   int64_t n_own() { return (int64_t)own->size(); }
   int64_t own_local(int64_t i) { return (*own)[i]; }
   int64_t n_rows() { return b->n; }
@@ -34,7 +39,7 @@ struct HostRows {
   }
   void fill(int64_t r, SgRow& row) {
     row.ts = b->ts[r];
-    row.index = b->base_index + (uint64_t)r;
+    row.index = index_of(r);
     row.stream = b->stream ? b->stream[r] : 0;
     row.nullmask = 0;
     for (int k = 0; k < d->n_ret; ++k) {

@@ -52,9 +52,14 @@ class HostInterpEngine:
         ky = np.ascontiguousarray(b.key, np.int32)
         cols = [np.ascontiguousarray(c) for c in b.cols]
         keep += [ts, st, ky] + cols
+        ix = 0
+        if getattr(b, "index", None) is not None:
+            ixa = np.ascontiguousarray(b.index, np.uint64)
+            keep.append(ixa)
+            ix = ixa.ctypes.data
         sb = self.N.make_batch(b.n, b.base_index, ts.ctypes.data, st.ctypes.data, ky.ctypes.data,
                                [c.ctypes.data for c in cols],
-                               [(x.ctypes.data if x is not None else 0) for x in b.nulls], 0, 0, keep)
+                               [(x.ctypes.data if x is not None else 0) for x in b.nulls], 0, 0, keep, index=ix)
         rc = self.lib.hi_push(self.h, ct.byref(sb))
         if rc != 0:
             raise RuntimeError(f"host interp error {rc}")

@@ -44,7 +44,7 @@ def run_engine(engine_cls, query_text, batches, **kw):
     outs = []
     for b in batches:
         if not ctx.partitioned:
-            b = Batch(b.n, b.base_index, b.ts, b.stream, np.zeros(b.n, np.int32), b.cols, b.nulls)
+            b = Batch(b.n, b.base_index, b.ts, b.stream, np.zeros(b.n, np.int32), b.cols, b.nulls, b.index)
         eng.push(b)
         outs.append(eng.fetch())
     eng.close()

@@ -61,7 +61,7 @@ def test_general_kernel_synthetic_parity(cfg, n, keys, rate):
 
 def test_general_kernel_absence_parity():
     from siddhi_amd._native import GpuEngine
-    b = _c4_batch(30_000, 2_000)
+    b = _c4_batch(4_000, 500)    # one GPU thread walks thousands of pending partials: keep it small
     q = synth.QUERIES["C4"]
     want = run_engine(OracleEngine, q, [b])
     got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True, pool=16384), q, [b])
