@@ -7,7 +7,8 @@ Workload (BASELINE.json configs[1]):
     select e1.id as id1, e2.id as id2, e1.price as p1, e2.price as p2 insert into M; end;
   100M synthetic events per GPU (SplitMix64 generator, siddhi_amd/synth.py), 10k keys, 1000 events/ms.
 A step = one sg_push of the whole 100M-event batch (inputs already resident in HBM) through the HIP
-pipeline (predicate-eval/pack -> key partition -> match count -> scan -> match write) on a fresh state.
+pipeline (predicate-eval bitmasks -> key partition -> per-key walker count -> scan -> walker write) on a
+fresh state.
 Multi-GPU (one process per GPU, torchrun): weak scaling, rank r owns the disjoint key range
 [r*K, (r+1)*K) with its own 100M-event stream; no data-path collective (keys never interact).
 
@@ -74,7 +75,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--events", type=int, default=0, help="events per GPU per step (default: config size, max 1e8)")
-    ap.add_argument("--cpu-sample", type=int, default=3_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=12_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -139,9 +140,9 @@ def main():
     # whole path 16.125 B/event (ts 8 + key 4 + price 4 + bit) + 36 B/match
     pred_bytes = 4.125 * n
     path_bytes = 16.125 * n + 36.0 * matches
-    stages = {"pred_pack_ms": stage[0], "key_partition_ms": stage[1], "match_count_scan_ms": stage[2],
-              "match_write_ms": stage[3], "kernels_total_ms": stage[4]}
-    names = ["pred_pack_ms", "key_partition_ms", "match_count_scan_ms", "match_write_ms"]
+    stages = {"pred_eval_ms": stage[0], "key_partition_ms": stage[1], "walk_count_scan_ms": stage[2],
+              "walk_write_ms": stage[3], "kernels_total_ms": stage[4]}
+    names = ["pred_eval_ms", "key_partition_ms", "walk_count_scan_ms", "walk_write_ms"]
     dom = names[int(np.argmax(stage[:4]))]
     path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9
     pred_gbs = pred_bytes / (stage[0] * 1e-3) / 1e9

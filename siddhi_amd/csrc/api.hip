@@ -244,7 +244,12 @@ int sg_get_timing(sg_handle* hh, sg_timing* t) {
     HIPCHK(hipEventElapsedTime(&a, h.ev[0], h.ev[1]));
     HIPCHK(hipEventElapsedTime(&b, h.ev[1], h.ev[2]));
     HIPCHK(hipEventElapsedTime(&c, h.ev[2], h.ev[3]));
-    HIPCHK(hipEventElapsedTime(&d, h.ev[3], h.ev[4]));
+    HIPCHK(hipEventElapsedTime(&d, h.split_out ? h.ev[5] : h.ev[3], h.ev[4]));
+    if (h.extra_marks) {
+      float x = 0;
+      HIPCHK(hipEventElapsedTime(&x, h.ev[6], h.ev[7]));
+      c += x;
+    }
     t->pred_ms = a;
     t->partition_ms = b;
     t->match_ms = c;

@@ -102,6 +102,8 @@ struct SgHandle {
   uint32_t key_bound_seen = 0;
   void* state = nullptr;      // per-shape persistent state (interp / absent)
   int state_kind = 0;         // 1 every->next closed form, 2 general machine, 3 absence closed form
+  int split_out = 0;          // 1: output stage timed from ev[5] (host work between ev[3] and ev[5])
+  int extra_marks = 0;        // 1: ev[6]..ev[7] hold an extra match-stage interval (overflow re-pass)
   void mark(int k) { hipEventRecord(ev[k], stream); }
 };
 
