@@ -1,4 +1,5 @@
-// MI355X closed-form pipeline for  every A[l] -> B[l' and B.x OP A.x] within T
+#pragma once
+// engine_impl.h — MI355X closed-form pipeline for  every A[l] -> B[l' and B.x OP A.x] within T
 // (SG_SHAPE_EVERY_NEXT_CMP: configs C1/C2/C5).
 //
 // Semantics, restated from StreamPreStateProcessor.processAndReturn
@@ -46,6 +47,8 @@
 
 #include "sg_device.h"
 #include "sg_engine.h"
+
+// (instantiated per value type by engine_{f32,f64,i32,i64}.hip so the build parallelises)
 
 #define HIPCHK(x)                                                                                   \
   do {                                                                                              \
@@ -98,7 +101,7 @@ __device__ __forceinline__ bool eval_row(const PredArgs& a, const SgCols& cols, 
 }
 
 // general: any program, scalar loads (rows 4l+s of the tile)
-__global__ void __launch_bounds__(256) k_pred(PredArgs a, SgCols cols, const DevDesc* __restrict__ dd,
+static __global__ void __launch_bounds__(256) k_pred(PredArgs a, SgCols cols, const DevDesc* __restrict__ dd,
                                               uint64_t* __restrict__ cand_m, uint64_t* __restrict__ cons_m) {
   const int lane = threadIdx.x & 63;
   const int64_t ntiles = (a.n + 255) >> 8;
@@ -124,50 +127,53 @@ __global__ void __launch_bounds__(256) k_pred(PredArgs a, SgCols cols, const Dev
 }
 
 // simple: A = `col CMP const` on a 4-byte column, stream column absent, B consumers = all rows.
+// The constant is pre-converted to the compare domain (f32 / f64 / i64, ExpressionParser's promotion).
 // One 16-B load per lane per tile, 4 tiles in flight per wave.
-template <class V>
-__global__ void __launch_bounds__(256) k_pred_simple(PredArgs a, const V* __restrict__ col,
-                                                     const uint8_t* __restrict__ nul,
-                                                     uint64_t* __restrict__ cand_m) {
+template <class D>
+__device__ __forceinline__ bool cmp_dom(int op, D a, D b) {
+  switch (op) {
+    case 0: return a == b;
+    case 1: return a != b;
+    case 2: return a > b;
+    case 3: return a >= b;
+    case 4: return a < b;
+    default: return a <= b;
+  }
+}
+template <class V, class D>
+__global__ void __launch_bounds__(256) k_pred_simple(int64_t n, int op, D c, const V* __restrict__ col,
+                                                     const uint8_t* __restrict__ nul, uint64_t* __restrict__ cand_m) {
   const int lane = threadIdx.x & 63;
-  const int64_t ntiles = (a.n + 255) >> 8;
+  const int64_t ntiles = (n + 255) >> 8;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t full = a.n >> 8;   // tiles without a tail
-  SgVal c = sg_val_from_bits(a.s_cbits, a.s_ctype, 0);
+  const int64_t full = n >> 8;   // tiles without a tail
+  typedef V V4 __attribute__((ext_vector_type(4)));
   for (int64_t g0 = wave; g0 < ntiles; g0 += 4 * nwaves) {
-    V x[4][4];
-    bool nn[4][4];
+    V4 x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int64_t g = g0 + (int64_t)u * nwaves;
       int64_t i = g * 256 + lane * 4;
       if (g < full) {
-        typedef V V4 __attribute__((ext_vector_type(4)));
-        V4 q = *(const V4*)(col + i);
-        x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
+        x[u] = *(const V4*)(col + i);
       } else {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) x[u][s] = (g < ntiles && i + s < a.n) ? col[i + s] : V(0);
+        x[u].x = (g < ntiles && i + 0 < n) ? col[i + 0] : V(0);
+        x[u].y = (g < ntiles && i + 1 < n) ? col[i + 1] : V(0);
+        x[u].z = (g < ntiles && i + 2 < n) ? col[i + 2] : V(0);
+        x[u].w = (g < ntiles && i + 3 < n) ? col[i + 3] : V(0);
       }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) nn[u][s] = nul ? (g < ntiles && i + s < a.n && nul[i + s]) : false;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       int64_t g = g0 + (int64_t)u * nwaves;
       if (g >= ntiles) break;
       int64_t i = g * 256 + lane * 4;
+      V xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        SgVal v;
-        v.type = a.s_type;
-        v.null = nn[u][s];
-        v.i = 0;
-        v.d = 0.0;
-        if (a.s_type == SG_T_FLOAT) v.d = (double)(float)x[u][s];
-        else v.i = (int64_t)x[u][s];
-        bool ok = (i + s < a.n) && !v.null && sg_cmp(a.s_op, a.s_dom, v, c);
+        bool ok = (i + s < n) && cmp_dom<D>(op, (D)xs[s], c);
+        if (nul && ok) ok = !nul[i + s];
         uint64_t m = __ballot(ok);
         if (lane == s) cand_m[g * 4 + s] = m;
       }
@@ -190,6 +196,9 @@ struct Virt {
   const uint8_t* c_flags;
   const void* c_val_a;
   const void* c_val_b;
+  const void* pcol;           // e1 payload column (one projected attribute carried in the pending list)
+  const void* c_pcol;
+  int32_t pw, pfloat;         // width 4/8; FLOAT bits zero-extended, integral sign-extended
 };
 
 struct KeyOf {   // sort key of virtual row r (the dense partition key; -1 sorts last)
@@ -215,21 +224,123 @@ __device__ __forceinline__ T v_val(const Virt& v, uint32_t r, bool side_a) {
   return ((const T*)(side_a ? v.val_a : v.val_b))[r - v.nc];
 }
 
-__global__ void k_bounds(const uint32_t* __restrict__ skey, int64_t n, uint32_t kb, uint32_t* __restrict__ seg_b,
-                         uint32_t* __restrict__ seg_e) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  uint32_t k = skey[t];
-  if (k >= kb) return;
-  if (t == 0 || skey[t - 1] != k) seg_b[k] = (uint32_t)t;
-  if (t == n - 1 || skey[t + 1] != k) seg_e[k] = (uint32_t)(t + 1);
+__device__ __forceinline__ int64_t v_payload(const Virt& v, uint32_t r) {
+  const void* c = r < v.nc ? v.c_pcol : v.pcol;
+  uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
+  if (v.pw == 8) return ((const int64_t*)c)[rr];
+  int32_t x = ((const int32_t*)c)[rr];
+  return v.pfloat ? (int64_t)(uint32_t)x : (int64_t)x;
+}
+
+// Walker record: one row of one key as the walkers read it (key-sorted for partitioned queries).
+// rowf = virtual row | condition flags << 30.  16 bytes for 4-byte compared values: rocPRIM's tuned
+// 8-bit-digit onesweep path, and 8 records per 128-B line for the walkers' whole-line loads.
+static const uint32_t ROW_MASK = 0x3fffffffu;
+template <class T, bool WIDE = (sizeof(T) > 4)>
+struct WRec {
+  int64_t ts;
+  uint32_t rowf;
+  T val;
+};
+template <class T>
+struct WRec<T, true> {
+  int64_t ts;
+  uint32_t rowf;
+  uint32_t pad;
+  T val;
+};
+
+template <class T>
+struct PackFn {   // builds the walker record of virtual row r (coalesced when r is sequential)
+  Virt v;
+  __host__ __device__ WRec<T> operator()(uint32_t r) const {
+    WRec<T> o;
+#ifdef __HIP_DEVICE_COMPILE__
+    uint32_t f = v_flags(v, r);
+    o.ts = v_ts(v, r);
+    o.rowf = r | (f << 30);
+    o.val = v_val<T>(v, r, (f & F_CAND) || v.val_a == v.val_b);
+#else
+    (void)r;
+    memset(&o, 0, sizeof(o));
+#endif
+    return o;
+  }
+};
+
+template <class T>
+struct Src {   // position -> record: the key-sorted records, or (unpartitioned) the rows themselves
+  const WRec<T>* srec;
+  PackFn<T> pk;
+  __device__ __forceinline__ WRec<T> at(uint32_t p) const { return srec ? srec[p] : pk(p); }
+  __device__ __forceinline__ uint32_t row(uint32_t p) const { return srec ? (srec[p].rowf & ROW_MASK) : p; }
+  __device__ __forceinline__ int64_t ts(uint32_t p) const { return srec ? srec[p].ts : v_ts(pk.v, p); }
+};
+
+// Records per group load: G records = a whole number of 128-B lines, loaded by one lane at once so a
+// line is fetched into registers exactly once (thousands of per-lane streams would otherwise thrash L2).
+template <class T>
+struct Grp {
+  static constexpr int G = sizeof(WRec<T>) == 16 ? 8 : 16;
+  static constexpr int QW = G * (int)sizeof(WRec<T>) / 16;
+  typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+  U4 q[QW];
+  __device__ __forceinline__ void load(const WRec<T>* base) {
+    const U4* p = (const U4*)base;
+#pragma unroll
+    for (int j = 0; j < QW; ++j) q[j] = __builtin_nontemporal_load(p + j);
+  }
+  __device__ __forceinline__ WRec<T> rec(int i) const {
+    WRec<T> r;
+    __builtin_memcpy(&r, (const char*)q + i * sizeof(WRec<T>), sizeof(WRec<T>));
+    return r;
+  }
+};
+
+// walker records + sort keys of every virtual row, in arrival order (coalesced)
+template <class T>
+__global__ void __launch_bounds__(256) k_pack(PackFn<T> pk, KeyOf kf, int64_t nt, WRec<T>* __restrict__ rec,
+                                              uint32_t* __restrict__ keys) {
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nt; r += stride) {
+    rec[r] = pk((uint32_t)r);
+    keys[r] = kf((uint32_t)r);
+  }
+}
+
+static __global__ void __launch_bounds__(256) k_bounds(const uint32_t* __restrict__ skey, int64_t n, uint32_t kb,
+                                                       uint32_t* __restrict__ seg_b, uint32_t* __restrict__ seg_e) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t t0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; t0 < n; t0 += stride) {
+    uint32_t k[6];
+    k[0] = t0 > 0 ? skey[t0 - 1] : 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) k[j + 1] = (t0 + j < n) ? skey[t0 + j] : 0xfffffffeu;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int64_t t = t0 + j;
+      uint32_t x = k[j + 1];
+      if (t >= n || x >= kb) continue;
+      if (k[j] != x) seg_b[x] = (uint32_t)t;
+      if (k[j + 2] != x) seg_e[x] = (uint32_t)(t + 1);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
 struct ProjPlan {
-  // per select column: src 0 = e1 row (pending partial), 1 = e2 row (trigger);
-  // kind 1 = the compared value, 2 = null (chain index beyond a single-event slot), 3 = column gather
+  // per select column: src 0 = e1 row (pending partial), 1 = e2 row (trigger); kind 0 = e1 payload carried
+  // in the pending list, 1 = the compared value, 2 = null (chain index beyond a single-event slot),
+  // 3 = column gather by row
   int32_t src[SG_MAX_SELECT], kind[SG_MAX_SELECT], col[SG_MAX_SELECT], type[SG_MAX_SELECT];
+};
+
+// A delivered match as the record walk leaves it at its final slot: e1/e2 virtual rows, e1's compared value
+// and e1's payload attribute (both taken from the pending list, so no gather reaches back into the window).
+struct MRec {
+  uint32_t r1, r2;
+  int64_t v1;                 // e1 compared-value bits
+  int64_t p1;                 // e1 payload bits
 };
 
 struct UnitDesc {
@@ -283,42 +394,51 @@ template <> __device__ __forceinline__ int64_t val_bits<double>(double v) { retu
 template <> __device__ __forceinline__ int64_t val_bits<int32_t>(int32_t v) { return (int64_t)v; }
 template <> __device__ __forceinline__ int64_t val_bits<int64_t>(int64_t v) { return v; }
 
-// Pending list storage.  LDS: ring of STACK_CAP entries per lane (SoA, lane-strided: conflict-free),
-// timestamps relative to the unit's first replayed row.  HBM (BIG): one unbounded list per overflowed
-// unit, indexed by push count (no wrap).
-template <class T, bool BIG>
+// Pending list: (value, timestamp, row[, payload]) per partial.  LDS: ring of STACK_CAP entries per lane
+// (SoA, lane-strided: conflict-free), timestamps relative to the unit's first replayed row.  HBM (BIG): one
+// unbounded list per overflowed unit, indexed by push count (no wrap).  PAY: the record walk also keeps e1's
+// payload attribute.
+template <class T, bool BIG, bool PAY>
 struct PendList {
   T* val;
   int32_t* dts;
   int64_t* ts;
   uint32_t* row;
+  int64_t* pay;
   int64_t base;
   __device__ __forceinline__ uint32_t ix(uint32_t s) const { return BIG ? s : (s & (STACK_CAP - 1)) * WALK_BLOCK; }
   __device__ __forceinline__ T gv(uint32_t s) const { return val[ix(s)]; }
   __device__ __forceinline__ int64_t gts(uint32_t s) const { return BIG ? ts[ix(s)] : base + (int64_t)dts[ix(s)]; }
   __device__ __forceinline__ uint32_t grow(uint32_t s) const { return row[ix(s)]; }
-  __device__ __forceinline__ void put(uint32_t s, T v, int64_t t, uint32_t r) {
-    val[ix(s)] = v;
-    if (BIG) ts[ix(s)] = t; else dts[ix(s)] = (int32_t)(t - base);
-    row[ix(s)] = r;
+  __device__ __forceinline__ int64_t gpay(uint32_t s) const { return PAY ? pay[ix(s)] : 0; }
+  __device__ __forceinline__ void put(uint32_t s, T v, int64_t t, uint32_t r, int64_t p) {
+    uint32_t i = ix(s);
+    val[i] = v;
+    if (BIG) ts[i] = t; else dts[i] = (int32_t)(t - base);
+    row[i] = r;
+    if (PAY) pay[i] = p;
   }
 };
+template <class T, bool PAY>
+struct PendBytes {   // bytes per entry
+  static constexpr int lds = sizeof(T) + 8 + (PAY ? 8 : 0);
+  static constexpr int hbm = sizeof(T) + 12 + (PAY ? 8 : 0);
+};
 
-__device__ __forceinline__ uint32_t lb_rows(const uint32_t* rows, uint32_t lo, uint32_t hi, uint32_t target,
-                                            bool part) {
+template <class T>
+__device__ __forceinline__ uint32_t lb_row(const Src<T>& src, uint32_t lo, uint32_t hi, uint32_t target, bool part) {
   if (!part) return target < lo ? lo : (target > hi ? hi : target);
   while (lo < hi) {
     uint32_t mid = lo + ((hi - lo) >> 1);
-    if (rows[mid] < target) lo = mid + 1; else hi = mid;
+    if (src.row(mid) < target) lo = mid + 1; else hi = mid;
   }
   return lo;
 }
-__device__ __forceinline__ uint32_t lb_ts(const Virt& v, const uint32_t* rows, uint32_t lo, uint32_t hi,
-                                          int64_t tmin, bool part) {
+template <class T>
+__device__ __forceinline__ uint32_t lb_ts(const Src<T>& src, uint32_t lo, uint32_t hi, int64_t tmin) {
   while (lo < hi) {
     uint32_t mid = lo + ((hi - lo) >> 1);
-    uint32_t r = part ? rows[mid] : mid;
-    if (v_ts(v, r) < tmin) lo = mid + 1; else hi = mid;
+    if (src.ts(mid) < tmin) lo = mid + 1; else hi = mid;
   }
   return lo;
 }
@@ -329,50 +449,161 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
   return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
 }
 
+// Match projection (QuerySelector.processNoGroupBy, C/query/selector/QuerySelector.java:125-163, with
+// SelectiveStateEventPopulator, C/event/state/populater/SelectiveStateEventPopulator.java:36-56): one
+// thread per delivered match builds its AoS record from the (e1 row, e2 row) pair the walker placed at the
+// match's final slot.  Slots are in delivery order, so the e2 gathers stream and the e1 gathers stay within
+// one `within` window behind them.
 template <class T>
-__device__ void emit_match(const WalkArgs& a, const Virt& v, const ProjPlan& pp, const SgCols& bc,
-                           const SgCols& cc, char* out, int64_t slot, uint32_t ri, T vi, uint32_t rj, T vj,
-                           int64_t tj, uint32_t key, uint32_t rank) {
-  char* o = out + (size_t)slot * (size_t)a.stride;
-  uint32_t nm = 0;
-  int64_t* vals = (int64_t*)(o + 32);
-  for (int s = 0; s < a.n_select; ++s) {
-    int kind = pp.kind[s];
-    uint32_t r = pp.src[s] ? rj : ri;
-    int64_t bits = 0;
-    if (kind == 1) {
-      bits = val_bits<T>(pp.src[s] ? vj : vi);
-    } else if (kind == 2) {
-      nm |= 1u << s;
-    } else {
-      SgVal x = r < v.nc ? sg_read_col(cc, pp.col[s], pp.type[s], r) : sg_read_col(bc, pp.col[s], pp.type[s], r - v.nc);
-      if (x.null) nm |= 1u << s;
-      bits = sg_val_bits(x);
+__global__ void __launch_bounds__(256) k_project(WalkArgs a, Virt v, ProjPlan pp, SgCols bc, SgCols cc,
+                                                 const MRec* __restrict__ mrec, const uint32_t* __restrict__ off,
+                                                 int64_t total, char* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char stage[];   // 256 records, written out contiguously
+  const int64_t per = (int64_t)blockDim.x;
+  for (int64_t s0 = (int64_t)blockIdx.x * per; s0 < total; s0 += (int64_t)gridDim.x * per) {
+    const int64_t sl = s0 + threadIdx.x;
+    if (sl < total) {
+      const MRec mr = mrec[sl];
+      const uint32_t r1 = mr.r1, r2 = mr.r2;
+      const uint64_t b = r2 - v.nc;
+      const uint32_t rank = (uint32_t)(sl - (int64_t)off[b]);
+      const uint32_t key = a.partitioned ? (uint32_t)v.key[b] : 0u;
+      const int64_t t2 = v.ts[b];
+      int64_t* o = (int64_t*)(stage + (size_t)threadIdx.x * a.stride);
+      uint32_t nm = 0;
+      for (int s = 0; s < a.n_select; ++s) {
+        const bool s2 = pp.src[s] != 0;
+        const int kind = pp.kind[s];
+        int64_t bits = 0;
+        if (kind == 0) {
+          bits = mr.p1;
+        } else if (kind == 1) {
+          bits = s2 ? val_bits<T>(v_val<T>(v, r2, v.val_a == v.val_b)) : mr.v1;
+        } else if (kind == 2) {
+          nm |= 1u << s;
+        } else {
+          const uint32_t r = s2 ? r2 : r1;
+          SgVal x = r < v.nc ? sg_read_col(cc, pp.col[s], pp.type[s], r) : sg_read_col(bc, pp.col[s], pp.type[s], r - v.nc);
+          if (x.null) nm |= 1u << s;
+          bits = sg_val_bits(x);
+        }
+        o[4 + s] = bits;
+      }
+      o[0] = (int64_t)(a.index ? a.index[b] : a.base_index + b);
+      o[1] = t2;
+      o[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (a.multi ? (uint32_t)a.b_slot : (0x800000u | rank))) << 32));
+      o[3] = (int64_t)nm;
     }
-    vals[s] = bits;
+    __syncthreads();
+    const int64_t nrec = (total - s0 < per) ? (total - s0) : per;
+    const size_t bytes = (size_t)nrec * a.stride;
+    char* dst = out + (size_t)(a.out_base + s0) * a.stride;
+    if ((((uintptr_t)dst) & 15) == 0) {
+      typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+      for (size_t q = (size_t)threadIdx.x * 16; q < bytes; q += (size_t)per * 16)
+        *(U4*)(dst + q) = *(const U4*)(stage + q);
+    } else {
+      for (size_t q = (size_t)threadIdx.x * 8; q < bytes; q += (size_t)per * 8)
+        *(uint64_t*)(dst + q) = *(const uint64_t*)(stage + q);
+    }
+    __syncthreads();
   }
-  uint64_t b = rj - v.nc;
-  uint64_t trig = a.index ? a.index[b] : a.base_index + b;
-  uint64_t* h64 = (uint64_t*)o;
-  h64[0] = trig;
-  h64[1] = (uint64_t)tj;
-  h64[2] = (uint64_t)key | ((uint64_t)((1u << 24) | (a.multi ? (uint32_t)a.b_slot : (0x800000u | rank))) << 32);
-  h64[3] = (uint64_t)nm;
 }
+
+// The reference's pending list for one event of one key (see the file header).
+template <class T, bool WRITE, bool BIG>
+struct Walker {
+  PendList<T, BIG, WRITE> L;
+  uint32_t head = 0, top = 0;
+  int64_t prev_t;
+  bool bad = false;
+  bool overflow = false;
+  uint32_t ew = 0xffffffffu, ebits = 0;   // count pass: emit bitmap word being built
+  __device__ __forceinline__ void flush_bits(uint32_t* __restrict__ emap) {
+    if (ebits) atomicOr(&emap[ew], ebits);
+    ebits = 0;
+  }
+  __device__ __forceinline__ void step(const WalkArgs& a, const Virt& v, const WRec<T>& rc, uint32_t pos,
+                                       bool in_chunk, uint32_t ofs, uint32_t* __restrict__ cnt,
+                                       uint32_t* __restrict__ emap, MRec* __restrict__ mrec, bool payload) {
+    const uint32_t f = rc.rowf >> 30;
+    if (!f) return;
+    const int64_t t = rc.ts;
+    const T x = rc.val;
+    bad |= t < prev_t;
+    prev_t = t;
+    // lazy `within` expiry of the oldest partials (StreamPreStateProcessor.isExpired :102-113)
+    while (head != top && t - L.gts(head) > a.within) ++head;
+    const uint32_t r = rc.rowf & ROW_MASK;
+    const bool emit = in_chunk && (r >= v.nc);
+    if ((f & F_CONS) && !is_nan_val<T>(x)) {
+      uint32_t m = 0;
+      if (a.stack_mode) {
+        // monotone stack: the completed partials are exactly a suffix, delivered oldest first
+        while (top != head && cmp_op<T>(a.op, x, L.gv(top - 1))) { --top; ++m; }
+        if (emit && m) {
+          if (!WRITE) {
+            cnt[r - v.nc] = m;
+          } else {
+            for (uint32_t q = 0; q < m; ++q) {
+              MRec e;
+              e.r1 = L.grow(top + q);
+              e.r2 = r;
+              e.v1 = val_bits<T>(L.gv(top + q));
+              e.p1 = L.gpay(top + q);
+              mrec[ofs + q] = e;
+            }
+          }
+        }
+      } else {
+        uint32_t wr = head;
+        for (uint32_t s = head; s != top; ++s) {
+          T e = L.gv(s);
+          if (cmp_op<T>(a.op, x, e)) {
+            if (WRITE && emit) {
+              MRec mr;
+              mr.r1 = L.grow(s);
+              mr.r2 = r;
+              mr.v1 = val_bits<T>(e);
+              mr.p1 = L.gpay(s);
+              mrec[ofs + m] = mr;
+            }
+            ++m;
+          } else {
+            if (wr != s) L.put(wr, e, L.gts(s), L.grow(s), L.gpay(s));
+            ++wr;
+          }
+        }
+        top = wr;
+        if (!WRITE && emit && m) cnt[r - v.nc] = m;
+      }
+      if (!WRITE && emit && m) {
+        const uint32_t wi = pos >> 5;
+        if (wi != ew) { flush_bits(emap); ew = wi; }
+        ebits |= 1u << (pos & 31);
+      }
+    }
+    if ((f & F_CAND) && !is_nan_val<T>(x)) {
+      if (!BIG && top - head == STACK_CAP) { overflow = true; return; }
+      L.put(top, x, t, r, (WRITE && payload) ? v_payload(v, r) : 0);
+      ++top;
+    }
+  }
+};
 
 // One lane per unit (chunk c, key k).  WRITE=false: count pass (also fixes the unit's replay range);
 // WRITE=true: record pass.  BIG: only units that overflowed the LDS ring, with an HBM list.
 template <class T, bool WRITE, bool BIG>
-__global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Virt v, const uint32_t* __restrict__ rows,
-                                                     const uint32_t* __restrict__ seg_b,
+__global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, const uint32_t* __restrict__ seg_b,
                                                      const uint32_t* __restrict__ seg_e, UnitDesc* __restrict__ ud,
                                                      uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                                     char* __restrict__ out, ProjPlan pp, SgCols bc, SgCols cc,
+                                                     MRec* __restrict__ mrec, uint32_t* __restrict__ emap,
                                                      WalkStats* __restrict__ st, char* __restrict__ big,
                                                      uint32_t* __restrict__ carry_q0, uint32_t* __restrict__ carry_n) {
-  __shared__ char lds[BIG ? 16 : (STACK_CAP * WALK_BLOCK * (sizeof(T) + 8))];
+  __shared__ __attribute__((aligned(16))) char lds[BIG ? 16 : (STACK_CAP * WALK_BLOCK * PendBytes<T, WRITE>::lds)];
   const uint32_t u = xcd_block(blockIdx.x, gridDim.x) * WALK_BLOCK + threadIdx.x;
   if (u >= a.n_units) return;
+  const Virt& v = src.pk.v;
   const bool part = a.partitioned != 0;
   const uint32_t c = u / a.K, k = u % a.K;
   uint32_t sb, se;
@@ -387,11 +618,10 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Virt v, const u
   if (!WRITE && !BIG) {
     if (sb >= se) { ud[u] = UnitDesc{0, 0, 0, 0}; return; }
     uint64_t lo_row = (uint64_t)c * a.R, hi_row = lo_row + a.R;
-    p0 = c == 0 ? sb : lb_rows(rows, sb, se, (uint32_t)std::min<uint64_t>(lo_row, a.nt), part);
-    p1 = c + 1 >= a.C ? se : lb_rows(rows, p0, se, (uint32_t)std::min<uint64_t>(hi_row, a.nt), part);
+    p0 = c == 0 ? sb : lb_row(src, sb, se, (uint32_t)(lo_row < (uint64_t)a.nt ? lo_row : a.nt), part);
+    p1 = c + 1 >= a.C ? se : lb_row(src, p0, se, (uint32_t)(hi_row < (uint64_t)a.nt ? hi_row : a.nt), part);
     if (p0 >= p1) { ud[u] = UnitDesc{p0, p0, p0, 0}; return; }
-    int64_t t0 = v_ts(v, part ? rows[p0] : p0);
-    w = lb_ts(v, rows, sb, p0, t0 - a.within, part);
+    w = lb_ts(src, sb, p0, src.ts(p0) - a.within);
     ud[u] = UnitDesc{p0, p1, w, 0};
   } else {
     UnitDesc d = ud[u];
@@ -399,118 +629,97 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Virt v, const u
     if (p0 >= p1) return;
     if (BIG != (ovf != 0)) return;
   }
-  PendList<T, BIG> L;
+  Walker<T, WRITE, BIG> W;
   if (BIG) {
     size_t cap = a.big_cap;
-    char* base = big + (size_t)(ovf - 1) * cap * (sizeof(T) + 12);
-    L.val = (T*)base;
-    L.ts = (int64_t*)(base + cap * sizeof(T));
-    L.row = (uint32_t*)(base + cap * (sizeof(T) + 8));
-    L.dts = nullptr;
+    char* base = big + (size_t)(ovf - 1) * cap * PendBytes<T, true>::hbm;
+    W.L.ts = (int64_t*)base;
+    W.L.pay = (int64_t*)(base + cap * 8);
+    W.L.val = (T*)(base + cap * 16);
+    W.L.row = (uint32_t*)(base + cap * (16 + sizeof(T)));
+    W.L.dts = nullptr;
   } else {
-    L.val = (T*)lds + threadIdx.x;
-    L.dts = (int32_t*)(lds + STACK_CAP * WALK_BLOCK * sizeof(T)) + threadIdx.x;
-    L.row = (uint32_t*)(lds + STACK_CAP * WALK_BLOCK * (sizeof(T) + 4)) + threadIdx.x;
-    L.ts = nullptr;
+    const size_t E = (size_t)STACK_CAP * WALK_BLOCK;
+    const size_t pb = WRITE ? 8 : 0;
+    W.L.pay = (int64_t*)lds + threadIdx.x;
+    W.L.val = (T*)(lds + E * pb) + threadIdx.x;
+    W.L.dts = (int32_t*)(lds + E * (pb + sizeof(T))) + threadIdx.x;
+    W.L.row = (uint32_t*)(lds + E * (pb + sizeof(T) + 4)) + threadIdx.x;
+    W.L.ts = nullptr;
   }
-  const uint32_t rw = part ? rows[w] : w;
-  const int64_t tw = v_ts(v, rw);
-  L.base = tw;
+  const bool payload = v.pcol != nullptr;
+  const int64_t tw = src.ts(w);
+  W.L.base = tw;
+  auto mark_overflow = [&]() {
+    uint32_t slot = atomicAdd(&st->n_ovf, 1u);
+    atomicMax(&st->ovf_need, p1 - w);
+    ud[u].ovf = slot + 1;
+  };
   if (!BIG && !WRITE) {
-    int64_t tl = v_ts(v, part ? rows[p1 - 1] : p1 - 1);
-    if (tl - tw > 0x7fffffffll || tl < tw) {   // relative timestamps would not fit (or order broken)
-      uint32_t slot = atomicAdd(&st->n_ovf, 1u);
-      atomicMax(&st->ovf_need, p1 - w);
-      ud[u].ovf = slot + 1;
-      return;
+    int64_t tl = src.ts(p1 - 1);
+    if (tl - tw > 0x7fffffffll || tl < tw) { mark_overflow(); return; }   // relative ts would not fit
+  }
+  W.prev_t = (w > sb) ? src.ts(w - 1) : tw;
+  // record walk: output offsets only for the positions the count pass marked as emitting
+  auto off_of = [&](const WRec<T>& rc, uint32_t pos, uint32_t bits) -> uint32_t {
+    uint32_t r = rc.rowf & ROW_MASK;
+    return (bits && pos >= p0 && pos < p1 && r >= v.nc) ? off[r - v.nc] : 0u;
+  };
+  if (src.srec) {
+    // key-sorted records: whole-line group loads, next group in flight while this one is walked
+    typedef Grp<T> GT;
+    const uint32_t G = GT::G;
+    GT cur, nxt;
+    uint32_t g = w & ~(G - 1);
+    cur.load(src.srec + g);
+    uint32_t ofs[GT::G], nofs[GT::G];
+    uint32_t eb = 0, neb = 0;
+    if (WRITE) {
+      eb = emap[g >> 5] >> (g & 31);
+#pragma unroll
+      for (int i = 0; i < GT::G; ++i) ofs[i] = off_of(cur.rec(i), g + i, (eb >> i) & 1u);
+    }
+    for (; g < p1; g += G) {
+      const uint32_t gn = g + G;
+      if (gn < p1) {
+        nxt.load(src.srec + gn);
+        if (WRITE) neb = emap[gn >> 5] >> (gn & 31);
+      }
+#pragma unroll
+      for (int i = 0; i < GT::G; ++i) {
+        const uint32_t p = g + i;
+        if (p < w || p >= p1) continue;
+        W.step(a, v, cur.rec(i), p, p >= p0, WRITE ? ofs[i] : 0u, cnt, emap, mrec, payload);
+        if (!BIG && W.overflow) break;
+      }
+      if (!BIG && W.overflow) break;
+      cur = nxt;
+      if (WRITE) {
+#pragma unroll
+        for (int i = 0; i < GT::G; ++i) nofs[i] = (gn < p1) ? off_of(cur.rec(i), gn + i, (neb >> i) & 1u) : 0u;
+#pragma unroll
+        for (int i = 0; i < GT::G; ++i) ofs[i] = nofs[i];
+      }
+    }
+  } else {
+    // unpartitioned: the rows themselves, in order
+    for (uint32_t p = w; p < p1; ++p) {
+      WRec<T> rc = src.pk(p);
+      uint32_t o = 0;
+      if (WRITE) o = off_of(rc, p, (emap[p >> 5] >> (p & 31)) & 1u);
+      W.step(a, v, rc, p, p >= p0, o, cnt, emap, mrec, payload);
+      if (!BIG && W.overflow) break;
     }
   }
-  int64_t prev_t = (w > sb) ? v_ts(v, part ? rows[w - 1] : w - 1) : tw;
-  const int64_t T_ = a.within;
-  const int op = a.op;
-  uint32_t head = 0, top = 0;
-  bool bad = false;
-  for (uint32_t p = w; p < p1; p += PF) {
-    uint32_t rr[PF], ff[PF];
-    int64_t tt[PF];
-    T vv[PF];
-#pragma unroll
-    for (int i = 0; i < PF; ++i) rr[i] = (p + i < p1) ? (part ? rows[p + i] : p + i) : 0u;
-#pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      ff[i] = 0;
-      if (p + i < p1) {
-        ff[i] = v_flags(v, rr[i]);
-        tt[i] = v_ts(v, rr[i]);
-        vv[i] = v_val<T>(v, rr[i], true);
-      }
-    }
-    if (v.val_a != v.val_b) {
-#pragma unroll
-      for (int i = 0; i < PF; ++i)
-        if (p + i < p1 && !(ff[i] & F_CAND)) vv[i] = v_val<T>(v, rr[i], false);
-    }
-#pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      uint32_t f = ff[i];
-      if (!f) continue;
-      const int64_t t = tt[i];
-      const T x = vv[i];
-      bad |= t < prev_t;
-      prev_t = t;
-      // lazy `within` expiry of the oldest partials (StreamPreStateProcessor.isExpired :102-113)
-      while (head != top && t - L.gts(head) > T_) ++head;
-      const uint32_t r = rr[i];
-      const bool emit = (p + i >= p0) && (r >= v.nc);
-      if ((f & F_CONS) && !is_nan_val<T>(x)) {
-        uint32_t m = 0;
-        if (a.stack_mode) {
-          while (top != head && cmp_op<T>(op, x, L.gv(top - 1))) { --top; ++m; }
-          if (emit && m) {
-            if (!WRITE) {
-              cnt[r - v.nc] = m;
-            } else {
-              int64_t o = a.out_base + off[r - v.nc];
-              for (uint32_t q = 0; q < m; ++q)
-                emit_match<T>(a, v, pp, bc, cc, out, o + q, L.grow(top + q), L.gv(top + q), r, x, t, k, q);
-            }
-          }
-        } else {
-          int64_t o = (WRITE && emit) ? a.out_base + off[r - v.nc] : 0;
-          uint32_t wr = head;
-          for (uint32_t s = head; s != top; ++s) {
-            T e = L.gv(s);
-            if (cmp_op<T>(op, x, e)) {
-              if (WRITE && emit) emit_match<T>(a, v, pp, bc, cc, out, o + m, L.grow(s), e, r, x, t, k, m);
-              ++m;
-            } else {
-              if (wr != s) L.put(wr, e, L.gts(s), L.grow(s));
-              ++wr;
-            }
-          }
-          top = wr;
-          if (!WRITE && emit && m) cnt[r - v.nc] = m;
-        }
-      }
-      if ((f & F_CAND) && !is_nan_val<T>(x)) {
-        if (!BIG && top - head == STACK_CAP) {
-          if (!WRITE) {
-            uint32_t slot = atomicAdd(&st->n_ovf, 1u);
-            atomicMax(&st->ovf_need, p1 - w);
-            ud[u].ovf = slot + 1;
-          }
-          return;   // the HBM-list walker redoes this unit
-        }
-        L.put(top, x, t, r);
-        ++top;
-      }
-    }
+  if (!WRITE) W.flush_bits(emap);
+  if (!BIG && W.overflow) {
+    if (!WRITE) mark_overflow();
+    return;   // the HBM-list walker redoes this unit
   }
-  if (bad) atomicOr(&st->order_err, 1u);
+  if (W.bad) atomicOr(&st->order_err, 1u);
   if (WRITE && a.carry_out && p1 == se) {
     // rows of this key still inside the window of its last event survive into the next push
-    int64_t tl = v_ts(v, part ? rows[se - 1] : se - 1);
-    uint32_t q0 = lb_ts(v, rows, sb, se, tl - T_, part);
+    uint32_t q0 = lb_ts(src, sb, se, src.ts(se - 1) - a.within);
     carry_q0[k] = q0;
     carry_n[k] = se - q0;
   }
@@ -525,17 +734,18 @@ struct CarryBufs {
   uint8_t* nul[SG_MAX_COLS];
 };
 
-__global__ void k_carry_copy(Virt v, const uint32_t* __restrict__ rows, int partitioned, uint32_t K,
-                             const uint32_t* __restrict__ q0s, const uint32_t* __restrict__ ns,
-                             const uint32_t* __restrict__ offs, int n_cols, const int32_t* __restrict__ widths,
-                             SgCols bc, SgCols cc, CarryBufs dst) {
+template <class T>
+__global__ void k_carry_copy(Src<T> src, uint32_t K, const uint32_t* __restrict__ q0s,
+                             const uint32_t* __restrict__ ns, const uint32_t* __restrict__ offs, int n_cols,
+                             const int32_t* __restrict__ widths, SgCols bc, SgCols cc, CarryBufs dst) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
   uint32_t n = ns[k];
   if (!n) return;
+  const Virt& v = src.pk.v;
   uint32_t q0 = q0s[k], o = offs[k];
   for (uint32_t q = 0; q < n; ++q) {
-    uint32_t r = partitioned ? rows[q0 + q] : q0 + q;
+    uint32_t r = src.row(q0 + q);
     uint32_t d = o + q;
     dst.ts[d] = v_ts(v, r);
     dst.key[d] = r < v.nc ? v.c_key[r] : (v.key ? v.key[r - v.nc] : 0);
@@ -582,11 +792,14 @@ struct CarrySet {
 struct EveryNextState {
   CarrySet carry[2];
   int cur = 0;
+  bool nul_seen[SG_MAX_COLS] = {};   // a column that ever had nulls is gathered by row, never carried
 };
 
-static int pick_chunks(uint32_t K, int64_t nt) {
-  const int64_t target = 160 * 1024;   // ≈10 waves on each of 256 CUs
-  int64_t C = (target + K - 1) / K;
+static int pick_chunks(uint32_t K, int64_t nt, int entry_bytes) {
+  // one round of resident walkers: LDS holds 160 KiB / (STACK_CAP * entry) lanes per CU, in whole blocks
+  int64_t blocks_per_cu = (160 * 1024) / ((int64_t)STACK_CAP * WALK_BLOCK * entry_bytes);
+  int64_t target = std::max<int64_t>(blocks_per_cu, 1) * WALK_BLOCK * 256;
+  int64_t C = std::max<int64_t>(1, target / K);
   C = std::min<int64_t>(C, 64);
   C = std::min<int64_t>(C, std::max<int64_t>(1, nt / 512));
   return (int)std::max<int64_t>(C, 1);
@@ -608,8 +821,32 @@ static bool simple_prog(const sg_nfa_desc& d, int off, int len, PredArgs& pa) {
   return true;
 }
 
+static SgVal sg_val_from_bits_host(int64_t bits, int type) {
+  SgVal v;
+  v.type = type;
+  v.null = 0;
+  v.i = 0;
+  v.d = 0.0;
+  if (type == SG_T_FLOAT) {
+    uint32_t u = (uint32_t)bits;
+    float f;
+    memcpy(&f, &u, 4);
+    v.d = f;
+  } else if (type == SG_T_DOUBLE) {
+    memcpy(&v.d, &bits, 8);
+  } else {
+    v.i = bits;
+  }
+  return v;
+}
+
+struct PushPlan {
+  ProjPlan pp;
+  int pcol = -1;              // e1 payload column carried in the pending list
+};
+
 template <class T>
-static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
+static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& plan) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
   const int* sa = d.shape_args;
@@ -618,7 +855,7 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   CarrySet& cs = es->carry[es->cur];
   const int64_t nc = h->opt.no_carry ? 0 : cs.n;
   const int64_t nt = nc + n;
-  if (nt >= (1ll << 31)) throw SgError(SG_EINVAL, "batch plus carried rows exceed 2^31");
+  if (nt >= (1ll << 30)) throw SgError(SG_EINVAL, "batch plus carried rows exceed 2^30");
   const int val_col_a = d.ret_col[sa[4]], val_col_b = d.ret_col[sa[3]];
 
   // ---- key bound
@@ -662,15 +899,34 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
     PredArgs sp = pa;
     bool simple = pa.cons_all && !bv.stream && pa.s_a == 0 && simple_prog(d, pa.prog_a_off, pa.prog_a_len, sp) &&
                   sp.s_col == val_col_a && (((uintptr_t)bv.cols.col[sp.s_col]) & 15) == 0;
-    int64_t waves = std::min<int64_t>((ntiles + 3) / 4, 256 * 16);
+    int64_t waves = std::min<int64_t>((ntiles + 3) / 4, 256 * 32);
     dim3 grd((unsigned)std::max<int64_t>(1, (waves + 3) / 4)), blk(256);
-    if (simple && sp.s_type == SG_T_FLOAT)
-      hipLaunchKernelGGL(k_pred_simple<float>, grd, blk, 0, st, sp, (const float*)bv.cols.col[sp.s_col],
-                         bv.cols.nul[sp.s_col], cand_m);
-    else if (simple)
-      hipLaunchKernelGGL(k_pred_simple<int32_t>, grd, blk, 0, st, sp, (const int32_t*)bv.cols.col[sp.s_col],
-                         bv.cols.nul[sp.s_col], cand_m);
-    else {
+    if (simple) {
+      // constant in the compare domain (sg_cmp: 0 integral, 1 f32, 2 f64)
+      SgVal cv = sg_val_from_bits_host(sp.s_cbits, sp.s_ctype);
+      const void* colp = bv.cols.col[sp.s_col];
+      const uint8_t* nul = bv.cols.nul[sp.s_col];
+      if (sp.s_dom == 1) {
+        float c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? (float)cv.d : (float)cv.i;
+        if (sp.s_type == SG_T_FLOAT)
+          hipLaunchKernelGGL((k_pred_simple<float, float>), grd, blk, 0, st, n, sp.s_op, c, (const float*)colp, nul, cand_m);
+        else
+          hipLaunchKernelGGL((k_pred_simple<int32_t, float>), grd, blk, 0, st, n, sp.s_op, c, (const int32_t*)colp, nul, cand_m);
+      } else if (sp.s_dom == 2) {
+        double c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? cv.d : (double)cv.i;
+        if (sp.s_type == SG_T_FLOAT)
+          hipLaunchKernelGGL((k_pred_simple<float, double>), grd, blk, 0, st, n, sp.s_op, c, (const float*)colp, nul, cand_m);
+        else
+          hipLaunchKernelGGL((k_pred_simple<int32_t, double>), grd, blk, 0, st, n, sp.s_op, c, (const int32_t*)colp, nul, cand_m);
+      } else {
+        int64_t c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? (int64_t)cv.d : cv.i;
+        if (sp.s_type == SG_T_FLOAT)
+          simple = false;   // integral domain on a float column: leave it to the VM's conversions
+        else
+          hipLaunchKernelGGL((k_pred_simple<int32_t, int64_t>), grd, blk, 0, st, n, sp.s_op, c, (const int32_t*)colp, nul, cand_m);
+      }
+    }
+    if (!simple) {
       int64_t w2 = std::min<int64_t>(ntiles, 256 * 16);
       hipLaunchKernelGGL(k_pred, dim3((unsigned)std::max<int64_t>(1, (w2 + 3) / 4)), blk, 0, st, pa, bv.cols,
                          h->ddesc, cand_m, cons_m);
@@ -679,8 +935,9 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   h->mark(1);
 
-  // ---- 2. key partition: per-key row lists in arrival order
+  // ---- 2. key partition: per-key walker records in arrival order
   Virt v;
+  memset(&v, 0, sizeof(v));
   v.nc = nc;
   v.n = n;
   v.ts = bv.ts;
@@ -694,31 +951,46 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   v.c_flags = cs.flags;
   v.c_val_a = cs.col[val_col_a];
   v.c_val_b = cs.col[val_col_b];
+  if (plan.pcol >= 0) {
+    const int c = plan.pcol;
+    v.pcol = bv.cols.col[c];
+    v.c_pcol = cs.col[c];
+    v.pw = (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE) ? 8 : 4;
+    v.pfloat = d.col_type[c] == SG_T_FLOAT;
+  }
   SgCols cc;
   memset(&cc, 0, sizeof(cc));
   for (int c = 0; c < d.n_cols; ++c) { cc.col[c] = cs.col[c]; cc.nul[c] = cs.nul[c]; }
 
+  typedef WRec<T> R;
+  Src<T> src;
+  src.srec = nullptr;
+  src.pk.v = v;
   const uint32_t K = d.partitioned ? kb : 1;
-  uint32_t* rows = nullptr;
   uint32_t* seg_b = nullptr;
   uint32_t* seg_e = nullptr;
   if (d.partitioned) {
     int end_bit = 1;
     while ((1ull << end_bit) <= (uint64_t)kb) ++end_bit;
     uint32_t* skeys = (uint32_t*)h->ws.get("skeys", sizeof(uint32_t) * nt, st);
-    rows = (uint32_t*)h->ws.get("rows", sizeof(uint32_t) * nt, st);
+    R* srec = (R*)h->ws.get("srec", sizeof(R) * nt, st);
+    R* prec = (R*)h->ws.get("prec", sizeof(R) * nt, st);
+    uint32_t* pkeys = (uint32_t*)h->ws.get("pkeys", sizeof(uint32_t) * nt, st);
     KeyOf kf{bv.key, cs.key, (uint32_t)nc};
-    auto kit = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0), kf);
-    auto vit = rocprim::make_counting_iterator<uint32_t>(0);
+    hipLaunchKernelGGL((k_pack<T>), dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32)), dim3(256), 0,
+                       st, src.pk, kf, nt, prec, pkeys);
+    HIPCHK(hipGetLastError());
     size_t tb = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, kit, skeys, vit, rows, (size_t)nt, 0, end_bit, st));
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
     void* tmp = h->ws.get("sort_tmp", tb, st);
-    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, kit, skeys, vit, rows, (size_t)nt, 0, end_bit, st));
+    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
+    src.srec = srec;
     seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
     seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
     HIPCHK(hipMemsetAsync(seg_b, 0, sizeof(uint32_t) * K, st));
     HIPCHK(hipMemsetAsync(seg_e, 0, sizeof(uint32_t) * K, st));
-    hipLaunchKernelGGL(k_bounds, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, skeys, nt, kb, seg_b, seg_e);
+    hipLaunchKernelGGL(k_bounds, dim3((unsigned)std::min<int64_t>((nt + 1023) / 1024, 256 * 16)), dim3(256), 0, st, skeys,
+                       nt, kb, seg_b, seg_e);
     HIPCHK(hipGetLastError());
   }
   h->mark(2);
@@ -729,7 +1001,7 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   wa.nt = nt;
   wa.within = d.within;
   wa.K = K;
-  wa.C = (uint32_t)pick_chunks(K, nt);
+  wa.C = (uint32_t)pick_chunks(K, nt, PendBytes<T, true>::lds);   // sized for the record walk's ring
   wa.R = (uint32_t)((nt + wa.C - 1) / wa.C);
   const uint64_t units = (uint64_t)K * wa.C;
   if (units >= (1ull << 32)) throw SgError(SG_EINVAL, "too many (key, chunk) units");
@@ -751,19 +1023,7 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   wa.n_select = d.n_select;
   wa.stride = 32 + 8 * d.n_select;
-  ProjPlan pp;
-  memset(&pp, 0, sizeof(pp));
-  for (int s = 0; s < d.n_select; ++s) {
-    int stt = d.sel_state[s];
-    pp.src[s] = (stt == b_state) ? 1 : 0;
-    int col = d.ret_col[d.sel_ret[s]];
-    int idx = d.sel_index[s];
-    pp.col[s] = col;
-    pp.type[s] = d.sel_type[s];
-    if (idx != 0 && idx != -1) pp.kind[s] = 2;
-    else if (col == (pp.src[s] ? val_col_b : val_col_a)) pp.kind[s] = 1;
-    else pp.kind[s] = 3;
-  }
+  const ProjPlan& pp = plan.pp;
 
   UnitDesc* ud = (UnitDesc*)h->ws.get("units", sizeof(UnitDesc) * units, st);
   WalkStats* wst = (WalkStats*)h->ws.get("walkstats", sizeof(WalkStats), st);
@@ -772,11 +1032,13 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   uint32_t* carry_q0 = (uint32_t*)h->ws.get("carry_q0", sizeof(uint32_t) * K, st);
   uint32_t* carry_n = (uint32_t*)h->ws.get("carry_n", sizeof(uint32_t) * (K + 1), st);
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
+  uint32_t* emap = (uint32_t*)h->ws.get("emap", sizeof(uint32_t) * (nt / 32 + 2), st);
+  HIPCHK(hipMemsetAsync(emap, 0, sizeof(uint32_t) * (nt / 32 + 2), st));
   HIPCHK(hipMemsetAsync(wst, 0, sizeof(WalkStats), st));
   if (wa.carry_out) HIPCHK(hipMemsetAsync(carry_n, 0, sizeof(uint32_t) * (K + 1), st));
   const dim3 wblk(WALK_BLOCK), wgrd((unsigned)((units + WALK_BLOCK - 1) / WALK_BLOCK));
-  hipLaunchKernelGGL((k_walk<T, false, false>), wgrd, wblk, 0, st, wa, v, rows, seg_b, seg_e, ud, cnt, off,
-                     (char*)nullptr, pp, bv.cols, cc, wst, (char*)nullptr, carry_q0, carry_n);
+  hipLaunchKernelGGL((k_walk<T, false, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
+                     (MRec*)nullptr, emap, wst, (char*)nullptr, carry_q0, carry_n);
   HIPCHK(hipGetLastError());
   auto scan_counts = [&]() {
     size_t tb = 0;
@@ -796,10 +1058,10 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   if (hs.n_ovf) {
     // units whose pending list outgrew the LDS ring: redo them with unbounded HBM lists
     wa.big_cap = (std::max<uint32_t>(hs.ovf_need, 1) + 1) & ~1u;
-    big = (char*)h->ws.get("big_lists", (size_t)hs.n_ovf * wa.big_cap * (sizeof(T) + 12), st);
+    big = (char*)h->ws.get("big_lists", (size_t)hs.n_ovf * wa.big_cap * PendBytes<T, true>::hbm, st);
     h->mark(6);
-    hipLaunchKernelGGL((k_walk<T, false, true>), wgrd, wblk, 0, st, wa, v, rows, seg_b, seg_e, ud, cnt, off,
-                       (char*)nullptr, pp, bv.cols, cc, wst, big, carry_q0, carry_n);
+    hipLaunchKernelGGL((k_walk<T, false, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
+                       (MRec*)nullptr, emap, wst, big, carry_q0, carry_n);
     HIPCHK(hipGetLastError());
     scan_counts();
     h->mark(7);
@@ -817,13 +1079,19 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   if (total || wa.carry_out) {
     out = h->out.reserve(total, d.n_select, st);
     wa.out_base = h->out.n;
+    MRec* mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
-    hipLaunchKernelGGL((k_walk<T, true, false>), wgrd, wblk, 0, st, wa, v, rows, seg_b, seg_e, ud, cnt, off, out,
-                       pp, bv.cols, cc, wst, (char*)nullptr, carry_q0, carry_n);
+    hipLaunchKernelGGL((k_walk<T, true, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec, emap,
+                       wst, (char*)nullptr, carry_q0, carry_n);
     HIPCHK(hipGetLastError());
     if (hs.n_ovf) {
-      hipLaunchKernelGGL((k_walk<T, true, true>), wgrd, wblk, 0, st, wa, v, rows, seg_b, seg_e, ud, cnt, off, out,
-                         pp, bv.cols, cc, wst, big, carry_q0, carry_n);
+      hipLaunchKernelGGL((k_walk<T, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec,
+                         emap, wst, big, carry_q0, carry_n);
+      HIPCHK(hipGetLastError());
+    }
+    if (total) {
+      hipLaunchKernelGGL((k_project<T>), dim3((unsigned)std::min<int64_t>(((int64_t)total + 255) / 256, 256 * 16)),
+                         dim3(256), (size_t)256 * wa.stride, st, wa, v, pp, bv.cols, cc, mrec, off, (int64_t)total, out);
       HIPCHK(hipGetLastError());
     }
     h->out.n += total;
@@ -854,8 +1122,8 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
     cb.flags = nx.flags;
     for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
     if (ncar)
-      hipLaunchKernelGGL(k_carry_copy, dim3((K + 255) / 256), dim3(256), 0, st, v, rows, d.partitioned, K, carry_q0,
-                         carry_n, coff, d.n_cols, widths, bv.cols, cc, cb);
+      hipLaunchKernelGGL((k_carry_copy<T>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n,
+                         coff, d.n_cols, widths, bv.cols, cc, cb);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
     nx.n = ncar;
@@ -866,32 +1134,33 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   h->last_matches = total;
 }
 
-void sg_run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
-  if (!h->state) { h->state = new EveryNextState(); h->state_kind = 1; }
+// Projection plan: which select columns are the compared value and which are gathered by row at emission.
+static PushPlan make_plan(SgHandle* h, const BatchView& bv) {
   const sg_nfa_desc& d = h->desc;
-  switch (d.shape_args[5]) {
-    case SG_T_FLOAT: run_every_next<float>(h, bv, n); break;
-    case SG_T_DOUBLE: run_every_next<double>(h, bv, n); break;
-    case SG_T_LONG: run_every_next<int64_t>(h, bv, n); break;
-    default: run_every_next<int32_t>(h, bv, n); break;
-  }
-}
-
-void sg_every_next_reset(SgHandle* h) {
-  if (h->state && h->state_kind == 1) {
-    EveryNextState* es = (EveryNextState*)h->state;
-    es->carry[0].n = 0;
-    es->carry[1].n = 0;
-  }
-  h->key_bound_seen = 0;
-}
-
-void sg_every_next_release(SgHandle* h) {
-  if (h->state_kind != 1) return;
   EveryNextState* es = (EveryNextState*)h->state;
-  es->carry[0].release();
-  es->carry[1].release();
-  delete es;
-  h->state = nullptr;
-  h->state_kind = 0;
+  for (int c = 0; c < d.n_cols; ++c) if (bv.cols.nul[c]) es->nul_seen[c] = true;
+  const int b_state = d.shape_args[1];
+  const int val_col_a = d.ret_col[d.shape_args[4]], val_col_b = d.ret_col[d.shape_args[3]];
+  PushPlan pl;
+  memset(&pl.pp, 0, sizeof(pl.pp));
+  for (int s = 0; s < d.n_select; ++s) {
+    ProjPlan& pp = pl.pp;
+    pp.src[s] = (d.sel_state[s] == b_state) ? 1 : 0;
+    int col = d.ret_col[d.sel_ret[s]];
+    int idx = d.sel_index[s];
+    pp.col[s] = col;
+    pp.type[s] = d.sel_type[s];
+    if (idx != 0 && idx != -1) pp.kind[s] = 2;
+    else if (col == (pp.src[s] ? val_col_b : val_col_a)) pp.kind[s] = 1;
+    else if (pp.src[s] == 0 && !es->nul_seen[col] && (pl.pcol < 0 || pl.pcol == col)) { pp.kind[s] = 0; pl.pcol = col; }
+    else pp.kind[s] = 3;
+  }
+  return pl;
+}
+
+template <class T>
+static void dispatch_np(SgHandle* h, const BatchView& bv, int64_t n) {
+  if (!h->state) { h->state = new EveryNextState(); h->state_kind = 1; }
+  PushPlan pl = make_plan(h, bv);   // (needs the state: null history)
+  run_every_next<T>(h, bv, n, pl);
 }

@@ -110,6 +110,10 @@ struct SgHandle {
 
 
 void sg_run_every_next(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_every_next_f32(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_every_next_f64(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_every_next_i32(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_every_next_i64(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_reset(SgHandle* h);
 void sg_every_next_release(SgHandle* h);
 void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n);
