@@ -511,7 +511,10 @@ __global__ void __launch_bounds__(256) k_project(WalkArgs a, Virt v, ProjPlan pp
 }
 
 // The reference's pending list for one event of one key (see the file header).
-template <class T, bool WRITE, bool BIG>
+template <int OP, class T>
+__device__ __forceinline__ bool cmp_sel(int op, T b, T a) { return cmp_op<T>(OP ? OP : op, b, a); }
+
+template <class T, bool WRITE, bool BIG, int OP = 0>
 struct Walker {
   PendList<T, BIG, WRITE> L;
   uint32_t head = 0, top = 0;
@@ -523,11 +526,18 @@ struct Walker {
     if (ebits) atomicOr(&emap[ew], ebits);
     ebits = 0;
   }
-  __device__ __forceinline__ void step(const WalkArgs& a, const Virt& v, const WRec<T>& rc, uint32_t pos,
-                                       bool in_chunk, uint32_t ofs, uint32_t* __restrict__ cnt,
-                                       uint32_t* __restrict__ emap, MRec* __restrict__ mrec, bool payload) {
+  __device__ __forceinline__ void mark_emit(uint32_t pos, uint32_t* __restrict__ emap) {
+    const uint32_t wi = pos >> 5;
+    if (wi != ew) { flush_bits(emap); ew = wi; }
+    ebits |= 1u << (pos & 31);
+  }
+  // returns true when this event (inside the unit's chunk) completed partials
+  __device__ __forceinline__ bool step(const WalkArgs& a, const Virt& v, const WRec<T>& rc, bool in_chunk,
+                                       uint32_t ofs, uint32_t* __restrict__ cnt, MRec* __restrict__ mrec,
+                                       bool payload) {
     const uint32_t f = rc.rowf >> 30;
-    if (!f) return;
+    if (!f) return false;
+    bool emitted = false;
     const int64_t t = rc.ts;
     const T x = rc.val;
     bad |= t < prev_t;
@@ -540,7 +550,7 @@ struct Walker {
       uint32_t m = 0;
       if (a.stack_mode) {
         // monotone stack: the completed partials are exactly a suffix, delivered oldest first
-        while (top != head && cmp_op<T>(a.op, x, L.gv(top - 1))) { --top; ++m; }
+        while (top != head && cmp_sel<OP, T>(a.op, x, L.gv(top - 1))) { --top; ++m; }
         if (emit && m) {
           if (!WRITE) {
             cnt[r - v.nc] = m;
@@ -559,7 +569,7 @@ struct Walker {
         uint32_t wr = head;
         for (uint32_t s = head; s != top; ++s) {
           T e = L.gv(s);
-          if (cmp_op<T>(a.op, x, e)) {
+          if (cmp_sel<OP, T>(a.op, x, e)) {
             if (WRITE && emit) {
               MRec mr;
               mr.r1 = L.grow(s);
@@ -577,17 +587,14 @@ struct Walker {
         top = wr;
         if (!WRITE && emit && m) cnt[r - v.nc] = m;
       }
-      if (!WRITE && emit && m) {
-        const uint32_t wi = pos >> 5;
-        if (wi != ew) { flush_bits(emap); ew = wi; }
-        ebits |= 1u << (pos & 31);
-      }
+      emitted = emit && m;
     }
     if ((f & F_CAND) && !is_nan_val<T>(x)) {
-      if (!BIG && top - head == STACK_CAP) { overflow = true; return; }
+      if (!BIG && top - head == STACK_CAP) { overflow = true; return emitted; }
       L.put(top, x, t, r, (WRITE && payload) ? v_payload(v, r) : 0);
       ++top;
     }
+    return emitted;
   }
 };
 
@@ -689,7 +696,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, con
       for (int i = 0; i < GT::G; ++i) {
         const uint32_t p = g + i;
         if (p < w || p >= p1) continue;
-        W.step(a, v, cur.rec(i), p, p >= p0, WRITE ? ofs[i] : 0u, cnt, emap, mrec, payload);
+        if (W.step(a, v, cur.rec(i), p >= p0, WRITE ? ofs[i] : 0u, cnt, mrec, payload) && !WRITE) W.mark_emit(p, emap);
         if (!BIG && W.overflow) break;
       }
       if (!BIG && W.overflow) break;
@@ -707,7 +714,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, con
       WRec<T> rc = src.pk(p);
       uint32_t o = 0;
       if (WRITE) o = off_of(rc, p, (emap[p >> 5] >> (p & 31)) & 1u);
-      W.step(a, v, rc, p, p >= p0, o, cnt, emap, mrec, payload);
+      if (W.step(a, v, rc, p >= p0, o, cnt, mrec, payload) && !WRITE) W.mark_emit(p, emap);
       if (!BIG && W.overflow) break;
     }
   }
@@ -719,6 +726,174 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, con
   if (W.bad) atomicOr(&st->order_err, 1u);
   if (WRITE && a.carry_out && p1 == se) {
     // rows of this key still inside the window of its last event survive into the next push
+    uint32_t q0 = lb_ts(src, sb, se, src.ts(se - 1) - a.within);
+    carry_q0[k] = q0;
+    carry_n[k] = se - q0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Lane-interleaved ("transposed") walker tiles for partitioned queries.  Logical wave W owns units
+// 64W..64W+63; row i of its tile holds record (w_u + i) of each of its units, so one wave-wide record load
+// is one contiguous 1 KB access and the emit flags of a row are one ballot word.
+
+// unit replay ranges (p0, p1, w) + per-wave tile length (rows, padded to TROWS)
+static const int TROWS = 16;
+template <class T>
+__global__ void __launch_bounds__(256) k_units(WalkArgs a, Src<T> src, const uint32_t* __restrict__ seg_b,
+                                               const uint32_t* __restrict__ seg_e, UnitDesc* __restrict__ ud,
+                                               uint32_t* __restrict__ wlen, WalkStats* __restrict__ st) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t len = 0;
+  if (u < a.n_units) {
+    const uint32_t c = u / a.K, k = u % a.K;
+    const uint32_t sb = seg_b[k], se = seg_e[k];
+    UnitDesc d{0, 0, 0, 0};
+    if (sb < se) {
+      uint64_t lo_row = (uint64_t)c * a.R, hi_row = lo_row + a.R;
+      uint32_t p0 = c == 0 ? sb : lb_row(src, sb, se, (uint32_t)(lo_row < (uint64_t)a.nt ? lo_row : a.nt), true);
+      uint32_t p1 = c + 1 >= a.C ? se : lb_row(src, p0, se, (uint32_t)(hi_row < (uint64_t)a.nt ? hi_row : a.nt), true);
+      d = UnitDesc{p0, p0, p0, 0};
+      if (p0 < p1) {
+        uint32_t w = lb_ts(src, sb, p0, src.ts(p0) - a.within);
+        d = UnitDesc{p0, p1, w, 0};
+        int64_t tw = src.ts(w), tl = src.ts(p1 - 1);
+        if (tl - tw > 0x7fffffffll || tl < tw) {   // relative ts would not fit: HBM-list walker
+          uint32_t slot = atomicAdd(&st->n_ovf, 1u);
+          atomicMax(&st->ovf_need, p1 - w);
+          d.ovf = slot + 1;
+        } else {
+          len = p1 - w;
+        }
+      }
+    }
+    ud[u] = d;
+  }
+  // wave max -> tile rows
+  uint32_t m = len;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0 && (u >> 6) < (a.n_units + 63) / 64) wlen[u >> 6] = (m + TROWS - 1) / TROWS * TROWS;
+}
+
+// row-block -> wave map
+static __global__ void k_rowmap(const uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wrow, uint32_t nw,
+                         uint32_t* __restrict__ map) {
+  uint32_t W = blockIdx.x * blockDim.x + threadIdx.x;
+  if (W >= nw) return;
+  for (uint32_t q = wrow[W] / TROWS, e = (wrow[W] + wlen[W]) / TROWS; q < e; ++q) map[q] = W;
+}
+
+// sorted records -> tiles, through an LDS transpose (coalesced reads per unit, 1 KB rows out)
+template <class T>
+__global__ void __launch_bounds__(256) k_transpose(const WRec<T>* __restrict__ srec, const UnitDesc* __restrict__ ud,
+                                                   const uint32_t* __restrict__ wrow, const uint32_t* __restrict__ map,
+                                                   uint32_t nq, WRec<T>* __restrict__ tile) {
+  __shared__ WRec<T> t[TROWS][64];
+  for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    const uint32_t W = map[q];
+    const uint32_t i0 = q * TROWS - wrow[W];
+    for (uint32_t idx = threadIdx.x; idx < TROWS * 64; idx += blockDim.x) {
+      const uint32_t l = idx / TROWS, ii = idx % TROWS;
+      const UnitDesc d = ud[W * 64 + l];
+      WRec<T> r;
+      const uint32_t len = (d.p1 > d.p0 && !d.ovf) ? d.p1 - d.w : 0;
+      if (i0 + ii < len) r = srec[d.w + i0 + ii];
+      else { memset(&r, 0, sizeof(r)); }
+      t[ii][l ^ ii] = r;
+    }
+    __syncthreads();
+    for (uint32_t idx = threadIdx.x; idx < TROWS * 64; idx += blockDim.x) {
+      const uint32_t ii = idx / 64, l = idx % 64;
+      tile[(size_t)(q * TROWS + ii) * 64 + l] = t[ii][l ^ ii];
+    }
+    __syncthreads();
+  }
+}
+
+// walker over tiles (partitioned, LDS list).  All 64 lanes step through rows together.
+template <class T, int OP, bool WRITE>
+__global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T> src, const uint32_t* __restrict__ seg_b,
+                                                       const uint32_t* __restrict__ seg_e,
+                                                       const UnitDesc* __restrict__ ud,
+                                                       const uint32_t* __restrict__ wlen,
+                                                       const uint32_t* __restrict__ wrow,
+                                                       const WRec<T>* __restrict__ tile, uint32_t* __restrict__ cnt,
+                                                       const uint32_t* __restrict__ off, MRec* __restrict__ mrec,
+                                                       uint64_t* __restrict__ emask, WalkStats* __restrict__ st,
+                                                       UnitDesc* __restrict__ ud_w, uint32_t* __restrict__ carry_q0,
+                                                       uint32_t* __restrict__ carry_n) {
+  __shared__ __attribute__((aligned(16))) char lds[STACK_CAP * WALK_BLOCK * PendBytes<T, WRITE>::lds];
+  const uint32_t u = xcd_block(blockIdx.x, gridDim.x) * WALK_BLOCK + threadIdx.x;
+  const uint32_t W = __builtin_amdgcn_readfirstlane(u >> 6), lane = threadIdx.x & 63;
+  if ((W << 6) >= a.n_units) return;   // whole wave out of range (n_units need not be a multiple of 64)
+  const Virt& v = src.pk.v;
+  const UnitDesc d = u < a.n_units ? ud[u] : UnitDesc{0, 0, 0, 0};
+  bool active = d.p0 < d.p1 && !d.ovf;
+  const uint32_t p0 = d.p0, p1 = d.p1, w = d.w;
+  const uint32_t len = active ? p1 - w : 0;
+  const uint32_t rows = __builtin_amdgcn_readfirstlane(wlen[W]), base = __builtin_amdgcn_readfirstlane(wrow[W]);
+  Walker<T, WRITE, false, OP> Wk;
+  {
+    const size_t E = (size_t)STACK_CAP * WALK_BLOCK;
+    const size_t pb = WRITE ? 8 : 0;
+    Wk.L.pay = (int64_t*)lds + threadIdx.x;
+    Wk.L.val = (T*)(lds + E * pb) + threadIdx.x;
+    Wk.L.dts = (int32_t*)(lds + E * (pb + sizeof(T))) + threadIdx.x;
+    Wk.L.row = (uint32_t*)(lds + E * (pb + sizeof(T) + 4)) + threadIdx.x;
+    Wk.L.ts = nullptr;
+  }
+  const uint32_t k = u % a.K;
+  const uint32_t sb = active ? seg_b[k] : 0;
+  const int64_t tw = active ? src.ts(w) : 0;
+  Wk.L.base = tw;
+  Wk.prev_t = (active && w > sb) ? src.ts(w - 1) : tw;
+  const bool payload = v.pcol != nullptr;
+  const uint32_t chunk_i = active ? p0 - w : 0;   // rows before this index only rebuild the pending list
+  const WRec<T>* tp = tile + (size_t)base * 64 + lane;
+  WRec<T> cur[PF], nxt[PF];
+  uint32_t ofs[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) cur[j] = (j < (int)rows) ? tp[(size_t)j * 64] : WRec<T>{};
+  auto gather_offs = [&](uint32_t i0) {   // output offsets of the rows the count pass marked as emitting
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const uint64_t mj = (i0 + j < rows) ? emask[base + i0 + j] : 0ull;
+      const uint32_t r = cur[j].rowf & ROW_MASK;
+      ofs[j] = ((mj >> lane) & 1ull) ? off[r - v.nc] : 0u;
+    }
+  };
+  if (WRITE) gather_offs(0);
+  for (uint32_t i = 0; i < rows; i += PF) {
+    const uint32_t in = i + PF;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) nxt[j] = (in + j < rows) ? tp[(size_t)(in + j) * 64] : WRec<T>{};
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      bool e = false;
+      if (active && i + j < len && !Wk.overflow)
+        e = Wk.step(a, v, cur[j], i + j >= chunk_i, WRITE ? ofs[j] : 0u, cnt, mrec, payload);
+      if (!WRITE) {
+        const uint64_t b = __ballot(e);
+        if (lane == 0) emask[base + i + j] = b;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PF; ++j) cur[j] = nxt[j];
+    if (WRITE) gather_offs(in);
+  }
+  if (!active) return;
+  if (Wk.overflow) {
+    if (!WRITE) {
+      uint32_t slot = atomicAdd(&st->n_ovf, 1u);
+      atomicMax(&st->ovf_need, p1 - w);
+      ud_w[u].ovf = slot + 1;
+    }
+    return;
+  }
+  if (Wk.bad) atomicOr(&st->order_err, 1u);
+  const uint32_t se = seg_e[k];
+  if (WRITE && a.carry_out && p1 == se) {
     uint32_t q0 = lb_ts(src, sb, se, src.ts(se - 1) - a.within);
     carry_q0[k] = q0;
     carry_n[k] = se - q0;
@@ -844,6 +1019,24 @@ struct PushPlan {
   ProjPlan pp;
   int pcol = -1;              // e1 payload column carried in the pending list
 };
+
+template <class T, bool WRITE>
+static void launch_walk_t(int op, dim3 g, dim3 b, hipStream_t st, const WalkArgs& wa, const Src<T>& src,
+                          const uint32_t* seg_b, const uint32_t* seg_e, UnitDesc* ud, const uint32_t* wlen,
+                          const uint32_t* wrow, const WRec<T>* tile, uint32_t* cnt, const uint32_t* off, MRec* mrec,
+                          uint64_t* emask, WalkStats* wst, uint32_t* carry_q0, uint32_t* carry_n) {
+#define SG_WALK_T(OPV)                                                                                          \
+  hipLaunchKernelGGL((k_walk_t<T, OPV, WRITE>), g, b, 0, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, \
+                     mrec, emask, wst, ud, carry_q0, carry_n)
+  switch (op) {
+    case 2: SG_WALK_T(2); break;
+    case 3: SG_WALK_T(3); break;
+    case 4: SG_WALK_T(4); break;
+    default: SG_WALK_T(5); break;
+  }
+#undef SG_WALK_T
+  HIPCHK(hipGetLastError());
+}
 
 template <class T>
 static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& plan) {
@@ -1037,9 +1230,44 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
   HIPCHK(hipMemsetAsync(wst, 0, sizeof(WalkStats), st));
   if (wa.carry_out) HIPCHK(hipMemsetAsync(carry_n, 0, sizeof(uint32_t) * (K + 1), st));
   const dim3 wblk(WALK_BLOCK), wgrd((unsigned)((units + WALK_BLOCK - 1) / WALK_BLOCK));
-  hipLaunchKernelGGL((k_walk<T, false, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
-                     (MRec*)nullptr, emap, wst, (char*)nullptr, carry_q0, carry_n);
-  HIPCHK(hipGetLastError());
+  const uint32_t nw = (uint32_t)((units + 63) / 64);
+  uint32_t* wlen = nullptr;
+  uint32_t* wrow = nullptr;
+  R* tile = nullptr;
+  uint64_t* emask = nullptr;
+  if (d.partitioned) {
+    // lane-interleaved tiles: unit ranges -> per-wave rows -> LDS transpose of the sorted records
+    wlen = (uint32_t*)h->ws.get("wlen", sizeof(uint32_t) * (nw + 1), st);
+    wrow = (uint32_t*)h->ws.get("wrow", sizeof(uint32_t) * (nw + 1), st);
+    HIPCHK(hipMemsetAsync(wlen, 0, sizeof(uint32_t) * (nw + 1), st));
+    hipLaunchKernelGGL((k_units<T>), dim3((unsigned)(nw * 64 + 255) / 256), dim3(256), 0, st, wa, src, seg_b, seg_e,
+                       ud, wlen, wst);
+    HIPCHK(hipGetLastError());
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, wlen, wrow, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("wscan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, wlen, wrow, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t rows_total = 0;
+    HIPCHK(hipMemcpyAsync(&rows_total, wrow + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    tile = (R*)h->ws.get("tile", sizeof(R) * 64 * (size_t)std::max<uint32_t>(rows_total, 1), st);
+    emask = (uint64_t*)h->ws.get("emask", sizeof(uint64_t) * std::max<uint32_t>(rows_total, 1), st);
+    const uint32_t nq = rows_total / TROWS;
+    if (nq) {
+      uint32_t* rmap = (uint32_t*)h->ws.get("rowmap", sizeof(uint32_t) * nq, st);
+      hipLaunchKernelGGL(k_rowmap, dim3((nw + 255) / 256), dim3(256), 0, st, wlen, wrow, nw, rmap);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL((k_transpose<T>), dim3(std::min<uint32_t>(nq, 256 * 32)), dim3(256), 0, st, src.srec, ud, wrow,
+                         rmap, nq, tile);
+      HIPCHK(hipGetLastError());
+    }
+    launch_walk_t<T, false>(op, wgrd, wblk, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, (MRec*)nullptr,
+                            emask, wst, carry_q0, carry_n);
+  } else {
+    hipLaunchKernelGGL((k_walk<T, false, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
+                       (MRec*)nullptr, emap, wst, (char*)nullptr, carry_q0, carry_n);
+    HIPCHK(hipGetLastError());
+  }
   auto scan_counts = [&]() {
     size_t tb = 0;
     HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
@@ -1081,9 +1309,14 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
     wa.out_base = h->out.n;
     MRec* mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
-    hipLaunchKernelGGL((k_walk<T, true, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec, emap,
-                       wst, (char*)nullptr, carry_q0, carry_n);
-    HIPCHK(hipGetLastError());
+    if (d.partitioned) {
+      launch_walk_t<T, true>(op, wgrd, wblk, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, mrec, emask, wst,
+                             carry_q0, carry_n);
+    } else {
+      hipLaunchKernelGGL((k_walk<T, true, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec, emap,
+                         wst, (char*)nullptr, carry_q0, carry_n);
+      HIPCHK(hipGetLastError());
+    }
     if (hs.n_ovf) {
       hipLaunchKernelGGL((k_walk<T, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec,
                          emap, wst, big, carry_q0, carry_n);
