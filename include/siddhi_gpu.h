@@ -175,6 +175,7 @@ typedef struct sg_matches {
 typedef struct sg_timing {
   float pred_ms, partition_ms, match_ms, output_ms, total_ms;   /* HIP-event times of the last push */
   int64_t events, matches;
+  int64_t spilled_units;        /* closed form: (chunk, key) units whose pending list spilled to HBM */
 } sg_timing;
 
 typedef struct sg_handle sg_handle;

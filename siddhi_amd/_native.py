@@ -73,7 +73,8 @@ class sg_match_records(ct.Structure):
 
 class sg_timing(ct.Structure):
     _fields_ = [("pred_ms", ct.c_float), ("partition_ms", ct.c_float), ("match_ms", ct.c_float),
-                ("output_ms", ct.c_float), ("total_ms", ct.c_float), ("events", I64), ("matches", I64)]
+                ("output_ms", ct.c_float), ("total_ms", ct.c_float), ("events", I64), ("matches", I64),
+                ("spilled_units", I64)]
 
 
 _lib = None

@@ -257,6 +257,7 @@ int sg_get_timing(sg_handle* hh, sg_timing* t) {
     t->total_ms = a + b + c + d;
     t->events = h.last_events;
     t->matches = h.last_matches;
+    t->spilled_units = h.last_spilled;
   });
 }
 

@@ -1365,6 +1365,7 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
   }
   h->last_events = n;
   h->last_matches = total;
+  h->last_spilled = hs.n_ovf;
 }
 
 // Projection plan: which select columns are the compared value and which are gathered by row at emission.

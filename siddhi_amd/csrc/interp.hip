@@ -348,6 +348,7 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   h->mark(4);
   h->last_events = n;
+  h->last_spilled = 0;
   h->last_matches = (int64_t)total;
 }
 

@@ -96,7 +96,7 @@ struct SgHandle {
   OutStore out;
   std::string err;
   hipEvent_t ev[8] = {};
-  int64_t last_events = 0, last_matches = 0;
+  int64_t last_events = 0, last_matches = 0, last_spilled = 0;
   int pushes = 0;
   int64_t clock = 0;          // playback clock (TimestampGeneratorImpl.lastEventTimestamp)
   uint32_t key_bound_seen = 0;
