@@ -11,7 +11,7 @@ import numpy as np
 from . import lowering as L
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsiddhi_gpu.so")
+LIB_PATH = os.environ.get("SIDDHI_GPU_LIB") or os.path.join(HERE, "libsiddhi_gpu.so")   # override: experiments
 
 SG_MAX_STATES, SG_MAX_STREAMS, SG_MAX_SELECT, SG_MAX_RET, SG_MAX_COLS, SG_MAX_CODE = 16, 16, 32, 16, 64, 512
 SG_ABI_VERSION = 1

@@ -41,6 +41,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -233,31 +234,56 @@ __device__ __forceinline__ int64_t v_payload(const Virt& v, uint32_t r) {
 }
 
 // Walker record: one row of one key as the walkers read it (key-sorted for partitioned queries).
-// rowf = virtual row | condition flags << 30.  16 bytes for 4-byte compared values: rocPRIM's tuned
-// 8-bit-digit onesweep path, and 8 records per 128-B line for the walkers' whole-line loads.
+// rowf = virtual row | condition flags << 30.  Narrow format (default): time as a 32-bit offset from the
+// push's first virtual row, plus (4-byte values) e1's payload attribute in 32 bits -- 16 bytes, rocPRIM's
+// tuned 8-bit-digit onesweep path and 8 records per 128-B line.  Wide format (fallback when a push spans
+// more than 2^31 ms): 64-bit time, no payload.
 static const uint32_t ROW_MASK = 0x3fffffffu;
-template <class T, bool WIDE = (sizeof(T) > 4)>
-struct WRec {
+template <class T, bool N, int S = (int)sizeof(T)>
+struct WRec {   // wide
   int64_t ts;
   uint32_t rowf;
   T val;
+  static constexpr bool has_pay = false;
+  __host__ __device__ int64_t t() const { return ts; }
+  __host__ __device__ int64_t p(int) const { return 0; }
 };
 template <class T>
-struct WRec<T, true> {
-  int64_t ts;
+struct WRec<T, true, 4> {   // narrow, 4-byte value: room for a 32-bit payload
+  int32_t dts;
   uint32_t rowf;
-  uint32_t pad;
   T val;
+  int32_t pay;
+  static constexpr bool has_pay = true;
+  __host__ __device__ int64_t t() const { return dts; }
+  __host__ __device__ int64_t p(int pzero) const { return pzero ? (int64_t)(uint32_t)pay : (int64_t)pay; }
 };
+template <class T>
+struct WRec<T, true, 8> {   // narrow, 8-byte value
+  int32_t dts;
+  uint32_t rowf;
+  T val;
+  static constexpr bool has_pay = false;
+  __host__ __device__ int64_t t() const { return dts; }
+  __host__ __device__ int64_t p(int) const { return 0; }
+};
+struct alignas(16) Blob16 { uint32_t w[4]; };   // 16-byte records sort as one opaque type
 
-template <class T>
+static const uint32_t PK_TS_RANGE = 1, PK_PAY_RANGE = 2;   // k_pack flags
+
+template <class T, bool N>
 struct PackFn {   // builds the walker record of virtual row r (coalesced when r is sequential)
   Virt v;
-  __host__ __device__ WRec<T> operator()(uint32_t r) const {
-    WRec<T> o;
+  __host__ __device__ WRec<T, N> operator()(uint32_t r) const {
+    WRec<T, N> o;
 #ifdef __HIP_DEVICE_COMPILE__
     uint32_t f = v_flags(v, r);
-    o.ts = v_ts(v, r);
+    if constexpr (N) {
+      o.dts = (int32_t)(v_ts(v, r) - v_ts(v, 0));
+      if constexpr (WRec<T, N>::has_pay) o.pay = v.pcol ? (int32_t)v_payload(v, r) : 0;
+    } else {
+      o.ts = v_ts(v, r);
+    }
     o.rowf = r | (f << 30);
     o.val = v_val<T>(v, r, (f & F_CAND) || v.val_a == v.val_b);
 #else
@@ -268,44 +294,56 @@ struct PackFn {   // builds the walker record of virtual row r (coalesced when r
   }
 };
 
-template <class T>
+template <class T, bool N>
 struct Src {   // position -> record: the key-sorted records, or (unpartitioned) the rows themselves
-  const WRec<T>* srec;
-  PackFn<T> pk;
-  __device__ __forceinline__ WRec<T> at(uint32_t p) const { return srec ? srec[p] : pk(p); }
+  const WRec<T, N>* srec;
+  PackFn<T, N> pk;
+  __device__ __forceinline__ WRec<T, N> at(uint32_t p) const { return srec ? srec[p] : pk(p); }
   __device__ __forceinline__ uint32_t row(uint32_t p) const { return srec ? (srec[p].rowf & ROW_MASK) : p; }
-  __device__ __forceinline__ int64_t ts(uint32_t p) const { return srec ? srec[p].ts : v_ts(pk.v, p); }
+  __device__ __forceinline__ int64_t ts(uint32_t p) const { return srec ? srec[p].t() : pk(p).t(); }
 };
 
 // Records per group load: G records = a whole number of 128-B lines, loaded by one lane at once so a
 // line is fetched into registers exactly once (thousands of per-lane streams would otherwise thrash L2).
-template <class T>
+template <class T, bool N>
 struct Grp {
-  static constexpr int G = sizeof(WRec<T>) == 16 ? 8 : 16;
-  static constexpr int QW = G * (int)sizeof(WRec<T>) / 16;
+  static constexpr int G = sizeof(WRec<T, N>) == 16 ? 8 : 16;
+  static constexpr int QW = G * (int)sizeof(WRec<T, N>) / 16;
   typedef uint32_t U4 __attribute__((ext_vector_type(4)));
   U4 q[QW];
-  __device__ __forceinline__ void load(const WRec<T>* base) {
+  __device__ __forceinline__ void load(const WRec<T, N>* base) {
     const U4* p = (const U4*)base;
 #pragma unroll
     for (int j = 0; j < QW; ++j) q[j] = __builtin_nontemporal_load(p + j);
   }
-  __device__ __forceinline__ WRec<T> rec(int i) const {
-    WRec<T> r;
-    __builtin_memcpy(&r, (const char*)q + i * sizeof(WRec<T>), sizeof(WRec<T>));
+  __device__ __forceinline__ WRec<T, N> rec(int i) const {
+    WRec<T, N> r;
+    __builtin_memcpy(&r, (const char*)q + i * sizeof(WRec<T, N>), sizeof(WRec<T, N>));
     return r;
   }
 };
 
-// walker records + sort keys of every virtual row, in arrival order (coalesced)
-template <class T>
-__global__ void __launch_bounds__(256) k_pack(PackFn<T> pk, KeyOf kf, int64_t nt, WRec<T>* __restrict__ rec,
-                                              uint32_t* __restrict__ keys) {
+// walker records + sort keys of every virtual row, in arrival order (coalesced).  Narrow records flag a
+// time outside +-2^31 ms of the first virtual row, or a payload that does not fit 32 bits.
+template <class T, bool N>
+__global__ void __launch_bounds__(256) k_pack(PackFn<T, N> pk, KeyOf kf, int64_t nt, WRec<T, N>* __restrict__ rec,
+                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ flags) {
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint32_t bad = 0;
+  const int64_t t0 = N ? v_ts(pk.v, 0) : 0;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nt; r += stride) {
     rec[r] = pk((uint32_t)r);
     keys[r] = kf((uint32_t)r);
+    if (N) {
+      const int64_t d = v_ts(pk.v, (uint32_t)r) - t0;
+      if (d != (int64_t)(int32_t)d) bad |= PK_TS_RANGE;
+      if (WRec<T, N>::has_pay && pk.v.pcol && pk.v.pw == 8) {
+        const int64_t pv = v_payload(pk.v, (uint32_t)r);
+        if (pv != (int64_t)(int32_t)pv) bad |= PK_PAY_RANGE;
+      }
+    }
   }
+  if (bad) atomicOr(flags, bad);
 }
 
 static __global__ void __launch_bounds__(256) k_bounds(const uint32_t* __restrict__ skey, int64_t n, uint32_t kb,
@@ -354,6 +392,11 @@ struct WalkStats {
   uint32_t pad;
 };
 
+struct LdsPlan {   // per-push layout of the record walk's LDS planes (count walk: value + time only)
+  int32_t pay;     // 1: narrow payload plane
+  int32_t row;     // 1: e1 row plane
+};
+
 struct WalkArgs {
   int64_t nt;                 // virtual rows
   int64_t within;
@@ -372,6 +415,8 @@ struct WalkArgs {
   int32_t stride;
   int64_t out_base;
   uint32_t big_cap;           // entries per HBM list (BIG)
+  LdsPlan lp;                 // record walk LDS planes
+  int32_t pay_in_rec;         // e1 payload rides in the (narrow) walker records
 };
 
 template <class T> __device__ __forceinline__ bool is_nan_val(T) { return false; }
@@ -394,39 +439,72 @@ template <> __device__ __forceinline__ int64_t val_bits<double>(double v) { retu
 template <> __device__ __forceinline__ int64_t val_bits<int32_t>(int32_t v) { return (int64_t)v; }
 template <> __device__ __forceinline__ int64_t val_bits<int64_t>(int64_t v) { return v; }
 
-// Pending list: (value, timestamp, row[, payload]) per partial.  LDS: ring of STACK_CAP entries per lane
-// (SoA, lane-strided: conflict-free), timestamps relative to the unit's first replayed row.  HBM (BIG): one
-// unbounded list per overflowed unit, indexed by push count (no wrap).  PAY: the record walk also keeps e1's
-// payload attribute.
-template <class T, bool BIG, bool PAY>
+// Pending list: value + timestamp per partial, plus (record walk only) e1's payload attribute and e1's row
+// when a select gathers other e1 attributes.  LDS: ring of STACK_CAP entries per lane, SoA planes,
+// lane-strided (conflict-free); timestamps relative to the unit's first replayed row; payload narrowed to
+// 32 bits (a LONG that does not fit sends the unit to the HBM path).  The count walk keeps 8 B per entry, so
+// it runs at twice the residency of the record walk.  HBM (BIG): one unbounded list per overflowed unit,
+// indexed by push count (no wrap), 64-bit times and payloads.
+template <class T, bool BIG>
 struct PendList {
   T* val;
   int32_t* dts;
   int64_t* ts;
-  uint32_t* row;
-  int64_t* pay;
+  uint32_t* row;              // null: not kept
+  int32_t* pay32;             // LDS narrow payload (null: none)
+  int64_t* pay64;             // HBM payload
+  int32_t pzero;              // narrow payload is zero-extended (FLOAT bits) rather than sign-extended
   int64_t base;
   __device__ __forceinline__ uint32_t ix(uint32_t s) const { return BIG ? s : (s & (STACK_CAP - 1)) * WALK_BLOCK; }
   __device__ __forceinline__ T gv(uint32_t s) const { return val[ix(s)]; }
   __device__ __forceinline__ int64_t gts(uint32_t s) const { return BIG ? ts[ix(s)] : base + (int64_t)dts[ix(s)]; }
-  __device__ __forceinline__ uint32_t grow(uint32_t s) const { return row[ix(s)]; }
-  __device__ __forceinline__ int64_t gpay(uint32_t s) const { return PAY ? pay[ix(s)] : 0; }
+  __device__ __forceinline__ uint32_t grow(uint32_t s) const { return row ? row[ix(s)] : 0u; }
+  __device__ __forceinline__ int64_t gpay(uint32_t s) const {
+    if (BIG) return pay64 ? pay64[ix(s)] : 0;
+    if (!pay32) return 0;
+    int32_t x = pay32[ix(s)];
+    return pzero ? (int64_t)(uint32_t)x : (int64_t)x;
+  }
   __device__ __forceinline__ void put(uint32_t s, T v, int64_t t, uint32_t r, int64_t p) {
     uint32_t i = ix(s);
     val[i] = v;
     if (BIG) ts[i] = t; else dts[i] = (int32_t)(t - base);
-    row[i] = r;
-    if (PAY) pay[i] = p;
+    if (row) row[i] = r;
+    if (BIG) { if (pay64) pay64[i] = p; } else if (pay32) pay32[i] = (int32_t)p;
   }
 };
-template <class T, bool PAY>
-struct PendBytes {   // bytes per entry
-  static constexpr int lds = sizeof(T) + 8 + (PAY ? 8 : 0);
-  static constexpr int hbm = sizeof(T) + 12 + (PAY ? 8 : 0);
-};
-
 template <class T>
-__device__ __forceinline__ uint32_t lb_row(const Src<T>& src, uint32_t lo, uint32_t hi, uint32_t target, bool part) {
+struct PendBytes {   // bytes per entry
+  static int lds(bool write, const LdsPlan& lp) { return (int)sizeof(T) + 4 + (write ? 4 * (lp.pay + lp.row) : 0); }
+  static constexpr int hbm = sizeof(T) + 20;   // val, ts, row, payload
+};
+// LDS planes of one block: [val][dts][pay32?][row?], each STACK_CAP * WALK_BLOCK entries
+template <class T, bool BIG>
+__device__ __forceinline__ void lds_planes(PendList<T, BIG>& L, char* lds, bool write, const LdsPlan& lp) {
+  const size_t E = (size_t)STACK_CAP * WALK_BLOCK;
+  char* p = lds;
+  L.val = (T*)p + threadIdx.x; p += E * sizeof(T);
+  L.dts = (int32_t*)p + threadIdx.x; p += E * 4;
+  L.pay32 = nullptr;
+  L.row = nullptr;
+  if (write && lp.pay) { L.pay32 = (int32_t*)p + threadIdx.x; p += E * 4; }
+  if (write && lp.row) { L.row = (uint32_t*)p + threadIdx.x; p += E * 4; }
+  L.ts = nullptr;
+  L.pay64 = nullptr;
+}
+template <class T, bool BIG>
+__device__ __forceinline__ void hbm_planes(PendList<T, BIG>& L, char* big, uint32_t slot, size_t cap) {
+  char* base = big + (size_t)slot * cap * PendBytes<T>::hbm;
+  L.ts = (int64_t*)base;
+  L.pay64 = (int64_t*)(base + cap * 8);
+  L.val = (T*)(base + cap * 16);
+  L.row = (uint32_t*)(base + cap * (16 + sizeof(T)));
+  L.dts = nullptr;
+  L.pay32 = nullptr;
+}
+
+template <class T, bool N>
+__device__ __forceinline__ uint32_t lb_row(const Src<T, N>& src, uint32_t lo, uint32_t hi, uint32_t target, bool part) {
   if (!part) return target < lo ? lo : (target > hi ? hi : target);
   while (lo < hi) {
     uint32_t mid = lo + ((hi - lo) >> 1);
@@ -434,8 +512,8 @@ __device__ __forceinline__ uint32_t lb_row(const Src<T>& src, uint32_t lo, uint3
   }
   return lo;
 }
-template <class T>
-__device__ __forceinline__ uint32_t lb_ts(const Src<T>& src, uint32_t lo, uint32_t hi, int64_t tmin) {
+template <class T, bool N>
+__device__ __forceinline__ uint32_t lb_ts(const Src<T, N>& src, uint32_t lo, uint32_t hi, int64_t tmin) {
   while (lo < hi) {
     uint32_t mid = lo + ((hi - lo) >> 1);
     if (src.ts(mid) < tmin) lo = mid + 1; else hi = mid;
@@ -460,53 +538,53 @@ __global__ void __launch_bounds__(256) k_project(WalkArgs a, Virt v, ProjPlan pp
                                                  int64_t total, char* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char stage[];   // 256 records, written out contiguously
   const int64_t per = (int64_t)blockDim.x;
-  for (int64_t s0 = (int64_t)blockIdx.x * per; s0 < total; s0 += (int64_t)gridDim.x * per) {
-    const int64_t sl = s0 + threadIdx.x;
-    if (sl < total) {
-      const MRec mr = mrec[sl];
-      const uint32_t r1 = mr.r1, r2 = mr.r2;
-      const uint64_t b = r2 - v.nc;
-      const uint32_t rank = (uint32_t)(sl - (int64_t)off[b]);
-      const uint32_t key = a.partitioned ? (uint32_t)v.key[b] : 0u;
-      const int64_t t2 = v.ts[b];
-      int64_t* o = (int64_t*)(stage + (size_t)threadIdx.x * a.stride);
-      uint32_t nm = 0;
-      for (int s = 0; s < a.n_select; ++s) {
-        const bool s2 = pp.src[s] != 0;
-        const int kind = pp.kind[s];
-        int64_t bits = 0;
-        if (kind == 0) {
-          bits = mr.p1;
-        } else if (kind == 1) {
-          bits = s2 ? val_bits<T>(v_val<T>(v, r2, v.val_a == v.val_b)) : mr.v1;
-        } else if (kind == 2) {
-          nm |= 1u << s;
-        } else {
-          const uint32_t r = s2 ? r2 : r1;
-          SgVal x = r < v.nc ? sg_read_col(cc, pp.col[s], pp.type[s], r) : sg_read_col(bc, pp.col[s], pp.type[s], r - v.nc);
-          if (x.null) nm |= 1u << s;
-          bits = sg_val_bits(x);
-        }
-        o[4 + s] = bits;
+  const int64_t s0 = (int64_t)blockIdx.x * per;   // one match per thread: every gather in flight at once
+  const int64_t sl = s0 + threadIdx.x;
+  if (sl < total) {
+    const MRec mr = mrec[sl];
+    const uint32_t r1 = mr.r1, r2 = mr.r2;
+    const uint64_t b = r2 - v.nc;
+    const uint32_t ob = off[b];
+    const uint32_t key = a.partitioned ? (uint32_t)v.key[b] : 0u;
+    const int64_t t2 = v.ts[b];
+    const uint64_t trig = a.index ? a.index[b] : a.base_index + b;
+    int64_t* o = (int64_t*)(stage + (size_t)threadIdx.x * a.stride);
+    uint32_t nm = 0;
+    for (int s = 0; s < a.n_select; ++s) {
+      const bool s2 = pp.src[s] != 0;
+      const int kind = pp.kind[s];
+      int64_t bits = 0;
+      if (kind == 0) {
+        bits = mr.p1;
+      } else if (kind == 1) {
+        bits = s2 ? val_bits<T>(v_val<T>(v, r2, v.val_a == v.val_b)) : mr.v1;
+      } else if (kind == 2) {
+        nm |= 1u << s;
+      } else {
+        const uint32_t r = s2 ? r2 : r1;
+        SgVal x = r < v.nc ? sg_read_col(cc, pp.col[s], pp.type[s], r) : sg_read_col(bc, pp.col[s], pp.type[s], r - v.nc);
+        if (x.null) nm |= 1u << s;
+        bits = sg_val_bits(x);
       }
-      o[0] = (int64_t)(a.index ? a.index[b] : a.base_index + b);
-      o[1] = t2;
-      o[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (a.multi ? (uint32_t)a.b_slot : (0x800000u | rank))) << 32));
-      o[3] = (int64_t)nm;
+      o[4 + s] = bits;
     }
-    __syncthreads();
-    const int64_t nrec = (total - s0 < per) ? (total - s0) : per;
-    const size_t bytes = (size_t)nrec * a.stride;
-    char* dst = out + (size_t)(a.out_base + s0) * a.stride;
-    if ((((uintptr_t)dst) & 15) == 0) {
-      typedef uint32_t U4 __attribute__((ext_vector_type(4)));
-      for (size_t q = (size_t)threadIdx.x * 16; q < bytes; q += (size_t)per * 16)
-        *(U4*)(dst + q) = *(const U4*)(stage + q);
-    } else {
-      for (size_t q = (size_t)threadIdx.x * 8; q < bytes; q += (size_t)per * 8)
-        *(uint64_t*)(dst + q) = *(const uint64_t*)(stage + q);
-    }
-    __syncthreads();
+    const uint32_t rank = (uint32_t)(sl - (int64_t)ob);
+    o[0] = (int64_t)trig;
+    o[1] = t2;
+    o[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (a.multi ? (uint32_t)a.b_slot : (0x800000u | rank))) << 32));
+    o[3] = (int64_t)nm;
+  }
+  __syncthreads();
+  const int64_t nrec = (total - s0 < per) ? (total - s0) : per;
+  const size_t bytes = (size_t)nrec * a.stride;
+  char* dst = out + (size_t)(a.out_base + s0) * a.stride;
+  if ((((uintptr_t)dst) & 15) == 0) {
+    typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+    for (size_t q = (size_t)threadIdx.x * 16; q < bytes; q += (size_t)per * 16)
+      *(U4*)(dst + q) = *(const U4*)(stage + q);
+  } else {
+    for (size_t q = (size_t)threadIdx.x * 8; q < bytes; q += (size_t)per * 8)
+      *(uint64_t*)(dst + q) = *(const uint64_t*)(stage + q);
   }
 }
 
@@ -516,12 +594,28 @@ __device__ __forceinline__ bool cmp_sel(int op, T b, T a) { return cmp_op<T>(OP 
 
 template <class T, bool WRITE, bool BIG, int OP = 0>
 struct Walker {
-  PendList<T, BIG, WRITE> L;
+  // LDS path: times relative to the unit's first replayed row (the unit's span was checked to fit 31 bits);
+  // HBM-list path: absolute 64-bit times.
+  typedef typename std::conditional<BIG, int64_t, int32_t>::type TT;
+  PendList<T, BIG> L;
   uint32_t head = 0, top = 0;
-  int64_t prev_t;
+  TT prev_t;
+  TT within;
   bool bad = false;
   bool overflow = false;
   uint32_t ew = 0xffffffffu, ebits = 0;   // count pass: emit bitmap word being built
+  __device__ __forceinline__ void set_within(int64_t w) {
+    within = BIG ? (TT)w : (TT)(w > 0x7fffffffll ? 0x7fffffffll : w);   // a wider window never expires in-unit
+  }
+  __device__ __forceinline__ TT rel(int64_t t) const { return BIG ? (TT)t : (TT)(t - L.base); }
+  // order check against the row before the replay window (which may lie far outside the 31-bit span)
+  __device__ __forceinline__ void init_prev(int64_t before, int64_t first) {
+    if (BIG) prev_t = (TT)before;
+    else prev_t = before > first ? (TT)0x7fffffff : (TT)0;
+  }
+  __device__ __forceinline__ TT at(uint32_t s) const {
+    return BIG ? (TT)L.ts[L.ix(s)] : (TT)L.dts[L.ix(s)];
+  }
   __device__ __forceinline__ void flush_bits(uint32_t* __restrict__ emap) {
     if (ebits) atomicOr(&emap[ew], ebits);
     ebits = 0;
@@ -531,41 +625,51 @@ struct Walker {
     if (wi != ew) { flush_bits(emap); ew = wi; }
     ebits |= 1u << (pos & 31);
   }
+  __device__ __forceinline__ void push(T x, int64_t tabs, uint32_t r, int64_t pay) {
+    L.put(top, x, tabs, r, pay);
+    ++top;
+  }
   // returns true when this event (inside the unit's chunk) completed partials
-  __device__ __forceinline__ bool step(const WalkArgs& a, const Virt& v, const WRec<T>& rc, bool in_chunk,
+  template <class R>
+  __device__ __forceinline__ bool step(const WalkArgs& a, const Virt& v, const R& rc, bool in_chunk,
                                        uint32_t ofs, uint32_t* __restrict__ cnt, MRec* __restrict__ mrec,
-                                       bool payload) {
+                                       bool payload, int64_t pay = 0, bool pay_ready = false) {
     const uint32_t f = rc.rowf >> 30;
     if (!f) return false;
-    bool emitted = false;
-    const int64_t t = rc.ts;
+#ifdef SG_EXP_STUB_STEP
+    {   // experiment: memory streaming only
+      const uint32_t r = rc.rowf & ROW_MASK;
+      top += (uint32_t)(rc.t() & 1) + (uint32_t)(rc.val > (T)0);
+      const bool e = in_chunk && ((r & 7) == 0);
+      if (!WRITE && e) cnt[r - v.nc] = top;
+      return e;
+    }
+#endif
     const T x = rc.val;
+    const TT t = rel(rc.t());
     bad |= t < prev_t;
     prev_t = t;
     // lazy `within` expiry of the oldest partials (StreamPreStateProcessor.isExpired :102-113)
-    while (head != top && t - L.gts(head) > a.within) ++head;
+    while (head != top && t - at(head) > within) ++head;
     const uint32_t r = rc.rowf & ROW_MASK;
-    const bool emit = in_chunk && (r >= v.nc);
-    if ((f & F_CONS) && !is_nan_val<T>(x)) {
-      uint32_t m = 0;
+    const bool live = !is_nan_val<T>(x);
+    uint32_t m = 0;
+    if ((f & F_CONS) && live) {
       if (a.stack_mode) {
         // monotone stack: the completed partials are exactly a suffix, delivered oldest first
         while (top != head && cmp_sel<OP, T>(a.op, x, L.gv(top - 1))) { --top; ++m; }
-        if (emit && m) {
-          if (!WRITE) {
-            cnt[r - v.nc] = m;
-          } else {
-            for (uint32_t q = 0; q < m; ++q) {
-              MRec e;
-              e.r1 = L.grow(top + q);
-              e.r2 = r;
-              e.v1 = val_bits<T>(L.gv(top + q));
-              e.p1 = L.gpay(top + q);
-              mrec[ofs + q] = e;
-            }
+        if (WRITE && in_chunk && r >= v.nc) {
+          for (uint32_t q = 0; q < m; ++q) {
+            MRec e;
+            e.r1 = L.grow(top + q);
+            e.r2 = r;
+            e.v1 = val_bits<T>(L.gv(top + q));
+            e.p1 = L.gpay(top + q);
+            mrec[ofs + q] = e;
           }
         }
       } else {
+        const bool emit = in_chunk && (r >= v.nc);
         uint32_t wr = head;
         for (uint32_t s = head; s != top; ++s) {
           T e = L.gv(s);
@@ -580,19 +684,25 @@ struct Walker {
             }
             ++m;
           } else {
-            if (wr != s) L.put(wr, e, L.gts(s), L.grow(s), L.gpay(s));
+            if (wr != s) L.put(wr, e, BIG ? (int64_t)at(s) : L.base + (int64_t)at(s), L.grow(s), L.gpay(s));
             ++wr;
           }
         }
         top = wr;
-        if (!WRITE && emit && m) cnt[r - v.nc] = m;
       }
-      emitted = emit && m;
     }
-    if ((f & F_CAND) && !is_nan_val<T>(x)) {
+    const bool emitted = m && in_chunk && (r >= v.nc);
+    if (!WRITE && emitted) cnt[r - v.nc] = m;
+    if ((f & F_CAND) && live) {
       if (!BIG && top - head == STACK_CAP) { overflow = true; return emitted; }
-      L.put(top, x, t, r, (WRITE && payload) ? v_payload(v, r) : 0);
-      ++top;
+      int64_t pv = 0;
+      if (WRITE && payload) {
+        if (R::has_pay && a.pay_in_rec) pv = rc.p(v.pfloat);
+        else pv = pay_ready ? pay : v_payload(v, r);
+      }
+      // the LDS ring keeps 32 payload bits: a wider LONG value sends the unit to the HBM path
+      if (!BIG && WRITE && payload && L.pay32 && !L.pzero && pv != (int64_t)(int32_t)pv) { overflow = true; return emitted; }
+      push(x, rc.t(), r, pv);
     }
     return emitted;
   }
@@ -600,14 +710,14 @@ struct Walker {
 
 // One lane per unit (chunk c, key k).  WRITE=false: count pass (also fixes the unit's replay range);
 // WRITE=true: record pass.  BIG: only units that overflowed the LDS ring, with an HBM list.
-template <class T, bool WRITE, bool BIG>
-__global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, const uint32_t* __restrict__ seg_b,
+template <class T, bool N, bool WRITE, bool BIG>
+__global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, const uint32_t* __restrict__ seg_b,
                                                      const uint32_t* __restrict__ seg_e, UnitDesc* __restrict__ ud,
                                                      uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
                                                      MRec* __restrict__ mrec, uint32_t* __restrict__ emap,
                                                      WalkStats* __restrict__ st, char* __restrict__ big,
                                                      uint32_t* __restrict__ carry_q0, uint32_t* __restrict__ carry_n) {
-  __shared__ __attribute__((aligned(16))) char lds[BIG ? 16 : (STACK_CAP * WALK_BLOCK * PendBytes<T, WRITE>::lds)];
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   const uint32_t u = xcd_block(blockIdx.x, gridDim.x) * WALK_BLOCK + threadIdx.x;
   if (u >= a.n_units) return;
   const Virt& v = src.pk.v;
@@ -637,23 +747,9 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, con
     if (BIG != (ovf != 0)) return;
   }
   Walker<T, WRITE, BIG> W;
-  if (BIG) {
-    size_t cap = a.big_cap;
-    char* base = big + (size_t)(ovf - 1) * cap * PendBytes<T, true>::hbm;
-    W.L.ts = (int64_t*)base;
-    W.L.pay = (int64_t*)(base + cap * 8);
-    W.L.val = (T*)(base + cap * 16);
-    W.L.row = (uint32_t*)(base + cap * (16 + sizeof(T)));
-    W.L.dts = nullptr;
-  } else {
-    const size_t E = (size_t)STACK_CAP * WALK_BLOCK;
-    const size_t pb = WRITE ? 8 : 0;
-    W.L.pay = (int64_t*)lds + threadIdx.x;
-    W.L.val = (T*)(lds + E * pb) + threadIdx.x;
-    W.L.dts = (int32_t*)(lds + E * (pb + sizeof(T))) + threadIdx.x;
-    W.L.row = (uint32_t*)(lds + E * (pb + sizeof(T) + 4)) + threadIdx.x;
-    W.L.ts = nullptr;
-  }
+  if (BIG) hbm_planes<T, BIG>(W.L, big, ovf - 1, a.big_cap);
+  else lds_planes<T, BIG>(W.L, lds, WRITE, a.lp);
+  W.L.pzero = v.pfloat;
   const bool payload = v.pcol != nullptr;
   const int64_t tw = src.ts(w);
   W.L.base = tw;
@@ -666,15 +762,16 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, con
     int64_t tl = src.ts(p1 - 1);
     if (tl - tw > 0x7fffffffll || tl < tw) { mark_overflow(); return; }   // relative ts would not fit
   }
-  W.prev_t = (w > sb) ? src.ts(w - 1) : tw;
+  W.set_within(a.within);
+  W.init_prev((w > sb) ? src.ts(w - 1) : tw, tw);
   // record walk: output offsets only for the positions the count pass marked as emitting
-  auto off_of = [&](const WRec<T>& rc, uint32_t pos, uint32_t bits) -> uint32_t {
+  auto off_of = [&](const WRec<T, N>& rc, uint32_t pos, uint32_t bits) -> uint32_t {
     uint32_t r = rc.rowf & ROW_MASK;
     return (bits && pos >= p0 && pos < p1 && r >= v.nc) ? off[r - v.nc] : 0u;
   };
   if (src.srec) {
     // key-sorted records: whole-line group loads, next group in flight while this one is walked
-    typedef Grp<T> GT;
+    typedef Grp<T, N> GT;
     const uint32_t G = GT::G;
     GT cur, nxt;
     uint32_t g = w & ~(G - 1);
@@ -711,7 +808,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, con
   } else {
     // unpartitioned: the rows themselves, in order
     for (uint32_t p = w; p < p1; ++p) {
-      WRec<T> rc = src.pk(p);
+      WRec<T, N> rc = src.pk(p);
       uint32_t o = 0;
       if (WRITE) o = off_of(rc, p, (emap[p >> 5] >> (p & 31)) & 1u);
       if (W.step(a, v, rc, p >= p0, o, cnt, mrec, payload) && !WRITE) W.mark_emit(p, emap);
@@ -739,8 +836,8 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T> src, con
 
 // unit replay ranges (p0, p1, w) + per-wave tile length (rows, padded to TROWS)
 static const int TROWS = 16;
-template <class T>
-__global__ void __launch_bounds__(256) k_units(WalkArgs a, Src<T> src, const uint32_t* __restrict__ seg_b,
+template <class T, bool N>
+__global__ void __launch_bounds__(256) k_units(WalkArgs a, Src<T, N> src, const uint32_t* __restrict__ seg_b,
                                                const uint32_t* __restrict__ seg_e, UnitDesc* __restrict__ ud,
                                                uint32_t* __restrict__ wlen, WalkStats* __restrict__ st) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -785,18 +882,18 @@ static __global__ void k_rowmap(const uint32_t* __restrict__ wlen, const uint32_
 }
 
 // sorted records -> tiles, through an LDS transpose (coalesced reads per unit, 1 KB rows out)
-template <class T>
-__global__ void __launch_bounds__(256) k_transpose(const WRec<T>* __restrict__ srec, const UnitDesc* __restrict__ ud,
+template <class T, bool N>
+__global__ void __launch_bounds__(256) k_transpose(const WRec<T, N>* __restrict__ srec, const UnitDesc* __restrict__ ud,
                                                    const uint32_t* __restrict__ wrow, const uint32_t* __restrict__ map,
-                                                   uint32_t nq, WRec<T>* __restrict__ tile) {
-  __shared__ WRec<T> t[TROWS][64];
+                                                   uint32_t nq, WRec<T, N>* __restrict__ tile) {
+  __shared__ WRec<T, N> t[TROWS][64];
   for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
     const uint32_t W = map[q];
     const uint32_t i0 = q * TROWS - wrow[W];
     for (uint32_t idx = threadIdx.x; idx < TROWS * 64; idx += blockDim.x) {
       const uint32_t l = idx / TROWS, ii = idx % TROWS;
       const UnitDesc d = ud[W * 64 + l];
-      WRec<T> r;
+      WRec<T, N> r;
       const uint32_t len = (d.p1 > d.p0 && !d.ovf) ? d.p1 - d.w : 0;
       if (i0 + ii < len) r = srec[d.w + i0 + ii];
       else { memset(&r, 0, sizeof(r)); }
@@ -812,18 +909,18 @@ __global__ void __launch_bounds__(256) k_transpose(const WRec<T>* __restrict__ s
 }
 
 // walker over tiles (partitioned, LDS list).  All 64 lanes step through rows together.
-template <class T, int OP, bool WRITE>
-__global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T> src, const uint32_t* __restrict__ seg_b,
+template <class T, bool N, int OP, bool WRITE>
+__global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src, const uint32_t* __restrict__ seg_b,
                                                        const uint32_t* __restrict__ seg_e,
                                                        const UnitDesc* __restrict__ ud,
                                                        const uint32_t* __restrict__ wlen,
                                                        const uint32_t* __restrict__ wrow,
-                                                       const WRec<T>* __restrict__ tile, uint32_t* __restrict__ cnt,
+                                                       const WRec<T, N>* __restrict__ tile, uint32_t* __restrict__ cnt,
                                                        const uint32_t* __restrict__ off, MRec* __restrict__ mrec,
                                                        uint64_t* __restrict__ emask, WalkStats* __restrict__ st,
                                                        UnitDesc* __restrict__ ud_w, uint32_t* __restrict__ carry_q0,
                                                        uint32_t* __restrict__ carry_n) {
-  __shared__ __attribute__((aligned(16))) char lds[STACK_CAP * WALK_BLOCK * PendBytes<T, WRITE>::lds];
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   const uint32_t u = xcd_block(blockIdx.x, gridDim.x) * WALK_BLOCK + threadIdx.x;
   const uint32_t W = __builtin_amdgcn_readfirstlane(u >> 6), lane = threadIdx.x & 63;
   if ((W << 6) >= a.n_units) return;   // whole wave out of range (n_units need not be a multiple of 64)
@@ -834,53 +931,54 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T> src, c
   const uint32_t len = active ? p1 - w : 0;
   const uint32_t rows = __builtin_amdgcn_readfirstlane(wlen[W]), base = __builtin_amdgcn_readfirstlane(wrow[W]);
   Walker<T, WRITE, false, OP> Wk;
-  {
-    const size_t E = (size_t)STACK_CAP * WALK_BLOCK;
-    const size_t pb = WRITE ? 8 : 0;
-    Wk.L.pay = (int64_t*)lds + threadIdx.x;
-    Wk.L.val = (T*)(lds + E * pb) + threadIdx.x;
-    Wk.L.dts = (int32_t*)(lds + E * (pb + sizeof(T))) + threadIdx.x;
-    Wk.L.row = (uint32_t*)(lds + E * (pb + sizeof(T) + 4)) + threadIdx.x;
-    Wk.L.ts = nullptr;
-  }
+  lds_planes<T, false>(Wk.L, lds, WRITE, a.lp);
+  Wk.L.pzero = v.pfloat;
   const uint32_t k = u % a.K;
   const uint32_t sb = active ? seg_b[k] : 0;
   const int64_t tw = active ? src.ts(w) : 0;
   Wk.L.base = tw;
-  Wk.prev_t = (active && w > sb) ? src.ts(w - 1) : tw;
+  Wk.set_within(a.within);
+  Wk.init_prev((active && w > sb) ? src.ts(w - 1) : tw, tw);
   const bool payload = v.pcol != nullptr;
   const uint32_t chunk_i = active ? p0 - w : 0;   // rows before this index only rebuild the pending list
-  const WRec<T>* tp = tile + (size_t)base * 64 + lane;
-  WRec<T> cur[PF], nxt[PF];
-  uint32_t ofs[PF];
+  const WRec<T, N>* tp = tile + (size_t)base * 64 + lane;
+  WRec<T, N> ba[PF], bb[PF];
+  uint32_t oa[PF], ob[PF];
+  int64_t qa[PF], qb[PF];   // e1 payload of candidate rows, fetched a batch ahead
+  auto load_rows = [&](WRec<T, N>* buf, uint32_t i0) {
 #pragma unroll
-  for (int j = 0; j < PF; ++j) cur[j] = (j < (int)rows) ? tp[(size_t)j * 64] : WRec<T>{};
-  auto gather_offs = [&](uint32_t i0) {   // output offsets of the rows the count pass marked as emitting
+    for (int j = 0; j < PF; ++j) buf[j] = (i0 + j < rows) ? tp[(size_t)(i0 + j) * 64] : WRec<T, N>{};
+  };
+  auto gather_offs = [&](const WRec<T, N>* buf, uint32_t i0, uint32_t* ofs, int64_t* pq) {   // rows the count pass marked
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const uint64_t mj = (i0 + j < rows) ? emask[base + i0 + j] : 0ull;
-      const uint32_t r = cur[j].rowf & ROW_MASK;
+      const uint32_t r = buf[j].rowf & ROW_MASK;
       ofs[j] = ((mj >> lane) & 1ull) ? off[r - v.nc] : 0u;
+      pq[j] = (payload && !a.pay_in_rec && (buf[j].rowf >> 30) & F_CAND) ? v_payload(v, r) : 0;
     }
   };
-  if (WRITE) gather_offs(0);
-  for (uint32_t i = 0; i < rows; i += PF) {
-    const uint32_t in = i + PF;
-#pragma unroll
-    for (int j = 0; j < PF; ++j) nxt[j] = (in + j < rows) ? tp[(size_t)(in + j) * 64] : WRec<T>{};
+  auto process = [&](const WRec<T, N>* buf, uint32_t i0, const uint32_t* ofs, const int64_t* pq) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       bool e = false;
-      if (active && i + j < len && !Wk.overflow)
-        e = Wk.step(a, v, cur[j], i + j >= chunk_i, WRITE ? ofs[j] : 0u, cnt, mrec, payload);
+      if (active && i0 + j < len && !Wk.overflow)
+        e = Wk.step(a, v, buf[j], i0 + j >= chunk_i, WRITE ? ofs[j] : 0u, cnt, mrec, payload, WRITE ? pq[j] : 0, true);
       if (!WRITE) {
         const uint64_t b = __ballot(e);
-        if (lane == 0) emask[base + i + j] = b;
+        if (lane == 0) emask[base + i0 + j] = b;
       }
     }
-#pragma unroll
-    for (int j = 0; j < PF; ++j) cur[j] = nxt[j];
-    if (WRITE) gather_offs(in);
+  };
+  load_rows(ba, 0);
+  if (WRITE) gather_offs(ba, 0, oa, qa);
+  for (uint32_t i = 0; i < rows; i += 2 * PF) {   // rows is a multiple of TROWS = 2 * PF
+    load_rows(bb, i + PF);
+    if (WRITE) gather_offs(bb, i + PF, ob, qb);
+    process(ba, i, oa, qa);
+    load_rows(ba, i + 2 * PF);
+    if (WRITE) gather_offs(ba, i + 2 * PF, oa, qa);
+    process(bb, i + PF, ob, qb);
   }
   if (!active) return;
   if (Wk.overflow) {
@@ -909,8 +1007,8 @@ struct CarryBufs {
   uint8_t* nul[SG_MAX_COLS];
 };
 
-template <class T>
-__global__ void k_carry_copy(Src<T> src, uint32_t K, const uint32_t* __restrict__ q0s,
+template <class T, bool N>
+__global__ void k_carry_copy(Src<T, N> src, uint32_t K, const uint32_t* __restrict__ q0s,
                              const uint32_t* __restrict__ ns, const uint32_t* __restrict__ offs, int n_cols,
                              const int32_t* __restrict__ widths, SgCols bc, SgCols cc, CarryBufs dst) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1018,15 +1116,16 @@ static SgVal sg_val_from_bits_host(int64_t bits, int type) {
 struct PushPlan {
   ProjPlan pp;
   int pcol = -1;              // e1 payload column carried in the pending list
+  bool e1_row = false;        // some select gathers another e1 attribute by row
 };
 
-template <class T, bool WRITE>
-static void launch_walk_t(int op, dim3 g, dim3 b, hipStream_t st, const WalkArgs& wa, const Src<T>& src,
+template <class T, bool N, bool WRITE>
+static void launch_walk_t(int op, dim3 g, dim3 b, size_t lds, hipStream_t st, const WalkArgs& wa, const Src<T, N>& src,
                           const uint32_t* seg_b, const uint32_t* seg_e, UnitDesc* ud, const uint32_t* wlen,
-                          const uint32_t* wrow, const WRec<T>* tile, uint32_t* cnt, const uint32_t* off, MRec* mrec,
+                          const uint32_t* wrow, const WRec<T, N>* tile, uint32_t* cnt, const uint32_t* off, MRec* mrec,
                           uint64_t* emask, WalkStats* wst, uint32_t* carry_q0, uint32_t* carry_n) {
 #define SG_WALK_T(OPV)                                                                                          \
-  hipLaunchKernelGGL((k_walk_t<T, OPV, WRITE>), g, b, 0, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, \
+  hipLaunchKernelGGL((k_walk_t<T, N, OPV, WRITE>), g, b, lds, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, \
                      mrec, emask, wst, ud, carry_q0, carry_n)
   switch (op) {
     case 2: SG_WALK_T(2); break;
@@ -1038,8 +1137,10 @@ static void launch_walk_t(int op, dim3 g, dim3 b, hipStream_t st, const WalkArgs
   HIPCHK(hipGetLastError());
 }
 
-template <class T>
-static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& plan) {
+// One push through the closed-form pipeline with walker records of format N (narrow / wide).  Returns false
+// (having changed no state) when narrow records cannot represent the push (time span beyond 2^31 ms).
+template <class T, bool N>
+static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan plan) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
   const int* sa = d.shape_args;
@@ -1155,11 +1256,12 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
   memset(&cc, 0, sizeof(cc));
   for (int c = 0; c < d.n_cols; ++c) { cc.col[c] = cs.col[c]; cc.nul[c] = cs.nul[c]; }
 
-  typedef WRec<T> R;
-  Src<T> src;
+  typedef WRec<T, N> R;
+  Src<T, N> src;
   src.srec = nullptr;
   src.pk.v = v;
   const uint32_t K = d.partitioned ? kb : 1;
+  uint32_t* pk_flags = nullptr;
   uint32_t* seg_b = nullptr;
   uint32_t* seg_e = nullptr;
   if (d.partitioned) {
@@ -1170,13 +1272,23 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
     R* prec = (R*)h->ws.get("prec", sizeof(R) * nt, st);
     uint32_t* pkeys = (uint32_t*)h->ws.get("pkeys", sizeof(uint32_t) * nt, st);
     KeyOf kf{bv.key, cs.key, (uint32_t)nc};
-    hipLaunchKernelGGL((k_pack<T>), dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32)), dim3(256), 0,
-                       st, src.pk, kf, nt, prec, pkeys);
+    pk_flags = (uint32_t*)h->ws.get("pack_flags", sizeof(uint32_t), st);
+    HIPCHK(hipMemsetAsync(pk_flags, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL((k_pack<T, N>), dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32)), dim3(256), 0,
+                       st, src.pk, kf, nt, prec, pkeys, pk_flags);
     HIPCHK(hipGetLastError());
     size_t tb = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
-    void* tmp = h->ws.get("sort_tmp", tb, st);
-    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
+    if constexpr (sizeof(R) == 16) {   // one onesweep instantiation for every 16-byte record format
+      Blob16* pb = (Blob16*)prec;
+      Blob16* sbb = (Blob16*)srec;
+      HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, pkeys, skeys, pb, sbb, (size_t)nt, 0, end_bit, st));
+      void* tmp = h->ws.get("sort_tmp", tb, st);
+      HIPCHK(rocprim::radix_sort_pairs(tmp, tb, pkeys, skeys, pb, sbb, (size_t)nt, 0, end_bit, st));
+    } else {
+      HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
+      void* tmp = h->ws.get("sort_tmp", tb, st);
+      HIPCHK(rocprim::radix_sort_pairs(tmp, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
+    }
     src.srec = srec;
     seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
     seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
@@ -1194,7 +1306,12 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
   wa.nt = nt;
   wa.within = d.within;
   wa.K = K;
-  wa.C = (uint32_t)pick_chunks(K, nt, PendBytes<T, true>::lds);   // sized for the record walk's ring
+  wa.lp.pay = plan.pcol >= 0 ? 1 : 0;
+  wa.lp.row = plan.e1_row ? 1 : 0;
+  wa.pay_in_rec = (R::has_pay && plan.pcol >= 0) ? 1 : 0;
+  const size_t lds_count = (size_t)STACK_CAP * WALK_BLOCK * PendBytes<T>::lds(false, wa.lp);
+  const size_t lds_write = (size_t)STACK_CAP * WALK_BLOCK * PendBytes<T>::lds(true, wa.lp);
+  wa.C = (uint32_t)pick_chunks(K, nt, PendBytes<T>::lds(true, wa.lp));   // sized for the record walk's ring
   wa.R = (uint32_t)((nt + wa.C - 1) / wa.C);
   const uint64_t units = (uint64_t)K * wa.C;
   if (units >= (1ull << 32)) throw SgError(SG_EINVAL, "too many (key, chunk) units");
@@ -1240,16 +1357,29 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
     wlen = (uint32_t*)h->ws.get("wlen", sizeof(uint32_t) * (nw + 1), st);
     wrow = (uint32_t*)h->ws.get("wrow", sizeof(uint32_t) * (nw + 1), st);
     HIPCHK(hipMemsetAsync(wlen, 0, sizeof(uint32_t) * (nw + 1), st));
-    hipLaunchKernelGGL((k_units<T>), dim3((unsigned)(nw * 64 + 255) / 256), dim3(256), 0, st, wa, src, seg_b, seg_e,
+    hipLaunchKernelGGL((k_units<T, N>), dim3((unsigned)(nw * 64 + 255) / 256), dim3(256), 0, st, wa, src, seg_b, seg_e,
                        ud, wlen, wst);
     HIPCHK(hipGetLastError());
     size_t tb = 0;
     HIPCHK(rocprim::exclusive_scan(nullptr, tb, wlen, wrow, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
     void* tmp = h->ws.get("wscan_tmp", tb, st);
     HIPCHK(rocprim::exclusive_scan(tmp, tb, wlen, wrow, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
-    uint32_t rows_total = 0;
+    uint32_t rows_total = 0, pkf = 0;
     HIPCHK(hipMemcpyAsync(&rows_total, wrow + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (pkf & PK_TS_RANGE) return false;   // the push spans more than 2^31 ms: wide records
+    if (pkf & PK_PAY_RANGE) {
+      // a payload value wider than 32 bits: gather e1's attributes by row instead
+      for (int s = 0; s < d.n_select; ++s)
+        if (plan.pp.kind[s] == 0) { plan.pp.kind[s] = 3; plan.e1_row = true; }
+      plan.pcol = -1;
+      wa.lp.pay = 0;
+      wa.lp.row = 1;
+      wa.pay_in_rec = 0;
+      v.pcol = nullptr;
+      src.pk.v.pcol = nullptr;
+    }
     tile = (R*)h->ws.get("tile", sizeof(R) * 64 * (size_t)std::max<uint32_t>(rows_total, 1), st);
     emask = (uint64_t*)h->ws.get("emask", sizeof(uint64_t) * std::max<uint32_t>(rows_total, 1), st);
     const uint32_t nq = rows_total / TROWS;
@@ -1257,14 +1387,14 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
       uint32_t* rmap = (uint32_t*)h->ws.get("rowmap", sizeof(uint32_t) * nq, st);
       hipLaunchKernelGGL(k_rowmap, dim3((nw + 255) / 256), dim3(256), 0, st, wlen, wrow, nw, rmap);
       HIPCHK(hipGetLastError());
-      hipLaunchKernelGGL((k_transpose<T>), dim3(std::min<uint32_t>(nq, 256 * 32)), dim3(256), 0, st, src.srec, ud, wrow,
+      hipLaunchKernelGGL((k_transpose<T, N>), dim3(std::min<uint32_t>(nq, 256 * 32)), dim3(256), 0, st, src.srec, ud, wrow,
                          rmap, nq, tile);
       HIPCHK(hipGetLastError());
     }
-    launch_walk_t<T, false>(op, wgrd, wblk, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, (MRec*)nullptr,
+    launch_walk_t<T, N, false>(op, wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, (MRec*)nullptr,
                             emask, wst, carry_q0, carry_n);
   } else {
-    hipLaunchKernelGGL((k_walk<T, false, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
+    hipLaunchKernelGGL((k_walk<T, N, false, false>), wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, cnt, off,
                        (MRec*)nullptr, emap, wst, (char*)nullptr, carry_q0, carry_n);
     HIPCHK(hipGetLastError());
   }
@@ -1286,9 +1416,9 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
   if (hs.n_ovf) {
     // units whose pending list outgrew the LDS ring: redo them with unbounded HBM lists
     wa.big_cap = (std::max<uint32_t>(hs.ovf_need, 1) + 1) & ~1u;
-    big = (char*)h->ws.get("big_lists", (size_t)hs.n_ovf * wa.big_cap * PendBytes<T, true>::hbm, st);
+    big = (char*)h->ws.get("big_lists", (size_t)hs.n_ovf * wa.big_cap * PendBytes<T>::hbm, st);
     h->mark(6);
-    hipLaunchKernelGGL((k_walk<T, false, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
+    hipLaunchKernelGGL((k_walk<T, N, false, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
                        (MRec*)nullptr, emap, wst, big, carry_q0, carry_n);
     HIPCHK(hipGetLastError());
     scan_counts();
@@ -1310,20 +1440,20 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
     MRec* mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
     if (d.partitioned) {
-      launch_walk_t<T, true>(op, wgrd, wblk, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, mrec, emask, wst,
+      launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, mrec, emask, wst,
                              carry_q0, carry_n);
     } else {
-      hipLaunchKernelGGL((k_walk<T, true, false>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec, emap,
+      hipLaunchKernelGGL((k_walk<T, N, true, false>), wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec, emap,
                          wst, (char*)nullptr, carry_q0, carry_n);
       HIPCHK(hipGetLastError());
     }
     if (hs.n_ovf) {
-      hipLaunchKernelGGL((k_walk<T, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec,
+      hipLaunchKernelGGL((k_walk<T, N, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec,
                          emap, wst, big, carry_q0, carry_n);
       HIPCHK(hipGetLastError());
     }
     if (total) {
-      hipLaunchKernelGGL((k_project<T>), dim3((unsigned)std::min<int64_t>(((int64_t)total + 255) / 256, 256 * 16)),
+      hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)),
                          dim3(256), (size_t)256 * wa.stride, st, wa, v, pp, bv.cols, cc, mrec, off, (int64_t)total, out);
       HIPCHK(hipGetLastError());
     }
@@ -1355,7 +1485,7 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
     cb.flags = nx.flags;
     for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
     if (ncar)
-      hipLaunchKernelGGL((k_carry_copy<T>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n,
+      hipLaunchKernelGGL((k_carry_copy<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n,
                          coff, d.n_cols, widths, bv.cols, cc, cb);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
@@ -1366,6 +1496,7 @@ static void run_every_next(SgHandle* h, const BatchView& bv, int64_t n, const Pu
   h->last_events = n;
   h->last_matches = total;
   h->last_spilled = hs.n_ovf;
+  return true;
 }
 
 // Projection plan: which select columns are the compared value and which are gathered by row at emission.
@@ -1386,8 +1517,13 @@ static PushPlan make_plan(SgHandle* h, const BatchView& bv) {
     pp.type[s] = d.sel_type[s];
     if (idx != 0 && idx != -1) pp.kind[s] = 2;
     else if (col == (pp.src[s] ? val_col_b : val_col_a)) pp.kind[s] = 1;
-    else if (pp.src[s] == 0 && !es->nul_seen[col] && (pl.pcol < 0 || pl.pcol == col)) { pp.kind[s] = 0; pl.pcol = col; }
-    else pp.kind[s] = 3;
+    else if (pp.src[s] == 0 && !es->nul_seen[col] && d.col_type[col] != SG_T_DOUBLE && (pl.pcol < 0 || pl.pcol == col)) {
+      pp.kind[s] = 0;
+      pl.pcol = col;
+    } else {
+      pp.kind[s] = 3;
+      if (pp.src[s] == 0) pl.e1_row = true;
+    }
   }
   return pl;
 }
@@ -1396,5 +1532,6 @@ template <class T>
 static void dispatch_np(SgHandle* h, const BatchView& bv, int64_t n) {
   if (!h->state) { h->state = new EveryNextState(); h->state_kind = 1; }
   PushPlan pl = make_plan(h, bv);   // (needs the state: null history)
-  run_every_next<T>(h, bv, n, pl);
+  // narrow walker records whenever the push fits them (partitioned queries); wide otherwise
+  if (!h->desc.partitioned || !run_every_next<T, true>(h, bv, n, pl)) run_every_next<T, false>(h, bv, n, pl);
 }

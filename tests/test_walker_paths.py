@@ -205,3 +205,19 @@ def test_multi_push_nulls_appear_later():
     parts = split(b, [25_000])
     parts[0].nulls = [None] * len(parts[0].nulls)
     check(app, parts)
+
+
+def test_wide_payload_values():
+    """e1.id values beyond 32 bits: the narrow records cannot carry them, e1 attributes are gathered by row."""
+    app = q_part("price > e1.price")
+    b = make_batch(app, 60_000, seed=11, keys=100, rate=20,
+                   values={"price": lambda r, n: r.random(n) * 40, "id": lambda r, n: (1 << 40) + np.arange(n) * 7})
+    check(app, [b])
+
+
+def test_wide_payload_in_later_push():
+    app = q_part("price > e1.price")
+    b = make_batch(app, 60_000, seed=12, keys=100, rate=20,
+                   values={"price": lambda r, n: r.random(n) * 40,
+                           "id": lambda r, n: np.where(np.arange(n) < 30_000, np.arange(n), (1 << 35) + np.arange(n))})
+    check(app, split(b, [30_000]))
