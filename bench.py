@@ -55,10 +55,16 @@ def make_handle(cfg):
     return N.Handle(N.build_desc(nfa), device=torch.cuda.current_device(), options=opts), nfa
 
 
+def _oracle_paths():
+    for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
 def cpu_baseline(cfg, n_sample, keys, rate):
-    """Oracle (C++ restatement of the reference state processors), 1 thread, first n_sample rows."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    """Oracle (C++ restatement of the reference state processors), 1 thread, first n_sample rows: the
+    reference's synchronous single-thread InputHandler.send path."""
+    _oracle_paths()
     from oracle import OracleEngine
     from parity_util import run_engine, synth_batch
     b = synth_batch(cfg, 0, n_sample, keys=keys, rate=rate)
@@ -66,6 +72,59 @@ def cpu_baseline(cfg, n_sample, keys, rate):
     out = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
     dt = time.perf_counter() - t0
     return n_sample / dt, len(out), dt
+
+
+_MC = {}
+
+
+def _mc_worker(w):
+    from oracle import OracleEngine
+    from parity_util import run_engine
+    b = _MC["shards"][w]
+    t0 = time.perf_counter()
+    out = run_engine(OracleEngine, synth.QUERIES[_MC["cfg"]], [b])
+    return time.perf_counter() - t0, len(out)
+
+
+def cpu_baseline_multicore(cfg, n_sample, keys, rate, workers):
+    """The same oracle on all host cores the box grants this job: rows sharded by partition key across
+    worker processes (keys never interact), each shard keeping its global event indices."""
+    import multiprocessing as mp
+    _oracle_paths()
+    from parity_util import synth_batch
+    from siddhi_amd.runtime import Batch
+    b = synth_batch(cfg, 0, n_sample, keys=keys, rate=rate)
+    shards = []
+    for w in range(workers):
+        ix = np.nonzero((b.key % workers) == w)[0]
+        shards.append(Batch(len(ix), 0, b.ts[ix], b.stream[ix], b.key[ix], [c[ix] for c in b.cols],
+                            [None] * len(b.cols), index=ix.astype(np.uint64)))
+    _MC["shards"], _MC["cfg"] = shards, cfg
+    ctx = mp.get_context("fork")
+    with ctx.Pool(workers) as pool:
+        t0 = time.perf_counter()
+        res = pool.map(_mc_worker, range(workers))
+        dt = time.perf_counter() - t0
+    return n_sample / dt, sum(r[1] for r in res), dt
+
+
+def path_traffic(profile_json, n, cfg):
+    """HBM-side bytes of one push from the committed PMC summary (profiles/collect.sh + summarize.py):
+    every kernel of the path (torch's synthetic-data kernels excluded), per dispatch."""
+    try:
+        with open(profile_json) as f:
+            prof = json.load(f)
+    except OSError:
+        return None, None
+    if prof.get("workload") != cfg or prof.get("events") != n:
+        return None, None
+    tot = 0.0
+    for k, d in prof["kernels"].items():
+        if k.startswith("torch::") or k.startswith("__amd_rocclr"):
+            continue
+        tot += d.get("read_bytes_per_dispatch", 0.0) * d.get("dispatches_per_push", 1)
+        tot += d.get("write_bytes_per_dispatch", 0.0) * d.get("dispatches_per_push", 1)
+    return tot, profile_json
 
 
 def main():
@@ -77,6 +136,9 @@ def main():
     ap.add_argument("--events", type=int, default=0, help="events per GPU per step (default: config size, max 1e8)")
     ap.add_argument("--cpu-sample", type=int, default=12_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=16, help="processes for the key-sharded CPU baseline")
+    ap.add_argument("--profile", default=os.path.join(ROOT, "profiles", "r01", "c2_profile.json"),
+                    help="committed PMC summary the roofline traffic is read from")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -152,13 +214,22 @@ def main():
             "pred_eval_pass": {"achieved": round(pred_gbs, 1), "frac": round(pred_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_event": 4.125},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()}}
+    traffic, tsrc = path_traffic(args.profile, n, cfg)
+    if traffic is not None:
+        roof["traffic"] = round(traffic / 1e9, 3)
+        roof["traffic_unit"] = "GB per push (L2-side EA requests incl. Infinity-Cache hits; %s)" % os.path.relpath(tsrc, ROOT)
     cpu = None
     if not args.no_cpu:
         try:
             r, nm, dt = cpu_baseline(cfg, args.cpu_sample, keys, rate)
             cpu = {"value": round(r, 1), "unit": "events/s", "cores": 1, "kind": "port",
                    "sample": f"first {args.cpu_sample} events of {cfg} ({keys} keys, {rate}/ms), oracle C++ "
-                             f"restatement single thread, {nm} matches, {dt:.1f}s"}
+                             f"restatement of the reference state processors, single thread, {nm} matches, {dt:.1f}s"}
+            wk = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+            if synth.CONFIGS[cfg][2] > 1 and wk > 1:
+                r2, nm2, dt2 = cpu_baseline_multicore(cfg, args.cpu_sample, keys, rate, wk)
+                cpu["multi_core"] = {"value": round(r2, 1), "cores": wk,
+                                     "sample": f"same rows key-sharded over {wk} processes, {nm2} matches, {dt2:.1f}s"}
         except Exception as e:  # report, never fake
             cpu = {"value": None, "unit": "events/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
     line = {

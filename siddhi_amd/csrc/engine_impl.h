@@ -538,7 +538,9 @@ __global__ void __launch_bounds__(256) k_project(WalkArgs a, Virt v, ProjPlan pp
                                                  int64_t total, char* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char stage[];   // 256 records, written out contiguously
   const int64_t per = (int64_t)blockDim.x;
-  const int64_t s0 = (int64_t)blockIdx.x * per;   // one match per thread: every gather in flight at once
+  // one match per thread (every gather in flight at once); each XCD takes a contiguous slot range so the
+  // trigger-ordered gathers of neighbouring slots share its L2 instead of being fetched by all eight
+  const int64_t s0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * per;
   const int64_t sl = s0 + threadIdx.x;
   if (sl < total) {
     const MRec mr = mrec[sl];
