@@ -152,10 +152,12 @@ def main():
     n = args.events or min(n_cfg, 100_000_000)
 
     # ---- synthetic rows of this rank's key shard, generated in HBM
+    # (each rank's keys are its own dense ids 0..K-1: the router re-densifies per rank, siddhi_amd/router.py)
     g = synth.generate_torch(cfg, rank * n, n, dev, keys=keys, rate=rate)
-    key = (g["key"] + rank * keys).to(torch.int32) if "key" in g else torch.zeros(n, dtype=torch.int32, device=dev)
-    sym = key
-    cols = [g["id"], sym, g["price"]]
+    key = g["key"].to(torch.int32) if "key" in g else torch.zeros(n, dtype=torch.int32, device=dev)
+    if cfg.startswith("C4"):
+        raise SystemExit("bench.py: C4 (absence, two streams) is covered by tests/, not benched")
+    cols = [g["id"], key, g["v"], g["w"]] if cfg.startswith("C3") else [g["id"], key, g["price"]]
     torch.cuda.synchronize()
 
     h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
@@ -163,7 +165,7 @@ def main():
     h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
     keep = []
     batch = N.make_batch(n, rank * n, g["ts"].data_ptr(), 0, key.data_ptr(), [c.data_ptr() for c in cols],
-                         [0, 0, 0], 1, keys * (rank + 1), keep)
+                         [0] * len(cols), 1, keys, keep)
 
     def step():
         h.reset()

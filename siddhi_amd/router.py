@@ -40,6 +40,45 @@ def shard_batch(batch, rank: int, world: int):
                       gidx)
 
 
+class RankShard:
+    """One rank's view of the key-sharded stream.  Its keys are re-densified to local ids 0..K_r-1 in
+    first-seen order (so a GPU sees a dense key space of its own size, not the node's), persistently across
+    pushes so carried per-key state keeps its id; `globalize` maps match keys back before `merge`."""
+
+    def __init__(self, rank: int, world: int):
+        self.rank, self.world = rank, world
+        self.g2l = np.full(0, -1, np.int32)
+        self.l2g = np.zeros(0, np.int32)
+
+    def shard(self, batch):
+        idx, mine = shard_batch(batch, self.rank, self.world)
+        k = mine.key
+        valid = k >= 0
+        if valid.any():
+            top = int(k[valid].max()) + 1
+            if top > len(self.g2l):
+                self.g2l = np.concatenate([self.g2l, np.full(top - len(self.g2l), -1, np.int32)])
+            uk, first = np.unique(k[valid], return_index=True)
+            new = uk[self.g2l[uk] < 0]
+            if len(new):
+                order = np.argsort(first[self.g2l[uk] < 0], kind="stable")   # first-seen order
+                new = new[order]
+                self.g2l[new] = np.arange(len(self.l2g), len(self.l2g) + len(new), dtype=np.int32)
+                self.l2g = np.concatenate([self.l2g, new.astype(np.int32)])
+        local = np.where(valid, self.g2l[np.maximum(k, 0)] if len(self.g2l) else -1, -1).astype(np.int32)
+        mine.key = local
+        return idx, mine
+
+    @property
+    def key_bound(self) -> int:
+        return len(self.l2g)
+
+    def globalize(self, out):
+        out.key = np.where(out.key >= 0, self.l2g[np.maximum(out.key, 0)] if len(self.l2g) else out.key,
+                           out.key).astype(out.key.dtype)
+        return out
+
+
 def merge(parts):
     """Merge per-rank Outputs (each already in delivery order) into the node's delivery order."""
     from .runtime import Outputs

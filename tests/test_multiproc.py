@@ -37,8 +37,10 @@ def _worker(rank, world, port, cfg, n, keys, rate, outdir):
     from siddhi_amd import router, synth
     b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
     b.key = dense_first_seen(b.key)
-    _, mine = router.shard_batch(b, rank, world)
-    out = run_engine(HostInterpEngine, synth.QUERIES[cfg], [mine])
+    rs = router.RankShard(rank, world)
+    _, mine = rs.shard(b)
+    assert mine.n == 0 or int(mine.key.max()) + 1 == rs.key_bound   # dense local ids
+    out = rs.globalize(run_engine(HostInterpEngine, synth.QUERIES[cfg], [mine]))
     parts = [None] * world
     dist.all_gather_object(parts, out)
     if rank == 0:
@@ -63,6 +65,26 @@ def test_two_rank_key_sharding_matches_single_process(tmp_path, cfg, n, keys, ra
     want = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
     assert len(want) > 0
     assert_same(merged, want)
+
+
+def test_rank_shard_local_ids_roundtrip():
+    """Local ids are dense per rank, stable across pushes, and map back to the global ids."""
+    from siddhi_amd import router
+    from siddhi_amd.runtime import Batch
+    rng = np.random.default_rng(0)
+    rs = router.RankShard(1, 4)
+    seen = {}
+    for push in range(3):
+        k = rng.integers(-1, 5000, 20_000).astype(np.int32)
+        b = Batch(len(k), push * len(k), np.arange(len(k), dtype=np.int64), np.zeros(len(k), np.int32), k,
+                  [k.copy()], [None])
+        idx, mine = rs.shard(b)
+        assert (mine.key[k[idx] < 0] == -1).all()
+        ok = k[idx] >= 0
+        for g, l in zip(k[idx][ok], mine.key[ok]):
+            assert seen.setdefault(int(g), int(l)) == int(l)
+        assert set(seen.values()) == set(range(rs.key_bound))
+        assert (rs.l2g[mine.key[ok]] == k[idx][ok]).all()
 
 
 def test_shards_are_disjoint_and_cover():
