@@ -148,7 +148,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     cfg = args.config
-    num, n_cfg, keys, rate = synth.CONFIGS[cfg]
+    num, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
     n = args.events or min(n_cfg, 100_000_000)
 
     # ---- synthetic rows of this rank's key shard, generated in HBM
@@ -180,12 +180,14 @@ def main():
     torch.cuda.synchronize()
     stage = np.zeros(5)
     matches = 0
+    spilled = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         t = h.timing()
         stage += [t.pred_ms, t.partition_ms, t.match_ms, t.output_ms, t.total_ms]
         matches = t.matches
+        spilled = t.spilled_units
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if ws > 1:
@@ -228,7 +230,7 @@ def main():
                    "sample": f"first {args.cpu_sample} events of {cfg} ({keys} keys, {rate}/ms), oracle C++ "
                              f"restatement of the reference state processors, single thread, {nm} matches, {dt:.1f}s"}
             wk = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-            if synth.CONFIGS[cfg][2] > 1 and wk > 1:
+            if synth.CONFIGS[cfg[:2]][2] > 1 and wk > 1:
                 r2, nm2, dt2 = cpu_baseline_multicore(cfg, args.cpu_sample, keys, rate, wk)
                 cpu["multi_core"] = {"value": round(r2, 1), "cores": wk,
                                      "sample": f"same rows key-sharded over {wk} processes, {nm2} matches, {dt2:.1f}s"}
@@ -241,6 +243,7 @@ def main():
         "dtype": "f32", "data": "synthetic (SplitMix64 generator, SURVEY.md §8d), resident in HBM",
         "config": {"workload": f"{cfg}: " + synth.QUERIES[cfg], "events_per_gpu_per_step": n,
                    "keys_per_gpu": keys, "rate_events_per_ms": rate, "matches_per_gpu_per_step": int(matches),
+                   "spilled_units": int(spilled),
                    "parallelism": f"key-sharded x{ws} (no collective)"},
         "roofline": roof,
         "cpu_baseline": cpu,

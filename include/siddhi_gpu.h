@@ -131,7 +131,9 @@ typedef struct sg_options {
   int32_t list_cap;         /* general engine: capacity of each pending / newAndEvery list */
   int32_t force_general;    /* 1: ignore closed-form shapes (parity testing of the general kernel) */
   int32_t no_carry;         /* 1: pushes are independent streams (no state carried between them) */
-  int32_t reserved[6];
+  int32_t ring_cap;         /* closed form: LDS pending-list ring per walker lane (power of two 2..256;
+                               0 = chosen per push from the rows per `within` window) */
+  int32_t reserved[5];
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)

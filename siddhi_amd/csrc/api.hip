@@ -71,6 +71,8 @@ int sg_open(int hip_device, const sg_nfa_desc* nfa, const sg_options* opt, sg_ha
     if (h.opt.pool_events <= 0) h.opt.pool_events = 256;
     if (h.opt.pool_chain <= 0) h.opt.pool_chain = 256;
     if (h.opt.list_cap <= 0) h.opt.list_cap = 256;
+    if (h.opt.ring_cap < 0 || h.opt.ring_cap == 1 || h.opt.ring_cap > 256 || (h.opt.ring_cap & (h.opt.ring_cap - 1)))
+      throw SgError(SG_EINVAL, "ring_cap must be 0 or a power of two in [2, 256]");
     HIPCHK(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
     h.own_stream = true;
     for (auto& e : h.ev) HIPCHK(hipEventCreate(&e));

@@ -59,7 +59,7 @@
 
 static const uint32_t F_CAND = 1, F_CONS = 2;
 static const int WALK_BLOCK = 256;
-static const int STACK_CAP = 16;   // LDS pending-list ring entries per lane (power of two)
+static const int STACK_CAP = 16;   // default LDS pending-list ring entries per lane (runtime: 16/32/64)
 static const int PF = 8;           // rows prefetched per lane per step
 
 // ---------------------------------------------------------------------------------------------
@@ -333,7 +333,7 @@ __global__ void __launch_bounds__(256) k_pack(PackFn<T, N> pk, KeyOf kf, int64_t
   const int64_t t0 = N ? v_ts(pk.v, 0) : 0;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nt; r += stride) {
     rec[r] = pk((uint32_t)r);
-    keys[r] = kf((uint32_t)r);
+    if (keys) keys[r] = kf((uint32_t)r);
     if (N) {
       const int64_t d = v_ts(pk.v, (uint32_t)r) - t0;
       if (d != (int64_t)(int32_t)d) bad |= PK_TS_RANGE;
@@ -392,9 +392,10 @@ struct WalkStats {
   uint32_t pad;
 };
 
-struct LdsPlan {   // per-push layout of the record walk's LDS planes (count walk: value + time only)
+struct LdsPlan {   // per-push layout of the walkers' LDS rings (count walk: value + time only)
   int32_t pay;     // 1: narrow payload plane
   int32_t row;     // 1: e1 row plane
+  int32_t cap;     // ring entries per lane (power of two; deeper for long `within` windows)
 };
 
 struct WalkArgs {
@@ -440,7 +441,7 @@ template <> __device__ __forceinline__ int64_t val_bits<int32_t>(int32_t v) { re
 template <> __device__ __forceinline__ int64_t val_bits<int64_t>(int64_t v) { return v; }
 
 // Pending list: value + timestamp per partial, plus (record walk only) e1's payload attribute and e1's row
-// when a select gathers other e1 attributes.  LDS: ring of STACK_CAP entries per lane, SoA planes,
+// when a select gathers other e1 attributes.  LDS: ring of `cap` (power of two) entries per lane, SoA planes,
 // lane-strided (conflict-free); timestamps relative to the unit's first replayed row; payload narrowed to
 // 32 bits (a LONG that does not fit sends the unit to the HBM path).  The count walk keeps 8 B per entry, so
 // it runs at twice the residency of the record walk.  HBM (BIG): one unbounded list per overflowed unit,
@@ -455,7 +456,8 @@ struct PendList {
   int64_t* pay64;             // HBM payload
   int32_t pzero;              // narrow payload is zero-extended (FLOAT bits) rather than sign-extended
   int64_t base;
-  __device__ __forceinline__ uint32_t ix(uint32_t s) const { return BIG ? s : (s & (STACK_CAP - 1)) * WALK_BLOCK; }
+  uint32_t cmask;             // LDS ring: capacity - 1
+  __device__ __forceinline__ uint32_t ix(uint32_t s) const { return BIG ? s : (s & cmask) * WALK_BLOCK; }
   __device__ __forceinline__ T gv(uint32_t s) const { return val[ix(s)]; }
   __device__ __forceinline__ int64_t gts(uint32_t s) const { return BIG ? ts[ix(s)] : base + (int64_t)dts[ix(s)]; }
   __device__ __forceinline__ uint32_t grow(uint32_t s) const { return row ? row[ix(s)] : 0u; }
@@ -478,10 +480,11 @@ struct PendBytes {   // bytes per entry
   static int lds(bool write, const LdsPlan& lp) { return (int)sizeof(T) + 4 + (write ? 4 * (lp.pay + lp.row) : 0); }
   static constexpr int hbm = sizeof(T) + 20;   // val, ts, row, payload
 };
-// LDS planes of one block: [val][dts][pay32?][row?], each STACK_CAP * WALK_BLOCK entries
+// LDS planes of one block: [val][dts][pay32?][row?], each cap * WALK_BLOCK entries
 template <class T, bool BIG>
 __device__ __forceinline__ void lds_planes(PendList<T, BIG>& L, char* lds, bool write, const LdsPlan& lp) {
-  const size_t E = (size_t)STACK_CAP * WALK_BLOCK;
+  const size_t E = (size_t)(lp.cap) * WALK_BLOCK;
+  L.cmask = (uint32_t)lp.cap - 1;
   char* p = lds;
   L.val = (T*)p + threadIdx.x; p += E * sizeof(T);
   L.dts = (int32_t*)p + threadIdx.x; p += E * 4;
@@ -696,7 +699,7 @@ struct Walker {
     const bool emitted = m && in_chunk && (r >= v.nc);
     if (!WRITE && emitted) cnt[r - v.nc] = m;
     if ((f & F_CAND) && live) {
-      if (!BIG && top - head == STACK_CAP) { overflow = true; return emitted; }
+      if (!BIG && top - head == L.cmask + 1) { overflow = true; return emitted; }
       int64_t pv = 0;
       if (WRITE && payload) {
         if (R::has_pay && a.pay_in_rec) pv = rc.p(v.pfloat);
@@ -1070,14 +1073,35 @@ struct EveryNextState {
   bool nul_seen[SG_MAX_COLS] = {};   // a column that ever had nulls is gathered by row, never carried
 };
 
-static int pick_chunks(uint32_t K, int64_t nt, int entry_bytes) {
-  // one round of resident walkers: LDS holds 160 KiB / (STACK_CAP * entry) lanes per CU, in whole blocks
-  int64_t blocks_per_cu = (160 * 1024) / ((int64_t)STACK_CAP * WALK_BLOCK * entry_bytes);
+// Time chunks per key.  More chunks = more resident walker lanes, but every unit also replays the `within`
+// window before its chunk: keep units at >= 2 windows of rows (estimated from the batch's time span) and at
+// most one round of resident lanes (LDS holds 160 KiB / (STACK_CAP * entry) lanes per CU).
+static int64_t window_rows(uint32_t K, int64_t nt, int64_t within, int64_t span_ms) {   // rows per key per window
+  int64_t per_key = std::max<int64_t>(1, nt / std::max<uint32_t>(K, 1));
+  return span_ms > 0 ? (int64_t)((double)per_key * (double)within / (double)span_ms) : per_key;
+}
+static int pick_cap(int64_t win) {   // a monotone stack over w random rows holds ~ln(w) partials
+  return win < 300 ? 16 : (win < 5000 ? 32 : 64);
+}
+static constexpr int64_t WALK_LDS_MAX = 160 * 1024;   // gfx950 LDS per CU = per workgroup ceiling
+// Largest ring (power of two) whose write-walk planes fit one workgroup's LDS.
+static int clamp_cap(int cap, int entry_bytes_write) {
+  while (cap > 2 && (int64_t)cap * WALK_BLOCK * entry_bytes_write > WALK_LDS_MAX) cap >>= 1;
+  return cap;
+}
+// Chunks per key.  Each (key, chunk) unit replays the `within` window before its chunk, so chunks shorter
+// than ~2 windows waste walker steps -- unless even such chunks leave the chip short of one walker lane
+// per SIMD slot (few keys, long windows: the C1 shape), where parallelism beats replay cost.
+static int pick_chunks(uint32_t K, int64_t nt, int entry_bytes, int cap, int64_t win) {
+  int64_t blocks_per_cu = WALK_LDS_MAX / ((int64_t)cap * WALK_BLOCK * entry_bytes);
   int64_t target = std::max<int64_t>(blocks_per_cu, 1) * WALK_BLOCK * 256;
+  int64_t per_key = std::max<int64_t>(1, nt / std::max<uint32_t>(K, 1));
   int64_t C = std::max<int64_t>(1, target / K);
-  C = std::min<int64_t>(C, 64);
-  C = std::min<int64_t>(C, std::max<int64_t>(1, nt / 512));
-  return (int)std::max<int64_t>(C, 1);
+  const int64_t c_cheap = std::max<int64_t>(1, per_key / std::max<int64_t>(256, 2 * win));
+  const int64_t c_short = std::max<int64_t>(1, per_key / 256);
+  const bool starved = (int64_t)K * c_cheap < 64 * 256;
+  C = std::min<int64_t>(C, starved ? c_short : c_cheap);
+  return (int)std::min<int64_t>(C, 1 << 16);
 }
 
 // `col CMP const` on a 4-byte column?  (the predicate pass then streams it with 16-B loads)
@@ -1127,6 +1151,9 @@ static void launch_walk_t(int op, dim3 g, dim3 b, size_t lds, hipStream_t st, co
                           const uint32_t* wrow, const WRec<T, N>* tile, uint32_t* cnt, const uint32_t* off, MRec* mrec,
                           uint64_t* emask, WalkStats* wst, uint32_t* carry_q0, uint32_t* carry_n) {
 #define SG_WALK_T(OPV)                                                                                          \
+  if (lds > 65536)                                                                                              \
+    HIPCHK(hipFuncSetAttribute((const void*)k_walk_t<T, N, OPV, WRITE>,                                        \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                          \
   hipLaunchKernelGGL((k_walk_t<T, N, OPV, WRITE>), g, b, lds, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, \
                      mrec, emask, wst, ud, carry_q0, carry_n)
   switch (op) {
@@ -1264,20 +1291,22 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   src.pk.v = v;
   const uint32_t K = d.partitioned ? kb : 1;
   uint32_t* pk_flags = nullptr;
-  uint32_t* seg_b = nullptr;
+  uint32_t* seg_b = nullptr;   // (unpartitioned: one segment [0, nt))
   uint32_t* seg_e = nullptr;
+  pk_flags = (uint32_t*)h->ws.get("pack_flags", sizeof(uint32_t), st);
+  HIPCHK(hipMemsetAsync(pk_flags, 0, sizeof(uint32_t), st));
+  R* prec = (R*)h->ws.get("prec", sizeof(R) * nt, st);
+  seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
+  seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
+  const dim3 pgrd((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32));
   if (d.partitioned) {
     int end_bit = 1;
     while ((1ull << end_bit) <= (uint64_t)kb) ++end_bit;
     uint32_t* skeys = (uint32_t*)h->ws.get("skeys", sizeof(uint32_t) * nt, st);
     R* srec = (R*)h->ws.get("srec", sizeof(R) * nt, st);
-    R* prec = (R*)h->ws.get("prec", sizeof(R) * nt, st);
     uint32_t* pkeys = (uint32_t*)h->ws.get("pkeys", sizeof(uint32_t) * nt, st);
     KeyOf kf{bv.key, cs.key, (uint32_t)nc};
-    pk_flags = (uint32_t*)h->ws.get("pack_flags", sizeof(uint32_t), st);
-    HIPCHK(hipMemsetAsync(pk_flags, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL((k_pack<T, N>), dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32)), dim3(256), 0,
-                       st, src.pk, kf, nt, prec, pkeys, pk_flags);
+    hipLaunchKernelGGL((k_pack<T, N>), pgrd, dim3(256), 0, st, src.pk, kf, nt, prec, pkeys, pk_flags);
     HIPCHK(hipGetLastError());
     size_t tb = 0;
     if constexpr (sizeof(R) == 16) {   // one onesweep instantiation for every 16-byte record format
@@ -1292,13 +1321,20 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       HIPCHK(rocprim::radix_sort_pairs(tmp, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
     }
     src.srec = srec;
-    seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
-    seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
     HIPCHK(hipMemsetAsync(seg_b, 0, sizeof(uint32_t) * K, st));
     HIPCHK(hipMemsetAsync(seg_e, 0, sizeof(uint32_t) * K, st));
     hipLaunchKernelGGL(k_bounds, dim3((unsigned)std::min<int64_t>((nt + 1023) / 1024, 256 * 16)), dim3(256), 0, st, skeys,
                        nt, kb, seg_b, seg_e);
     HIPCHK(hipGetLastError());
+  } else {
+    // unpartitioned: one key whose rows are already in arrival order
+    KeyOf kf{nullptr, nullptr, 0};
+    hipLaunchKernelGGL((k_pack<T, N>), pgrd, dim3(256), 0, st, src.pk, kf, nt, prec, (uint32_t*)nullptr, pk_flags);
+    HIPCHK(hipGetLastError());
+    src.srec = prec;
+    const uint32_t seg[2] = {0u, (uint32_t)nt};
+    HIPCHK(hipMemcpyAsync(seg_b, &seg[0], sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(seg_e, &seg[1], sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
   h->mark(2);
 
@@ -1311,9 +1347,20 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   wa.lp.pay = plan.pcol >= 0 ? 1 : 0;
   wa.lp.row = plan.e1_row ? 1 : 0;
   wa.pay_in_rec = (R::has_pay && plan.pcol >= 0) ? 1 : 0;
-  const size_t lds_count = (size_t)STACK_CAP * WALK_BLOCK * PendBytes<T>::lds(false, wa.lp);
-  const size_t lds_write = (size_t)STACK_CAP * WALK_BLOCK * PendBytes<T>::lds(true, wa.lp);
-  wa.C = (uint32_t)pick_chunks(K, nt, PendBytes<T>::lds(true, wa.lp));   // sized for the record walk's ring
+  // (ring capacity and chunking from the batch's time span: rows per key per `within` window)
+  int64_t span_ms = 0;
+  {
+    int64_t tfl[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    span_ms = tfl[1] - tfl[0];
+  }
+  const int64_t win = window_rows(K, nt, d.within, span_ms);
+  wa.lp.cap = clamp_cap(h->opt.ring_cap > 0 ? h->opt.ring_cap : pick_cap(win), PendBytes<T>::lds(true, wa.lp));
+  const size_t lds_count = (size_t)wa.lp.cap * WALK_BLOCK * PendBytes<T>::lds(false, wa.lp);
+  const size_t lds_write = (size_t)wa.lp.cap * WALK_BLOCK * PendBytes<T>::lds(true, wa.lp);
+  wa.C = (uint32_t)pick_chunks(K, nt, PendBytes<T>::lds(true, wa.lp), wa.lp.cap, win);   // record walk's ring
   wa.R = (uint32_t)((nt + wa.C - 1) / wa.C);
   const uint64_t units = (uint64_t)K * wa.C;
   if (units >= (1ull << 32)) throw SgError(SG_EINVAL, "too many (key, chunk) units");
@@ -1354,7 +1401,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   uint32_t* wrow = nullptr;
   R* tile = nullptr;
   uint64_t* emask = nullptr;
-  if (d.partitioned) {
+  {
     // lane-interleaved tiles: unit ranges -> per-wave rows -> LDS transpose of the sorted records
     wlen = (uint32_t*)h->ws.get("wlen", sizeof(uint32_t) * (nw + 1), st);
     wrow = (uint32_t*)h->ws.get("wrow", sizeof(uint32_t) * (nw + 1), st);
@@ -1395,10 +1442,6 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     }
     launch_walk_t<T, N, false>(op, wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, (MRec*)nullptr,
                             emask, wst, carry_q0, carry_n);
-  } else {
-    hipLaunchKernelGGL((k_walk<T, N, false, false>), wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, cnt, off,
-                       (MRec*)nullptr, emap, wst, (char*)nullptr, carry_q0, carry_n);
-    HIPCHK(hipGetLastError());
   }
   auto scan_counts = [&]() {
     size_t tb = 0;
@@ -1441,14 +1484,8 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     wa.out_base = h->out.n;
     MRec* mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
-    if (d.partitioned) {
-      launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, mrec, emask, wst,
-                             carry_q0, carry_n);
-    } else {
-      hipLaunchKernelGGL((k_walk<T, N, true, false>), wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec, emap,
-                         wst, (char*)nullptr, carry_q0, carry_n);
-      HIPCHK(hipGetLastError());
-    }
+    launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, mrec,
+                              emask, wst, carry_q0, carry_n);
     if (hs.n_ovf) {
       hipLaunchKernelGGL((k_walk<T, N, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec,
                          emap, wst, big, carry_q0, carry_n);
@@ -1535,5 +1572,5 @@ static void dispatch_np(SgHandle* h, const BatchView& bv, int64_t n) {
   if (!h->state) { h->state = new EveryNextState(); h->state_kind = 1; }
   PushPlan pl = make_plan(h, bv);   // (needs the state: null history)
   // narrow walker records whenever the push fits them (partitioned queries); wide otherwise
-  if (!h->desc.partitioned || !run_every_next<T, true>(h, bv, n, pl)) run_every_next<T, false>(h, bv, n, pl);
+  if (!run_every_next<T, true>(h, bv, n, pl)) run_every_next<T, false>(h, bv, n, pl);
 }

@@ -72,10 +72,11 @@ def split(b, cuts):
 class _Spy:
     """GpuEngine wrapper recording how many units spilled to HBM lists per push."""
     spilled = []
+    ring_cap = 0
 
     def __init__(self, ctx):
         from siddhi_amd._native import GpuEngine
-        self.e = GpuEngine(ctx)
+        self.e = GpuEngine(ctx, ring_cap=_Spy.ring_cap)
 
     def push(self, b):
         self.e.push(b)
@@ -88,10 +89,11 @@ class _Spy:
         self.e.close()
 
 
-def check(app, batches, min_matches=1, expect_spill=None):
+def check(app, batches, min_matches=1, expect_spill=None, ring_cap=0):
     assert shape_of(app) == L.SHAPE_EVERY_NEXT_CMP, "case must exercise the closed-form walker"
     want = run_engine(OracleEngine, app, batches)
     _Spy.spilled = []
+    _Spy.ring_cap = ring_cap
     got = run_engine(_Spy, app, batches)
     assert len(want) >= min_matches
     assert_same(got, want)
@@ -143,7 +145,7 @@ def test_stack_overflow_unpartitioned():
     falling = lambda r, n: np.where(np.arange(n) % 200 < 150, 40.0 - (np.arange(n) % 200) * 0.1, r.random(n) * 40)
     app = q_flat("price > e1.price")
     b = make_batch(app, n, seed=3, rate=50, values={"price": falling})
-    check(app, [b], expect_spill=True)
+    check(app, [b], expect_spill=True, ring_cap=16)
 
 
 def test_stack_overflow_partitioned():
@@ -152,7 +154,7 @@ def test_stack_overflow_partitioned():
                                     r.random(n) * 40)
     app = q_part("price > e1.price")
     b = make_batch(app, n, seed=4, keys=3, rate=40, values={"price": falling})
-    check(app, [b], expect_spill=True)
+    check(app, [b], expect_spill=True, ring_cap=16)
 
 
 def test_list_mode_local_filter():
@@ -205,6 +207,13 @@ def test_multi_push_nulls_appear_later():
     parts = split(b, [25_000])
     parts[0].nulls = [None] * len(parts[0].nulls)
     check(app, parts)
+
+
+@pytest.mark.parametrize("cap", [2, 4, 64])
+def test_ring_capacity_does_not_change_results(cap):
+    app = q_part("price > e1.price")
+    b = make_batch(app, 40_000, seed=13, keys=50, rate=20, values=PRICE_TIES)
+    check(app, [b], ring_cap=cap, expect_spill=True if cap == 2 else None)
 
 
 def test_wide_payload_values():
