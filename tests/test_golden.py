@@ -1,0 +1,53 @@
+"""Committed golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py): fixed synthetic
+inputs for every benchmark config with the oracle's frozen ordered match output.
+
+CPU: the generator still produces the fixture inputs, and the oracle still produces the frozen outputs.
+GPU: the HIP engine reproduces the frozen outputs bit for bit on both kernels (closed-form walker where
+the shape allows it, and the general per-key machine)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+import make_golden as G                     # noqa: E402
+from parity_util import assert_same, run_engine   # noqa: E402
+
+NAMES = sorted(G.CASES)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fixture_inputs_match_generator(name):
+    q, b, _ = G.load(name)
+    cfg, n, keys, rate = G.CASES[name]
+    g = G.golden_batch(cfg, n, keys, rate)
+    assert np.array_equal(b.ts, g.ts) and np.array_equal(b.key, g.key) and np.array_equal(b.stream, g.stream)
+    for x, y in zip(b.cols, g.cols):
+        assert x.dtype == y.dtype and np.array_equal(x.view(np.uint8), y.view(np.uint8))
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_reproduces_golden(name):
+    from oracle import OracleEngine
+    q, b, want = G.load(name)
+    assert_same(run_engine(OracleEngine, q, [b]), want)
+    if name != "c3":               # literal C3 emits nothing in the reference
+        assert len(want) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_reproduces_golden(name):
+    from siddhi_amd._native import GpuEngine
+    q, b, want = G.load(name)
+    assert_same(run_engine(GpuEngine, q, [b]), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_general_kernel_reproduces_golden(name):
+    from siddhi_amd._native import GpuEngine
+    q, b, want = G.load(name)
+    pool = 16384 if name == "c4" else 0     # C4: thousands of live partials on one key
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, pool=pool), q, [b]), want)
