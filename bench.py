@@ -134,7 +134,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--events", type=int, default=0, help="events per GPU per step (default: config size, max 1e8)")
-    ap.add_argument("--cpu-sample", type=int, default=12_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="events for the CPU baseline (default: 12M; C4 60k -- the oracle walks ~5k partials per event)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16, help="processes for the key-sharded CPU baseline")
     ap.add_argument("--profile", default=os.path.join(ROOT, "profiles", "r01", "c2_profile.json"),
@@ -148,6 +149,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     cfg = args.config
+    if not args.cpu_sample:
+        args.cpu_sample = 60_000 if cfg.startswith("C4") else 12_000_000
     num, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
     n = args.events or min(n_cfg, 100_000_000)
 
@@ -155,9 +158,12 @@ def main():
     # (each rank's keys are its own dense ids 0..K-1: the router re-densifies per rank, siddhi_amd/router.py)
     g = synth.generate_torch(cfg, rank * n, n, dev, keys=keys, rate=rate)
     key = g["key"].to(torch.int32) if "key" in g else torch.zeros(n, dtype=torch.int32, device=dev)
-    if cfg.startswith("C4"):
-        raise SystemExit("bench.py: C4 (absence, two streams) is covered by tests/, not benched")
-    cols = [g["id"], key, g["v"], g["w"]] if cfg.startswith("C3") else [g["id"], key, g["price"]]
+    if cfg.startswith("C4"):     # S(id, seq) rows only (the Tick stream's column is never read)
+        cols = [g["id"], g["seq"], torch.zeros(n, dtype=torch.int32, device=dev)]
+    elif cfg.startswith("C3"):
+        cols = [g["id"], key, g["v"], g["w"]]
+    else:
+        cols = [g["id"], key, g["price"]]
     torch.cuda.synchronize()
 
     h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
@@ -203,21 +209,25 @@ def main():
     value = ws * n * args.steps / elapsed
 
     # algorithmic bytes: predicate pass 4.125 B/event (price read + condition bit);
-    # whole path 16.125 B/event (ts 8 + key 4 + price 4 + bit) + 36 B/match
+    # whole path 16.125 B/event (ts 8 + key 4 + price 4 + bit) + 36 B/match (C1: no key, 12.125);
+    # C4 (no local predicate): ts 8 + id 8 B/event + 28 B/emission
     pred_bytes = 4.125 * n
-    path_bytes = 16.125 * n + 36.0 * matches
+    per_ev, per_m = {"C1": (12.125, 36.0), "C4": (16.0, 28.0)}.get(cfg[:2], (16.125, 36.0))
+    path_bytes = per_ev * n + per_m * matches
     stages = {"pred_eval_ms": stage[0], "key_partition_ms": stage[1], "walk_count_scan_ms": stage[2],
               "walk_write_ms": stage[3], "kernels_total_ms": stage[4]}
     names = ["pred_eval_ms", "key_partition_ms", "walk_count_scan_ms", "walk_write_ms"]
     dom = names[int(np.argmax(stage[:4]))]
     path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9
-    pred_gbs = pred_bytes / (stage[0] * 1e-3) / 1e9
+    pred_gbs = pred_bytes / (stage[0] * 1e-3) / 1e9 if stage[0] > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(path_gbs / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": "whole NFA path (all kernels of one push; dominant stage: %s)" % dom,
             "pred_eval_pass": {"achieved": round(pred_gbs, 1), "frac": round(pred_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_event": 4.125},
             "stages_ms": {k: round(v, 4) for k, v in stages.items()}}
+    if cfg.startswith("C4"):
+        roof["pred_eval_pass"] = None   # no local predicate: the path starts at the role/value pass
     traffic, tsrc = path_traffic(args.profile, n, cfg)
     if traffic is not None:
         roof["traffic"] = round(traffic / 1e9, 3)
@@ -230,7 +240,8 @@ def main():
                    "sample": f"first {args.cpu_sample} events of {cfg} ({keys} keys, {rate}/ms), oracle C++ "
                              f"restatement of the reference state processors, single thread, {nm} matches, {dt:.1f}s"}
             wk = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-            if synth.CONFIGS[cfg[:2]][2] > 1 and wk > 1:
+            partitioned = cfg[:2] in ("C2", "C3", "C5")   # C1 / C4 are single runtimes
+            if partitioned and wk > 1:
                 r2, nm2, dt2 = cpu_baseline_multicore(cfg, args.cpu_sample, keys, rate, wk)
                 cpu["multi_core"] = {"value": round(r2, 1), "cores": wk,
                                      "sample": f"same rows key-sharded over {wk} processes, {nm2} matches, {dt2:.1f}s"}

@@ -1,0 +1,477 @@
+// absent.hip — MI355X closed form for  every A[l] -> not B[l' and B.x == A.x] for W   (@app:playback,
+// unpartitioned; SG_SHAPE_EVERY_ABSENT_EQ, config C4).
+//
+// Semantics, restated from AbsentStreamPreStateProcessor (C/query/input/stream/state/
+// AbsentStreamPreStateProcessor.java: addState :77-101 schedules ts_i + W, the timer pass :140-228 emits
+// every pending partial with S.ts + W <= T stamped S.ts = T, processAndReturn :230-244 drops a partial
+// whose `not` filter matched), AbsentStreamPostStateProcessor.process (:36-56) and Scheduler's FIFO
+// (C/util/Scheduler.java:74-86,179-214) driven by TimestampGeneratorImpl.setCurrentTimestamp
+// (C/util/timestamp/TimestampGeneratorImpl.java:106-125) before each row is dispatched:
+//   every A row i passing A's filter opens partial i with deadline d_i = ts_i + W; the partial is
+//   KILLED iff some later B row j passing B's local filter with x_j == x_i arrives with ts_j < d_i;
+//   otherwise it is EMITTED in the timer pass that runs just before the first row (any stream) with
+//   ts >= d_i, with output ts = d_i.  Every FIFO entry is "row ts + W" pushed in row order, so the
+//   FIFO stays sorted and the timer-pass epilogue never schedules; emissions are therefore ordered by
+//   deadline then arrival, i.e. by i, and the g-th emission of one timer pass is callback group g.
+//
+// Pipeline per sg_push (one HIP stream, inputs in HBM):
+//   1. k_abs_rows     per virtual row (carried partials first): candidate / killer roles (A and B local
+//                     predicates through the postfix VM), the compared value, a min/max of the values
+//                     and the timestamp-order check.
+//   2. sort           stable radix sort of the virtual rows by compared value (rocPRIM, only the bits
+//                     the value range needs): per value, its rows in arrival order.
+//   3. next killer    reverse min-scan over sorted positions -> the first killer after each position.
+//   4. k_abs_decide   per candidate: killed (first later killer of the same value is before d_i),
+//                     emitted (trigger = first row with ts >= d_i, binary search) or still pending.
+//   5. scan           emission and carry offsets in arrival order.
+//   6. k_abs_write    AoS match records (QuerySelector.processNoGroupBy projection of e1's attributes),
+//                     callback group = rank within the trigger's timer pass; carried partials saved.
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <string>
+
+#include "sg_device.h"
+#include "sg_engine.h"
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw SgError(SG_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+const uint32_t R_CAND = 1, R_KILL = 2, R_SORT = 4;   // role bits
+const uint32_t NONE = 0xffffffffu;
+
+// Pending partials carried into the next push (arrival order): deadline, compared value, projection.
+struct AbsCarry {
+  int64_t n = 0, cap = 0;
+  int64_t* dl = nullptr;       // deadline ts_i + W
+  int64_t* val = nullptr;      // compared value bits
+  uint8_t* vnul = nullptr;     // compared value is null (never killed)
+  int64_t* sel = nullptr;      // [cap][n_select] projected bits
+  uint32_t* snul = nullptr;    // projected null mask
+  void reserve(int64_t want, int nsel) {
+    if (want <= cap) return;
+    release();
+    cap = std::max<int64_t>(want + want / 4, 1024);
+    if (hipMalloc(&dl, cap * 8) != hipSuccess || hipMalloc(&val, cap * 8) != hipSuccess ||
+        hipMalloc(&vnul, cap) != hipSuccess || hipMalloc(&sel, cap * 8 * std::max(nsel, 1)) != hipSuccess ||
+        hipMalloc(&snul, cap * 4) != hipSuccess)
+      throw SgError(SG_EHIP, "hipMalloc failed for absence carry");
+  }
+  void release() {
+    for (void* p : {(void*)dl, (void*)val, (void*)vnul, (void*)sel, (void*)snul}) if (p) hipFree(p);
+    dl = val = sel = nullptr;
+    vnul = nullptr;
+    snul = nullptr;
+    cap = 0;
+  }
+};
+
+struct AbsState {
+  AbsCarry carry[2];
+  int cur = 0;
+  int64_t* dlast = nullptr;    // device: last timestamp seen (order check across pushes)
+  int64_t* dminmax = nullptr;  // device: [min, max] of compared values (as order-preserving u64)
+  uint32_t* dflag = nullptr;   // device: order error
+};
+
+struct AbsArgs {
+  int64_t n, nc, nt;
+  int64_t W;
+  int32_t s_a, s_b;
+  int32_t col_a, col_b, type;
+  int32_t prog_a_off, prog_a_len, prog_b_off, prog_b_len;
+  int32_t has_stream;
+  int32_t first_push;
+  int32_t keep_carry;          // 0 (no_carry): partials still pending at the end of the push are dropped
+};
+
+struct RowRd {
+  const SgCols* c;
+  const int32_t* ret_col;
+  int64_t row;
+  __device__ SgVal read(int, int, int slot, int type) { return sg_read_col(*c, ret_col[slot], type, row); }
+};
+
+__device__ __forceinline__ uint64_t ord64(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
+
+// 1. roles, compared values, value range, order check
+__global__ void __launch_bounds__(256) k_abs_rows(AbsArgs a, SgCols cols, const DevDesc* __restrict__ dd,
+                                                  const int64_t* __restrict__ ts, const int32_t* __restrict__ stream,
+                                                  const int64_t* __restrict__ c_val, const uint8_t* __restrict__ c_vnul,
+                                                  uint8_t* __restrict__ role, int64_t* __restrict__ vals,
+                                                  unsigned long long* __restrict__ minmax, const int64_t* __restrict__ dlast,
+                                                  uint32_t* __restrict__ oflag) {
+  uint64_t lo = ~0ull, hi = 0;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.nt; v += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t r = 0;
+    int64_t x = 0;
+    if (v < a.nc) {
+      r = R_CAND;
+      if (!c_vnul[v]) { r |= R_SORT; x = c_val[v]; }
+    } else {
+      const int64_t i = v - a.nc;
+      const int s = a.has_stream ? stream[i] : 0;
+      RowRd rd{&cols, dd->ret_col, i};
+      bool ca = s == a.s_a && sg_eval(dd->code + a.prog_a_off, a.prog_a_len, rd);
+      bool ki = s == a.s_b && sg_eval(dd->code + a.prog_b_off, a.prog_b_len, rd);
+      const int col = ca ? a.col_a : a.col_b;   // same column when A and B read one stream (checked on host)
+      if (ca || ki) {
+        SgVal sv = sg_read_col(cols, col, a.type, i);
+        if (!sv.null) { x = sv.i; r |= R_SORT; }
+        if (ca) r |= R_CAND;
+        if (ki && !sv.null) r |= R_KILL;   // `==` with a null operand is false
+      }
+      if ((i > 0 && ts[i - 1] > ts[i]) || (i == 0 && !a.first_push && ts[0] < *dlast)) atomicOr(oflag, 1u);
+    }
+    role[v] = (uint8_t)r;
+    vals[v] = x;
+    if (r & R_SORT) {
+      uint64_t o = ord64(x);
+      lo = o < lo ? o : lo;
+      hi = o > hi ? o : hi;
+    }
+  }
+  // wave-reduce, one atomic pair per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    uint64_t l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (lo != ~0ull) atomicMin(&minmax[0], (unsigned long long)lo);
+    if (hi != 0 || lo != ~0ull) atomicMax(&minmax[1], (unsigned long long)hi);
+  }
+}
+
+// sort keys: value - min (order preserving) for sorted rows, a sentinel above the range for the rest
+template <class K>
+__global__ void k_abs_keys(int64_t nt, const uint8_t* __restrict__ role, const int64_t* __restrict__ vals,
+                           uint64_t omin, K sentinel, K* __restrict__ keys, uint32_t* __restrict__ ids) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nt; v += (int64_t)gridDim.x * blockDim.x) {
+    keys[v] = (role[v] & R_SORT) ? (K)(ord64(vals[v]) - omin) : sentinel;
+    ids[v] = (uint32_t)v;
+  }
+}
+
+// 3. reversed killer positions (input of the min-scan): rk[nt-1-p] = p if sorted position p is a killer
+__global__ void k_abs_rkill(int64_t nt, const uint32_t* __restrict__ sid, const uint8_t* __restrict__ role,
+                            uint32_t* __restrict__ rk) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nt; p += (int64_t)gridDim.x * blockDim.x)
+    rk[nt - 1 - p] = (role[sid[p]] & R_KILL) ? (uint32_t)p : NONE;
+}
+
+__device__ __forceinline__ int64_t vts(const AbsArgs& a, const int64_t* ts, const int64_t* c_dl, uint32_t v) {
+  return v < a.nc ? c_dl[v] - a.W : ts[v - a.nc];
+}
+
+// 4a. kill: a candidate at sorted position p dies if the first killer after it has its value and arrives
+//     before its deadline
+template <class K>
+__global__ void k_abs_kill(AbsArgs a, const K* __restrict__ skeys, const uint32_t* __restrict__ sid,
+                           const uint8_t* __restrict__ role, const uint32_t* __restrict__ nks,
+                           const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
+                           uint8_t* __restrict__ dead) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nt; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = sid[p];
+    const uint8_t r = role[v];
+    if ((r & (R_CAND | R_SORT)) != (R_CAND | R_SORT)) continue;
+    const uint32_t q = (p + 1 < a.nt) ? nks[a.nt - 2 - p] : NONE;   // min killer position >= p + 1
+    if (q == NONE || skeys[q] != skeys[p]) continue;
+    const uint32_t vq = sid[q];
+    if (vts(a, ts, c_dl, vq) < vts(a, ts, c_dl, v) + a.W) dead[v] = 1;
+  }
+}
+
+// 4b. per candidate: trigger row (first row with ts >= deadline) or pending; packed counts for the scan
+__global__ void k_abs_decide(AbsArgs a, const uint8_t* __restrict__ role, const uint8_t* __restrict__ dead,
+                             const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
+                             uint32_t* __restrict__ trig, uint64_t* __restrict__ cnt) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.nt; v += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t c = 0;
+    uint32_t t = NONE;
+    if ((role[v] & R_CAND) && !dead[v]) {
+      const int64_t d = vts(a, ts, c_dl, (uint32_t)v) + a.W;
+      int64_t lo = v < a.nc ? 0 : v - a.nc + 1, hi = a.n;   // W > 0: the trigger follows the row
+      while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (ts[mid] < d) lo = mid + 1; else hi = mid;
+      }
+      if (lo < a.n) { t = (uint32_t)lo; c = 1; } else { c = 1ull << 32; }
+    }
+    trig[v] = t;
+    cnt[v] = c;
+  }
+}
+
+struct AbsOut {
+  int32_t n_select, stride;
+  uint64_t base_index;
+  const uint64_t* index;
+  int32_t sel_ok[SG_MAX_SELECT];    // 1: e1 attribute (projected), 0: null (`not` slot / chain index > 0)
+  int32_t sel_col[SG_MAX_SELECT], sel_type[SG_MAX_SELECT];
+};
+
+// 6. emission records and carried partials
+__global__ void __launch_bounds__(256) k_abs_write(AbsArgs a, AbsOut o, SgCols cols, const int64_t* __restrict__ ts,
+                                                   const uint32_t* __restrict__ trig, const uint64_t* __restrict__ cnt,
+                                                   const uint64_t* __restrict__ off, const int64_t* __restrict__ vals,
+                                                   const uint8_t* __restrict__ role, AbsCarry cin, AbsCarry cout,
+                                                   const uint32_t* __restrict__ slot_trig, int64_t n_emit,
+                                                   char* __restrict__ out) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.nt; v += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = cnt[v];
+    if (!c) continue;
+    const uint64_t ofs = off[v];
+    const bool carried = v < a.nc;
+    const int64_t i = v - a.nc;
+    const int64_t d = carried ? cin.dl[v] : ts[i] + a.W;
+    int64_t sv[SG_MAX_SELECT];
+    uint32_t nm = 0;
+    for (int s = 0; s < o.n_select; ++s) {
+      if (carried) {
+        sv[s] = cin.sel[v * o.n_select + s];
+      } else if (o.sel_ok[s]) {
+        SgVal x = sg_read_col(cols, o.sel_col[s], o.sel_type[s], i);
+        sv[s] = sg_val_bits(x);
+        if (x.null) nm |= 1u << s;
+      } else {
+        sv[s] = 0;
+        nm |= 1u << s;
+      }
+    }
+    if (carried) nm = cin.snul[v];
+    if (c & 0xffffffffull) {   // emitted in this push
+      const uint32_t sl = (uint32_t)ofs;
+      const uint32_t t = trig[v];
+      // rank within the trigger's timer pass: emissions are contiguous per trigger (arrival order)
+      int64_t lo = 0, hi = sl;
+      while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (slot_trig[mid] < t) lo = mid + 1; else hi = mid;
+      }
+      int64_t* r = (int64_t*)(out + (size_t)sl * o.stride);
+      r[0] = (int64_t)(o.index ? o.index[t] : o.base_index + t);
+      r[1] = d;
+      r[2] = (int64_t)((uint64_t)(uint32_t)(sl - lo) << 32);   // key 0 | group = rank (timer phase 0)
+      r[3] = (int64_t)nm;
+      for (int s = 0; s < o.n_select; ++s) r[4 + s] = (nm >> s) & 1 ? 0 : sv[s];
+    } else if (a.keep_carry) { // still pending: carried into the next push
+      const uint32_t cs = (uint32_t)(ofs >> 32);
+      cout.dl[cs] = d;
+      cout.val[cs] = vals[v];
+      cout.vnul[cs] = (role[v] & R_SORT) ? 0 : 1;
+      for (int s = 0; s < o.n_select; ++s) cout.sel[(int64_t)cs * o.n_select + s] = sv[s];
+      cout.snul[cs] = nm;
+    }
+  }
+}
+
+__global__ void k_abs_slot_trig(int64_t nt, const uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+                                const uint32_t* __restrict__ trig, uint32_t* __restrict__ slot_trig) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nt; v += (int64_t)gridDim.x * blockDim.x)
+    if (cnt[v] & 0xffffffffull) slot_trig[(uint32_t)off[v]] = trig[v];
+}
+
+__global__ void k_abs_init(unsigned long long* __restrict__ minmax, uint32_t* __restrict__ oflag) {
+  if (threadIdx.x == 0) {
+    minmax[0] = ~0ull;
+    minmax[1] = 0ull;
+    *oflag = 0;
+  }
+}
+
+__global__ void k_abs_last(int64_t n, const int64_t* __restrict__ ts, int64_t* __restrict__ dlast) {
+  if (threadIdx.x == 0 && n > 0) *dlast = ts[n - 1];
+}
+
+AbsState* astate(SgHandle* h) {
+  if (!h->state) {
+    AbsState* s = new AbsState();
+    if (hipMalloc(&s->dlast, 8) != hipSuccess || hipMalloc(&s->dminmax, 16) != hipSuccess ||
+        hipMalloc(&s->dflag, 4) != hipSuccess)
+      throw SgError(SG_EHIP, "hipMalloc failed for absence state");
+    h->state = s;
+    h->state_kind = 3;
+  }
+  return (AbsState*)h->state;
+}
+
+unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 256 * 16)); }
+
+template <class K>
+void sort_and_kill(SgHandle* h, const AbsArgs& a, uint64_t omin, int bits, const uint8_t* role, const int64_t* vals,
+                   const int64_t* ts, const int64_t* c_dl, uint8_t* dead) {
+  hipStream_t st = h->stream;
+  const int64_t nt = a.nt;
+  K* keys = (K*)h->ws.get("abs_keys", sizeof(K) * nt, st);
+  K* skeys = (K*)h->ws.get("abs_skeys", sizeof(K) * nt, st);
+  uint32_t* ids = (uint32_t*)h->ws.get("abs_ids", 4 * nt, st);
+  uint32_t* sid = (uint32_t*)h->ws.get("abs_sid", 4 * nt, st);
+  const K sentinel = (K)(bits >= (int)(8 * sizeof(K)) ? ~(K)0 : ((K)1 << bits) - 1);
+  hipLaunchKernelGGL((k_abs_keys<K>), dim3(grid_for(nt)), dim3(256), 0, st, nt, role, vals, omin, sentinel, keys, ids);
+  size_t tb = 0;
+  HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, ids, sid, (size_t)nt, 0, bits, st));
+  void* tmp = h->ws.get("abs_sort_tmp", tb, st);
+  HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, ids, sid, (size_t)nt, 0, bits, st));
+  uint32_t* rk = (uint32_t*)h->ws.get("abs_rk", 4 * nt, st);
+  uint32_t* nks = (uint32_t*)h->ws.get("abs_nks", 4 * nt, st);
+  hipLaunchKernelGGL(k_abs_rkill, dim3(grid_for(nt)), dim3(256), 0, st, nt, sid, role, rk);
+  tb = 0;
+  HIPCHK(rocprim::inclusive_scan(nullptr, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
+  tmp = h->ws.get("abs_scan_tmp", tb, st);
+  HIPCHK(rocprim::inclusive_scan(tmp, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
+  hipLaunchKernelGGL((k_abs_kill<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, role, nks, ts, c_dl, dead);
+  HIPCHK(hipGetLastError());
+}
+
+}  // namespace
+
+bool sg_every_absent_supported(const sg_nfa_desc& d) {
+  const int a = d.shape_args[0], b = d.shape_args[1];
+  const int ca = d.ret_col[d.shape_args[4]], cb = d.ret_col[d.shape_args[3]];
+  if (d.partitioned || d.within != -1 || !d.playback) return false;
+  if (d.states[b].waiting_time <= 0) return false;
+  if (d.states[a].stream == d.states[b].stream && ca != cb) return false;   // one compared value per row
+  return d.col_type[ca] == d.col_type[cb];
+}
+
+void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
+  const sg_nfa_desc& d = h->desc;
+  if (!sg_every_absent_supported(d)) {
+    sg_run_general(h, bv, n);
+    return;
+  }
+  hipStream_t st = h->stream;
+  AbsState* as = astate(h);
+  AbsCarry& cin = as->carry[as->cur];
+  AbsCarry& cout = as->carry[as->cur ^ 1];
+  const int a_state = d.shape_args[0], b_state = d.shape_args[1];
+  AbsArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = n;
+  a.nc = h->opt.no_carry ? 0 : cin.n;
+  a.nt = a.nc + n;
+  if (a.nt >= (1ll << 31)) throw SgError(SG_EINVAL, "batch plus pending partials exceed 2^31");
+  a.W = d.states[b_state].waiting_time;
+  a.s_a = d.states[a_state].stream;
+  a.s_b = d.states[b_state].stream;
+  a.col_a = d.ret_col[d.shape_args[4]];
+  a.col_b = d.ret_col[d.shape_args[3]];
+  a.type = d.col_type[a.col_a];
+  a.prog_a_off = d.states[a_state].prog_off;
+  a.prog_a_len = d.states[a_state].prog_len;
+  a.prog_b_off = d.shape_prog_off;
+  a.prog_b_len = d.shape_prog_len;
+  a.has_stream = bv.stream ? 1 : 0;
+  a.first_push = h->pushes == 0 || h->opt.no_carry ? 1 : 0;
+  a.keep_carry = h->opt.no_carry ? 0 : 1;
+  const int64_t nt = a.nt;
+  h->split_out = 0;
+  h->extra_marks = 0;
+  h->mark(0);
+  // ---- 1. roles and value range
+  uint8_t* role = (uint8_t*)h->ws.get("abs_role", nt, st);
+  int64_t* vals = (int64_t*)h->ws.get("abs_vals", 8 * nt, st);
+  uint8_t* dead = (uint8_t*)h->ws.get("abs_dead", nt, st);
+  hipLaunchKernelGGL(k_abs_init, dim3(1), dim3(64), 0, st, (unsigned long long*)as->dminmax, as->dflag);
+  HIPCHK(hipMemsetAsync(dead, 0, nt, st));
+  if (nt > 0)
+    hipLaunchKernelGGL(k_abs_rows, dim3(grid_for(nt)), dim3(256), 0, st, a, bv.cols, h->ddesc, bv.ts, bv.stream,
+                       cin.val, cin.vnul, role, vals, (unsigned long long*)as->dminmax, as->dlast, as->dflag);
+  HIPCHK(hipGetLastError());
+  h->mark(1);
+  uint64_t mm[2] = {0, 0};
+  uint32_t oflag = 0;
+  HIPCHK(hipMemcpyAsync(mm, as->dminmax, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&oflag, as->dflag, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (oflag) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps");
+  // ---- 2-4. sort by value, kill
+  if (mm[0] <= mm[1] && nt > 0) {
+    const uint64_t range = mm[1] - mm[0];   // sentinel = range + 1 must fit in the key bits
+    int bits = 1;
+    while (bits < 64 && (range + 1) >> bits) ++bits;
+    if (range + 1 == 0) bits = 64;
+    if (bits <= 32)
+      sort_and_kill<uint32_t>(h, a, mm[0], bits, role, vals, bv.ts, cin.dl, dead);
+    else
+      sort_and_kill<uint64_t>(h, a, mm[0], bits, role, vals, bv.ts, cin.dl, dead);
+  }
+  h->mark(2);
+  // ---- decide, scan
+  uint32_t* trig = (uint32_t*)h->ws.get("abs_trig", 4 * nt, st);
+  uint64_t* cnt = (uint64_t*)h->ws.get("abs_cnt", 8 * (nt + 1), st);
+  uint64_t* off = (uint64_t*)h->ws.get("abs_off", 8 * (nt + 1), st);
+  if (nt > 0)
+    hipLaunchKernelGGL(k_abs_decide, dim3(grid_for(nt)), dim3(256), 0, st, a, role, dead, bv.ts, cin.dl, trig, cnt);
+  HIPCHK(hipMemsetAsync(cnt + nt, 0, 8, st));
+  size_t tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint64_t)0, (size_t)nt + 1, rocprim::plus<uint64_t>(), st));
+  void* tmp = h->ws.get("abs_oscan_tmp", tb, st);
+  HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint64_t)0, (size_t)nt + 1, rocprim::plus<uint64_t>(), st));
+  uint64_t tot = 0;
+  HIPCHK(hipMemcpyAsync(&tot, off + nt, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const int64_t n_emit = (int64_t)(tot & 0xffffffffull), n_carry = (int64_t)(tot >> 32);
+  h->mark(3);
+  // ---- 6. write
+  AbsOut o;
+  memset(&o, 0, sizeof(o));
+  o.n_select = d.n_select;
+  o.stride = 32 + 8 * d.n_select;
+  o.base_index = bv.base_index;
+  o.index = bv.index;
+  for (int s = 0; s < d.n_select; ++s) {
+    const int idx = d.sel_index[s];
+    o.sel_ok[s] = d.sel_state[s] == a_state && (idx == 0 || idx == -1);
+    o.sel_col[s] = d.ret_col[d.sel_ret[s]];
+    o.sel_type[s] = d.sel_type[s];
+  }
+  char* rec = h->out.reserve(n_emit, d.n_select, st);
+  char* dst = rec + (size_t)h->out.n * o.stride;
+  if (!h->opt.no_carry) cout.reserve(n_carry, d.n_select);
+  uint32_t* slot_trig = (uint32_t*)h->ws.get("abs_slot_trig", 4 * (n_emit + 1), st);
+  if (nt > 0) {
+    hipLaunchKernelGGL(k_abs_slot_trig, dim3(grid_for(nt)), dim3(256), 0, st, nt, cnt, off, trig, slot_trig);
+    hipLaunchKernelGGL(k_abs_write, dim3(grid_for(nt)), dim3(256), 0, st, a, o, bv.cols, bv.ts, trig, cnt, off, vals,
+                       role, cin, cout, slot_trig, n_emit, dst);
+  }
+  if (n > 0) hipLaunchKernelGGL(k_abs_last, dim3(1), dim3(64), 0, st, n, bv.ts, as->dlast);
+  HIPCHK(hipGetLastError());
+  h->mark(4);
+  h->out.n += n_emit;
+  if (!h->opt.no_carry) {
+    cout.n = n_carry;
+    as->cur ^= 1;
+  }
+  h->last_events = n;
+  h->last_matches = n_emit;
+  h->last_spilled = 0;
+}
+
+void sg_every_absent_reset(SgHandle* h) {
+  if (h->state && h->state_kind == 3) {
+    AbsState* as = (AbsState*)h->state;
+    as->carry[0].n = as->carry[1].n = 0;
+  }
+}
+
+void sg_every_absent_release(SgHandle* h) {
+  if (!h->state || h->state_kind != 3) return;
+  AbsState* as = (AbsState*)h->state;
+  as->carry[0].release();
+  as->carry[1].release();
+  hipFree(as->dlast);
+  hipFree(as->dminmax);
+  hipFree(as->dflag);
+  delete as;
+  h->state = nullptr;
+  h->state_kind = 0;
+}

@@ -222,6 +222,7 @@ int sg_reset(sg_handle* hh) {
     h.pushes = 0;
     h.clock = 0;
     sg_every_next_reset(&h);
+    sg_every_absent_reset(&h);
     sg_general_reset(&h);
   });
 }
@@ -269,6 +270,7 @@ int sg_close(sg_handle* hh) {
   hipSetDevice(h.device);
   if (h.stream) hipStreamSynchronize(h.stream);
   sg_every_next_release(&h);
+  sg_every_absent_release(&h);
   sg_general_release(&h);
   h.ws.release();
   h.out.release();

@@ -118,5 +118,7 @@ void sg_every_next_reset(SgHandle* h);
 void sg_every_next_release(SgHandle* h);
 void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_every_absent_reset(SgHandle* h);
+void sg_every_absent_release(SgHandle* h);
 void sg_general_reset(SgHandle* h);
 void sg_general_release(SgHandle* h);
