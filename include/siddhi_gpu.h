@@ -133,7 +133,10 @@ typedef struct sg_options {
   int32_t no_carry;         /* 1: pushes are independent streams (no state carried between them) */
   int32_t ring_cap;         /* closed form: LDS pending-list ring per walker lane (power of two 2..256;
                                0 = chosen per push from the rows per `within` window) */
-  int32_t reserved[5];
+  int32_t chunk_rows;       /* general engine: a key's rows are cut into units of this many rows, each unit
+                               rebuilding its state by replaying the rows inside the query's horizon before
+                               it (0 = chosen per push, -1 = one unit per key) */
+  int32_t reserved[4];
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)

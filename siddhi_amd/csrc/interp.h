@@ -77,6 +77,7 @@ struct KeyMachine {
   uint32_t group;
   int64_t now;          // playback clock value (TimestampGeneratorImpl.currentTime)
   int failed;
+  int silent;           // replaying a unit's horizon: state only, no emission
 
   // ---------------------------------------------------------------- raw accessors
   SG_HD int32_t* hdr() { return a; }
@@ -297,7 +298,7 @@ struct KeyMachine {
 
   // ---------------------------------------------------------------- emission (QuerySelector)
   SG_HD void emit(int p) {
-    if (failed) return;
+    if (failed || silent) return;
     unsigned long long o = atomic_bump(sink.count);
     if ((int64_t)o >= sink.cap) { *sink.overflow = 1; return; }
     char* r = sink.buf + (size_t)o * (size_t)sink.stride;
@@ -732,8 +733,11 @@ struct KeyMachine {
 // Rows interface:  n_own(), own_local(i) (local row index of the i-th own row), fill(local, SgRow&),
 //                  ts(local), find_ge(from_local, value) -> first local row >= from_local with ts >= value
 //                  (or n_rows), n_rows(), plus has_receiver(stream).
+//
+// emit_from: own rows before this index only rebuild state (a chunked unit's replay window, see
+// interp.hip): their matches are not emitted.
 template <class Rows>
-SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start) {
+SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t emit_from = 0) {
   const int A = m.g->A;
   int abs_state[SG_MAX_STATES];
   for (int s = 0, k = 0; s < m.g->S; ++s)
@@ -754,6 +758,7 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start) {
         if (r < ltim) ltim = r;
       }
     }
+    m.silent = i < emit_from ? 1 : 0;
     if (ltim < nrows && ltim <= lev) {
       m.now = rows.ts(ltim);
       m.trigger = rows.index_of(ltim);
@@ -788,6 +793,74 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start) {
     m.set_pos((int64_t)row.index);
     ++i;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Chunked units.  A key's rows can be cut into units that run in parallel when the state reached before
+// a unit's first row is a function of a bounded suffix of the key's history (the "horizon"); each unit
+// then starts from a fresh runtime and replays that suffix without emitting:
+//   patterns with `within T` whose start states all re-arm themselves with `every` (and no
+//   withinEvery re-arm outside partition clones): a partial started more than T before a row is expired
+//   at that row (StreamPreStateProcessor.isExpired, C/query/input/stream/state/
+//   StreamPreStateProcessor.java:102-113) and can neither advance nor emit again, so the rows with
+//   ts >= ts(first) - T rebuild every live partial;
+//   single-stream sequences whose start states re-arm with `every` and whose counts are bounded: every
+//   event resets the partials that did not advance on it (StateStreamRuntime.resetAndUpdate,
+//   C/query/input/stream/state/StateStreamRuntime.java:96-99), so a live partial is at most
+//   sum(max count or 1) events old.
+// Absence (timers on the global clock) is never chunked.
+struct SgChunkRule {
+  int kind;            // 0 none, 1 time horizon, 2 event horizon
+  int64_t within;      // kind 1
+  int64_t events;      // kind 2
+};
+SG_HD inline SgChunkRule sg_chunk_rule(const sg_nfa_desc& d) {
+  SgChunkRule r{0, 0, 0};
+  int starts = 0;
+  for (int s = 0; s < d.n_states; ++s) {
+    if (d.states[s].kind == SG_K_ABSENT) return r;
+    if (d.states[s].is_start) {
+      if (d.states[s].next_every != s) return r;
+      ++starts;
+    }
+  }
+  if (!starts) return r;
+  if (d.type == 0) {
+    if (d.within < 0) return r;
+    if (!d.partitioned)
+      for (int s = 0; s < d.n_states; ++s) if (d.states[s].within_every >= 0) return r;
+    r.kind = 1;
+    r.within = d.within;
+    return r;
+  }
+  int recv = 0;
+  for (int s = 0; s < SG_MAX_STREAMS; ++s) if (d.recv_of_stream[s] >= 0) ++recv;
+  if (recv != 1) return r;
+  int64_t h = 0;
+  for (int s = 0; s < d.n_states; ++s) {
+    const sg_state_desc& x = d.states[s];
+    if (x.kind == SG_K_COUNT) {
+      if (x.max_count < 0 || x.max_count > 4096) return r;
+      h += x.max_count;
+    } else {
+      h += 1;
+    }
+  }
+  r.kind = 2;
+  r.events = h;
+  return r;
+}
+// First own row a unit starting at own row p0 (> 0) must replay from; ts_at(i) = timestamp of own row i.
+template <class TsAt>
+SG_HD int64_t sg_replay_start(const SgChunkRule& r, int64_t p0, TsAt ts_at) {
+  if (r.kind == 2) return p0 > r.events ? p0 - r.events : 0;
+  const int64_t lo_ts = ts_at(p0) - r.within;
+  int64_t lo = 0, hi = p0;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (ts_at(mid) < lo_ts) lo = mid + 1; else hi = mid;
+  }
+  return lo;
 }
 
 // Arena geometry for a descriptor and pool capacities (words of int32 per key).

@@ -8,7 +8,10 @@
 //                   in arrival order (PartitionStreamReceiver routing)
 //   3. k_nfa        one thread per key that ever appeared: runs the key machine over its rows and the
 //                   absence timers its schedulers fire on the global playback clock; every match is
-//                   appended (atomic bump) with a sort key (trigger row, timer-before-event, key)
+//                   appended (atomic bump) with a sort key (trigger row, timer-before-event, key).
+//      k_nfa_units  (shapes with a bounded horizon, interp.h sg_chunk_rule) one thread per (key, chunk of
+//                   R rows): a unit rebuilds its key's state by replaying the rows inside the horizon before
+//                   its chunk, so a key's rows run on many lanes instead of one
 //   4. radix sort of the sort keys (stable: per-key emission order is kept) + k_gather into the
 //                   pending match store in the reference's delivery order.
 #include <cstring>
@@ -159,6 +162,7 @@ __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDes
   m.phase = 1;
   m.group = 0;
   m.now = 0;
+  m.silent = 0;
   m.failed = ar[K_OVERFLOW];
   if (m.failed) { atomicCAS(fail_code, 0, m.failed); return; }
   DevRowsTs rows;
@@ -173,6 +177,105 @@ __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDes
   rows.index = a.index;
   sg_run_key(m, rows, !a.partitioned);
   if (m.failed) atomicCAS(fail_code, 0, m.failed);
+}
+
+// ---- chunked units (interp.h sg_chunk_rule): unit u = (key, chunk c) over the key's own rows
+// [c*R, min(nown, (c+1)*R)).  Unit 0 continues the key's carried runtime in place; unit c > 0 runs in a
+// scratch arena from a fresh runtime (or from the key's state at the push start when its horizon reaches
+// the key's first row of this push) and replays its horizon without emitting.  After the pass the last
+// unit's arena becomes the key's runtime.
+struct UnitArgs {
+  uint32_t R;
+  SgChunkRule rule;
+  const uint32_t* umap;     // unit -> key
+  const uint32_t* uoff;     // key -> first unit
+  int64_t n_units;
+  int32_t* scratch;         // per-unit arenas
+  const int32_t* snap;      // arenas at the push start
+};
+
+__global__ void k_unit_count(int64_t nkeys, const uint32_t* __restrict__ beg, const uint32_t* __restrict__ end,
+                             uint32_t R, uint32_t* __restrict__ nch) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > nkeys) return;
+  uint32_t rows = (k < nkeys && end[k] > beg[k]) ? end[k] - beg[k] : 0u;
+  nch[k] = (rows + R - 1) / R;
+}
+
+__global__ void k_unit_map(int64_t nkeys, const uint32_t* __restrict__ uoff, uint32_t* __restrict__ umap) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nkeys) return;
+  for (uint32_t u = uoff[k]; u < uoff[k + 1]; ++u) umap[u] = (uint32_t)k;
+}
+
+__global__ void __launch_bounds__(64) k_nfa_units(NfaArgs a, UnitArgs ua, SgCols cols, const DevDesc* __restrict__ dd,
+                                                  const SgGeo* __restrict__ geo, int32_t* __restrict__ arena,
+                                                  SgEmitSink sink, int32_t* __restrict__ fail_code) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= ua.n_units) return;
+  const uint32_t k = ua.umap[u];
+  const uint32_t c = (uint32_t)(u - ua.uoff[k]);
+  const uint32_t b = a.beg[k], e = a.end[k];
+  const int64_t nown = (int64_t)(e - b);
+  const int64_t p0 = (int64_t)c * ua.R, p1 = p0 + ua.R < nown ? p0 + ua.R : nown;
+  const size_t kw = (size_t)geo->key_words;
+  int32_t* ar;
+  int64_t q = 0;
+  if (c == 0) {
+    ar = arena + (size_t)k * kw;
+  } else {
+    ar = ua.scratch + (size_t)u * kw;
+    const uint32_t* own = a.rows + b;
+    const int64_t* ts = a.ts;
+    q = sg_replay_start(ua.rule, p0, [&](int64_t i) { return ts[own[i]]; });
+    if (q == 0) {
+      const int32_t* src = ua.snap + (size_t)k * kw;
+      for (size_t w = 0; w < kw; ++w) ar[w] = src[w];
+    } else {
+      ar[K_CREATED] = 0;
+      ar[K_OVERFLOW] = 0;
+    }
+  }
+  KeyMachine m;
+  m.d = dd;
+  m.g = geo;
+  m.a = ar;
+  m.key = (int32_t)k;
+  m.clone = a.clone;
+  m.sink = sink;
+  m.base_index = a.base_index;
+  m.trigger = a.base_index;
+  m.phase = 1;
+  m.group = 0;
+  m.now = 0;
+  m.silent = 0;
+  m.failed = ar[K_OVERFLOW];
+  if (m.failed) { atomicCAS(fail_code, 0, m.failed); return; }
+  DevRowsTs rows;
+  rows.rows = a.rows + b + q;
+  rows.nown = p1 - q;
+  rows.n = a.n;
+  rows.DevRows::ts = a.ts;
+  rows.stream = a.stream;
+  rows.cols = &cols;
+  rows.d = dd;
+  rows.base = a.base_index;
+  rows.index = a.index;
+  sg_run_key(m, rows, !a.partitioned, p0 - q);
+  if (m.failed) atomicCAS(fail_code, 0, m.failed);
+}
+
+// the last unit's runtime becomes the key's runtime (one block per key)
+__global__ void k_unit_keep(int64_t nkeys, const uint32_t* __restrict__ uoff, const int32_t* __restrict__ scratch,
+                            const SgGeo* __restrict__ geo, int32_t* __restrict__ arena) {
+  for (int64_t k = blockIdx.x; k < nkeys; k += gridDim.x) {
+    const uint32_t u0 = uoff[k], u1 = uoff[k + 1];
+    if (u1 - u0 < 2) continue;
+    const size_t kw = (size_t)geo->key_words;
+    const int32_t* src = scratch + (size_t)(u1 - 1) * kw;
+    int32_t* dst = arena + (size_t)k * kw;
+    for (size_t w = threadIdx.x; w < kw; w += blockDim.x) dst[w] = src[w];
+  }
 }
 
 __global__ void k_sortkeys(int64_t n, const char* __restrict__ buf, int32_t stride, uint64_t* __restrict__ sk,
@@ -310,8 +413,66 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   sink.overflow = eover;
   sink.stride = stride;
   sink.key_bits = kbits;
-  hipLaunchKernelGGL(k_nfa, dim3((unsigned)((kb + 63) / 64)), dim3(64), 0, st, na, bv.cols, h->ddesc, gs->dgeo,
-                     gs->arena, sink, gs->dfail);
+  // ---- unit plan: one unit per key, or (chunkable shapes) per (key, chunk of R rows)
+  const SgChunkRule rule = sg_chunk_rule(d);
+  uint32_t R = 0;
+  if (rule.kind != 0 && h->opt.chunk_rows >= 0 && n > 0) {
+    if (h->opt.chunk_rows > 0) {
+      R = (uint32_t)h->opt.chunk_rows;
+    } else {
+      // horizon rows per unit (rows of an average key inside `within`, or the sequence's event horizon);
+      // units at least 4x their horizon, enough of them to fill the chip, scratch arenas within budget
+      int64_t span = 1;
+      {
+        int64_t tfl[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        span = std::max<int64_t>(1, tfl[1] - tfl[0]);
+      }
+      const double per_key = (double)n / (double)std::max<uint32_t>(kb, 1);
+      const double hz = rule.kind == 2 ? (double)rule.events : per_key * (double)rule.within / (double)span;
+      const int64_t target_units = 256 * 8 * 64;
+      const int64_t mem_units = std::max<int64_t>(1, ((int64_t)8 << 30) / ((int64_t)gs->geo.key_words * 4));
+      int64_t r = std::max<int64_t>({(int64_t)(4.0 * hz) + 1, 32, (n + target_units - 1) / target_units,
+                                     (n + mem_units - 1) / mem_units});
+      R = (uint32_t)std::min<int64_t>(r, 1 << 30);
+      if ((double)R >= per_key * 2.0) R = 0;   // hardly any key would be cut
+    }
+  }
+  if (R > 0) {
+    uint32_t* nch = (uint32_t*)h->ws.get("g_nch", sizeof(uint32_t) * (kb + 1), st);
+    uint32_t* uoff = (uint32_t*)h->ws.get("g_uoff", sizeof(uint32_t) * (kb + 1), st);
+    hipLaunchKernelGGL(k_unit_count, dim3((unsigned)((kb + 1 + 255) / 256)), blk, 0, st, (int64_t)kb, beg, end, R, nch);
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, nch, uoff, (uint32_t)0, (size_t)kb + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("g_uscan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, nch, uoff, (uint32_t)0, (size_t)kb + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t U = 0;
+    HIPCHK(hipMemcpyAsync(&U, uoff + kb, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const size_t kw = (size_t)gs->geo.key_words;
+    UnitArgs ua;
+    ua.R = R;
+    ua.rule = rule;
+    ua.n_units = U;
+    ua.uoff = uoff;
+    uint32_t* umap = (uint32_t*)h->ws.get("g_umap", sizeof(uint32_t) * std::max<uint32_t>(U, 1), st);
+    ua.umap = umap;
+    ua.scratch = (int32_t*)h->ws.get("g_uarena", sizeof(int32_t) * kw * std::max<uint32_t>(U, 1), st);
+    int32_t* snap = (int32_t*)h->ws.get("g_snap", sizeof(int32_t) * kw * kb, st);
+    HIPCHK(hipMemcpyAsync(snap, gs->arena, sizeof(int32_t) * kw * kb, hipMemcpyDeviceToDevice, st));
+    ua.snap = snap;
+    hipLaunchKernelGGL(k_unit_map, dim3((unsigned)((kb + 255) / 256)), blk, 0, st, (int64_t)kb, uoff, umap);
+    if (U)
+      hipLaunchKernelGGL(k_nfa_units, dim3((unsigned)((U + 63) / 64)), dim3(64), 0, st, na, ua, bv.cols, h->ddesc,
+                         gs->dgeo, gs->arena, sink, gs->dfail);
+    hipLaunchKernelGGL(k_unit_keep, dim3((unsigned)std::min<uint32_t>(std::max<uint32_t>(kb, 1), 65535)), blk, 0, st,
+                       (int64_t)kb, uoff, ua.scratch, gs->dgeo, gs->arena);
+  } else {
+    hipLaunchKernelGGL(k_nfa, dim3((unsigned)((kb + 63) / 64)), dim3(64), 0, st, na, bv.cols, h->ddesc, gs->dgeo,
+                       gs->arena, sink, gs->dfail);
+  }
   HIPCHK(hipGetLastError());
   h->mark(3);
   unsigned long long total = 0;

@@ -17,6 +17,7 @@ struct HiHandle {
   std::vector<std::vector<int32_t>> arenas;
   std::vector<std::vector<char>> out;
   int err = 0;
+  int chunk_rows = 0;   // >0: cut each key's rows into units replaying their horizon (as interp.hip does)
 };
 
 struct HostRows {
@@ -70,6 +71,14 @@ HiHandle* hi_open(const sg_nfa_desc* d, int P, int E, int C, int L) {
 
 void hi_close(HiHandle* h) { delete h; }
 
+void hi_set_chunk(HiHandle* h, int chunk_rows) { h->chunk_rows = chunk_rows; }
+
+int hi_chunk_rule(const sg_nfa_desc* d, int64_t* horizon) {
+  SgChunkRule r = sg_chunk_rule(*d);
+  *horizon = r.kind == 2 ? r.events : r.within;
+  return r.kind;
+}
+
 int hi_push(HiHandle* h, const sg_batch* b) {
   const sg_nfa_desc& d = h->d;
   int64_t n = b->n;
@@ -97,18 +106,45 @@ int hi_push(HiHandle* h, const sg_batch* b) {
       if (own[k].empty() && d.partitioned) continue;
       h->arenas[k].assign((size_t)h->g.key_words, 0);
     }
-    KeyMachine m;
-    memset(&m, 0, sizeof(m));
-    m.d = &d;
-    m.g = &h->g;
-    m.a = h->arenas[k].data();
-    m.key = (int32_t)k;
-    m.clone = d.partitioned;
-    m.sink = SgEmitSink{buf.data(), (int64_t)cap, &count, &overflow, stride, kb};
-    m.base_index = b->base_index;
-    HostRows rows{b, &d, &own[k]};
-    sg_run_key(m, rows, !d.partitioned);
-    if (m.failed) { h->err = m.failed; return m.failed; }
+    auto run = [&](int32_t* arena, const std::vector<int64_t>* rws, int64_t emit_from) {
+      KeyMachine m;
+      memset(&m, 0, sizeof(m));
+      m.d = &d;
+      m.g = &h->g;
+      m.a = arena;
+      m.key = (int32_t)k;
+      m.clone = d.partitioned;
+      m.sink = SgEmitSink{buf.data(), (int64_t)cap, &count, &overflow, stride, kb};
+      m.base_index = b->base_index;
+      HostRows rows{b, &d, rws};
+      sg_run_key(m, rows, !d.partitioned, emit_from);
+      return m.failed;
+    };
+    const SgChunkRule rule = sg_chunk_rule(d);
+    const int64_t nown = (int64_t)own[k].size();
+    const int64_t R = h->chunk_rows;
+    if (R <= 0 || rule.kind == 0 || nown <= R) {
+      if (int f = run(h->arenas[k].data(), &own[k], 0)) { h->err = f; return f; }
+      continue;
+    }
+    // chunked units: unit 0 continues the key's state; unit c > 0 replays its horizon from a fresh runtime
+    // (or from the state at the push start when the horizon reaches the key's first row of this push)
+    const std::vector<int32_t> snap = h->arenas[k];
+    std::vector<int32_t> last;
+    for (int64_t p0 = 0; p0 < nown; p0 += R) {
+      const int64_t p1 = std::min(nown, p0 + R);
+      if (p0 == 0) {
+        std::vector<int64_t> sub(own[k].begin(), own[k].begin() + p1);
+        if (int f = run(h->arenas[k].data(), &sub, 0)) { h->err = f; return f; }
+        continue;
+      }
+      const int64_t q = sg_replay_start(rule, p0, [&](int64_t i) { return b->ts[own[k][i]]; });
+      std::vector<int32_t> arena = q == 0 ? snap : std::vector<int32_t>((size_t)h->g.key_words, 0);
+      std::vector<int64_t> sub(own[k].begin() + q, own[k].begin() + p1);
+      if (int f = run(arena.data(), &sub, p0 - q)) { h->err = f; return f; }
+      if (p1 == nown) last.swap(arena);
+    }
+    h->arenas[k].swap(last);
   }
   if (overflow) { h->err = SG_ECAPACITY; return SG_ECAPACITY; }
   std::vector<size_t> idx(count);

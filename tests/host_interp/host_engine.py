@@ -30,12 +30,13 @@ def _load():
         lib.hi_count.restype = ct.c_int64
         lib.hi_count.argtypes = [P]
         lib.hi_fetch.argtypes = [P, P, P, P, P, P, P]
+        lib.hi_set_chunk.argtypes = [P, ct.c_int]
         _lib = lib
     return _lib
 
 
 class HostInterpEngine:
-    def __init__(self, ctx, pool=256):
+    def __init__(self, ctx, pool=256, chunk_rows=0):
         from siddhi_amd import lowering as L
         from siddhi_amd import _native as N
         self.lib = _load()
@@ -44,6 +45,7 @@ class HostInterpEngine:
         self.desc = N.build_desc(self.nfa)
         self.nsel = len(self.nfa.select)
         self.h = self.lib.hi_open(ct.byref(self.desc), pool, pool, pool, pool)
+        self.lib.hi_set_chunk(self.h, chunk_rows)
 
     def push(self, b):
         keep = []

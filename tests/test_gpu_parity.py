@@ -133,3 +133,38 @@ def test_every_next_multi_push_carry(cfg, n, keys, rate, splits):
         lo = hi
     got = run_engine(gpu_engine(), q, parts)
     assert_same(got, want)
+
+
+@pytest.mark.parametrize("chunk", [0, 5, 64])
+@pytest.mark.parametrize("cfg,n,keys,rate", [
+    ("C3b", 300_000, 1_000, 1_000),
+    ("C3c", 300_000, 1_000, 100),
+    ("C3c", 200_000, 30, 10),
+    ("C2", 200_000, 1_000, 100),
+])
+def test_general_kernel_chunked_units(cfg, n, keys, rate, chunk):
+    """(key, chunk) units replaying their horizon (interp.hip k_nfa_units); chunk 0 = the automatic size."""
+    from siddhi_amd._native import GpuEngine
+    b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
+    b.key = dense_first_seen(b.key)
+    q = synth.QUERIES[cfg]
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True, chunk_rows=chunk), q, [b])
+    assert_same(got, want)
+
+
+@pytest.mark.parametrize("cfg", ["C3b", "C3c"])
+def test_general_kernel_chunked_multi_push(cfg):
+    from siddhi_amd._native import GpuEngine
+    from siddhi_amd.runtime import Batch
+    b = synth_batch(cfg, 0, 200_000, keys=300, rate=100)
+    b.key = dense_first_seen(b.key)
+    q = synth.QUERIES[cfg]
+    want = run_engine(OracleEngine, q, [b])
+    parts, lo = [], 0
+    for hi in (60_000, 60_001, 150_000, 200_000):
+        parts.append(Batch(hi - lo, lo, b.ts[lo:hi], b.stream[lo:hi], b.key[lo:hi],
+                           [c[lo:hi] for c in b.cols], [None] * len(b.cols)))
+        lo = hi
+    got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True, chunk_rows=9), q, parts)
+    assert_same(got, want)

@@ -59,3 +59,60 @@ def test_machine_multi_push():
         lo = hi
     got = run_engine(HostInterpEngine, synth.QUERIES["C3c"], parts)
     assert_same(got, want)
+
+
+# ---- chunked units (interp.h sg_chunk_rule / sg_replay_start): tiny units so nearly every row sits in
+# some unit's replay horizon
+@pytest.mark.parametrize("chunk", [1, 3, 17])
+@pytest.mark.parametrize("case", KATS, ids=lambda k: k["name"])
+def test_machine_kat_chunked(case, chunk):
+    rows, tss = run_kat(case, lambda ctx: HostInterpEngine(ctx, chunk_rows=chunk))
+    assert rows == case["expect"]
+
+
+@pytest.mark.parametrize("chunk", [5, 64])
+@pytest.mark.parametrize("cfg,n,keys,rate", [
+    ("C3", 60_000, 200, 1_000), ("C3b", 60_000, 200, 1_000), ("C3c", 60_000, 200, 100),
+    ("C3c", 60_000, 20, 10), ("C2", 60_000, 100, 100), ("C1", 30_000, 1, 1),
+])
+def test_machine_synthetic_chunked(cfg, n, keys, rate, chunk):
+    b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
+    b.key = dense_first_seen(b.key)
+    want = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, chunk_rows=chunk), synth.QUERIES[cfg], [b])
+    assert_same(got, want)
+
+
+@pytest.mark.parametrize("cfg", ["C3b", "C3c"])
+def test_machine_multi_push_chunked(cfg):
+    """Units whose horizon reaches back to the push start replay from the key's carried state."""
+    from siddhi_amd.runtime import Batch
+    b = synth_batch(cfg, 0, 60_000, keys=100, rate=100)
+    b.key = dense_first_seen(b.key)
+    want = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
+    parts, lo = [], 0
+    for hi in (20_000, 20_001, 41_000, 60_000):
+        parts.append(Batch(hi - lo, lo, b.ts[lo:hi], b.stream[lo:hi], b.key[lo:hi],
+                           [c[lo:hi] for c in b.cols], [None] * len(b.cols)))
+        lo = hi
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, chunk_rows=7), synth.QUERIES[cfg], parts)
+    assert_same(got, want)
+
+
+def test_chunk_rules():
+    """Which shapes may be cut into units (horizon kind: 0 none, 1 `within`, 2 sequence event count)."""
+    import ctypes as ct
+    from host_engine import _load
+    from parity_util import context
+    from siddhi_amd import _native as N
+    from siddhi_amd import lowering as L
+    lib = _load()
+    lib.hi_chunk_rule.restype = ct.c_int
+    lib.hi_chunk_rule.argtypes = [ct.c_void_p, ct.POINTER(ct.c_int64)]
+    want = {"C1": 0, "C2": 1, "C3": 0, "C3b": 2, "C3c": 1, "C4": 0, "C5": 1}   # C1: withinEvery re-arm
+    for cfg, kind in want.items():
+        desc = N.build_desc(L.lower(context(synth.QUERIES[cfg])))
+        h = ct.c_int64(0)
+        assert lib.hi_chunk_rule(ct.byref(desc), ct.byref(h)) == kind, cfg
+        if cfg == "C3b":
+            assert h.value == 1 + 5 + 1 + 1
