@@ -135,7 +135,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--events", type=int, default=0, help="events per GPU per step (default: config size, max 1e8)")
     ap.add_argument("--cpu-sample", type=int, default=0,
-                    help="events for the CPU baseline (default: 12M; C4 60k -- the oracle walks ~5k partials per event)")
+                    help="events for the CPU baseline (default per config: ~5-20 s of oracle work; C4 60k -- the "
+                         "oracle walks ~5k partials per event)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16, help="processes for the key-sharded CPU baseline")
     ap.add_argument("--profile", default=os.path.join(ROOT, "profiles", "r01", "c2_profile.json"),
@@ -149,8 +150,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     cfg = args.config
-    if not args.cpu_sample:
-        args.cpu_sample = 60_000 if cfg.startswith("C4") else 12_000_000
+    if not args.cpu_sample:   # ~5-20 s of single-thread oracle work per config (measured rates)
+        args.cpu_sample = {"C1": 1_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000,
+                           "C5": 3_000_000}.get(cfg, 12_000_000)
     num, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
     n = args.events or min(n_cfg, 100_000_000)
 

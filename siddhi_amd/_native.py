@@ -289,7 +289,7 @@ class GpuEngine:
         import numpy as np
         keep = []
         ts = np.ascontiguousarray(b.ts, np.int64)
-        st = np.ascontiguousarray(b.stream, np.int32)
+        st = None if b.stream is None else np.ascontiguousarray(b.stream, np.int32)   # None: every row stream 0
         ky = np.ascontiguousarray(b.key, np.int32)
         cols = [np.ascontiguousarray(c) for c in b.cols]
         keep += [ts, st, ky] + cols + [x for x in b.nulls if x is not None]
@@ -299,7 +299,7 @@ class GpuEngine:
             ixa = np.ascontiguousarray(b.index, np.uint64)
             keep.append(ixa)
             ix = ixa.ctypes.data
-        sb = make_batch(b.n, b.base_index, ts.ctypes.data, st.ctypes.data, ky.ctypes.data,
+        sb = make_batch(b.n, b.base_index, ts.ctypes.data, 0 if st is None else st.ctypes.data, ky.ctypes.data,
                         [c.ctypes.data for c in cols], [(x.ctypes.data if x is not None else 0) for x in b.nulls],
                         0, kb, keep, index=ix)
         self.handle.push(sb)

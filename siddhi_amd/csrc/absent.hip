@@ -90,6 +90,8 @@ struct AbsArgs {
   int32_t has_stream;
   int32_t first_push;
   int32_t keep_carry;          // 0 (no_carry): partials still pending at the end of the push are dropped
+  int32_t fast;                // one stream, no local filters, no stream column, no nulls: every row is
+                               // candidate and killer (the C4 shape)
 };
 
 struct RowRd {
@@ -100,6 +102,30 @@ struct RowRd {
 };
 
 __device__ __forceinline__ uint64_t ord64(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
+
+// value range: wave shuffles, then LDS across the block's waves, then ONE atomic pair per block (a pair
+// per wave on two global words serialises in L2: measured 0.39 ms for 10M rows)
+__device__ __forceinline__ void block_minmax(uint64_t lo, uint64_t hi, unsigned long long* __restrict__ minmax) {
+  __shared__ uint64_t slo[4], shi[4];
+  for (int off = 32; off > 0; off >>= 1) {
+    uint64_t l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { slo[w] = lo; shi[w] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+      lo = slo[k] < lo ? slo[k] : lo;
+      hi = shi[k] > hi ? shi[k] : hi;
+    }
+    if (lo != ~0ull) {
+      atomicMin(&minmax[0], (unsigned long long)lo);
+      atomicMax(&minmax[1], (unsigned long long)hi);
+    }
+  }
+}
 
 // 1. roles, compared values, value range, order check
 __global__ void __launch_bounds__(256) k_abs_rows(AbsArgs a, SgCols cols, const DevDesc* __restrict__ dd,
@@ -138,16 +164,42 @@ __global__ void __launch_bounds__(256) k_abs_rows(AbsArgs a, SgCols cols, const 
       hi = o > hi ? o : hi;
     }
   }
-  // wave-reduce, one atomic pair per wave
-  for (int off = 32; off > 0; off >>= 1) {
-    uint64_t l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
-    lo = l2 < lo ? l2 : lo;
-    hi = h2 > hi ? h2 : hi;
+  block_minmax(lo, hi, minmax);
+}
+
+// 1'. the C4 shape (one stream, no local filters, no nulls): every row is candidate and killer; no VM
+// (the VM's operand stack would cost this streaming pass its occupancy)
+template <class V>
+__global__ void __launch_bounds__(256) k_abs_rows_fast(AbsArgs a, const V* __restrict__ col, const int64_t* __restrict__ ts,
+                                                       const int64_t* __restrict__ c_val, const uint8_t* __restrict__ c_vnul,
+                                                       uint8_t* __restrict__ role, int64_t* __restrict__ vals,
+                                                       unsigned long long* __restrict__ minmax,
+                                                       const int64_t* __restrict__ dlast, uint32_t* __restrict__ oflag) {
+  uint64_t lo = ~0ull, hi = 0;
+  bool bad = false;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.nt; v += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t r;
+    int64_t x = 0;
+    if (v < a.nc) {
+      r = R_CAND;
+      if (!c_vnul[v]) { r |= R_SORT; x = c_val[v]; }
+    } else {
+      const int64_t i = v - a.nc;
+      x = (int64_t)col[i];
+      r = R_CAND | R_KILL | R_SORT;
+      const int64_t t = ts[i];
+      bad |= (i > 0 && ts[i - 1] > t) || (i == 0 && !a.first_push && t < *dlast);
+    }
+    role[v] = (uint8_t)r;
+    vals[v] = x;
+    if (r & R_SORT) {
+      uint64_t o = ord64(x);
+      lo = o < lo ? o : lo;
+      hi = o > hi ? o : hi;
+    }
   }
-  if ((threadIdx.x & 63) == 0) {
-    if (lo != ~0ull) atomicMin(&minmax[0], (unsigned long long)lo);
-    if (hi != 0 || lo != ~0ull) atomicMax(&minmax[1], (unsigned long long)hi);
-  }
+  if (bad) atomicOr(oflag, 1u);
+  block_minmax(lo, hi, minmax);
 }
 
 // sort keys: value - min (order preserving) for sorted rows, a sentinel above the range for the rest
@@ -182,7 +234,13 @@ __global__ void k_abs_kill(AbsArgs a, const K* __restrict__ skeys, const uint32_
     const uint32_t v = sid[p];
     const uint8_t r = role[v];
     if ((r & (R_CAND | R_SORT)) != (R_CAND | R_SORT)) continue;
-    const uint32_t q = (p + 1 < a.nt) ? nks[a.nt - 2 - p] : NONE;   // min killer position >= p + 1
+    uint32_t q = NONE;
+    if (a.fast) {
+      for (int64_t x = p + 1; x < a.nt && skeys[x] == skeys[p]; ++x)
+        if (sid[x] >= a.nc) { q = (uint32_t)x; break; }
+    } else if (p + 1 < a.nt) {
+      q = nks[a.nt - 2 - p];   // min killer position >= p + 1
+    }
     if (q == NONE || skeys[q] != skeys[p]) continue;
     const uint32_t vq = sid[q];
     if (vts(a, ts, c_dl, vq) < vts(a, ts, c_dl, v) + a.W) dead[v] = 1;
@@ -218,13 +276,19 @@ struct AbsOut {
   int32_t sel_col[SG_MAX_SELECT], sel_type[SG_MAX_SELECT];
 };
 
-// 6. emission records and carried partials
+// 6. emission records and carried partials (e1's projected attributes read straight into the record)
+__device__ __forceinline__ int64_t abs_sel(const AbsOut& o, const SgCols& cols, int s, int64_t i, uint32_t& nm) {
+  if (!o.sel_ok[s]) { nm |= 1u << s; return 0; }
+  SgVal x = sg_read_col(cols, o.sel_col[s], o.sel_type[s], i);
+  if (x.null) { nm |= 1u << s; return 0; }
+  return sg_val_bits(x);
+}
+
 __global__ void __launch_bounds__(256) k_abs_write(AbsArgs a, AbsOut o, SgCols cols, const int64_t* __restrict__ ts,
                                                    const uint32_t* __restrict__ trig, const uint64_t* __restrict__ cnt,
                                                    const uint64_t* __restrict__ off, const int64_t* __restrict__ vals,
                                                    const uint8_t* __restrict__ role, AbsCarry cin, AbsCarry cout,
-                                                   const uint32_t* __restrict__ slot_trig, int64_t n_emit,
-                                                   char* __restrict__ out) {
+                                                   const uint32_t* __restrict__ first_slot, char* __restrict__ out) {
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.nt; v += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t c = cnt[v];
     if (!c) continue;
@@ -232,45 +296,36 @@ __global__ void __launch_bounds__(256) k_abs_write(AbsArgs a, AbsOut o, SgCols c
     const bool carried = v < a.nc;
     const int64_t i = v - a.nc;
     const int64_t d = carried ? cin.dl[v] : ts[i] + a.W;
-    int64_t sv[SG_MAX_SELECT];
-    uint32_t nm = 0;
-    for (int s = 0; s < o.n_select; ++s) {
-      if (carried) {
-        sv[s] = cin.sel[v * o.n_select + s];
-      } else if (o.sel_ok[s]) {
-        SgVal x = sg_read_col(cols, o.sel_col[s], o.sel_type[s], i);
-        sv[s] = sg_val_bits(x);
-        if (x.null) nm |= 1u << s;
-      } else {
-        sv[s] = 0;
-        nm |= 1u << s;
-      }
-    }
-    if (carried) nm = cin.snul[v];
+    uint32_t nm = carried ? cin.snul[v] : 0u;
     if (c & 0xffffffffull) {   // emitted in this push
       const uint32_t sl = (uint32_t)ofs;
       const uint32_t t = trig[v];
-      // rank within the trigger's timer pass: emissions are contiguous per trigger (arrival order)
-      int64_t lo = 0, hi = sl;
-      while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (slot_trig[mid] < t) lo = mid + 1; else hi = mid;
-      }
       int64_t* r = (int64_t*)(out + (size_t)sl * o.stride);
+      for (int s = 0; s < o.n_select; ++s) {
+        int64_t x = carried ? cin.sel[v * o.n_select + s] : abs_sel(o, cols, s, i, nm);
+        r[4 + s] = (nm >> s) & 1 ? 0 : x;
+      }
       r[0] = (int64_t)(o.index ? o.index[t] : o.base_index + t);
       r[1] = d;
-      r[2] = (int64_t)((uint64_t)(uint32_t)(sl - lo) << 32);   // key 0 | group = rank (timer phase 0)
+      // key 0 | group = rank within the trigger's timer pass (emissions are contiguous per trigger)
+      r[2] = (int64_t)((uint64_t)(sl - first_slot[sl]) << 32);
       r[3] = (int64_t)nm;
-      for (int s = 0; s < o.n_select; ++s) r[4 + s] = (nm >> s) & 1 ? 0 : sv[s];
     } else if (a.keep_carry) { // still pending: carried into the next push
       const uint32_t cs = (uint32_t)(ofs >> 32);
       cout.dl[cs] = d;
       cout.val[cs] = vals[v];
       cout.vnul[cs] = (role[v] & R_SORT) ? 0 : 1;
-      for (int s = 0; s < o.n_select; ++s) cout.sel[(int64_t)cs * o.n_select + s] = sv[s];
+      for (int s = 0; s < o.n_select; ++s)
+        cout.sel[(int64_t)cs * o.n_select + s] = carried ? cin.sel[v * o.n_select + s] : abs_sel(o, cols, s, i, nm);
       cout.snul[cs] = nm;
     }
   }
+}
+
+// first slot of each slot's trigger: segment heads, then an inclusive max-scan
+__global__ void k_abs_heads(int64_t ne, const uint32_t* __restrict__ slot_trig, uint32_t* __restrict__ head) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ne; s += (int64_t)gridDim.x * blockDim.x)
+    head[s] = (s == 0 || slot_trig[s] != slot_trig[s - 1]) ? (uint32_t)s : 0u;
 }
 
 __global__ void k_abs_slot_trig(int64_t nt, const uint64_t* __restrict__ cnt, const uint64_t* __restrict__ off,
@@ -304,6 +359,7 @@ AbsState* astate(SgHandle* h) {
 }
 
 unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 256 * 16)); }
+unsigned grid_red(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)); }
 
 template <class K>
 void sort_and_kill(SgHandle* h, const AbsArgs& a, uint64_t omin, int bits, const uint8_t* role, const int64_t* vals,
@@ -320,13 +376,16 @@ void sort_and_kill(SgHandle* h, const AbsArgs& a, uint64_t omin, int bits, const
   HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, ids, sid, (size_t)nt, 0, bits, st));
   void* tmp = h->ws.get("abs_sort_tmp", tb, st);
   HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, ids, sid, (size_t)nt, 0, bits, st));
-  uint32_t* rk = (uint32_t*)h->ws.get("abs_rk", 4 * nt, st);
-  uint32_t* nks = (uint32_t*)h->ws.get("abs_nks", 4 * nt, st);
-  hipLaunchKernelGGL(k_abs_rkill, dim3(grid_for(nt)), dim3(256), 0, st, nt, sid, role, rk);
-  tb = 0;
-  HIPCHK(rocprim::inclusive_scan(nullptr, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
-  tmp = h->ws.get("abs_scan_tmp", tb, st);
-  HIPCHK(rocprim::inclusive_scan(tmp, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
+  uint32_t* nks = nullptr;
+  if (!a.fast) {
+    uint32_t* rk = (uint32_t*)h->ws.get("abs_rk", 4 * nt, st);
+    nks = (uint32_t*)h->ws.get("abs_nks", 4 * nt, st);
+    hipLaunchKernelGGL(k_abs_rkill, dim3(grid_for(nt)), dim3(256), 0, st, nt, sid, role, rk);
+    tb = 0;
+    HIPCHK(rocprim::inclusive_scan(nullptr, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
+    tmp = h->ws.get("abs_scan_tmp", tb, st);
+    HIPCHK(rocprim::inclusive_scan(tmp, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
+  }
   hipLaunchKernelGGL((k_abs_kill<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, role, nks, ts, c_dl, dead);
   HIPCHK(hipGetLastError());
 }
@@ -372,6 +431,8 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   a.has_stream = bv.stream ? 1 : 0;
   a.first_push = h->pushes == 0 || h->opt.no_carry ? 1 : 0;
   a.keep_carry = h->opt.no_carry ? 0 : 1;
+  a.fast = (a.s_a == 0 && a.s_b == 0 && a.col_a == a.col_b && !bv.stream && a.prog_a_len == 0 && a.prog_b_len == 0 &&
+            !bv.cols.nul[a.col_a] && (a.type == SG_T_LONG || a.type == SG_T_INT || a.type == SG_T_STRING)) ? 1 : 0;
   const int64_t nt = a.nt;
   h->split_out = 0;
   h->extra_marks = 0;
@@ -382,8 +443,16 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   uint8_t* dead = (uint8_t*)h->ws.get("abs_dead", nt, st);
   hipLaunchKernelGGL(k_abs_init, dim3(1), dim3(64), 0, st, (unsigned long long*)as->dminmax, as->dflag);
   HIPCHK(hipMemsetAsync(dead, 0, nt, st));
-  if (nt > 0)
-    hipLaunchKernelGGL(k_abs_rows, dim3(grid_for(nt)), dim3(256), 0, st, a, bv.cols, h->ddesc, bv.ts, bv.stream,
+  if (nt > 0 && a.fast && a.type == SG_T_LONG)
+    hipLaunchKernelGGL((k_abs_rows_fast<int64_t>), dim3(grid_red(nt)), dim3(256), 0, st, a,
+                       (const int64_t*)bv.cols.col[a.col_a], bv.ts, cin.val, cin.vnul, role, vals,
+                       (unsigned long long*)as->dminmax, as->dlast, as->dflag);
+  else if (nt > 0 && a.fast)
+    hipLaunchKernelGGL((k_abs_rows_fast<int32_t>), dim3(grid_red(nt)), dim3(256), 0, st, a,
+                       (const int32_t*)bv.cols.col[a.col_a], bv.ts, cin.val, cin.vnul, role, vals,
+                       (unsigned long long*)as->dminmax, as->dlast, as->dflag);
+  else if (nt > 0)
+    hipLaunchKernelGGL(k_abs_rows, dim3(grid_red(nt)), dim3(256), 0, st, a, bv.cols, h->ddesc, bv.ts, bv.stream,
                        cin.val, cin.vnul, role, vals, (unsigned long long*)as->dminmax, as->dlast, as->dflag);
   HIPCHK(hipGetLastError());
   h->mark(1);
@@ -438,11 +507,19 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   char* dst = rec + (size_t)h->out.n * o.stride;
   if (!h->opt.no_carry) cout.reserve(n_carry, d.n_select);
   uint32_t* slot_trig = (uint32_t*)h->ws.get("abs_slot_trig", 4 * (n_emit + 1), st);
-  if (nt > 0) {
+  uint32_t* first_slot = (uint32_t*)h->ws.get("abs_first_slot", 4 * (n_emit + 1), st);
+  if (n_emit > 0) {
     hipLaunchKernelGGL(k_abs_slot_trig, dim3(grid_for(nt)), dim3(256), 0, st, nt, cnt, off, trig, slot_trig);
-    hipLaunchKernelGGL(k_abs_write, dim3(grid_for(nt)), dim3(256), 0, st, a, o, bv.cols, bv.ts, trig, cnt, off, vals,
-                       role, cin, cout, slot_trig, n_emit, dst);
+    uint32_t* head = (uint32_t*)h->ws.get("abs_head", 4 * (n_emit + 1), st);
+    hipLaunchKernelGGL(k_abs_heads, dim3(grid_for(n_emit)), dim3(256), 0, st, n_emit, slot_trig, head);
+    size_t tb2 = 0;
+    HIPCHK(rocprim::inclusive_scan(nullptr, tb2, head, first_slot, (size_t)n_emit, rocprim::maximum<uint32_t>(), st));
+    void* tmp2 = h->ws.get("abs_head_scan_tmp", tb2, st);
+    HIPCHK(rocprim::inclusive_scan(tmp2, tb2, head, first_slot, (size_t)n_emit, rocprim::maximum<uint32_t>(), st));
   }
+  if (nt > 0)
+    hipLaunchKernelGGL(k_abs_write, dim3(grid_for(nt)), dim3(256), 0, st, a, o, bv.cols, bv.ts, trig, cnt, off, vals,
+                       role, cin, cout, first_slot, dst);
   if (n > 0) hipLaunchKernelGGL(k_abs_last, dim3(1), dim3(64), 0, st, n, bv.ts, as->dlast);
   HIPCHK(hipGetLastError());
   h->mark(4);

@@ -162,3 +162,30 @@ def test_gpu_c4_full_size_vs_numpy():
     b = c4_batch(n, synth.CONFIGS["C4"][2])
     got = run_engine(gpu(), synth.QUERIES["C4"], [b])
     check_np(b, got)
+
+
+def _no_stream(b):
+    return Batch(b.n, b.base_index, b.ts, None, b.key, b.cols, b.nulls)
+
+
+@pytest.mark.gpu
+def test_gpu_c4_fast_path_full_size_vs_numpy():
+    """No stream column (every row is S): the role pass reads the id column directly and the kill pass steps
+    to the next sorted row (absent.hip `fast`)."""
+    n = synth.CONFIGS["C4"][1]
+    b = c4_batch(n, synth.CONFIGS["C4"][2], tick=False)
+    got = run_engine(gpu(), synth.QUERIES["C4"], [_no_stream(b)])
+    check_np(b, got)
+
+
+@pytest.mark.gpu
+def test_gpu_c4_fast_path_multi_push_vs_oracle():
+    b = c4_batch(30_000, 2_000, tick=False)
+    want = run_engine(OracleEngine, synth.QUERIES["C4"], [b])
+    parts, lo = [], 0
+    for hi in (4_000, 4_001, 17_000, b.n):
+        parts.append(Batch(hi - lo, lo, b.ts[lo:hi], None, b.key[lo:hi], [c[lo:hi] for c in b.cols], [None] * 3))
+        lo = hi
+    got = run_engine(gpu(), synth.QUERIES["C4"], parts)
+    assert len(want) > 0
+    assert_same(got, want)
