@@ -432,8 +432,10 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
       }
       const double per_key = (double)n / (double)std::max<uint32_t>(kb, 1);
       const double hz = rule.kind == 2 ? (double)rule.events : per_key * (double)rule.within / (double)span;
-      const int64_t target_units = 256 * 8 * 64;
-      const int64_t mem_units = std::max<int64_t>(1, ((int64_t)8 << 30) / ((int64_t)gs->geo.key_words * 4));
+      // (measured on C3b/C3c: 131k -> 524k units took 372 -> 245 ms and 3150 -> 2347 ms per 100M events;
+      // 1M units gained nothing more)
+      const int64_t target_units = 256 * 32 * 64;
+      const int64_t mem_units = std::max<int64_t>(1, ((int64_t)24 << 30) / ((int64_t)gs->geo.key_words * 4));
       int64_t r = std::max<int64_t>({(int64_t)(4.0 * hz) + 1, 32, (n + target_units - 1) / target_units,
                                      (n + mem_units - 1) / mem_units});
       R = (uint32_t)std::min<int64_t>(r, 1 << 30);
