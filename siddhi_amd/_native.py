@@ -205,6 +205,10 @@ class Handle:
     def push(self, b: sg_batch):
         self.check(self.lib.sg_push(self.h, ct.byref(b)))
 
+    def advance_time(self, now: int, trigger_index: int):
+        """Heartbeat: fire the timers due at `now` (sg_advance_time; one clock-only row)."""
+        self.check(self.lib.sg_advance_time(self.h, int(now), int(trigger_index)))
+
     def pending(self) -> int:
         n = I64()
         self.check(self.lib.sg_pending(self.h, ct.byref(n)))

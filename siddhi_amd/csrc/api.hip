@@ -149,11 +149,31 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
   });
 }
 
+// A heartbeat is one clock-only row (stream -1): timers whose time has come fire in front of it, exactly as
+// for an event row (TimestampGeneratorImpl.setCurrentTimestamp runs before the row is dispatched); no
+// state consumes it.  trigger_index is its global event index (the sequence number the host assigned).
 int sg_advance_time(sg_handle* hh, int64_t now, uint64_t trigger_index) {
   if (!hh) return SG_EINVAL;
-  (void)now;
-  (void)trigger_index;
-  return SG_OK;
+  const sg_nfa_desc& d = hh->h.desc;
+  int64_t ts = now;
+  int32_t stream = -1, key = -1;
+  uint64_t index = trigger_index;
+  int64_t zero[SG_MAX_COLS] = {};
+  const void* cols[SG_MAX_COLS];
+  for (int c = 0; c < SG_MAX_COLS; ++c) cols[c] = &zero[c];
+  sg_batch b;
+  memset(&b, 0, sizeof(b));
+  b.n = 1;
+  b.base_index = trigger_index;
+  b.ts = &ts;
+  b.stream = &stream;
+  b.key = &key;
+  b.index = &index;
+  b.cols = cols;
+  b.on_device = 0;
+  b.key_bound = 0;
+  (void)d;
+  return sg_push(hh, &b);
 }
 
 int sg_pending(sg_handle* hh, int64_t* n) {

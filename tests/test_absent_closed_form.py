@@ -189,3 +189,23 @@ def test_gpu_c4_fast_path_multi_push_vs_oracle():
     got = run_engine(gpu(), synth.QUERIES["C4"], parts)
     assert len(want) > 0
     assert_same(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("general", [False, True])
+def test_gpu_advance_time_heartbeat(general):
+    """sg_advance_time (a heartbeat with no event) fires the pending timers exactly like a clock-only row."""
+    from siddhi_amd._native import GpuEngine
+    from parity_util import context
+    b = c4_batch(8_000, 3_000, tick=False)
+    hb_ts = int(b.ts[-1]) + W + 1
+    ref = Batch(b.n + 1, 0, np.append(b.ts, hb_ts), np.append(b.stream, np.int32(-1)).astype(np.int32),
+                np.zeros(b.n + 1, np.int32), [np.append(c, 0).astype(c.dtype) for c in b.cols], [None] * 3)
+    want = run_engine(OracleEngine, synth.QUERIES["C4"], [ref])
+    eng = GpuEngine(context(synth.QUERIES["C4"]), force_general=general, pool=16384 if general else 0)
+    eng.push(b)
+    eng.handle.advance_time(hb_ts, b.n)
+    got = eng.fetch()
+    eng.close()
+    assert len(want) > 0 and int(want.trigger[-1]) == b.n
+    assert_same(got, want)
