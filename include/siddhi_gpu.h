@@ -136,7 +136,9 @@ typedef struct sg_options {
   int32_t chunk_rows;       /* general engine: a key's rows are cut into units of this many rows, each unit
                                rebuilding its state by replaying the rows inside the query's horizon before
                                it (0 = chosen per push, -1 = one unit per key) */
-  int32_t reserved[4];
+  int32_t walker_only;      /* closed form, unpartitioned streams: 1 = always the chunked walker instead of the
+                               per-candidate search (testing both paths) */
+  int32_t reserved[3];
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)

@@ -54,7 +54,7 @@ class sg_nfa_desc(ct.Structure):
 class sg_options(ct.Structure):
     _fields_ = [("max_batch", I64), ("pool_partials", I32), ("pool_events", I32), ("pool_chain", I32),
                 ("list_cap", I32), ("force_general", I32), ("no_carry", I32), ("ring_cap", I32),
-                ("chunk_rows", I32), ("reserved", I32 * 4)]
+                ("chunk_rows", I32), ("walker_only", I32), ("reserved", I32 * 3)]
 
 
 class sg_batch(ct.Structure):
@@ -275,7 +275,7 @@ class GpuEngine:
     """Engine interface (see siddhi_amd/runtime.py) on the MI355X kernels."""
 
     def __init__(self, ctx: L.QueryContext, device: int = 0, force_general: bool = False, pool: int = 0,
-                 no_carry: bool = False, ring_cap: int = 0, chunk_rows: int = 0):
+                 no_carry: bool = False, ring_cap: int = 0, chunk_rows: int = 0, walker_only: bool = False):
         self.ctx = ctx
         self.nfa = L.lower(ctx)
         self.desc = build_desc(self.nfa)
@@ -284,6 +284,7 @@ class GpuEngine:
         opts.no_carry = 1 if no_carry else 0
         opts.ring_cap = ring_cap
         opts.chunk_rows = chunk_rows
+        opts.walker_only = 1 if walker_only else 0
         if pool:
             opts.pool_partials = opts.pool_events = opts.pool_chain = opts.list_cap = pool
         self.handle = Handle(self.desc, device, opts)

@@ -1184,6 +1184,224 @@ static void launch_walk_t(int op, dim3 g, dim3 b, size_t lds, hipStream_t st, co
 
 // One push through the closed-form pipeline with walker records of format N (narrow / wide).  Returns false
 // (having changed no state) when narrow records cannot represent the push (time span beyond 2^31 ms).
+// ---------------------------------------------------------------------------------------------
+// Unpartitioned streams: per-candidate search instead of the walker.  One key means the walker's units are
+// time chunks of a single row sequence, each replaying a whole `within` window before it: few, long,
+// latency-bound lanes (C1: 1000-row windows).  Every partial of this shape is independent:
+// partial i completes at the first later consumer j with x_j OP x_i, unless the oldest-first expiry
+// (StreamPreStateProcessor.isExpired, C/query/input/stream/state/StreamPreStateProcessor.java:102-113) drops
+// it first, i.e. iff ts_j - ts_i <= T.  So one lane per candidate scans forward (lanes of a wave read
+// neighbouring rows: coalesced), matches become (trigger j, partial i) pairs, and a stable radix sort by j
+// of the pairs compacted in i order yields the reference's delivery order (trigger, then pending order).
+// A search longer than NGE_MAX_SCAN rows sends the push to the walker (bounded work per lane).
+static const uint32_t NGE_MAX_SCAN = 4096;
+static const uint32_t NGE_NONE = 0xffffffffu;
+
+template <class T, int OP>
+__global__ void __launch_bounds__(256) k_nge(Virt v, int64_t nt, int64_t within, int op, uint32_t* __restrict__ mj,
+                                             uint32_t* __restrict__ mflag, uint32_t* __restrict__ cnt,
+                                             uint32_t* __restrict__ st_flags) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nt; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t f = v_flags(v, (uint32_t)p);
+    const int64_t tp = v_ts(v, (uint32_t)p);
+    if (p + 1 < nt && v_ts(v, (uint32_t)(p + 1)) < tp) atomicOr(&st_flags[0], 1u);   // order check
+    uint32_t j = NGE_NONE;
+    if (f & F_CAND) {
+      const T xp = v_val<T>(v, (uint32_t)p, true);
+      if (!is_nan_val<T>(xp)) {
+        uint32_t steps = 0;
+        for (int64_t q = p + 1; q < nt; ++q) {
+          if (v_ts(v, (uint32_t)q) - tp > within) break;              // expired before q
+          if (++steps > NGE_MAX_SCAN) { atomicOr(&st_flags[1], 1u); break; }
+          if (!(v_flags(v, (uint32_t)q) & F_CONS)) continue;
+          const T xq = v_val<T>(v, (uint32_t)q, false);
+          if (!is_nan_val<T>(xq) && cmp_sel<OP, T>(op, xq, xp)) {
+            if (q >= v.nc) j = (uint32_t)q;                               // (carried triggers were emitted before)
+            break;
+          }
+        }
+      }
+    }
+    mj[p] = j;
+    mflag[p] = j != NGE_NONE ? 1u : 0u;
+    if (j != NGE_NONE) atomicAdd(&cnt[j - v.nc], 1u);
+  }
+}
+
+static __global__ void k_nge_pairs(int64_t nt, uint32_t nc, const uint32_t* __restrict__ mj, const uint32_t* __restrict__ mpos,
+                            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nt; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = mj[p];
+    if (j == NGE_NONE) continue;
+    keys[mpos[p]] = j - nc;
+    vals[mpos[p]] = (uint32_t)p;
+  }
+}
+
+template <class T>
+__global__ void k_nge_mrec(Virt v, int64_t total, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
+                           MRec* __restrict__ mrec) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = svals[s];
+    MRec m;
+    m.r1 = p;
+    m.r2 = skeys[s] + (uint32_t)v.nc;
+    m.v1 = val_bits<T>(v_val<T>(v, p, true));
+    m.p1 = v.pcol ? v_payload(v, p) : 0;
+    mrec[s] = m;
+  }
+}
+
+// rows still inside `within` of the last row survive into the next push (one key: a suffix)
+static __global__ void k_nge_carry_start(Virt v, int64_t nt, int64_t within, uint32_t* __restrict__ q0) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t tmin = v_ts(v, (uint32_t)(nt - 1)) - within;
+  int64_t lo = 0, hi = nt;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (v_ts(v, (uint32_t)mid) < tmin) lo = mid + 1; else hi = mid;
+  }
+  *q0 = (uint32_t)lo;
+}
+
+static __global__ void k_nge_carry_copy(Virt v, uint32_t q0, uint32_t ncar, int n_cols, const int32_t* __restrict__ widths,
+                                 SgCols bc, SgCols cc, CarryBufs dst) {
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ncar; d += gridDim.x * blockDim.x) {
+    const uint32_t r = q0 + d;
+    dst.ts[d] = v_ts(v, r);
+    dst.key[d] = 0;
+    dst.flags[d] = (uint8_t)v_flags(v, r);
+    const SgCols& s = r < v.nc ? cc : bc;
+    const uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
+    for (int c = 0; c < n_cols; ++c) {
+      if (!s.col[c]) continue;
+      if (widths[c] == 8) ((int64_t*)dst.col[c])[d] = ((const int64_t*)s.col[c])[rr];
+      else ((int32_t*)dst.col[c])[d] = ((const int32_t*)s.col[c])[rr];
+      dst.nul[c][d] = s.nul[c] ? s.nul[c][rr] : 0;
+    }
+  }
+}
+
+template <class T>
+static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, const PushPlan& plan, const Virt& v,
+                    const SgCols& cc, int op, EveryNextState* es) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  const int64_t nt = nc + n;
+  const int b_state = d.shape_args[1];
+  auto grid = [](int64_t m) { return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 256 * 16))); };
+  uint32_t* mj = (uint32_t*)h->ws.get("nge_mj", 4 * nt, st);
+  uint32_t* mflag = (uint32_t*)h->ws.get("nge_mflag", 4 * (nt + 1), st);
+  uint32_t* mpos = (uint32_t*)h->ws.get("nge_mpos", 4 * (nt + 1), st);
+  uint32_t* cnt = (uint32_t*)h->ws.get("cnt", sizeof(uint32_t) * (n + 1), st);
+  uint32_t* off = (uint32_t*)h->ws.get("off", sizeof(uint32_t) * (n + 1), st);
+  uint32_t* stf = (uint32_t*)h->ws.get("nge_flags", 8, st);
+  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
+  HIPCHK(hipMemsetAsync(mflag + nt, 0, 4, st));
+  HIPCHK(hipMemsetAsync(stf, 0, 8, st));
+  switch (op) {
+    case 2: hipLaunchKernelGGL((k_nge<T, 2>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
+    case 3: hipLaunchKernelGGL((k_nge<T, 3>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
+    case 4: hipLaunchKernelGGL((k_nge<T, 4>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
+    default: hipLaunchKernelGGL((k_nge<T, 5>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
+  }
+  HIPCHK(hipGetLastError());
+  h->mark(2);
+  size_t tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, mflag, mpos, (uint32_t)0, (size_t)nt + 1, rocprim::plus<uint32_t>(), st));
+  void* tmp = h->ws.get("nge_scan_tmp", tb, st);
+  HIPCHK(rocprim::exclusive_scan(tmp, tb, mflag, mpos, (uint32_t)0, (size_t)nt + 1, rocprim::plus<uint32_t>(), st));
+  uint32_t hflags[2] = {0, 0};
+  uint32_t total = 0;
+  HIPCHK(hipMemcpyAsync(hflags, stf, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&total, mpos + nt, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (hflags[0]) throw SgError(SG_EORDER, "closed-form kernel requires non-decreasing timestamps per key");
+  if (hflags[1]) return false;   // a search outgrew NGE_MAX_SCAN: the walker takes this push
+  tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+  tmp = h->ws.get("scan_tmp", tb, st);
+  HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+  MRec* mrec = nullptr;
+  if (total) {
+    uint32_t* keys = (uint32_t*)h->ws.get("nge_keys", 4 * total, st);
+    uint32_t* vals = (uint32_t*)h->ws.get("nge_vals", 4 * total, st);
+    uint32_t* skeys = (uint32_t*)h->ws.get("nge_skeys", 4 * total, st);
+    uint32_t* svals = (uint32_t*)h->ws.get("nge_svals", 4 * total, st);
+    hipLaunchKernelGGL(k_nge_pairs, grid(nt), dim3(256), 0, st, nt, (uint32_t)nc, mj, mpos, keys, vals);
+    int end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) <= (uint64_t)n) ++end_bit;
+    tb = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, vals, svals, (size_t)total, 0, end_bit, st));
+    tmp = h->ws.get("nge_sort_tmp", tb, st);
+    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, vals, svals, (size_t)total, 0, end_bit, st));
+    mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * total, st);
+    hipLaunchKernelGGL((k_nge_mrec<T>), grid(total), dim3(256), 0, st, v, (int64_t)total, skeys, svals, mrec);
+    HIPCHK(hipGetLastError());
+  }
+  h->mark(3);
+  h->extra_marks = 0;
+  h->split_out = 1;
+  WalkArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  wa.partitioned = 0;
+  wa.base_index = bv.base_index;
+  wa.index = bv.index;
+  const int rb = d.recv_of_stream[d.states[b_state].stream];
+  wa.multi = d.receivers[rb].multi;
+  if (wa.multi) {
+    const sg_receiver_desc& r = d.receivers[rb];
+    for (int q = 0; q < r.n; ++q)
+      if (r.pres[r.n - 1 - q] == b_state) wa.b_slot = q;   // eventSequence = reversed init order
+  }
+  wa.n_select = d.n_select;
+  wa.stride = 32 + 8 * d.n_select;
+  char* out = h->out.reserve(total, d.n_select, st);
+  wa.out_base = h->out.n;
+  h->mark(5);
+  if (total) {
+    hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)), dim3(256), (size_t)256 * wa.stride, st,
+                       wa, v, plan.pp, bv.cols, cc, mrec, off, (int64_t)total, out);
+    HIPCHK(hipGetLastError());
+  }
+  h->out.n += total;
+  h->mark(4);
+  // carry: the suffix inside `within` of the last row
+  CarrySet& cs = es->carry[es->cur];
+  if (!h->opt.no_carry && nt > 0) {
+    uint32_t* q0d = (uint32_t*)h->ws.get("nge_q0", 4, st);
+    hipLaunchKernelGGL(k_nge_carry_start, dim3(1), dim3(64), 0, st, v, nt, d.within, q0d);
+    uint32_t q0 = 0;
+    HIPCHK(hipMemcpyAsync(&q0, q0d, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint32_t ncar = (uint32_t)(nt - q0);
+    CarrySet& nx = es->carry[es->cur ^ 1];
+    nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
+    int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
+    int32_t hw[SG_MAX_COLS];
+    for (int c = 0; c < SG_MAX_COLS; ++c)
+      hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
+    HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
+    CarryBufs cb;
+    memset(&cb, 0, sizeof(cb));
+    cb.ts = nx.ts;
+    cb.key = nx.key;
+    cb.flags = nx.flags;
+    for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
+    if (ncar)
+      hipLaunchKernelGGL(k_nge_carry_copy, grid(ncar), dim3(256), 0, st, v, q0, ncar, d.n_cols, widths, bv.cols, cc, cb);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    nx.n = ncar;
+    cs.n = 0;
+    es->cur ^= 1;
+  }
+  h->last_events = n;
+  h->last_matches = total;
+  h->last_spilled = 0;
+  return true;
+}
+
 template <class T, bool N>
 static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan plan) {
   const sg_nfa_desc& d = h->desc;
@@ -1300,6 +1518,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   SgCols cc;
   memset(&cc, 0, sizeof(cc));
   for (int c = 0; c < d.n_cols; ++c) { cc.col[c] = cs.col[c]; cc.nul[c] = cs.nul[c]; }
+  if (!d.partitioned && !h->opt.walker_only && run_nge<T>(h, bv, n, nc, plan, v, cc, op, es)) return true;
 
   typedef WRec<T, N> R;
   Src<T, N> src;

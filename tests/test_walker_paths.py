@@ -73,10 +73,11 @@ class _Spy:
     """GpuEngine wrapper recording how many units spilled to HBM lists per push."""
     spilled = []
     ring_cap = 0
+    walker_only = False
 
     def __init__(self, ctx):
         from siddhi_amd._native import GpuEngine
-        self.e = GpuEngine(ctx, ring_cap=_Spy.ring_cap)
+        self.e = GpuEngine(ctx, ring_cap=_Spy.ring_cap, walker_only=_Spy.walker_only)
 
     def push(self, b):
         self.e.push(b)
@@ -89,11 +90,12 @@ class _Spy:
         self.e.close()
 
 
-def check(app, batches, min_matches=1, expect_spill=None, ring_cap=0):
+def check(app, batches, min_matches=1, expect_spill=None, ring_cap=0, walker_only=False):
     assert shape_of(app) == L.SHAPE_EVERY_NEXT_CMP, "case must exercise the closed-form walker"
     want = run_engine(OracleEngine, app, batches)
     _Spy.spilled = []
     _Spy.ring_cap = ring_cap
+    _Spy.walker_only = walker_only
     got = run_engine(_Spy, app, batches)
     assert len(want) >= min_matches
     assert_same(got, want)
@@ -122,11 +124,12 @@ PRICE_TIES = {"price": lambda r, n: 20 + r.integers(0, 12, n)}          # few di
 
 
 @pytest.mark.parametrize("op", [">", ">=", "<", "<="])
-@pytest.mark.parametrize("part", [True, False])
-def test_compare_operators(op, part):
+@pytest.mark.parametrize("part,walker_only", [(True, False), (False, False), (False, True)])
+def test_compare_operators(op, part, walker_only):
+    """Unpartitioned streams run the per-candidate search by default; walker_only keeps the walker covered."""
     app = (q_part if part else q_flat)(f"price {op} e1.price")
     b = make_batch(app, 60_000, seed=1, keys=200 if part else 1, rate=20, values=PRICE_TIES)
-    check(app, [b])
+    check(app, [b], walker_only=walker_only)
 
 
 @pytest.mark.parametrize("typ,attr", [("int", "v"), ("long", "v"), ("double", "v")])
@@ -145,7 +148,7 @@ def test_stack_overflow_unpartitioned():
     falling = lambda r, n: np.where(np.arange(n) % 200 < 150, 40.0 - (np.arange(n) % 200) * 0.1, r.random(n) * 40)
     app = q_flat("price > e1.price")
     b = make_batch(app, n, seed=3, rate=50, values={"price": falling})
-    check(app, [b], expect_spill=True, ring_cap=16)
+    check(app, [b], expect_spill=True, ring_cap=16, walker_only=True)
 
 
 def test_stack_overflow_partitioned():
@@ -230,3 +233,31 @@ def test_wide_payload_in_later_push():
                    values={"price": lambda r, n: r.random(n) * 40,
                            "id": lambda r, n: np.where(np.arange(n) < 30_000, np.arange(n), (1 << 35) + np.arange(n))})
     check(app, split(b, [30_000]))
+
+
+# ---- unpartitioned streams: per-candidate search (engine_impl.h k_nge) and its fallback to the walker
+
+@pytest.mark.parametrize("cond", ["price > e1.price", "price >= e1.price and volume > 400", "price < e1.price"])
+@pytest.mark.parametrize("walker_only", [False, True])
+def test_unpartitioned_multi_push(cond, walker_only):
+    app = q_flat(cond, sel="e1.id as i1, e2.id as i2, e1.volume as v1, e2.price as p2")
+    b = make_batch(app, 60_000, seed=21, rate=20, values=PRICE_TIES, null_frac={"volume": 0.05})
+    check(app, split(b, [1, 15_000, 15_001, 41_000]), walker_only=walker_only)
+
+
+def test_unpartitioned_two_streams():
+    app = ("define stream A (id long, symbol string, price float); "
+           "define stream B (id long, symbol string, price float); "
+           "@info(name='q') from every e1=A[price>20] -> e2=B[price>e1.price] within 1 sec "
+           "select e1.id as i1, e2.id as i2, e1.price as p1, e2.price as p2 insert into M;")
+    b = make_batch(app, 60_000, seed=22, rate=20, streams=[0, 1], values={"price": lambda r, n: r.random(n) * 40})
+    check(app, split(b, [30_000]))
+
+
+def test_unpartitioned_search_longer_than_limit():
+    """A falling run longer than the search limit (4096 rows) inside one window: the push goes to the walker."""
+    n = 12_000
+    falling = lambda r, n: np.where(np.arange(n) < 6_000, 40.0 - np.arange(n) * 0.003, r.random(n) * 40)
+    app = q_flat("price > e1.price", within="1 hour")
+    b = make_batch(app, n, seed=23, rate=10, values={"price": falling})
+    check(app, [b])
