@@ -1197,10 +1197,31 @@ static void launch_walk_t(int op, dim3 g, dim3 b, size_t lds, hipStream_t st, co
 static const uint32_t NGE_MAX_SCAN = 4096;
 static const uint32_t NGE_NONE = 0xffffffffu;
 
+// per 64-row block of virtual rows: the most completing consumer value (max for > >=, min for < <=) and
+// whether the block has a live consumer at all -- lets a search skip blocks that cannot complete it
+template <class T, int OP>
+__global__ void k_nge_blocks(Virt v, int64_t nt, T* __restrict__ best, uint8_t* __restrict__ has) {
+  const int64_t nb = (nt + 63) >> 6;
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (int64_t)gridDim.x * blockDim.x) {
+    T m{};
+    bool any = false;
+    for (int64_t q = b << 6, e = (q + 64 < nt ? q + 64 : nt); q < e; ++q) {
+      if (!(v_flags(v, (uint32_t)q) & F_CONS)) continue;
+      const T x = v_val<T>(v, (uint32_t)q, false);
+      if (is_nan_val<T>(x)) continue;
+      if (!any || ((OP == 2 || OP == 3) ? x > m : x < m)) m = x;
+      any = true;
+    }
+    best[b] = m;
+    has[b] = any ? 1 : 0;
+  }
+}
+
 template <class T, int OP>
 __global__ void __launch_bounds__(256) k_nge(Virt v, int64_t nt, int64_t within, int op, uint32_t* __restrict__ mj,
                                              uint32_t* __restrict__ mflag, uint32_t* __restrict__ cnt,
-                                             uint32_t* __restrict__ st_flags) {
+                                             uint32_t* __restrict__ st_flags, const T* __restrict__ best,
+                                             const uint8_t* __restrict__ has) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nt; p += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t f = v_flags(v, (uint32_t)p);
     const int64_t tp = v_ts(v, (uint32_t)p);
@@ -1210,15 +1231,23 @@ __global__ void __launch_bounds__(256) k_nge(Virt v, int64_t nt, int64_t within,
       const T xp = v_val<T>(v, (uint32_t)p, true);
       if (!is_nan_val<T>(xp)) {
         uint32_t steps = 0;
-        for (int64_t q = p + 1; q < nt; ++q) {
-          if (v_ts(v, (uint32_t)q) - tp > within) break;              // expired before q
+        int64_t q = p + 1;
+        while (q < nt) {
           if (++steps > NGE_MAX_SCAN) { atomicOr(&st_flags[1], 1u); break; }
-          if (!(v_flags(v, (uint32_t)q) & F_CONS)) continue;
-          const T xq = v_val<T>(v, (uint32_t)q, false);
-          if (!is_nan_val<T>(xq) && cmp_sel<OP, T>(op, xq, xp)) {
-            if (q >= v.nc) j = (uint32_t)q;                               // (carried triggers were emitted before)
-            break;
+          if ((q & 63) == 0 && q + 64 <= nt && !(has[q >> 6] && cmp_sel<OP, T>(op, best[q >> 6], xp)) &&
+              v_ts(v, (uint32_t)(q + 63)) - tp <= within) {
+            q += 64;                                                       // nothing in this block completes i
+            continue;
           }
+          if (v_ts(v, (uint32_t)q) - tp > within) break;                  // expired before q
+          if (v_flags(v, (uint32_t)q) & F_CONS) {
+            const T xq = v_val<T>(v, (uint32_t)q, false);
+            if (!is_nan_val<T>(xq) && cmp_sel<OP, T>(op, xq, xp)) {
+              if (q >= v.nc) j = (uint32_t)q;                             // (carried triggers were emitted before)
+              break;
+            }
+          }
+          ++q;
         }
       }
     }
@@ -1299,12 +1328,19 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
   HIPCHK(hipMemsetAsync(mflag + nt, 0, 4, st));
   HIPCHK(hipMemsetAsync(stf, 0, 8, st));
+  const int64_t nb = (nt + 63) >> 6;
+  T* best = (T*)h->ws.get("nge_best", sizeof(T) * (nb + 1), st);
+  uint8_t* has = (uint8_t*)h->ws.get("nge_has", nb + 1, st);
+#define SG_NGE_LAUNCH(OPV)                                                                                       \
+  hipLaunchKernelGGL((k_nge_blocks<T, OPV>), grid(nb), dim3(256), 0, st, v, nt, best, has);                     \
+  hipLaunchKernelGGL((k_nge<T, OPV>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf, best, has)
   switch (op) {
-    case 2: hipLaunchKernelGGL((k_nge<T, 2>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
-    case 3: hipLaunchKernelGGL((k_nge<T, 3>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
-    case 4: hipLaunchKernelGGL((k_nge<T, 4>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
-    default: hipLaunchKernelGGL((k_nge<T, 5>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf); break;
+    case 2: SG_NGE_LAUNCH(2); break;
+    case 3: SG_NGE_LAUNCH(3); break;
+    case 4: SG_NGE_LAUNCH(4); break;
+    default: SG_NGE_LAUNCH(5); break;
   }
+#undef SG_NGE_LAUNCH
   HIPCHK(hipGetLastError());
   h->mark(2);
   size_t tb = 0;
