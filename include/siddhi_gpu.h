@@ -23,6 +23,15 @@
  *   sg_poll          QuerySelector.process -> OutputRateLimiter.sendToCallBacks
  *                    (C/query/selector/QuerySelector.java:76-163, C/query/output/ratelimit/OutputRateLimiter.java:61-100):
  *                    projected matches in the reference's delivery order.
+ *   sg_snapshot      SiddhiAppRuntime.snapshot (C/SiddhiAppRuntime.java:613-623) -> SnapshotService.fullSnapshot
+ *                    (C/util/snapshot/SnapshotService.java:97-157) for this query's Snapshotables: the pending /
+ *                    newAndEvery lists of every pre-state processor (StreamPreStateProcessor.currentState,
+ *                    C/query/input/stream/state/StreamPreStateProcessor.java:352-359), the scheduler's
+ *                    ToNotifyQueue (C/util/Scheduler.java:147-152) and every partition clone's copy of them
+ *                    (C/partition/PartitionRuntime.java:342-356).
+ *   sg_restore       SiddhiAppRuntime.restore (C/SiddhiAppRuntime.java:625-635) -> SnapshotService.restore
+ *                    (:271-345) / restoreState of the same objects (StreamPreStateProcessor.java:361-367,
+ *                    Scheduler.java:154-160).
  *   sg_close         SiddhiAppRuntime.shutdown for the query's state.
  * No exceptions cross the ABI: every call returns SG_OK or a negative status; sg_last_error() explains.
  */
@@ -200,6 +209,13 @@ int sg_flush(sg_handle* h);             /* wait for all work on the handle's str
 int sg_reset(sg_handle* h);             /* forget all per-key state (fresh runtime) */
 int sg_set_stream(sg_handle* h, void* hip_stream);   /* launch on a caller-owned hipStream_t */
 int sg_get_timing(sg_handle* h, sg_timing* t);
+/* Serialise the per-key state (partial matches, carried rows, timer queues) into buf; *size receives the
+ * blob size (buf == NULL or cap < size: size query only, nothing copied).  SG_EINVAL while matches are
+ * pending (poll or discard them first: the reference has delivered them before persist() can run). */
+int sg_snapshot(sg_handle* h, void* buf, size_t cap, size_t* size);
+/* Replace the handle's state by a blob from sg_snapshot of a handle opened with the same query and
+ * options (SG_EINVAL otherwise); pending matches are dropped.  On error call sg_reset before reuse. */
+int sg_restore(sg_handle* h, const void* buf, size_t size);
 int sg_close(sg_handle* h);
 const char* sg_last_error(const sg_handle* h);
 const char* sg_version(void);

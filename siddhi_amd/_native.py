@@ -17,7 +17,8 @@ SG_MAX_STATES, SG_MAX_STREAMS, SG_MAX_SELECT, SG_MAX_RET, SG_MAX_COLS, SG_MAX_CO
 SG_ABI_VERSION = 1
 
 SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
-           "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version"]
+           "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version",
+           "sg_snapshot", "sg_restore"]
 
 I32, I64, U64 = ct.c_int32, ct.c_int64, ct.c_uint64
 
@@ -108,6 +109,8 @@ def load_library(path: str = LIB_PATH):
         lib.sg_set_stream.argtypes = [P, P]
         lib.sg_get_timing.argtypes = [P, P]
         lib.sg_close.argtypes = [P]
+        lib.sg_snapshot.argtypes = [P, P, ct.c_size_t, ct.POINTER(ct.c_size_t)]
+        lib.sg_restore.argtypes = [P, P, ct.c_size_t]
         lib.sg_last_error.argtypes = [P]
         lib.sg_last_error.restype = ct.c_char_p
         lib.sg_version.restype = ct.c_char_p
@@ -242,6 +245,17 @@ class Handle:
     def reset(self):
         self.check(self.lib.sg_reset(self.h))
 
+    def snapshot(self) -> bytes:
+        """sg_snapshot: the handle's per-key state as an opaque blob (no undelivered matches allowed)."""
+        size = ct.c_size_t()
+        self.check(self.lib.sg_snapshot(self.h, None, 0, ct.byref(size)))
+        buf = ct.create_string_buffer(max(size.value, 1))
+        self.check(self.lib.sg_snapshot(self.h, buf, size.value, ct.byref(size)))
+        return buf.raw[:size.value]
+
+    def restore(self, blob: bytes):
+        self.check(self.lib.sg_restore(self.h, blob, len(blob)))
+
     def discard(self):
         self.check(self.lib.sg_discard(self.h))
 
@@ -316,6 +330,12 @@ class GpuEngine:
         for k in range(self.nsel):
             vnull[:, k] = (vn >> np.uint32(k)) & np.uint32(1)
         return Outputs(tr, ts, ky, gr, vals, vnull)
+
+    def snapshot(self) -> bytes:
+        return self.handle.snapshot()
+
+    def restore(self, blob: bytes):
+        self.handle.restore(blob)
 
     def close(self):
         self.handle.close()

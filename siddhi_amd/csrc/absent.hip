@@ -552,3 +552,47 @@ void sg_every_absent_release(SgHandle* h) {
   h->state = nullptr;
   h->state_kind = 0;
 }
+
+// Snapshot of the absence closed form: the pending partials in arrival order (deadline, compared value,
+// projection) -- the Scheduler's ToNotifyQueue plus the absent pre-state's pending list
+// (C/util/Scheduler.java:147-160, AbsentStreamPreStateProcessor's StreamPreStateProcessor.currentState
+// C/query/input/stream/state/StreamPreStateProcessor.java:352-359) -- and the last timestamp seen.
+void sg_every_absent_snapshot(SgHandle* h, SnapW& w) {
+  AbsState* as = (h->state && h->state_kind == 3) ? (AbsState*)h->state : nullptr;
+  const int64_t n = as ? as->carry[as->cur].n : 0;
+  const int ns = std::max(h->desc.n_select, 1);
+  w.pod(n);
+  int64_t last = INT64_MIN;
+  if (as && h->pushes > 0) {
+    HIPCHK(hipMemcpyAsync(&last, as->dlast, 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  w.pod(last);
+  if (!n) return;
+  const AbsCarry& c = as->carry[as->cur];
+  w.dev(c.dl, n * 8, h->stream);
+  w.dev(c.val, n * 8, h->stream);
+  w.dev(c.vnul, n, h->stream);
+  w.dev(c.sel, n * 8 * ns, h->stream);
+  w.dev(c.snul, n * 4, h->stream);
+}
+
+void sg_every_absent_restore(SgHandle* h, SnapR& r) {
+  AbsState* as = astate(h);
+  const int ns = std::max(h->desc.n_select, 1);
+  const int64_t n = r.pod<int64_t>();
+  if (n < 0 || n >= (1ll << 31)) throw SgError(SG_EINVAL, "snapshot: bad pending-partial count");
+  const int64_t last = r.pod<int64_t>();
+  as->carry[0].n = as->carry[1].n = 0;
+  HIPCHK(hipMemcpyAsync(as->dlast, &last, 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (!n) return;
+  AbsCarry& c = as->carry[as->cur];
+  c.reserve(n, h->desc.n_select);
+  r.dev(c.dl, n * 8, h->stream);
+  r.dev(c.val, n * 8, h->stream);
+  r.dev(c.vnul, n, h->stream);
+  r.dev(c.sel, n * 8 * ns, h->stream);
+  r.dev(c.snul, n * 4, h->stream);
+  c.n = n;
+}

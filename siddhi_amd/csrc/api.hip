@@ -301,6 +301,98 @@ int sg_close(sg_handle* hh) {
   return SG_OK;
 }
 
+// ---- snapshot / restore -------------------------------------------------------------------------
+static const char SNAP_MAGIC[8] = {'S', 'G', 'S', 'N', 'A', 'P', '0', '1'};
+
+// Fingerprint of everything the persisted state's meaning depends on: the lowered query and the engine
+// route (closed form or general machine).  Field-wise, so struct padding never enters it.
+static uint64_t query_fingerprint(const SgHandle& h) {
+  const sg_nfa_desc& d = h.desc;
+  uint64_t x = 1469598103934665603ull;
+  auto mix = [&](int64_t v) {
+    for (int b = 0; b < 8; ++b) { x ^= (uint64_t)((v >> (8 * b)) & 0xff); x *= 1099511628211ull; }
+  };
+  mix(d.type); mix(d.within); mix(d.playback); mix(d.partitioned);
+  mix(d.n_states); mix(d.n_streams); mix(d.n_cols); mix(d.n_ret); mix(d.n_select);
+  mix(h.opt.force_general ? SG_SHAPE_GENERAL : d.shape);
+  for (int k = 0; k < 8; ++k) mix(d.shape_args[k]);
+  for (int s = 0; s < d.n_states; ++s) {
+    const sg_state_desc& st = d.states[s];
+    mix(st.kind); mix(st.stream); mix(st.is_start); mix(st.min_count); mix(st.max_count); mix(st.logical_type);
+    mix(st.partner); mix(st.next_state); mix(st.next_every); mix(st.within_every); mix(st.waiting_time);
+  }
+  for (int c = 0; c < d.n_cols; ++c) { mix(d.col_type[c]); mix(d.col_stream[c]); }
+  for (int k = 0; k < d.n_select; ++k) { mix(d.sel_state[k]); mix(d.sel_index[k]); mix(d.sel_ret[k]); }
+  mix(d.code_len);
+  for (int k = 0; k < d.code_len; ++k) mix(d.code[k]);
+  return x;
+}
+
+// Serialise the handle's state (persist between events: SiddhiAppRuntime.snapshot,
+// C/SiddhiAppRuntime.java:613-623 -> SnapshotService.fullSnapshot, C/util/snapshot/SnapshotService.java:97-157).
+// buf == NULL (or cap too small) only reports the size.  Matches not yet polled are not state -- the
+// reference has delivered them inside send() -- so a handle with pending matches is refused.
+int sg_snapshot(sg_handle* hh, void* buf, size_t cap, size_t* size) {
+  if (!hh || !size) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipSetDevice(h.device));
+    HIPCHK(hipStreamSynchronize(h.stream));
+    if (h.out.n) throw SgError(SG_EINVAL, "snapshot with undelivered matches: poll or discard them first");
+    SnapW w;
+    w.put(SNAP_MAGIC, 8);
+    w.pod((int32_t)SG_ABI_VERSION);
+    w.pod((int32_t)h.state_kind);
+    w.pod(query_fingerprint(h));
+    w.pod((int64_t)h.pushes);
+    w.pod((int64_t)h.clock);
+    w.pod((uint32_t)h.key_bound_seen);
+    switch (h.state_kind) {
+      case 1: sg_every_next_snapshot(&h, w); break;
+      case 2: sg_general_snapshot(&h, w); break;
+      case 3: sg_every_absent_snapshot(&h, w); break;
+      default: break;
+    }
+    *size = w.b.size();
+    if (buf && cap >= w.b.size()) memcpy(buf, w.b.data(), w.b.size());
+  });
+}
+
+// Replace the handle's state by a snapshot of a handle opened with the same query and options
+// (SiddhiAppRuntime.restore, C/SiddhiAppRuntime.java:625-635 -> SnapshotService.restore :271-345).
+int sg_restore(sg_handle* hh, const void* buf, size_t size) {
+  if (!hh || (!buf && size)) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipSetDevice(h.device));
+    HIPCHK(hipStreamSynchronize(h.stream));
+    SnapR r{(const char*)buf, (const char*)buf + size};
+    if (memcmp(r.take(8), SNAP_MAGIC, 8) != 0) throw SgError(SG_EINVAL, "not a siddhi_gpu snapshot");
+    if (r.pod<int32_t>() != SG_ABI_VERSION) throw SgError(SG_EINVAL, "snapshot ABI version mismatch");
+    const int32_t kind = r.pod<int32_t>();
+    if (r.pod<uint64_t>() != query_fingerprint(h)) throw SgError(SG_EINVAL, "snapshot was taken for another query");
+    const int64_t pushes = r.pod<int64_t>();
+    const int64_t clock = r.pod<int64_t>();
+    const uint32_t kb = r.pod<uint32_t>();
+    if (kind < 0 || kind > 3 || (h.state_kind && kind && h.state_kind != kind))
+      throw SgError(SG_EINVAL, "snapshot engine kind does not match the handle");
+    h.out.n = 0;
+    sg_every_next_reset(&h);
+    sg_every_absent_reset(&h);
+    sg_general_reset(&h);
+    switch (kind) {
+      case 1: sg_every_next_restore(&h, r); break;
+      case 2: sg_general_restore(&h, r); break;
+      case 3: sg_every_absent_restore(&h, r); break;
+      default: break;
+    }
+    if (r.p != r.e) throw SgError(SG_EINVAL, "trailing bytes in snapshot");
+    h.pushes = (int)pushes;
+    h.clock = clock;
+    h.key_bound_seen = kb;
+  });
+}
+
 const char* sg_last_error(const sg_handle* hh) { return hh ? hh->h.err.c_str() : "null handle"; }
 
 }  // extern "C"

@@ -532,3 +532,47 @@ void sg_general_release(SgHandle* h) {
   h->state = nullptr;
   h->state_kind = 0;
 }
+
+// Snapshot of the general machine: the per-key runtimes (pending / newAndEvery lists, partial, event-copy
+// and chain pools, timer FIFOs) of the keys seen so far, i.e. what StreamPreStateProcessor.currentState,
+// CountPreStateProcessor, LogicalPreStateProcessor and Scheduler.currentState persist per partition clone
+// (C/query/input/stream/state/StreamPreStateProcessor.java:352-359, C/util/Scheduler.java:147-160,
+// C/partition/PartitionRuntime.java:342-356).  The arena geometry must match on restore.
+void sg_general_snapshot(SgHandle* h, SnapW& w) {
+  GeneralState* gs = (h->state && h->state_kind == 2) ? (GeneralState*)h->state : nullptr;
+  const int64_t keys = gs ? std::min<int64_t>(gs->keys_alloc, (int64_t)h->key_bound_seen) : 0;
+  w.pod(keys);
+  if (!keys) return;
+  w.pod(gs->geo);
+  w.dev(gs->arena, (size_t)keys * gs->geo.key_words * 4, h->stream);
+}
+
+void sg_general_restore(SgHandle* h, SnapR& r) {
+  GeneralState* gs = gstate(h);
+  hipStream_t st = h->stream;
+  const int64_t keys = r.pod<int64_t>();
+  if (keys < 0 || keys > (1ll << 31)) throw SgError(SG_EINVAL, "snapshot: bad key count");
+  if (gs->arena) HIPCHK(hipMemsetAsync(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4, st));
+  if (!keys) {
+    HIPCHK(hipStreamSynchronize(st));
+    return;
+  }
+  SgGeo g = r.pod<SgGeo>();
+  const SgGeo& m = gs->geo;
+  if (g.S != m.S || g.R != m.R || g.P != m.P || g.E != m.E || g.C != m.C || g.L != m.L || g.Q != m.Q ||
+      g.A != m.A || g.nsel != m.nsel || g.key_words != m.key_words)
+    throw SgError(SG_EINVAL, "snapshot: per-key arena geometry differs (pool / list options must match)");
+  if (keys > gs->keys_alloc) {
+    size_t bytes = (size_t)keys * (size_t)gs->geo.key_words * 4;
+    int32_t* na = nullptr;
+    if (hipMalloc(&na, bytes) != hipSuccess)
+      throw SgError(SG_ECAPACITY, "cannot allocate per-key NFA arenas (" + std::to_string(bytes >> 20) + " MiB)");
+    if (gs->arena) {
+      HIPCHK(hipStreamSynchronize(st));
+      hipFree(gs->arena);
+    }
+    gs->arena = na;
+    gs->keys_alloc = keys;
+  }
+  r.dev(gs->arena, (size_t)keys * gs->geo.key_words * 4, st);
+}

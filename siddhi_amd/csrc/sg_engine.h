@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -108,6 +109,52 @@ struct SgHandle {
 };
 
 
+
+// Snapshot blob writer / reader (sg_snapshot / sg_restore).  Device sections are copied synchronously on the
+// handle's stream; the reader throws SG_EINVAL on a truncated or mismatching blob.
+struct SnapW {
+  std::vector<char> b;
+  void put(const void* p, size_t n) {
+    size_t o = b.size();
+    b.resize(o + n);
+    if (n) memcpy(b.data() + o, p, n);
+  }
+  template <class T> void pod(const T& v) { put(&v, sizeof(T)); }
+  void dev(const void* dp, size_t n, hipStream_t st) {
+    size_t o = b.size();
+    b.resize(o + n);
+    if (!n) return;
+    if (hipMemcpyAsync(b.data() + o, dp, n, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+      throw SgError(SG_EHIP, "snapshot: device copy failed");
+  }
+};
+struct SnapR {
+  const char* p;
+  const char* e;
+  const char* take(size_t n) {
+    if ((size_t)(e - p) < n) throw SgError(SG_EINVAL, "snapshot blob truncated");
+    const char* q = p;
+    p += n;
+    return q;
+  }
+  template <class T> T pod() {
+    T v;
+    memcpy(&v, take(sizeof(T)), sizeof(T));
+    return v;
+  }
+  void dev(void* dp, size_t n, hipStream_t st) {
+    const char* q = take(n);
+    if (!n) return;
+    if (hipMemcpyAsync(dp, q, n, hipMemcpyHostToDevice, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+      throw SgError(SG_EHIP, "restore: device copy failed");
+  }
+};
+void sg_every_next_snapshot(SgHandle* h, SnapW& w);
+void sg_every_next_restore(SgHandle* h, SnapR& r);
+void sg_every_absent_snapshot(SgHandle* h, SnapW& w);
+void sg_every_absent_restore(SgHandle* h, SnapR& r);
+void sg_general_snapshot(SgHandle* h, SnapW& w);
+void sg_general_restore(SgHandle* h, SnapR& r);
 
 void sg_run_every_next(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_f32(SgHandle* h, const BatchView& bv, int64_t n);

@@ -21,6 +21,7 @@ also the order the reference registers per-key schedulers in (PartitionRuntime.j
 """
 from __future__ import annotations
 
+import json
 import math
 import struct
 import time
@@ -213,6 +214,48 @@ class SiddhiAppRuntime:
         self.flush()
         for q in self.queries:
             q.engine.close()
+
+    # -- persistence (SiddhiAppRuntime.snapshot / restore, C/SiddhiAppRuntime.java:613-635)
+    _SNAP_MAGIC = b"SDAPSNP1"
+
+    def snapshot(self) -> bytes:
+        """Persist the app's pattern state between events: every query engine's per-key state plus the host
+        dictionaries (string ids, partition-key first-seen order) and the event counter.  Buffered rows are
+        flushed (and their matches delivered) first, as persist() runs between send() calls."""
+        self.flush()
+        blobs = [q.engine.snapshot() for q in self.queries]
+        meta = {"strings": self.string_list_from_dict(), "key_dicts": [list(kd.keys()) for kd in self.key_dicts],
+                "next_index": self.next_index, "blobs": [len(b) for b in blobs],
+                "queries": [q.query.name for q in self.queries]}
+        mj = json.dumps(meta).encode()
+        return self._SNAP_MAGIC + struct.pack("<Q", len(mj)) + mj + b"".join(blobs)
+
+    def restore(self, snapshot: bytes):
+        """Restore a snapshot() of an app built from the same SiddhiQL (CannotRestoreSiddhiAppStateException
+        -> ValueError otherwise)."""
+        if snapshot[:8] != self._SNAP_MAGIC:
+            raise ValueError("not a siddhi_amd app snapshot")
+        (ml,) = struct.unpack("<Q", snapshot[8:16])
+        meta = json.loads(snapshot[16:16 + ml].decode())
+        if meta["queries"] != [q.query.name for q in self.queries]:
+            raise ValueError("snapshot was taken from another app")
+        self._rows = []
+        off = 16 + ml
+        for q, n in zip(self.queries, meta["blobs"]):
+            q.engine.restore(snapshot[off:off + n])
+            off += n
+        if off != len(snapshot):
+            raise ValueError("trailing bytes in snapshot")
+        self.strings = {s: i for i, s in enumerate(meta["strings"])}
+        self.string_list = []
+        self.key_dicts = [{k: i for i, k in enumerate(ks)} for ks in meta["key_dicts"]]
+        self.next_index = meta["next_index"]
+
+    def string_list_from_dict(self) -> List[str]:
+        out = [None] * len(self.strings)
+        for s, i in self.strings.items():
+            out[i] = s
+        return out
 
     # -- ingestion
     def _string_id(self, s: str) -> int:
