@@ -89,6 +89,8 @@ extern "C" {
 #define SG_OP_OR 5
 #define SG_OP_NOT 6
 #define SG_OP_ISNULL 7
+#define SG_OP_MATH 8    /* MATH op(0 + 1 - 2 * 3 / 4 %) result_type: Java arithmetic, null on a null operand or a
+                           zero divisor (C/executor/math/{add,subtract,multiply,divide,mod}/*.java) */
 
 typedef struct sg_state_desc {
   int32_t kind, stream, is_start, min_count, max_count, logical_type, partner;
@@ -130,6 +132,13 @@ typedef struct sg_nfa_desc {
   int32_t shape_prog_off, shape_prog_len;
   int32_t code_len;
   int64_t code[SG_MAX_CODE];
+  /* Select expressions (QuerySelector over math executors, C/query/selector/QuerySelector.java:125-163):
+   * n_out > 0 -> output column k is the postfix program code[out_off[k] .. +out_len[k]) over the n_select
+   * projected slots (VAR operands: word 3 = slot); matches then carry n_out values of type out_type[k].
+   * n_out == 0 -> the n_select projected slots are the output. */
+  int32_t n_out;
+  int32_t out_type[SG_MAX_SELECT], out_off[SG_MAX_SELECT], out_len[SG_MAX_SELECT];
+  int32_t reserved_out;
 } sg_nfa_desc;
 
 typedef struct sg_options {
@@ -167,7 +176,8 @@ typedef struct sg_batch {
   int32_t key_bound;            /* exclusive upper bound of key ids in this batch (0 = unknown) */
 } sg_batch;
 
-/* Pending matches as they sit in HBM: n AoS records of record_bytes = 32 + 8*n_select bytes,
+/* Pending matches as they sit in HBM: n AoS records of record_bytes = 32 + 8*n_select bytes (n_select = the
+ * output column count: sg_nfa_desc.n_out when set, else n_select),
  * {u64 trigger; i64 ts; i32 key; u32 group; u32 vnull; u32 pad; i64 vals[n_select]} (see sg_matches). */
 typedef struct sg_match_records {
   int64_t n;

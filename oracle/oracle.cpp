@@ -209,7 +209,7 @@ static std::unique_ptr<Expr> read_expr(Reader& r) {
     case X_CMP: e->op = (int)r.next(); e->l = read_expr(r); e->r = read_expr(r); break;
     case X_AND: case X_OR: e->l = read_expr(r); e->r = read_expr(r); break;
     case X_NOT: case X_ISNULL: e->l = read_expr(r); break;
-    case X_MATH: fail("arithmetic expressions are not supported by the oracle");
+    case X_MATH: e->op = (int)r.next(); e->l = read_expr(r); e->r = read_expr(r); break;
     default: fail("bad expr kind");
   }
   return e;
@@ -312,6 +312,58 @@ static bool cmp_num(int op, const Val& l, const Val& r, int pt) {
 
 static Val eval(const Expr* x, StateEvent* s);
 
+// Arithmetic (select expressions).  Result type: ExpressionParser.parseArithmeticOperationResultType
+// (C/util/parser/ExpressionParser.java:1413-1431), stored in x->vtype at resolution.  Executors
+// C/executor/math/{add,subtract,multiply,divide,mod}/*ExpressionExecutor{Int,Long,Float,Double}.java: a null
+// operand gives null; Divide/Mod return null when the divisor equals zero (intValue()/longValue() == 0,
+// floatValue() == 0.0f, doubleValue() == 0.0); otherwise Java's operator on the converted operands.  Integer ops
+// are evaluated in a wider type and narrowed, which is exactly Java's two's-complement wrap (incl. MIN / -1).
+static double as_double(const Val& v) { return (v.type == T_FLOAT || v.type == T_DOUBLE) ? v.d : (double)v.i; }
+static Val eval_math(const Expr* x, const Val& l, const Val& r) {
+  const int t = x->vtype, op = x->op;
+  if (l.null || r.null) return vnull(t);
+  Val o = vnull(t);
+  o.null = false;
+  if (t == T_INT || t == T_LONG) {
+    __int128 a = l.i, b = r.i, c = 0;
+    if ((op == 3 || op == 4) && b == 0) return vnull(t);
+    switch (op) {
+      case 0: c = a + b; break;
+      case 1: c = a - b; break;
+      case 2: c = a * b; break;
+      case 3: c = a / b; break;       // truncates toward zero, as Java
+      default: c = a % b; break;      // sign of the dividend, as Java
+    }
+    o.i = (t == T_INT) ? (int64_t)(int32_t)(uint32_t)(uint64_t)c : (int64_t)(uint64_t)c;
+    return o;
+  }
+  if (t == T_FLOAT) {
+    volatile float a = (float)as_double(l), b = (float)as_double(r), c = 0.0f;
+    if (l.type != T_FLOAT && l.type != T_DOUBLE) a = (float)l.i;    // long -> float rounds once (JLS 5.1.2)
+    if (r.type != T_FLOAT && r.type != T_DOUBLE) b = (float)r.i;
+    if ((op == 3 || op == 4) && b == 0.0f) return vnull(t);
+    switch (op) {
+      case 0: c = a + b; break;
+      case 1: c = a - b; break;
+      case 2: c = a * b; break;
+      case 3: c = a / b; break;
+      default: c = std::fmod((float)a, (float)b); break;
+    }
+    o.d = (double)c;
+    return o;
+  }
+  double a = as_double(l), b = as_double(r);
+  if ((op == 3 || op == 4) && b == 0.0) return vnull(t);
+  switch (op) {
+    case 0: o.d = a + b; break;
+    case 1: o.d = a - b; break;
+    case 2: o.d = a * b; break;
+    case 3: o.d = a / b; break;
+    default: o.d = std::fmod(a, b); break;
+  }
+  return o;
+}
+
 static Val read_var(const Expr* x, StateEvent* s) {
   StreamEvent* e = get_stream_event(s, x->chain, x->in_chain);
   if (!e) return vnull(x->vtype);
@@ -345,6 +397,7 @@ static Val eval(const Expr* x, StateEvent* s) {
     }
     case X_NOT: return vbool(truth(eval(x->l.get(), s)) != 1);  // NotCondition...java:43-49
     case X_ISNULL: return vbool(eval(x->l.get(), s).null);
+    case X_MATH: return eval_math(x, eval(x->l.get(), s), eval(x->r.get(), s));
   }
   fail("eval: bad expr");
 }
@@ -551,7 +604,7 @@ struct Engine {
   int64_t next_id = 0;
   std::string error;
   // select resolution
-  std::vector<int> sel_chain, sel_idx, sel_attr, sel_type;
+  // select expressions: app.select (resolved in orc_create)
   uint64_t stats_partials = 0;
   void setCurrentTimestamp(int64_t ts, uint64_t trigger);
 };
@@ -913,11 +966,7 @@ void KeyRuntime::emit(const SE& s) {
   o.ts = s->ts;
   o.key = key;
   o.group = ((uint32_t)cur_phase << 24) | (cur_group & 0xFFFFFF);
-  for (size_t i = 0; i < e->sel_chain.size(); i++) {
-    StreamEvent* se = get_stream_event(s.get(), e->sel_chain[i], e->sel_idx[i]);
-    if (!se) o.vals.push_back(vnull(e->sel_type[i]));
-    else o.vals.push_back(se->data->vals[e->sel_attr[i]]);
-  }
+  for (auto& x : e->app.select) o.vals.push_back(eval(x.get(), s.get()));   // SelectiveStateEventPopulator
   e->out.push_back(std::move(o));
   if (cur_phase == 0) cur_group++;   // every timer emission is its own callback (sendEvent per partial)
 }
@@ -1215,6 +1264,24 @@ struct OrcHandle {
 
 extern "C" {
 
+// Select expression types (SelectorParser -> ExpressionParser.parseExpression): attributes, constants and
+// arithmetic.  String / bool operands are refused here (the reference's executors would throw
+// ClassCastException on the first event).
+static int select_type(Expr* x) {
+  switch (x->kind) {
+    case X_VAR: return x->vtype;
+    case X_CONST: return x->cval.type;
+    case X_MATH: {
+      int a = select_type(x->l.get()), b = select_type(x->r.get());
+      if (a == T_STRING || a == T_BOOL || b == T_STRING || b == T_BOOL) fail("arithmetic on a non-numeric attribute");
+      x->vtype = promote_order(a, b);
+      return x->vtype;
+    }
+    default: fail("unsupported select expression");
+  }
+  return 0;
+}
+
 OrcHandle* orc_create(const int64_t* image, int64_t n, char* err, int errlen) {
   try {
     auto* h = new OrcHandle();
@@ -1234,10 +1301,8 @@ OrcHandle* orc_create(const int64_t* image, int64_t n, char* err, int errlen) {
     // select resolution (SelectorParser: default chain index 0, UNKNOWN_STATE scope)
     Builder b{&h->eng, nullptr};
     for (auto& x : h->eng.app.select) {
-      if (x->kind != X_VAR) throw Err{"only attribute projections are supported in select"};
       b.resolve(x.get(), -1, true);
-      h->eng.sel_chain.push_back(x->chain); h->eng.sel_idx.push_back(x->in_chain);
-      h->eng.sel_attr.push_back(x->attr_idx); h->eng.sel_type.push_back(x->vtype);
+      select_type(x.get());
     }
     return h;
   } catch (Err& e) {
@@ -1316,7 +1381,7 @@ int64_t orc_fetch(OrcHandle* h, int64_t cap, uint64_t* trigger, int64_t* ts, int
                   int64_t* vals, uint8_t* vnull) {
   Engine& E = h->eng;
   int64_t n = std::min<int64_t>(cap, (int64_t)E.out.size());
-  size_t ns = E.sel_chain.size();
+  size_t ns = E.app.select.size();
   for (int64_t i = 0; i < n; i++) {
     const Output& o = E.out[i];
     trigger[i] = o.trigger; ts[i] = o.ts; key[i] = o.key; group[i] = o.group;

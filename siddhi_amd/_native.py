@@ -49,7 +49,9 @@ class sg_nfa_desc(ct.Structure):
                 ("sel_state", I32 * SG_MAX_SELECT), ("sel_index", I32 * SG_MAX_SELECT),
                 ("sel_ret", I32 * SG_MAX_SELECT), ("sel_type", I32 * SG_MAX_SELECT),
                 ("shape", I32), ("shape_args", I32 * 8), ("shape_prog_off", I32), ("shape_prog_len", I32),
-                ("code_len", I32), ("code", I64 * SG_MAX_CODE)]
+                ("code_len", I32), ("code", I64 * SG_MAX_CODE),
+                ("n_out", I32), ("out_type", I32 * SG_MAX_SELECT), ("out_off", I32 * SG_MAX_SELECT),
+                ("out_len", I32 * SG_MAX_SELECT), ("reserved_out", I32)]
 
 
 class sg_options(ct.Structure):
@@ -147,6 +149,12 @@ def build_desc(nfa: L.FlatNFA) -> sg_nfa_desc:
     d.shape_prog_off = len(code)
     d.shape_prog_len = len(nfa.shape_prog)
     code += nfa.shape_prog
+    d.n_out = len(nfa.out_progs)
+    for k, (w, t) in enumerate(zip(nfa.out_progs, nfa.out_types)):
+        d.out_off[k] = len(code)
+        d.out_len[k] = len(w)
+        d.out_type[k] = L.TYPE_CODE[t]
+        code += w
     if len(code) > SG_MAX_CODE:
         raise L.LoweringError("predicate programs too long")
     d.code_len = len(code)
@@ -302,7 +310,7 @@ class GpuEngine:
         if pool:
             opts.pool_partials = opts.pool_events = opts.pool_chain = opts.list_cap = pool
         self.handle = Handle(self.desc, device, opts)
-        self.nsel = len(self.nfa.select)
+        self.nsel = len(self.nfa.out_progs) or len(self.nfa.select)
 
     def push(self, b):
         import numpy as np

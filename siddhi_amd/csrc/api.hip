@@ -20,6 +20,58 @@ struct sg_handle {
 };
 
 static int col_width(int type) { return (type == SG_T_LONG || type == SG_T_DOUBLE) ? 8 : 4; }
+static int out_cols(const sg_nfa_desc& d) { return d.n_out > 0 ? d.n_out : d.n_select; }
+
+// ---- select expressions (QuerySelector.processNoGroupBy over math executors,
+// C/query/selector/QuerySelector.java:125-163; SelectorParser.java:199-233): the engines project the matched
+// slots the expressions read (n_select base values per record); this pass evaluates each output column's
+// postfix program over them, one record per lane, in delivery order.
+struct SelReader {
+  const int64_t* vals;
+  uint32_t vnull;
+  __device__ SgVal read(int, int, int slot, int type) { return sg_val_from_bits(vals[slot], type, (vnull >> slot) & 1); }
+};
+
+__global__ void k_select(int64_t n, const char* __restrict__ src, int sstride, char* __restrict__ dst, int dstride,
+                         const DevDesc* __restrict__ d) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const char* r = src + (size_t)i * sstride;
+  char* o = dst + (size_t)i * dstride;
+  SelReader rd;
+  rd.vals = (const int64_t*)(r + 32);
+  rd.vnull = *(const uint32_t*)(r + 24);
+  ((uint64_t*)o)[0] = ((const uint64_t*)r)[0];   // trigger
+  ((uint64_t*)o)[1] = ((const uint64_t*)r)[1];   // ts
+  ((uint64_t*)o)[2] = ((const uint64_t*)r)[2];   // key, group
+  uint32_t vn = 0;
+  const int nout = d->n_out;
+  for (int k = 0; k < nout; ++k) {
+    SgVal top;
+    if (!sg_run(d->code + d->out_off[k], d->out_len[k], rd, top)) top.null = 1;
+    if (top.null) vn |= 1u << k;
+    ((int64_t*)(o + 32))[k] = sg_val_bits(top);
+  }
+  ((uint32_t*)o)[6] = vn;
+  ((uint32_t*)o)[7] = 0;
+}
+
+// Engines append base records to h.stage (swapped in for the push); the select pass appends the output
+// records to h.out.
+static void run_select(SgHandle& h) {
+  const sg_nfa_desc& d = h.desc;
+  hipStream_t st = h.stream;
+  const int64_t n = h.stage.n;
+  if (n > 0) {
+    char* out = h.out.reserve(n, d.n_out, st);
+    const int ostride = 32 + 8 * d.n_out;
+    hipLaunchKernelGGL(k_select, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, (const char*)h.stage.rec,
+                       32 + 8 * d.n_select, out + (size_t)h.out.n * ostride, ostride, h.ddesc);
+    HIPCHK(hipGetLastError());
+    h.out.n += n;
+  }
+  h.stage.n = 0;
+}
 
 template <class F>
 static int guard(sg_handle* hh, F&& f) {
@@ -43,6 +95,10 @@ static void validate(const sg_nfa_desc* d) {
   if (d->n_ret < 0 || d->n_ret > SG_MAX_RET) throw SgError(SG_EINVAL, "bad n_ret");
   if (d->n_select < 0 || d->n_select > SG_MAX_SELECT) throw SgError(SG_EINVAL, "bad n_select");
   if (d->code_len < 0 || d->code_len > SG_MAX_CODE) throw SgError(SG_EINVAL, "bad code_len");
+  if (d->n_out < 0 || d->n_out > SG_MAX_SELECT) throw SgError(SG_EINVAL, "bad n_out");
+  for (int k = 0; k < d->n_out; ++k)
+    if (d->out_off[k] < 0 || d->out_len[k] < 1 || d->out_off[k] + d->out_len[k] > d->code_len)
+      throw SgError(SG_EINVAL, "bad select program range");
   for (int s = 0; s < d->n_states; ++s) {
     const sg_state_desc& st = d->states[s];
     if (st.stream < 0 || st.stream >= d->n_streams) throw SgError(SG_EINVAL, "state stream out of range");
@@ -135,15 +191,26 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
     for (int r = 0; r < d.n_ret; ++r)
       if (!bv.cols.col[d.ret_col[r]]) throw SgError(SG_EINVAL, "batch is missing a column the query reads");
     int shape = h.opt.force_general ? SG_SHAPE_GENERAL : d.shape;
-    switch (shape) {
-      case SG_SHAPE_EVERY_NEXT_CMP:
-        sg_run_every_next(&h, bv, n);
-        break;
-      case SG_SHAPE_EVERY_ABSENT_EQ:
-        sg_run_every_absent(&h, bv, n);
-        break;
-      default:
-        sg_run_general(&h, bv, n);
+    const bool sel = d.n_out > 0;
+    if (sel) std::swap(h.out, h.stage);   // engines append base records to the stage
+    try {
+      switch (shape) {
+        case SG_SHAPE_EVERY_NEXT_CMP:
+          sg_run_every_next(&h, bv, n);
+          break;
+        case SG_SHAPE_EVERY_ABSENT_EQ:
+          sg_run_every_absent(&h, bv, n);
+          break;
+        default:
+          sg_run_general(&h, bv, n);
+      }
+    } catch (...) {
+      if (sel) { std::swap(h.out, h.stage); h.stage.n = 0; }
+      throw;
+    }
+    if (sel) {
+      std::swap(h.out, h.stage);
+      run_select(h);
     }
     h.pushes++;
   });
@@ -186,8 +253,8 @@ int sg_device_records(sg_handle* hh, sg_match_records* v) {
   if (!hh || !v) return SG_EINVAL;
   OutStore& o = hh->h.out;
   v->n = o.n;
-  v->record_bytes = 32 + 8 * hh->h.desc.n_select;
-  v->n_select = hh->h.desc.n_select;
+  v->record_bytes = 32 + 8 * out_cols(hh->h.desc);
+  v->n_select = out_cols(hh->h.desc);
   v->base = o.rec;
   return SG_OK;
 }
@@ -200,7 +267,7 @@ int sg_poll(sg_handle* hh, sg_matches* out, int64_t cap, int64_t* n) {
     OutStore& o = h.out;
     int64_t k = std::min<int64_t>(cap, o.n);
     hipStream_t st = h.stream;
-    int ns = h.desc.n_select;
+    int ns = out_cols(h.desc);
     size_t stride = 32 + 8 * (size_t)ns;
     if (k > 0) {
       std::vector<char> tmp((size_t)k * stride);
@@ -294,6 +361,7 @@ int sg_close(sg_handle* hh) {
   sg_general_release(&h);
   h.ws.release();
   h.out.release();
+  h.stage.release();
   if (h.ddesc) hipFree(h.ddesc);
   for (auto& e : h.ev) if (e) hipEventDestroy(e);
   if (h.own_stream && h.stream) hipStreamDestroy(h.stream);
@@ -323,6 +391,8 @@ static uint64_t query_fingerprint(const SgHandle& h) {
   }
   for (int c = 0; c < d.n_cols; ++c) { mix(d.col_type[c]); mix(d.col_stream[c]); }
   for (int k = 0; k < d.n_select; ++k) { mix(d.sel_state[k]); mix(d.sel_index[k]); mix(d.sel_ret[k]); }
+  mix(d.n_out);
+  for (int k = 0; k < d.n_out; ++k) { mix(d.out_type[k]); mix(d.out_off[k]); mix(d.out_len[k]); }
   mix(d.code_len);
   for (int k = 0; k < d.code_len; ++k) mix(d.code[k]);
   return x;

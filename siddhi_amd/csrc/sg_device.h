@@ -115,12 +115,86 @@ __device__ __forceinline__ bool sg_cmp(int op, int dom, const SgVal& l, const Sg
   }
 }
 
+// Java arithmetic of the math executors (C/executor/math/{add,subtract,multiply,divide,mod}/*ExpressionExecutor*.java):
+// operands converted to the result type (ExpressionParser.parseArithmeticOperationResultType,
+// C/util/parser/ExpressionParser.java:1413-1431); null operand -> null; / and % by zero -> null (int/long: right == 0;
+// float/double: right == 0.0, so NaN divisors divide); int/long wrap two's complement; MIN / -1 = MIN, MIN % -1 = 0
+// (JLS 15.17.2-3); float arithmetic in binary32, % is fmod (JLS 15.17.3).
+__device__ __forceinline__ SgVal sg_math(int op, int rt, const SgVal& l, const SgVal& r) {
+  SgVal o;
+  o.type = rt;
+  o.null = 0;
+  o.i = 0;
+  o.d = 0.0;
+  if (l.null || r.null) { o.null = 1; return o; }
+  auto as_d = [](const SgVal& v) { return (v.type == SG_T_FLOAT || v.type == SG_T_DOUBLE) ? v.d : (double)v.i; };
+  if (rt == SG_T_DOUBLE) {
+    double a = as_d(l), b = as_d(r);
+    switch (op) {
+      case 0: o.d = a + b; break;
+      case 1: o.d = a - b; break;
+      case 2: o.d = a * b; break;
+      case 3: if (b == 0.0) o.null = 1; else o.d = a / b; break;
+      default: if (b == 0.0) o.null = 1; else o.d = fmod(a, b); break;
+    }
+  } else if (rt == SG_T_FLOAT) {
+    float a = (l.type == SG_T_FLOAT || l.type == SG_T_DOUBLE) ? (float)l.d : (float)l.i;
+    float b = (r.type == SG_T_FLOAT || r.type == SG_T_DOUBLE) ? (float)r.d : (float)r.i;
+    float c = 0.0f;
+    switch (op) {
+      case 0: c = a + b; break;
+      case 1: c = a - b; break;
+      case 2: c = a * b; break;
+      case 3: if (b == 0.0f) o.null = 1; else c = a / b; break;
+      default: if (b == 0.0f) o.null = 1; else c = fmodf(a, b); break;
+    }
+    o.d = (double)c;
+  } else if (rt == SG_T_LONG) {
+    uint64_t a = (uint64_t)l.i, b = (uint64_t)r.i;
+    switch (op) {
+      case 0: o.i = (int64_t)(a + b); break;
+      case 1: o.i = (int64_t)(a - b); break;
+      case 2: o.i = (int64_t)(a * b); break;
+      case 3:
+        if (r.i == 0) o.null = 1;
+        else if (r.i == -1) o.i = (int64_t)(0 - a);
+        else o.i = l.i / r.i;
+        break;
+      default:
+        if (r.i == 0) o.null = 1;
+        else if (r.i == -1) o.i = 0;
+        else o.i = l.i % r.i;
+        break;
+    }
+  } else {   // INT
+    int32_t ai = (int32_t)l.i, bi = (int32_t)r.i;
+    uint32_t a = (uint32_t)ai, b = (uint32_t)bi;
+    int32_t c = 0;
+    switch (op) {
+      case 0: c = (int32_t)(a + b); break;
+      case 1: c = (int32_t)(a - b); break;
+      case 2: c = (int32_t)(a * b); break;
+      case 3:
+        if (bi == 0) o.null = 1;
+        else if (bi == -1) c = (int32_t)(0u - a);
+        else c = ai / bi;
+        break;
+      default:
+        if (bi == 0) o.null = 1;
+        else if (bi == -1) c = 0;
+        else c = ai % bi;
+        break;
+    }
+    o.i = c;
+  }
+  return o;
+}
+
 // Postfix VM. `Reader` supplies VAR operands: SgVal read(int state, int index_in_chain, int ret_slot, int type).
 // Booleans are kept tri-state in SgVal (i = 0/1, null) so `not` of null is true (NotConditionExpressionExecutor).
 #define SG_VM_STACK 16
 template <class Reader>
-__device__ __forceinline__ bool sg_eval(const int64_t* code, int len, Reader& rd) {
-  if (len <= 0) return true;
+__device__ __forceinline__ bool sg_run(const int64_t* code, int len, Reader& rd, SgVal& top) {
   SgVal st[SG_VM_STACK];
   int sp = 0;
   int pc = 0;
@@ -179,9 +253,26 @@ __device__ __forceinline__ bool sg_eval(const int64_t* code, int len, Reader& rd
         pc += 1;
         break;
       }
+      case SG_OP_MATH: {
+        SgVal r = st[--sp];
+        SgVal l = st[--sp];
+        st[sp++] = sg_math((int)code[pc + 1], (int)code[pc + 2], l, r);
+        pc += 3;
+        break;
+      }
       default:
         return false;
     }
   }
-  return sp > 0 && !st[sp - 1].null && st[sp - 1].i != 0;
+  if (sp <= 0) return false;
+  top = st[sp - 1];
+  return true;
+}
+
+template <class Reader>
+__device__ __forceinline__ bool sg_eval(const int64_t* code, int len, Reader& rd) {
+  if (len <= 0) return true;
+  SgVal top;
+  if (!sg_run(code, len, rd, top)) return false;
+  return !top.null && top.i != 0;
 }

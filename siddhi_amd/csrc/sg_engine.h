@@ -95,6 +95,7 @@ struct SgHandle {
   bool own_stream = false;
   Workspace ws;
   OutStore out;
+  OutStore stage;             // base records of the running push when select expressions follow (desc.n_out > 0)
   std::string err;
   hipEvent_t ev[8] = {};
   int64_t last_events = 0, last_matches = 0, last_spilled = 0;

@@ -3,6 +3,7 @@
 #pragma once
 #include <cstring>
 #include <cstdint>
+#include <cmath>
 #define __host__
 #define __device__
 #define __forceinline__ inline

@@ -105,7 +105,7 @@ def _enc_expr(ctx: QueryContext, e) -> List[int]:
     if isinstance(e, C.IsNull):
         return [16] + _enc_expr(ctx, e.expr)
     if isinstance(e, C.Math):
-        return [17]
+        return [17, MATH_CODE[e.op]] + _enc_expr(ctx, e.left) + _enc_expr(ctx, e.right)
     raise LoweringError(f"unsupported expression {e}")
 
 
@@ -168,7 +168,18 @@ K_STREAM, K_COUNT, K_LOGICAL, K_ABSENT = 0, 1, 2, 3
 SHAPE_GENERAL, SHAPE_EVERY_NEXT_CMP, SHAPE_EVERY_ABSENT_EQ = 0, 1, 2
 
 # postfix predicate opcodes (shared with siddhi_amd/csrc/nfa_desc.h)
-OP_VAR, OP_CONST, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ISNULL = 1, 2, 3, 4, 5, 6, 7
+OP_VAR, OP_CONST, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ISNULL, OP_MATH = 1, 2, 3, 4, 5, 6, 7, 8
+MATH_CODE = {"+": 0, "-": 1, "*": 2, "/": 3, "%": 4}
+
+
+def math_type(lt: str, rt: str) -> str:
+    """ExpressionParser.parseArithmeticOperationResultType (C/util/parser/ExpressionParser.java:1413-1431)."""
+    for t in ("DOUBLE", "FLOAT", "LONG", "INT"):
+        if lt == t or rt == t:
+            if lt in ("STRING", "BOOL") or rt in ("STRING", "BOOL"):
+                break
+            return t
+    raise LoweringError(f"Arithmetic operation between {lt} and {rt} cannot be executed")
 # comparison domains
 D_I64, D_F32, D_F64, D_ID = 0, 1, 2, 3
 
@@ -224,6 +235,11 @@ class FlatNFA:
     shape: int = SHAPE_GENERAL
     shape_args: List[int] = field(default_factory=lambda: [0] * 8)
     shape_prog: list = field(default_factory=list)    # local conjuncts of the closed-form's second state
+    # select expressions beyond plain attributes (QuerySelector with math executors): per output column a
+    # postfix program over the projected `select` slots ([OP_VAR, 0, 0, slot, type] / OP_CONST / OP_MATH);
+    # empty when every output is a plain attribute (then `select` is the output)
+    out_progs: list = field(default_factory=list)
+    out_types: List[str] = field(default_factory=list)
 
 
 def _cmp_domain(lt: str, rt: str, op: str) -> int:
@@ -488,17 +504,42 @@ class _FlatBuilder:
         ro, uo = [], []
         self.reset_ops(root, ro)
         self.update_ops(root, uo)
-        select = []
+        select, out_progs, out_types = [], [], []
+        plain = all(isinstance(oa.expr, C.Var) for oa in q.select)
+
+        def base_slot(v):
+            chain, idx, ai, t = self.resolve(v, -1, True)
+            ent = (chain, idx, self.ret_slot(self.states[chain].stream, ai), t)
+            if plain or ent not in select:
+                select.append(ent)
+            return select.index(ent) if not plain else len(select) - 1, t
+
+        def sel_prog(e):     # SelectorParser -> ExpressionParser.parseExpression over the matched slots
+            if isinstance(e, C.Var):
+                k, t = base_slot(e)
+                return [OP_VAR, 0, 0, k, TYPE_CODE[t]], t
+            if isinstance(e, C.Const):
+                img = _enc_const(self.ctx, e)
+                return [OP_CONST, img[1], img[2]], e.type
+            if isinstance(e, C.Math):
+                lw, lt = sel_prog(e.left)
+                rw, rt = sel_prog(e.right)
+                t = math_type(lt, rt)
+                return lw + rw + [OP_MATH, MATH_CODE[e.op], TYPE_CODE[t]], t
+            raise LoweringError(f"unsupported select expression {e}")
+
         for oa in q.select:
-            if not isinstance(oa.expr, C.Var):
-                raise LoweringError("only attribute projections are supported in select")
-            chain, idx, ai, t = self.resolve(oa.expr, -1, True)
-            select.append((chain, idx, self.ret_slot(self.states[chain].stream, ai), t))
-        if len(select) > MAX_SELECT:
+            w, t = sel_prog(oa.expr)
+            out_progs.append(w)
+            out_types.append(t)
+        if plain:
+            out_progs, out_types = [], []
+        if len(select) > MAX_SELECT or len(q.select) > MAX_SELECT:
             raise LoweringError("too many select attributes")
         nfa = FlatNFA(self.stype, within, 1 if self.ctx.app.playback else 0, 1 if self.ctx.partitioned else 0,
                       self.states, receivers, order, ro, uo, start_ids, self.retained, select,
                       column_layout(self.ctx))
+        nfa.out_progs, nfa.out_types = out_progs, out_types
         _classify(nfa, root, self)
         return nfa
 

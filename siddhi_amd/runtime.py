@@ -118,8 +118,15 @@ class _QueryRuntime:
         self.query_callbacks: List[QueryCallback] = []
 
     def _select_type(self, e):
+        if isinstance(e, C.Const):
+            return e.type
+        if isinstance(e, C.Math):      # ExpressionParser.parseArithmeticOperationResultType (:1413-1431)
+            try:
+                return L.math_type(self._select_type(e.left), self._select_type(e.right))
+            except L.LoweringError as x:
+                raise SiddhiAppCreationException(str(x)) from x
         if not isinstance(e, C.Var):
-            raise SiddhiAppCreationException("only attribute projections are supported in select")
+            raise SiddhiAppCreationException(f"unsupported select expression {e}")
         # resolve type by reference or attribute name (SelectorParser / parseVariable)
         elems = []
 
