@@ -135,10 +135,12 @@ typedef struct sg_nfa_desc {
   /* Select expressions (QuerySelector over math executors, C/query/selector/QuerySelector.java:125-163):
    * n_out > 0 -> output column k is the postfix program code[out_off[k] .. +out_len[k]) over the n_select
    * projected slots (VAR operands: word 3 = slot); matches then carry n_out values of type out_type[k].
-   * n_out == 0 -> the n_select projected slots are the output. */
+   * n_out == 0 -> the n_select projected slots are the output.
+   * having_len > 0 -> matches whose program code[having_off ..) over the output columns is not TRUE are
+   * dropped (QuerySelector.java:138-142); requires n_out > 0. */
   int32_t n_out;
   int32_t out_type[SG_MAX_SELECT], out_off[SG_MAX_SELECT], out_len[SG_MAX_SELECT];
-  int32_t reserved_out;
+  int32_t having_off, having_len;
 } sg_nfa_desc;
 
 typedef struct sg_options {

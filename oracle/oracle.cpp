@@ -154,7 +154,8 @@ static StreamEvent* get_stream_event(StateEvent* s, int chain, int idx) {
 struct StreamDef { std::vector<int> types; std::vector<int> names; int name_id; };
 
 enum ElemKind { E_STREAM = 1, E_ABSENT = 2, E_NEXT = 3, E_EVERY = 4, E_LOGICAL = 5, E_COUNT = 6 };
-enum ExprKind { X_CONST = 10, X_VAR = 11, X_CMP = 12, X_AND = 13, X_OR = 14, X_NOT = 15, X_ISNULL = 16, X_MATH = 17 };
+enum ExprKind { X_CONST = 10, X_VAR = 11, X_CMP = 12, X_AND = 13, X_OR = 14, X_NOT = 15, X_ISNULL = 16, X_MATH = 17,
+                X_OUT = 18 /* having: attribute of the output stream (HAVING_STATE) */ };
 
 struct Expr {
   int kind = 0;
@@ -184,6 +185,7 @@ struct App {
   std::vector<int> key_attr;  // per stream
   std::unique_ptr<Elem> root;
   std::vector<std::unique_ptr<Expr>> select;
+  std::unique_ptr<Expr> having;   // QuerySelector.havingConditionExecutor or null
 };
 
 struct Reader {
@@ -210,6 +212,7 @@ static std::unique_ptr<Expr> read_expr(Reader& r) {
     case X_AND: case X_OR: e->l = read_expr(r); e->r = read_expr(r); break;
     case X_NOT: case X_ISNULL: e->l = read_expr(r); break;
     case X_MATH: e->op = (int)r.next(); e->l = read_expr(r); e->r = read_expr(r); break;
+    case X_OUT: e->index = (int)r.next(); break;
     default: fail("bad expr kind");
   }
   return e;
@@ -254,6 +257,7 @@ static App read_app(const int64_t* img, int64_t n) {
   a.root = read_elem(r);
   int nsel = (int)r.next();
   for (int i = 0; i < nsel; i++) a.select.push_back(read_expr(r));
+  if (r.next()) a.having = read_expr(r);
   return a;
 }
 
@@ -311,6 +315,7 @@ static bool cmp_num(int op, const Val& l, const Val& r, int pt) {
 }
 
 static Val eval(const Expr* x, StateEvent* s);
+static const std::vector<Val>* g_out_vals = nullptr;   // output row under the having condition
 
 // Arithmetic (select expressions).  Result type: ExpressionParser.parseArithmeticOperationResultType
 // (C/util/parser/ExpressionParser.java:1413-1431), stored in x->vtype at resolution.  Executors
@@ -398,6 +403,7 @@ static Val eval(const Expr* x, StateEvent* s) {
     case X_NOT: return vbool(truth(eval(x->l.get(), s)) != 1);  // NotCondition...java:43-49
     case X_ISNULL: return vbool(eval(x->l.get(), s).null);
     case X_MATH: return eval_math(x, eval(x->l.get(), s), eval(x->r.get(), s));
+    case X_OUT: return (*g_out_vals)[x->index];
   }
   fail("eval: bad expr");
 }
@@ -967,6 +973,16 @@ void KeyRuntime::emit(const SE& s) {
   o.key = key;
   o.group = ((uint32_t)cur_phase << 24) | (cur_group & 0xFFFFFF);
   for (auto& x : e->app.select) o.vals.push_back(eval(x.get(), s.get()));   // SelectiveStateEventPopulator
+  bool keep = true;
+  if (e->app.having) {   // QuerySelector.processNoGroupBy: remove unless having is TRUE (QuerySelector.java:138-142)
+    g_out_vals = &o.vals;
+    keep = truth(eval(e->app.having.get(), s.get())) == 1;
+    g_out_vals = nullptr;
+  }
+  if (!keep) {
+    if (cur_phase == 0) cur_group++;
+    return;
+  }
   e->out.push_back(std::move(o));
   if (cur_phase == 0) cur_group++;   // every timer emission is its own callback (sendEvent per partial)
 }
@@ -1282,6 +1298,27 @@ static int select_type(Expr* x) {
   return 0;
 }
 
+static int having_type(Expr* x, const App& a) {
+  switch (x->kind) {
+    case X_OUT:
+      if (x->index < 0 || x->index >= (int)a.select.size()) fail("having: bad output index");
+      return select_type(a.select[x->index].get());
+    case X_CONST: return x->cval.type;
+    case X_MATH: {
+      int l = having_type(x->l.get(), a), r = having_type(x->r.get(), a);
+      if (l == T_STRING || l == T_BOOL || r == T_STRING || r == T_BOOL) fail("arithmetic on a non-numeric attribute");
+      x->vtype = promote_order(l, r);
+      return x->vtype;
+    }
+    case X_VAR: fail("having: only output attributes are supported");
+    default:
+      if (x->l) having_type(x->l.get(), a);
+      if (x->r) having_type(x->r.get(), a);
+      return T_BOOL;
+  }
+  return T_BOOL;
+}
+
 OrcHandle* orc_create(const int64_t* image, int64_t n, char* err, int errlen) {
   try {
     auto* h = new OrcHandle();
@@ -1304,6 +1341,7 @@ OrcHandle* orc_create(const int64_t* image, int64_t n, char* err, int errlen) {
       b.resolve(x.get(), -1, true);
       select_type(x.get());
     }
+    if (h->eng.app.having) having_type(h->eng.app.having.get(), h->eng.app);
     return h;
   } catch (Err& e) {
     if (err) snprintf(err, errlen, "%s", e.msg.c_str());

@@ -51,7 +51,7 @@ class sg_nfa_desc(ct.Structure):
                 ("shape", I32), ("shape_args", I32 * 8), ("shape_prog_off", I32), ("shape_prog_len", I32),
                 ("code_len", I32), ("code", I64 * SG_MAX_CODE),
                 ("n_out", I32), ("out_type", I32 * SG_MAX_SELECT), ("out_off", I32 * SG_MAX_SELECT),
-                ("out_len", I32 * SG_MAX_SELECT), ("reserved_out", I32)]
+                ("out_len", I32 * SG_MAX_SELECT), ("having_off", I32), ("having_len", I32)]
 
 
 class sg_options(ct.Structure):
@@ -155,6 +155,10 @@ def build_desc(nfa: L.FlatNFA) -> sg_nfa_desc:
         d.out_len[k] = len(w)
         d.out_type[k] = L.TYPE_CODE[t]
         code += w
+    if nfa.having_prog:
+        d.having_off = len(code)
+        d.having_len = len(nfa.having_prog)
+        code += nfa.having_prog
     if len(code) > SG_MAX_CODE:
         raise L.LoweringError("predicate programs too long")
     d.code_len = len(code)

@@ -153,6 +153,7 @@ class Query:
     input: StateInputStream
     select: List[OutputAttribute]
     output_stream: str
+    having: Optional[object] = None     # QuerySelector havingConditionExecutor (SelectorParser.java:98-100)
 
 
 @dataclass
@@ -199,7 +200,7 @@ _TOKEN_RE = re.compile(r"""
 
 _KEYWORDS = {"define", "stream", "from", "select", "insert", "into", "every", "within", "and", "or",
              "not", "for", "partition", "with", "of", "begin", "end", "is", "null", "true", "false",
-             "last", "as"}
+             "last", "as", "having"}
 
 _TIME_UNITS = {
     "millisecond": 1, "milliseconds": 1, "millisec": 1, "millisecs": 1, "ms": 1,
@@ -390,11 +391,12 @@ class _Parser:
             select.append(OutputAttribute(e, rename))
             if not self.accept(","):
                 break
+        having = self.expr() if self.accept("having") else None
         self.eat("insert")
         self.eat("into")
         out = self.ident()
         self.accept(";")
-        return Query(name, inp, select, out)
+        return Query(name, inp, select, out, having)
 
     # -- state input
     def state_input(self) -> StateInputStream:

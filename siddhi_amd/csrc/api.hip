@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include <rocprim/rocprim.hpp>
+
 #include "sg_engine.h"
 
 #define HIPCHK(x)                                                                                   \
@@ -32,8 +34,9 @@ struct SelReader {
   __device__ SgVal read(int, int, int slot, int type) { return sg_val_from_bits(vals[slot], type, (vnull >> slot) & 1); }
 };
 
+// keep (optional): 1 if the match survives `having`, for the compaction that follows.
 __global__ void k_select(int64_t n, const char* __restrict__ src, int sstride, char* __restrict__ dst, int dstride,
-                         const DevDesc* __restrict__ d) {
+                         const DevDesc* __restrict__ d, uint32_t* __restrict__ keep) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const char* r = src + (size_t)i * sstride;
@@ -46,29 +49,69 @@ __global__ void k_select(int64_t n, const char* __restrict__ src, int sstride, c
   ((uint64_t*)o)[2] = ((const uint64_t*)r)[2];   // key, group
   uint32_t vn = 0;
   const int nout = d->n_out;
+  int64_t* ov = (int64_t*)(o + 32);
   for (int k = 0; k < nout; ++k) {
     SgVal top;
     if (!sg_run(d->code + d->out_off[k], d->out_len[k], rd, top)) top.null = 1;
     if (top.null) vn |= 1u << k;
-    ((int64_t*)(o + 32))[k] = sg_val_bits(top);
+    ov[k] = sg_val_bits(top);
   }
   ((uint32_t*)o)[6] = vn;
   ((uint32_t*)o)[7] = 0;
+  if (keep) {
+    SelReader hr;
+    hr.vals = ov;
+    hr.vnull = vn;
+    keep[i] = sg_eval(d->code + d->having_off, d->having_len, hr) ? 1u : 0u;
+  }
+}
+
+// Stable compaction of the surviving matches (delivery order kept).
+__global__ void k_having_scatter(int64_t n, const char* __restrict__ src, const uint32_t* __restrict__ keep,
+                                 const uint32_t* __restrict__ pos, int stride, char* __restrict__ dst) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !keep[i]) return;
+  const uint64_t* s = (const uint64_t*)(src + (size_t)i * stride);
+  uint64_t* t = (uint64_t*)(dst + (size_t)pos[i] * stride);
+  for (int w = 0; w < stride / 8; ++w) t[w] = s[w];
 }
 
 // Engines append base records to h.stage (swapped in for the push); the select pass appends the output
-// records to h.out.
+// records (those passing `having`) to h.out.
 static void run_select(SgHandle& h) {
   const sg_nfa_desc& d = h.desc;
   hipStream_t st = h.stream;
   const int64_t n = h.stage.n;
-  if (n > 0) {
+  const int ostride = 32 + 8 * d.n_out;
+  const dim3 grd((unsigned)((n + 255) / 256)), blk(256);
+  if (n > 0 && d.having_len <= 0) {
     char* out = h.out.reserve(n, d.n_out, st);
-    const int ostride = 32 + 8 * d.n_out;
-    hipLaunchKernelGGL(k_select, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, (const char*)h.stage.rec,
-                       32 + 8 * d.n_select, out + (size_t)h.out.n * ostride, ostride, h.ddesc);
+    hipLaunchKernelGGL(k_select, grd, blk, 0, st, n, (const char*)h.stage.rec, 32 + 8 * d.n_select,
+                       out + (size_t)h.out.n * ostride, ostride, h.ddesc, (uint32_t*)nullptr);
     HIPCHK(hipGetLastError());
     h.out.n += n;
+  } else if (n > 0) {
+    char* tmp = (char*)h.ws.get("having_rec", (size_t)n * ostride, st);
+    uint32_t* keep = (uint32_t*)h.ws.get("having_keep", 4 * (size_t)(n + 1), st);
+    uint32_t* pos = (uint32_t*)h.ws.get("having_pos", 4 * (size_t)(n + 1), st);
+    HIPCHK(hipMemsetAsync(keep + n, 0, 4, st));
+    hipLaunchKernelGGL(k_select, grd, blk, 0, st, n, (const char*)h.stage.rec, 32 + 8 * d.n_select, tmp, ostride,
+                       h.ddesc, keep);
+    HIPCHK(hipGetLastError());
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, keep, pos, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+    void* tsc = h.ws.get("having_scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tsc, tb, keep, pos, 0u, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t kept = 0;
+    HIPCHK(hipMemcpyAsync(&kept, pos + n, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (kept) {
+      char* out = h.out.reserve(kept, d.n_out, st);
+      hipLaunchKernelGGL(k_having_scatter, grd, blk, 0, st, n, (const char*)tmp, keep, pos, ostride,
+                         out + (size_t)h.out.n * ostride);
+      HIPCHK(hipGetLastError());
+      h.out.n += kept;
+    }
   }
   h.stage.n = 0;
 }
@@ -96,6 +139,8 @@ static void validate(const sg_nfa_desc* d) {
   if (d->n_select < 0 || d->n_select > SG_MAX_SELECT) throw SgError(SG_EINVAL, "bad n_select");
   if (d->code_len < 0 || d->code_len > SG_MAX_CODE) throw SgError(SG_EINVAL, "bad code_len");
   if (d->n_out < 0 || d->n_out > SG_MAX_SELECT) throw SgError(SG_EINVAL, "bad n_out");
+  if (d->having_len > 0 && (d->n_out <= 0 || d->having_off < 0 || d->having_off + d->having_len > d->code_len))
+    throw SgError(SG_EINVAL, "bad having program");
   for (int k = 0; k < d->n_out; ++k)
     if (d->out_off[k] < 0 || d->out_len[k] < 1 || d->out_off[k] + d->out_len[k] > d->code_len)
       throw SgError(SG_EINVAL, "bad select program range");
@@ -391,7 +436,7 @@ static uint64_t query_fingerprint(const SgHandle& h) {
   }
   for (int c = 0; c < d.n_cols; ++c) { mix(d.col_type[c]); mix(d.col_stream[c]); }
   for (int k = 0; k < d.n_select; ++k) { mix(d.sel_state[k]); mix(d.sel_index[k]); mix(d.sel_ret[k]); }
-  mix(d.n_out);
+  mix(d.n_out); mix(d.having_off); mix(d.having_len);
   for (int k = 0; k < d.n_out; ++k) { mix(d.out_type[k]); mix(d.out_off[k]); mix(d.out_len[k]); }
   mix(d.code_len);
   for (int k = 0; k < d.code_len; ++k) mix(d.code[k]);

@@ -147,7 +147,39 @@ def oracle_image(ctx: QueryContext) -> List[int]:
     img += [len(q.select)]
     for oa in q.select:
         img += _enc_expr(ctx, oa.expr)
+    if q.having is None:
+        img += [0]
+    else:
+        img += [1] + _enc_having(ctx, q.having)
     return img
+
+
+def having_output_index(q, v) -> int:
+    """A `having` variable is an attribute of the query's output stream (HAVING_STATE resolution,
+    ExpressionParser.parseVariable, C/util/parser/ExpressionParser.java:1300-1310).  The reference falls back to
+    the input streams for names the output does not define; that fallback (and qualified eN.x references) is
+    refused here."""
+    names = [oa.rename for oa in q.select]
+    if v.stream_ref is not None or v.index is not None or v.attr not in names:
+        raise LoweringError(f"having may only reference output attributes {names}, not {v}")
+    return names.index(v.attr)
+
+
+def _enc_having(ctx: QueryContext, e) -> List[int]:
+    """Oracle image of a having expression: output attributes become [18, output index]."""
+    if isinstance(e, C.Var):
+        return [18, having_output_index(ctx.query, e)]
+    if isinstance(e, C.Const):
+        return _enc_const(ctx, e)
+    if isinstance(e, C.Compare):
+        return [12, CMP_CODE[e.op]] + _enc_having(ctx, e.left) + _enc_having(ctx, e.right)
+    if isinstance(e, (C.And, C.Or)):
+        return [13 if isinstance(e, C.And) else 14] + _enc_having(ctx, e.left) + _enc_having(ctx, e.right)
+    if isinstance(e, (C.Not, C.IsNull)):
+        return [15 if isinstance(e, C.Not) else 16] + _enc_having(ctx, e.expr)
+    if isinstance(e, C.Math):
+        return [17, MATH_CODE[e.op]] + _enc_having(ctx, e.left) + _enc_having(ctx, e.right)
+    raise LoweringError(f"unsupported expression in having: {e}")
 
 
 # ------------------------------------------------------------------------------ column layout
@@ -240,6 +272,7 @@ class FlatNFA:
     # empty when every output is a plain attribute (then `select` is the output)
     out_progs: list = field(default_factory=list)
     out_types: List[str] = field(default_factory=list)
+    having_prog: list = field(default_factory=list)   # postfix over the output columns (VAR word 3 = column)
 
 
 def _cmp_domain(lt: str, rt: str, op: str) -> int:
@@ -532,14 +565,38 @@ class _FlatBuilder:
             w, t = sel_prog(oa.expr)
             out_progs.append(w)
             out_types.append(t)
-        if plain:
+        having_prog = []
+        if q.having is not None:
+            def hav(e):
+                if isinstance(e, C.Var):
+                    k = having_output_index(q, e)
+                    return [OP_VAR, 0, 0, k, TYPE_CODE[out_types[k]]], out_types[k]
+                if isinstance(e, C.Const):
+                    img = _enc_const(self.ctx, e)
+                    return [OP_CONST, img[1], img[2]], e.type
+                if isinstance(e, C.Math):
+                    lw, lt = hav(e.left)
+                    rw, rt = hav(e.right)
+                    t = math_type(lt, rt)
+                    return lw + rw + [OP_MATH, MATH_CODE[e.op], TYPE_CODE[t]], t
+                if isinstance(e, C.Compare):
+                    lw, lt = hav(e.left)
+                    rw, rt = hav(e.right)
+                    return lw + rw + [OP_CMP, CMP_CODE[e.op], _cmp_domain(lt, rt, e.op)], "BOOL"
+                if isinstance(e, (C.And, C.Or)):
+                    return hav(e.left)[0] + hav(e.right)[0] + [OP_AND if isinstance(e, C.And) else OP_OR], "BOOL"
+                if isinstance(e, (C.Not, C.IsNull)):
+                    return hav(e.expr)[0] + [OP_NOT if isinstance(e, C.Not) else OP_ISNULL], "BOOL"
+                raise LoweringError(f"unsupported expression in having: {e}")
+            having_prog = hav(q.having)[0]
+        elif plain:
             out_progs, out_types = [], []
         if len(select) > MAX_SELECT or len(q.select) > MAX_SELECT:
             raise LoweringError("too many select attributes")
         nfa = FlatNFA(self.stype, within, 1 if self.ctx.app.playback else 0, 1 if self.ctx.partitioned else 0,
                       self.states, receivers, order, ro, uo, start_ids, self.retained, select,
                       column_layout(self.ctx))
-        nfa.out_progs, nfa.out_types = out_progs, out_types
+        nfa.out_progs, nfa.out_types, nfa.having_prog = out_progs, out_types, having_prog
         _classify(nfa, root, self)
         return nfa
 

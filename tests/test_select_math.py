@@ -167,6 +167,33 @@ def test_string_arithmetic_is_rejected():
         SiddhiManager(engine=OracleEngine).createSiddhiAppRuntime(app)
 
 
+HAVING_APP = EDGE_APP.replace("insert into M;", "having raw > 0 and not (f4 is null) or s4 == 0 insert into M;")
+
+
+def _expected_having():
+    out = []
+    for r in _expected_edge():
+        raw, f4, s4 = r[19], r[10], r[3]
+        if (raw is not None and raw > 0 and f4 is not None) or (s4 is not None and s4 == 0):
+            out.append(r)
+    return out
+
+
+def test_oracle_having_filters_output_rows():
+    """QuerySelector.processNoGroupBy drops rows whose having condition is not TRUE (QuerySelector.java:138-142);
+    having variables name output attributes (HAVING_STATE, ExpressionParser.java:1300-1310)."""
+    want = _expected_having()
+    assert 0 < len(want) < len(_expected_edge())
+    _assert_rows(_run_app(OracleEngine, HAVING_APP, EDGE_ROWS), want)
+
+
+def test_having_on_input_attribute_is_refused():
+    app = ("define stream S (a int); @info(name='q') from every e1=S -> e2=S select e1.a as x having e2.a > 1 "
+           "insert into M;")
+    with pytest.raises((SiddhiAppCreationException, L.LoweringError)):
+        SiddhiManager(engine=OracleEngine).createSiddhiAppRuntime(app)
+
+
 # ---- GPU: the select pass on every engine route, bit-exact with the oracle
 MATH_QUERIES = {
     "C2": synth.QUERIES["C2"].replace(
@@ -184,6 +211,46 @@ MATH_QUERIES = {
         "select e1.seq as seq1, e1.id as id1",
         "select e1.seq * 10 + e1.id as k, e1.id % 7 as m, e1.seq / 3 as t"),
 }
+
+
+HAVING_QUERIES = {
+    "C2": MATH_QUERIES["C2"].replace("insert into M;", "having dp > 5.0 or m < 1 insert into M;"),
+    "C1": synth.QUERIES["C1"].replace("insert into M;", "having p2 - p1 >= 2 insert into M;"),
+    "C3b": MATH_QUERIES["C3b"].replace("insert into M;", "having i3p is null and span > 0 insert into M;"),
+    "C4": MATH_QUERIES["C4"].replace("insert into M;", "having m == 3 insert into M;"),
+}
+
+
+@pytest.mark.gpu
+def test_gpu_having_edge_values():
+    from siddhi_amd._native import GpuEngine
+    _assert_rows(_run_app(GpuEngine, HAVING_APP, EDGE_ROWS), _expected_having())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,n,keys,rate,kw", [
+    ("C2", 400_000, 2_000, 1_000, {}),
+    ("C2", 100_000, 500, 100, {"force_general": True}),
+    ("C1", 200_000, 1, 1, {}),
+    ("C3b", 200_000, 500, 1_000, {}),
+    ("C4", 100_000, 10_000, 1, {}),
+], ids=["C2", "C2-general", "C1", "C3b", "C4"])
+def test_gpu_having_parity(cfg, n, keys, rate, kw):
+    from siddhi_amd._native import GpuEngine
+    b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
+    if cfg == "C4":
+        ts = np.append(b.ts, b.ts[-1] + 5001)
+        st = np.append(b.stream, np.int32(1)).astype(np.int32)
+        cols = [np.append(b.cols[0], 0), np.append(b.cols[1], 0), np.append(b.cols[2], 0).astype(np.int32)]
+        b = Batch(n + 1, 0, ts, st, np.zeros(n + 1, np.int32), cols, [None] * 3)
+    else:
+        b.key = dense_first_seen(b.key)
+    q = HAVING_QUERIES[cfg]
+    want = run_engine(OracleEngine, q, [b])
+    unfiltered = run_engine(OracleEngine, MATH_QUERIES.get(cfg, synth.QUERIES[cfg]), [b])
+    got = run_engine(lambda ctx: GpuEngine(ctx, **kw), q, [b])
+    assert 0 < len(want) < len(unfiltered)
+    assert_same(got, want)
 
 
 @pytest.mark.gpu
