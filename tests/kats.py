@@ -199,6 +199,56 @@ KATS = [
         sends=[("CustomerStream", 0, ["customerA"]), ("CustomerStream", 0, ["customerB"]),
                ("CustomerStream", 500, ["customerB"]), ("Tick", 1000, [1])],
         expect=[["customerA"]]),
+    # ---- absent-in-sequence (T/query/sequence/absent/AbsentSequenceTestCase.java), re-expressed in playback:
+    # ts = cumulative Thread.sleep, and the trailing TestUtil.waitForInEvents(500, cb, 10) (up to 5 s of wall
+    # clock for the timers) becomes a Tick event 5 s after the last send.
+    dict(  # B17 AbsentSequenceTestCase.java:38-69 (testQueryAbsent1)
+        name="B17_seq_then_absent_fires",
+        app="@app:playback " + S1_S2 + "define stream Tick (x int); @info(name = 'query1') "
+        "from e1=Stream1[price>20], not Stream2[price>e1.price] for 1 sec "
+        "select e1.symbol as symbol1 insert into OutputStream ;",
+        sends=[("Stream1", 0, ["WSO2", 55.6, 100]), ("Tick", 5000, [1])],
+        expect=[["WSO2"]], expect_ts=[1000]),
+    dict(  # B18 AbsentSequenceTestCase.java:71-106 (testQueryAbsent2): the timer fires before the late event
+        name="B18_seq_absent_then_late_event",
+        app="@app:playback " + S1_S2 + "define stream Tick (x int); @info(name = 'query1') "
+        "from e1=Stream1[price>20], not Stream2[price>e1.price] for 1 sec "
+        "select e1.symbol as symbol1 insert into OutputStream ;",
+        sends=[("Stream1", 0, ["WSO2", 55.6, 100]), ("Stream2", 1100, ["IBM", 58.7, 100]), ("Tick", 6100, [1])],
+        expect=[["WSO2"]]),
+    dict(  # B19 AbsentSequenceTestCase.java:108-143 (testQueryAbsent3): a matching Stream2 event kills it
+        name="B19_seq_absent_killed",
+        app="@app:playback " + S1_S2 + "define stream Tick (x int); @info(name = 'query1') "
+        "from e1=Stream1[price>20], not Stream2[price>e1.price] for 1 sec "
+        "select e1.symbol as symbol1 insert into OutputStream ;",
+        sends=[("Stream1", 0, ["WSO2", 55.6, 100]), ("Stream2", 100, ["IBM", 58.7, 100]), ("Tick", 5100, [1])],
+        expect=[]),
+    dict(  # B20 AbsentSequenceTestCase.java:145-180 (testQueryAbsent4): a non-matching Stream2 event does not
+        name="B20_seq_absent_not_killed",
+        app="@app:playback " + S1_S2 + "define stream Tick (x int); @info(name = 'query1') "
+        "from e1=Stream1[price>20], not Stream2[price>e1.price] for 1 sec "
+        "select e1.symbol as symbol1 insert into OutputStream ;",
+        sends=[("Stream1", 0, ["WSO2", 55.6, 100]), ("Stream2", 100, ["IBM", 50.7, 100]), ("Tick", 5100, [1])],
+        expect=[["WSO2"]]),
+    dict(  # B21 AbsentSequenceTestCase.java:329-368 (testQueryAbsent9): three states, killed by Stream3
+        name="B21_seq_two_then_absent_killed",
+        app="@app:playback " + S1_S2 + "define stream Stream3 (symbol string, price float, volume int); "
+        "define stream Tick (x int); @info(name = 'query1') "
+        "from e1=Stream1[price>10], e2=Stream2[price>20], not Stream3[price>30] for 1 sec "
+        "select e1.symbol as symbol1, e2.symbol as symbol2 insert into OutputStream ;",
+        sends=[("Stream1", 0, ["WSO2", 15.6, 100]), ("Stream2", 100, ["IBM", 28.7, 100]),
+               ("Stream3", 200, ["GOOGLE", 55.7, 100]), ("Tick", 5200, [1])],
+        expect=[]),
+    dict(  # B22 AbsentSequenceTestCase.java:370-410 (testQueryAbsent10): Stream3 below the threshold
+        name="B22_seq_two_then_absent_fires",
+        app="@app:playback " + S1_S2 + "define stream Stream3 (symbol string, price float, volume int); "
+        "define stream Tick (x int); @info(name = 'query1') "
+        "from e1=Stream1[price>10], e2=Stream2[price>20], not Stream3[price>30] for 1 sec "
+        "select e1.symbol as symbol1, e2.symbol as symbol2 insert into OutputStream ;",
+        sends=[("Stream1", 0, ["WSO2", 15.6, 100]), ("Stream2", 100, ["IBM", 28.7, 100]),
+               ("Stream3", 200, ["GOOGLE", 25.7, 100]), ("Tick", 5200, [1])],
+        expect=[["WSO2", "IBM"]]),
+
 ]
 
 
