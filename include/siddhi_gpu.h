@@ -158,7 +158,10 @@ typedef struct sg_options {
                                it (0 = chosen per push, -1 = one unit per key) */
   int32_t walker_only;      /* closed form, unpartitioned streams: 1 = always the chunked walker instead of the
                                per-candidate search (testing both paths) */
-  int32_t reserved[3];
+  int32_t ingress_rows;     /* host batches (on_device = 0) are copied and processed in chunks of this many rows,
+                               the copy of chunk k+1 overlapping the kernels of chunk k (<= 0: one copy); results
+                               are identical to one push.  no_carry handles never split. */
+  int32_t reserved[2];
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)
@@ -230,6 +233,9 @@ int sg_snapshot(sg_handle* h, void* buf, size_t cap, size_t* size);
 int sg_restore(sg_handle* h, const void* buf, size_t size);
 int sg_close(sg_handle* h);
 const char* sg_last_error(const sg_handle* h);
+/* Pinned host memory for batch columns (the ingress then copies asynchronously at full PCIe rate). */
+int sg_host_alloc(size_t bytes, void** p);
+int sg_host_free(void* p);
 const char* sg_version(void);
 
 #ifdef __cplusplus

@@ -18,7 +18,7 @@ SG_ABI_VERSION = 1
 
 SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
            "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version",
-           "sg_snapshot", "sg_restore"]
+           "sg_snapshot", "sg_restore", "sg_host_alloc", "sg_host_free"]
 
 I32, I64, U64 = ct.c_int32, ct.c_int64, ct.c_uint64
 
@@ -57,7 +57,8 @@ class sg_nfa_desc(ct.Structure):
 class sg_options(ct.Structure):
     _fields_ = [("max_batch", I64), ("pool_partials", I32), ("pool_events", I32), ("pool_chain", I32),
                 ("list_cap", I32), ("force_general", I32), ("no_carry", I32), ("ring_cap", I32),
-                ("chunk_rows", I32), ("walker_only", I32), ("reserved", I32 * 3)]
+                ("chunk_rows", I32), ("walker_only", I32), ("ingress_rows", I32),
+                ("reserved", I32 * 2)]
 
 
 class sg_batch(ct.Structure):
@@ -113,6 +114,8 @@ def load_library(path: str = LIB_PATH):
         lib.sg_close.argtypes = [P]
         lib.sg_snapshot.argtypes = [P, P, ct.c_size_t, ct.POINTER(ct.c_size_t)]
         lib.sg_restore.argtypes = [P, P, ct.c_size_t]
+        lib.sg_host_alloc.argtypes = [ct.c_size_t, ct.POINTER(P)]
+        lib.sg_host_free.argtypes = [P]
         lib.sg_last_error.argtypes = [P]
         lib.sg_last_error.restype = ct.c_char_p
         lib.sg_version.restype = ct.c_char_p
@@ -286,6 +289,26 @@ class Handle:
             pass
 
 
+class PinnedArray:
+    """A numpy array over pinned host memory from sg_host_alloc (freed with the object)."""
+
+    def __init__(self, n: int, dtype):
+        self.lib = load_library()
+        self.p = ct.c_void_p()
+        dt = np.dtype(dtype)
+        rc = self.lib.sg_host_alloc(max(n, 1) * dt.itemsize, ct.byref(self.p))
+        if rc != 0:
+            raise SgError(rc, "sg_host_alloc failed")
+        buf = (ct.c_char * (max(n, 1) * dt.itemsize)).from_address(self.p.value)
+        self.array = np.frombuffer(buf, dtype=dt, count=n)
+
+    def __del__(self):
+        if getattr(self, "p", None) and self.p.value:
+            self.array = None
+            self.lib.sg_host_free(self.p)
+            self.p = ct.c_void_p()
+
+
 def make_batch(n, base_index, ts, stream, key, cols, nulls, on_device, key_bound=0, keep=None, index=0):
     """Assemble an sg_batch from raw pointers (ints); `keep` collects ctypes arrays to keep alive."""
     ncol = len(cols)
@@ -301,7 +324,8 @@ class GpuEngine:
     """Engine interface (see siddhi_amd/runtime.py) on the MI355X kernels."""
 
     def __init__(self, ctx: L.QueryContext, device: int = 0, force_general: bool = False, pool: int = 0,
-                 no_carry: bool = False, ring_cap: int = 0, chunk_rows: int = 0, walker_only: bool = False):
+                 no_carry: bool = False, ring_cap: int = 0, chunk_rows: int = 0, walker_only: bool = False,
+                 ingress_rows: int = 0):
         self.ctx = ctx
         self.nfa = L.lower(ctx)
         self.desc = build_desc(self.nfa)
@@ -311,6 +335,7 @@ class GpuEngine:
         opts.ring_cap = ring_cap
         opts.chunk_rows = chunk_rows
         opts.walker_only = 1 if walker_only else 0
+        opts.ingress_rows = ingress_rows
         if pool:
             opts.pool_partials = opts.pool_events = opts.pool_chain = opts.list_cap = pool
         self.handle = Handle(self.desc, device, opts)

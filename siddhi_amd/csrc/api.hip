@@ -153,6 +153,87 @@ static void validate(const sg_nfa_desc* d) {
     if (d->ret_col[r] < 0 || d->ret_col[r] >= d->n_cols) throw SgError(SG_EINVAL, "retained column out of range");
 }
 
+// One push of rows already in HBM: the engine route, then the select pass.
+static void push_view(SgHandle& h, BatchView& bv, int64_t n) {
+  const sg_nfa_desc& d = h.desc;
+  for (int r = 0; r < d.n_ret; ++r)
+    if (!bv.cols.col[d.ret_col[r]]) throw SgError(SG_EINVAL, "batch is missing a column the query reads");
+  int shape = h.opt.force_general ? SG_SHAPE_GENERAL : d.shape;
+  const bool sel = d.n_out > 0;
+  if (sel) std::swap(h.out, h.stage);   // engines append base records to the stage
+  try {
+    switch (shape) {
+      case SG_SHAPE_EVERY_NEXT_CMP:
+        sg_run_every_next(&h, bv, n);
+        break;
+      case SG_SHAPE_EVERY_ABSENT_EQ:
+        sg_run_every_absent(&h, bv, n);
+        break;
+      default:
+        sg_run_general(&h, bv, n);
+    }
+  } catch (...) {
+    if (sel) { std::swap(h.out, h.stage); h.stage.n = 0; }
+    throw;
+  }
+  if (sel) {
+    std::swap(h.out, h.stage);
+    run_select(h);
+  }
+  h.pushes++;
+}
+
+static std::string slot_name(const char* what, int c, int slot) {
+  char nm[48];
+  snprintf(nm, sizeof nm, "in_%s%d#%d", what, c, slot);
+  return nm;
+}
+
+static void reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int slot) {
+  const sg_nfa_desc& d = h.desc;
+  h.ws.get(slot_name("ts", 0, slot), 8 * rows, h.stream);
+  if (b->stream) h.ws.get(slot_name("stream", 0, slot), 4 * rows, h.stream);
+  if (b->key) h.ws.get(slot_name("key", 0, slot), 4 * rows, h.stream);
+  if (b->index) h.ws.get(slot_name("index", 0, slot), 8 * rows, h.stream);
+  for (int c = 0; c < d.n_cols; ++c) {
+    if (b->cols && b->cols[c]) h.ws.get(slot_name("col", c, slot), (size_t)col_width(d.col_type[c]) * rows, h.stream);
+    if (b->nulls && b->nulls[c]) h.ws.get(slot_name("nul", c, slot), rows, h.stream);
+  }
+}
+
+// Copy rows [lo, lo + cnt) of a host batch into HBM slot `slot` on stream `st`; returns the device view.
+static BatchView upload(SgHandle& h, const sg_batch* b, int64_t lo, int64_t cnt, int slot, hipStream_t st) {
+  const sg_nfa_desc& d = h.desc;
+  BatchView bv;
+  bv.n = cnt;
+  bv.base_index = b->base_index + (uint64_t)lo;
+  bv.key_bound = b->key_bound;
+  memset(&bv.cols, 0, sizeof(bv.cols));
+  auto up = [&](const char* what, int c, const void* src, size_t width) -> void* {
+    if (!src) return nullptr;
+    void* p = h.ws.get(slot_name(what, c, slot), width * cnt, h.stream);
+    HIPCHK(hipMemcpyAsync(p, (const char*)src + width * lo, width * cnt, hipMemcpyHostToDevice, st));
+    return p;
+  };
+  bv.ts = (const int64_t*)up("ts", 0, b->ts, 8);
+  bv.stream = (const int32_t*)up("stream", 0, b->stream, 4);
+  bv.key = (const int32_t*)up("key", 0, b->key, 4);
+  bv.index = (const uint64_t*)up("index", 0, b->index, 8);
+  for (int c = 0; c < d.n_cols; ++c) {
+    bv.cols.col[c] = b->cols ? up("col", c, b->cols[c], (size_t)col_width(d.col_type[c])) : nullptr;
+    bv.cols.nul[c] = (const uint8_t*)(b->nulls ? up("nul", c, b->nulls[c], 1) : nullptr);
+  }
+  return bv;
+}
+
+// Pinned host memory for batches (cudaHostAlloc-style): the ingress copies from it run asynchronously at
+// full PCIe rate, overlapped with the previous chunk's kernels.
+extern "C" int sg_host_alloc(size_t bytes, void** p) {
+  if (!p) return SG_EINVAL;
+  return hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? SG_OK : SG_EHIP;
+}
+extern "C" int sg_host_free(void* p) { return hipHostFree(p) == hipSuccess ? SG_OK : SG_EHIP; }
+
 extern "C" {
 
 const char* sg_version(void) { return "siddhi_gpu 0.1 (gfx950)"; }
@@ -199,65 +280,61 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
     if (n <= 0) return;
     if (n >= (1ll << 30) - 1) throw SgError(SG_EINVAL, "batch too large (max 2^30-2 rows)");
     if (!b->ts) throw SgError(SG_EINVAL, "batch without timestamps");
-    BatchView bv;
-    bv.n = n;
-    bv.base_index = b->base_index;
-    bv.key_bound = b->key_bound;
-    memset(&bv.cols, 0, sizeof(bv.cols));
-    hipStream_t st = h.stream;
     if (b->on_device) {
+      BatchView bv;
+      bv.n = n;
+      bv.base_index = b->base_index;
+      bv.key_bound = b->key_bound;
       bv.ts = b->ts;
       bv.stream = b->stream;
       bv.key = b->key;
       bv.index = b->index;
+      memset(&bv.cols, 0, sizeof(bv.cols));
       for (int c = 0; c < d.n_cols; ++c) {
         bv.cols.col[c] = b->cols ? b->cols[c] : nullptr;
         bv.cols.nul[c] = b->nulls ? b->nulls[c] : nullptr;
       }
-    } else {
-      auto up = [&](const char* name, const void* src, size_t bytes) -> void* {
-        if (!src) return nullptr;
-        void* p = h.ws.get(name, bytes, st);
-        HIPCHK(hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, st));
-        return p;
-      };
-      bv.ts = (const int64_t*)up("in_ts", b->ts, sizeof(int64_t) * n);
-      bv.stream = (const int32_t*)up("in_stream", b->stream, sizeof(int32_t) * n);
-      bv.key = (const int32_t*)up("in_key", b->key, sizeof(int32_t) * n);
-      bv.index = (const uint64_t*)up("in_index", b->index, sizeof(uint64_t) * n);
-      for (int c = 0; c < d.n_cols; ++c) {
-        char nm[32];
-        snprintf(nm, sizeof nm, "in_col%d", c);
-        bv.cols.col[c] = b->cols ? up(nm, b->cols[c], (size_t)col_width(d.col_type[c]) * n) : nullptr;
-        snprintf(nm, sizeof nm, "in_nul%d", c);
-        bv.cols.nul[c] = (const uint8_t*)(b->nulls ? up(nm, b->nulls[c], (size_t)n) : nullptr);
+      push_view(h, bv, n);
+      return;
+    }
+    // host batch: ingress in chunks (replacing StreamJunction's per-row fan-out,
+    // C/stream/StreamJunction.java:255-316).  Chunk k+1 is copied on a second HIP stream into the other of
+    // two HBM slots while chunk k runs on the handle's stream; consecutive chunks are consecutive sub-pushes,
+    // which the carried state makes identical to one push (no_carry handles are therefore never split).
+    // Opt-in (measured): per-chunk engine overheads currently exceed the overlap won.
+    int64_t C = h.opt.ingress_rows > 0 ? h.opt.ingress_rows : n;
+    if (h.opt.no_carry || n <= C) C = n;
+    const int64_t nch = (n + C - 1) / C;
+    if (nch == 1) {
+      BatchView bv = upload(h, b, 0, n, 0, h.stream);
+      push_view(h, bv, n);
+      return;
+    }
+    if (!h.copy_stream) {
+      HIPCHK(hipStreamCreateWithFlags(&h.copy_stream, hipStreamNonBlocking));
+      for (int k = 0; k < 2; ++k) {
+        HIPCHK(hipEventCreateWithFlags(&h.ev_copied[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h.ev_consumed[k], hipEventDisableTiming));
       }
     }
-    for (int r = 0; r < d.n_ret; ++r)
-      if (!bv.cols.col[d.ret_col[r]]) throw SgError(SG_EINVAL, "batch is missing a column the query reads");
-    int shape = h.opt.force_general ? SG_SHAPE_GENERAL : d.shape;
-    const bool sel = d.n_out > 0;
-    if (sel) std::swap(h.out, h.stage);   // engines append base records to the stage
-    try {
-      switch (shape) {
-        case SG_SHAPE_EVERY_NEXT_CMP:
-          sg_run_every_next(&h, bv, n);
-          break;
-        case SG_SHAPE_EVERY_ABSENT_EQ:
-          sg_run_every_absent(&h, bv, n);
-          break;
-        default:
-          sg_run_general(&h, bv, n);
+    for (int s = 0; s < 2; ++s) reserve_slot(h, b, C, s);   // no workspace growth inside the pipeline
+    BatchView cur = upload(h, b, 0, C, 0, h.copy_stream);
+    HIPCHK(hipEventRecord(h.ev_copied[0], h.copy_stream));
+    for (int64_t k = 0; k < nch; ++k) {
+      const int64_t lo = k * C, cnt = std::min(C, n - lo);
+      BatchView next;
+      if (k + 1 < nch) {
+        const int s = (int)((k + 1) & 1);
+        if (k + 1 >= 2) HIPCHK(hipStreamWaitEvent(h.copy_stream, h.ev_consumed[s], 0));
+        next = upload(h, b, lo + C, std::min(C, n - lo - C), s, h.copy_stream);
+        HIPCHK(hipEventRecord(h.ev_copied[s], h.copy_stream));
       }
-    } catch (...) {
-      if (sel) { std::swap(h.out, h.stage); h.stage.n = 0; }
-      throw;
+      HIPCHK(hipStreamWaitEvent(h.stream, h.ev_copied[k & 1], 0));
+      push_view(h, cur, cnt);
+      HIPCHK(hipEventRecord(h.ev_consumed[k & 1], h.stream));
+      if (k + 1 < nch) cur = next;
     }
-    if (sel) {
-      std::swap(h.out, h.stage);
-      run_select(h);
-    }
-    h.pushes++;
+    HIPCHK(hipStreamSynchronize(h.copy_stream));
   });
 }
 
@@ -407,6 +484,11 @@ int sg_close(sg_handle* hh) {
   h.ws.release();
   h.out.release();
   h.stage.release();
+  if (h.copy_stream) {
+    hipStreamSynchronize(h.copy_stream);
+    hipStreamDestroy(h.copy_stream);
+    for (int k = 0; k < 2; ++k) { hipEventDestroy(h.ev_copied[k]); hipEventDestroy(h.ev_consumed[k]); }
+  }
   if (h.ddesc) hipFree(h.ddesc);
   for (auto& e : h.ev) if (e) hipEventDestroy(e);
   if (h.own_stream && h.stream) hipStreamDestroy(h.stream);

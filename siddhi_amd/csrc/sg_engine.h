@@ -98,6 +98,8 @@ struct SgHandle {
   OutStore stage;             // base records of the running push when select expressions follow (desc.n_out > 0)
   std::string err;
   hipEvent_t ev[8] = {};
+  hipStream_t copy_stream = nullptr;            // host-batch ingress (sg_push, on_device = 0)
+  hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
   int64_t last_events = 0, last_matches = 0, last_spilled = 0;
   int pushes = 0;
   int64_t clock = 0;          // playback clock (TimestampGeneratorImpl.lastEventTimestamp)
