@@ -28,7 +28,34 @@ CASES = {
     "c3c": ("C3c", 40_000, 200, 20),
     "c4": ("C4", 8_000, 3_000, 1),
     "c5": ("C5", 60_000, 5_000, 200),
+    # select arithmetic + having (QuerySelector over the math executors)
+    "c2_sel": ("C2", 40_000, 200, 20),
+    "c3b_sel": ("C3b", 40_000, 200, 100),
+    "c4_sel": ("C4", 8_000, 3_000, 1),
 }
+
+# query text per case (default: the config's query, siddhi_amd/synth.py)
+SELECT_QUERIES = {
+    "c2_sel": ("define stream StockStream (id long, symbol string, price float); "
+               "partition with (symbol of StockStream) begin @info(name='q') "
+               "from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec "
+               "select e1.id as id1, e2.id - e1.id as gap, e2.price - e1.price as dp, e2.price / e1.price as ratio, "
+               "(e2.price * 100) % 7 as m having dp > 5.0 or m < 1 insert into M; end;"),
+    "c3b_sel": ("define stream S (id long, symbol string, v int, w int); "
+                "partition with (symbol of S) begin @info(name='q') "
+                "from every e1=S[v>500], e2=S[v>e1.v]<1:5>, e3=S[v<e1.v] or e4=S[w<e1.w] "
+                "select e1.id as i1, e2[last].id - e2[0].id as span, e3.id + 1 as i3p, e4.id * 2 as i4d, "
+                "e2[last].v - e1.v as dv, e1.w / (e1.v - 500) as q having i3p is null and span > 0 "
+                "insert into M; end;"),
+    "c4_sel": ("@app:playback define stream S (id long, seq long); define stream Tick (x int); "
+               "@info(name='q') from every e1=S -> not S[id==e1.id] for 5 sec "
+               "select e1.seq * 10 + e1.id as k, e1.id % 7 as m, e1.seq / 3 as t having m == 3 insert into M;"),
+}
+
+
+def query_of(name):
+    from siddhi_amd import synth
+    return SELECT_QUERIES.get(name) or synth.QUERIES[CASES[name][0]]
 
 
 def golden_batch(cfg, n, keys, rate):
@@ -65,19 +92,21 @@ def load(name):
     n = len(z["ts"])
     b = Batch(n, 0, z["ts"], z["stream"], z["key"], cols, [None] * len(cols))
     want = Outputs(*[z["out_" + f] for f in ("trigger", "ts", "key", "group", "vals", "vnull")])
-    return synth.QUERIES[cfg], b, want
+    return query_of(name), b, want
 
 
-def main():
+def main(only=None):
     from oracle import OracleEngine
     from parity_util import run_engine
     from siddhi_amd import synth
     for name, (cfg, n, keys, rate) in CASES.items():
         b = golden_batch(cfg, n, keys, rate)
-        out = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
+        if only and name not in only:
+            continue
+        out = run_engine(OracleEngine, query_of(name), [b])
         save(name, cfg, b, out)
         print(f"{name}: {cfg} {n} events -> {len(out)} matches")
 
 
 if __name__ == "__main__":
-    main()
+    main(set(sys.argv[1:]) or None)    # optional case names: regenerate only those

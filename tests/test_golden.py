@@ -49,5 +49,5 @@ def test_gpu_reproduces_golden(name):
 def test_gpu_general_kernel_reproduces_golden(name):
     from siddhi_amd._native import GpuEngine
     q, b, want = G.load(name)
-    pool = 16384 if name == "c4" else 0     # C4: thousands of live partials on one key
+    pool = 16384 if name.startswith("c4") else 0     # C4: thousands of live partials on one key
     assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, pool=pool), q, [b]), want)
