@@ -1028,30 +1028,32 @@ struct CarryBufs {
   uint8_t* nul[SG_MAX_COLS];
 };
 
+// one thread per carried row (coalesced writes; a key's suffix is found by binary search over the key offsets,
+// so keys with long suffixes no longer serialise one lane)
 template <class T, bool N>
-__global__ void k_carry_copy(Src<T, N> src, uint32_t K, const uint32_t* __restrict__ q0s,
-                             const uint32_t* __restrict__ ns, const uint32_t* __restrict__ offs, int n_cols,
-                             const int32_t* __restrict__ widths, SgCols bc, SgCols cc, CarryBufs dst) {
-  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  uint32_t n = ns[k];
-  if (!n) return;
+__global__ void k_carry_copy(Src<T, N> src, uint32_t K, uint32_t ncar, const uint32_t* __restrict__ q0s,
+                             const uint32_t* __restrict__ offs, int n_cols, const int32_t* __restrict__ widths,
+                             SgCols bc, SgCols cc, CarryBufs dst) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= ncar) return;
+  uint32_t lo = 0, hi = K;   // last key k with offs[k] <= d (offs: exclusive scan of the suffix lengths)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (offs[mid] <= d) lo = mid;
+    else hi = mid;
+  }
   const Virt& v = src.pk.v;
-  uint32_t q0 = q0s[k], o = offs[k];
-  for (uint32_t q = 0; q < n; ++q) {
-    uint32_t r = src.row(q0 + q);
-    uint32_t d = o + q;
-    dst.ts[d] = v_ts(v, r);
-    dst.key[d] = r < v.nc ? v.c_key[r] : (v.key ? v.key[r - v.nc] : 0);
-    dst.flags[d] = (uint8_t)v_flags(v, r);
-    for (int c = 0; c < n_cols; ++c) {
-      const SgCols& s = r < v.nc ? cc : bc;
-      uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
-      if (!s.col[c]) continue;
-      if (widths[c] == 8) ((int64_t*)dst.col[c])[d] = ((const int64_t*)s.col[c])[rr];
-      else ((int32_t*)dst.col[c])[d] = ((const int32_t*)s.col[c])[rr];
-      dst.nul[c][d] = s.nul[c] ? s.nul[c][rr] : 0;
-    }
+  const uint32_t r = src.row(q0s[lo] + (d - offs[lo]));
+  dst.ts[d] = v_ts(v, r);
+  dst.key[d] = r < v.nc ? v.c_key[r] : (v.key ? v.key[r - v.nc] : 0);
+  dst.flags[d] = (uint8_t)v_flags(v, r);
+  const SgCols& s = r < v.nc ? cc : bc;
+  const uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
+  for (int c = 0; c < n_cols; ++c) {
+    if (!s.col[c]) continue;
+    if (widths[c] == 8) ((int64_t*)dst.col[c])[d] = ((const int64_t*)s.col[c])[rr];
+    else ((int32_t*)dst.col[c])[d] = ((const int32_t*)s.col[c])[rr];
+    dst.nul[c][d] = s.nul[c] ? s.nul[c][rr] : 0;
   }
 }
 
@@ -1795,7 +1797,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     cb.flags = nx.flags;
     for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
     if (ncar)
-      hipLaunchKernelGGL((k_carry_copy<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n,
+      hipLaunchKernelGGL((k_carry_copy<T, N>), dim3((ncar + 255) / 256), dim3(256), 0, st, src, K, ncar, carry_q0,
                          coff, d.n_cols, widths, bv.cols, cc, cb);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
