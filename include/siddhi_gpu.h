@@ -159,8 +159,9 @@ typedef struct sg_options {
   int32_t walker_only;      /* closed form, unpartitioned streams: 1 = always the chunked walker instead of the
                                per-candidate search (testing both paths) */
   int32_t ingress_rows;     /* host batches (on_device = 0) are copied and processed in chunks of this many rows,
-                               the copy of chunk k+1 overlapping the kernels of chunk k (<= 0: one copy); results
-                               are identical to one push.  no_carry handles never split. */
+                               the copy of chunk k+1 overlapping the kernels of chunk k (0: 4 chunks for batches of
+                               >= 32M rows, else one copy; -1: one copy); results are identical to one push.
+                               no_carry handles never split. */
   int32_t reserved[2];
 } sg_options;
 

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rocprim/rocprim.hpp>
@@ -189,41 +190,58 @@ static std::string slot_name(const char* what, int c, int slot) {
   return nm;
 }
 
-static void reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int slot) {
+// Device buffers of one ingress slot (resolved on the calling thread: the workspace map is not thread-safe).
+struct SlotPtrs {
+  void* ts = nullptr;
+  void* stream = nullptr;
+  void* key = nullptr;
+  void* index = nullptr;
+  void* col[SG_MAX_COLS] = {};
+  void* nul[SG_MAX_COLS] = {};
+};
+
+static SlotPtrs reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int slot) {
   const sg_nfa_desc& d = h.desc;
-  h.ws.get(slot_name("ts", 0, slot), 8 * rows, h.stream);
-  if (b->stream) h.ws.get(slot_name("stream", 0, slot), 4 * rows, h.stream);
-  if (b->key) h.ws.get(slot_name("key", 0, slot), 4 * rows, h.stream);
-  if (b->index) h.ws.get(slot_name("index", 0, slot), 8 * rows, h.stream);
+  SlotPtrs p;
+  p.ts = h.ws.get(slot_name("ts", 0, slot), 8 * rows, h.stream);
+  if (b->stream) p.stream = h.ws.get(slot_name("stream", 0, slot), 4 * rows, h.stream);
+  if (b->key) p.key = h.ws.get(slot_name("key", 0, slot), 4 * rows, h.stream);
+  if (b->index) p.index = h.ws.get(slot_name("index", 0, slot), 8 * rows, h.stream);
   for (int c = 0; c < d.n_cols; ++c) {
-    if (b->cols && b->cols[c]) h.ws.get(slot_name("col", c, slot), (size_t)col_width(d.col_type[c]) * rows, h.stream);
-    if (b->nulls && b->nulls[c]) h.ws.get(slot_name("nul", c, slot), rows, h.stream);
+    if (b->cols && b->cols[c])
+      p.col[c] = h.ws.get(slot_name("col", c, slot), (size_t)col_width(d.col_type[c]) * rows, h.stream);
+    if (b->nulls && b->nulls[c]) p.nul[c] = h.ws.get(slot_name("nul", c, slot), rows, h.stream);
   }
+  return p;
 }
 
-// Copy rows [lo, lo + cnt) of a host batch into HBM slot `slot` on stream `st`; returns the device view.
-static BatchView upload(SgHandle& h, const sg_batch* b, int64_t lo, int64_t cnt, int slot, hipStream_t st) {
-  const sg_nfa_desc& d = h.desc;
+// Copy rows [lo, lo + cnt) of a host batch into a slot on stream `st`; returns the device view.  Touches no
+// handle state besides the descriptor, so it may run on a helper thread.
+static BatchView upload_to(const sg_nfa_desc& d, const SlotPtrs& p, const sg_batch* b, int64_t lo, int64_t cnt,
+                           hipStream_t st) {
   BatchView bv;
   bv.n = cnt;
   bv.base_index = b->base_index + (uint64_t)lo;
   bv.key_bound = b->key_bound;
   memset(&bv.cols, 0, sizeof(bv.cols));
-  auto up = [&](const char* what, int c, const void* src, size_t width) -> void* {
+  auto up = [&](void* dst, const void* src, size_t width) -> void* {
     if (!src) return nullptr;
-    void* p = h.ws.get(slot_name(what, c, slot), width * cnt, h.stream);
-    HIPCHK(hipMemcpyAsync(p, (const char*)src + width * lo, width * cnt, hipMemcpyHostToDevice, st));
-    return p;
+    HIPCHK(hipMemcpyAsync(dst, (const char*)src + width * lo, width * cnt, hipMemcpyHostToDevice, st));
+    return dst;
   };
-  bv.ts = (const int64_t*)up("ts", 0, b->ts, 8);
-  bv.stream = (const int32_t*)up("stream", 0, b->stream, 4);
-  bv.key = (const int32_t*)up("key", 0, b->key, 4);
-  bv.index = (const uint64_t*)up("index", 0, b->index, 8);
+  bv.ts = (const int64_t*)up(p.ts, b->ts, 8);
+  bv.stream = (const int32_t*)up(p.stream, b->stream, 4);
+  bv.key = (const int32_t*)up(p.key, b->key, 4);
+  bv.index = (const uint64_t*)up(p.index, b->index, 8);
   for (int c = 0; c < d.n_cols; ++c) {
-    bv.cols.col[c] = b->cols ? up("col", c, b->cols[c], (size_t)col_width(d.col_type[c])) : nullptr;
-    bv.cols.nul[c] = (const uint8_t*)(b->nulls ? up("nul", c, b->nulls[c], 1) : nullptr);
+    bv.cols.col[c] = b->cols ? up(p.col[c], b->cols[c], (size_t)col_width(d.col_type[c])) : nullptr;
+    bv.cols.nul[c] = (const uint8_t*)(b->nulls ? up(p.nul[c], b->nulls[c], 1) : nullptr);
   }
   return bv;
+}
+
+static BatchView upload(SgHandle& h, const sg_batch* b, int64_t lo, int64_t cnt, int slot, hipStream_t st) {
+  return upload_to(h.desc, reserve_slot(h, b, cnt, slot), b, lo, cnt, st);
 }
 
 // Pinned host memory for batches (cudaHostAlloc-style): the ingress copies from it run asynchronously at
@@ -301,8 +319,10 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
     // C/stream/StreamJunction.java:255-316).  Chunk k+1 is copied on a second HIP stream into the other of
     // two HBM slots while chunk k runs on the handle's stream; consecutive chunks are consecutive sub-pushes,
     // which the carried state makes identical to one push (no_carry handles are therefore never split).
-    // Opt-in (measured): per-chunk engine overheads currently exceed the overlap won.
-    int64_t C = h.opt.ingress_rows > 0 ? h.opt.ingress_rows : n;
+    // Default (measured): batches of >= 32M rows in 4 chunks (copy-bound: 59.0 -> 55.1 ms per
+    // 100M C2 events); smaller chunks lose to per-sub-push kernel overheads, smaller batches are one copy.
+    int64_t C = h.opt.ingress_rows > 0 ? h.opt.ingress_rows : (n >= ((int64_t)32 << 20) ? (n + 3) / 4 : n);
+    if (h.opt.ingress_rows < 0) C = n;
     if (h.opt.no_carry || n <= C) C = n;
     const int64_t nch = (n + C - 1) / C;
     if (nch == 1) {
@@ -317,21 +337,41 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
         HIPCHK(hipEventCreateWithFlags(&h.ev_consumed[k], hipEventDisableTiming));
       }
     }
-    for (int s = 0; s < 2; ++s) reserve_slot(h, b, C, s);   // no workspace growth inside the pipeline
-    BatchView cur = upload(h, b, 0, C, 0, h.copy_stream);
+    SlotPtrs slots[2];
+    for (int s = 0; s < 2; ++s) slots[s] = reserve_slot(h, b, C, s);   // no workspace growth inside the pipeline
+    BatchView cur = upload_to(d, slots[0], b, 0, C, h.copy_stream);
     HIPCHK(hipEventRecord(h.ev_copied[0], h.copy_stream));
+    // The next chunk's copies are issued from a helper thread: a large hipMemcpyAsync can hold the calling
+    // thread, which would otherwise delay this chunk's kernels (measured).
     for (int64_t k = 0; k < nch; ++k) {
       const int64_t lo = k * C, cnt = std::min(C, n - lo);
       BatchView next;
+      std::thread copier;
+      int copy_rc = hipSuccess;
       if (k + 1 < nch) {
         const int s = (int)((k + 1) & 1);
         if (k + 1 >= 2) HIPCHK(hipStreamWaitEvent(h.copy_stream, h.ev_consumed[s], 0));
-        next = upload(h, b, lo + C, std::min(C, n - lo - C), s, h.copy_stream);
-        HIPCHK(hipEventRecord(h.ev_copied[s], h.copy_stream));
+        copier = std::thread([&, s, lo] {
+          try {
+            if (hipSetDevice(h.device) != hipSuccess) { copy_rc = hipErrorInvalidDevice; return; }
+            next = upload_to(d, slots[s], b, lo + C, std::min(C, n - lo - C), h.copy_stream);
+            copy_rc = hipEventRecord(h.ev_copied[s], h.copy_stream);
+          } catch (...) {
+            copy_rc = hipErrorUnknown;
+          }
+        });
       }
-      HIPCHK(hipStreamWaitEvent(h.stream, h.ev_copied[k & 1], 0));
-      push_view(h, cur, cnt);
-      HIPCHK(hipEventRecord(h.ev_consumed[k & 1], h.stream));
+      try {
+        HIPCHK(hipStreamWaitEvent(h.stream, h.ev_copied[k & 1], 0));
+        push_view(h, cur, cnt);
+        HIPCHK(hipEventRecord(h.ev_consumed[k & 1], h.stream));
+      } catch (...) {
+        if (copier.joinable()) copier.join();
+        hipStreamSynchronize(h.copy_stream);
+        throw;
+      }
+      if (copier.joinable()) copier.join();
+      if (copy_rc != hipSuccess) throw SgError(SG_EHIP, "ingress copy failed");
       if (k + 1 < nch) cur = next;
     }
     HIPCHK(hipStreamSynchronize(h.copy_stream));
