@@ -4,7 +4,7 @@ Partition keys are independent (each key has its own cloned runtime, C/partition
 the oracle run on the rows of a sample of keys -- global event indices kept -- must reproduce exactly the GPU's
 output rows for those keys.  Together with size-independent properties of the whole output (delivery order is
 non-decreasing in trigger index; the match count the bench reports), this checks the 100M-event configs end to end:
-C2 and C5 on the closed-form walker, C3b on the general machine.  C1 (1M events) is compared in full."""
+C2 and C5 on the closed-form walker, C3b and C3c on the general machine.  C1 (1M events) is compared in full."""
 import numpy as np
 import pytest
 
@@ -66,7 +66,8 @@ def _check_sampled_keys(cfg, got, host, sample):
     ("C2", 100_000_000, 10_000, 1_000, 12, 48_942_666),     # BASELINE configs[1], the bench workload
     ("C5", 100_000_000, 1_000_000, 10_000, 200, 38_852_524),  # C5 per-GPU slice (1M keys)
     ("C3b", 100_000_000, 10_000, 1_000, 12, 10_159_775),    # general machine at 100M events
-], ids=["C2", "C5", "C3b"])
+    ("C3c", 100_000_000, 10_000, 1_000, 6, 47_100_761),     # general machine: counts, and, within
+], ids=["C2", "C5", "C3b", "C3c"])
 def test_full_size_sampled_keys(cfg, n, keys, rate, sample, expect):
     got, host = _gpu_full(cfg, n, keys, rate)
     assert len(got) > 0
