@@ -182,6 +182,7 @@ static void push_view(SgHandle& h, BatchView& bv, int64_t n) {
     run_select(h);
   }
   h.pushes++;
+  h.gen++;
 }
 
 static std::string slot_name(const char* what, int c, int slot) {
@@ -470,6 +471,7 @@ int sg_reset(sg_handle* hh) {
     h.out.n = 0;
     h.pushes = 0;
     h.clock = 0;
+    h.gen++;
     sg_every_next_reset(&h);
     sg_every_absent_reset(&h);
     sg_general_reset(&h);
@@ -576,6 +578,17 @@ int sg_snapshot(sg_handle* hh, void* buf, size_t cap, size_t* size) {
     HIPCHK(hipSetDevice(h.device));
     HIPCHK(hipStreamSynchronize(h.stream));
     if (h.out.n) throw SgError(SG_EINVAL, "snapshot with undelivered matches: poll or discard them first");
+    // the usual two calls (size query, then copy) serialise the device state once
+    if (buf && h.snap_gen == h.gen && !h.snap_cache.empty()) {
+      *size = h.snap_cache.size();
+      if (cap >= h.snap_cache.size()) {
+        memcpy(buf, h.snap_cache.data(), h.snap_cache.size());
+        h.snap_cache.clear();
+        h.snap_cache.shrink_to_fit();
+        h.snap_gen = ~0ull;
+      }
+      return;
+    }
     SnapW w;
     w.put(SNAP_MAGIC, 8);
     w.pod((int32_t)SG_ABI_VERSION);
@@ -591,7 +604,12 @@ int sg_snapshot(sg_handle* hh, void* buf, size_t cap, size_t* size) {
       default: break;
     }
     *size = w.b.size();
-    if (buf && cap >= w.b.size()) memcpy(buf, w.b.data(), w.b.size());
+    if (buf && cap >= w.b.size()) {
+      memcpy(buf, w.b.data(), w.b.size());
+    } else {
+      h.snap_cache.swap(w.b);
+      h.snap_gen = h.gen;
+    }
   });
 }
 
@@ -603,6 +621,7 @@ int sg_restore(sg_handle* hh, const void* buf, size_t size) {
   return guard(hh, [&] {
     HIPCHK(hipSetDevice(h.device));
     HIPCHK(hipStreamSynchronize(h.stream));
+    h.gen++;   // from here on the state changes (or is reset on error)
     SnapR r{(const char*)buf, (const char*)buf + size};
     if (memcmp(r.take(8), SNAP_MAGIC, 8) != 0) throw SgError(SG_EINVAL, "not a siddhi_gpu snapshot");
     if (r.pod<int32_t>() != SG_ABI_VERSION) throw SgError(SG_EINVAL, "snapshot ABI version mismatch");
@@ -627,6 +646,7 @@ int sg_restore(sg_handle* hh, const void* buf, size_t size) {
     h.pushes = (int)pushes;
     h.clock = clock;
     h.key_bound_seen = kb;
+    h.gen++;
   });
 }
 

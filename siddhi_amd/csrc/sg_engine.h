@@ -102,6 +102,9 @@ struct SgHandle {
   hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
   int64_t last_events = 0, last_matches = 0, last_spilled = 0;
   int pushes = 0;
+  uint64_t gen = 0;           // state generation: bumped by every push / reset / restore
+  std::vector<char> snap_cache;   // blob of the last size query (sg_snapshot), valid while gen == snap_gen
+  uint64_t snap_gen = ~0ull;
   int64_t clock = 0;          // playback clock (TimestampGeneratorImpl.lastEventTimestamp)
   uint32_t key_bound_seen = 0;
   void* state = nullptr;      // per-shape persistent state (interp / absent)

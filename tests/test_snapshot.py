@@ -110,6 +110,33 @@ def test_snapshot_refused_with_undelivered_matches():
 
 
 @gpu
+def test_snapshot_size_query_then_push_is_not_stale():
+    """sg_snapshot caches the blob of a size query for the copy call; any push in between invalidates it."""
+    import ctypes as ct
+    from siddhi_amd._native import GpuEngine
+    b = synth_batch("C2", 0, 200_000, keys=500, rate=100)
+    b.key = dense_first_seen(b.key)
+    q = synth.QUERIES["C2"]
+    want = run_engine(OracleEngine, q, [b])
+    ctx = context(q)
+    eng = GpuEngine(ctx)
+    eng.push(_slice(b, 0, 80_000))
+    outs = [eng.fetch()]
+    size = ct.c_size_t()
+    eng.handle.check(eng.handle.lib.sg_snapshot(eng.handle.h, None, 0, ct.byref(size)))   # caches state @80k
+    eng.push(_slice(b, 80_000, 140_000))
+    outs.append(eng.fetch())
+    blob = eng.snapshot()                                                                   # must be state @140k
+    eng.close()
+    eng2 = GpuEngine(ctx)
+    eng2.restore(blob)
+    eng2.push(_slice(b, 140_000, 200_000))
+    outs.append(eng2.fetch())
+    eng2.close()
+    assert_same(_cat(outs), want)
+
+
+@gpu
 def test_restore_rejects_foreign_or_damaged_blobs():
     from siddhi_amd._native import GpuEngine, SgError
     b = synth_batch("C2", 0, 50_000, keys=100, rate=100)
