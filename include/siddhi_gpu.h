@@ -90,7 +90,7 @@ extern "C" {
 #define SG_OP_NOT 6
 #define SG_OP_ISNULL 7
 #define SG_OP_MATH 8    /* MATH op(0 + 1 - 2 * 3 / 4 %) result_type: Java arithmetic, null on a null operand or a
-                           zero divisor (C/executor/math/{add,subtract,multiply,divide,mod}/*.java) */
+                           zero divisor (C/executor/math/{add,subtract,multiply,divide,mod}/ *.java) */
 
 typedef struct sg_state_desc {
   int32_t kind, stream, is_start, min_count, max_count, logical_type, partner;

@@ -556,8 +556,11 @@ class _Parser:
             if unit not in _TIME_UNITS:
                 raise SiddhiParserException(f"unknown time unit {unit}")
             total += n * _TIME_UNITS[unit]
-            if not self.accept("and"):
+            # time_value: `1 min and 30 sec` -- an `and` that is not followed by a number belongs to the
+            # enclosing logical state (`not S for 1 sec and e2=T`)
+            if not (self.at("and") and self.peek(1).kind == "num"):
                 break
+            self.i += 1
         return total
 
     # -- expressions (SiddhiQL.g4 expression rules; precedence or < and < not < compare < math)

@@ -161,6 +161,7 @@ static void push_view(SgHandle& h, BatchView& bv, int64_t n) {
     if (!bv.cols.col[d.ret_col[r]]) throw SgError(SG_EINVAL, "batch is missing a column the query reads");
   int shape = h.opt.force_general ? SG_SHAPE_GENERAL : d.shape;
   const bool sel = d.n_out > 0;
+  h.bump_gen();   // the state changes from here on (a failed push leaves no valid snapshot cache either)
   if (sel) std::swap(h.out, h.stage);   // engines append base records to the stage
   try {
     switch (shape) {
@@ -179,10 +180,14 @@ static void push_view(SgHandle& h, BatchView& bv, int64_t n) {
   }
   if (sel) {
     std::swap(h.out, h.stage);
-    run_select(h);
+    try {
+      run_select(h);
+    } catch (...) {
+      h.stage.n = 0;   // base records of a failed select pass must not be delivered by the next push
+      throw;
+    }
   }
   h.pushes++;
-  h.gen++;
 }
 
 static std::string slot_name(const char* what, int c, int slot) {
@@ -470,8 +475,7 @@ int sg_reset(sg_handle* hh) {
     HIPCHK(hipStreamSynchronize(h.stream));
     h.out.n = 0;
     h.pushes = 0;
-    h.clock = 0;
-    h.gen++;
+    h.bump_gen();
     sg_every_next_reset(&h);
     sg_every_absent_reset(&h);
     sg_general_reset(&h);
@@ -539,7 +543,7 @@ int sg_close(sg_handle* hh) {
 }
 
 // ---- snapshot / restore -------------------------------------------------------------------------
-static const char SNAP_MAGIC[8] = {'S', 'G', 'S', 'N', 'A', 'P', '0', '1'};
+static const char SNAP_MAGIC[8] = {'S', 'G', 'S', 'N', 'A', 'P', '0', '2'};
 
 // Fingerprint of everything the persisted state's meaning depends on: the lowered query and the engine
 // route (closed form or general machine).  Field-wise, so struct padding never enters it.
@@ -595,7 +599,6 @@ int sg_snapshot(sg_handle* hh, void* buf, size_t cap, size_t* size) {
     w.pod((int32_t)h.state_kind);
     w.pod(query_fingerprint(h));
     w.pod((int64_t)h.pushes);
-    w.pod((int64_t)h.clock);
     w.pod((uint32_t)h.key_bound_seen);
     switch (h.state_kind) {
       case 1: sg_every_next_snapshot(&h, w); break;
@@ -621,14 +624,13 @@ int sg_restore(sg_handle* hh, const void* buf, size_t size) {
   return guard(hh, [&] {
     HIPCHK(hipSetDevice(h.device));
     HIPCHK(hipStreamSynchronize(h.stream));
-    h.gen++;   // from here on the state changes (or is reset on error)
+    h.bump_gen();   // from here on the state changes (or is reset on error)
     SnapR r{(const char*)buf, (const char*)buf + size};
     if (memcmp(r.take(8), SNAP_MAGIC, 8) != 0) throw SgError(SG_EINVAL, "not a siddhi_gpu snapshot");
     if (r.pod<int32_t>() != SG_ABI_VERSION) throw SgError(SG_EINVAL, "snapshot ABI version mismatch");
     const int32_t kind = r.pod<int32_t>();
     if (r.pod<uint64_t>() != query_fingerprint(h)) throw SgError(SG_EINVAL, "snapshot was taken for another query");
     const int64_t pushes = r.pod<int64_t>();
-    const int64_t clock = r.pod<int64_t>();
     const uint32_t kb = r.pod<uint32_t>();
     if (kind < 0 || kind > 3 || (h.state_kind && kind && h.state_kind != kind))
       throw SgError(SG_EINVAL, "snapshot engine kind does not match the handle");
@@ -644,9 +646,8 @@ int sg_restore(sg_handle* hh, const void* buf, size_t size) {
     }
     if (r.p != r.e) throw SgError(SG_EINVAL, "trailing bytes in snapshot");
     h.pushes = (int)pushes;
-    h.clock = clock;
     h.key_bound_seen = kb;
-    h.gen++;
+    h.bump_gen();
   });
 }
 

@@ -285,7 +285,7 @@ struct WRec<T, true, 8> {   // narrow, 8-byte value
 };
 struct alignas(16) Blob16 { uint32_t w[4]; };   // 16-byte records sort as one opaque type
 
-static const uint32_t PK_TS_RANGE = 1, PK_PAY_RANGE = 2;   // k_pack flags
+static const uint32_t PK_TS_RANGE = 1, PK_PAY_RANGE = 2, PK_KEY_RANGE = 4;   // k_pack flags
 
 template <class T, bool N>
 struct PackFn {   // builds the walker record of virtual row r (coalesced when r is sequential)
@@ -342,14 +342,19 @@ struct Grp {
 // walker records + sort keys of every virtual row, in arrival order (coalesced).  Narrow records flag a
 // time outside +-2^31 ms of the first virtual row, or a payload that does not fit 32 bits.
 template <class T, bool N>
-__global__ void __launch_bounds__(256) k_pack(PackFn<T, N> pk, KeyOf kf, int64_t nt, WRec<T, N>* __restrict__ rec,
-                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ flags) {
+__global__ void __launch_bounds__(256) k_pack(PackFn<T, N> pk, KeyOf kf, uint32_t kbound, int64_t nt,
+                                              WRec<T, N>* __restrict__ rec, uint32_t* __restrict__ keys,
+                                              uint32_t* __restrict__ flags) {
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   uint32_t bad = 0;
   const int64_t t0 = N ? v_ts(pk.v, 0) : 0;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nt; r += stride) {
     rec[r] = pk((uint32_t)r);
-    if (keys) keys[r] = kf((uint32_t)r);
+    if (keys) {
+      const uint32_t kk = kf((uint32_t)r);
+      if (kk >= kbound && kk != 0xffffffffu) bad |= PK_KEY_RANGE;   // beyond the caller's key_bound
+      keys[r] = kk;
+    }
     if (N) {
       const int64_t d = v_ts(pk.v, (uint32_t)r) - t0;
       if (d != (int64_t)(int32_t)d) bad |= PK_TS_RANGE;
@@ -1579,7 +1584,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     R* srec = (R*)h->ws.get("srec", sizeof(R) * nt, st);
     uint32_t* pkeys = (uint32_t*)h->ws.get("pkeys", sizeof(uint32_t) * nt, st);
     KeyOf kf{bv.key, cs.key, (uint32_t)nc};
-    hipLaunchKernelGGL((k_pack<T, N>), pgrd, dim3(256), 0, st, src.pk, kf, nt, prec, pkeys, pk_flags);
+    hipLaunchKernelGGL((k_pack<T, N>), pgrd, dim3(256), 0, st, src.pk, kf, kb, nt, prec, pkeys, pk_flags);
     HIPCHK(hipGetLastError());
     size_t tb = 0;
     if constexpr (sizeof(R) == 16) {   // one onesweep instantiation for every 16-byte record format
@@ -1602,7 +1607,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   } else {
     // unpartitioned: one key whose rows are already in arrival order
     KeyOf kf{nullptr, nullptr, 0};
-    hipLaunchKernelGGL((k_pack<T, N>), pgrd, dim3(256), 0, st, src.pk, kf, nt, prec, (uint32_t*)nullptr, pk_flags);
+    hipLaunchKernelGGL((k_pack<T, N>), pgrd, dim3(256), 0, st, src.pk, kf, kb, nt, prec, (uint32_t*)nullptr, pk_flags);
     HIPCHK(hipGetLastError());
     src.srec = prec;
     const uint32_t seg[2] = {0u, (uint32_t)nt};
@@ -1690,6 +1695,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemcpyAsync(&rows_total, wrow + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (pkf & PK_KEY_RANGE) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
     if (pkf & PK_TS_RANGE) return false;   // the push spans more than 2^31 ms: wide records
     if (pkf & PK_PAY_RANGE) {
       // a payload value wider than 32 bits: gather e1's attributes by row instead

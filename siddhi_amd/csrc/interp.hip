@@ -52,7 +52,11 @@ __global__ void k_route(int64_t n, const int32_t* __restrict__ stream, const int
     if (!partitioned) k = 0;
     else {
       int32_t kk = key ? key[i] : -1;
-      if (kk >= 0) k = (uint32_t)kk;
+      if (kk >= 0) {
+        // a key at or above the caller's key_bound would fall outside the sorted bits and the per-key tables
+        if ((uint32_t)kk >= sentinel) atomicOr(order_err, 2);
+        else k = (uint32_t)kk;
+      }
     }
   }
   okey[i] = k;
@@ -146,10 +150,8 @@ __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDes
   if (k >= a.nkeys) return;
   int32_t* ar = arena + k * geo->key_words;
   uint32_t b = a.beg[k], e = a.end[k];
-  if (!a.partitioned || true) {
-    // keys that never received a row have no runtime yet (and no timers)
-    if (ar[K_CREATED] == 0 && e <= b && a.partitioned) return;
-  }
+  // keys that never received a row have no runtime yet (and no timers)
+  if (ar[K_CREATED] == 0 && e <= b && a.partitioned) return;
   KeyMachine m;
   m.d = dd;
   m.g = geo;
@@ -389,11 +391,10 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(hipMemsetAsync(eover, 0, 4, st));
   HIPCHK(hipMemsetAsync(gs->dfail, 0, 4, st));
   int32_t oerr = 0;
-  if (has_absent) {
-    HIPCHK(hipMemcpyAsync(&oerr, order_err, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (oerr) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps within a push");
-  }
+  HIPCHK(hipMemcpyAsync(&oerr, order_err, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (oerr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+  if (oerr & 1) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps within a push");
   NfaArgs na;
   na.n = n;
   na.base_index = bv.base_index;

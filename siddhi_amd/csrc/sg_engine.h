@@ -105,13 +105,16 @@ struct SgHandle {
   uint64_t gen = 0;           // state generation: bumped by every push / reset / restore
   std::vector<char> snap_cache;   // blob of the last size query (sg_snapshot), valid while gen == snap_gen
   uint64_t snap_gen = ~0ull;
-  int64_t clock = 0;          // playback clock (TimestampGeneratorImpl.lastEventTimestamp)
   uint32_t key_bound_seen = 0;
   void* state = nullptr;      // per-shape persistent state (interp / absent)
   int state_kind = 0;         // 1 every->next closed form, 2 general machine, 3 absence closed form
   int split_out = 0;          // 1: output stage timed from ev[5] (host work between ev[3] and ev[5])
   int extra_marks = 0;        // 1: ev[6]..ev[7] hold an extra match-stage interval (overflow re-pass)
   void mark(int k) { hipEventRecord(ev[k], stream); }
+  void bump_gen() {   // any state change invalidates the serialised-state cache of sg_snapshot
+    ++gen;
+    if (!snap_cache.empty()) { std::vector<char>().swap(snap_cache); snap_gen = ~0ull; }
+  }
 };
 
 

@@ -291,27 +291,43 @@ class SiddhiAppRuntime:
                     v = cols.get(name)
                     if v is None:
                         raise SiddhiAppCreationException(f"missing column {name}")
+                    v = np.asarray(v)
+                    if t == "STRING" and v.dtype.kind in "OUS":   # raw strings -> dictionary ids
+                        v = np.fromiter((self._string_id(str(x)) for x in v), dtype=np.int32, count=len(v))
                     allcols.append(np.ascontiguousarray(v, dtype=_NP[t]))
                 else:
                     allcols.append(np.zeros(n, dtype=_NP[t]))
                 nulls.append(None)
         for qi, q in enumerate(self.queries):
             if q.ctx.partitioned and q.ctx.key_attr[stream] >= 0:
-                name = d.attrs[q.ctx.key_attr[stream]][0]
-                key = self._dense_keys(qi, np.asarray(cols[name]))
+                ai = q.ctx.key_attr[stream]
+                name, t = d.attrs[ai]
+                # the partition column as the engines see it (STRING: dictionary ids)
+                key = self._dense_keys(qi, allcols[self._col_base(stream) + ai], t)
             else:
                 key = np.zeros(n, np.int32) if not q.ctx.partitioned else np.full(n, -1, np.int32)
             q.engine.push(Batch(n, base, ts, stream_col, key, allcols, nulls))
             self._deliver(q, q.engine.fetch())
 
-    def _dense_keys(self, qi: int, vals: np.ndarray) -> np.ndarray:
-        """First-seen dense ids of partition key values (PartitionRuntime clone order)."""
+    def _col_base(self, stream: int) -> int:
+        return sum(len(self.app.streams[sid].attrs) for sid in self.stream_ids[:stream])
+
+    def _dense_keys(self, qi: int, vals: np.ndarray, t: str) -> np.ndarray:
+        """First-seen dense ids of partition key values (PartitionRuntime clone order).  The key identity is
+        String.valueOf(value) exactly as on the row path (`_key_string`), so a key sent through send() and
+        send_columns() is one partition instance."""
         kd = self.key_dicts[qi]
         uniq, first = np.unique(vals, return_index=True)
         order = np.argsort(first, kind="stable")
         ids = np.empty(len(uniq), np.int32)
+        strings = self.string_list_from_dict() if t == "STRING" else None
         for k in order:
-            ks = str(uniq[k].item())
+            u = uniq[k].item()
+            if t == "STRING":
+                if not 0 <= u < len(strings):
+                    raise SiddhiAppCreationException(f"string id {u} was never assigned")
+                u = strings[u]
+            ks = _key_string(u, t)
             i = kd.get(ks)
             if i is None:
                 i = len(kd)
