@@ -18,6 +18,7 @@
 //   C/query/input/stream/state/CountPre/PostStateProcessor.java -> CountPre/CountPost
 //   C/query/input/stream/state/LogicalPre/PostStateProcessor.java -> LogicalPre/LogicalPost
 //   C/query/input/stream/state/AbsentStreamPre/PostStateProcessor.java -> AbsentPre/AbsentPost
+//   C/query/input/stream/state/AbsentLogicalPre/PostStateProcessor.java -> AbsentLogicalPre/AbsentLogicalPost
 //   C/query/input/stream/state/runtime/*InnerStateRuntime.java -> RtNode
 //   C/query/input/{Multi,Single,StateMulti}ProcessStreamReceiver.java, receiver/*.java -> Receiver
 //   C/event/state/StateEvent.java:138-236, StateEventCloner.java:48-60 -> StateEvent, chain ops
@@ -435,7 +436,9 @@ struct PostBase {
   virtual void setNextEveryStatePre(PreBase* p) { nextEveryStatePre = p; }
 };
 
-enum PreKind { P_STREAM, P_COUNT, P_LOGICAL, P_ABSENT };
+enum PreKind { P_STREAM, P_COUNT, P_LOGICAL, P_ABSENT, P_ALOGICAL /* AbsentLogicalPreStateProcessor */ };
+// `instanceof AbsentPreStateProcessor` (AbsentStreamPre and AbsentLogicalPre implement it)
+static inline bool is_absent_kind(PreKind k) { return k == P_ABSENT || k == P_ALOGICAL; }
 
 struct PreBase {
   KeyRuntime* rt = nullptr;
@@ -484,6 +487,8 @@ struct PreBase {
   }
   virtual void processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret);
   virtual bool removeOnNoStateChange() { return stateType == SEQUENCE; }
+  virtual void processTimer(int64_t) { fail("timer event for a processor without a scheduler"); }
+  virtual void start() {}
 };
 
 struct CountPre : PreBase {
@@ -536,14 +541,34 @@ struct AbsentPre : PreBase {
   void addState(const SE& s) override;
   void addEveryState(const SE& s) override;
   void resetState() override;
-  void processTimer(int64_t currentTime);
+  void processTimer(int64_t currentTime) override;
   void sendEvent(const SE& s);
   void processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) override;
   bool removeOnNoStateChange() override { return false; }
-  void start();
+  void start() override;
 };
 
 struct AbsentPost : PostBase {
+  void process(const SE& s) override;
+};
+
+// AbsentLogicalPreStateProcessor (C/query/input/stream/state/AbsentLogicalPreStateProcessor.java:36-384):
+// the `not S [for T]` side of `not A [for T] and|or B` (and `not A for T and|or not B for T`)
+struct AbsentLogicalPre : LogicalPre {
+  Scheduler* scheduler = nullptr;
+  int64_t waitingTime = -1;
+  int64_t lastArrivalTime = 0;
+  bool active = true;
+  void addState(const SE& s) override;
+  void addEveryState(const SE& s) override;
+  void processTimer(int64_t currentTime) override;
+  void processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) override;
+  bool partnerCanProceed(StateEvent* s);
+  void sendEvent(const SE& s);
+  void start() override;
+};
+
+struct AbsentLogicalPost : LogicalPost {   // AbsentLogicalPostStateProcessor.java:29-57
   void process(const SE& s) override;
 };
 
@@ -570,7 +595,7 @@ struct Receiver {
 // Scheduler (C/util/Scheduler.java): FIFO toNotifyQueue, listener on the app clock
 struct Scheduler {
   std::deque<int64_t> q;
-  AbsentPre* target = nullptr;
+  PreBase* target = nullptr;
   KeyRuntime* rt = nullptr;
   uint32_t order = 0;
 };
@@ -615,6 +640,13 @@ struct Engine {
   void setCurrentTimestamp(int64_t ts, uint64_t trigger);
 };
 
+static Ref<StreamEvent> blank_event(Engine* E, int stream) {
+  EventData* d = new EventData();
+  d->ts = -1; d->index = 0; d->stream = stream;
+  for (int t : E->app.streams[stream].types) d->vals.push_back(vnull(t));
+  return Ref<StreamEvent>(new_se(Ref<EventData>(d)));
+}
+
 // ---- PostBase::process  (StreamPostStateProcessor.java:53-72)
 void PostBase::process(const SE& s) {
   thisStatePre->stateChanged = true;
@@ -640,7 +672,7 @@ void PreBase::addEveryState(const SE& s) { newAndEvery.add(clone_state(s)); }
 void PreBase::init() {  // StreamPreStateProcessor.java:157-166
   if (isStartState && (!initialized || thisStatePost->nextEveryStatePre != nullptr ||
                        (stateType == SEQUENCE && thisStatePost->nextStatePre &&
-                        thisStatePost->nextStatePre->kind == P_ABSENT))) {
+                        is_absent_kind(thisStatePost->nextStatePre->kind)))) {
     StateEvent* s = new StateEvent();
     s->slots.resize(rt->eng->nstates);
     s->id = ++rt->eng->next_id;
@@ -836,8 +868,10 @@ void LogicalPre::processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret
 // ---- LogicalPost (LogicalPostStateProcessor.java:59-87)
 void LogicalPost::process(const SE& s) {
   if (type == 0) {  // AND
-    if (partnerPre->kind == P_ABSENT) fail("logical absent patterns are not supported");
-    if (s->slots[partnerPre->stateId]) PostBase::process(s);
+    bool proceed;
+    if (partnerPre->kind == P_ALOGICAL) proceed = static_cast<AbsentLogicalPre*>(partnerPre)->partnerCanProceed(s.get());
+    else proceed = (bool)s->slots[partnerPre->stateId];   // event received from a present processor
+    if (proceed) PostBase::process(s);
     else thisStatePre->stateChanged = true;
   } else {          // OR
     PostBase::process(s);
@@ -948,6 +982,163 @@ void AbsentPost::process(const SE& s) {
   static_cast<AbsentPre*>(thisStatePre)->updateLastArrivalTime(e->data->ts);
 }
 
+// ---- AbsentLogical (AbsentLogicalPreStateProcessor.java:72-383, AbsentLogicalPostStateProcessor.java:37-49)
+void AbsentLogicalPre::addState(const SE& s) {   // :83-105
+  if (!active) return;
+  LogicalPre::addState(s);
+  if (!isStartState && waitingTime != -1) {
+    notify_at(scheduler, s->ts + waitingTime);
+    if (partner->kind == P_ALOGICAL) {
+      auto* p = static_cast<AbsentLogicalPre*>(partner);
+      notify_at(p->scheduler, s->ts + p->waitingTime);
+    }
+  }
+}
+void AbsentLogicalPre::addEveryState(const SE& s) {   // :107-120
+  SE c = clone_state(s);
+  if (c->slots[stateId]) c->ts = c->slots[stateId]->data->ts;   // timestamp of the last arrived event
+  c->slots[stateId] = Ref<StreamEvent>();
+  c->slots[partner->stateId] = Ref<StreamEvent>();
+  newAndEvery.add(c);
+  partner->newAndEvery.add(c);
+}
+// a fresh pooled StreamEvent (StreamEventPool.borrowEvent): timestamp -1, every attribute null
+static Ref<StreamEvent> blank_event(Engine* E, int stream);
+static bool waiting_time_passed(int64_t now, StateEvent* s, int stateId, int64_t w) {   // :212-220
+  if (!s->slots[stateId]) return now >= s->ts + w;
+  return now >= s->slots[stateId]->data->ts + w;
+}
+void AbsentLogicalPre::processTimer(int64_t currentTime) {   // process(ComplexEventChunk) :122-210
+  if (!active) return;
+  bool notProcessed = true;
+  if (currentTime >= lastArrivalTime + waitingTime) {
+    if (isStartState && stateType == SEQUENCE && newAndEvery.empty() && pending.empty()) {
+      StateEvent* n = new StateEvent();
+      n->slots.resize(rt->eng->nstates);
+      n->id = ++rt->eng->next_id;
+      addState(SE(n));
+    } else if (stateType == SEQUENCE && !newAndEvery.empty()) {
+      resetState();
+    }
+    updateState();
+    std::vector<SE> retl;
+    auto& v = pending.v;
+    pending.iterating++;
+    size_t w = 0;
+    for (size_t r = 0; r < v.size(); r++) {
+      SE s = v[r];
+      if (isExpired(s.get(), currentTime)) {
+        if (withinEvery) {
+          pending.iterating--;
+          withinEvery->addEveryState(s);
+          withinEvery->updateState();
+          pending.iterating++;
+        }
+        continue;
+      }
+      if (waiting_time_passed(currentTime, s.get(), stateId, waitingTime)) {
+        const bool partnerBound = (bool)s->slots[partner->stateId];
+        if (logicalType == 1 && !partnerBound) {            // OR: partner not received
+          add_event(s.get(), stateId, blank_event(rt->eng, rt->eng->meta[stateId].stream));
+          retl.push_back(s);
+        } else if (logicalType == 0 && partnerBound) {      // AND: partner received but did not send out
+          retl.push_back(s);
+        } else if (logicalType == 0) {                      // AND: let the partner process (or not)
+          add_event(s.get(), stateId, blank_event(rt->eng, rt->eng->meta[stateId].stream));
+        }
+        continue;   // iterator.remove()
+      }
+      v[w++] = s;
+    }
+    v.resize(w);
+    pending.iterating--;
+    notProcessed = retl.empty();
+    for (auto& s : retl) sendEvent(s);
+    lastArrivalTime = 0;
+  }
+  if (thisStatePost->nextEveryStatePre || (notProcessed && isStartState)) {   // schedule again :199-209
+    int64_t nextBreak = lastArrivalTime == 0 ? rt->eng->lastEventTimestamp + waitingTime : lastArrivalTime + waitingTime;
+    notify_at(scheduler, nextBreak);
+  }
+}
+void AbsentLogicalPre::sendEvent(const SE& s) {   // :222-242
+  if (thisStatePost->hasSelector) rt->emit(s);
+  if (thisStatePost->nextStatePre) thisStatePost->nextStatePre->addState(s);
+  if (thisStatePost->nextEveryStatePre) thisStatePost->nextEveryStatePre->addEveryState(s);
+  else if (isStartState) {
+    active = false;
+    if (logicalType == 1 && partner->kind == P_ALOGICAL) static_cast<AbsentLogicalPre*>(partner)->active = false;
+  }
+  if (thisStatePost->callbackPre) static_cast<CountPre*>(thisStatePost->callbackPre)->startStateReset();
+}
+void AbsentLogicalPre::processAndReturn(const Ref<EventData>& ev, std::vector<SE>& ret) {   // :244-305
+  (void)ret;   // never returns a match (the chunk it returns is always empty)
+  if (!active) return;
+  auto& v = pending.v;
+  pending.iterating++;
+  size_t w = 0;
+  for (size_t r = 0; r < v.size(); r++) {
+    SE s = v[r];
+    if (isExpired(s.get(), ev->ts)) {
+      if (withinEvery) {
+        pending.iterating--;
+        withinEvery->addEveryState(s);
+        withinEvery->updateState();
+        pending.iterating++;
+      }
+      continue;
+    }
+    if (logicalType == 1 && s->slots[partner->stateId]) continue;
+    Ref<StreamEvent> cur = s->slots[stateId];
+    s->slots[stateId] = Ref<StreamEvent>(new_se(ev));
+    process(s);
+    if (waitingTime != -1 || (stateType == SEQUENCE && logicalType == 0 && thisStatePost->nextEveryStatePre))
+      s->slots[stateId] = cur;   // reset to the original state after processing
+    bool remove = false;
+    if (thisLastPost->isEventReturned) {   // passed the filter: no longer an absence candidate
+      thisLastPost->isEventReturned = false;
+      remove = true;
+      if (stateType == SEQUENCE) {
+        auto& pv = partner->pending.v;
+        for (size_t k = 0; k < pv.size(); k++)
+          if (pv[k] == s) { pv.erase(pv.begin() + (long)k); break; }
+      }
+    }
+    if (!stateChanged) {
+      s->slots[stateId] = cur;
+      if (stateType == SEQUENCE) {
+        if (remove) fail("IllegalStateException: double iterator.remove() (reference behaviour)");
+        remove = true;
+      }
+    }
+    if (!remove) v[w++] = s;
+  }
+  v.resize(w);
+  pending.iterating--;
+}
+bool AbsentLogicalPre::partnerCanProceed(StateEvent* s) {   // :353-383
+  if (stateType == SEQUENCE && thisStatePost->nextEveryStatePre == nullptr && lastArrivalTime > 0) return false;
+  if (waitingTime == -1) {
+    if (thisStatePost->nextEveryStatePre == nullptr) return !s->slots[stateId];
+    if (lastArrivalTime > 0) {
+      lastArrivalTime = 0;
+      init();
+      return false;
+    }
+    return true;
+  }
+  return (bool)s->slots[stateId];
+}
+void AbsentLogicalPre::start() {   // :334-345
+  if (isStartState && waitingTime != -1 && active) notify_at(scheduler, rt->eng->lastEventTimestamp + waitingTime);
+}
+void AbsentLogicalPost::process(const SE& s) {   // AbsentLogicalPostStateProcessor.process :37-49
+  thisStatePre->stateChanged = true;
+  StreamEvent* e = s->slots[stateId].get();
+  isEventReturned = true;
+  static_cast<AbsentLogicalPre*>(thisStatePre)->lastArrivalTime = e->data->ts;   // updateLastArrivalTime
+}
+
 // ---- runtime reset/update (InnerStateRuntime implementations)
 void KeyRuntime::reset(RtNode* n) {
   switch (n->kind) {
@@ -1039,6 +1230,12 @@ struct Builder {
     }
     resolve(x->l.get(), cur, in_select);
     resolve(x->r.get(), cur, in_select);
+    if (x->kind == X_MATH) {   // arithmetic inside a filter: ExpressionParser.parseArithmeticOperationResultType
+      auto ty = [](const Expr* e) { return e->kind == X_CONST ? e->cval.type : e->vtype; };
+      int a = ty(x->l.get()), b = ty(x->r.get());
+      if (a == T_STRING || a == T_BOOL || b == T_STRING || b == T_BOOL) fail("arithmetic on a non-numeric attribute");
+      x->vtype = promote_order(a, b);
+    }
   }
 
   void count_streams(const Elem* e) {
@@ -1049,7 +1246,7 @@ struct Builder {
 
   RtNode* node(int kind) { rt->nodes.emplace_back(new RtNode()); rt->nodes.back()->kind = kind; return rt->nodes.back().get(); }
 
-  Scheduler* new_scheduler(AbsentPre* p) {
+  Scheduler* new_scheduler(PreBase* p) {
     rt->schedulers.emplace_back(new Scheduler());
     Scheduler* s = rt->schedulers.back().get();
     s->target = p; s->rt = rt;
@@ -1110,11 +1307,25 @@ struct Builder {
         return n;
       }
       case E_LOGICAL: {
-        if (e->a->kind != E_STREAM || e->b->kind != E_STREAM) fail("logical absent patterns are not supported");
-        auto* pre1 = new LogicalPre(); pre1->kind = P_LOGICAL; pre1->logicalType = e->logical; pre1->stateType = type;
-        auto* post1 = new LogicalPost(); post1->type = e->logical;
-        auto* pre2 = new LogicalPre(); pre2->kind = P_LOGICAL; pre2->logicalType = e->logical; pre2->stateType = type;
-        auto* post2 = new LogicalPost(); post2->type = e->logical;
+        // StateInputStreamParser.java:281-374: an AbsentStreamStateElement side gets AbsentLogicalPre/Post and its
+        // own Scheduler (created with the processor: element1's before element2's)
+        auto mk = [&](const Elem* x, LogicalPre*& pre, LogicalPost*& post) {
+          if (x->kind == E_ABSENT) {
+            auto* ap = new AbsentLogicalPre(); ap->kind = P_ALOGICAL; ap->waitingTime = x->waiting;
+            if (!rt->is_clone) ap->scheduler = new_scheduler(ap);
+            pre = ap;
+            post = new AbsentLogicalPost();
+          } else {
+            pre = new LogicalPre(); pre->kind = P_LOGICAL;
+            post = new LogicalPost();
+          }
+          pre->logicalType = e->logical; pre->stateType = type;
+          post->type = e->logical;
+        };
+        LogicalPre *pre1, *pre2;
+        LogicalPost *post1, *post2;
+        mk(e->a.get(), pre1, post1);
+        mk(e->b.get(), pre2, post2);
         post1->partnerPre = pre2; post2->partnerPre = pre1;
         post1->partnerPost = post2; post2->partnerPost = post1;
         pre1->partner = pre2; pre2->partner = pre1;
@@ -1204,7 +1415,8 @@ struct Builder {
       case E_LOGICAL: clone_schedulers(n->a); clone_schedulers(n->b); break;
       case E_EVERY: clone_schedulers(n->a); break;
       default:
-        if (n->first->kind == P_ABSENT) static_cast<AbsentPre*>(n->first)->scheduler = new_scheduler(static_cast<AbsentPre*>(n->first));
+        if (n->first->kind == P_ABSENT) static_cast<AbsentPre*>(n->first)->scheduler = new_scheduler(n->first);
+        else if (n->first->kind == P_ALOGICAL) static_cast<AbsentLogicalPre*>(n->first)->scheduler = new_scheduler(n->first);
         break;
     }
   }
@@ -1327,9 +1539,8 @@ OrcHandle* orc_create(const int64_t* image, int64_t n, char* err, int errlen) {
     h->eng.meta.resize(h->eng.nstates);
     if (!h->eng.app.partitioned) {
       h->eng.single.reset(make_runtime(&h->eng, 0, false));
-      // SiddhiAppRuntime.start(): AbsentStreamPreStateProcessor.start() for start-state absence
-      for (auto& p : h->eng.single->pres)
-        if (p->kind == P_ABSENT) static_cast<AbsentPre*>(p.get())->start();
+      // SiddhiAppRuntime.start(): Absent{Stream,Logical}PreStateProcessor.start() for start-state absence
+      for (auto& p : h->eng.single->pres) p->start();
     } else {
       // resolve select against a template runtime (metadata only)
       std::unique_ptr<KeyRuntime> tmpl(make_runtime(&h->eng, -1, true));

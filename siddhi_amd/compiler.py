@@ -106,7 +106,7 @@ class AbsentStreamStateElement:
     stream_id: str
     ref: Optional[str]
     filters: List[Expr]
-    waiting_time: int
+    waiting_time: Optional[int]     # None: `not S` inside `and` without `for`
 
 
 @dataclass
@@ -380,7 +380,16 @@ class _Parser:
         inp = self.state_input()
         self.eat("select")
         select = []
-        while True:
+        star = self.accept("*")
+        if star:
+            # select * over a state input: every attribute of every state's stream, states in parse order, as an
+            # unqualified variable; a repeated name is a DuplicateAttributeException (SelectorParser.java:165-193)
+            for sid in _state_streams(inp.element):
+                for (n, _) in self.streams[sid].attrs:
+                    if any(oa.rename == n for oa in select):
+                        raise SiddhiParserException(f"Duplicate attribute {n} in select *")
+                    select.append(OutputAttribute(Var(n), n))
+        while not star:
             e = self.expr()
             if self.accept("as"):
                 rename = self.ident()
@@ -476,14 +485,46 @@ class _Parser:
         return self.source(allow_seq_count=True)
 
     def _paren_is_logical_absent(self):
-        return False
+        """'(' logical_absent_stateful_source ')' (SiddhiQL.g4:252-262): a parenthesised group holding `not` and
+        `and`/`or` at its own depth and no `->` / `,` chain separator."""
+        if not self.at("("):
+            return False
+        depth, j, seen_not, seen_logic = 0, self.i, False, False
+        while True:
+            t = self.toks[j]
+            if t.kind == "eof":
+                return False
+            if t.text in ("(", "["):
+                depth += 1
+            elif t.text in (")", "]"):
+                depth -= 1
+                if depth == 0:
+                    return seen_not and seen_logic
+            elif depth == 1:
+                if t.text in ("->", ","):
+                    return False
+                if t.text == "not":
+                    seen_not = True
+                elif t.text in ("and", "or") and not (self.toks[j + 1].kind == "num"):
+                    seen_logic = True
+            j += 1
 
     def source(self, allow_seq_count):
         # pattern_source: logical | collection | standard | logical_absent | absent
+        if self._paren_is_logical_absent():
+            self.eat("(")
+            el = self.source(allow_seq_count)
+            self.eat(")")
+            if not (isinstance(el, LogicalStateElement) and
+                    (isinstance(el.e1, AbsentStreamStateElement) or isinstance(el.e2, AbsentStreamStateElement))):
+                raise SiddhiParserException("expected a logical absent pattern inside parentheses")
+            return el
         if self.at("not"):
-            a = self.absent_source()
+            a = self.absent_source(optional_for=True)
             if self.at("and") or self.at("or"):
-                raise SiddhiParserException("logical absent patterns are not supported yet")
+                return self._logical_absent(a)
+            if a.waiting_time is None:
+                raise SiddhiParserException("'not' without 'for' is only allowed with 'and' (SiddhiQL.g4:254-255)")
             return a
         s = self.standard_source()
         if self.at("<"):
@@ -512,10 +553,27 @@ class _Parser:
             typ = self.peek().text.upper()
             self.i += 1
             if self.at("not"):
-                raise SiddhiParserException("logical absent patterns are not supported yet")
+                a = self.absent_source(optional_for=(typ == "AND"))
+                # State.logicalNotAnd / logicalOr(absent, present): the absent element is always element1
+                # (A/execution/query/input/state/State.java:39-68; visitor :989-1020)
+                return LogicalStateElement(a, typ, s)
             s2 = self.standard_source()
             return LogicalStateElement(s, typ, s2)
         return s
+
+    def _logical_absent(self, a):
+        """`not A [for T] and|or <standard | not B for T>` (SiddhiQL.g4:252-262, visitor :975-1024)."""
+        typ = self.peek().text.upper()
+        self.i += 1
+        if self.at("not"):
+            b = self.absent_source(optional_for=False)
+            if a.waiting_time is None:
+                raise SiddhiParserException("'not' without 'for' cannot be combined with another absent state")
+            return LogicalStateElement(a, typ, b)
+        if typ == "OR" and a.waiting_time is None:
+            raise SiddhiParserException("'not ... or' needs 'for <time>' (SiddhiQL.g4:259-261)")
+        s2 = self.standard_source()
+        return LogicalStateElement(a, typ, s2)
 
     def standard_source(self) -> StreamStateElement:
         ref = None
@@ -528,12 +586,19 @@ class _Parser:
         filters = self.filters()
         return StreamStateElement(sid, ref, filters)
 
-    def absent_source(self) -> AbsentStreamStateElement:
+    def absent_source(self, optional_for=False) -> AbsentStreamStateElement:
+        """basic_absent_pattern_source `not S[..] for T` (SiddhiQL.g4:271-273); inside `and` the `for` may be
+        absent (`standard AND NOT basic_source`, :254-255): waiting_time None (AbsentLogicalPreStateProcessor
+        waitingTime = -1).  NOT states carry no event reference (State.logicalNot, State.java:44-50)."""
         self.eat("not")
+        if self.peek(1).text == "=" and self.peek(1).kind == "op":
+            raise SiddhiParserException("NOT pattern cannot have reference id")
         sid = self.ident()
         if sid not in self.streams:
             raise SiddhiParserException(f"stream '{sid}' is not defined")
         filters = self.filters()
+        if optional_for and not self.at("for"):
+            return AbsentStreamStateElement(sid, None, filters, None)
         self.eat("for")
         wt = self.time_value()
         return AbsentStreamStateElement(sid, None, filters, wt)
@@ -668,6 +733,19 @@ class _Parser:
         if index is not None:
             raise SiddhiParserException("stream index without attribute")
         return Var(name)
+
+
+def _state_streams(el) -> List[str]:
+    """Stream ids of the state elements in parse order (StateInputStreamParser: logical element2 first)."""
+    if isinstance(el, (StreamStateElement, AbsentStreamStateElement)):
+        return [el.stream_id]
+    if isinstance(el, NextStateElement):
+        return _state_streams(el.current) + _state_streams(el.next)
+    if isinstance(el, (EveryStateElement, CountStateElement)):
+        return _state_streams(el.inner)
+    if isinstance(el, LogicalStateElement):
+        return _state_streams(el.e2) + _state_streams(el.e1)
+    return []
 
 
 def parse(text: str) -> SiddhiApp:

@@ -114,7 +114,7 @@ def _enc_elem(ctx: QueryContext, el) -> List[int]:
         out = [2, ctx.stream_index(el.stream_id), -1, len(el.filters)]
         for f in el.filters:
             out += _enc_expr(ctx, f)
-        return out + [el.waiting_time]
+        return out + [el.waiting_time if el.waiting_time is not None else -1]
     if isinstance(el, C.StreamStateElement):
         ref = ctx.name_id(el.ref) if el.ref else -1
         out = [1, ctx.stream_index(el.stream_id), ref, len(el.filters)]
@@ -375,6 +375,11 @@ class _FlatBuilder:
         if isinstance(e, C.IsNull):
             w, _, l_ = self.compile_expr(e.expr, cur)
             return w + [OP_ISNULL], "BOOL", l_
+        if isinstance(e, C.Math):   # math executors inside a filter (C/executor/math/**)
+            lw, lt, ll = self.compile_expr(e.left, cur)
+            rw, rt, rl = self.compile_expr(e.right, cur)
+            t = math_type(lt, rt)
+            return lw + rw + [OP_MATH, MATH_CODE[e.op], TYPE_CODE[t]], t, ll and rl
         raise LoweringError(f"unsupported expression in filter: {e}")
 
     # ---- element parse (StateInputStreamParser.parse :143-404)
