@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 1
+#define SG_ABI_VERSION 2
 
 #define SG_MAX_STATES 16
 #define SG_MAX_STREAMS 16
@@ -67,6 +67,7 @@ extern "C" {
 #define SG_K_COUNT 1        /* CountPre/PostStateProcessor */
 #define SG_K_LOGICAL 2      /* LogicalPre/PostStateProcessor */
 #define SG_K_ABSENT 3       /* AbsentStreamPre/PostStateProcessor */
+#define SG_K_ALOGICAL 4     /* AbsentLogicalPre/PostStateProcessor: the `not S [for T]` side of a logical state */
 
 /* attribute types (Attribute.Type) */
 #define SG_T_STRING 0       /* dictionary id, int32 */
@@ -101,7 +102,7 @@ typedef struct sg_state_desc {
   int32_t has_selector;   /* post.nextProcessor != null */
   int32_t this_last;      /* pre.thisLastProcessor = post of this state id */
   int32_t prog_off, prog_len, local;
-  int64_t waiting_time;   /* absent: `for T` in ms */
+  int64_t waiting_time;   /* absent: `for T` in ms (SG_K_ALOGICAL: -1 = `not S` without `for`) */
 } sg_state_desc;
 
 typedef struct sg_receiver_desc {
@@ -141,6 +142,11 @@ typedef struct sg_nfa_desc {
   int32_t n_out;
   int32_t out_type[SG_MAX_SELECT], out_off[SG_MAX_SELECT], out_len[SG_MAX_SELECT];
   int32_t having_off, having_len;
+  /* Schedulers (timer FIFOs) of the SG_K_ABSENT / SG_K_ALOGICAL states in their creation order
+   * (StateInputStreamParser.java:167-185,290-320 for the app runtime; *InnerStateRuntime.clone order for
+   * partition clones): timers of one clock advance fire scheduler by scheduler in this order. */
+  int32_t n_sched;
+  int32_t sched_state[SG_MAX_STATES];
 } sg_nfa_desc;
 
 typedef struct sg_options {

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SIDDHI_GPU_LIB") or os.path.join(HERE, "libsiddhi_gpu.so")   # override: experiments
 
 SG_MAX_STATES, SG_MAX_STREAMS, SG_MAX_SELECT, SG_MAX_RET, SG_MAX_COLS, SG_MAX_CODE = 16, 16, 32, 16, 64, 512
-SG_ABI_VERSION = 1
+SG_ABI_VERSION = 2
 
 SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
            "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version",
@@ -51,7 +51,8 @@ class sg_nfa_desc(ct.Structure):
                 ("shape", I32), ("shape_args", I32 * 8), ("shape_prog_off", I32), ("shape_prog_len", I32),
                 ("code_len", I32), ("code", I64 * SG_MAX_CODE),
                 ("n_out", I32), ("out_type", I32 * SG_MAX_SELECT), ("out_off", I32 * SG_MAX_SELECT),
-                ("out_len", I32 * SG_MAX_SELECT), ("having_off", I32), ("having_len", I32)]
+                ("out_len", I32 * SG_MAX_SELECT), ("having_off", I32), ("having_len", I32),
+                ("n_sched", I32), ("sched_state", I32 * SG_MAX_STATES)]
 
 
 class sg_options(ct.Structure):
@@ -197,6 +198,9 @@ def build_desc(nfa: L.FlatNFA) -> sg_nfa_desc:
         d.ret_type[r] = L.TYPE_CODE[t]
     for k, (st, idx, slot, t) in enumerate(nfa.select):
         d.sel_state[k], d.sel_index[k], d.sel_ret[k], d.sel_type[k] = st, idx, slot, L.TYPE_CODE[t]
+    d.n_sched = len(nfa.sched)
+    for k, v in enumerate(nfa.sched):
+        d.sched_state[k] = v
     return d
 
 

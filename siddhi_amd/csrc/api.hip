@@ -152,6 +152,15 @@ static void validate(const sg_nfa_desc* d) {
   }
   for (int r = 0; r < d->n_ret; ++r)
     if (d->ret_col[r] < 0 || d->ret_col[r] >= d->n_cols) throw SgError(SG_EINVAL, "retained column out of range");
+  int timed = 0;
+  for (int s = 0; s < d->n_states; ++s) timed += (d->states[s].kind == SG_K_ABSENT || d->states[s].kind == SG_K_ALOGICAL);
+  if (d->n_sched != timed) throw SgError(SG_EINVAL, "sched_state must list every absent state once");
+  for (int k = 0; k < d->n_sched; ++k) {
+    const int s = d->sched_state[k];
+    if (s < 0 || s >= d->n_states || (d->states[s].kind != SG_K_ABSENT && d->states[s].kind != SG_K_ALOGICAL))
+      throw SgError(SG_EINVAL, "bad sched_state entry");
+    for (int j = 0; j < k; ++j) if (d->sched_state[j] == s) throw SgError(SG_EINVAL, "duplicate sched_state entry");
+  }
 }
 
 // One push of rows already in HBM: the engine route, then the select pass.

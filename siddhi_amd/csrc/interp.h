@@ -208,7 +208,7 @@ struct KeyMachine {
     int listed = 0;
     for (int s = 0; s < g->S; ++s) listed += list(s, 0)[0] + list(s, 1)[0];
     int32_t* h = hdr();
-    int need_p = 2 * listed + 2 * g->S + 4, need_c = listed + 4, need_e = 4;
+    int need_p = 2 * listed + 2 * g->S + 4, need_c = listed + 4, need_e = 4 + (g->A ? listed : 0);
     if (h[K_NFREE_P] < need_p || h[K_NFREE_C] < need_c || h[K_NFREE_E] < need_e) {
       gc();
       if (h[K_NFREE_P] < need_p || h[K_NFREE_C] < need_c || h[K_NFREE_E] < need_e) fail(SG_ECAPACITY);
@@ -338,6 +338,7 @@ struct KeyMachine {
       case SG_K_COUNT: count_post(s, p); return;
       case SG_K_LOGICAL: logical_post(s, p); return;
       case SG_K_ABSENT: absent_post(s, p); return;
+      case SG_K_ALOGICAL: alogical_post(s, p); return;
       default: stream_post(s, p); return;
     }
   }
@@ -378,7 +379,9 @@ struct KeyMachine {
   SG_HD void logical_post(int s, int p) {
     const sg_state_desc& x = st(s);
     if (x.logical_type == 0) {
-      if (slot(p, x.partner) != SG_NIL) stream_post(s, p);
+      const bool proceed = st(x.partner).kind == SG_K_ALOGICAL ? partner_can_proceed(x.partner, p)
+                                                               : slot(p, x.partner) != SG_NIL;
+      if (proceed) stream_post(s, p);
       else sth(s)[H_CHANGED] = 1;
     } else {
       stream_post(s, p);
@@ -387,6 +390,28 @@ struct KeyMachine {
     }
   }
   // AbsentStreamPostStateProcessor.process :36-56
+  // AbsentLogicalPostStateProcessor.process :37-49 -- no forwarding, only the arrival is recorded
+  SG_HD void alogical_post(int s, int p) {
+    sth(s)[H_CHANGED] = 1;
+    sth(s)[H_RETURNED] = 1;
+    wr64(sth(s) + H_LST_LO, slot_ts(p, s));   // updateLastArrivalTime
+  }
+  SG_HD int64_t last_arrival(int s) { return rd64(sth(s) + H_LST_LO); }
+  // AbsentLogicalPreStateProcessor.partnerCanProceed :353-383 (asked by the partner's AND post)
+  SG_HD bool partner_can_proceed(int q, int p) {
+    const sg_state_desc& x = st(q);
+    if (d->type == 1 && x.next_every < 0 && last_arrival(q) > 0) return false;
+    if (x.waiting_time == -1) {
+      if (x.next_every < 0) return slot(p, q) == SG_NIL;
+      if (last_arrival(q) > 0) {
+        wr64(sth(q) + H_LST_LO, 0);
+        init_state(q);
+        return false;
+      }
+      return true;
+    }
+    return slot(p, q) != SG_NIL;
+  }
   SG_HD void absent_post(int s, int p) {
     const sg_state_desc& x = st(s);
     sth(s)[H_CHANGED] = 1;
@@ -401,17 +426,17 @@ struct KeyMachine {
   SG_HD void add_state(int s, int p) {
     const sg_state_desc& x = st(s);
     switch (x.kind) {
-      case SG_K_LOGICAL: {   // LogicalPreStateProcessor.addState :62-83
-        int q = x.partner;
-        if (x.is_start || d->type == 1) {
-          if (llen(s, 1) == 0) ladd(s, 1, p);
-          if (llen(q, 1) == 0) ladd(q, 1, p);
-        } else {
-          ladd(s, 1, p);
-          ladd(q, 1, p);
+      case SG_K_ALOGICAL:    // AbsentLogicalPreStateProcessor.addState :83-105
+        if (!sth(s)[H_ACTIVE]) return;
+        logical_add(s, p);
+        if (!x.is_start && x.waiting_time != -1) {
+          tq_push(s, pts(p) + x.waiting_time);
+          if (st(x.partner).kind == SG_K_ALOGICAL) tq_push(x.partner, pts(p) + st(x.partner).waiting_time);
         }
         return;
-      }
+      case SG_K_LOGICAL:     // LogicalPreStateProcessor.addState :62-83
+        logical_add(s, p);
+        return;
       case SG_K_ABSENT: {    // AbsentStreamPreStateProcessor.addState :77-101
         if (!sth(s)[H_ACTIVE]) return;
         if (d->type == 1) { lclear(s, 1); ladd(s, 1, p); }
@@ -430,12 +455,30 @@ struct KeyMachine {
         return;
     }
   }
+  SG_HD void logical_add(int s, int p) {
+    const sg_state_desc& x = st(s);
+    int q = x.partner;
+    if (x.is_start || d->type == 1) {
+      if (llen(s, 1) == 0) ladd(s, 1, p);
+      if (llen(q, 1) == 0) ladd(q, 1, p);
+    } else {
+      ladd(s, 1, p);
+      ladd(q, 1, p);
+    }
+  }
   // ---- addEveryState
   SG_HD void add_every_state(int s, int p) {
     const sg_state_desc& x = st(s);
     int c = clone_partial(p);
     if (failed) return;
     switch (x.kind) {
+      case SG_K_ALOGICAL:    // AbsentLogicalPreStateProcessor.addEveryState :107-120
+        if (slot(c, s) != SG_NIL) set_pts(c, slot_ts(c, s));   // timestamp of the last arrived event
+        slot(c, s) = SG_NIL;
+        slot(c, x.partner) = SG_NIL;
+        ladd(s, 1, c);
+        ladd(x.partner, 1, c);
+        return;
       case SG_K_LOGICAL:     // LogicalPreStateProcessor.addEveryState :86-92
         slot(c, s) = SG_NIL;
         ladd(s, 1, c);
@@ -454,7 +497,8 @@ struct KeyMachine {
   // ---- init (StreamPreStateProcessor.init :157-166)
   SG_HD void init_state(int s) {
     const sg_state_desc& x = st(s);
-    bool seq_abs = d->type == 1 && x.next_state >= 0 && st(x.next_state).kind == SG_K_ABSENT;
+    bool seq_abs = d->type == 1 && x.next_state >= 0 &&
+                   (st(x.next_state).kind == SG_K_ABSENT || st(x.next_state).kind == SG_K_ALOGICAL);   // instanceof AbsentPreStateProcessor
     if (x.is_start && (!sth(s)[H_INIT] || x.next_every >= 0 || seq_abs)) {
       int p = new_partial();
       if (failed) return;
@@ -467,7 +511,7 @@ struct KeyMachine {
     const sg_state_desc& x = st(s);
     if (x.kind == SG_K_COUNT && sth(s)[H_SRESET]) { sth(s)[H_SRESET] = 0; init_state(s); }
     move_nae(s);
-    if (x.kind == SG_K_LOGICAL) move_nae(x.partner);
+    if (x.kind == SG_K_LOGICAL || x.kind == SG_K_ALOGICAL) move_nae(x.partner);
   }
   SG_HD void move_nae(int s) {
     int32_t* n = list(s, 1);
@@ -485,7 +529,7 @@ struct KeyMachine {
   }
   SG_HD void reset_state(int s) {
     const sg_state_desc& x = st(s);
-    if (x.kind == SG_K_LOGICAL) {   // LogicalPreStateProcessor.resetState :94-116
+    if (x.kind == SG_K_LOGICAL || x.kind == SG_K_ALOGICAL) {   // LogicalPreStateProcessor.resetState :94-116
       int q = x.partner;
       if (x.logical_type == 1 || llen(s, 0) == llen(q, 0)) {
         lclear(s, 0);
@@ -536,6 +580,7 @@ struct KeyMachine {
   SG_HD int process_and_return(int s, int e, int* ret, int retcap) {
     const sg_state_desc& x = st(s);
     if (x.kind == SG_K_ABSENT && !sth(s)[H_ACTIVE]) return 0;
+    if (x.kind == SG_K_ALOGICAL) { alogical_process(s, e); return 0; }
     int nret = 0;
     int32_t* l = list(s, 0);
     int n = l[0];
@@ -591,19 +636,148 @@ struct KeyMachine {
     return nret;
   }
 
-  // ---------------------------------------------------------------- absence timers (Scheduler FIFO)
-  SG_HD int absent_index(int s) {
-    int k = 0;
-    for (int i = 0; i < s; ++i) if (st(i).kind == SG_K_ABSENT) ++k;
-    return k;
+  // AbsentLogicalPreStateProcessor.processAndReturn :244-305 (an S event on the absent side; returns nothing)
+  SG_HD void alogical_process(int s, int e) {
+    const sg_state_desc& x = st(s);
+    if (!sth(s)[H_ACTIVE]) return;
+    int32_t* l = list(s, 0);
+    int n = l[0], w = 0;
+    const int64_t t = ets(e);
+    for (int r = 0; r < n && !failed; ++r) {
+      int p = l[1 + r];
+      if (is_expired(s, p, t)) {
+        int we = within_every(s);
+        if (we >= 0) {
+          if (we == s || we == x.partner) { fail(SG_EUNSUPPORTED); break; }   // CME in the reference
+          add_every_state(we, p);
+          update_state(we);
+        }
+        continue;
+      }
+      if (x.logical_type == 1 && slot(p, x.partner) != SG_NIL) continue;
+      const int cur = slot(p, s);
+      slot(p, s) = e;
+      sth(s)[H_CHANGED] = 0;
+      if (filter(s, p)) post_process(s, p);
+      if (x.waiting_time != -1 || (d->type == 1 && x.logical_type == 0 && x.next_every >= 0)) slot(p, s) = cur;
+      bool remove = false;
+      if (sth(x.this_last)[H_RETURNED]) {   // passed the filter: no longer an absence candidate
+        sth(x.this_last)[H_RETURNED] = 0;
+        remove = true;
+        if (d->type == 1) list_remove_first(x.partner, 0, p);
+      }
+      if (!sth(s)[H_CHANGED]) {
+        slot(p, s) = cur;
+        if (d->type == 1) {
+          if (remove) { fail(SG_EUNSUPPORTED); break; }   // double iterator.remove() in the reference
+          remove = true;
+        }
+      }
+      if (!remove) l[1 + w++] = p;
+    }
+    if (!failed) l[0] = w;
   }
-  SG_HD void absent_schedule(int s, int64_t t) {   // lastScheduledTime = t; scheduler.notifyAt(t)
-    wr64(sth(s) + H_LST_LO, t);
+  SG_HD void list_remove_first(int s, int which, int p) {   // LinkedList.remove(Object)
+    int32_t* l = list(s, which);
+    for (int i = 0; i < l[0]; ++i)
+      if (l[1 + i] == p) {
+        for (int j = i + 1; j < l[0]; ++j) l[j] = l[1 + j];
+        l[0]--;
+        return;
+      }
+  }
+  // a fresh pooled StreamEvent (StreamEventPool.borrowEvent): timestamp -1, every attribute null
+  SG_HD int blank_event() {
+    int e = alloc_ev();
+    if (failed) return 0;
+    int32_t* x = ev(e);
+    wr64(x, -1);
+    wr64(x + 2, 0);
+    x[4] = -1;
+    for (int k = 0; k < g->R; ++k) wr64(x + 6 + 2 * k, 0);
+    return e;
+  }
+  // AbsentLogicalPreStateProcessor.process(ComplexEventChunk) :122-210 for one TIMER event at currentTime
+  SG_HD void alogical_timer(int s, int64_t current) {
+    const sg_state_desc& x = st(s);
+    if (!sth(s)[H_ACTIVE]) return;
+    bool not_processed = true;
+    if (current >= last_arrival(s) + x.waiting_time) {
+      if (x.is_start && d->type == 1 && llen(s, 1) == 0 && llen(s, 0) == 0) {
+        int p = new_partial();
+        if (failed) return;
+        add_state(s, p);
+      } else if (d->type == 1 && llen(s, 1) != 0) {
+        reset_state(s);
+      }
+      update_state(s);
+      int32_t* l = list(s, 0);
+      int n = l[0], w = 0;
+      int emitted[64];
+      int ne = 0;
+      for (int r = 0; r < n && !failed; ++r) {
+        int p = l[1 + r];
+        if (is_expired(s, p, current)) {
+          int we = within_every(s);
+          if (we >= 0) {
+            if (we == s || we == x.partner) { fail(SG_EUNSUPPORTED); break; }
+            add_every_state(we, p);
+            update_state(we);
+          }
+          continue;
+        }
+        const int own = slot(p, s);
+        const bool passed = own == SG_NIL ? current >= pts(p) + x.waiting_time : current >= ets(own) + x.waiting_time;
+        if (passed) {
+          const bool partner_bound = slot(p, x.partner) != SG_NIL;
+          if (x.logical_type == 0 && partner_bound) {              // AND: partner received but did not send out
+            if (ne < 64) emitted[ne++] = p; else fail(SG_ECAPACITY);
+          } else if (!partner_bound) {                               // OR: partner not received; AND: let it process
+            if (own != SG_NIL) { fail(SG_EUNSUPPORTED); break; }     // (a chained absent slot is not representable)
+            slot(p, s) = blank_event();
+            if (x.logical_type == 1) { if (ne < 64) emitted[ne++] = p; else fail(SG_ECAPACITY); }
+          }
+          continue;   // removed
+        }
+        l[1 + w++] = p;
+      }
+      if (failed) return;
+      l[0] = w;
+      not_processed = ne == 0;
+      for (int i = 0; i < ne && !failed; ++i) {   // sendEvent :222-242
+        int p = emitted[i];
+        if (x.has_selector) emit(p);
+        if (x.next_state >= 0) add_state(x.next_state, p);
+        if (x.next_every >= 0) add_every_state(x.next_every, p);
+        else if (x.is_start) {
+          sth(s)[H_ACTIVE] = 0;
+          if (x.logical_type == 1 && st(x.partner).kind == SG_K_ALOGICAL) sth(x.partner)[H_ACTIVE] = 0;
+        }
+        if (x.callback >= 0) count_start_state_reset(x.callback, 0);
+      }
+      wr64(sth(s) + H_LST_LO, 0);
+    }
+    if (x.next_every >= 0 || (not_processed && x.is_start)) {   // schedule again :199-209
+      const int64_t la = last_arrival(s);
+      tq_push(s, (la == 0 ? now : la) + x.waiting_time);
+    }
+  }
+
+  // ---------------------------------------------------------------- absence timers (Scheduler FIFO)
+  SG_HD int absent_index(int s) {   // this state's scheduler (sg_nfa_desc.sched_state: creation order)
+    for (int k = 0; k < d->n_sched; ++k) if (d->sched_state[k] == s) return k;
+    return 0;
+  }
+  SG_HD void tq_push(int s, int64_t t) {   // scheduler.notifyAt(t)
     int32_t* q = tq(absent_index(s));
     if (q[1] >= g->Q) { fail(SG_ECAPACITY); return; }
     int pos = (q[0] + q[1]) % g->Q;
     wr64(q + 2 + 2 * pos, t);
     q[1]++;
+  }
+  SG_HD void absent_schedule(int s, int64_t t) {   // lastScheduledTime = t; scheduler.notifyAt(t)
+    wr64(sth(s) + H_LST_LO, t);
+    tq_push(s, t);
   }
   SG_HD void absent_update_last_arrival(int s, int64_t ts) { absent_schedule(s, ts + st(s).waiting_time); }
   SG_HD bool tq_empty(int ai) { return tq(ai)[1] == 0; }
@@ -671,9 +845,12 @@ struct KeyMachine {
   SG_HD void create_runtime() {   // QueryRuntime.clone -> init (StreamInnerStateRuntime.init per state)
     format();
     for (int k = 0; k < d->n_init && !failed; ++k) init_state(d->init_order[k]);
-    if (!clone) {   // SiddhiAppRuntime.start -> AbsentStreamPreStateProcessor.start :277-286 (not for clones)
-      for (int s = 0; s < g->S; ++s)
+    if (!clone) {   // SiddhiAppRuntime.start -> Absent{Stream,Logical}PreStateProcessor.start (not for clones)
+      for (int s = 0; s < g->S; ++s) {
         if (st(s).kind == SG_K_ABSENT && st(s).is_start && sth(s)[H_ACTIVE]) absent_schedule(s, now + st(s).waiting_time);
+        if (st(s).kind == SG_K_ALOGICAL && st(s).is_start && st(s).waiting_time != -1 && sth(s)[H_ACTIVE])
+          tq_push(s, now + st(s).waiting_time);   // :334-345
+      }
     }
   }
   SG_HD void reset_and_update() {   // StateStreamRuntime.resetAndUpdate :96-99
@@ -739,9 +916,7 @@ struct KeyMachine {
 template <class Rows>
 SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t emit_from = 0) {
   const int A = m.g->A;
-  int abs_state[SG_MAX_STATES];
-  for (int s = 0, k = 0; s < m.g->S; ++s)
-    if (m.st(s).kind == SG_K_ABSENT) abs_state[k++] = s;
+  const int32_t* abs_state = m.d->sched_state;   // scheduler order
   if (create_at_start && !m.hdr()[K_CREATED]) m.create_runtime();
   int64_t nown = rows.n_own();
   int64_t nrows = rows.n_rows();
@@ -771,7 +946,8 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t em
           m.tq_pop(ai);
           m.maybe_gc();
           if (m.failed) break;
-          m.absent_timer(abs_state[ai], t);
+          if (m.st(abs_state[ai]).kind == SG_K_ALOGICAL) m.alogical_timer(abs_state[ai], t);
+          else m.absent_timer(abs_state[ai], t);
         }
       }
       m.set_pos((int64_t)rows.index_of(ltim));
@@ -818,7 +994,7 @@ SG_HD inline SgChunkRule sg_chunk_rule(const sg_nfa_desc& d) {
   SgChunkRule r{0, 0, 0};
   int starts = 0;
   for (int s = 0; s < d.n_states; ++s) {
-    if (d.states[s].kind == SG_K_ABSENT) return r;
+    if (d.states[s].kind == SG_K_ABSENT || d.states[s].kind == SG_K_ALOGICAL) return r;
     if (d.states[s].is_start) {
       if (d.states[s].next_every != s) return r;
       ++starts;
@@ -874,7 +1050,7 @@ inline SgGeo sg_make_geo(const sg_nfa_desc& d, int P, int E, int C, int L, int Q
   g.L = L;
   g.Q = Q;
   g.A = 0;
-  for (int s = 0; s < d.n_states; ++s) if (d.states[s].kind == SG_K_ABSENT) g.A++;
+  g.A = d.n_sched;   // one timer FIFO per absent state (Scheduler)
   g.nsel = d.n_select;
   g.part_words = 3 + g.S;
   g.ev_words = 6 + 2 * g.R;

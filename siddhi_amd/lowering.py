@@ -196,7 +196,7 @@ def column_layout(ctx: QueryContext) -> List[Tuple[int, int, str]]:
 # ==============================================================================================
 # Flat NFA lowering for the HIP engine
 # ==============================================================================================
-K_STREAM, K_COUNT, K_LOGICAL, K_ABSENT = 0, 1, 2, 3
+K_STREAM, K_COUNT, K_LOGICAL, K_ABSENT, K_ALOGICAL = 0, 1, 2, 3, 4
 SHAPE_GENERAL, SHAPE_EVERY_NEXT_CMP, SHAPE_EVERY_ABSENT_EQ = 0, 1, 2
 
 # postfix predicate opcodes (shared with siddhi_amd/csrc/nfa_desc.h)
@@ -273,6 +273,7 @@ class FlatNFA:
     out_progs: list = field(default_factory=list)
     out_types: List[str] = field(default_factory=list)
     having_prog: list = field(default_factory=list)   # postfix over the output columns (VAR word 3 = column)
+    sched: List[int] = field(default_factory=list)    # scheduler states in creation order (sg_nfa_desc.sched_state)
 
 
 def _cmp_domain(lt: str, rt: str, op: str) -> int:
@@ -428,11 +429,17 @@ class _FlatBuilder:
             pres.extend(inner_pres)
             return ("E", inner)
         if isinstance(el, C.LogicalStateElement):
-            if not isinstance(el.e1, C.StreamStateElement) or not isinstance(el.e2, C.StreamStateElement):
-                raise LoweringError("logical absent patterns are not supported")
+            # a `not S [for T]` side becomes an AbsentLogicalPre/PostStateProcessor pair
+            # (StateInputStreamParser.java:281-374); its waiting time is -1 without `for`
             lt = 0 if el.type == "AND" else 1
-            s2 = FlatState(K_LOGICAL, -1, None, logical_type=lt)
-            s1 = FlatState(K_LOGICAL, -1, None, logical_type=lt)
+
+            def side(x):
+                if isinstance(x, C.AbsentStreamStateElement):
+                    wt = x.waiting_time if x.waiting_time is not None else -1
+                    return FlatState(K_ALOGICAL, -1, None, logical_type=lt, waiting_time=wt)
+                return FlatState(K_LOGICAL, -1, None, logical_type=lt)
+            s1 = side(el.e1)
+            s2 = side(el.e2)
             r2 = self.parse(el.e2, is_start, pres, s2)    # element2 parsed first (:345-357)
             r1 = self.parse(el.e1, is_start, pres, s1)
             s1.partner, s2.partner = r2[1], r1[1]
@@ -466,7 +473,7 @@ class _FlatBuilder:
     def set_next(self, post: int, pre: int):
         st = self.states[post]
         st.next_state = pre
-        if st.kind == K_LOGICAL:
+        if st.kind in (K_LOGICAL, K_ALOGICAL):   # LogicalPostStateProcessor.setNextStatePreProcessor :134-137
             self.states[st.partner].next_state = pre
         if st.kind == K_COUNT and st.is_start and self.stype == 1 and st.min_count == 0:
             self.states[pre].callback = post
@@ -474,7 +481,7 @@ class _FlatBuilder:
     def set_next_every(self, post: int, pre: int):
         st = self.states[post]
         st.next_every = pre
-        if st.kind == K_LOGICAL:
+        if st.kind in (K_LOGICAL, K_ALOGICAL):   # :139-142
             self.states[st.partner].next_every = pre
 
     def set_selector(self, n):
@@ -506,6 +513,21 @@ class _FlatBuilder:
             r.selector = self.states[s].has_selector if r.multi else self.states[st.this_last].has_selector
             r.stab.append(s)
             order.append(s)
+
+    def sched_order(self, n, out):
+        """Scheduler creation order: the parser creates an absent processor's Scheduler with the processor -- a
+        logical state's element1 side before element2 (StateInputStreamParser.java:290-320) -- and clones follow
+        the same order (NextInnerStateRuntime / LogicalInnerStateRuntime.clone)."""
+        if n[0] == "N":
+            self.sched_order(n[1], out)
+            self.sched_order(n[2], out)
+        elif n[0] == "L":
+            self.sched_order(n[1], out)
+            self.sched_order(n[2], out)
+        elif n[0] == "E":
+            self.sched_order(n[1], out)
+        elif self.states[n[1]].kind in (K_ABSENT, K_ALOGICAL):
+            out.append(n[1])
 
     def reset_ops(self, n, out):
         if n[0] == "N":
@@ -602,6 +624,7 @@ class _FlatBuilder:
                       self.states, receivers, order, ro, uo, start_ids, self.retained, select,
                       column_layout(self.ctx))
         nfa.out_progs, nfa.out_types, nfa.having_prog = out_progs, out_types, having_prog
+        self.sched_order(root, nfa.sched)
         _classify(nfa, root, self)
         return nfa
 

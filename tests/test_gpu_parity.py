@@ -168,3 +168,19 @@ def test_general_kernel_chunked_multi_push(cfg):
         lo = hi
     got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True, chunk_rows=9), q, parts)
     assert_same(got, want)
+
+
+from ref_kats import REF_KATS, check, run_ref_kat  # noqa: E402
+
+
+@pytest.mark.parametrize("case", REF_KATS, ids=[k["name"] for k in REF_KATS])
+def test_ref_kat_on_gpu(case):
+    """The reference suites' own assertions (tests/golden/ref_kats.json) through the C-ABI on the MI355X, on the
+    engine route lowering picks and on the general kernel, both row- and timestamp-identical to the oracle."""
+    from siddhi_amd._native import GpuEngine
+    rows_o, tss_o = run_ref_kat(case, OracleEngine)
+    rows, tss = run_ref_kat(case, gpu_engine())
+    check(case, rows)
+    assert (rows, tss) == (rows_o, tss_o)
+    rows_g, tss_g = run_ref_kat(case, lambda ctx: GpuEngine(ctx, force_general=True))
+    assert (rows_g, tss_g) == (rows_o, tss_o)

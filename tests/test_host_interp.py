@@ -116,3 +116,15 @@ def test_chunk_rules():
         assert lib.hi_chunk_rule(ct.byref(desc), ct.byref(h)) == kind, cfg
         if cfg == "C3b":
             assert h.value == 1 + 5 + 1 + 1
+
+
+from ref_kats import REF_KATS, check, run_ref_kat  # noqa: E402
+
+
+@pytest.mark.parametrize("case", REF_KATS, ids=[k["name"] for k in REF_KATS])
+def test_machine_ref_kat(case):
+    """The reference suites' own assertions (tests/golden/ref_kats.json) on the GPU machine's logic, on the CPU."""
+    rows, tss = run_ref_kat(case, HostInterpEngine)
+    check(case, rows)
+    rows_o, tss_o = run_ref_kat(case, OracleEngine)
+    assert rows == rows_o and tss == tss_o
