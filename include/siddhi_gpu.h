@@ -210,6 +210,19 @@ typedef struct sg_matches {
   uint32_t* vnull;
 } sg_matches;
 
+/* Typed SoA delivery of match tuples (sg_poll_columns / sg_push_deliver): each non-NULL array receives one entry
+ * per delivered match, in delivery order.  cols[k] is output column k (k < n_select of sg_match_records) as its
+ * Attribute.Type: 4 bytes for INT / FLOAT / STRING id / BOOL, 8 bytes for LONG / DOUBLE; nulls[k] (optional)
+ * one byte per row, 1 = null.  Pinned host memory (sg_host_alloc) makes the copies asynchronous DMA. */
+typedef struct sg_match_columns {
+  uint64_t* trigger;
+  int64_t* ts;
+  int32_t* key;
+  uint32_t* group;
+  void* cols[SG_MAX_SELECT];
+  uint8_t* nulls[SG_MAX_SELECT];
+} sg_match_columns;
+
 typedef struct sg_timing {
   float pred_ms, partition_ms, match_ms, output_ms, total_ms;   /* HIP-event times of the last push */
   int64_t events, matches;
@@ -224,6 +237,17 @@ int sg_advance_time(sg_handle* h, int64_t now, uint64_t trigger_index);
 int sg_pending(sg_handle* h, int64_t* n);
 /* Copy up to cap pending matches into host arrays (fields may be NULL to skip) and consume them. */
 int sg_poll(sg_handle* h, sg_matches* out, int64_t cap, int64_t* n);
+/* Copy up to cap pending matches, transposed on the GPU into typed SoA columns, into out (NULL arrays are
+ * skipped) and consume them (QuerySelector -> QueryCallback.receiveStreamEvent delivery,
+ * C/query/output/callback/QueryCallback.java:52-85, as columns). */
+int sg_poll_columns(sg_handle* h, const sg_match_columns* out, int64_t cap, int64_t* n);
+/* One call for a batch and its matches (InputHandler.send ... QueryCallback delivery,
+ * C/stream/input/InputHandler.java:57-86): a host batch is copied in chunks (sg_options.ingress_rows), each
+ * chunk's kernels run while the next chunk's columns are copied in, and each chunk's matches are transposed into
+ * SoA columns and copied out into `out` while the next chunk computes; *n receives the number of rows written.
+ * Matches pending before the call are delivered first.  If more than cap matches are produced, the surplus
+ * stays pending (sg_pending / sg_poll_columns) and SG_ECAPACITY is returned after the whole batch ran. */
+int sg_push_deliver(sg_handle* h, const sg_batch* b, const sg_match_columns* out, int64_t cap, int64_t* n);
 /* Zero-copy view of the pending match records in HBM (valid until the next push/poll/reset). */
 int sg_device_records(sg_handle* h, sg_match_records* view);
 int sg_discard(sg_handle* h);           /* drop pending matches without copying */
@@ -240,6 +264,17 @@ int sg_snapshot(sg_handle* h, void* buf, size_t cap, size_t* size);
 int sg_restore(sg_handle* h, const void* buf, size_t size);
 int sg_close(sg_handle* h);
 const char* sg_last_error(const sg_handle* h);
+/* Host partition router (router.cpp): replaces the per-event key lookup of PartitionStreamReceiver.receive /
+ * PartitionRuntime.cloneIfNotExist (C/partition/PartitionStreamReceiver.java:80-275,
+ * C/partition/PartitionRuntime.java:255-308) for SoA batches.  Raw partition-key values (64-bit: integers, float
+ * bits, or string-dictionary ids) become dense ids in first-seen order (the reference's clone order); each key is
+ * assigned to shard mix64(dense) mod n_shards (one shard per GPU) and gets a dense id inside its shard.  The
+ * dictionary persists across calls.  threads = 0: all hardware threads. */
+typedef struct sg_router sg_router;
+int sg_router_open(int n_shards, int threads, sg_router** out);
+int sg_router_route(sg_router* r, int64_t n, const int64_t* raw, int32_t* dense, int32_t* shard, int32_t* local);
+int sg_router_keys(const sg_router* r, int64_t* n_keys, int32_t shard, int64_t* shard_keys);
+int sg_router_close(sg_router* r);
 /* Pinned host memory for batch columns (the ingress then copies asynchronously at full PCIe rate). */
 int sg_host_alloc(size_t bytes, void** p);
 int sg_host_free(void* p);

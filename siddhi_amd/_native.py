@@ -18,7 +18,8 @@ SG_ABI_VERSION = 2
 
 SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
            "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version",
-           "sg_snapshot", "sg_restore", "sg_host_alloc", "sg_host_free"]
+           "sg_snapshot", "sg_restore", "sg_host_alloc", "sg_host_free", "sg_poll_columns", "sg_push_deliver",
+           "sg_router_open", "sg_router_route", "sg_router_keys", "sg_router_close"]
 
 I32, I64, U64 = ct.c_int32, ct.c_int64, ct.c_uint64
 
@@ -73,6 +74,11 @@ class sg_matches(ct.Structure):
                 ("group", ct.c_void_p), ("vals", ct.c_void_p), ("vnull", ct.c_void_p)]
 
 
+class sg_match_columns(ct.Structure):
+    _fields_ = [("trigger", ct.c_void_p), ("ts", ct.c_void_p), ("key", ct.c_void_p), ("group", ct.c_void_p),
+                ("cols", ct.c_void_p * SG_MAX_SELECT), ("nulls", ct.c_void_p * SG_MAX_SELECT)]
+
+
 class sg_match_records(ct.Structure):
     _fields_ = [("n", I64), ("record_bytes", I32), ("n_select", I32), ("base", ct.c_void_p)]
 
@@ -117,6 +123,12 @@ def load_library(path: str = LIB_PATH):
         lib.sg_restore.argtypes = [P, P, ct.c_size_t]
         lib.sg_host_alloc.argtypes = [ct.c_size_t, ct.POINTER(P)]
         lib.sg_host_free.argtypes = [P]
+        lib.sg_poll_columns.argtypes = [P, P, I64, ct.POINTER(I64)]
+        lib.sg_push_deliver.argtypes = [P, P, P, I64, ct.POINTER(I64)]
+        lib.sg_router_open.argtypes = [ct.c_int, ct.c_int, ct.POINTER(P)]
+        lib.sg_router_route.argtypes = [P, I64, P, P, P, P]
+        lib.sg_router_keys.argtypes = [P, ct.POINTER(I64), I32, ct.POINTER(I64)]
+        lib.sg_router_close.argtypes = [P]
         lib.sg_last_error.argtypes = [P]
         lib.sg_last_error.restype = ct.c_char_p
         lib.sg_version.restype = ct.c_char_p
@@ -251,6 +263,18 @@ class Handle:
             self.check(self.lib.sg_poll(self.h, ct.byref(m), n, ct.byref(got)))
         return tr, ts, ky, gr, vals[:, :nsel], vn
 
+    def poll_columns(self, cols: "sg_match_columns", cap: int) -> int:
+        """sg_poll_columns: up to cap pending matches as typed SoA columns into `cols` (host arrays)."""
+        n = I64()
+        self.check(self.lib.sg_poll_columns(self.h, ct.byref(cols), int(cap), ct.byref(n)))
+        return n.value
+
+    def push_deliver(self, b: sg_batch, cols: "sg_match_columns", cap: int) -> int:
+        """sg_push_deliver: push a batch and receive its matches (and any pending ones) as SoA columns."""
+        n = I64()
+        self.check(self.lib.sg_push_deliver(self.h, ct.byref(b), ct.byref(cols), int(cap), ct.byref(n)))
+        return n.value
+
     def device_records(self) -> sg_match_records:
         m = sg_match_records()
         self.check(self.lib.sg_device_records(self.h, ct.byref(m)))
@@ -285,6 +309,79 @@ class Handle:
         if self.h:
             self.lib.sg_close(self.h)
             self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def column_dtypes(nfa: L.FlatNFA):
+    """numpy dtypes of the delivered output columns (sg_match_columns.cols): 4 or 8 bytes by Attribute.Type."""
+    types = nfa.out_types if nfa.out_progs else [t for (_, _, _, t) in nfa.select]
+    m = {"STRING": np.int32, "INT": np.int32, "BOOL": np.int32, "FLOAT": np.float32, "LONG": np.int64,
+         "DOUBLE": np.float64}
+    return [m[t] for t in types]
+
+
+class ColumnSink:
+    """Host arrays for SoA delivery (sg_match_columns), pinned when `pinned` (sg_host_alloc)."""
+
+    def __init__(self, nfa: L.FlatNFA, cap: int, pinned: bool = True, fields=("trigger", "ts", "key", "group"),
+                 nulls: bool = True):
+        self.cap = cap
+        self._keep = []
+
+        def arr(dt):
+            if pinned:
+                p = PinnedArray(cap, dt)
+                self._keep.append(p)
+                return p.array
+            return np.zeros(cap, dt)
+        self.trigger = arr(np.uint64) if "trigger" in fields else None
+        self.ts = arr(np.int64) if "ts" in fields else None
+        self.key = arr(np.int32) if "key" in fields else None
+        self.group = arr(np.uint32) if "group" in fields else None
+        self.cols = [arr(dt) for dt in column_dtypes(nfa)]
+        self.nulls = [arr(np.uint8) for _ in self.cols] if nulls else None
+        s = sg_match_columns()
+        for f in ("trigger", "ts", "key", "group"):
+            a = getattr(self, f)
+            setattr(s, f, a.ctypes.data if a is not None else None)
+        for k, a in enumerate(self.cols):
+            s.cols[k] = a.ctypes.data
+            if self.nulls is not None:
+                s.nulls[k] = self.nulls[k].ctypes.data
+        self.struct = s
+
+
+class Router:
+    """The native host partition router (sg_router_*): dense first-seen key ids, shard and per-shard dense ids."""
+
+    def __init__(self, n_shards: int = 1, threads: int = 0):
+        self.lib = load_library()
+        self.r = ct.c_void_p()
+        rc = self.lib.sg_router_open(n_shards, threads, ct.byref(self.r))
+        if rc != 0:
+            raise SgError(rc, "sg_router_open failed")
+
+    def route(self, raw: np.ndarray, dense=None, shard=None, local=None):
+        raw = np.ascontiguousarray(raw, np.int64)
+        ptr = lambda a: a.ctypes.data if a is not None else None   # noqa: E731
+        rc = self.lib.sg_router_route(self.r, len(raw), raw.ctypes.data, ptr(dense), ptr(shard), ptr(local))
+        if rc != 0:
+            raise SgError(rc, "sg_router_route failed")
+
+    def keys(self, shard: int = -1):
+        n, sk = I64(), I64()
+        self.lib.sg_router_keys(self.r, ct.byref(n), shard, ct.byref(sk))
+        return n.value, sk.value
+
+    def close(self):
+        if self.r:
+            self.lib.sg_router_close(self.r)
+            self.r = None
 
     def __del__(self):
         try:

@@ -259,6 +259,228 @@ static BatchView upload(SgHandle& h, const sg_batch* b, int64_t lo, int64_t cnt,
   return upload_to(h.desc, reserve_slot(h, b, cnt, slot), b, lo, cnt, st);
 }
 
+struct ChunkHook {
+  virtual void chunk_done() = 0;
+  virtual ~ChunkHook() {}
+};
+
+static void check_batch(const sg_batch* b) {
+  if (b->n >= (1ll << 30) - 1) throw SgError(SG_EINVAL, "batch too large (max 2^30-2 rows)");
+  if (!b->ts) throw SgError(SG_EINVAL, "batch without timestamps");
+}
+
+static BatchView device_view(const sg_nfa_desc& d, const sg_batch* b) {
+  BatchView bv;
+  bv.n = b->n;
+  bv.base_index = b->base_index;
+  bv.key_bound = b->key_bound;
+  bv.ts = b->ts;
+  bv.stream = b->stream;
+  bv.key = b->key;
+  bv.index = b->index;
+  memset(&bv.cols, 0, sizeof(bv.cols));
+  for (int c = 0; c < d.n_cols; ++c) {
+    bv.cols.col[c] = b->cols ? b->cols[c] : nullptr;
+    bv.cols.nul[c] = b->nulls ? b->nulls[c] : nullptr;
+  }
+  return bv;
+}
+
+// ---- SoA match delivery (QuerySelector -> QueryCallback.receiveStreamEvent, C/query/output/callback/
+// QueryCallback.java:52-85, as typed columns).  The pending AoS records are transposed on the GPU into a staging
+// buffer of columns; the columns are copied to the caller on a D2H stream, double-buffered so one chunk's copy
+// overlaps the next chunk's kernels.
+struct ColLayout {   // staging layout for `cap` rows
+  int ns;
+  int32_t width[SG_MAX_SELECT];
+  size_t off_trig, off_ts, off_key, off_grp, off_col[SG_MAX_SELECT], off_nul[SG_MAX_SELECT], bytes;
+};
+static ColLayout col_layout(const sg_nfa_desc& d, int64_t cap) {
+  ColLayout L;
+  L.ns = out_cols(d);
+  size_t o = 0;
+  auto take = [&](size_t w) { size_t r = o; o += ((w * (size_t)cap + 255) / 256) * 256; return r; };
+  L.off_trig = take(8);
+  L.off_ts = take(8);
+  L.off_key = take(4);
+  L.off_grp = take(4);
+  for (int k = 0; k < L.ns; ++k) {
+    const int t = d.n_out > 0 ? d.out_type[k] : d.sel_type[k];
+    L.width[k] = col_width(t);
+    L.off_col[k] = take((size_t)L.width[k]);
+  }
+  for (int k = 0; k < L.ns; ++k) L.off_nul[k] = take(1);
+  L.bytes = o;
+  return L;
+}
+
+// one thread per record: 16-B loads of the record, one coalesced store per column
+__global__ void __launch_bounds__(256) k_to_columns(int64_t n, const char* __restrict__ rec, int stride, ColLayout L,
+                                                    char* __restrict__ stage) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+  const U4* r = (const U4*)(rec + (size_t)i * stride);
+  const U4 h0 = r[0], h1 = r[1];   // trigger, ts | key, group, vnull, pad
+  ((uint64_t*)(stage + L.off_trig))[i] = ((uint64_t)h0.y << 32) | h0.x;
+  ((uint64_t*)(stage + L.off_ts))[i] = ((uint64_t)h0.w << 32) | h0.z;
+  ((uint32_t*)(stage + L.off_key))[i] = h1.x;
+  ((uint32_t*)(stage + L.off_grp))[i] = h1.y;
+  const uint32_t vn = h1.z;
+  const uint64_t* v = (const uint64_t*)(rec + (size_t)i * stride + 32);
+  for (int k = 0; k < L.ns; ++k) {
+    const uint64_t bits = v[k];
+    if (L.width[k] == 8) ((uint64_t*)(stage + L.off_col[k]))[i] = bits;
+    else ((uint32_t*)(stage + L.off_col[k]))[i] = (uint32_t)bits;
+    ((uint8_t*)(stage + L.off_nul[k]))[i] = (uint8_t)((vn >> k) & 1u);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_to_matches(int64_t n, const char* __restrict__ rec, int stride, int ns,
+                                                    uint64_t* __restrict__ trig, int64_t* __restrict__ ts,
+                                                    int32_t* __restrict__ key, uint32_t* __restrict__ grp,
+                                                    int64_t* __restrict__ vals, uint32_t* __restrict__ vn) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const char* r = rec + (size_t)i * stride;
+  trig[i] = *(const uint64_t*)r;
+  ts[i] = *(const int64_t*)(r + 8);
+  key[i] = *(const int32_t*)(r + 16);
+  grp[i] = *(const uint32_t*)(r + 20);
+  vn[i] = *(const uint32_t*)(r + 24);
+  for (int k = 0; k < ns; ++k) vals[(size_t)i * ns + k] = ((const int64_t*)(r + 32))[k];
+}
+
+static void egress_init(SgHandle& h) {
+  if (h.eg.d2h) return;
+  HIPCHK(hipStreamCreateWithFlags(&h.eg.d2h, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k) {
+    HIPCHK(hipEventCreateWithFlags(&h.eg.ready[k], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&h.eg.done[k], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(h.eg.done[k], h.eg.d2h));
+  }
+}
+
+// Deliver up to `cap` pending matches into out (rows [row0, row0 + k)) through staging slot `slot`; returns k.
+// The copies are left in flight on the D2H stream (the caller synchronises it before returning to its caller).
+static int64_t deliver_pending(SgHandle& h, const sg_match_columns* out, int64_t row0, int64_t cap, int slot) {
+  OutStore& o = h.out;
+  const int64_t k = std::min<int64_t>(cap, o.n);
+  if (k <= 0) return 0;
+  egress_init(h);
+  const sg_nfa_desc& d = h.desc;
+  const ColLayout L = col_layout(d, k);
+  if (h.eg.cap[slot] < (int64_t)L.bytes) {   // grow: wait until this slot's last copy has read it
+    HIPCHK(hipEventSynchronize(h.eg.done[slot]));
+    if (h.eg.stage[slot]) HIPCHK(hipFree(h.eg.stage[slot]));
+    h.eg.stage[slot] = nullptr;
+    const size_t want = L.bytes + L.bytes / 4;
+    HIPCHK(hipMalloc(&h.eg.stage[slot], want));
+    h.eg.cap[slot] = (int64_t)want;
+  }
+  char* st = h.eg.stage[slot];
+  HIPCHK(hipStreamWaitEvent(h.stream, h.eg.done[slot], 0));   // slot free again
+  hipLaunchKernelGGL(k_to_columns, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, h.stream, k, (const char*)o.rec,
+                     o.stride, L, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(h.eg.ready[slot], h.stream));
+  o.consume(k, h.stream);   // (stream-ordered after the transpose)
+  HIPCHK(hipStreamWaitEvent(h.eg.d2h, h.eg.ready[slot], 0));
+  auto cp = [&](void* dst, size_t off, size_t w) {
+    if (dst) HIPCHK(hipMemcpyAsync((char*)dst + w * (size_t)row0, st + off, w * (size_t)k, hipMemcpyDeviceToHost, h.eg.d2h));
+  };
+  cp(out->trigger, L.off_trig, 8);
+  cp(out->ts, L.off_ts, 8);
+  cp(out->key, L.off_key, 4);
+  cp(out->group, L.off_grp, 4);
+  for (int c = 0; c < L.ns; ++c) {
+    cp(out->cols[c], L.off_col[c], (size_t)L.width[c]);
+    cp(out->nulls[c], L.off_nul[c], 1);
+  }
+  HIPCHK(hipEventRecord(h.eg.done[slot], h.eg.d2h));
+  return k;
+}
+
+struct DeliverHook : ChunkHook {
+  SgHandle& h;
+  const sg_match_columns* out;
+  int64_t cap, rows = 0;
+  int slot = 0;
+  DeliverHook(SgHandle& hh, const sg_match_columns* o, int64_t c) : h(hh), out(o), cap(c) {}
+  void chunk_done() override {
+    rows += deliver_pending(h, out, rows, cap - rows, slot);
+    slot ^= 1;
+  }
+};
+
+// Host batch ingress in chunks (replacing StreamJunction's per-row fan-out,
+// C/stream/StreamJunction.java:255-316): chunk k+1 is copied on a second HIP stream into the other of two HBM
+// slots while chunk k runs on the handle's stream; consecutive chunks are consecutive sub-pushes, which the
+// carried state makes identical to one push (no_carry handles are therefore never split).  `after` (optional)
+// runs after each chunk's engine pass (match delivery, sg_push_deliver).
+static void ingest_host(SgHandle& h, const sg_batch* b, ChunkHook* after) {
+  const sg_nfa_desc& d = h.desc;
+  const int64_t n = b->n;
+  // Default (measured): batches of >= 32M rows in 4 chunks (copy-bound: 59.0 -> 55.1 ms per
+  // 100M C2 events); smaller chunks lose to per-sub-push kernel overheads, smaller batches are one copy.
+  int64_t C = h.opt.ingress_rows > 0 ? h.opt.ingress_rows : (n >= ((int64_t)32 << 20) ? (n + 3) / 4 : n);
+  if (h.opt.ingress_rows < 0) C = n;
+  if (h.opt.no_carry || n <= C) C = n;
+  const int64_t nch = (n + C - 1) / C;
+  if (nch == 1) {
+    BatchView bv = upload(h, b, 0, n, 0, h.stream);
+    push_view(h, bv, n);
+    if (after) after->chunk_done();
+    return;
+  }
+  if (!h.copy_stream) {
+    HIPCHK(hipStreamCreateWithFlags(&h.copy_stream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(hipEventCreateWithFlags(&h.ev_copied[k], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&h.ev_consumed[k], hipEventDisableTiming));
+    }
+  }
+  SlotPtrs slots[2];
+  for (int s = 0; s < 2; ++s) slots[s] = reserve_slot(h, b, C, s);   // no workspace growth inside the pipeline
+  BatchView cur = upload_to(d, slots[0], b, 0, C, h.copy_stream);
+  HIPCHK(hipEventRecord(h.ev_copied[0], h.copy_stream));
+  // The next chunk's copies are issued from a helper thread: a large hipMemcpyAsync can hold the calling
+  // thread, which would otherwise delay this chunk's kernels (measured).
+  for (int64_t k = 0; k < nch; ++k) {
+    const int64_t lo = k * C, cnt = std::min(C, n - lo);
+    BatchView next;
+    std::thread copier;
+    int copy_rc = hipSuccess;
+    if (k + 1 < nch) {
+      const int s = (int)((k + 1) & 1);
+      if (k + 1 >= 2) HIPCHK(hipStreamWaitEvent(h.copy_stream, h.ev_consumed[s], 0));
+      copier = std::thread([&, s, lo] {
+        try {
+          if (hipSetDevice(h.device) != hipSuccess) { copy_rc = hipErrorInvalidDevice; return; }
+          next = upload_to(d, slots[s], b, lo + C, std::min(C, n - lo - C), h.copy_stream);
+          copy_rc = hipEventRecord(h.ev_copied[s], h.copy_stream);
+        } catch (...) {
+          copy_rc = hipErrorUnknown;
+        }
+      });
+    }
+    try {
+      HIPCHK(hipStreamWaitEvent(h.stream, h.ev_copied[k & 1], 0));
+      push_view(h, cur, cnt);
+      HIPCHK(hipEventRecord(h.ev_consumed[k & 1], h.stream));
+      if (after) after->chunk_done();
+    } catch (...) {
+      if (copier.joinable()) copier.join();
+      hipStreamSynchronize(h.copy_stream);
+      throw;
+    }
+    if (copier.joinable()) copier.join();
+    if (copy_rc != hipSuccess) throw SgError(SG_EHIP, "ingress copy failed");
+    if (k + 1 < nch) cur = next;
+  }
+  HIPCHK(hipStreamSynchronize(h.copy_stream));
+}
+
 // Pinned host memory for batches (cudaHostAlloc-style): the ingress copies from it run asynchronously at
 // full PCIe rate, overlapped with the previous chunk's kernels.
 extern "C" int sg_host_alloc(size_t bytes, void** p) {
@@ -311,85 +533,13 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
     const sg_nfa_desc& d = h.desc;
     int64_t n = b->n;
     if (n <= 0) return;
-    if (n >= (1ll << 30) - 1) throw SgError(SG_EINVAL, "batch too large (max 2^30-2 rows)");
-    if (!b->ts) throw SgError(SG_EINVAL, "batch without timestamps");
+    check_batch(b);
     if (b->on_device) {
-      BatchView bv;
-      bv.n = n;
-      bv.base_index = b->base_index;
-      bv.key_bound = b->key_bound;
-      bv.ts = b->ts;
-      bv.stream = b->stream;
-      bv.key = b->key;
-      bv.index = b->index;
-      memset(&bv.cols, 0, sizeof(bv.cols));
-      for (int c = 0; c < d.n_cols; ++c) {
-        bv.cols.col[c] = b->cols ? b->cols[c] : nullptr;
-        bv.cols.nul[c] = b->nulls ? b->nulls[c] : nullptr;
-      }
+      BatchView bv = device_view(d, b);
       push_view(h, bv, n);
       return;
     }
-    // host batch: ingress in chunks (replacing StreamJunction's per-row fan-out,
-    // C/stream/StreamJunction.java:255-316).  Chunk k+1 is copied on a second HIP stream into the other of
-    // two HBM slots while chunk k runs on the handle's stream; consecutive chunks are consecutive sub-pushes,
-    // which the carried state makes identical to one push (no_carry handles are therefore never split).
-    // Default (measured): batches of >= 32M rows in 4 chunks (copy-bound: 59.0 -> 55.1 ms per
-    // 100M C2 events); smaller chunks lose to per-sub-push kernel overheads, smaller batches are one copy.
-    int64_t C = h.opt.ingress_rows > 0 ? h.opt.ingress_rows : (n >= ((int64_t)32 << 20) ? (n + 3) / 4 : n);
-    if (h.opt.ingress_rows < 0) C = n;
-    if (h.opt.no_carry || n <= C) C = n;
-    const int64_t nch = (n + C - 1) / C;
-    if (nch == 1) {
-      BatchView bv = upload(h, b, 0, n, 0, h.stream);
-      push_view(h, bv, n);
-      return;
-    }
-    if (!h.copy_stream) {
-      HIPCHK(hipStreamCreateWithFlags(&h.copy_stream, hipStreamNonBlocking));
-      for (int k = 0; k < 2; ++k) {
-        HIPCHK(hipEventCreateWithFlags(&h.ev_copied[k], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&h.ev_consumed[k], hipEventDisableTiming));
-      }
-    }
-    SlotPtrs slots[2];
-    for (int s = 0; s < 2; ++s) slots[s] = reserve_slot(h, b, C, s);   // no workspace growth inside the pipeline
-    BatchView cur = upload_to(d, slots[0], b, 0, C, h.copy_stream);
-    HIPCHK(hipEventRecord(h.ev_copied[0], h.copy_stream));
-    // The next chunk's copies are issued from a helper thread: a large hipMemcpyAsync can hold the calling
-    // thread, which would otherwise delay this chunk's kernels (measured).
-    for (int64_t k = 0; k < nch; ++k) {
-      const int64_t lo = k * C, cnt = std::min(C, n - lo);
-      BatchView next;
-      std::thread copier;
-      int copy_rc = hipSuccess;
-      if (k + 1 < nch) {
-        const int s = (int)((k + 1) & 1);
-        if (k + 1 >= 2) HIPCHK(hipStreamWaitEvent(h.copy_stream, h.ev_consumed[s], 0));
-        copier = std::thread([&, s, lo] {
-          try {
-            if (hipSetDevice(h.device) != hipSuccess) { copy_rc = hipErrorInvalidDevice; return; }
-            next = upload_to(d, slots[s], b, lo + C, std::min(C, n - lo - C), h.copy_stream);
-            copy_rc = hipEventRecord(h.ev_copied[s], h.copy_stream);
-          } catch (...) {
-            copy_rc = hipErrorUnknown;
-          }
-        });
-      }
-      try {
-        HIPCHK(hipStreamWaitEvent(h.stream, h.ev_copied[k & 1], 0));
-        push_view(h, cur, cnt);
-        HIPCHK(hipEventRecord(h.ev_consumed[k & 1], h.stream));
-      } catch (...) {
-        if (copier.joinable()) copier.join();
-        hipStreamSynchronize(h.copy_stream);
-        throw;
-      }
-      if (copier.joinable()) copier.join();
-      if (copy_rc != hipSuccess) throw SgError(SG_EHIP, "ingress copy failed");
-      if (k + 1 < nch) cur = next;
-    }
-    HIPCHK(hipStreamSynchronize(h.copy_stream));
+    ingest_host(h, b, nullptr);
   });
 }
 
@@ -442,28 +592,88 @@ int sg_poll(sg_handle* hh, sg_matches* out, int64_t cap, int64_t* n) {
   return guard(hh, [&] {
     HIPCHK(hipSetDevice(h.device));
     OutStore& o = h.out;
-    int64_t k = std::min<int64_t>(cap, o.n);
-    hipStream_t st = h.stream;
-    int ns = out_cols(h.desc);
-    size_t stride = 32 + 8 * (size_t)ns;
+    const int64_t k = std::min<int64_t>(cap, o.n);
     if (k > 0) {
-      std::vector<char> tmp((size_t)k * stride);
-      HIPCHK(hipMemcpyAsync(tmp.data(), o.rec, (size_t)k * stride, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      for (int64_t i = 0; i < k; ++i) {
-        const char* r = tmp.data() + (size_t)i * stride;
-        if (out->trigger) memcpy(out->trigger + i, r, 8);
-        if (out->ts) memcpy(out->ts + i, r + 8, 8);
-        if (out->key) memcpy(out->key + i, r + 16, 4);
-        if (out->group) memcpy(out->group + i, r + 20, 4);
-        if (out->vnull) memcpy(out->vnull + i, r + 24, 4);
-        if (out->vals && ns) memcpy(out->vals + i * ns, r + 32, 8 * (size_t)ns);
+      // the sg_matches layout is built on the GPU (header fields split into columns, values row-major as in the
+      // records), then copied field by field: no host-side transpose
+      egress_init(h);
+      const int ns = out_cols(h.desc);
+      const size_t need = (size_t)k * (8 + 8 + 4 + 4 + 4) + (size_t)k * 8 * ns + 1024;
+      if (h.eg.cap[0] < (int64_t)need) {
+        HIPCHK(hipEventSynchronize(h.eg.done[0]));
+        if (h.eg.stage[0]) HIPCHK(hipFree(h.eg.stage[0]));
+        h.eg.stage[0] = nullptr;
+        HIPCHK(hipMalloc(&h.eg.stage[0], need + need / 4));
+        h.eg.cap[0] = (int64_t)(need + need / 4);
       }
-      o.consume(k, st);
+      char* st = h.eg.stage[0];
+      uint64_t* trig = (uint64_t*)st;
+      int64_t* ts = (int64_t*)(trig + k);
+      int64_t* vals = ts + k;
+      int32_t* key = (int32_t*)(vals + (size_t)k * ns);
+      uint32_t* grp = (uint32_t*)(key + k);
+      uint32_t* vn = grp + k;
+      hipLaunchKernelGGL(k_to_matches, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, h.stream, k, (const char*)o.rec,
+                         o.stride, ns, trig, ts, key, grp, vals, vn);
+      HIPCHK(hipGetLastError());
+      auto cp = [&](void* dst, const void* src, size_t bytes) {
+        if (dst) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h.stream));
+      };
+      cp(out->trigger, trig, 8 * (size_t)k);
+      cp(out->ts, ts, 8 * (size_t)k);
+      cp(out->key, key, 4 * (size_t)k);
+      cp(out->group, grp, 4 * (size_t)k);
+      cp(out->vnull, vn, 4 * (size_t)k);
+      if (ns) cp(out->vals, vals, 8 * (size_t)k * ns);
+      HIPCHK(hipStreamSynchronize(h.stream));
+      o.consume(k, h.stream);
     }
     out->n = k;
     if (n) *n = k;
   });
+}
+
+int sg_poll_columns(sg_handle* hh, const sg_match_columns* out, int64_t cap, int64_t* n) {
+  if (!hh || !out) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  return guard(hh, [&] {
+    HIPCHK(hipSetDevice(h.device));
+    const int64_t k = deliver_pending(h, out, 0, cap, 0);
+    if (h.eg.d2h) HIPCHK(hipStreamSynchronize(h.eg.d2h));
+    if (n) *n = k;
+  });
+}
+
+int sg_push_deliver(sg_handle* hh, const sg_batch* b, const sg_match_columns* out, int64_t cap, int64_t* n) {
+  if (!hh || !b || !out) return SG_EINVAL;
+  SgHandle& h = hh->h;
+  int64_t rows = 0;
+  int rc = guard(hh, [&] {
+    HIPCHK(hipSetDevice(h.device));
+    DeliverHook dh(h, out, cap);
+    try {
+      dh.chunk_done();   // matches pending before this batch come first
+      if (b->n > 0) {
+        check_batch(b);
+        if (b->on_device) {
+          BatchView bv = device_view(h.desc, b);
+          push_view(h, bv, b->n);
+          dh.chunk_done();
+        } else {
+          ingest_host(h, b, &dh);
+        }
+      }
+    } catch (...) {
+      if (h.eg.d2h) hipStreamSynchronize(h.eg.d2h);
+      rows = dh.rows;
+      throw;
+    }
+    if (h.eg.d2h) HIPCHK(hipStreamSynchronize(h.eg.d2h));
+    rows = dh.rows;
+    if (h.out.n) throw SgError(SG_ECAPACITY, "more matches than the output capacity: the rest stay pending");
+  });
+  if (n) *n = rows;
+  return rc;
 }
 
 int sg_discard(sg_handle* hh) {
@@ -539,6 +749,15 @@ int sg_close(sg_handle* hh) {
   h.ws.release();
   h.out.release();
   h.stage.release();
+  if (h.eg.d2h) {
+    hipStreamSynchronize(h.eg.d2h);
+    for (int k = 0; k < 2; ++k) {
+      if (h.eg.stage[k]) hipFree(h.eg.stage[k]);
+      hipEventDestroy(h.eg.ready[k]);
+      hipEventDestroy(h.eg.done[k]);
+    }
+    hipStreamDestroy(h.eg.d2h);
+  }
   if (h.copy_stream) {
     hipStreamSynchronize(h.copy_stream);
     hipStreamDestroy(h.copy_stream);

@@ -100,6 +100,12 @@ struct SgHandle {
   hipEvent_t ev[8] = {};
   hipStream_t copy_stream = nullptr;            // host-batch ingress (sg_push, on_device = 0)
   hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
+  struct Egress {                               // SoA match delivery (sg_poll_columns / sg_push_deliver)
+    hipStream_t d2h = nullptr;
+    char* stage[2] = {};
+    int64_t cap[2] = {};
+    hipEvent_t ready[2] = {}, done[2] = {};
+  } eg;
   int64_t last_events = 0, last_matches = 0, last_spilled = 0;
   int pushes = 0;
   uint64_t gen = 0;           // state generation: bumped by every push / reset / restore

@@ -32,14 +32,17 @@ def test_struct_layout_matches_c(tmp_path):
     src.write_text('#include "siddhi_gpu.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){'
                    'printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(sg_state_desc), sizeof(sg_receiver_desc),'
                     ' sizeof(sg_nfa_desc), sizeof(sg_options), sizeof(sg_batch), sizeof(sg_matches), sizeof(sg_timing),'
-                   ' offsetof(sg_nfa_desc, code), offsetof(sg_nfa_desc, shape), sizeof(sg_match_records));return 0;}')
+                   ' offsetof(sg_nfa_desc, code), offsetof(sg_nfa_desc, shape), sizeof(sg_match_records));'
+                   'printf("%zu %zu %zu\\n", sizeof(sg_match_columns), offsetof(sg_nfa_desc, n_sched),'
+                   ' offsetof(sg_match_columns, nulls));return 0;}')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.dirname(HDR), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [ctypes.sizeof(N.sg_state_desc), ctypes.sizeof(N.sg_receiver_desc), ctypes.sizeof(N.sg_nfa_desc),
             ctypes.sizeof(N.sg_options), ctypes.sizeof(N.sg_batch), ctypes.sizeof(N.sg_matches),
             ctypes.sizeof(N.sg_timing), N.sg_nfa_desc.code.offset, N.sg_nfa_desc.shape.offset,
-            ctypes.sizeof(N.sg_match_records)]
+            ctypes.sizeof(N.sg_match_records), ctypes.sizeof(N.sg_match_columns), N.sg_nfa_desc.n_sched.offset,
+            N.sg_match_columns.nulls.offset]
     assert got == want
 
 
