@@ -1,22 +1,33 @@
 #!/usr/bin/env python3
-"""Benchmark: whole-node events/sec of the partitioned pattern query on MI355X.
+"""Benchmark: events/sec of the partitioned pattern query on MI355X (BASELINE.json metric, configs[1] = C2).
 
-Workload (BASELINE.json configs[1]):
+Workload:
   partition with (symbol of StockStream) begin
     from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec
     select e1.id as id1, e2.id as id2, e1.price as p1, e2.price as p2 insert into M; end;
   100M synthetic events per GPU (SplitMix64 generator, siddhi_amd/synth.py), 10k keys, 1000 events/ms.
-A step = one sg_push of the whole 100M-event batch (inputs already resident in HBM) through the HIP
-pipeline (predicate-eval bitmasks -> key partition -> per-key walker count -> scan -> walker write) on a
-fresh state.
-Multi-GPU (one process per GPU, torchrun): weak scaling, rank r owns the disjoint key range
-[r*K, (r+1)*K) with its own 100M-event stream; no data-path collective (keys never interact).
 
-Prints ONE JSON line (rank 0).  Roofline figures use algorithmic bytes.
+Two rates, both in the one JSON line rank 0 prints:
+  value       (task contract: inputs already resident in HBM when the timed region starts) -- a step is one
+              sg_push of the 100M-event batch through the whole HIP pipeline on a fresh state, ending with every
+              compacted match tuple projected in HBM (sg_device_records: the C-ABI's zero-copy delivery).
+  whole_node  (SURVEY.md §8d's definition, reported beside it): host raw columns -> native host router
+              (dictionary-encodes the raw symbol to first-seen dense ids, sg_router_route) -> sg_push_deliver
+              from pinned memory (chunked H2D, kernels, per-chunk GPU-transposed SoA match columns copied back into
+              pinned host memory, overlapped) -> every match tuple in host memory.  PCIe-bound; never `value`.
+Multi-GPU (one process per GPU, torchrun): weak scaling, rank r owns the disjoint key range [r*K, (r+1)*K) with
+its own stream; no data-path collective (keys never interact); times are max over ranks.
+
+roofline: the dominant kernel of the `value` step (largest HIP-event time, recorded on the launch stream by the
+engine, sg_timing.kernel_ms) against the §8d algorithmic bytes of the whole path (16.125 B/event + 36 B/match),
+plus the predicate pass (4.125 B/event) and the end-to-end path; `traffic` comes from a rocprofv3 PMC summary of
+this same command (profiles/collect_r02.sh) and is only used when its source hash matches the tree.
 """
 import argparse
+import hashlib
 import json
 import os
+import platform
 import subprocess
 import sys
 import time
@@ -33,6 +44,7 @@ from siddhi_amd import lowering as L          # noqa: E402
 from siddhi_amd import synth                  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+DEFAULT_PMC = os.path.join(ROOT, "profiles", "r02", "c2_pmc.json")
 
 
 def dist_env():
@@ -40,6 +52,20 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return ws, rank, local
+
+
+def source_hash():
+    """Hash of everything the measured kernels are built from (a PMC summary is valid only for this tree)."""
+    h = hashlib.sha256()
+    files = []
+    for d, exts in ((os.path.join(ROOT, "siddhi_amd", "csrc"), (".hip", ".h", ".cpp")),
+                    (os.path.join(ROOT, "include"), (".h",))):
+        files += sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(exts))
+    files.append(os.path.join(ROOT, "siddhi_amd", "lowering.py"))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
 
 
 def make_handle(cfg, no_carry=1, ingress_rows=0):
@@ -60,6 +86,22 @@ def _oracle_paths():
     for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
+
+
+def host_info():
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except Exception:
+        nproc = os.cpu_count()
+    return {"nproc": nproc, "cpu_model": model}
 
 
 def cpu_baseline(cfg, n_sample, keys, rate):
@@ -88,8 +130,8 @@ def _mc_worker(w):
 
 
 def cpu_baseline_multicore(cfg, n_sample, keys, rate, workers):
-    """The same oracle on all host cores the box grants this job: rows sharded by partition key across
-    worker processes (keys never interact), each shard keeping its global event indices."""
+    """The same oracle on the host cores the box grants this job: rows sharded by partition key across worker
+    processes (keys never interact), each shard keeping its global event indices."""
     import multiprocessing as mp
     _oracle_paths()
     from parity_util import synth_batch
@@ -109,23 +151,86 @@ def cpu_baseline_multicore(cfg, n_sample, keys, rate, workers):
     return n_sample / dt, sum(r[1] for r in res), dt
 
 
-def path_traffic(profile_json, n, cfg):
-    """HBM-side bytes of one push from the committed PMC summary (profiles/collect.sh + summarize.py):
-    every kernel of the path (torch's synthetic-data kernels excluded), per dispatch."""
+def pmc_traffic(path, cfg, n, dominant):
+    """HBM-side bytes per launch of the dominant kernel and per push of the whole path, from a committed
+    rocprofv3 PMC summary of this command -- only if it was collected on this exact kernel source."""
     try:
-        with open(profile_json) as f:
+        with open(path) as f:
             prof = json.load(f)
     except OSError:
-        return None, None
+        return None, "no PMC summary at %s" % os.path.relpath(path, ROOT)
+    if prof.get("source_hash") != source_hash():
+        return None, "stale PMC summary (source hash %s != tree %s): rerun profiles/collect_r02.sh" % (
+            prof.get("source_hash"), source_hash())
     if prof.get("workload") != cfg or prof.get("events") != n:
-        return None, None
-    tot = 0.0
-    for k, d in prof["kernels"].items():
-        if k.startswith("torch::") or k.startswith("__amd_rocclr"):
-            continue
-        tot += d.get("read_bytes_per_dispatch", 0.0) * d.get("dispatches_per_push", 1)
-        tot += d.get("write_bytes_per_dispatch", 0.0) * d.get("dispatches_per_push", 1)
-    return tot, profile_json
+        return None, "PMC summary is for %s/%s events" % (prof.get("workload"), prof.get("events"))
+    k = prof["kernels"].get(dominant)
+    dom = None if k is None else round(k["bytes_per_push"] / 1e9, 4)
+    path_tot = sum(v["bytes_per_push"] for v in prof["kernels"].values())
+    return {"dominant_GB": dom, "path_GB": round(path_tot / 1e9, 4),
+            "source": os.path.relpath(path, ROOT), "collected_at_head": prof.get("git_head")}, None
+
+
+def synth_columns(cfg, rank, n, keys, rate, dev):
+    g = synth.generate_torch(cfg, rank * n, n, dev, keys=keys, rate=rate)
+    key = g["key"].to(torch.int32) if "key" in g else torch.zeros(n, dtype=torch.int32, device=dev)
+    if cfg.startswith("C4"):     # S(id, seq) rows only (the Tick stream's column is never read)
+        cols = [g["id"], g["seq"], torch.zeros(n, dtype=torch.int32, device=dev)]
+    elif cfg.startswith("C3"):
+        cols = [g["id"], key, g["v"], g["w"]]
+    else:
+        cols = [g["id"], key, g["price"]]
+    return g, key, cols
+
+
+def whole_node(cfg, rank, n, keys, rate, steps, dev, threads):
+    """SURVEY §8d whole-node rate on this rank's stream: raw host columns -> native router -> sg_push_deliver
+    (pinned H2D in chunks, kernels, GPU-transposed SoA match columns D2H into pinned memory, overlapped)."""
+    g, key, cols = synth_columns(cfg, rank, n, keys, rate, dev)
+    keep = []
+
+    def pinned(a, dtype=None):
+        a = np.ascontiguousarray(a if dtype is None else a.astype(dtype))
+        p = N.PinnedArray(len(a), a.dtype)
+        p.array[:] = a
+        keep.append(p)
+        return p.array
+    # host raw columns: the partition attribute arrives as a raw 64-bit symbol value (not a dense id)
+    raw = synth.raw_symbols(key.cpu().numpy())
+    ts_h = pinned(g["ts"].cpu().numpy())
+    col_h = [pinned(c.cpu().numpy()) for c in cols]
+    key_h = pinned(np.zeros(n, np.int32))
+    partitioned = "partition with" in synth.QUERIES[cfg]
+    col_ptrs = [c.ctypes.data for c in col_h]
+    if partitioned:
+        col_ptrs[1] = 0   # the symbol column itself is never read by the query (only its dense key)
+    h, nfa = make_handle(cfg, no_carry=0)
+    batch = N.make_batch(n, rank * n, ts_h.ctypes.data, 0, key_h.ctypes.data, col_ptrs, [0] * len(col_h), 0, 0, keep)
+    # matches bound: every event can complete at most one partial per state
+    sink = N.ColumnSink(nfa, n + 1, pinned=True, fields=("trigger", "ts"), nulls=False)
+    times, rts, delivered = [], [], 0
+    for s in range(steps + 1):
+        h.reset()
+        router = N.Router(1, threads)
+        t0 = time.perf_counter()
+        if partitioned:
+            router.route(raw, key_h)
+            batch.key_bound = keys
+        t1 = time.perf_counter()
+        delivered = h.push_deliver(batch, sink.struct, sink.cap)
+        t2 = time.perf_counter()
+        router.close()
+        if s:   # first step warms the pinned paths and workspaces
+            times.append(t2 - t0)
+            rts.append(t1 - t0)
+    h.close()
+    ms = 1000.0 * float(np.mean(times))
+    bytes_in = n * (8 + (4 if partitioned else 0) + sum(np.dtype(c.dtype).itemsize for c in col_h)
+                    - (col_h[1].dtype.itemsize if partitioned else 0))
+    bytes_out = delivered * (8 + 8 + sum(np.dtype(d).itemsize for d in N.column_dtypes(nfa)))
+    return {"ms_per_step": round(ms, 3), "router_ms": round(1000.0 * float(np.mean(rts)), 3),
+            "matches": int(delivered), "h2d_GB": round(bytes_in / 1e9, 3), "d2h_GB": round(bytes_out / 1e9, 3),
+            "router_threads": threads}
 
 
 def main():
@@ -136,16 +241,12 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--events", type=int, default=0, help="events per GPU per step (default: config size, max 1e8)")
     ap.add_argument("--cpu-sample", type=int, default=0,
-                    help="events for the CPU baseline (default per config: ~5-20 s of oracle work; C4 60k -- the "
-                         "oracle walks ~5k partials per event)")
+                    help="events for the CPU baseline (default per config: ~5-20 s of oracle work)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16, help="processes for the key-sharded CPU baseline")
-    ap.add_argument("--host-input", action="store_true",
-                    help="columns in pinned host memory, pushed through the chunked ingress (PCIe-inclusive rate; "
-                         "never the headline value)")
-    ap.add_argument("--ingress-rows", type=int, default=0, help="ingress chunk rows for --host-input (0 = engine default, -1 = one copy)")
-    ap.add_argument("--profile", default=os.path.join(ROOT, "profiles", "r01", "c2_profile.json"),
-                    help="committed PMC summary the roofline traffic is read from")
+    ap.add_argument("--whole-node-steps", type=int, default=3, help="steps of the §8d whole-node rate (0: skip)")
+    ap.add_argument("--router-threads", type=int, default=16)
+    ap.add_argument("--pmc", default=DEFAULT_PMC, help="rocprofv3 PMC summary of this command (profiles/collect_r02.sh)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -155,41 +256,19 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     cfg = args.config
-    if not args.cpu_sample:   # ~5-20 s of single-thread oracle work per config (measured rates)
+    if not args.cpu_sample:
         args.cpu_sample = {"C1": 1_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000,
                            "C5": 3_000_000}.get(cfg, 12_000_000)
     num, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
     n = args.events or min(n_cfg, 100_000_000)
 
-    # ---- synthetic rows of this rank's key shard, generated in HBM
-    # (each rank's keys are its own dense ids 0..K-1: the router re-densifies per rank, siddhi_amd/router.py)
-    g = synth.generate_torch(cfg, rank * n, n, dev, keys=keys, rate=rate)
-    key = g["key"].to(torch.int32) if "key" in g else torch.zeros(n, dtype=torch.int32, device=dev)
-    if cfg.startswith("C4"):     # S(id, seq) rows only (the Tick stream's column is never read)
-        cols = [g["id"], g["seq"], torch.zeros(n, dtype=torch.int32, device=dev)]
-    elif cfg.startswith("C3"):
-        cols = [g["id"], key, g["v"], g["w"]]
-    else:
-        cols = [g["id"], key, g["price"]]
+    # ---- value: inputs resident in HBM (each rank's keys are its own dense ids 0..K-1, siddhi_amd/router.py)
+    g, key, cols = synth_columns(cfg, rank, n, keys, rate, dev)
     torch.cuda.synchronize()
-
     keep = []
-    if args.host_input:
-        # pinned host columns; chunks are consecutive sub-pushes, so the handle carries state (reset per step)
-        h, nfa = make_handle(cfg, no_carry=0, ingress_rows=args.ingress_rows)
-
-        def pinned(t):
-            a = t.cpu().numpy()
-            p = N.PinnedArray(len(a), a.dtype)
-            p.array[:] = a
-            keep.append(p)
-            return p.array.ctypes.data
-        batch = N.make_batch(n, rank * n, pinned(g["ts"]), 0, pinned(key), [pinned(c) for c in cols],
-                             [0] * len(cols), 0, keys, keep)
-    else:
-        h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
-        batch = N.make_batch(n, rank * n, g["ts"].data_ptr(), 0, key.data_ptr(), [c.data_ptr() for c in cols],
-                             [0] * len(cols), 1, keys, keep)
+    h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
+    batch = N.make_batch(n, rank * n, g["ts"].data_ptr(), 0, key.data_ptr(), [c.data_ptr() for c in cols],
+                         [0] * len(cols), 1, keys, keep)
     stream = torch.cuda.current_stream()
     h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
 
@@ -205,14 +284,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     stage = np.zeros(5)
-    matches = 0
-    spilled = 0
+    kern = {}
+    matches = spilled = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         t = h.timing()
         stage += [t.pred_ms, t.partition_ms, t.match_ms, t.output_ms, t.total_ms]
-        matches = h.pending() if args.host_input else t.matches   # (timing covers the last ingress chunk)
+        for name, ms in t.kernels():
+            kern[name] = kern.get(name, 0.0) + ms
+        matches = t.matches
         spilled = t.spilled_units
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -223,6 +304,28 @@ def main():
         elapsed = float(tt.item())
         dist.barrier()
     stage /= args.steps
+    kern = {k: v / args.steps for k, v in kern.items()}
+    h.close()
+    del g, key, cols
+    torch.cuda.empty_cache()
+
+    # ---- whole_node (§8d): host routing + PCIe both ways, per rank, max over ranks
+    wn = None
+    if args.whole_node_steps > 0:
+        try:
+            wn = whole_node(cfg, rank, n, keys, rate, args.whole_node_steps, dev, args.router_threads)
+        except Exception as e:   # report, never fake
+            wn = {"error": str(e)}
+        if ws > 1 and "ms_per_step" in wn:
+            import torch.distributed as dist
+            tt = torch.tensor([wn["ms_per_step"]], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            wn["ms_per_step"] = round(float(tt.item()), 3)
+        if "ms_per_step" in wn:
+            wn["value"] = round(ws * n / (wn["ms_per_step"] * 1e-3), 1)
+            wn["unit"] = "events/s"
+            wn["definition"] = ("SURVEY.md §8d: raw host columns -> native router (first-seen dense keys) -> pinned "
+                                "chunked H2D -> kernels -> GPU-transposed SoA match columns in pinned host memory")
     if rank != 0:
         return
     ms_step = elapsed * 1000.0 / args.steps
@@ -231,34 +334,40 @@ def main():
     # algorithmic bytes: predicate pass 4.125 B/event (price read + condition bit);
     # whole path 16.125 B/event (ts 8 + key 4 + price 4 + bit) + 36 B/match (C1: no key, 12.125);
     # C4 (no local predicate): ts 8 + id 8 B/event + 28 B/emission
-    pred_bytes = 4.125 * n
     per_ev, per_m = {"C1": (12.125, 36.0), "C4": (16.0, 28.0)}.get(cfg[:2], (16.125, 36.0))
     path_bytes = per_ev * n + per_m * matches
-    stages = {"pred_eval_ms": stage[0], "key_partition_ms": stage[1], "walk_count_scan_ms": stage[2],
-              "walk_write_ms": stage[3], "kernels_total_ms": stage[4]}
-    names = ["pred_eval_ms", "key_partition_ms", "walk_count_scan_ms", "walk_write_ms"]
-    dom = names[int(np.argmax(stage[:4]))]
-    path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9
-    pred_gbs = pred_bytes / (stage[0] * 1e-3) / 1e9 if stage[0] > 0 else 0.0
-    roof = {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(path_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "whole NFA path (all kernels of one push; dominant stage: %s)" % dom,
-            "pred_eval_pass": {"achieved": round(pred_gbs, 1), "frac": round(pred_gbs / HBM_PEAK_GBS, 4),
-                               "bytes_per_event": 4.125},
-            "stages_ms": {k: round(v, 4) for k, v in stages.items()}}
-    if args.host_input:
-        roof["note"] = "stages_ms / achieved cover the last ingress chunk's kernels only"
-    if cfg.startswith("C4"):
-        roof["pred_eval_pass"] = None   # no local predicate: the path starts at the role/value pass
-    traffic, tsrc = path_traffic(args.profile, n, cfg)
-    if traffic is not None:
-        roof["traffic"] = round(traffic / 1e9, 3)
-        roof["traffic_unit"] = "GB per push (L2-side EA requests incl. Infinity-Cache hits; %s)" % os.path.relpath(tsrc, ROOT)
+    dominant = max(kern, key=kern.get) if kern else None
+    t_dom = kern.get(dominant, 0.0)
+    dom_gbs = path_bytes / (t_dom * 1e-3) / 1e9 if t_dom else 0.0
+    path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9 if stage[4] else 0.0
+    roof = {"bound": "hbm", "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": dominant, "kernel_ms": round(t_dom, 4),
+            "algorithmic_GB_per_launch": round(path_bytes / 1e9, 4),
+            "bytes_definition": "SURVEY.md §8d whole-path algorithmic bytes (%.3f B/event + %.0f B/match) over the "
+                                "dominant kernel's HIP-event time" % (per_ev, per_m),
+            "path": {"achieved": round(path_gbs, 1), "frac": round(path_gbs / HBM_PEAK_GBS, 4),
+                     "kernels_total_ms": round(float(stage[4]), 4)},
+            "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])}}
+    if "pred" in kern and not cfg.startswith("C4"):
+        pg = 4.125 * n / (kern["pred"] * 1e-3) / 1e9
+        roof["pred_eval_pass"] = {"achieved": round(pg, 1), "frac": round(pg / HBM_PEAK_GBS, 4),
+                                  "bytes_per_event": 4.125, "ms": round(kern["pred"], 4)}
+    tr, why = pmc_traffic(args.pmc, cfg, n, dominant)
+    if tr is not None:
+        roof["traffic"] = tr["dominant_GB"]
+        roof["traffic_unit"] = "GB per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)"
+        roof["path_traffic_GB"] = tr["path_GB"]
+        roof["traffic_source"] = tr["source"]
+    else:
+        roof["traffic_note"] = why
     cpu = None
     if not args.no_cpu:
+        hi = host_info()
         try:
             r, nm, dt = cpu_baseline(cfg, args.cpu_sample, keys, rate)
             cpu = {"value": round(r, 1), "unit": "events/s", "cores": 1, "kind": "port",
+                   "nproc": hi["nproc"], "cpu_model": hi["cpu_model"],
                    "sample": f"first {args.cpu_sample} events of {cfg} ({keys} keys, {rate}/ms), oracle C++ "
                              f"restatement of the reference state processors, single thread, {nm} matches, {dt:.1f}s"}
             wk = max(1, min(args.cpu_workers, os.cpu_count() or 1))
@@ -268,20 +377,21 @@ def main():
                 cpu["multi_core"] = {"value": round(r2, 1), "cores": wk,
                                      "sample": f"same rows key-sharded over {wk} processes, {nm2} matches, {dt2:.1f}s"}
         except Exception as e:  # report, never fake
-            cpu = {"value": None, "unit": "events/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
+            cpu = {"value": None, "unit": "events/s", "cores": 1, "kind": "port", "sample": f"failed: {e}",
+                   "nproc": hi["nproc"], "cpu_model": hi["cpu_model"]}
     line = {
         "metric": "events/sec (whole node) for partitioned pattern query at 1/2/4/8 GPUs; % HBM peak",
         "value": round(value, 1), "unit": "events/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f32", "data": "synthetic (SplitMix64 generator, SURVEY.md §8d), " +
-        ("in pinned host memory: PCIe-inclusive chunked ingress (not the headline figure)" if args.host_input
-         else "resident in HBM"),
+        "dtype": "f32", "data": "synthetic (SplitMix64 generator, SURVEY.md §8d), inputs resident in HBM; matches "
+                               "projected in HBM (zero-copy sg_device_records)",
         "config": {"workload": f"{cfg}: " + synth.QUERIES[cfg], "events_per_gpu_per_step": n,
                    "keys_per_gpu": keys, "rate_events_per_ms": rate, "matches_per_gpu_per_step": int(matches),
-                   "spilled_units": int(spilled),
-                   "parallelism": f"key-sharded x{ws} (no collective)"},
+                   "spilled_units": int(spilled), "parallelism": f"key-sharded x{ws} (no collective)"},
+        "whole_node": wn,
         "roofline": roof,
         "cpu_baseline": cpu,
+        "source_hash": source_hash(),
     }
     print(json.dumps(line))
 

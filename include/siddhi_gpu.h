@@ -223,10 +223,14 @@ typedef struct sg_match_columns {
   uint8_t* nulls[SG_MAX_SELECT];
 } sg_match_columns;
 
+#define SG_MAX_KMARKS 24
 typedef struct sg_timing {
   float pred_ms, partition_ms, match_ms, output_ms, total_ms;   /* HIP-event times of the last push */
   int64_t events, matches;
   int64_t spilled_units;        /* closed form: (chunk, key) units whose pending list spilled to HBM */
+  int32_t n_kernels;            /* per-kernel HIP-event times of the last push, recorded on the launch stream */
+  float kernel_ms[SG_MAX_KMARKS];
+  char kernel_name[SG_MAX_KMARKS][32];
 } sg_timing;
 
 typedef struct sg_handle sg_handle;

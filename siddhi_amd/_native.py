@@ -83,10 +83,18 @@ class sg_match_records(ct.Structure):
     _fields_ = [("n", I64), ("record_bytes", I32), ("n_select", I32), ("base", ct.c_void_p)]
 
 
+SG_MAX_KMARKS = 24
+
+
 class sg_timing(ct.Structure):
     _fields_ = [("pred_ms", ct.c_float), ("partition_ms", ct.c_float), ("match_ms", ct.c_float),
                 ("output_ms", ct.c_float), ("total_ms", ct.c_float), ("events", I64), ("matches", I64),
-                ("spilled_units", I64)]
+                ("spilled_units", I64), ("n_kernels", I32), ("kernel_ms", ct.c_float * SG_MAX_KMARKS),
+                ("kernel_name", (ct.c_char * 32) * SG_MAX_KMARKS)]
+
+    def kernels(self):
+        """[(name, ms)] of the last push's marked kernels (HIP events on the launch stream)."""
+        return [(self.kernel_name[k].value.decode(), self.kernel_ms[k]) for k in range(self.n_kernels)]
 
 
 _lib = None

@@ -443,6 +443,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   uint8_t* dead = (uint8_t*)h->ws.get("abs_dead", nt, st);
   hipLaunchKernelGGL(k_abs_init, dim3(1), dim3(64), 0, st, (unsigned long long*)as->dminmax, as->dflag);
   HIPCHK(hipMemsetAsync(dead, 0, nt, st));
+  h->kbeg("abs_roles");
   if (nt > 0 && a.fast && a.type == SG_T_LONG)
     hipLaunchKernelGGL((k_abs_rows_fast<int64_t>), dim3(grid_red(nt)), dim3(256), 0, st, a,
                        (const int64_t*)bv.cols.col[a.col_a], bv.ts, cin.val, cin.vnul, role, vals,
@@ -455,6 +456,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
     hipLaunchKernelGGL(k_abs_rows, dim3(grid_red(nt)), dim3(256), 0, st, a, bv.cols, h->ddesc, bv.ts, bv.stream,
                        cin.val, cin.vnul, role, vals, (unsigned long long*)as->dminmax, as->dlast, as->dflag);
   HIPCHK(hipGetLastError());
+  h->kend();
   h->mark(1);
   uint64_t mm[2] = {0, 0};
   uint32_t oflag = 0;
@@ -463,6 +465,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(hipStreamSynchronize(st));
   if (oflag) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps");
   // ---- 2-4. sort by value, kill
+  h->kbeg("abs_sort_kill");
   if (mm[0] <= mm[1] && nt > 0) {
     const uint64_t range = mm[1] - mm[0];   // sentinel = range + 1 must fit in the key bits
     int bits = 1;
@@ -473,11 +476,13 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
     else
       sort_and_kill<uint64_t>(h, a, mm[0], bits, role, vals, bv.ts, cin.dl, dead);
   }
+  h->kend();
   h->mark(2);
   // ---- decide, scan
   uint32_t* trig = (uint32_t*)h->ws.get("abs_trig", 4 * nt, st);
   uint64_t* cnt = (uint64_t*)h->ws.get("abs_cnt", 8 * (nt + 1), st);
   uint64_t* off = (uint64_t*)h->ws.get("abs_off", 8 * (nt + 1), st);
+  h->kbeg("abs_decide_scan");
   if (nt > 0)
     hipLaunchKernelGGL(k_abs_decide, dim3(grid_for(nt)), dim3(256), 0, st, a, role, dead, bv.ts, cin.dl, trig, cnt);
   HIPCHK(hipMemsetAsync(cnt + nt, 0, 8, st));
@@ -485,6 +490,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint64_t)0, (size_t)nt + 1, rocprim::plus<uint64_t>(), st));
   void* tmp = h->ws.get("abs_oscan_tmp", tb, st);
   HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint64_t)0, (size_t)nt + 1, rocprim::plus<uint64_t>(), st));
+  h->kend();
   uint64_t tot = 0;
   HIPCHK(hipMemcpyAsync(&tot, off + nt, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -508,6 +514,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   if (!h->opt.no_carry) cout.reserve(n_carry, d.n_select);
   uint32_t* slot_trig = (uint32_t*)h->ws.get("abs_slot_trig", 4 * (n_emit + 1), st);
   uint32_t* first_slot = (uint32_t*)h->ws.get("abs_first_slot", 4 * (n_emit + 1), st);
+  h->kbeg("abs_write");
   if (n_emit > 0) {
     hipLaunchKernelGGL(k_abs_slot_trig, dim3(grid_for(nt)), dim3(256), 0, st, nt, cnt, off, trig, slot_trig);
     uint32_t* head = (uint32_t*)h->ws.get("abs_head", 4 * (n_emit + 1), st);
@@ -522,6 +529,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
                        role, cin, cout, first_slot, dst);
   if (n > 0) hipLaunchKernelGGL(k_abs_last, dim3(1), dim3(64), 0, st, n, bv.ts, as->dlast);
   HIPCHK(hipGetLastError());
+  h->kend();
   h->mark(4);
   h->out.n += n_emit;
   if (!h->opt.no_carry) {

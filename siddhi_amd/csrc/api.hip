@@ -171,6 +171,7 @@ static void push_view(SgHandle& h, BatchView& bv, int64_t n) {
   int shape = h.opt.force_general ? SG_SHAPE_GENERAL : d.shape;
   const bool sel = d.n_out > 0;
   h.bump_gen();   // the state changes from here on (a failed push leaves no valid snapshot cache either)
+  h.n_km = 0;
   if (sel) std::swap(h.out, h.stage);   // engines append base records to the stage
   try {
     switch (shape) {
@@ -735,6 +736,13 @@ int sg_get_timing(sg_handle* hh, sg_timing* t) {
     t->events = h.last_events;
     t->matches = h.last_matches;
     t->spilled_units = h.last_spilled;
+    t->n_kernels = h.n_km;
+    for (int k = 0; k < h.n_km; ++k) {
+      float x = 0;
+      HIPCHK(hipEventElapsedTime(&x, h.km[k][0], h.km[k][1]));
+      t->kernel_ms[k] = x;
+      snprintf(t->kernel_name[k], sizeof t->kernel_name[k], "%s", h.km_name[k] ? h.km_name[k] : "?");
+    }
   });
 }
 
@@ -765,6 +773,7 @@ int sg_close(sg_handle* hh) {
   }
   if (h.ddesc) hipFree(h.ddesc);
   for (auto& e : h.ev) if (e) hipEventDestroy(e);
+  for (auto& pr : h.km) for (auto& e : pr) if (e) hipEventDestroy(e);
   if (h.own_stream && h.stream) hipStreamDestroy(h.stream);
   delete hh;
   return SG_OK;

@@ -1341,6 +1341,7 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
 #define SG_NGE_LAUNCH(OPV)                                                                                       \
   hipLaunchKernelGGL((k_nge_blocks<T, OPV>), grid(nb), dim3(256), 0, st, v, nt, best, has);                     \
   hipLaunchKernelGGL((k_nge<T, OPV>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf, best, has)
+  h->kbeg("nge_search");
   switch (op) {
     case 2: SG_NGE_LAUNCH(2); break;
     case 3: SG_NGE_LAUNCH(3); break;
@@ -1349,6 +1350,7 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   }
 #undef SG_NGE_LAUNCH
   HIPCHK(hipGetLastError());
+  h->kend();
   h->mark(2);
   size_t tb = 0;
   HIPCHK(rocprim::exclusive_scan(nullptr, tb, mflag, mpos, (uint32_t)0, (size_t)nt + 1, rocprim::plus<uint32_t>(), st));
@@ -1403,8 +1405,10 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   wa.out_base = h->out.n;
   h->mark(5);
   if (total) {
+    h->kbeg("project");
     hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)), dim3(256), (size_t)256 * wa.stride, st,
                        wa, v, plan.pp, bv.cols, cc, mrec, off, (int64_t)total, out);
+    h->kend();
     HIPCHK(hipGetLastError());
   }
   h->out.n += total;
@@ -1495,6 +1499,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   uint64_t* cand_m = (uint64_t*)h->ws.get("cand_m", sizeof(uint64_t) * 4 * (ntiles + 1), st);
   uint64_t* cons_m = pa.cons_all ? nullptr : (uint64_t*)h->ws.get("cons_m", sizeof(uint64_t) * 4 * (ntiles + 1), st);
   h->mark(0);
+  h->kbeg("pred");
   {
     PredArgs sp = pa;
     bool simple = pa.cons_all && !bv.stream && pa.s_a == 0 && simple_prog(d, pa.prog_a_off, pa.prog_a_len, sp) &&
@@ -1533,6 +1538,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     }
     HIPCHK(hipGetLastError());
   }
+  h->kend();
   h->mark(1);
 
   // ---- 2. key partition: per-key walker records in arrival order
@@ -1584,8 +1590,11 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     R* srec = (R*)h->ws.get("srec", sizeof(R) * nt, st);
     uint32_t* pkeys = (uint32_t*)h->ws.get("pkeys", sizeof(uint32_t) * nt, st);
     KeyOf kf{bv.key, cs.key, (uint32_t)nc};
+    h->kbeg("pack");
     hipLaunchKernelGGL((k_pack<T, N>), pgrd, dim3(256), 0, st, src.pk, kf, kb, nt, prec, pkeys, pk_flags);
     HIPCHK(hipGetLastError());
+    h->kend();
+    h->kbeg("key_sort");
     size_t tb = 0;
     if constexpr (sizeof(R) == 16) {   // one onesweep instantiation for every 16-byte record format
       Blob16* pb = (Blob16*)prec;
@@ -1598,11 +1607,14 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       void* tmp = h->ws.get("sort_tmp", tb, st);
       HIPCHK(rocprim::radix_sort_pairs(tmp, tb, pkeys, skeys, prec, srec, (size_t)nt, 0, end_bit, st));
     }
+    h->kend();
     src.srec = srec;
     HIPCHK(hipMemsetAsync(seg_b, 0, sizeof(uint32_t) * K, st));
     HIPCHK(hipMemsetAsync(seg_e, 0, sizeof(uint32_t) * K, st));
+    h->kbeg("bounds");
     hipLaunchKernelGGL(k_bounds, dim3((unsigned)std::min<int64_t>((nt + 1023) / 1024, 256 * 16)), dim3(256), 0, st, skeys,
                        nt, kb, seg_b, seg_e);
+    h->kend();
     HIPCHK(hipGetLastError());
   } else {
     // unpartitioned: one key whose rows are already in arrival order
@@ -1684,6 +1696,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     wlen = (uint32_t*)h->ws.get("wlen", sizeof(uint32_t) * (nw + 1), st);
     wrow = (uint32_t*)h->ws.get("wrow", sizeof(uint32_t) * (nw + 1), st);
     HIPCHK(hipMemsetAsync(wlen, 0, sizeof(uint32_t) * (nw + 1), st));
+    h->kbeg("units");
     hipLaunchKernelGGL((k_units<T, N>), dim3((unsigned)(nw * 64 + 255) / 256), dim3(256), 0, st, wa, src, seg_b, seg_e,
                        ud, wlen, wst);
     HIPCHK(hipGetLastError());
@@ -1691,6 +1704,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(rocprim::exclusive_scan(nullptr, tb, wlen, wrow, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
     void* tmp = h->ws.get("wscan_tmp", tb, st);
     HIPCHK(rocprim::exclusive_scan(tmp, tb, wlen, wrow, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
+    h->kend();
     uint32_t rows_total = 0, pkf = 0;
     HIPCHK(hipMemcpyAsync(&rows_total, wrow + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -1715,12 +1729,16 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       uint32_t* rmap = (uint32_t*)h->ws.get("rowmap", sizeof(uint32_t) * nq, st);
       hipLaunchKernelGGL(k_rowmap, dim3((nw + 255) / 256), dim3(256), 0, st, wlen, wrow, nw, rmap);
       HIPCHK(hipGetLastError());
+      h->kbeg("tile_transpose");
       hipLaunchKernelGGL((k_transpose<T, N>), dim3(std::min<uint32_t>(nq, 256 * 32)), dim3(256), 0, st, src.srec, ud, wrow,
                          rmap, nq, tile);
       HIPCHK(hipGetLastError());
+      h->kend();
     }
+    h->kbeg("walk_count");
     launch_walk_t<T, N, false>(op, wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, (MRec*)nullptr,
                             emask, wst, carry_q0, carry_n);
+    h->kend();
   }
   auto scan_counts = [&]() {
     size_t tb = 0;
@@ -1728,7 +1746,9 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     void* tmp = h->ws.get("scan_tmp", tb, st);
     HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
   };
+  h->kbeg("count_scan");
   scan_counts();
+  h->kend();
   h->mark(3);
   WalkStats hs;
   uint32_t total = 0;
@@ -1763,17 +1783,21 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     wa.out_base = h->out.n;
     MRec* mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
+    h->kbeg("walk_record");
     launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, mrec,
                               emask, wst, carry_q0, carry_n);
+    h->kend();
     if (hs.n_ovf) {
       hipLaunchKernelGGL((k_walk<T, N, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec,
                          emap, wst, big, carry_q0, carry_n);
       HIPCHK(hipGetLastError());
     }
     if (total) {
+      h->kbeg("project");
       hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)),
                          dim3(256), (size_t)256 * wa.stride, st, wa, v, pp, bv.cols, cc, mrec, off, (int64_t)total, out);
       HIPCHK(hipGetLastError());
+      h->kend();
     }
     h->out.n += total;
   }

@@ -364,10 +364,13 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   int32_t* order_err = (int32_t*)h->ws.get("order_err", sizeof(int32_t), st);
   HIPCHK(hipMemsetAsync(order_err, 0, sizeof(int32_t), st));
   h->mark(0);
+  h->kbeg("route");
   hipLaunchKernelGGL(k_route, grd, blk, 0, st, n, bv.stream, bv.key, bv.ts, h->ddesc, d.partitioned, sentinel,
                      has_absent ? 1 : 0, keys, rows, order_err);
   HIPCHK(hipGetLastError());
+  h->kend();
   h->mark(1);
+  h->kbeg("key_sort");
   {
     size_t tb = 0;
     HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, rows, srows, (size_t)n, 0, end_bit, st));
@@ -380,6 +383,7 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(hipMemsetAsync(end, 0, sizeof(uint32_t) * kb, st));
   hipLaunchKernelGGL(k_segments, grd, blk, 0, st, n, skeys, sentinel, beg, end);
   HIPCHK(hipGetLastError());
+  h->kend();
   h->mark(2);
   // ---- per-key machines
   int32_t stride = sg_emit_stride(d.n_select);
@@ -467,14 +471,18 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
     HIPCHK(hipMemcpyAsync(snap, gs->arena, sizeof(int32_t) * kw * kb, hipMemcpyDeviceToDevice, st));
     ua.snap = snap;
     hipLaunchKernelGGL(k_unit_map, dim3((unsigned)((kb + 255) / 256)), blk, 0, st, (int64_t)kb, uoff, umap);
+    h->kbeg("nfa_units");
     if (U)
       hipLaunchKernelGGL(k_nfa_units, dim3((unsigned)((U + 63) / 64)), dim3(64), 0, st, na, ua, bv.cols, h->ddesc,
                          gs->dgeo, gs->arena, sink, gs->dfail);
+    h->kend();
     hipLaunchKernelGGL(k_unit_keep, dim3((unsigned)std::min<uint32_t>(std::max<uint32_t>(kb, 1), 65535)), blk, 0, st,
                        (int64_t)kb, uoff, ua.scratch, gs->dgeo, gs->arena);
   } else {
+    h->kbeg("nfa_keys");
     hipLaunchKernelGGL(k_nfa, dim3((unsigned)((kb + 63) / 64)), dim3(64), 0, st, na, bv.cols, h->ddesc, gs->dgeo,
                        gs->arena, sink, gs->dfail);
+    h->kend();
   }
   HIPCHK(hipGetLastError());
   h->mark(3);
@@ -495,6 +503,7 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
     uint32_t* ix = (uint32_t*)h->ws.get("g_ix", 4 * total, st);
     uint32_t* ix2 = (uint32_t*)h->ws.get("g_ix2", 4 * total, st);
     dim3 g2((unsigned)((total + 255) / 256));
+    h->kbeg("match_order");
     hipLaunchKernelGGL(k_sortkeys, g2, blk, 0, st, (int64_t)total, ebuf, stride, sk, ix);
     HIPCHK(hipGetLastError());
     int sbits = 31 + 1 + kbits;
@@ -508,6 +517,7 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
     hipLaunchKernelGGL(k_gather, g2, blk, 0, st, (int64_t)total, ebuf, stride, ix2, out + (size_t)h->out.n * ostride,
                        ostride);
     HIPCHK(hipGetLastError());
+    h->kend();
     h->out.n += (int64_t)total;
   }
   h->mark(4);

@@ -117,6 +117,21 @@ struct SgHandle {
   int split_out = 0;          // 1: output stage timed from ev[5] (host work between ev[3] and ev[5])
   int extra_marks = 0;        // 1: ev[6]..ev[7] hold an extra match-stage interval (overflow re-pass)
   void mark(int k) { hipEventRecord(ev[k], stream); }
+  // per-kernel HIP events on the launch stream (sg_timing.kernel_ms): kbeg/kend bracket one kernel or group
+  hipEvent_t km[SG_MAX_KMARKS][2] = {};
+  const char* km_name[SG_MAX_KMARKS] = {};
+  int n_km = 0;
+  void kbeg(const char* name) {
+    if (n_km >= SG_MAX_KMARKS) return;
+    if (!km[n_km][0]) { hipEventCreate(&km[n_km][0]); hipEventCreate(&km[n_km][1]); }
+    km_name[n_km] = name;
+    hipEventRecord(km[n_km][0], stream);
+  }
+  void kend() {
+    if (n_km >= SG_MAX_KMARKS) return;
+    hipEventRecord(km[n_km][1], stream);
+    ++n_km;
+  }
   void bump_gen() {   // any state change invalidates the serialised-state cache of sg_snapshot
     ++gen;
     if (!snap_cache.empty()) { std::vector<char>().swap(snap_cache); snap_gen = ~0ull; }

@@ -141,3 +141,9 @@ def generate_torch(cfg: str, start: int, count: int, device, keys: int = None, r
     else:
         out["price"] = umod(x(1), 4001).to(torch.float32) / 100.0
     return out
+
+
+def raw_symbols(key: np.ndarray) -> np.ndarray:
+    """The partition attribute as a host sees it before dictionary encoding: one 64-bit value per symbol
+    ("S%07d" % key hashed), for the native router (sg_router_route) to map to first-seen dense ids."""
+    return splitmix64_np(key.astype(np.uint64) ^ np.uint64(0x5359_4D42_4F4C_0000)).view(np.int64)
