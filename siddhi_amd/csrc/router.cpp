@@ -8,9 +8,9 @@
 // so each GPU's key space stays dense.
 //
 // One call routes a batch with T threads in two parallel passes and one serial merge:
-//   1. each thread scans its contiguous slice and collects, in order, the keys the global dictionary lacks;
-//   2. the slices' new keys are appended to the dictionary slice by slice (so the ids follow first arrival);
-//   3. each thread maps its slice through the (now read-only) dictionary.
+//   1. each thread numbers the keys of its contiguous slice in first-arrival order (one hash lookup per row);
+//   2. the slices' keys are merged into the dictionary slice by slice (so new ids follow first arrival);
+//   3. each thread maps its slice-local ids to dictionary ids (array lookups).
 #include <stdint.h>
 #include <string.h>
 
@@ -34,49 +34,58 @@ inline uint64_t mix64(uint64_t x) {   // splitmix64 step (same as siddhi_amd/rou
   return x;
 }
 
-// open-addressing map int64 raw key -> int32 value (linear probing, power-of-two capacity)
+// open-addressing map int64 raw key -> int32 value (linear probing, power-of-two capacity, key and value in one
+// 16-byte slot so a probe touches one cache line)
 struct KeyMap {
-  std::vector<int64_t> keys;
-  std::vector<int32_t> vals;   // -1 = empty
+  struct Slot {
+    int64_t key;
+    int32_t val;   // -1 = empty
+    int32_t pad;
+  };
+  std::vector<Slot> slots;
   size_t mask = 0, size = 0;
+  int shift = 64;
   void init(size_t cap_pow2) {
-    keys.assign(cap_pow2, 0);
-    vals.assign(cap_pow2, -1);
+    slots.assign(cap_pow2, Slot{0, -1, 0});
     mask = cap_pow2 - 1;
     size = 0;
+    shift = 64;
+    for (size_t c = cap_pow2; c > 1; c >>= 1) --shift;
   }
+  // Fibonacci hashing: one multiply, the top bits index the table
+  size_t home(int64_t k) const { return (size_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> shift) & mask; }
+  void prefetch(int64_t k) const { __builtin_prefetch(&slots[home(k)]); }
   int32_t find(int64_t k) const {
-    size_t i = (size_t)mix64((uint64_t)k) & mask;
+    size_t i = home(k);
     while (true) {
-      const int32_t v = vals[i];
-      if (v < 0) return -1;
-      if (keys[i] == k) return v;
+      const Slot& s = slots[i];
+      if (s.val < 0) return -1;
+      if (s.key == k) return s.val;
       i = (i + 1) & mask;
     }
   }
   // returns the existing value, or inserts v and returns -1
   int32_t insert(int64_t k, int32_t v) {
-    if ((size + 1) * 2 > keys.size()) grow();
-    size_t i = (size_t)mix64((uint64_t)k) & mask;
+    if ((size + 1) * 2 > slots.size()) grow();
+    size_t i = home(k);
     while (true) {
-      if (vals[i] < 0) {
-        keys[i] = k;
-        vals[i] = v;
+      Slot& s = slots[i];
+      if (s.val < 0) {
+        s.key = k;
+        s.val = v;
         ++size;
         return -1;
       }
-      if (keys[i] == k) return vals[i];
+      if (s.key == k) return s.val;
       i = (i + 1) & mask;
     }
   }
   void grow() {
-    std::vector<int64_t> ok;
-    std::vector<int32_t> ov;
-    ok.swap(keys);
-    ov.swap(vals);
-    init(std::max<size_t>(ok.size() * 2, 1024));
-    for (size_t i = 0; i < ok.size(); ++i)
-      if (ov[i] >= 0) insert(ok[i], ov[i]);
+    std::vector<Slot> old;
+    old.swap(slots);
+    init(std::max<size_t>(old.size() * 2, 1024));
+    for (const Slot& s : old)
+      if (s.val >= 0) insert(s.key, s.val);
   }
 };
 
@@ -107,23 +116,38 @@ int sg_router_open(int n_shards, int threads, sg_router** out) {
 int sg_router_route(sg_router* r, int64_t n, const int64_t* raw, int32_t* dense, int32_t* shard, int32_t* local) {
   if (!r || n < 0 || (n && !raw)) return SG_EINVAL;
   if (n == 0) return SG_OK;
+  std::vector<int32_t> tmp;
+  if (!dense) {
+    tmp.resize((size_t)n);
+    dense = tmp.data();
+  }
   const int T = (int)std::max<int64_t>(1, std::min<int64_t>(r->threads, n / 65536 + 1));
-  std::vector<std::vector<int64_t>> fresh(T);
+  std::vector<std::vector<int64_t>> keys_of(T);   // per slice: its distinct keys in first-arrival order
+  std::vector<std::vector<int32_t>> remap(T);     // per slice: slice-local id -> dictionary id
   auto slice = [&](int t, int64_t& lo, int64_t& hi) {
     lo = n * t / T;
     hi = n * (t + 1) / T;
   };
-  // 1. new keys per slice, in first-arrival order (a thread-local set filters repeats inside the slice)
+  // 1. every slice numbers its own keys in first-arrival order (one hash lookup per row; slots of the next 16
+  //    rows are prefetched) and writes those slice-local ids
   auto pass1 = [&](int t) {
     int64_t lo, hi;
     slice(t, lo, hi);
-    KeyMap seen;
-    seen.init(1 << 10);
-    std::vector<int64_t>& f = fresh[t];
+    KeyMap m;
+    m.init(1 << 12);
+    std::vector<int64_t>& ks = keys_of[t];
+    constexpr int G = 16;
     for (int64_t i = lo; i < hi; ++i) {
+      if (i + G < hi) m.prefetch(raw[i + G]);
       const int64_t k = raw[i];
-      if (r->dict.find(k) >= 0) continue;
-      if (seen.insert(k, 0) < 0) f.push_back(k);
+      const int32_t nid = (int32_t)ks.size();
+      const int32_t id = m.insert(k, nid);
+      if (id < 0) {
+        ks.push_back(k);
+        dense[i] = nid;
+      } else {
+        dense[i] = id;
+      }
     }
   };
   std::vector<std::thread> pool;
@@ -131,24 +155,36 @@ int sg_router_route(sg_router* r, int64_t n, const int64_t* raw, int32_t* dense,
   pass1(0);
   for (auto& th : pool) th.join();
   pool.clear();
-  // 2. serial merge: dictionary ids in first-seen order, shard by mix64(id), dense id inside the shard
-  for (int t = 0; t < T; ++t)
-    for (int64_t k : fresh[t]) {
+  // 2. serial merge, slice by slice: dictionary ids in first-seen order (new keys get the next id, shard
+  //    mix64(id) mod n_shards and the next dense id of that shard)
+  for (int t = 0; t < T; ++t) {
+    remap[t].resize(keys_of[t].size());
+    for (size_t j = 0; j < keys_of[t].size(); ++j) {
+      const int64_t k = keys_of[t][j];
       const int32_t id = (int32_t)r->shard_of.size();
-      if (r->dict.insert(k, id) >= 0) continue;   // first seen by an earlier slice
+      const int32_t old = r->dict.insert(k, id);
+      if (old >= 0) {
+        remap[t][j] = old;
+        continue;
+      }
+      remap[t][j] = id;
       const int32_t s = (int32_t)(mix64((uint64_t)id) % (uint64_t)r->n_shards);
       r->shard_of.push_back(s);
       r->local_of.push_back(r->shard_keys[s]++);
     }
-  // 3. map every row
+  }
+  // 3. slice-local ids -> dictionary ids (and shard / per-shard ids): array lookups only
   auto pass3 = [&](int t) {
     int64_t lo, hi;
     slice(t, lo, hi);
+    const int32_t* rm = remap[t].data();
+    const int32_t* so = r->shard_of.data();
+    const int32_t* lc = r->local_of.data();
     for (int64_t i = lo; i < hi; ++i) {
-      const int32_t id = r->dict.find(raw[i]);
-      if (dense) dense[i] = id;
-      if (shard) shard[i] = r->shard_of[id];
-      if (local) local[i] = r->local_of[id];
+      const int32_t id = rm[dense[i]];
+      dense[i] = id;
+      if (shard) shard[i] = so[id];
+      if (local) local[i] = lc[id];
     }
   };
   for (int t = 1; t < T; ++t) pool.emplace_back(pass3, t);
