@@ -168,7 +168,9 @@ typedef struct sg_options {
                                the copy of chunk k+1 overlapping the kernels of chunk k (0: 4 chunks for batches of
                                >= 32M rows, else one copy; -1: one copy); results are identical to one push.
                                no_carry handles never split. */
-  int32_t reserved[2];
+  int32_t partition_sort;   /* closed form, partitioned: 0 = LDS-staged counting partition when key_bound <= 65536
+                               (rocPRIM radix sort above), 1 = always the radix sort (testing both paths) */
+  int32_t reserved[1];
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)

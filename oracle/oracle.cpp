@@ -85,7 +85,16 @@ struct StreamEvent {
   Ref<StreamEvent> next;
   static void destroy(StreamEvent* e);
 };
-static std::vector<StreamEvent*> g_se_free;
+// pool of released StreamEvents (reused by new_se); the pool owns them and frees them at exit
+struct SePool {
+  std::vector<StreamEvent*> v;
+  ~SePool();
+  bool empty() const { return v.empty(); }
+  StreamEvent* back() const { return v.back(); }
+  void pop_back() { v.pop_back(); }
+  void push_back(StreamEvent* e) { v.push_back(e); }
+};
+static SePool g_se_free;
 void StreamEvent::destroy(StreamEvent* e) {
   // iterative chain release to avoid deep recursion on long chains
   while (e) {
@@ -95,6 +104,9 @@ void StreamEvent::destroy(StreamEvent* e) {
     g_se_free.push_back(e);
     if (nx && --nx->rc == 0) e = nx; else e = nullptr;
   }
+}
+SePool::~SePool() {
+  for (StreamEvent* e : v) delete e;
 }
 static StreamEvent* new_se(const Ref<EventData>& d) {
   StreamEvent* e;

@@ -308,6 +308,37 @@ struct PackFn {   // builds the walker record of virtual row r (coalesced when r
 #endif
     return o;
   }
+  // batch row b (virtual row nc + b) without the carried-row branches, so a run of rows issues its loads
+  // back to back; also flags a time / payload outside the narrow format's 32 bits
+  __device__ __forceinline__ WRec<T, N> batch(uint32_t b, int64_t t0, uint32_t& bad) const {
+    WRec<T, N> o;
+    uint32_t f = mask_bit(v.cand_m, b);
+    f |= v.cons_m ? (mask_bit(v.cons_m, b) << 1) : F_CONS;
+    const int64_t ts = v.ts[b];
+    if constexpr (N) {
+      const int64_t dt = ts - t0;
+      bad |= (dt != (int64_t)(int32_t)dt) ? PK_TS_RANGE : 0u;
+      o.dts = (int32_t)dt;
+      if constexpr (WRec<T, N>::has_pay) {
+        int64_t pv = 0;
+        if (v.pcol) {   // (uniform)
+          if (v.pw == 8) {
+            pv = ((const int64_t*)v.pcol)[b];
+            bad |= (pv != (int64_t)(int32_t)pv) ? PK_PAY_RANGE : 0u;
+          } else {
+            pv = ((const int32_t*)v.pcol)[b];
+          }
+        }
+        o.pay = (int32_t)pv;
+      }
+    } else {
+      o.ts = ts;
+    }
+    o.rowf = (uint32_t)(v.nc + b) | (f << 30);
+    const T* src = ((f & F_CAND) || v.val_a == v.val_b) ? (const T*)v.val_a : (const T*)v.val_b;
+    o.val = src[b];
+    return o;
+  }
 };
 
 template <class T, bool N>
@@ -387,6 +418,299 @@ static __global__ void __launch_bounds__(256) k_bounds(const uint32_t* __restric
 }
 
 // ---------------------------------------------------------------------------------------------
+// 2'. Key partition without a general sort (K <= 65536).  A stable MSD counting sort in one pass (K <= 256:
+// digit = key) or two (digit = key group = high bits, then key within its group = low bits).  Each pass
+// cuts its input into segments; a histogram kernel counts digits per segment, one exclusive scan over the
+// (digit, segment) table gives every segment's output position per digit, and the scatter kernel ranks each
+// 4096-row sub-tile stably by digit in LDS (wave ballots over the digit bits) and writes every digit run out
+// as whole lines.  Pass 1 reads the raw columns and builds the walker records on the way (no pack pass);
+// pass 2 reads pass 1's records and 1-byte in-group keys.  The per-key segments are read off the last
+// pass's offsets (no bounds pass).  Same result as the radix sort: per key its rows in arrival order.
+static const int PT_ROWS = 4096;   // rows per LDS-staged sub-tile (16 per thread)
+static const int PT_D = 256;       // digit values per pass (8 bits)
+
+struct PartPlan {
+  uint32_t K, lb, ng, two;    // keys; pass-2 digit bits (key & (2^lb - 1)); pass-1 digit values (key >> lb); 2 passes?
+  uint32_t nb1, nb2;          // bits that tell the digits apart (ballots per 64-row step)
+  uint32_t seg1, ns1;         // rows per pass-1 segment (multiple of PT_ROWS); pass-1 segments
+  uint32_t ts2, nj;           // pass-1 segments per pass-2 segment; pass-2 segments per group
+};
+
+template <class R>
+struct PartLds {
+  R stage[PT_ROWS];           // the sub-tile's records, sorted by digit
+  uint16_t tag[PT_ROWS];      // key (pass 1) / in-group key (pass 2) of each staged record
+  uint32_t cw[4][PT_D];       // per-wave digit counts, then per-wave slot cursors
+  uint32_t ls[PT_D];          // sub-tile start of each digit
+  uint32_t tot[PT_D];         // sub-tile count of each digit
+  uint32_t run[PT_D];         // next output position of each digit
+  uint32_t wsum[4];
+};
+
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t add = 0;
+  for (int i = 0; i < w; ++i) add += wsum[i];
+  return add + inc - x;
+}
+
+// lanes of the wave holding the same digit: rank among them (arrival order) and their count
+__device__ __forceinline__ void peer_rank(bool valid, uint32_t d, uint32_t nb, uint32_t& rank, uint32_t& cnt) {
+  uint64_t m = __ballot(valid);
+  for (uint32_t b = 0; b < nb; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = __ballot(bit);
+    m &= bit ? bb : ~bb;
+  }
+  rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  cnt = (uint32_t)__popcll(m);
+}
+
+// digit counts -> per-wave slot cursors and sub-tile digit starts; returns the sub-tile's staged rows
+template <class R>
+__device__ __forceinline__ uint32_t part_cursors(PartLds<R>& L) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t c0 = L.cw[0][t], c1 = L.cw[1][t], c2 = L.cw[2][t], c3 = L.cw[3][t];
+  const uint32_t tot = c0 + c1 + c2 + c3;
+  const uint32_t ex = block_excl_scan256(tot, L.wsum);
+  L.ls[t] = ex;
+  L.tot[t] = tot;
+  L.cw[0][t] = ex;
+  L.cw[1][t] = ex + c0;
+  L.cw[2][t] = ex + c0 + c1;
+  L.cw[3][t] = ex + c0 + c1 + c2;
+  __syncthreads();
+  return L.ls[PT_D - 1] + L.tot[PT_D - 1];
+}
+
+// pass-1 histogram: segment j = virtual rows [j*seg1, (j+1)*seg1); h1[group * ns1 + j]
+static __global__ void __launch_bounds__(256) k_part1_hist(KeyOf kf, PartPlan pp, int64_t nt, uint32_t* __restrict__ h1,
+                                                           uint32_t* __restrict__ flags) {
+  __shared__ uint32_t cnt[PT_D];
+  const uint32_t j = blockIdx.x;
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)j * pp.seg1, r1 = (nt < r0 + pp.seg1) ? nt : r0 + pp.seg1;
+  uint32_t bad = 0;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+    const uint32_t k = kf((uint32_t)r);
+    if (k < pp.K) atomicAdd(&cnt[k >> pp.lb], 1u);
+    else if (k != 0xffffffffu) bad |= PK_KEY_RANGE;   // beyond the caller's key_bound
+  }
+  __syncthreads();
+  if (threadIdx.x < pp.ng) h1[(size_t)threadIdx.x * pp.ns1 + j] = cnt[threadIdx.x];
+  if (bad) atomicOr(flags, bad);
+}
+
+// pass-1 scatter: records of segment j, grouped (two passes) or final (one pass)
+template <class T, bool N>
+__global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPlan pp, int64_t nt,
+                                               const uint32_t* __restrict__ o1, WRec<T, N>* __restrict__ orec,
+                                               uint8_t* __restrict__ olk, uint32_t* __restrict__ flags) {
+  typedef WRec<T, N> R;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  PartLds<R>& L = *(PartLds<R>*)lds_raw;
+  const uint32_t j = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t lmask = (1u << pp.lb) - 1u;
+  if (t < pp.ng) L.run[t] = o1[(size_t)t * pp.ns1 + j];
+  const int64_t rb = (int64_t)j * pp.seg1, re = (nt < rb + pp.seg1) ? nt : rb + pp.seg1;
+  const int64_t t0 = N ? v_ts(pk.v, 0) : 0;
+  uint32_t bad = 0;
+  for (int64_t base = rb; base < re; base += PT_ROWS) {
+    const uint32_t rows = (uint32_t)((re - base < PT_ROWS) ? re - base : PT_ROWS);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
+    __syncthreads();
+    // every load of the sub-tile is issued before the first use (one memory latency per sub-tile)
+    uint32_t tg[16];
+    R rc[16];
+    if (base >= (int64_t)pk.v.nc) {
+      // batch rows only: branch-free loads (rows past the end re-read the last row and are dropped)
+      const uint32_t b0 = (uint32_t)(base - pk.v.nc), last = rows - 1;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const uint32_t i = w * 1024 + s * 64 + lane;
+        const uint32_t b = b0 + (i < rows ? i : last);
+        const uint32_t k = (uint32_t)pk.v.key[b];
+        uint32_t bd = 0;
+        rc[s] = pk.batch(b, t0, bd);
+        tg[s] = (i < rows && k < pp.K) ? k : 0xffffffffu;
+        bad |= (i < rows && k != 0xffffffffu) ? bd : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const uint32_t i = w * 1024 + s * 64 + lane;
+        const uint32_t r = (uint32_t)(base + i);
+        const uint32_t k = i < rows ? kf(r) : 0xffffffffu;
+        tg[s] = k < pp.K ? k : 0xffffffffu;
+        if (k < pp.K) {
+          rc[s] = pk(r);
+          if (N) {
+            const int64_t dt = v_ts(pk.v, r) - t0;
+            if (dt != (int64_t)(int32_t)dt) bad |= PK_TS_RANGE;
+            if (R::has_pay && pk.v.pcol && pk.v.pw == 8) {
+              const int64_t pv = v_payload(pk.v, r);
+              if (pv != (int64_t)(int32_t)pv) bad |= PK_PAY_RANGE;
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      if (tg[s] != 0xffffffffu) atomicAdd(&L.cw[w][tg[s] >> pp.lb], 1u);
+    __syncthreads();
+    const uint32_t staged = part_cursors(L);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool valid = tg[s] != 0xffffffffu;
+      const uint32_t d = valid ? tg[s] >> pp.lb : 0u;
+      uint32_t rank, cnt;
+      peer_rank(valid, d, pp.nb1, rank, cnt);
+      if (valid) {
+        const uint32_t slot = L.cw[w][d] + rank;
+        if (rank == 0) L.cw[w][d] = slot + cnt;
+        L.stage[slot] = rc[s];
+        L.tag[slot] = (uint16_t)tg[s];
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < staged; q += 256) {
+      const uint32_t k = L.tag[q], d = k >> pp.lb;
+      const uint32_t dst = L.run[d] + q - L.ls[d];
+      orec[dst] = L.stage[q];
+      if (olk) olk[dst] = (uint8_t)(k & lmask);
+    }
+    __syncthreads();
+    L.run[t] += L.tot[t];
+  }
+  if (bad) atomicOr(flags, bad);
+}
+
+// pass-2 segment (g, jj): group g's rows that came from pass-1 segments [jj*ts2, (jj+1)*ts2)
+__device__ __forceinline__ void part2_range(const PartPlan& pp, const uint32_t* o1, uint32_t g, uint32_t jj,
+                                            uint32_t& lo, uint32_t& hi) {
+  lo = o1[(size_t)g * pp.ns1 + jj * pp.ts2];
+  hi = o1[(size_t)g * pp.ns1 + min(pp.ns1, (jj + 1) * pp.ts2)];
+}
+
+static __global__ void __launch_bounds__(256) k_part2_hist(PartPlan pp, const uint32_t* __restrict__ o1,
+                                                           const uint8_t* __restrict__ glk, uint32_t* __restrict__ h2) {
+  __shared__ uint32_t cnt[PT_D];
+  const uint32_t g = blockIdx.x / pp.nj, jj = blockIdx.x % pp.nj;
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t lo, hi;
+  part2_range(pp, o1, g, jj, lo, hi);
+  for (uint32_t p = lo + threadIdx.x; p < hi; p += 256) atomicAdd(&cnt[glk[p]], 1u);
+  __syncthreads();
+  if (threadIdx.x < (1u << pp.lb)) h2[(size_t)((g << pp.lb) + threadIdx.x) * pp.nj + jj] = cnt[threadIdx.x];
+}
+
+template <class R>
+__global__ void __launch_bounds__(256) k_part2(PartPlan pp, const uint32_t* __restrict__ o1, const uint32_t* __restrict__ o2,
+                                               const R* __restrict__ grec, const uint8_t* __restrict__ glk,
+                                               R* __restrict__ srec) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  PartLds<R>& L = *(PartLds<R>*)lds_raw;
+  const uint32_t g = blockIdx.x / pp.nj, jj = blockIdx.x % pp.nj;
+  const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
+  if (t < (1u << pp.lb)) L.run[t] = o2[(size_t)((g << pp.lb) + t) * pp.nj + jj];
+  uint32_t lo, hi;
+  part2_range(pp, o1, g, jj, lo, hi);
+  for (uint32_t base = lo; base < hi; base += PT_ROWS) {
+    const uint32_t rows = (hi - base < (uint32_t)PT_ROWS) ? hi - base : (uint32_t)PT_ROWS;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
+    __syncthreads();
+    uint32_t tg[16];
+    R rc[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t i = w * 1024 + s * 64 + lane;
+      const uint32_t p = base + (i < rows ? i : rows - 1);   // (clamped: branch-free loads)
+      const uint32_t lk = glk[p];
+      rc[s] = grec[p];
+      tg[s] = i < rows ? lk : 0xffffffffu;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      if (tg[s] != 0xffffffffu) atomicAdd(&L.cw[w][tg[s]], 1u);
+    __syncthreads();
+    const uint32_t staged = part_cursors(L);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool valid = tg[s] != 0xffffffffu;
+      const uint32_t d = valid ? tg[s] : 0u;
+      uint32_t rank, cnt;
+      peer_rank(valid, d, pp.nb2, rank, cnt);
+      if (valid) {
+        const uint32_t slot = L.cw[w][d] + rank;
+        if (rank == 0) L.cw[w][d] = slot + cnt;
+        L.stage[slot] = rc[s];
+        L.tag[slot] = (uint16_t)d;
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < staged; q += 256) {
+      const uint32_t d = L.tag[q];
+      srec[L.run[d] + q - L.ls[d]] = L.stage[q];
+    }
+    __syncthreads();
+    L.run[t] += L.tot[t];
+  }
+}
+
+// pass 2 moves records as opaque words (vector / scalar members keep the 16 per thread in registers)
+typedef uint32_t PtU4 __attribute__((ext_vector_type(4)));
+struct PtB24 { uint64_t a, b, c; };
+template <class R>
+using PtRaw = typename std::conditional<sizeof(R) == 16, PtU4, PtB24>::type;
+
+// per-key segments [seg_b, seg_e) of the sorted records from the last pass's offsets (stride = its segments)
+static __global__ void k_part_segs(uint32_t K, const uint32_t* __restrict__ o, uint32_t stride,
+                                   uint32_t* __restrict__ seg_b, uint32_t* __restrict__ seg_e) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  seg_b[k] = o[(size_t)k * stride];
+  seg_e[k] = o[(size_t)(k + 1) * stride];
+}
+
+static PartPlan part_plan(uint32_t K, int64_t nt) {
+  PartPlan p;
+  memset(&p, 0, sizeof(p));
+  p.K = K;
+  uint32_t bits = 0;
+  while ((1ull << bits) < (uint64_t)K) ++bits;
+  auto nbits = [](uint32_t nd) { uint32_t b = 0; while ((1u << b) < nd) ++b; return b; };
+  if (K <= (uint32_t)PT_D) {
+    p.two = 0; p.lb = 0; p.ng = K;
+  } else {
+    const uint32_t hb = (bits + 1) / 2;
+    p.two = 1; p.lb = bits - hb; p.ng = (K + (1u << p.lb) - 1) >> p.lb;
+  }
+  p.nb1 = nbits(p.ng);
+  p.nb2 = p.lb;
+  // >= ~1024 pass-1 segments when the batch allows (4 workgroups per CU), at most 16 sub-tiles each
+  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(16, nt / ((int64_t)PT_ROWS * 1024)));
+  p.seg1 = (uint32_t)(PT_ROWS * sub);
+  p.ns1 = (uint32_t)std::max<int64_t>(1, (nt + p.seg1 - 1) / p.seg1);
+  // pass-2 segments of ~8192 rows of one group
+  p.ts2 = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(p.ns1, (int64_t)8192 * p.ng / p.seg1));
+  p.nj = (p.ns1 + p.ts2 - 1) / p.ts2;
+  return p;
+}
+
+// ---------------------------------------------------------------------------------------------
 struct ProjPlan {
   // per select column: src 0 = e1 row (pending partial), 1 = e2 row (trigger); kind 0 = e1 payload carried
   // in the pending list, 1 = the compared value, 2 = null (chain index beyond a single-event slot),
@@ -400,6 +724,28 @@ struct MRec {
   uint32_t r1, r2;
   int64_t v1;                 // e1 compared-value bits
   int64_t p1;                 // e1 payload bits
+};
+
+// Where the record walk leaves each delivered match (k_project builds the output record from it).  Narrow form
+// (narrow walker records of a 4-byte value type, whose LDS ring already keeps 32-bit payloads): 16 B per match in
+// one store; wide form: MRec.
+struct MRec16 {
+  uint32_t r1, r2, v1, p1;
+};
+struct MatchSink {
+  void* rec;
+  int32_t narrow;
+  __device__ __forceinline__ void put(uint32_t slot, uint32_t r1, uint32_t r2, int64_t v1, int64_t p1) const {
+    if (narrow) {
+      PtU4 q;
+      q.x = r1; q.y = r2; q.z = (uint32_t)v1; q.w = (uint32_t)p1;
+      ((PtU4*)rec)[slot] = q;
+    } else {
+      MRec m;
+      m.r1 = r1; m.r2 = r2; m.v1 = v1; m.p1 = p1;
+      ((MRec*)rec)[slot] = m;
+    }
+  }
 };
 
 struct UnitDesc {
@@ -558,7 +904,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 // one `within` window behind them.
 template <class T>
 __global__ void __launch_bounds__(256) k_project(WalkArgs a, Virt v, ProjPlan pp, SgCols bc, SgCols cc,
-                                                 const MRec* __restrict__ mrec, const uint32_t* __restrict__ off,
+                                                 const MatchSink ms, const uint32_t* __restrict__ off,
                                                  int64_t total, char* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char stage[];   // 256 records, written out contiguously
   const int64_t per = (int64_t)blockDim.x;
@@ -567,7 +913,16 @@ __global__ void __launch_bounds__(256) k_project(WalkArgs a, Virt v, ProjPlan pp
   const int64_t s0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * per;
   const int64_t sl = s0 + threadIdx.x;
   if (sl < total) {
-    const MRec mr = mrec[sl];
+    MRec mr;
+    if (ms.narrow) {   // 32-bit value / payload bits widened as val_bits and the LDS ring (pzero) widen them
+      const PtU4 q = ((const PtU4*)ms.rec)[sl];
+      mr.r1 = q.x;
+      mr.r2 = q.y;
+      mr.v1 = std::is_same<T, float>::value ? (int64_t)q.z : (int64_t)(int32_t)q.z;
+      mr.p1 = v.pfloat ? (int64_t)q.w : (int64_t)(int32_t)q.w;
+    } else {
+      mr = ((const MRec*)ms.rec)[sl];
+    }
     const uint32_t r1 = mr.r1, r2 = mr.r2;
     const uint64_t b = r2 - v.nc;
     const uint32_t ob = off[b];
@@ -658,7 +1013,7 @@ struct Walker {
   // returns true when this event (inside the unit's chunk) completed partials
   template <class R>
   __device__ __forceinline__ bool step(const WalkArgs& a, const Virt& v, const R& rc, bool in_chunk,
-                                       uint32_t ofs, uint32_t* __restrict__ cnt, MRec* __restrict__ mrec,
+                                       uint32_t ofs, uint32_t* __restrict__ cnt, const MatchSink& em,
                                        bool payload, int64_t pay = 0, bool pay_ready = false) {
     const uint32_t f = rc.rowf >> 30;
     if (!f) return false;
@@ -685,14 +1040,8 @@ struct Walker {
         // monotone stack: the completed partials are exactly a suffix, delivered oldest first
         while (top != head && cmp_sel<OP, T>(a.op, x, L.gv(top - 1))) { --top; ++m; }
         if (WRITE && in_chunk && r >= v.nc) {
-          for (uint32_t q = 0; q < m; ++q) {
-            MRec e;
-            e.r1 = L.grow(top + q);
-            e.r2 = r;
-            e.v1 = val_bits<T>(L.gv(top + q));
-            e.p1 = L.gpay(top + q);
-            mrec[ofs + q] = e;
-          }
+          for (uint32_t q = 0; q < m; ++q)
+            em.put(ofs + q, L.grow(top + q), r, val_bits<T>(L.gv(top + q)), L.gpay(top + q));
         }
       } else {
         const bool emit = in_chunk && (r >= v.nc);
@@ -700,14 +1049,7 @@ struct Walker {
         for (uint32_t s = head; s != top; ++s) {
           T e = L.gv(s);
           if (cmp_sel<OP, T>(a.op, x, e)) {
-            if (WRITE && emit) {
-              MRec mr;
-              mr.r1 = L.grow(s);
-              mr.r2 = r;
-              mr.v1 = val_bits<T>(e);
-              mr.p1 = L.gpay(s);
-              mrec[ofs + m] = mr;
-            }
+            if (WRITE && emit) em.put(ofs + m, L.grow(s), r, val_bits<T>(e), L.gpay(s));
             ++m;
           } else {
             if (wr != s) L.put(wr, e, BIG ? (int64_t)at(s) : L.base + (int64_t)at(s), L.grow(s), L.gpay(s));
@@ -740,7 +1082,7 @@ template <class T, bool N, bool WRITE, bool BIG>
 __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, const uint32_t* __restrict__ seg_b,
                                                      const uint32_t* __restrict__ seg_e, UnitDesc* __restrict__ ud,
                                                      uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                                     MRec* __restrict__ mrec, uint32_t* __restrict__ emap,
+                                                     const MatchSink em, uint32_t* __restrict__ emap,
                                                      WalkStats* __restrict__ st, char* __restrict__ big,
                                                      uint32_t* __restrict__ carry_q0, uint32_t* __restrict__ carry_n) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -819,7 +1161,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
       for (int i = 0; i < GT::G; ++i) {
         const uint32_t p = g + i;
         if (p < w || p >= p1) continue;
-        if (W.step(a, v, cur.rec(i), p >= p0, WRITE ? ofs[i] : 0u, cnt, mrec, payload) && !WRITE) W.mark_emit(p, emap);
+        if (W.step(a, v, cur.rec(i), p >= p0, WRITE ? ofs[i] : 0u, cnt, em, payload) && !WRITE) W.mark_emit(p, emap);
         if (!BIG && W.overflow) break;
       }
       if (!BIG && W.overflow) break;
@@ -837,7 +1179,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
       WRec<T, N> rc = src.pk(p);
       uint32_t o = 0;
       if (WRITE) o = off_of(rc, p, (emap[p >> 5] >> (p & 31)) & 1u);
-      if (W.step(a, v, rc, p >= p0, o, cnt, mrec, payload) && !WRITE) W.mark_emit(p, emap);
+      if (W.step(a, v, rc, p >= p0, o, cnt, em, payload) && !WRITE) W.mark_emit(p, emap);
       if (!BIG && W.overflow) break;
     }
   }
@@ -942,7 +1284,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
                                                        const uint32_t* __restrict__ wlen,
                                                        const uint32_t* __restrict__ wrow,
                                                        const WRec<T, N>* __restrict__ tile, uint32_t* __restrict__ cnt,
-                                                       const uint32_t* __restrict__ off, MRec* __restrict__ mrec,
+                                                       const uint32_t* __restrict__ off, const MatchSink em,
                                                        uint64_t* __restrict__ emask, WalkStats* __restrict__ st,
                                                        UnitDesc* __restrict__ ud_w, uint32_t* __restrict__ carry_q0,
                                                        uint32_t* __restrict__ carry_n) {
@@ -989,7 +1331,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
     for (int j = 0; j < PF; ++j) {
       bool e = false;
       if (active && i0 + j < len && !Wk.overflow)
-        e = Wk.step(a, v, buf[j], i0 + j >= chunk_i, WRITE ? ofs[j] : 0u, cnt, mrec, payload, WRITE ? pq[j] : 0, true);
+        e = Wk.step(a, v, buf[j], i0 + j >= chunk_i, WRITE ? ofs[j] : 0u, cnt, em, payload, WRITE ? pq[j] : 0, true);
       if (!WRITE) {
         const uint64_t b = __ballot(e);
         if (lane == 0) emask[base + i0 + j] = b;
@@ -1171,14 +1513,14 @@ struct PushPlan {
 template <class T, bool N, bool WRITE>
 static void launch_walk_t(int op, dim3 g, dim3 b, size_t lds, hipStream_t st, const WalkArgs& wa, const Src<T, N>& src,
                           const uint32_t* seg_b, const uint32_t* seg_e, UnitDesc* ud, const uint32_t* wlen,
-                          const uint32_t* wrow, const WRec<T, N>* tile, uint32_t* cnt, const uint32_t* off, MRec* mrec,
+                          const uint32_t* wrow, const WRec<T, N>* tile, uint32_t* cnt, const uint32_t* off, const MatchSink& ms,
                           uint64_t* emask, WalkStats* wst, uint32_t* carry_q0, uint32_t* carry_n) {
 #define SG_WALK_T(OPV)                                                                                          \
   if (lds > 65536)                                                                                              \
     HIPCHK(hipFuncSetAttribute((const void*)k_walk_t<T, N, OPV, WRITE>,                                        \
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                          \
   hipLaunchKernelGGL((k_walk_t<T, N, OPV, WRITE>), g, b, lds, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, \
-                     mrec, emask, wst, ud, carry_q0, carry_n)
+                     ms, emask, wst, ud, carry_q0, carry_n)
   switch (op) {
     case 2: SG_WALK_T(2); break;
     case 3: SG_WALK_T(3); break;
@@ -1407,7 +1749,7 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   if (total) {
     h->kbeg("project");
     hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)), dim3(256), (size_t)256 * wa.stride, st,
-                       wa, v, plan.pp, bv.cols, cc, mrec, off, (int64_t)total, out);
+                       wa, v, plan.pp, bv.cols, cc, MatchSink{mrec, 0}, off, (int64_t)total, out);
     h->kend();
     HIPCHK(hipGetLastError());
   }
@@ -1583,7 +1925,63 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
   seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
   const dim3 pgrd((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32));
-  if (d.partitioned) {
+  const bool lds_part = d.partitioned && kb <= 65536u && h->opt.partition_sort == 0;
+  if (lds_part) {
+    const PartPlan pp = part_plan(kb, nt);
+    KeyOf kf{bv.key, cs.key, (uint32_t)nc};
+    const size_t n1 = (size_t)pp.ng * pp.ns1 + 1;
+    uint32_t* h1 = (uint32_t*)h->ws.get("part_h1", sizeof(uint32_t) * n1, st);
+    uint32_t* o1 = (uint32_t*)h->ws.get("part_o1", sizeof(uint32_t) * n1, st);
+    R* srec = (R*)h->ws.get("srec", sizeof(R) * nt, st);
+    const size_t lds = std::max(sizeof(PartLds<R>), sizeof(PartLds<PtRaw<R>>));
+    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    typedef PtRaw<R> RW;
+    static_assert(sizeof(RW) == sizeof(R), "raw record layout");
+    HIPCHK(hipFuncSetAttribute((const void*)k_part2<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    h->kbeg("part_hist");
+    HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pp, nt, h1, pk_flags);
+    HIPCHK(hipGetLastError());
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, h1, o1, (uint32_t)0, n1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("part_scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, h1, o1, (uint32_t)0, n1, rocprim::plus<uint32_t>(), st));
+    h->kend();
+    if (!pp.two) {
+      h->kbeg("part_scatter");
+      hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds, st, src.pk, kf, pp, nt, o1, srec, (uint8_t*)nullptr,
+                         pk_flags);
+      HIPCHK(hipGetLastError());
+      h->kend();
+      hipLaunchKernelGGL(k_part_segs, dim3((kb + 255) / 256), dim3(256), 0, st, kb, o1, pp.ns1, seg_b, seg_e);
+    } else {
+      R* grec = (R*)h->ws.get("grec", sizeof(R) * nt, st);
+      uint8_t* glk = (uint8_t*)h->ws.get("glk", nt, st);
+      const size_t n2 = ((size_t)pp.ng << pp.lb) * pp.nj + 1;
+      uint32_t* h2 = (uint32_t*)h->ws.get("part_h2", sizeof(uint32_t) * n2, st);
+      uint32_t* o2 = (uint32_t*)h->ws.get("part_o2", sizeof(uint32_t) * n2, st);
+      h->kbeg("part_group");
+      hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds, st, src.pk, kf, pp, nt, o1, grec, glk, pk_flags);
+      HIPCHK(hipGetLastError());
+      h->kend();
+      h->kbeg("part_hist2");
+      HIPCHK(hipMemsetAsync(h2 + n2 - 1, 0, sizeof(uint32_t), st));
+      hipLaunchKernelGGL(k_part2_hist, dim3(pp.ng * pp.nj), dim3(256), 0, st, pp, o1, glk, h2);
+      HIPCHK(hipGetLastError());
+      tb = 0;
+      HIPCHK(rocprim::exclusive_scan(nullptr, tb, h2, o2, (uint32_t)0, n2, rocprim::plus<uint32_t>(), st));
+      tmp = h->ws.get("part_scan_tmp2", tb, st);
+      HIPCHK(rocprim::exclusive_scan(tmp, tb, h2, o2, (uint32_t)0, n2, rocprim::plus<uint32_t>(), st));
+      h->kend();
+      h->kbeg("part_key");
+      hipLaunchKernelGGL((k_part2<RW>), dim3(pp.ng * pp.nj), dim3(256), lds, st, pp, o1, o2, (const RW*)grec, glk, (RW*)srec);
+      HIPCHK(hipGetLastError());
+      h->kend();
+      hipLaunchKernelGGL(k_part_segs, dim3((kb + 255) / 256), dim3(256), 0, st, kb, o2, pp.nj, seg_b, seg_e);
+    }
+    HIPCHK(hipGetLastError());
+    src.srec = srec;
+  } else if (d.partitioned) {
     int end_bit = 1;
     while ((1ull << end_bit) <= (uint64_t)kb) ++end_bit;
     uint32_t* skeys = (uint32_t*)h->ws.get("skeys", sizeof(uint32_t) * nt, st);
@@ -1672,8 +2070,6 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   }
   wa.n_select = d.n_select;
   wa.stride = 32 + 8 * d.n_select;
-  const ProjPlan& pp = plan.pp;
-
   UnitDesc* ud = (UnitDesc*)h->ws.get("units", sizeof(UnitDesc) * units, st);
   WalkStats* wst = (WalkStats*)h->ws.get("walkstats", sizeof(WalkStats), st);
   uint32_t* cnt = (uint32_t*)h->ws.get("cnt", sizeof(uint32_t) * (n + 1), st);
@@ -1687,6 +2083,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   if (wa.carry_out) HIPCHK(hipMemsetAsync(carry_n, 0, sizeof(uint32_t) * (K + 1), st));
   const dim3 wblk(WALK_BLOCK), wgrd((unsigned)((units + WALK_BLOCK - 1) / WALK_BLOCK));
   const uint32_t nw = (uint32_t)((units + 63) / 64);
+  MatchSink ms{nullptr, 0};   // (record pass: set once the match list is allocated)
   uint32_t* wlen = nullptr;
   uint32_t* wrow = nullptr;
   R* tile = nullptr;
@@ -1736,8 +2133,8 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       h->kend();
     }
     h->kbeg("walk_count");
-    launch_walk_t<T, N, false>(op, wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, (MRec*)nullptr,
-                            emask, wst, carry_q0, carry_n);
+    launch_walk_t<T, N, false>(op, wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, ms,
+                               emask, wst, carry_q0, carry_n);
     h->kend();
   }
   auto scan_counts = [&]() {
@@ -1763,7 +2160,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     big = (char*)h->ws.get("big_lists", (size_t)hs.n_ovf * wa.big_cap * PendBytes<T>::hbm, st);
     h->mark(6);
     hipLaunchKernelGGL((k_walk<T, N, false, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
-                       (MRec*)nullptr, emap, wst, big, carry_q0, carry_n);
+                       ms, emap, wst, big, carry_q0, carry_n);
     HIPCHK(hipGetLastError());
     scan_counts();
     h->mark(7);
@@ -1781,21 +2178,23 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   if (total || wa.carry_out) {
     out = h->out.reserve(total, d.n_select, st);
     wa.out_base = h->out.n;
-    MRec* mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * std::max<uint32_t>(total, 1), st);
+    // narrow match records when the value type is 4 bytes and every payload fits 32 bits (narrow walker records)
+    ms.narrow = (N && sizeof(T) == 4) ? 1 : 0;
+    ms.rec = h->ws.get("mrec", (ms.narrow ? sizeof(MRec16) : sizeof(MRec)) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
     h->kbeg("walk_record");
-    launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, mrec,
+    launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, ms,
                               emask, wst, carry_q0, carry_n);
     h->kend();
     if (hs.n_ovf) {
-      hipLaunchKernelGGL((k_walk<T, N, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, mrec,
+      hipLaunchKernelGGL((k_walk<T, N, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, ms,
                          emap, wst, big, carry_q0, carry_n);
       HIPCHK(hipGetLastError());
     }
     if (total) {
       h->kbeg("project");
       hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)),
-                         dim3(256), (size_t)256 * wa.stride, st, wa, v, pp, bv.cols, cc, mrec, off, (int64_t)total, out);
+                         dim3(256), (size_t)256 * wa.stride, st, wa, v, plan.pp, bv.cols, cc, ms, off, (int64_t)total, out);
       HIPCHK(hipGetLastError());
       h->kend();
     }

@@ -65,3 +65,36 @@ def assert_same(a: Outputs, b: Outputs):
     if not np.array_equal(vals_a, vals_b):
         k = int(np.nonzero((vals_a != vals_b).any(axis=1))[0][0])
         raise AssertionError(f"vals differ first at {k}: {vals_a[k]} vs {vals_b[k]}")
+
+
+_SHARDS = {}
+
+
+def _shard_worker(w):
+    from oracle import OracleEngine
+    return run_engine(OracleEngine, _SHARDS["q"], [_SHARDS["shards"][w]])
+
+
+def sharded_oracle(query_text, batch, workers):
+    """The oracle over a partitioned `batch` with its rows sharded by partition key over `workers` forked
+    processes.  Keys never interact (each has its own cloned runtime, C/partition/PartitionRuntime.java:255-308),
+    every shard keeps the rows' global event indices, and all matches of one trigger event come from its key's
+    shard in pending order -- so a stable merge of the shards' outputs by trigger index is the reference's delivery
+    order for the whole batch.  Test infrastructure only (full-size parity)."""
+    import multiprocessing as mp
+    shards = []
+    for w in range(workers):
+        ix = np.nonzero((batch.key % workers) == w)[0]
+        idx = batch.index[ix] if batch.index is not None else (np.uint64(batch.base_index) + ix.astype(np.uint64))
+        shards.append(Batch(len(ix), 0, batch.ts[ix], batch.stream[ix], batch.key[ix], [c[ix] for c in batch.cols],
+                            [None if x is None else x[ix] for x in batch.nulls], index=idx))
+    _SHARDS["shards"], _SHARDS["q"] = shards, query_text
+    try:
+        with mp.get_context("fork").Pool(workers) as pool:
+            outs = pool.map(_shard_worker, range(workers))
+    finally:
+        _SHARDS.clear()
+    fields = ("trigger", "ts", "key", "group", "vals", "vnull")
+    cat = [np.concatenate([getattr(o, f) for o in outs]) for f in fields]
+    order = np.argsort(cat[0], kind="stable")
+    return Outputs(*[c[order] for c in cat])
