@@ -21,6 +21,8 @@ sys.path.insert(0, ROOT)
 
 MARKS = [   # kernel name pattern -> engine mark (siddhi_amd/csrc: h->kbeg names)
     (r"k_pred_simple|k_pred\b", "pred"), (r"k_pack\b", "pack"), (r"onesweep", "key_sort"),
+    (r"k_part1_hist", "part_hist"), (r"k_part2_hist", "part_hist2"), (r"k_part1<", "part_group"),
+    (r"k_part2<|k_part_segs", "part_key"),
     (r"k_bounds\b", "bounds"), (r"k_units\b|k_rowmap\b", "units"), (r"k_transpose\b", "tile_transpose"),
     (r"k_walk_t<[^>]*false>", "walk_count"), (r"k_walk_t<[^>]*true>", "walk_record"),
     (r"k_walk<[^>]*false, true>", "walk_count"), (r"k_walk<[^>]*true, true>", "walk_record"),

@@ -285,7 +285,7 @@ struct WRec<T, true, 8> {   // narrow, 8-byte value
 };
 struct alignas(16) Blob16 { uint32_t w[4]; };   // 16-byte records sort as one opaque type
 
-static const uint32_t PK_TS_RANGE = 1, PK_PAY_RANGE = 2, PK_KEY_RANGE = 4;   // k_pack flags
+static const uint32_t PK_TS_RANGE = 1, PK_PAY_RANGE = 2, PK_KEY_RANGE = 4, PK_INTERNAL = 8;   // k_pack flags
 
 template <class T, bool N>
 struct PackFn {   // builds the walker record of virtual row r (coalesced when r is sequential)
@@ -422,11 +422,12 @@ static __global__ void __launch_bounds__(256) k_bounds(const uint32_t* __restric
 // digit = key) or two (digit = key group = high bits, then key within its group = low bits).  Each pass
 // cuts its input into segments; a histogram kernel counts digits per segment, one exclusive scan over the
 // (digit, segment) table gives every segment's output position per digit, and the scatter kernel ranks each
-// 4096-row sub-tile stably by digit in LDS (wave ballots over the digit bits) and writes every digit run out
+// 2048-row sub-tile stably by digit in LDS (wave ballots over the digit bits) and writes every digit run out
 // as whole lines.  Pass 1 reads the raw columns and builds the walker records on the way (no pack pass);
 // pass 2 reads pass 1's records and 1-byte in-group keys.  The per-key segments are read off the last
 // pass's offsets (no bounds pass).  Same result as the radix sort: per key its rows in arrival order.
-static const int PT_ROWS = 4096;   // rows per LDS-staged sub-tile (16 per thread)
+static const int PT_PER = 8;                 // rows per thread per sub-tile
+static const int PT_ROWS = 256 * PT_PER;   // rows per LDS-staged sub-tile (2048: 4 workgroups per CU)
 static const int PT_D = 256;       // digit values per pass (8 bits)
 
 struct PartPlan {
@@ -491,22 +492,32 @@ __device__ __forceinline__ uint32_t part_cursors(PartLds<R>& L) {
   return L.ls[PT_D - 1] + L.tot[PT_D - 1];
 }
 
-// pass-1 histogram: segment j = virtual rows [j*seg1, (j+1)*seg1); h1[group * ns1 + j]
+// pass-1 histogram: segment j = virtual rows [j*seg1, (j+1)*seg1); h1[group * ns1 + j].  Per-wave counters
+// (fewer same-address LDS atomics), eight rows per thread in flight.
 static __global__ void __launch_bounds__(256) k_part1_hist(KeyOf kf, PartPlan pp, int64_t nt, uint32_t* __restrict__ h1,
                                                            uint32_t* __restrict__ flags) {
-  __shared__ uint32_t cnt[PT_D];
-  const uint32_t j = blockIdx.x;
-  cnt[threadIdx.x] = 0;
+  __shared__ uint32_t cnt[4][PT_D];
+  const uint32_t j = blockIdx.x, t = threadIdx.x, w = t >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cnt[q][t] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)j * pp.seg1, r1 = (nt < r0 + pp.seg1) ? nt : r0 + pp.seg1;
   uint32_t bad = 0;
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
-    const uint32_t k = kf((uint32_t)r);
-    if (k < pp.K) atomicAdd(&cnt[k >> pp.lb], 1u);
-    else if (k != 0xffffffffu) bad |= PK_KEY_RANGE;   // beyond the caller's key_bound
+  for (int64_t rb = r0; rb < r1; rb += 256 * 8) {
+    uint32_t k[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int64_t r = rb + s * 256 + t;
+      k[s] = r < r1 ? kf((uint32_t)r) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (k[s] < pp.K) atomicAdd(&cnt[w][k[s] >> pp.lb], 1u);
+      else if (k[s] != 0xffffffffu) bad |= PK_KEY_RANGE;   // beyond the caller's key_bound
+    }
   }
   __syncthreads();
-  if (threadIdx.x < pp.ng) h1[(size_t)threadIdx.x * pp.ns1 + j] = cnt[threadIdx.x];
+  if (t < pp.ng) h1[(size_t)t * pp.ns1 + j] = cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
   if (bad) atomicOr(flags, bad);
 }
 
@@ -524,20 +535,15 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
   const int64_t rb = (int64_t)j * pp.seg1, re = (nt < rb + pp.seg1) ? nt : rb + pp.seg1;
   const int64_t t0 = N ? v_ts(pk.v, 0) : 0;
   uint32_t bad = 0;
-  for (int64_t base = rb; base < re; base += PT_ROWS) {
+  // the sub-tile's loads, all issued before the first use (one memory latency per sub-tile)
+  auto load = [&](int64_t base, uint32_t* tg, R* rc) {
     const uint32_t rows = (uint32_t)((re - base < PT_ROWS) ? re - base : PT_ROWS);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
-    __syncthreads();
-    // every load of the sub-tile is issued before the first use (one memory latency per sub-tile)
-    uint32_t tg[16];
-    R rc[16];
     if (base >= (int64_t)pk.v.nc) {
       // batch rows only: branch-free loads (rows past the end re-read the last row and are dropped)
       const uint32_t b0 = (uint32_t)(base - pk.v.nc), last = rows - 1;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const uint32_t i = w * 1024 + s * 64 + lane;
+      for (int s = 0; s < PT_PER; ++s) {
+        const uint32_t i = w * (PT_PER * 64) + s * 64 + lane;
         const uint32_t b = b0 + (i < rows ? i : last);
         const uint32_t k = (uint32_t)pk.v.key[b];
         uint32_t bd = 0;
@@ -547,8 +553,8 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
       }
     } else {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const uint32_t i = w * 1024 + s * 64 + lane;
+      for (int s = 0; s < PT_PER; ++s) {
+        const uint32_t i = w * (PT_PER * 64) + s * 64 + lane;
         const uint32_t r = (uint32_t)(base + i);
         const uint32_t k = i < rows ? kf(r) : 0xffffffffu;
         tg[s] = k < pp.K ? k : 0xffffffffu;
@@ -565,13 +571,21 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
         }
       }
     }
+  };
+  uint32_t tg[PT_PER], tn[PT_PER];
+  R rc[PT_PER], rn[PT_PER];
+  if (rb < re) load(rb, tg, rc);
+  for (int64_t base = rb; base < re; base += PT_ROWS) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
+    for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PT_PER; ++s)
       if (tg[s] != 0xffffffffu) atomicAdd(&L.cw[w][tg[s] >> pp.lb], 1u);
     __syncthreads();
     const uint32_t staged = part_cursors(L);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < PT_PER; ++s) {
       const bool valid = tg[s] != 0xffffffffu;
       const uint32_t d = valid ? tg[s] >> pp.lb : 0u;
       uint32_t rank, cnt;
@@ -583,15 +597,19 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
         L.tag[slot] = (uint16_t)tg[s];
       }
     }
+    if (base + PT_ROWS < re) load(base + PT_ROWS, tn, rn);   // next sub-tile in flight during the write-out
     __syncthreads();
     for (uint32_t q = t; q < staged; q += 256) {
       const uint32_t k = L.tag[q], d = k >> pp.lb;
       const uint32_t dst = L.run[d] + q - L.ls[d];
+      if ((int64_t)dst >= nt) { bad |= PK_INTERNAL; continue; }
       orec[dst] = L.stage[q];
       if (olk) olk[dst] = (uint8_t)(k & lmask);
     }
     __syncthreads();
     L.run[t] += L.tot[t];
+#pragma unroll
+    for (int s = 0; s < PT_PER; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
   }
   if (bad) atomicOr(flags, bad);
 }
@@ -605,21 +623,32 @@ __device__ __forceinline__ void part2_range(const PartPlan& pp, const uint32_t* 
 
 static __global__ void __launch_bounds__(256) k_part2_hist(PartPlan pp, const uint32_t* __restrict__ o1,
                                                            const uint8_t* __restrict__ glk, uint32_t* __restrict__ h2) {
-  __shared__ uint32_t cnt[PT_D];
-  const uint32_t g = blockIdx.x / pp.nj, jj = blockIdx.x % pp.nj;
-  cnt[threadIdx.x] = 0;
+  __shared__ uint32_t cnt[4][PT_D];
+  const uint32_t g = blockIdx.x / pp.nj, jj = blockIdx.x % pp.nj, t = threadIdx.x, w = t >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cnt[q][t] = 0;
   __syncthreads();
   uint32_t lo, hi;
   part2_range(pp, o1, g, jj, lo, hi);
-  for (uint32_t p = lo + threadIdx.x; p < hi; p += 256) atomicAdd(&cnt[glk[p]], 1u);
+  for (uint32_t pb = lo; pb < hi; pb += 256 * 8) {
+    uint32_t d[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const uint32_t p = pb + s * 256 + t;
+      d[s] = p < hi ? (uint32_t)glk[p] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (d[s] != 0xffffffffu) atomicAdd(&cnt[w][d[s]], 1u);
+  }
   __syncthreads();
-  if (threadIdx.x < (1u << pp.lb)) h2[(size_t)((g << pp.lb) + threadIdx.x) * pp.nj + jj] = cnt[threadIdx.x];
+  if (t < (1u << pp.lb)) h2[(size_t)((g << pp.lb) + t) * pp.nj + jj] = cnt[0][t] + cnt[1][t] + cnt[2][t] + cnt[3][t];
 }
 
 template <class R>
 __global__ void __launch_bounds__(256) k_part2(PartPlan pp, const uint32_t* __restrict__ o1, const uint32_t* __restrict__ o2,
                                                const R* __restrict__ grec, const uint8_t* __restrict__ glk,
-                                               R* __restrict__ srec) {
+                                               R* __restrict__ srec, uint32_t cap, uint32_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   PartLds<R>& L = *(PartLds<R>*)lds_raw;
   const uint32_t g = blockIdx.x / pp.nj, jj = blockIdx.x % pp.nj;
@@ -627,28 +656,31 @@ __global__ void __launch_bounds__(256) k_part2(PartPlan pp, const uint32_t* __re
   if (t < (1u << pp.lb)) L.run[t] = o2[(size_t)((g << pp.lb) + t) * pp.nj + jj];
   uint32_t lo, hi;
   part2_range(pp, o1, g, jj, lo, hi);
-  for (uint32_t base = lo; base < hi; base += PT_ROWS) {
+  auto load = [&](uint32_t base, uint32_t* tg, R* rc) {
     const uint32_t rows = (hi - base < (uint32_t)PT_ROWS) ? hi - base : (uint32_t)PT_ROWS;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
-    __syncthreads();
-    uint32_t tg[16];
-    R rc[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const uint32_t i = w * 1024 + s * 64 + lane;
+    for (int s = 0; s < PT_PER; ++s) {
+      const uint32_t i = w * (PT_PER * 64) + s * 64 + lane;
       const uint32_t p = base + (i < rows ? i : rows - 1);   // (clamped: branch-free loads)
       const uint32_t lk = glk[p];
       rc[s] = grec[p];
       tg[s] = i < rows ? lk : 0xffffffffu;
     }
+  };
+  uint32_t tg[PT_PER], tn[PT_PER];
+  R rc[PT_PER], rn[PT_PER];
+  if (lo < hi) load(lo, tg, rc);
+  for (uint32_t base = lo; base < hi; base += PT_ROWS) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
+    for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PT_PER; ++s)
       if (tg[s] != 0xffffffffu) atomicAdd(&L.cw[w][tg[s]], 1u);
     __syncthreads();
     const uint32_t staged = part_cursors(L);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < PT_PER; ++s) {
       const bool valid = tg[s] != 0xffffffffu;
       const uint32_t d = valid ? tg[s] : 0u;
       uint32_t rank, cnt;
@@ -660,13 +692,18 @@ __global__ void __launch_bounds__(256) k_part2(PartPlan pp, const uint32_t* __re
         L.tag[slot] = (uint16_t)d;
       }
     }
+    if (hi - base > (uint32_t)PT_ROWS) load(base + PT_ROWS, tn, rn);   // next sub-tile in flight during the write-out
     __syncthreads();
     for (uint32_t q = t; q < staged; q += 256) {
       const uint32_t d = L.tag[q];
-      srec[L.run[d] + q - L.ls[d]] = L.stage[q];
+      const uint32_t dst = L.run[d] + q - L.ls[d];
+      if (dst >= cap) { atomicOr(flags, PK_INTERNAL); continue; }
+      srec[dst] = L.stage[q];
     }
     __syncthreads();
     L.run[t] += L.tot[t];
+#pragma unroll
+    for (int s = 0; s < PT_PER; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
   }
 }
 
@@ -700,8 +737,8 @@ static PartPlan part_plan(uint32_t K, int64_t nt) {
   }
   p.nb1 = nbits(p.ng);
   p.nb2 = p.lb;
-  // >= ~1024 pass-1 segments when the batch allows (4 workgroups per CU), at most 16 sub-tiles each
-  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(16, nt / ((int64_t)PT_ROWS * 1024)));
+  // >= ~2048 pass-1 segments when the batch allows (8 workgroups per CU), at most 32 sub-tiles each
+  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(32, nt / ((int64_t)PT_ROWS * 2048)));
   p.seg1 = (uint32_t)(PT_ROWS * sub);
   p.ns1 = (uint32_t)std::max<int64_t>(1, (nt + p.seg1 - 1) / p.seg1);
   // pass-2 segments of ~8192 rows of one group
@@ -735,7 +772,10 @@ struct MRec16 {
 struct MatchSink {
   void* rec;
   int32_t narrow;
+  uint32_t cap;               // slots allocated (a slot beyond it trips the internal guard)
+  uint32_t* err;
   __device__ __forceinline__ void put(uint32_t slot, uint32_t r1, uint32_t r2, int64_t v1, int64_t p1) const {
+    if (slot >= cap) { atomicOr(err, 8u); return; }
     if (narrow) {
       PtU4 q;
       q.x = r1; q.y = r2; q.z = (uint32_t)v1; q.w = (uint32_t)p1;
@@ -756,7 +796,8 @@ struct WalkStats {
   uint32_t order_err;
   uint32_t n_ovf;
   uint32_t ovf_need;
-  uint32_t pad;
+  uint32_t internal;          // internal consistency guards tripped (bit 1 unit range, 2 tile source, 4 count row,
+                              // 8 match slot): reported as SG_EINVAL instead of touching memory out of range
 };
 
 struct LdsPlan {   // per-push layout of the walkers' LDS rings (count walk: value + time only)
@@ -980,9 +1021,12 @@ struct Walker {
   typedef typename std::conditional<BIG, int64_t, int32_t>::type TT;
   PendList<T, BIG> L;
   uint32_t head = 0, top = 0;
+  TT hts = 0;                 // register copies (valid while head != top): time of the oldest partial and
+  T tv = T();                 // value of the newest one -- the common step touches no LDS for either
   TT prev_t;
   TT within;
   bool bad = false;
+  bool oob = false;           // internal guard: a row outside the batch (never expected)
   bool overflow = false;
   uint32_t ew = 0xffffffffu, ebits = 0;   // count pass: emit bitmap word being built
   __device__ __forceinline__ void set_within(int64_t w) {
@@ -1008,6 +1052,8 @@ struct Walker {
   }
   __device__ __forceinline__ void push(T x, int64_t tabs, uint32_t r, int64_t pay) {
     L.put(top, x, tabs, r, pay);
+    if (top == head) hts = rel(tabs);
+    tv = x;
     ++top;
   }
   // returns true when this event (inside the unit's chunk) completed partials
@@ -1031,14 +1077,30 @@ struct Walker {
     bad |= t < prev_t;
     prev_t = t;
     // lazy `within` expiry of the oldest partials (StreamPreStateProcessor.isExpired :102-113)
-    while (head != top && t - at(head) > within) ++head;
+    if (head != top && t - hts > within) {
+      ++head;
+      while (head != top) {
+        hts = at(head);
+        if (t - hts <= within) break;
+        ++head;
+      }
+    }
     const uint32_t r = rc.rowf & ROW_MASK;
     const bool live = !is_nan_val<T>(x);
     uint32_t m = 0;
     if ((f & F_CONS) && live) {
       if (a.stack_mode) {
         // monotone stack: the completed partials are exactly a suffix, delivered oldest first
-        while (top != head && cmp_sel<OP, T>(a.op, x, L.gv(top - 1))) { --top; ++m; }
+        if (top != head && cmp_sel<OP, T>(a.op, x, tv)) {
+          --top;
+          ++m;
+          while (top != head) {
+            tv = L.gv(top - 1);
+            if (!cmp_sel<OP, T>(a.op, x, tv)) break;
+            --top;
+            ++m;
+          }
+        }
         if (WRITE && in_chunk && r >= v.nc) {
           for (uint32_t q = 0; q < m; ++q)
             em.put(ofs + q, L.grow(top + q), r, val_bits<T>(L.gv(top + q)), L.gpay(top + q));
@@ -1057,10 +1119,17 @@ struct Walker {
           }
         }
         top = wr;
+        if (head != top) {   // (compaction moved entries: refresh the register copies)
+          hts = at(head);
+          tv = L.gv(top - 1);
+        }
       }
     }
     const bool emitted = m && in_chunk && (r >= v.nc);
-    if (!WRITE && emitted) cnt[r - v.nc] = m;
+    if (!WRITE && emitted) {
+      if (r - v.nc < (uint64_t)v.n) cnt[r - v.nc] = m;
+      else oob = true;
+    }
     if ((f & F_CAND) && live) {
       if (!BIG && top - head == L.cmask + 1) { overflow = true; return emitted; }
       int64_t pv = 0;
@@ -1188,6 +1257,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
     if (!WRITE) mark_overflow();
     return;   // the HBM-list walker redoes this unit
   }
+  if (W.oob) atomicOr(&st->internal, 4u);
   if (W.bad) atomicOr(&st->order_err, 1u);
   if (WRITE && a.carry_out && p1 == se) {
     // rows of this key still inside the window of its last event survive into the next push
@@ -1212,8 +1282,9 @@ __global__ void __launch_bounds__(256) k_units(WalkArgs a, Src<T, N> src, const 
   uint32_t len = 0;
   if (u < a.n_units) {
     const uint32_t c = u / a.K, k = u % a.K;
-    const uint32_t sb = seg_b[k], se = seg_e[k];
+    uint32_t sb = seg_b[k], se = seg_e[k];
     UnitDesc d{0, 0, 0, 0};
+    if (se > a.nt || sb > se) { atomicOr(&st->internal, 1u); sb = se = 0; }
     if (sb < se) {
       uint64_t lo_row = (uint64_t)c * a.R, hi_row = lo_row + a.R;
       uint32_t p0 = c == 0 ? sb : lb_row(src, sb, se, (uint32_t)(lo_row < (uint64_t)a.nt ? lo_row : a.nt), true);
@@ -1253,18 +1324,25 @@ static __global__ void k_rowmap(const uint32_t* __restrict__ wlen, const uint32_
 template <class T, bool N>
 __global__ void __launch_bounds__(256) k_transpose(const WRec<T, N>* __restrict__ srec, const UnitDesc* __restrict__ ud,
                                                    const uint32_t* __restrict__ wrow, const uint32_t* __restrict__ map,
-                                                   uint32_t nq, WRec<T, N>* __restrict__ tile) {
+                                                   uint32_t nq, WRec<T, N>* __restrict__ tile, uint32_t nsrc,
+                                                   uint32_t n_units, WalkStats* __restrict__ st) {
   __shared__ WRec<T, N> t[TROWS][64];
   for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
     const uint32_t W = map[q];
     const uint32_t i0 = q * TROWS - wrow[W];
     for (uint32_t idx = threadIdx.x; idx < TROWS * 64; idx += blockDim.x) {
       const uint32_t l = idx / TROWS, ii = idx % TROWS;
-      const UnitDesc d = ud[W * 64 + l];
+      const uint32_t u = W * 64 + l;   // (the last wave's lanes past n_units have no descriptor)
+      const UnitDesc d = u < n_units ? ud[u] : UnitDesc{0, 0, 0, 0};
       WRec<T, N> r;
       const uint32_t len = (d.p1 > d.p0 && !d.ovf) ? d.p1 - d.w : 0;
-      if (i0 + ii < len) r = srec[d.w + i0 + ii];
-      else { memset(&r, 0, sizeof(r)); }
+      const uint32_t p = d.w + i0 + ii;
+      if (i0 + ii < len && p < nsrc) {
+        r = srec[p];
+      } else {
+        if (i0 + ii < len) atomicOr(&st->internal, 2u);
+        memset(&r, 0, sizeof(r));
+      }
       t[ii][l ^ ii] = r;
     }
     __syncthreads();
@@ -1348,6 +1426,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
     if (WRITE) gather_offs(ba, i + 2 * PF, oa, qa);
     process(bb, i + PF, ob, qb);
   }
+  if (Wk.oob) atomicOr(&st->internal, 4u);
   if (!active) return;
   if (Wk.overflow) {
     if (!WRITE) {
@@ -1749,7 +1828,7 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   if (total) {
     h->kbeg("project");
     hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)), dim3(256), (size_t)256 * wa.stride, st,
-                       wa, v, plan.pp, bv.cols, cc, MatchSink{mrec, 0}, off, (int64_t)total, out);
+                       wa, v, plan.pp, bv.cols, cc, MatchSink{mrec, 0, (uint32_t)total, nullptr}, off, (int64_t)total, out);
     h->kend();
     HIPCHK(hipGetLastError());
   }
@@ -1974,7 +2053,8 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       HIPCHK(rocprim::exclusive_scan(tmp, tb, h2, o2, (uint32_t)0, n2, rocprim::plus<uint32_t>(), st));
       h->kend();
       h->kbeg("part_key");
-      hipLaunchKernelGGL((k_part2<RW>), dim3(pp.ng * pp.nj), dim3(256), lds, st, pp, o1, o2, (const RW*)grec, glk, (RW*)srec);
+      hipLaunchKernelGGL((k_part2<RW>), dim3(pp.ng * pp.nj), dim3(256), lds, st, pp, o1, o2, (const RW*)grec, glk, (RW*)srec,
+                         (uint32_t)nt, pk_flags);
       HIPCHK(hipGetLastError());
       h->kend();
       hipLaunchKernelGGL(k_part_segs, dim3((kb + 255) / 256), dim3(256), 0, st, kb, o2, pp.nj, seg_b, seg_e);
@@ -2083,7 +2163,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   if (wa.carry_out) HIPCHK(hipMemsetAsync(carry_n, 0, sizeof(uint32_t) * (K + 1), st));
   const dim3 wblk(WALK_BLOCK), wgrd((unsigned)((units + WALK_BLOCK - 1) / WALK_BLOCK));
   const uint32_t nw = (uint32_t)((units + 63) / 64);
-  MatchSink ms{nullptr, 0};   // (record pass: set once the match list is allocated)
+  MatchSink ms{nullptr, 0, 0, &wst->internal};   // (record pass: set once the match list is allocated)
   uint32_t* wlen = nullptr;
   uint32_t* wrow = nullptr;
   R* tile = nullptr;
@@ -2107,6 +2187,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (pkf & PK_KEY_RANGE) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+    if (pkf & PK_INTERNAL) throw SgError(SG_EINVAL, "internal: key partition offsets out of range");
     if (pkf & PK_TS_RANGE) return false;   // the push spans more than 2^31 ms: wide records
     if (pkf & PK_PAY_RANGE) {
       // a payload value wider than 32 bits: gather e1's attributes by row instead
@@ -2128,7 +2209,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       HIPCHK(hipGetLastError());
       h->kbeg("tile_transpose");
       hipLaunchKernelGGL((k_transpose<T, N>), dim3(std::min<uint32_t>(nq, 256 * 32)), dim3(256), 0, st, src.srec, ud, wrow,
-                         rmap, nq, tile);
+                         rmap, nq, tile, (uint32_t)nt, wa.n_units, wst);
       HIPCHK(hipGetLastError());
       h->kend();
     }
@@ -2169,6 +2250,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemcpyAsync(&hs, wst, sizeof(WalkStats), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
+  if (hs.internal) throw SgError(SG_EINVAL, "internal: walker guard tripped (" + std::to_string(hs.internal) + ")");
   if (hs.order_err) throw SgError(SG_EORDER, "closed-form kernel requires non-decreasing timestamps per key");
 
   // ---- 5. record pass
@@ -2180,6 +2262,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     wa.out_base = h->out.n;
     // narrow match records when the value type is 4 bytes and every payload fits 32 bits (narrow walker records)
     ms.narrow = (N && sizeof(T) == 4) ? 1 : 0;
+    ms.cap = total;
     ms.rec = h->ws.get("mrec", (ms.narrow ? sizeof(MRec16) : sizeof(MRec)) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
     h->kbeg("walk_record");
@@ -2209,9 +2292,11 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(rocprim::exclusive_scan(nullptr, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
     void* tmp = h->ws.get("carry_scan_tmp", tb, st);
     HIPCHK(rocprim::exclusive_scan(tmp, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
-    uint32_t ncar = 0;
+    uint32_t ncar = 0, guard = 0;
     HIPCHK(hipMemcpyAsync(&ncar, coff + K, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&guard, &wst->internal, sizeof(uint32_t), hipMemcpyDeviceToHost, st));   // record-pass guards
     HIPCHK(hipStreamSynchronize(st));
+    if (guard) throw SgError(SG_EINVAL, "internal: record-pass guard tripped (" + std::to_string(guard) + ")");
     CarrySet& nx = es->carry[es->cur ^ 1];
     nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
     int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
