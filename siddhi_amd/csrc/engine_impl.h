@@ -1416,12 +1416,17 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
       }
     }
   };
+  // Explicit drain at each batch boundary: the batch about to be walked (loaded one batch earlier) and the
+  // stores of the last batch are complete, so the branchy walk of a batch never waits on memory -- without it
+  // the compiler drains every outstanding access (including the prefetch) inside each step.
   load_rows(ba, 0);
   if (WRITE) gather_offs(ba, 0, oa, qa);
   for (uint32_t i = 0; i < rows; i += 2 * PF) {   // rows is a multiple of TROWS = 2 * PF
+    __builtin_amdgcn_s_waitcnt(0);
     load_rows(bb, i + PF);
     if (WRITE) gather_offs(bb, i + PF, ob, qb);
     process(ba, i, oa, qa);
+    __builtin_amdgcn_s_waitcnt(0);
     load_rows(ba, i + 2 * PF);
     if (WRITE) gather_offs(ba, i + 2 * PF, oa, qa);
     process(bb, i + PF, ob, qb);
