@@ -4,5 +4,6 @@ The product path is the HIP engine in siddhi_amd/csrc behind the C-ABI declared 
 include/siddhi_gpu.h; siddhi_amd.runtime mirrors Siddhi's host API (SiddhiManager,
 SiddhiAppRuntime, InputHandler, QueryCallback, StreamCallback) on top of it.
 """
-from .runtime import (Event, InputHandler, QueryCallback, SiddhiAppCreationException,  # noqa: F401
-                      SiddhiAppRuntime, SiddhiManager, StreamCallback)
+from .runtime import (CannotRestoreSiddhiAppStateException, Event, InMemoryPersistenceStore,  # noqa: F401
+                      InputHandler, NoPersistenceStoreException, PersistenceStore, QueryCallback,
+                      SiddhiAppCreationException, SiddhiAppRuntime, SiddhiManager, StreamCallback)

@@ -62,141 +62,7 @@ static const int WALK_BLOCK = 256;
 static const int STACK_CAP = 16;   // default LDS pending-list ring entries per lane (runtime: 16/32/64)
 static const int PF = 8;           // rows prefetched per lane per step
 
-// ---------------------------------------------------------------------------------------------
-// 1. predicate-evaluation pass.  Bitmask layout ("interleaved"): tile g = rows [256g, 256g+256),
-//    word[4g+s] bit l <-> row 256g + 4l + s  (lane l evaluates rows 4l..4l+3 with one 16-B load).
-__device__ __forceinline__ uint32_t mask_bit(const uint64_t* m, uint64_t r) {
-  return (uint32_t)(m[(r >> 8) * 4 + (r & 3)] >> ((r >> 2) & 63)) & 1u;
-}
-
-struct PredArgs {
-  int64_t n;
-  const int32_t* stream;
-  int32_t s_a, s_b;
-  int32_t val_col_a, val_col_b;
-  int32_t prog_a_off, prog_a_len, prog_b_off, prog_b_len;
-  int32_t cons_all;           // B's consumers are every row: skip the second mask
-  // fast path: A's program is `col CMP const` on a 4-byte column read with 16-B loads
-  int32_t simple;             // 0 general VM, 1 simple
-  int32_t s_col, s_type, s_op, s_dom, s_ctype;
-  int64_t s_cbits;
-};
-
-struct RowReader {
-  const SgCols* c;
-  const int32_t* ret_col;
-  int64_t row;
-  __device__ SgVal read(int, int, int slot, int type) { return sg_read_col(*c, ret_col[slot], type, row); }
-};
-
-__device__ __forceinline__ bool eval_row(const PredArgs& a, const SgCols& cols, const DevDesc* dd, int64_t i,
-                                         bool side_b) {
-  int s = a.stream ? a.stream[i] : 0;
-  int want = side_b ? a.s_b : a.s_a;
-  if (s != want) return false;
-  int vc = side_b ? a.val_col_b : a.val_col_a;
-  if (cols.nul[vc] && cols.nul[vc][i]) return false;
-  RowReader rd{&cols, dd->ret_col, i};
-  return side_b ? sg_eval(dd->code + a.prog_b_off, a.prog_b_len, rd)
-                : sg_eval(dd->code + a.prog_a_off, a.prog_a_len, rd);
-}
-
-// general: any program, scalar loads (rows 4l+s of the tile)
-static __global__ void __launch_bounds__(256) k_pred(PredArgs a, SgCols cols, const DevDesc* __restrict__ dd,
-                                              uint64_t* __restrict__ cand_m, uint64_t* __restrict__ cons_m) {
-  const int lane = threadIdx.x & 63;
-  const int64_t ntiles = (a.n + 255) >> 8;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t g = wave; g < ntiles; g += nwaves) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      int64_t i = g * 256 + lane * 4 + s;
-      bool ca = false, co = false;
-      if (i < a.n) {
-        ca = eval_row(a, cols, dd, i, false);
-        if (!a.cons_all) co = eval_row(a, cols, dd, i, true);
-      }
-      uint64_t ma = __ballot(ca);
-      uint64_t mb = __ballot(co);
-      if (lane == s) {
-        cand_m[g * 4 + s] = ma;
-        if (!a.cons_all) cons_m[g * 4 + s] = mb;
-      }
-    }
-  }
-}
-
-// simple: A = `col CMP const` on a 4-byte column, stream column absent, B consumers = all rows.
-// The constant is pre-converted to the compare domain (f32 / f64 / i64, ExpressionParser's promotion);
-// the operator is a template parameter.  One-shot grid: each wave owns 4 consecutive 256-row tiles
-// (4 contiguous 1 KB wave loads in flight), loaded non-temporally -- the column is read exactly once
-// and must not displace the walker's working set from L2 / MALL (measured: 3.3 -> 6.2 TB/s,
-// exp/predbench.hip).  The 4 tile words are stored by lanes 0..3 in one 32-B write.
-template <int OP, class D>
-__device__ __forceinline__ bool cmp_op(D a, D b) {
-  if (OP == 0) return a == b;
-  if (OP == 1) return a != b;
-  if (OP == 2) return a > b;
-  if (OP == 3) return a >= b;
-  if (OP == 4) return a < b;
-  return a <= b;
-}
-constexpr int PRED_TILES_PER_WAVE = 4;
-template <class V, class D, int OP>
-__global__ void __launch_bounds__(256) k_pred_simple(int64_t n, D c, const V* __restrict__ col,
-                                                     const uint8_t* __restrict__ nul, uint64_t* __restrict__ cand_m) {
-  constexpr int U = PRED_TILES_PER_WAVE;
-  const int lane = threadIdx.x & 63;
-  const int64_t ntiles = (n + 255) >> 8;
-  const int64_t g0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * U;
-  typedef V V4 __attribute__((ext_vector_type(4)));
-  V4 x[U];
-  if (g0 + U <= (n >> 8)) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load((const V4*)(col + (g0 + u) * 256 + lane * 4));
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = (g0 + u) * 256 + lane * 4;
-      x[u].x = i + 0 < n ? col[i + 0] : V(0);
-      x[u].y = i + 1 < n ? col[i + 1] : V(0);
-      x[u].z = i + 2 < n ? col[i + 2] : V(0);
-      x[u].w = i + 3 < n ? col[i + 3] : V(0);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t g = g0 + u;
-    if (g >= ntiles) break;
-    const int64_t i = g * 256 + lane * 4;
-    const V xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-    uint64_t mine = 0;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bool ok = (i + s < n) && cmp_op<OP, D>((D)xs[s], c);
-      if (nul && ok) ok = !nul[i + s];
-      const uint64_t m = __ballot(ok);
-      if (lane == s) mine = m;
-    }
-    if (lane < 4) cand_m[g * 4 + lane] = mine;
-  }
-}
-template <class V, class D>
-static void launch_pred_simple(int op, int64_t n, D c, const V* col, const uint8_t* nul, uint64_t* cand_m,
-                               hipStream_t st) {
-  const int64_t ntiles = (n + 255) >> 8;
-  const int64_t waves = (ntiles + PRED_TILES_PER_WAVE - 1) / PRED_TILES_PER_WAVE;
-  const dim3 grd((unsigned)std::max<int64_t>(1, (waves + 3) / 4)), blk(256);
-  switch (op) {
-    case 0: hipLaunchKernelGGL((k_pred_simple<V, D, 0>), grd, blk, 0, st, n, c, col, nul, cand_m); break;
-    case 1: hipLaunchKernelGGL((k_pred_simple<V, D, 1>), grd, blk, 0, st, n, c, col, nul, cand_m); break;
-    case 2: hipLaunchKernelGGL((k_pred_simple<V, D, 2>), grd, blk, 0, st, n, c, col, nul, cand_m); break;
-    case 3: hipLaunchKernelGGL((k_pred_simple<V, D, 3>), grd, blk, 0, st, n, c, col, nul, cand_m); break;
-    case 4: hipLaunchKernelGGL((k_pred_simple<V, D, 4>), grd, blk, 0, st, n, c, col, nul, cand_m); break;
-    default: hipLaunchKernelGGL((k_pred_simple<V, D, 5>), grd, blk, 0, st, n, c, col, nul, cand_m); break;
-  }
-}
+#include "pred.h"
 
 // ---------------------------------------------------------------------------------------------
 // virtual row domain: [0, nc) carried rows of earlier pushes, [nc, nc + n) this batch
@@ -1553,41 +1419,6 @@ static int pick_chunks(uint32_t K, int64_t nt, int entry_bytes, int cap, int64_t
   return (int)std::min<int64_t>(C, 1 << 16);
 }
 
-// `col CMP const` on a 4-byte column?  (the predicate pass then streams it with 16-B loads)
-static bool simple_prog(const sg_nfa_desc& d, int off, int len, PredArgs& pa) {
-  if (len != 11) return false;   // VAR(5 words) CONST(3) CMP(3)
-  const int64_t* c = d.code + off;
-  if (c[0] != SG_OP_VAR || c[5] != SG_OP_CONST || c[8] != SG_OP_CMP) return false;
-  int slot = (int)c[3], type = (int)c[4];
-  if (type != SG_T_FLOAT && type != SG_T_INT) return false;
-  pa.s_col = d.ret_col[slot];
-  pa.s_type = type;
-  pa.s_ctype = (int)c[6];
-  pa.s_cbits = c[7];
-  pa.s_op = (int)c[9];
-  pa.s_dom = (int)c[10];
-  return true;
-}
-
-static SgVal sg_val_from_bits_host(int64_t bits, int type) {
-  SgVal v;
-  v.type = type;
-  v.null = 0;
-  v.i = 0;
-  v.d = 0.0;
-  if (type == SG_T_FLOAT) {
-    uint32_t u = (uint32_t)bits;
-    float f;
-    memcpy(&f, &u, 4);
-    v.d = f;
-  } else if (type == SG_T_DOUBLE) {
-    memcpy(&v.d, &bits, 8);
-  } else {
-    v.i = bits;
-  }
-  return v;
-}
-
 struct PushPlan {
   ProjPlan pp;
   int pcol = -1;              // e1 payload column carried in the pending list
@@ -1926,44 +1757,8 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   uint64_t* cons_m = pa.cons_all ? nullptr : (uint64_t*)h->ws.get("cons_m", sizeof(uint64_t) * 4 * (ntiles + 1), st);
   h->mark(0);
   h->kbeg("pred");
-  {
-    PredArgs sp = pa;
-    bool simple = pa.cons_all && !bv.stream && pa.s_a == 0 && simple_prog(d, pa.prog_a_off, pa.prog_a_len, sp) &&
-                  sp.s_col == val_col_a && (((uintptr_t)bv.cols.col[sp.s_col]) & 15) == 0;
-    int64_t waves = std::min<int64_t>((ntiles + 3) / 4, 256 * 32);
-    dim3 grd((unsigned)std::max<int64_t>(1, (waves + 3) / 4)), blk(256);
-    if (simple) {
-      // constant in the compare domain (sg_cmp: 0 integral, 1 f32, 2 f64)
-      SgVal cv = sg_val_from_bits_host(sp.s_cbits, sp.s_ctype);
-      const void* colp = bv.cols.col[sp.s_col];
-      const uint8_t* nul = bv.cols.nul[sp.s_col];
-      if (sp.s_dom == 1) {
-        float c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? (float)cv.d : (float)cv.i;
-        if (sp.s_type == SG_T_FLOAT)
-          launch_pred_simple<float, float>(sp.s_op, n, c, (const float*)colp, nul, cand_m, st);
-        else
-          launch_pred_simple<int32_t, float>(sp.s_op, n, c, (const int32_t*)colp, nul, cand_m, st);
-      } else if (sp.s_dom == 2) {
-        double c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? cv.d : (double)cv.i;
-        if (sp.s_type == SG_T_FLOAT)
-          launch_pred_simple<float, double>(sp.s_op, n, c, (const float*)colp, nul, cand_m, st);
-        else
-          launch_pred_simple<int32_t, double>(sp.s_op, n, c, (const int32_t*)colp, nul, cand_m, st);
-      } else {
-        int64_t c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? (int64_t)cv.d : cv.i;
-        if (sp.s_type == SG_T_FLOAT)
-          simple = false;   // integral domain on a float column: leave it to the VM's conversions
-        else
-          launch_pred_simple<int32_t, int64_t>(sp.s_op, n, c, (const int32_t*)colp, nul, cand_m, st);
-      }
-    }
-    if (!simple) {
-      int64_t w2 = std::min<int64_t>(ntiles, 256 * 16);
-      hipLaunchKernelGGL(k_pred, dim3((unsigned)std::max<int64_t>(1, (w2 + 3) / 4)), blk, 0, st, pa, bv.cols,
-                         h->ddesc, cand_m, cons_m);
-    }
-    HIPCHK(hipGetLastError());
-  }
+  launch_pred(d, pa, bv.stream, bv.cols, h->ddesc, cand_m, cons_m, st);
+  HIPCHK(hipGetLastError());
   h->kend();
   h->mark(1);
 

@@ -78,6 +78,9 @@ struct KeyMachine {
   int64_t now;          // playback clock value (TimestampGeneratorImpl.currentTime)
   int failed;
   int silent;           // replaying a unit's horizon: state only, no emission
+  // condition bits of the states whose filter reads only the arriving event (predicate-evaluation pass,
+  // pred.h; row = trig_local), or null: evaluate the program here
+  const uint64_t* const* lbits = nullptr;
 
   // ---------------------------------------------------------------- raw accessors
   SG_HD int32_t* hdr() { return a; }
@@ -292,6 +295,10 @@ struct KeyMachine {
     }
   };
   SG_HD bool filter(int s, int p) {
+    if (lbits && lbits[s]) {   // (pred.h interleaved layout)
+      const uint64_t r = (uint64_t)trig_local;
+      return ((lbits[s][(r >> 8) * 4 + (r & 3)] >> ((r >> 2) & 63)) & 1u) != 0;
+    }
     PReader rd{this, p};
     return sg_eval(d->code + st(s).prog_off, st(s).prog_len, rd);
   }

@@ -24,6 +24,7 @@
 #include "sg_device.h"
 #include "sg_engine.h"
 #include "interp.h"
+#include "pred.h"
 
 #define HIPCHK(x)                                                                                   \
   do {                                                                                              \
@@ -129,6 +130,31 @@ struct DevRowsTs : DevRows {
   __device__ int64_t ts(int64_t r) { return DevRows::ts[r]; }
 };
 
+// The descriptor (programs, state tables: ~9.6 KB) and the arena geometry are read hundreds of times per event;
+// each workgroup copies them into LDS once so those reads are LDS hits instead of L2 round trips.
+struct NfaLds {
+  DevDesc d;
+  SgGeo g;
+  const uint64_t* lbits[SG_MAX_STATES];
+  int32_t any_bits;
+};
+__device__ __forceinline__ void nfa_stage_desc(NfaLds& L, const DevDesc* __restrict__ dd, const SgGeo* __restrict__ geo,
+                                               const uint64_t* const* lbits) {
+  if (threadIdx.x < SG_MAX_STATES) L.lbits[threadIdx.x] = lbits[threadIdx.x];
+  if (threadIdx.x == 0) {
+    int any = 0;
+    for (int s = 0; s < SG_MAX_STATES; ++s) any |= lbits[s] != nullptr;
+    L.any_bits = any;
+  }
+  const uint32_t* src = (const uint32_t*)dd;
+  uint32_t* dst = (uint32_t*)&L.d;
+  for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) dst[i] = src[i];
+  const uint32_t* gs = (const uint32_t*)geo;
+  uint32_t* gd = (uint32_t*)&L.g;
+  for (uint32_t i = threadIdx.x; i < sizeof(SgGeo) / 4; i += blockDim.x) gd[i] = gs[i];
+  __syncthreads();
+}
+
 struct NfaArgs {
   int64_t n;
   uint64_t base_index;
@@ -141,11 +167,16 @@ struct NfaArgs {
   const int64_t* ts;
   const int32_t* stream;
   const uint64_t* index;
+  const uint64_t* lbits[SG_MAX_STATES];   // predicate-pass condition bits per state (null: none)
 };
 
 __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDesc* __restrict__ dd,
                                             const SgGeo* __restrict__ geo, int32_t* __restrict__ arena,
                                             SgEmitSink sink, int32_t* __restrict__ fail_code) {
+  __shared__ NfaLds L;
+  nfa_stage_desc(L, dd, geo, a.lbits);
+  dd = &L.d;
+  geo = &L.g;
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= a.nkeys) return;
   int32_t* ar = arena + k * geo->key_words;
@@ -165,6 +196,7 @@ __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDes
   m.group = 0;
   m.now = 0;
   m.silent = 0;
+  m.lbits = L.any_bits ? L.lbits : nullptr;
   m.failed = ar[K_OVERFLOW];
   if (m.failed) { atomicCAS(fail_code, 0, m.failed); return; }
   DevRowsTs rows;
@@ -213,6 +245,10 @@ __global__ void k_unit_map(int64_t nkeys, const uint32_t* __restrict__ uoff, uin
 __global__ void __launch_bounds__(64) k_nfa_units(NfaArgs a, UnitArgs ua, SgCols cols, const DevDesc* __restrict__ dd,
                                                   const SgGeo* __restrict__ geo, int32_t* __restrict__ arena,
                                                   SgEmitSink sink, int32_t* __restrict__ fail_code) {
+  __shared__ NfaLds L;
+  nfa_stage_desc(L, dd, geo, a.lbits);
+  dd = &L.d;
+  geo = &L.g;
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= ua.n_units) return;
   const uint32_t k = ua.umap[u];
@@ -251,6 +287,7 @@ __global__ void __launch_bounds__(64) k_nfa_units(NfaArgs a, UnitArgs ua, SgCols
   m.group = 0;
   m.now = 0;
   m.silent = 0;
+  m.lbits = L.any_bits ? L.lbits : nullptr;
   m.failed = ar[K_OVERFLOW];
   if (m.failed) { atomicCAS(fail_code, 0, m.failed); return; }
   DevRowsTs rows;
@@ -411,6 +448,33 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   na.ts = bv.ts;
   na.stream = bv.stream;
   na.index = bv.index;
+  // ---- predicate-evaluation pass: condition bits of every state whose filter reads only the arriving event
+  for (int s = 0; s < SG_MAX_STATES; ++s) na.lbits[s] = nullptr;
+  {
+    const int64_t ntiles = (n + 255) / 256;
+    bool any = false;
+    for (int s = 0; s < d.n_states; ++s) {
+      const sg_state_desc& x = d.states[s];
+      if (!x.local || x.prog_len <= 0) continue;
+      if (!any) h->kbeg("pred");
+      any = true;
+      PredArgs pa;
+      memset(&pa, 0, sizeof(pa));
+      pa.n = n;
+      pa.stream = bv.stream;
+      pa.s_a = x.stream;
+      pa.prog_a_off = x.prog_off;
+      pa.prog_a_len = x.prog_len;
+      pa.val_col_a = -1;
+      pa.val_col_b = -1;
+      pa.cons_all = 1;
+      uint64_t* bits = (uint64_t*)h->ws.get("g_lbits" + std::to_string(s), sizeof(uint64_t) * 4 * (ntiles + 1), st);
+      launch_pred(d, pa, bv.stream, bv.cols, h->ddesc, bits, nullptr, st);
+      HIPCHK(hipGetLastError());
+      na.lbits[s] = bits;
+    }
+    if (any) h->kend();
+  }
   SgEmitSink sink;
   sink.buf = ebuf;
   sink.cap = cap;

@@ -62,6 +62,64 @@ class StreamCallback:
         pass
 
 
+class NoPersistenceStoreException(Exception):
+    """persist() / restoreLastRevision() without a store (C/util/snapshot/SnapshotService.java:530, :546)."""
+
+
+class CannotRestoreSiddhiAppStateException(Exception):
+    """A revision that does not restore into this app (C/SiddhiAppRuntime.java:625-661)."""
+
+
+class PersistenceStore:
+    """C/util/persistence/PersistenceStore.java: revisions of an app's state blobs."""
+
+    def save(self, siddhi_app_id: str, revision: str, data: bytes):
+        raise NotImplementedError
+
+    def load(self, siddhi_app_id: str, revision: str):
+        raise NotImplementedError
+
+    def getLastRevision(self, siddhi_app_id: str):
+        raise NotImplementedError
+
+    def clearAllRevisions(self, siddhi_app_id: str):
+        raise NotImplementedError
+
+
+class InMemoryPersistenceStore(PersistenceStore):
+    """C/util/persistence/InMemoryPersistenceStore.java:30-90: revisions per app in insertion order, a revision
+    saved twice in a row listed once."""
+
+    def __init__(self):
+        self.data: Dict[str, bytes] = {}
+        self.revisions: Dict[str, List[str]] = {}
+
+    def save(self, siddhi_app_id, revision, data):
+        self.data[revision] = bytes(data)
+        lst = self.revisions.setdefault(siddhi_app_id, [])
+        if not lst or lst[-1] != revision:
+            lst.append(revision)
+
+    def load(self, siddhi_app_id, revision):
+        return self.data.get(revision)
+
+    def getLastRevision(self, siddhi_app_id):
+        lst = self.revisions.get(siddhi_app_id)
+        return lst[-1] if lst else None
+
+    def clearAllRevisions(self, siddhi_app_id):
+        for r in self.revisions.pop(siddhi_app_id, []):
+            self.data.pop(r, None)
+
+
+class PersistenceReference:
+    def __init__(self, revision: str):
+        self.revision = revision
+
+    def getRevision(self):
+        return self.revision
+
+
 class SiddhiAppCreationException(Exception):
     pass
 
@@ -198,6 +256,7 @@ class SiddhiAppRuntime:
         self._rows: List[tuple] = []
         self.next_index = 0
         self.started = False
+        self.persistence_store: Optional[PersistenceStore] = None
 
     # -- API
     def getInputHandler(self, stream_id: str) -> InputHandler:
@@ -224,6 +283,42 @@ class SiddhiAppRuntime:
 
     # -- persistence (SiddhiAppRuntime.snapshot / restore, C/SiddhiAppRuntime.java:613-635)
     _SNAP_MAGIC = b"SDAPSNP1"
+
+    def getName(self):
+        return self.app.name or "SiddhiApp"
+
+    def persist(self) -> PersistenceReference:
+        """SiddhiAppRuntime.persist (C/SiddhiAppRuntime.java:595-611): snapshot() saved to the manager's store
+        under revision "<millis>_<app name>" (SnapshotService.persist)."""
+        if self.persistence_store is None:
+            raise NoPersistenceStoreException(f"No persistence store assigned for siddhi app {self.getName()}")
+        rev = f"{int(time.time() * 1000)}_{self.getName()}"
+        last = self.persistence_store.getLastRevision(self.getName())
+        if last is not None and last >= rev:   # (revisions stay ordered within one millisecond)
+            rev = f"{int(last.split('_', 1)[0]) + 1}_{self.getName()}"
+        self.persistence_store.save(self.getName(), rev, self.snapshot())
+        return PersistenceReference(rev)
+
+    def restoreRevision(self, revision: str):
+        """C/SiddhiAppRuntime.java:637-647."""
+        if self.persistence_store is None:
+            raise NoPersistenceStoreException(f"No persistence store assigned for siddhi app {self.getName()}")
+        blob = self.persistence_store.load(self.getName(), revision)
+        if blob is None:
+            raise CannotRestoreSiddhiAppStateException(f"no revision {revision} of {self.getName()}")
+        try:
+            self.restore(blob)
+        except Exception as e:
+            raise CannotRestoreSiddhiAppStateException(str(e)) from e
+
+    def restoreLastRevision(self):
+        """C/SiddhiAppRuntime.java:649-661: the last saved revision, if any (returns it, or None)."""
+        if self.persistence_store is None:
+            raise NoPersistenceStoreException(f"No persistence store assigned for siddhi app {self.getName()}")
+        rev = self.persistence_store.getLastRevision(self.getName())
+        if rev is not None:
+            self.restoreRevision(rev)
+        return rev
 
     def snapshot(self) -> bytes:
         """Persist the app's pattern state between events: every query engine's per-key state plus the host
@@ -443,13 +538,19 @@ class SiddhiManager:
 
     def __init__(self, engine=None):
         self.engine = engine
+        self.persistence_store = None
+
+    def setPersistenceStore(self, store: PersistenceStore):
+        self.persistence_store = store
 
     def createSiddhiAppRuntime(self, text: str) -> SiddhiAppRuntime:
         factory = self.engine
         if factory is None:
             from ._native import GpuEngine
             factory = GpuEngine
-        return SiddhiAppRuntime(text, factory)
+        rt = SiddhiAppRuntime(text, factory)
+        rt.persistence_store = self.persistence_store
+        return rt
 
     def shutdown(self):
         pass
