@@ -170,7 +170,9 @@ typedef struct sg_options {
                                no_carry handles never split. */
   int32_t partition_sort;   /* closed form, partitioned: 0 = LDS-staged counting partition when key_bound <= 65536
                                (rocPRIM radix sort above), 1 = always the radix sort (testing both paths) */
-  int32_t reserved[1];
+  int32_t partial_lanes;    /* general engine, patterns whose partial matches never interact (every e1 -> ... within T
+                               over stream / count / logical states of one stream): 0 = one GPU lane per partial
+                               match while timestamps never decrease, -1 = always the per-key machine (testing) */
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)

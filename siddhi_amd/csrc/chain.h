@@ -1,0 +1,279 @@
+// chain.h -- per-partial pattern machine (SG route "partial lanes") for MI355X.
+//
+// For a PATTERN whose only `every` re-arms its single start state (`every e1=S[local] -> ... within T`, every state on
+// one stream, no absence), the partial matches started by different e1 rows never interact: each one is created by
+// the start state's `every` clone (StreamPostStateProcessor.process -> addEveryState, C/query/input/stream/state/
+// StreamPostStateProcessor.java:53-72, StreamPreStateProcessor.addEveryState :219-227), is handed from state to state
+// by the object itself (addState :203-216), and every decision the Pre/Post processors take on it reads only its own
+// slots (StreamPreStateProcessor.processAndReturn :292-337, isExpired :102-113, CountPreStateProcessor.processAndReturn
+// :53-93, LogicalPreStateProcessor.processAndReturn :132-176).  So one GPU lane can run one partial from its e1 row
+// forward, alone, over the rows of its key, instead of one lane walking every pending partial of the key per event.
+//
+// What other partials contribute is only ORDER: matches of one event are delivered state by state in the receiver's
+// visit order (MultiProcessStreamReceiver.receive :271-309) and, within a state, in pending-list order.  A pending list
+// is the survivors of earlier rows followed by the newAndEvery list moved in by updateState (:281-289), and
+// newAndEvery is filled in the order addState is called -- which is the order the predecessor state walked ITS list
+// at that row.  Hence a partial's position in any list is the lexicographic order of its insertion history read
+// backwards: (row and visit slot of the latest addState, then of the one before, ... down to its e1 row).  Each lane
+// records that history (`hist`) and the match records carry it as a tie-break key; a stable radix sort by
+// (trigger row, visit slot, history) restores the reference's delivery order exactly.
+//
+// State kept per lane (registers / scratch): each state's slot (row) or count chain, list membership bits for the
+// pending (l0) and newAndEvery (l1) lists, the partial's timestamp, the per-state processor flags and the history.
+// Every method restates the KeyMachine method of interp.h with the same name (which cites its reference method).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/siddhi_gpu.h"
+
+#ifndef SG_HD
+#define SG_HD __host__ __device__
+#endif
+
+#define PP_MAX_CHAIN 16   // count-chain entries over all count states of the query
+#define PP_MAX_HIST 4     // insertions recorded (elements after the start state)
+
+struct SgPpRule {
+  int32_t ok;
+  int32_t start;                      // the start state
+  int32_t recv;                       // the single (multi) receiver
+  int32_t n_hist;                     // tie components of an emission (= elements after the start)
+  int32_t coff[SG_MAX_STATES];        // count state -> offset of its chain in PpLane.chain
+  int32_t visit_rank[SG_MAX_STATES];  // state -> its slot in the receiver's visit order
+};
+
+// Which queries may run as partial lanes (checked at lowering-independent level, on the flat descriptor).
+SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
+  SgPpRule r;
+  r.ok = 0;
+  r.start = -1;
+  r.recv = -1;
+  r.n_hist = 0;
+  for (int s = 0; s < SG_MAX_STATES; ++s) { r.coff[s] = -1; r.visit_rank[s] = -1; }
+  if (d.type != 0 || d.within < 0 || d.n_states < 2 || d.n_sched != 0) return r;
+  int nrecv = 0;
+  for (int s = 0; s < SG_MAX_STREAMS; ++s)
+    if (d.recv_of_stream[s] >= 0) { ++nrecv; r.recv = d.recv_of_stream[s]; }
+  if (nrecv != 1) return r;
+  const sg_receiver_desc& rv = d.receivers[r.recv];
+  if (!rv.multi || rv.n != d.n_states || !rv.selector) return r;
+  for (int k = 0; k < rv.n; ++k) r.visit_rank[rv.pres[rv.n - 1 - k]] = k;
+  int starts = 0, chain = 0, elems = 0;
+  for (int s = 0; s < d.n_states; ++s) {
+    const sg_state_desc& x = d.states[s];
+    if (r.visit_rank[s] < 0) return r;
+    if (x.kind != SG_K_STREAM && x.kind != SG_K_COUNT && x.kind != SG_K_LOGICAL) return r;
+    if (x.callback >= 0) return r;
+    if (x.is_start) {
+      ++starts;
+      r.start = s;
+      if (x.kind != SG_K_STREAM || x.next_every != s || !x.local || x.has_selector || x.next_state < 0) return r;
+      continue;
+    }
+    if (x.next_every >= 0 || x.within_every >= 0 || x.this_last != s) return r;
+    if (x.kind == SG_K_COUNT) {
+      if (x.min_count < 1 || x.max_count < x.min_count || x.max_count > 8 || x.has_selector) return r;
+      if (x.next_state >= 0 && d.states[x.next_state].kind == SG_K_COUNT) return r;
+      r.coff[s] = chain;
+      chain += x.max_count;
+    }
+    if (x.kind == SG_K_LOGICAL && (x.partner < 0 || d.states[x.partner].kind != SG_K_LOGICAL)) return r;
+    if (x.kind != SG_K_LOGICAL || s < x.partner) ++elems;
+  }
+  if (starts != 1 || d.n_start != 1 || chain > PP_MAX_CHAIN || elems > PP_MAX_HIST) return r;
+  r.n_hist = elems;
+  r.ok = 1;
+  return r;
+}
+
+// Tie key of an emission: bit 63 set for partial lanes (0: the carried-state machine, ordered by its own sequence),
+// then the history newest first, 31 bits per component, two components per word.
+SG_HD inline uint32_t pp_tkey(int64_t row, int rank) { return (uint32_t)(((uint64_t)row << 4) | (uint32_t)(rank & 15)); }
+
+// Src interface: int64_t ts(int64_t row); SgVal read(int64_t row, int ret_slot, int type);
+//                int lbit(int state, int64_t row) -> 0/1, or -1 when the state's filter must be evaluated.
+template <class Src>
+struct PpLane {
+  const sg_nfa_desc* d;
+  const SgPpRule* ru;
+  Src* src;
+  int32_t slot[SG_MAX_STATES];
+  int32_t clen[SG_MAX_STATES];
+  int32_t chain[PP_MAX_CHAIN];
+  uint32_t l0, l1;
+  uint32_t f_changed, f_returned, f_success;
+  int64_t pts;
+  int64_t e1_ts;
+  uint32_t hist[PP_MAX_HIST];
+  int32_t nh;
+  int32_t overflow;
+  // current row
+  int64_t cur_row;
+  int cur_rank;
+
+  SG_HD const sg_state_desc& st(int s) const { return d->states[s]; }
+  SG_HD static uint32_t bit(int s) { return 1u << s; }
+
+  // does the start state's armed partial accept this row (its filter, evaluated with e1 bound to the row)?
+  SG_HD bool start_ok(int64_t row) {
+    for (int s = 0; s < SG_MAX_STATES; ++s) { slot[s] = -1; clen[s] = 0; }
+    slot[ru->start] = (int32_t)row;
+    cur_row = row;
+    return filter(ru->start);
+  }
+  SG_HD void start(int64_t row) {   // the armed start partial takes e1 = row (process_and_return of the start state)
+    for (int s = 0; s < SG_MAX_STATES; ++s) { slot[s] = -1; clen[s] = 0; }
+    l0 = l1 = 0;
+    f_changed = f_returned = f_success = 0;
+    nh = 0;
+    overflow = 0;
+    cur_row = row;
+    cur_rank = ru->visit_rank[ru->start];
+    slot[ru->start] = (int32_t)row;
+    e1_ts = src->ts(row);
+    stream_post(ru->start);   // the `every` clone it also makes stays behind in the start state's lists
+  }
+
+  // ---- event access (KeyMachine::get_event): row of (state, index in chain) or -1
+  SG_HD int64_t get_event(int s, int idx) {
+    if (st(s).kind != SG_K_COUNT) {
+      if (slot[s] < 0) return -1;
+      return (idx == 0 || idx == -1) ? slot[s] : -1;
+    }
+    const int n = clen[s];
+    if (n == 0) return -1;
+    const int32_t* c = chain + ru->coff[s];
+    int k;
+    if (idx >= 0) k = idx;
+    else if (idx == -1) k = n - 1;
+    else if (idx == -2) k = n - 2;
+    else k = n + idx;
+    if (k < 0 || k >= n) return -1;
+    return c[k];
+  }
+  SG_HD int64_t slot_ts(int s) {
+    int64_t r = st(s).kind == SG_K_COUNT ? (clen[s] ? chain[ru->coff[s]] : -1) : slot[s];
+    return src->ts(r);
+  }
+  struct Reader {
+    PpLane* m;
+    SG_HD SgVal read(int s, int idx, int slotk, int type) {
+      const int64_t r = m->get_event(s, idx);
+      if (r < 0) {
+        SgVal v;
+        v.type = type;
+        v.i = 0;
+        v.d = 0;
+        v.null = 1;
+        return v;
+      }
+      return m->src->read(r, slotk, type);
+    }
+  };
+  SG_HD bool filter(int s) {
+    const int b = src->lbit(s, cur_row);
+    if (b >= 0) return b != 0;
+    Reader rd{this};
+    return sg_eval(d->code + st(s).prog_off, st(s).prog_len, rd);
+  }
+
+  // ---- posts
+  SG_HD void stream_post(int s) {
+    const sg_state_desc& x = st(s);
+    f_changed |= bit(s);
+    pts = slot_ts(s);
+    if (x.has_selector) f_returned |= bit(s);
+    if (x.next_state >= 0) add_state(x.next_state);
+  }
+  SG_HD void count_post(int s) {
+    const sg_state_desc& x = st(s);
+    const int n = clen[s];
+    f_success |= bit(s);
+    pts = src->ts(chain[ru->coff[s] + n - 1]);
+    if (n >= x.min_count) {
+      if (n == x.min_count && x.next_state >= 0) add_state(x.next_state);   // count_min_reached (no selector)
+      if (n == x.max_count) f_changed |= bit(s);
+    }
+  }
+  SG_HD void logical_post(int s) {
+    const sg_state_desc& x = st(s);
+    if (x.logical_type == 0) {
+      if (slot[x.partner] >= 0) stream_post(s);
+      else f_changed |= bit(s);
+    } else {
+      stream_post(s);
+    }
+  }
+  SG_HD void add_state(int s) {
+    const sg_state_desc& x = st(s);
+    if (nh < PP_MAX_HIST) hist[nh++] = pp_tkey(cur_row, cur_rank);
+    else overflow = 1;
+    l1 |= bit(s);
+    if (x.kind == SG_K_LOGICAL) l1 |= bit(x.partner);
+  }
+  SG_HD bool is_expired(int64_t t) {
+    int64_t dt = e1_ts - t;
+    if (dt < 0) dt = -dt;
+    return dt > d->within;
+  }
+
+  // ---- one row: updateState of every state, then the states in visit order (KeyMachine::receive)
+  // Returns the visit slot that emitted (one emission per row at most: the partial leaves the emitting state), or -1.
+  SG_HD int step(int64_t row) {
+    cur_row = row;
+    const sg_receiver_desc& rv = d->receivers[ru->recv];
+    const uint32_t moved = l1;
+    l0 |= moved;
+    l1 = 0;
+    const int64_t t = src->ts(row);
+    int emitted = -1;
+    for (int k = 0; k < rv.n; ++k) {
+      const int s = rv.pres[rv.n - 1 - k];
+      if (!(l0 & bit(s)) || s == ru->start) continue;
+      cur_rank = k;
+      const sg_state_desc& x = st(s);
+      bool remove = false;
+      if (x.kind == SG_K_COUNT) {
+        if ((s + 1 < d->n_states && get_any(s + 1)) || (s + 2 < d->n_states && get_any(s + 2))) {
+          l0 &= ~bit(s);
+          continue;
+        }
+        if (clen[s] >= st(s).max_count) { overflow = 1; return -1; }
+        chain[ru->coff[s] + clen[s]++] = (int32_t)row;
+        f_success &= ~bit(s);
+        f_changed &= ~bit(s);
+        if (filter(s)) count_post(s);
+        if (f_changed & bit(s)) remove = true;
+        if (!(f_success & bit(s))) --clen[s];
+      } else {
+        if (is_expired(t)) { l0 &= ~bit(s); continue; }
+        if (x.kind == SG_K_LOGICAL && x.logical_type == 1 && slot[x.partner] >= 0) { l0 &= ~bit(s); continue; }
+        slot[s] = (int32_t)row;
+        f_changed &= ~bit(s);
+        if (filter(s)) {
+          if (x.kind == SG_K_LOGICAL) logical_post(s);
+          else stream_post(s);
+        }
+        if (f_returned & bit(s)) {
+          f_returned &= ~bit(s);
+          if (emitted < 0) emitted = k;
+          else overflow = 1;
+        }
+        if (f_changed & bit(s)) remove = true;
+        else slot[s] = -1;
+      }
+      if (remove) l0 &= ~bit(s);
+    }
+    return emitted;
+  }
+  SG_HD bool get_any(int s) { return st(s).kind == SG_K_COUNT ? clen[s] > 0 : slot[s] >= 0; }
+  SG_HD bool dead() const { return (l0 | l1) == 0; }
+
+  // tie words of an emission (bit 63: partial lane)
+  SG_HD void tie(uint64_t& hi, uint64_t& lo) const {
+    uint32_t c[PP_MAX_HIST] = {0, 0, 0, 0};
+    for (int i = 0; i < nh; ++i) c[i] = hist[nh - 1 - i] & 0x7FFFFFFFu;
+    hi = (1ull << 63) | ((uint64_t)c[0] << 31) | c[1];
+    lo = ((uint64_t)c[2] << 31) | c[3];
+  }
+};

@@ -1012,6 +1012,13 @@ SG_HD inline SgChunkRule sg_chunk_rule(const sg_nfa_desc& d) {
     if (d.within < 0) return r;
     if (!d.partitioned)
       for (int s = 0; s < d.n_states; ++s) if (d.states[s].within_every >= 0) return r;
+    // CountPreStateProcessor.processAndReturn never checks `within` (CountPreStateProcessor.java:53-93): a count
+    // state that emits itself, or hands over to another count state, keeps advancing an expired partial
+    for (int s = 0; s < d.n_states; ++s) {
+      const sg_state_desc& x = d.states[s];
+      if (x.kind != SG_K_COUNT) continue;
+      if (x.has_selector || (x.next_state >= 0 && d.states[x.next_state].kind == SG_K_COUNT)) return r;
+    }
     r.kind = 1;
     r.within = d.within;
     return r;

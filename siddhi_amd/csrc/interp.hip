@@ -38,6 +38,9 @@ struct GeneralState {
   int64_t keys_alloc = 0;     // arenas allocated
   SgGeo* dgeo = nullptr;
   int32_t* dfail = nullptr;
+  PartialState* pp = nullptr; // partial-lane route (partial.hip) while the query and the stream allow it
+  int pp_checked = 0;
+  int64_t max_ts = INT64_MIN;  // largest timestamp pushed (INT64_MAX once a timestamp went back)
 };
 
 __global__ void k_route(int64_t n, const int32_t* __restrict__ stream, const int32_t* __restrict__ key,
@@ -348,12 +351,9 @@ static GeneralState* gstate(SgHandle* h) {
   return (GeneralState*)h->state;
 }
 
-void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
+static uint32_t general_key_bound(SgHandle* h, const BatchView& bv, int64_t n) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
-  GeneralState* gs = gstate(h);
-  bool has_absent = gs->geo.A > 0;
-  // ---- key bound
   uint32_t kb = 1;
   if (d.partitioned) {
     kb = bv.key_bound > 0 ? (uint32_t)bv.key_bound : 0;
@@ -371,6 +371,39 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   if (kb < h->key_bound_seen) kb = h->key_bound_seen;
   h->key_bound_seen = kb;
+  return kb;
+}
+
+static void run_machine(SgHandle* h, const BatchView& bv, int64_t n);
+
+void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
+  GeneralState* gs = gstate(h);
+  if (!gs->pp_checked) {
+    gs->pp = sg_partial_new(h->desc);
+    gs->pp_checked = 1;
+  }
+  if (gs->pp && sg_partial_active(gs->pp) && h->opt.partial_lanes >= 0) {
+    const uint32_t kb = general_key_bound(h, bv, n);
+    if (sg_partial_push(h, gs->pp, bv, n, kb)) return;
+    // the stream left the route's precondition (a timestamp went back): rebuild the general machine's per-key runtimes
+    // by replaying the carried rows without emitting (they were delivered already), then continue on the machine
+    BatchView cv = sg_partial_carried_view(h, gs->pp, (int32_t)kb);
+    sg_partial_deactivate(gs->pp);
+    if (cv.n) {
+      const int64_t delivered = h->out.n;
+      run_machine(h, cv, cv.n);
+      h->out.n = delivered;
+    }
+  }
+  run_machine(h, bv, n);
+}
+
+static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  GeneralState* gs = gstate(h);
+  bool has_absent = gs->geo.A > 0;
+  const uint32_t kb = general_key_bound(h, bv, n);
   // ---- grow arenas (new ones zeroed: runtime not created yet)
   if ((int64_t)kb > gs->keys_alloc) {
     int64_t nk = std::max<int64_t>((int64_t)kb, gs->keys_alloc * 3 / 2);
@@ -402,8 +435,9 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(hipMemsetAsync(order_err, 0, sizeof(int32_t), st));
   h->mark(0);
   h->kbeg("route");
+  const SgChunkRule rule = sg_chunk_rule(d);
   hipLaunchKernelGGL(k_route, grd, blk, 0, st, n, bv.stream, bv.key, bv.ts, h->ddesc, d.partitioned, sentinel,
-                     has_absent ? 1 : 0, keys, rows, order_err);
+                     (has_absent || rule.kind == 1) ? 1 : 0, keys, rows, order_err);
   HIPCHK(hipGetLastError());
   h->kend();
   h->mark(1);
@@ -432,10 +466,20 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(hipMemsetAsync(eover, 0, 4, st));
   HIPCHK(hipMemsetAsync(gs->dfail, 0, 4, st));
   int32_t oerr = 0;
+  int64_t tfl[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(&oerr, order_err, 4, hipMemcpyDeviceToHost, st));
+  if (n > 0) {
+    HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), 8, hipMemcpyDeviceToHost, st));
+  }
   HIPCHK(hipStreamSynchronize(st));
   if (oerr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-  if (oerr & 1) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps within a push");
+  if ((oerr & 1) && has_absent) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps within a push");
+  // time-horizon units rebuild a key's state from the rows inside `within` before them: only sound while timestamps
+  // never decrease, within this push and after the earlier ones
+  const bool ts_monotone = !(oerr & 1) && (n == 0 || tfl[0] >= gs->max_ts);
+  if (n > 0) gs->max_ts = std::max(gs->max_ts, ts_monotone ? tfl[1] : std::max(tfl[0], tfl[1]));
+  if (!ts_monotone) gs->max_ts = INT64_MAX;   // from now on the order of the stream is unknown
   NfaArgs na;
   na.n = n;
   na.base_index = bv.base_index;
@@ -483,22 +527,14 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   sink.stride = stride;
   sink.key_bits = kbits;
   // ---- unit plan: one unit per key, or (chunkable shapes) per (key, chunk of R rows)
-  const SgChunkRule rule = sg_chunk_rule(d);
   uint32_t R = 0;
-  if (rule.kind != 0 && h->opt.chunk_rows >= 0 && n > 0) {
+  if (rule.kind != 0 && (rule.kind == 2 || ts_monotone) && h->opt.chunk_rows >= 0 && n > 0) {
     if (h->opt.chunk_rows > 0) {
       R = (uint32_t)h->opt.chunk_rows;
     } else {
       // horizon rows per unit (rows of an average key inside `within`, or the sequence's event horizon);
       // units at least 4x their horizon, enough of them to fill the chip, scratch arenas within budget
-      int64_t span = 1;
-      {
-        int64_t tfl[2] = {0, 0};
-        HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        span = std::max<int64_t>(1, tfl[1] - tfl[0]);
-      }
+      const int64_t span = std::max<int64_t>(1, tfl[1] - tfl[0]);
       const double per_key = (double)n / (double)std::max<uint32_t>(kb, 1);
       const double hz = rule.kind == 2 ? (double)rule.events : per_key * (double)rule.within / (double)span;
       // (measured on C3b/C3c: 131k -> 524k units took 372 -> 245 ms and 3150 -> 2347 ms per 100M events;
@@ -594,6 +630,8 @@ void sg_general_reset(SgHandle* h) {
   if (!h->state || h->state_kind != 2) return;
   GeneralState* gs = (GeneralState*)h->state;
   if (gs->arena) hipMemset(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4);
+  sg_partial_reset(gs->pp);
+  gs->max_ts = INT64_MIN;
   h->key_bound_seen = 0;
 }
 
@@ -603,6 +641,7 @@ void sg_general_release(SgHandle* h) {
   if (gs->arena) hipFree(gs->arena);
   if (gs->dgeo) hipFree(gs->dgeo);
   if (gs->dfail) hipFree(gs->dfail);
+  sg_partial_free(gs->pp);
   delete gs;
   h->state = nullptr;
   h->state_kind = 0;
@@ -615,6 +654,13 @@ void sg_general_release(SgHandle* h) {
 // C/partition/PartitionRuntime.java:342-356).  The arena geometry must match on restore.
 void sg_general_snapshot(SgHandle* h, SnapW& w) {
   GeneralState* gs = (h->state && h->state_kind == 2) ? (GeneralState*)h->state : nullptr;
+  const int32_t route = (gs && gs->pp && sg_partial_active(gs->pp) && h->opt.partial_lanes >= 0) ? 1 : 0;   // 1: partial lanes' carried rows
+  w.pod(route);
+  w.pod(gs ? gs->max_ts : (int64_t)INT64_MIN);
+  if (route) {
+    sg_partial_snapshot(h, gs->pp, w);
+    return;
+  }
   const int64_t keys = gs ? std::min<int64_t>(gs->keys_alloc, (int64_t)h->key_bound_seen) : 0;
   w.pod(keys);
   if (!keys) return;
@@ -625,6 +671,21 @@ void sg_general_snapshot(SgHandle* h, SnapW& w) {
 void sg_general_restore(SgHandle* h, SnapR& r) {
   GeneralState* gs = gstate(h);
   hipStream_t st = h->stream;
+  if (!gs->pp_checked) {
+    gs->pp = sg_partial_new(h->desc);
+    gs->pp_checked = 1;
+  }
+  const int32_t route = r.pod<int32_t>();
+  const int64_t max_ts = r.pod<int64_t>();
+  if (route != 0 && route != 1) throw SgError(SG_EINVAL, "snapshot: bad general-route marker");
+  if (route == 1) {
+    if (!gs->pp || h->opt.partial_lanes < 0) throw SgError(SG_EINVAL, "snapshot: taken on the partial-lane route");
+    sg_partial_restore(h, gs->pp, r);
+    gs->max_ts = max_ts;
+    return;
+  }
+  if (gs->pp) sg_partial_deactivate(gs->pp);
+  gs->max_ts = max_ts;
   const int64_t keys = r.pod<int64_t>();
   if (keys < 0 || keys > (1ll << 31)) throw SgError(SG_EINVAL, "snapshot: bad key count");
   if (gs->arena) HIPCHK(hipMemsetAsync(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4, st));

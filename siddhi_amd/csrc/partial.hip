@@ -1,0 +1,610 @@
+// Partial lanes (chain.h): the general machine's route for patterns whose partial matches never interact
+// (sg_pp_rule: `every e1=S[local] -> ... within T` over stream / count / logical states of one stream).
+//
+// Per sg_push, with the rows carried from earlier pushes listed first ("carried rows": per key, the rows inside
+// `within` of the key's last row -- they rebuild every partial that can still match, StreamPreStateProcessor.isExpired,
+// C/query/input/stream/state/StreamPreStateProcessor.java:102-113):
+//   1. k_pp_route      combined rows (carried, then the batch) -> partition key (PartitionStreamReceiver routing)
+//   2. key partition   stable radix sort of (key, combined row): each key's rows contiguous, in arrival order;
+//                      k_pp_segments: per-key bounds and the route's precondition -- a key's timestamps never decrease
+//                      (also across pushes), as for the closed forms
+//   3. predicate pass  condition bits of every event-local filter over the batch (pred.h)
+//   4. k_pp_lanes      one lane per row that starts a partial (passes the start state's filter): chain.h's PpLane runs
+//                      that partial alone over the key's following rows until it dies or leaves `within`; a match is
+//                      written with its sort key (trigger row, visit slot) and its insertion history (tie key)
+//   5. match order     stable radix sorts: tie words, then (trigger, visit slot) -> the reference's delivery order;
+//                      k_pp_gather writes the match records
+//   6. carry           per key, the rows with ts >= last ts - within become the next push's carried rows
+// A push that breaks the ordering precondition leaves this route: the carried rows are handed back so the caller can
+// replay them through the general machine (interp.hip) and continue there.  That replay is exact unless the query has a
+// count state: CountPreStateProcessor never expires a partial (CountPreStateProcessor.java:53-93), so with time going
+// back a partial parked in a count state longer than `within` could still complete, and the carried rows do not hold
+// it -- such a push fails with SG_EORDER, like the closed forms (open the handle with partial_lanes = -1 for streams
+// whose timestamps go back).
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <string>
+
+#include "sg_device.h"
+#include "sg_engine.h"
+#include "interp.h"
+#include "chain.h"
+#include "pred.h"
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw SgError(SG_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Carried rows: SoA in the batch's own column formats (so the general machine can replay them as a batch).
+struct PpRows {
+  int64_t n = 0, cap = 0;
+  int64_t* ts = nullptr;
+  int32_t* key = nullptr;
+  void* col[SG_MAX_COLS] = {};
+  uint8_t* nul[SG_MAX_COLS] = {};
+};
+
+struct PartialState {
+  SgPpRule rule;
+  SgPpRule* drule = nullptr;
+  int used_col[SG_MAX_COLS] = {};
+  int col_bytes[SG_MAX_COLS] = {};
+  PpRows rows[2];       // carried rows (cur) and the next push's (double buffer)
+  int cur = 0;
+  int has_count = 0;
+  int active = 1;
+};
+
+static void rows_free(PpRows& r) {
+  if (r.ts) hipFree(r.ts);
+  if (r.key) hipFree(r.key);
+  for (int c = 0; c < SG_MAX_COLS; ++c) {
+    if (r.col[c]) hipFree(r.col[c]);
+    if (r.nul[c]) hipFree(r.nul[c]);
+  }
+  r = PpRows();
+}
+
+static void rows_reserve(PartialState* ps, PpRows& r, int64_t need) {
+  if (need <= r.cap) return;
+  const int64_t cap = std::max<int64_t>(need + need / 4, 1024);
+  PpRows nr;
+  nr.cap = cap;
+  if (hipMalloc(&nr.ts, 8 * cap) != hipSuccess || hipMalloc(&nr.key, 4 * cap) != hipSuccess)
+    throw SgError(SG_EHIP, "hipMalloc carried rows");
+  for (int c = 0; c < SG_MAX_COLS; ++c) {
+    if (!ps->used_col[c]) continue;
+    if (hipMalloc(&nr.col[c], (size_t)ps->col_bytes[c] * cap) != hipSuccess || hipMalloc(&nr.nul[c], cap) != hipSuccess)
+      throw SgError(SG_EHIP, "hipMalloc carried rows");
+  }
+  rows_free(r);
+  r = nr;
+}
+
+PartialState* sg_partial_new(const sg_nfa_desc& d) {
+  SgPpRule ru = sg_pp_rule(d);
+  if (!ru.ok) return nullptr;
+  PartialState* ps = new PartialState();
+  ps->rule = ru;
+  for (int s = 0; s < d.n_states; ++s) ps->has_count |= d.states[s].kind == SG_K_COUNT;
+  for (int k = 0; k < d.n_ret; ++k) {
+    const int c = d.ret_col[k];
+    ps->used_col[c] = 1;
+    ps->col_bytes[c] = (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE) ? 8 : 4;
+  }
+  if (hipMalloc(&ps->drule, sizeof(SgPpRule)) != hipSuccess) { delete ps; throw SgError(SG_EHIP, "hipMalloc rule"); }
+  hipMemcpy(ps->drule, &ps->rule, sizeof(SgPpRule), hipMemcpyHostToDevice);
+  return ps;
+}
+
+void sg_partial_free(PartialState* ps) {
+  if (!ps) return;
+  rows_free(ps->rows[0]);
+  rows_free(ps->rows[1]);
+  if (ps->drule) hipFree(ps->drule);
+  delete ps;
+}
+
+void sg_partial_reset(PartialState* ps) {
+  if (!ps) return;
+  ps->rows[0].n = ps->rows[1].n = 0;
+  ps->active = 1;
+}
+
+int sg_partial_active(const PartialState* ps) { return ps && ps->active; }
+void sg_partial_deactivate(PartialState* ps) {
+  if (ps) ps->active = 0;
+}
+
+// ---- device side --------------------------------------------------------------------------------------------
+struct PpArgs {
+  int64_t nc;                 // carried rows (combined rows [0, nc)); batch row r is combined row nc + r
+  int64_t n;
+  uint64_t base_index;
+  const uint64_t* index;
+  const int64_t* bts;
+  const int64_t* cts;
+  const int32_t* stream;
+  const int32_t* bkey;
+  const int32_t* ckey;
+  const uint64_t* lbits[SG_MAX_STATES];
+  int32_t any_bits;
+};
+
+struct PpSrc {
+  const PpArgs* a;
+  const SgCols* bc;
+  const SgCols* cc;
+  const DevDesc* d;
+  __device__ int64_t ts(int64_t c) const { return c < a->nc ? a->cts[c] : a->bts[c - a->nc]; }
+  __device__ SgVal read(int64_t c, int slotk, int type) const {
+    const int col = d->ret_col[slotk];
+    return c < a->nc ? sg_read_col(*cc, col, type, c) : sg_read_col(*bc, col, type, c - a->nc);
+  }
+  __device__ int lbit(int s, int64_t c) const {
+    if (c < a->nc || !a->lbits[s]) return -1;
+    return (int)mask_bit(a->lbits[s], (uint64_t)(c - a->nc));
+  }
+};
+
+__global__ void k_pp_route(PpArgs a, const DevDesc* __restrict__ dd, int partitioned, uint32_t sentinel,
+                           uint32_t* __restrict__ okey, uint32_t* __restrict__ orow, int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nc + a.n) return;
+  uint32_t k = sentinel;
+  if (i < a.nc) {
+    k = partitioned ? (uint32_t)a.ckey[i] : 0u;
+  } else {
+    const int64_t r = i - a.nc;
+    const int s = a.stream ? a.stream[r] : 0;
+    if (s >= 0 && s < SG_MAX_STREAMS && dd->recv_of_stream[s] >= 0) {
+      if (!partitioned) k = 0;
+      else {
+        const int32_t kk = a.bkey ? a.bkey[r] : -1;
+        if (kk >= 0) {
+          if ((uint32_t)kk >= sentinel) atomicOr(err, 2);
+          else k = (uint32_t)kk;
+        }
+      }
+    }
+  }
+  okey[i] = k;
+  orow[i] = (uint32_t)i;
+}
+
+__global__ void k_pp_segments(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
+                              uint32_t sentinel, uint32_t* __restrict__ beg, uint32_t* __restrict__ end,
+                              int32_t* __restrict__ err) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m) return;
+  const uint32_t k = skey[p];
+  if (k == sentinel) return;
+  if (p == 0 || skey[p - 1] != k) beg[k] = (uint32_t)p;
+  else {
+    const int64_t c0 = sid[p - 1], c1 = sid[p];
+    const int64_t t0 = c0 < a.nc ? a.cts[c0] : a.bts[c0 - a.nc], t1 = c1 < a.nc ? a.cts[c1] : a.bts[c1 - a.nc];
+    if (t0 > t1) atomicOr(err, 1);
+  }
+  if (p == m - 1 || skey[p + 1] != k) end[k] = (uint32_t)p + 1;
+}
+
+struct PpOut {
+  char* rec;                  // match records (sg_match_records layout, 32 + 8 * n_select bytes)
+  uint64_t* k1;               // (trigger row << 8) | visit slot
+  uint64_t* th;               // tie words
+  uint64_t* tl;
+  unsigned long long* count;
+  int32_t* fail;
+  int32_t rstride;
+};
+
+__device__ __forceinline__ uint64_t pp_index(const PpArgs& a, int64_t r) { return a.index ? a.index[r] : a.base_index + (uint64_t)r; }
+
+__global__ void __launch_bounds__(256) k_pp_lanes(PpArgs a, SgCols bc, SgCols cc, const DevDesc* __restrict__ ddg,
+                                                  const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ skey,
+                                                  const uint32_t* __restrict__ sid, const uint32_t* __restrict__ end,
+                                                  uint32_t sentinel, PpOut o) {
+  __shared__ DevDesc dl;
+  __shared__ SgPpRule rl;
+  __shared__ SgCols bcl, ccl;
+  __shared__ PpArgs al;
+  {
+    const uint32_t* s1 = (const uint32_t*)&bc;
+    const uint32_t* s2 = (const uint32_t*)&cc;
+    const uint32_t* s3 = (const uint32_t*)&a;
+    for (uint32_t i = threadIdx.x; i < sizeof(SgCols) / 4; i += blockDim.x) {
+      ((uint32_t*)&bcl)[i] = s1[i];
+      ((uint32_t*)&ccl)[i] = s2[i];
+    }
+    for (uint32_t i = threadIdx.x; i < sizeof(PpArgs) / 4; i += blockDim.x) ((uint32_t*)&al)[i] = s3[i];
+    const uint32_t* src = (const uint32_t*)ddg;
+    uint32_t* dst = (uint32_t*)&dl;
+    for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) dst[i] = src[i];
+    const uint32_t* rs = (const uint32_t*)rug;
+    uint32_t* rd = (uint32_t*)&rl;
+    for (uint32_t i = threadIdx.x; i < sizeof(SgPpRule) / 4; i += blockDim.x) rd[i] = rs[i];
+    __syncthreads();
+  }
+  const DevDesc* dd = &dl;
+  const int64_t m = a.nc + a.n;
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m) return;
+  const uint32_t k = skey[p];
+  if (k == sentinel) return;
+  PpSrc src{&al, &bcl, &ccl, dd};
+  PpLane<PpSrc> L;
+  L.d = dd;
+  L.ru = &rl;
+  L.src = &src;
+  const int64_t c0 = sid[p];
+  if (!L.start_ok(c0)) return;
+  L.start(c0);
+  const int64_t e = end[k];
+  for (int64_t q = p + 1; q < e; ++q) {
+    const int64_t c = sid[q];
+    if (src.ts(c) - L.e1_ts > dd->within) break;   // expired everywhere it can still emit (sg_pp_rule)
+    const int em = L.step(c);
+    if (L.overflow) { atomicCAS(o.fail, 0, SG_EUNSUPPORTED); return; }
+    if (em >= 0 && c >= a.nc) {
+      const unsigned long long w = atomicAdd(o.count, 1ull);
+      const int64_t r = c - a.nc;
+      o.k1[w] = ((uint64_t)r << 8) | (uint32_t)em;
+      L.tie(o.th[w], o.tl[w]);
+      char* rec = o.rec + (size_t)w * (size_t)o.rstride;
+      uint64_t* h64 = (uint64_t*)rec;
+      h64[0] = pp_index(a, r);
+      h64[1] = (uint64_t)L.pts;
+      uint32_t* h32 = (uint32_t*)(rec + 16);
+      h32[0] = k;
+      h32[1] = (1u << 24) | (uint32_t)em;
+      uint32_t nm = 0;
+      int64_t* vals = (int64_t*)(rec + 32);
+      for (int s = 0; s < dd->n_select; ++s) {
+        const int64_t ev = L.get_event(dd->sel_state[s], dd->sel_index[s]);
+        const int rs = dd->sel_ret[s];
+        SgVal v;
+        if (ev < 0) { nm |= 1u << s; vals[s] = 0; continue; }
+        v = src.read(ev, rs, dd->ret_type[rs]);
+        if (v.null) { nm |= 1u << s; vals[s] = 0; continue; }
+        vals[s] = sg_val_bits(v);
+      }
+      h32[2] = nm;
+      h32[3] = 0;
+    }
+    if (L.dead()) break;
+  }
+}
+
+__global__ void k_pp_iota(int64_t n, uint32_t* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = (uint32_t)i;
+}
+__global__ void k_pp_take(int64_t n, const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx, uint64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+__global__ void k_pp_gather(int64_t n, const char* __restrict__ rec, const uint32_t* __restrict__ idx, int32_t stride,
+                            char* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t* s = (const uint64_t*)(rec + (size_t)idx[i] * stride);
+  uint64_t* t = (uint64_t*)(out + (size_t)i * stride);
+  for (int w = 0; w < stride / 8; ++w) t[w] = s[w];
+}
+
+// carry: keep sorted position p if ts >= ts(last row of its key) - within
+__global__ void k_pp_keep(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
+                          const uint32_t* __restrict__ end, uint32_t sentinel, int64_t within, uint32_t* __restrict__ keep) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m) return;
+  const uint32_t k = skey[p];
+  uint32_t f = 0;
+  if (k != sentinel) {
+    const int64_t c = sid[p], cl = sid[end[k] - 1];
+    const int64_t t = c < a.nc ? a.cts[c] : a.bts[c - a.nc];
+    const int64_t tl = cl < a.nc ? a.cts[cl] : a.bts[cl - a.nc];
+    f = t >= tl - within ? 1u : 0u;
+  }
+  keep[p] = f;
+}
+
+struct PpCopyCols {
+  const void* bsrc[SG_MAX_COLS];
+  const uint8_t* bnul[SG_MAX_COLS];
+  const void* csrc[SG_MAX_COLS];
+  const uint8_t* cnul[SG_MAX_COLS];
+  void* dst[SG_MAX_COLS];
+  uint8_t* dnul[SG_MAX_COLS];
+  int32_t bytes[SG_MAX_COLS];
+  int32_t ncols;
+};
+
+__global__ void k_pp_carry(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
+                           const uint32_t* __restrict__ keep, const uint32_t* __restrict__ pos, PpCopyCols cc,
+                           int64_t* __restrict__ nts, int32_t* __restrict__ nkey) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m || !keep[p]) return;
+  const int64_t c = sid[p];
+  const int64_t o = pos[p];
+  const bool carried = c < a.nc;
+  const int64_t r = carried ? c : c - a.nc;
+  nts[o] = carried ? a.cts[r] : a.bts[r];
+  nkey[o] = (int32_t)skey[p];
+  for (int j = 0; j < cc.ncols; ++j) {
+    if (!cc.dst[j]) continue;
+    const void* s = carried ? cc.csrc[j] : cc.bsrc[j];
+    const uint8_t* sn = carried ? cc.cnul[j] : cc.bnul[j];
+    if (cc.bytes[j] == 8) ((int64_t*)cc.dst[j])[o] = ((const int64_t*)s)[r];
+    else ((int32_t*)cc.dst[j])[o] = ((const int32_t*)s)[r];
+    cc.dnul[j][o] = sn ? sn[r] : 0;
+  }
+}
+
+// ---- host side ------------------------------------------------------------------------------------------------
+static SgCols carried_cols(const PartialState* ps, const PpRows& r) {
+  SgCols c;
+  for (int j = 0; j < SG_MAX_COLS; ++j) { c.col[j] = ps->used_col[j] ? r.col[j] : nullptr; c.nul[j] = ps->used_col[j] ? r.nul[j] : nullptr; }
+  return c;
+}
+
+// A view of the carried rows as a batch (for the replay through the general machine when the route is left).
+BatchView sg_partial_carried_view(SgHandle* h, PartialState* ps, int32_t key_bound) {
+  const PpRows& r = ps->rows[ps->cur];
+  BatchView v;
+  v.n = r.n;
+  v.base_index = 0;
+  v.ts = r.ts;
+  v.key = r.key;
+  v.index = nullptr;
+  v.cols = carried_cols(ps, r);
+  v.key_bound = key_bound;
+  v.stream = nullptr;
+  const int rs = h->desc.receivers[ps->rule.recv].stream;
+  if (rs != 0 && r.n) {   // every carried row belongs to the query's stream
+    int32_t* s = (int32_t*)h->ws.get("pp_stream", 4 * r.n, h->stream);
+    std::vector<int32_t> host((size_t)r.n, rs);
+    HIPCHK(hipMemcpy(s, host.data(), 4 * r.n, hipMemcpyHostToDevice));
+    v.stream = s;
+  }
+  return v;
+}
+
+static void sort_pairs64(SgHandle* h, const char* tag, uint64_t* k_in, uint64_t* k_out, uint32_t* v_in, uint32_t* v_out,
+                         int64_t n, int end_bit) {
+  hipStream_t st = h->stream;
+  size_t tb = 0;
+  HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, k_in, k_out, v_in, v_out, (size_t)n, 0, end_bit, st));
+  void* tmp = h->ws.get(std::string("pp_sorttmp_") + tag, tb, st);
+  HIPCHK(rocprim::radix_sort_pairs(tmp, tb, k_in, k_out, v_in, v_out, (size_t)n, 0, end_bit, st));
+}
+
+// Returns 1 when the push ran on partial lanes, 0 when it breaks the route's precondition (nothing was changed).
+int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t n, uint32_t kb) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  const PpRows& cr = ps->rows[ps->cur];
+  const int64_t nc = h->opt.no_carry ? 0 : cr.n;
+  const int64_t m = nc + n;
+  if (m >= ((int64_t)1 << 27)) return 0;   // tie components hold a combined row in 27 bits
+  PpArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nc = nc;
+  a.n = n;
+  a.base_index = bv.base_index;
+  a.index = bv.index;
+  a.bts = bv.ts;
+  a.cts = cr.ts;
+  a.stream = bv.stream;
+  a.bkey = bv.key;
+  a.ckey = cr.key;
+  const SgCols cc = carried_cols(ps, cr);
+  int end_bit = 1;
+  while ((1ull << end_bit) <= (uint64_t)kb) ++end_bit;
+  const uint32_t sentinel = kb;
+  const dim3 blk(256), grd((unsigned)((m + 255) / 256));
+  uint32_t* keys = (uint32_t*)h->ws.get("pp_keys", 4 * m, st);
+  uint32_t* ids = (uint32_t*)h->ws.get("pp_ids", 4 * m, st);
+  uint32_t* skeys = (uint32_t*)h->ws.get("pp_skeys", 4 * m, st);
+  uint32_t* sids = (uint32_t*)h->ws.get("pp_sids", 4 * m, st);
+  int32_t* err = (int32_t*)h->ws.get("pp_err", 8, st);
+  HIPCHK(hipMemsetAsync(err, 0, 8, st));
+  h->mark(0);
+  h->kbeg("route");
+  hipLaunchKernelGGL(k_pp_route, grd, blk, 0, st, a, h->ddesc, d.partitioned, sentinel, keys, ids, err);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  h->mark(1);
+  h->kbeg("key_sort");
+  {
+    size_t tb = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, ids, sids, (size_t)m, 0, end_bit, st));
+    void* tmp = h->ws.get("pp_sort_tmp", tb, st);
+    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, ids, sids, (size_t)m, 0, end_bit, st));
+  }
+  uint32_t* beg = (uint32_t*)h->ws.get("pp_beg", 4 * (size_t)kb, st);
+  uint32_t* end = (uint32_t*)h->ws.get("pp_end", 4 * (size_t)kb, st);
+  HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
+  HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
+  if (m) hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, sentinel, beg, end, err);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  {
+    int32_t herr = 0;
+    HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (herr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+    if (herr & 1) {
+      if (ps->has_count && nc > 0)
+        throw SgError(SG_EORDER, "partial-lane route requires non-decreasing timestamps per key once a count state holds "
+                                 "partials (open the handle with partial_lanes = -1 for such streams)");
+      return 0;
+    }
+  }
+  h->mark(2);
+  // ---- predicate-evaluation pass over the batch rows
+  for (int s = 0; s < SG_MAX_STATES; ++s) a.lbits[s] = nullptr;
+  {
+    const int64_t ntiles = (n + 255) / 256;
+    bool any = false;
+    for (int s = 0; s < d.n_states && n > 0; ++s) {
+      const sg_state_desc& x = d.states[s];
+      if (!x.local || x.prog_len <= 0) continue;
+      if (!any) h->kbeg("pred");
+      any = true;
+      PredArgs pa;
+      memset(&pa, 0, sizeof(pa));
+      pa.n = n;
+      pa.stream = bv.stream;
+      pa.s_a = x.stream;
+      pa.prog_a_off = x.prog_off;
+      pa.prog_a_len = x.prog_len;
+      pa.val_col_a = -1;
+      pa.val_col_b = -1;
+      pa.cons_all = 1;
+      uint64_t* bits = (uint64_t*)h->ws.get("pp_lbits" + std::to_string(s), sizeof(uint64_t) * 4 * (ntiles + 1), st);
+      launch_pred(d, pa, bv.stream, bv.cols, h->ddesc, bits, nullptr, st);
+      HIPCHK(hipGetLastError());
+      a.lbits[s] = bits;
+    }
+    if (any) h->kend();
+  }
+  // ---- partial lanes
+  const int nsel = d.n_select;
+  const int32_t rstride = 32 + 8 * nsel;
+  const int64_t cap = std::max<int64_t>(m, 1);   // a partial completes at most once (sg_pp_rule)
+  PpOut o;
+  o.rec = (char*)h->ws.get("pp_rec", (size_t)cap * rstride, st);
+  o.k1 = (uint64_t*)h->ws.get("pp_k1", 8 * cap, st);
+  o.th = (uint64_t*)h->ws.get("pp_th", 8 * cap, st);
+  o.tl = (uint64_t*)h->ws.get("pp_tl", 8 * cap, st);
+  o.count = (unsigned long long*)h->ws.get("pp_count", 8, st);
+  o.fail = err + 1;
+  o.rstride = rstride;
+  HIPCHK(hipMemsetAsync(o.count, 0, 8, st));
+  h->kbeg("partial_lanes");
+  if (m)
+    hipLaunchKernelGGL(k_pp_lanes, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->drule, skeys, sids, end, sentinel, o);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  h->mark(3);
+  unsigned long long total = 0;
+  int32_t fail = 0;
+  HIPCHK(hipMemcpyAsync(&total, o.count, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&fail, o.fail, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (fail) throw SgError(fail, "partial lane capacity exceeded (query outside the route's shape)");
+  // ---- delivery order: LSD stable sorts (tie low word, tie high word, then trigger row and visit slot)
+  if (total) {
+    const int64_t T = (int64_t)total;
+    const dim3 g2((unsigned)((T + 255) / 256));
+    uint32_t* ia = (uint32_t*)h->ws.get("pp_ia", 4 * T, st);
+    uint32_t* ib = (uint32_t*)h->ws.get("pp_ib", 4 * T, st);
+    uint64_t* ka = (uint64_t*)h->ws.get("pp_ka", 8 * T, st);
+    uint64_t* kb2 = (uint64_t*)h->ws.get("pp_kb", 8 * T, st);
+    h->kbeg("match_order");
+    hipLaunchKernelGGL(k_pp_iota, g2, blk, 0, st, T, ia);
+    int tb = 1;
+    while ((1ll << tb) < m) ++tb;
+    const int comp_bits = tb + 4;   // one history component: combined row << 4 | visit slot
+    if (ps->rule.n_hist > 2) {
+      const int eb = std::min(64, 31 + comp_bits);
+      hipLaunchKernelGGL(k_pp_take, g2, blk, 0, st, T, o.tl, ia, ka);
+      sort_pairs64(h, "lo", ka, kb2, ia, ib, T, eb);
+      std::swap(ia, ib);
+    }
+    hipLaunchKernelGGL(k_pp_take, g2, blk, 0, st, T, o.th, ia, ka);
+    sort_pairs64(h, "hi", ka, kb2, ia, ib, T, 64);
+    std::swap(ia, ib);
+    hipLaunchKernelGGL(k_pp_take, g2, blk, 0, st, T, o.k1, ia, ka);
+    int rb = 1;
+    while ((1ll << rb) < n) ++rb;
+    sort_pairs64(h, "k1", ka, kb2, ia, ib, T, std::min(64, rb + 8));
+    std::swap(ia, ib);
+    char* out = h->out.reserve(T, nsel, st);
+    hipLaunchKernelGGL(k_pp_gather, g2, blk, 0, st, T, o.rec, ia, rstride, out + (size_t)h->out.n * rstride);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->out.n += T;
+  }
+  // ---- carry
+  if (!h->opt.no_carry && m) {
+    h->kbeg("carry");
+    uint32_t* keep = (uint32_t*)h->ws.get("pp_keep", 4 * (m + 1), st);
+    uint32_t* pos = (uint32_t*)h->ws.get("pp_pos", 4 * (m + 1), st);
+    hipLaunchKernelGGL(k_pp_keep, grd, blk, 0, st, m, a, skeys, sids, end, sentinel, (int64_t)d.within, keep);
+    HIPCHK(hipMemsetAsync(keep + m, 0, 4, st));
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, keep, pos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("pp_scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, keep, pos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t nn = 0;
+    HIPCHK(hipMemcpyAsync(&nn, pos + m, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    PpRows& nr = ps->rows[1 - ps->cur];
+    rows_reserve(ps, nr, nn);
+    PpCopyCols c2;
+    memset(&c2, 0, sizeof(c2));
+    c2.ncols = d.n_cols;
+    for (int j = 0; j < d.n_cols; ++j) {
+      if (!ps->used_col[j]) continue;
+      c2.bsrc[j] = bv.cols.col[j];
+      c2.bnul[j] = bv.cols.nul[j];
+      c2.csrc[j] = cr.col[j];
+      c2.cnul[j] = cr.nul[j];
+      c2.dst[j] = nr.col[j];
+      c2.dnul[j] = nr.nul[j];
+      c2.bytes[j] = ps->col_bytes[j];
+    }
+    hipLaunchKernelGGL(k_pp_carry, grd, blk, 0, st, m, a, skeys, sids, keep, pos, c2, nr.ts, nr.key);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    nr.n = nn;
+    ps->rows[ps->cur].n = 0;
+    ps->cur = 1 - ps->cur;
+    h->kend();
+  }
+  h->mark(4);
+  h->last_events = n;
+  h->last_spilled = 0;
+  h->last_matches = (int64_t)total;
+  return 1;
+}
+
+// Snapshot of the route's state: the carried rows (per key, the rows inside `within` of its last row -- replaying them
+// rebuilds every partial the reference still holds in StreamPreStateProcessor.pendingStateEventList /
+// newAndEveryStateEventList, C/query/input/stream/state/StreamPreStateProcessor.java:352-367) and the latest timestamp.
+void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
+  const PpRows& r = ps->rows[ps->cur];
+  w.pod(r.n);
+  if (!r.n) return;
+  w.dev(r.ts, 8 * r.n, h->stream);
+  w.dev(r.key, 4 * r.n, h->stream);
+  for (int j = 0; j < SG_MAX_COLS; ++j) {
+    if (!ps->used_col[j]) continue;
+    w.dev(r.col[j], (size_t)ps->col_bytes[j] * r.n, h->stream);
+    w.dev(r.nul[j], r.n, h->stream);
+  }
+}
+
+void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& rd) {
+  sg_partial_reset(ps);
+  const int64_t n = rd.pod<int64_t>();
+  if (n < 0 || n >= ((int64_t)1 << 31)) throw SgError(SG_EINVAL, "snapshot: bad carried row count");
+  PpRows& r = ps->rows[ps->cur];
+  rows_reserve(ps, r, n);
+  if (n) {
+    rd.dev(r.ts, 8 * n, h->stream);
+    rd.dev(r.key, 4 * n, h->stream);
+    for (int j = 0; j < SG_MAX_COLS; ++j) {
+      if (!ps->used_col[j]) continue;
+      rd.dev(r.col[j], (size_t)ps->col_bytes[j] * n, h->stream);
+      rd.dev(r.nul[j], n, h->stream);
+    }
+  }
+  r.n = n;
+}

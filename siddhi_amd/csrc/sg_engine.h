@@ -199,3 +199,14 @@ void sg_every_absent_reset(SgHandle* h);
 void sg_every_absent_release(SgHandle* h);
 void sg_general_reset(SgHandle* h);
 void sg_general_release(SgHandle* h);
+// partial-lane route of the general machine (partial.hip, chain.h)
+struct PartialState;
+PartialState* sg_partial_new(const sg_nfa_desc& d);   // nullptr: the query is outside the route (sg_pp_rule)
+void sg_partial_free(PartialState* ps);
+void sg_partial_reset(PartialState* ps);
+int sg_partial_active(const PartialState* ps);
+void sg_partial_deactivate(PartialState* ps);
+int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t n, uint32_t key_bound);
+BatchView sg_partial_carried_view(SgHandle* h, PartialState* ps, int32_t key_bound);
+void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w);
+void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& r);

@@ -10,6 +10,7 @@
 
 #include "../../siddhi_amd/csrc/sg_device.h"
 #include "../../siddhi_amd/csrc/interp.h"
+#include "../../siddhi_amd/csrc/chain.h"
 
 struct HiHandle {
   sg_nfa_desc d;
@@ -18,6 +19,11 @@ struct HiHandle {
   std::vector<std::vector<char>> out;
   int err = 0;
   int chunk_rows = 0;   // >0: cut each key's rows into units replaying their horizon (as interp.hip does)
+  // partial lanes (chain.h, as partial.hip runs them): carried rows per push, values as retained-slot bits
+  int pp = 0;
+  int pp_active = 1;
+  struct CRow { int64_t ts; int32_t key; int64_t vals[SG_MAX_RET]; int32_t nullmask; };
+  std::vector<CRow> carried;
 };
 
 struct HostRows {
@@ -60,7 +66,144 @@ struct HostRows {
   }
 };
 
+static int64_t read_bits(const sg_batch* b, const sg_nfa_desc* d, int k, int64_t r, int* null) {
+  int c = d->ret_col[k];
+  int t = d->ret_type[k];
+  *null = (b->nulls && b->nulls[c] && b->nulls[c][r]) ? 1 : 0;
+  if (*null) return 0;
+  const void* col = b->cols[c];
+  int64_t bits;
+  switch (t) {
+    case SG_T_LONG: bits = ((const int64_t*)col)[r]; break;
+    case SG_T_DOUBLE: memcpy(&bits, (const double*)col + r, 8); break;
+    case SG_T_FLOAT: { uint32_t u; memcpy(&u, (const float*)col + r, 4); bits = u; break; }
+    default: bits = ((const int32_t*)col)[r]; break;
+  }
+  return bits;
+}
+
+struct HostPpSrc {
+  const sg_batch* b;
+  const sg_nfa_desc* d;
+  const std::vector<HiHandle::CRow>* c;
+  int64_t nc;
+  int64_t ts(int64_t x) const { return x < nc ? (*c)[x].ts : b->ts[x - nc]; }
+  SgVal read(int64_t x, int slotk, int type) const {
+    int null = 0;
+    int64_t bits;
+    if (x < nc) {
+      null = ((*c)[x].nullmask >> slotk) & 1;
+      bits = (*c)[x].vals[slotk];
+    } else {
+      bits = read_bits(b, d, slotk, x - nc, &null);
+    }
+    return sg_val_from_bits(bits, type, null);
+  }
+  int lbit(int, int64_t) const { return -1; }
+};
+
+// partial-lane push (partial.hip restated on the host); returns 0 when the push breaks the route's precondition
+static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std::vector<uint64_t>& k1,
+                   std::vector<uint64_t>& th, std::vector<uint64_t>& tl) {
+  const sg_nfa_desc& d = h->d;
+  const SgPpRule ru = sg_pp_rule(d);
+  const int64_t n = b->n;
+  const int64_t nc = (int64_t)h->carried.size();
+  int kmax = 0;
+  for (auto& r : h->carried) kmax = std::max(kmax, r.key + 1);
+  for (int64_t i = 0; i < n; ++i) if (d.partitioned && b->key && b->key[i] >= 0) kmax = std::max(kmax, b->key[i] + 1);
+  std::vector<std::vector<int64_t>> own((size_t)std::max(kmax, 1));
+  for (int64_t c = 0; c < nc; ++c) own[d.partitioned ? h->carried[c].key : 0].push_back(c);
+  for (int64_t i = 0; i < n; ++i) {
+    int s = b->stream ? b->stream[i] : 0;
+    if (s < 0 || d.recv_of_stream[s] < 0) continue;
+    int k = d.partitioned ? (b->key ? b->key[i] : -1) : 0;
+    if (k < 0) continue;
+    own[k].push_back(nc + i);
+  }
+  HostPpSrc src{b, &d, &h->carried, nc};
+  bool has_count = false;
+  for (int s = 0; s < d.n_states; ++s) has_count |= d.states[s].kind == SG_K_COUNT;
+  for (const auto& rows : own)   // the route's precondition: a key's timestamps never decrease (also across pushes)
+    for (size_t p = 1; p < rows.size(); ++p)
+      if (src.ts(rows[p - 1]) > src.ts(rows[p])) return (has_count && nc > 0) ? -2 : 0;
+  const int rstride = 32 + 8 * d.n_select;
+  for (size_t k = 0; k < own.size(); ++k) {
+    const auto& rows = own[k];
+    for (size_t p = 0; p < rows.size(); ++p) {
+      PpLane<HostPpSrc> L;
+      L.d = &d;
+      L.ru = &ru;
+      L.src = &src;
+      if (!L.start_ok(rows[p])) continue;
+      L.start(rows[p]);
+      for (size_t q = p + 1; q < rows.size(); ++q) {
+        const int64_t c = rows[q];
+        if (src.ts(c) - L.e1_ts > d.within) break;
+        const int em = L.step(c);
+        if (L.overflow) return -1;
+        if (em >= 0 && c >= nc) {
+          const int64_t r = c - nc;
+          k1.push_back(((uint64_t)r << 8) | (uint32_t)em);
+          uint64_t a, z;
+          L.tie(a, z);
+          th.push_back(a);
+          tl.push_back(z);
+          const size_t o = recs.size();
+          recs.resize(o + rstride);
+          char* rec = recs.data() + o;
+          uint64_t trig = b->index ? b->index[r] : b->base_index + (uint64_t)r;
+          memcpy(rec, &trig, 8);
+          int64_t pts = L.pts;
+          memcpy(rec + 8, &pts, 8);
+          uint32_t h32[4] = {(uint32_t)k, (1u << 24) | (uint32_t)em, 0, 0};
+          for (int s = 0; s < d.n_select; ++s) {
+            int64_t v = 0;
+            const int64_t ev = L.get_event(d.sel_state[s], d.sel_index[s]);
+            if (ev < 0) { h32[2] |= 1u << s; }
+            else {
+              SgVal x = src.read(ev, d.sel_ret[s], d.ret_type[d.sel_ret[s]]);
+              if (x.null) h32[2] |= 1u << s; else v = sg_val_bits(x);
+            }
+            memcpy(rec + 32 + 8 * s, &v, 8);
+          }
+          memcpy(rec + 16, h32, 16);
+        }
+        if (L.dead()) break;
+      }
+    }
+  }
+  // carry: per key, rows with ts >= last ts - within
+  std::vector<HiHandle::CRow> next;
+  for (size_t k = 0; k < own.size(); ++k) {
+    const auto& rows = own[k];
+    if (rows.empty()) continue;
+    const int64_t last = src.ts(rows.back());
+    for (int64_t c : rows) {
+      if (src.ts(c) < last - d.within) continue;
+      HiHandle::CRow cr;
+      memset(&cr, 0, sizeof(cr));
+      cr.ts = src.ts(c);
+      cr.key = (int32_t)k;
+      if (c < nc) cr = h->carried[c];
+      else {
+        for (int j = 0; j < d.n_ret; ++j) {
+          int null = 0;
+          cr.vals[j] = read_bits(b, &d, j, c - nc, &null);
+          if (null) cr.nullmask |= 1 << j;
+        }
+      }
+      next.push_back(cr);
+    }
+  }
+  h->carried.swap(next);
+  return 1;
+}
+
 extern "C" {
+
+void hi_set_pp(HiHandle* h, int on) { h->pp = on; }
+int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
 
 HiHandle* hi_open(const sg_nfa_desc* d, int P, int E, int C, int L) {
   HiHandle* h = new HiHandle();
@@ -79,7 +222,73 @@ int hi_chunk_rule(const sg_nfa_desc* d, int64_t* horizon) {
   return r.kind;
 }
 
+static int machine_push(HiHandle* h, const sg_batch* b, bool silent);
+
 int hi_push(HiHandle* h, const sg_batch* b) {
+  if (h->pp && h->pp_active && sg_pp_rule(h->d).ok) {
+    std::vector<char> recs;
+    std::vector<uint64_t> k1, th, tl;
+    const int rc = pp_push(h, b, recs, k1, th, tl);
+    if (rc == -2) { h->err = SG_EORDER; return SG_EORDER; }
+    if (rc < 0) { h->err = SG_EUNSUPPORTED; return SG_EUNSUPPORTED; }
+    if (rc == 1) {
+      const int rstride = 32 + 8 * h->d.n_select;
+      std::vector<size_t> idx(k1.size());
+      for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+      std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
+        if (k1[x] != k1[y]) return k1[x] < k1[y];
+        if (th[x] != th[y]) return th[x] < th[y];
+        return tl[x] < tl[y];
+      });
+      for (size_t i : idx) h->out.emplace_back(recs.begin() + i * rstride, recs.begin() + (i + 1) * rstride);
+      return 0;
+    }
+    // leave the route: replay the carried rows through the machine without emitting
+    h->pp_active = 0;
+    const size_t nc = h->carried.size();
+    if (nc) {
+      std::vector<int64_t> ts(nc), colv[SG_MAX_COLS];
+      std::vector<int32_t> key(nc), stream(nc, h->d.receivers[sg_pp_rule(h->d).recv].stream);
+      std::vector<uint8_t> nul[SG_MAX_COLS];
+      const void* cols[SG_MAX_COLS] = {};
+      const uint8_t* nuls[SG_MAX_COLS] = {};
+      for (int j = 0; j < h->d.n_ret; ++j) {
+        const int c = h->d.ret_col[j];
+        colv[c].resize(nc);
+        nul[c].resize(nc);
+        for (size_t i = 0; i < nc; ++i) {
+          int64_t bits = h->carried[i].vals[j];
+          const int t = h->d.ret_type[j];
+          if (t == SG_T_LONG || t == SG_T_DOUBLE) colv[c][i] = bits;
+          else { int32_t w = (int32_t)(uint32_t)bits; memcpy(&colv[c][i], &w, 4); }
+          nul[c][i] = (h->carried[i].nullmask >> j) & 1;
+        }
+        // 4-byte columns are read as int32/float from the start of each 8-byte cell: pack them densely
+        if (!(h->d.ret_type[j] == SG_T_LONG || h->d.ret_type[j] == SG_T_DOUBLE)) {
+          std::vector<int64_t> packed((nc + 1) / 2);
+          for (size_t i = 0; i < nc; ++i) memcpy((char*)packed.data() + 4 * i, &colv[c][i], 4);
+          colv[c].swap(packed);
+        }
+        cols[c] = colv[c].data();
+        nuls[c] = nul[c].data();
+      }
+      for (size_t i = 0; i < nc; ++i) { ts[i] = h->carried[i].ts; key[i] = h->carried[i].key; }
+      sg_batch cb;
+      memset(&cb, 0, sizeof(cb));
+      cb.n = (int64_t)nc;
+      cb.ts = ts.data();
+      cb.stream = stream.data();
+      cb.key = key.data();
+      cb.cols = cols;
+      cb.nulls = nuls;
+      h->carried.clear();
+      if (int f = machine_push(h, &cb, true)) return f;
+    }
+  }
+  return machine_push(h, b, false);
+}
+
+static int machine_push(HiHandle* h, const sg_batch* b, bool silent) {
   const sg_nfa_desc& d = h->d;
   int64_t n = b->n;
   int32_t kmax = -1;
@@ -147,6 +356,7 @@ int hi_push(HiHandle* h, const sg_batch* b) {
     h->arenas[k].swap(last);
   }
   if (overflow) { h->err = SG_ECAPACITY; return SG_ECAPACITY; }
+  if (silent) return 0;
   std::vector<size_t> idx(count);
   for (size_t i = 0; i < count; ++i) idx[i] = i;
   auto sk = [&](size_t i) { uint64_t v; memcpy(&v, buf.data() + i * stride, 8); return v; };

@@ -16,7 +16,7 @@ def _load():
     global _lib
     if _lib is None:
         srcs = [os.path.join(HERE, "harness.cpp"), os.path.join(ROOT, "siddhi_amd", "csrc", "interp.h"),
-                os.path.join(ROOT, "siddhi_amd", "csrc", "sg_device.h")]
+                os.path.join(ROOT, "siddhi_amd", "csrc", "sg_device.h"), os.path.join(ROOT, "siddhi_amd", "csrc", "chain.h")]
         if not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(s) for s in srcs):
             os.makedirs(os.path.dirname(LIB), exist_ok=True)
             subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, srcs[0]], check=True)
@@ -31,12 +31,15 @@ def _load():
         lib.hi_count.argtypes = [P]
         lib.hi_fetch.argtypes = [P, P, P, P, P, P, P]
         lib.hi_set_chunk.argtypes = [P, ct.c_int]
+        lib.hi_set_pp.argtypes = [P, ct.c_int]
+        lib.hi_pp_rule.restype = ct.c_int
+        lib.hi_pp_rule.argtypes = [P]
         _lib = lib
     return _lib
 
 
 class HostInterpEngine:
-    def __init__(self, ctx, pool=256, chunk_rows=0):
+    def __init__(self, ctx, pool=256, chunk_rows=0, pp=True):
         from siddhi_amd import lowering as L
         from siddhi_amd import _native as N
         self.lib = _load()
@@ -46,6 +49,7 @@ class HostInterpEngine:
         self.nsel = len(self.nfa.select)
         self.h = self.lib.hi_open(ct.byref(self.desc), pool, pool, pool, pool)
         self.lib.hi_set_chunk(self.h, chunk_rows)
+        self.lib.hi_set_pp(self.h, 1 if pp else 0)   # partial lanes (chain.h) where sg_pp_rule allows, as the GPU
 
     def push(self, b):
         keep = []

@@ -99,6 +99,24 @@ def test_machine_multi_push_chunked(cfg):
     assert_same(got, want)
 
 
+COUNT_LAST = ("define stream S (id long, symbol string, v int, w int); "
+              "partition with (symbol of S) begin @info(name='q') "
+              "from every e1=S[v>500] -> e2=S[v>e1.v]<2:3> within 1 sec "
+              "select e1.id as i1, e2[0].id as i2a, e2[last].id as i2z insert into M; end;")
+
+
+@pytest.mark.parametrize("chunk", [0, 16])
+def test_count_state_ignores_within(chunk):
+    """A count state never checks `within` (CountPreStateProcessor.java:53-93): when it emits itself, a partial
+    older than `within` still completes, so such shapes must not be cut into time-horizon units."""
+    b = synth_batch("C3c", 0, 20_000, keys=20, rate=1)
+    b.key = dense_first_seen(b.key)
+    want = run_engine(OracleEngine, COUNT_LAST, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, chunk_rows=chunk), COUNT_LAST, [b])
+    assert len(want) > 0
+    assert_same(got, want)
+
+
 def test_chunk_rules():
     """Which shapes may be cut into units (horizon kind: 0 none, 1 `within`, 2 sequence event count)."""
     import ctypes as ct
@@ -116,6 +134,8 @@ def test_chunk_rules():
         assert lib.hi_chunk_rule(ct.byref(desc), ct.byref(h)) == kind, cfg
         if cfg == "C3b":
             assert h.value == 1 + 5 + 1 + 1
+    desc = N.build_desc(L.lower(context(COUNT_LAST)))
+    assert lib.hi_chunk_rule(ct.byref(desc), ct.byref(ct.c_int64(0))) == 0
 
 
 from ref_kats import REF_KATS, check, run_ref_kat  # noqa: E402

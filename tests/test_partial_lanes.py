@@ -1,0 +1,196 @@
+"""Partial lanes (siddhi_amd/csrc/chain.h, partial.hip): patterns whose partial matches never interact run one partial
+per lane, and the delivery order is rebuilt from each partial's insertion history.  The same chain.h code runs on the
+CPU here (tests/host_interp) against the oracle over a family of pattern shapes, value domains small enough to make
+ties, multi-push carries and a stream whose timestamps go back (the route hands its carried rows to the per-key
+machine).  GPU tests run the HIP route through the C-ABI against the oracle."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import OracleEngine
+from parity_util import assert_same, context, dense_first_seen, run_engine
+from siddhi_amd import _native as N
+from siddhi_amd import lowering as L
+from siddhi_amd import synth
+from siddhi_amd.runtime import Batch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "host_interp"))
+from host_engine import HostInterpEngine, _load  # noqa: E402
+
+HEAD = "define stream S (id long, symbol string, v int, w int); "
+PART = "partition with (symbol of S) begin @info(name='q') "
+SEL3 = " select e1.id as i1, e2.id as i2, e3.id as i3 insert into M; end;"
+
+SHAPES = {
+    "next": PART + "from every e1=S[v>50] -> e2=S[v>e1.v] within 40 milliseconds "
+                   "select e1.id as i1, e2.id as i2, e2.w as w2 insert into M; end;",
+    "next3": PART + "from every e1=S[v>40] -> e2=S[v>e1.v] -> e3=S[w<e1.w] within 60 milliseconds" + SEL3,
+    "count13": PART + "from every e1=S[v>30] -> e2=S[v>e1.v]<1:3> -> e3=S[v<e1.v] within 50 milliseconds "
+                      "select e1.id as i1, e2[0].id as a, e2[last].id as z, e3.id as i3 insert into M; end;",
+    "count22": PART + "from every e1=S[v>30] -> e2=S[v>=e1.v]<2:2> -> e3=S[v<e2[last].v] within 50 milliseconds "
+                      "select e1.id as i1, e2[0].id as a, e2[1].id as b, e3.id as i3 insert into M; end;",
+    "or": PART + "from every e1=S[v>50] -> e2=S[v>e1.v] or e3=S[w<e1.w] within 40 milliseconds" + SEL3,
+    "and": PART + "from every e1=S[v>50] -> e2=S[v>e1.v] and e3=S[w<e1.w] within 40 milliseconds" + SEL3,
+    "and_next": PART + "from every e1=S[v>50] -> e2=S[v>e1.v] and e3=S[w<e1.w] -> e4=S[v==e1.v] within 80 milliseconds "
+                       "select e1.id as i1, e2.id as i2, e3.id as i3, e4.id as i4 insert into M; end;",
+    "c3c": PART + "from every e1=S[v>50] -> e2=S[v>e1.v]<2:5> -> e3=S[v<e1.v] and e4=S[w<e1.w] within 60 milliseconds "
+                  "select e1.id as i1, e2[0].id as a, e2[last].id as z, e3.id as i3, e4.id as i4 insert into M; end;",
+    "count_or": PART + "from every e1=S[v>20] -> e2=S[v>e1.v]<1:4> -> e3=S[v<e1.v] or e4=S[w<e1.w] within 60 milliseconds "
+                       "select e1.id as i1, e2[0].id as a, e2[last].id as z, e3.id as i3, e4.id as i4 insert into M; end;",
+    "filter_cross": PART + "from every e1=S[v>50 and w<80] -> e2=S[w>e1.w and v<e1.v] -> e3=S[v+w>e2.v+e1.w] "
+                           "within 70 milliseconds select e1.id as i1, e2.id as i2, e3.id as i3, e3.v as v3 "
+                           "insert into M; end;",
+}
+UNPART = ("@info(name='q') from every e1=S[v>50] -> e2=S[v>e1.v]<1:3> -> e3=S[w<e1.w] within 15 milliseconds "
+          "select e1.id as i1, e2[last].id as z, e3.id as i3 insert into M;")
+
+
+def small_batch(n, keys, vmax, rate, seed, start=0, t0=0):
+    rng = np.random.default_rng(seed)
+    ts = (synth.T0 + t0 + (np.arange(start, start + n) // rate)).astype(np.int64)
+    key = dense_first_seen(rng.integers(0, keys, n).astype(np.int64)) if keys > 1 else np.zeros(n, np.int32)
+    v = (rng.integers(0, vmax, n) * (100 // vmax)).astype(np.int32)   # vmax 10: values 0, 10, .. 90 (many ties)
+    w = (rng.integers(0, vmax, n) * (100 // vmax)).astype(np.int32)
+    ids = np.arange(start, start + n, dtype=np.int64)
+    return Batch(n, start, ts, np.zeros(n, np.int32), key.astype(np.int32), [ids, key.astype(np.int32), v, w],
+                 [None] * 4)
+
+
+def split(b, cuts):
+    parts, lo = [], 0
+    for hi in list(cuts) + [b.n]:
+        parts.append(Batch(hi - lo, b.base_index + lo, b.ts[lo:hi], b.stream[lo:hi], b.key[lo:hi],
+                           [c[lo:hi] for c in b.cols], [None] * len(b.cols)))
+        lo = hi
+    return parts
+
+
+def test_rule_covers_the_shapes():
+    import ctypes as ct
+    lib = _load()
+    for name, q in SHAPES.items():
+        d = N.build_desc(L.lower(context(HEAD + q)))
+        assert lib.hi_pp_rule(ct.byref(d)) == 1, name
+    for cfg, ok in (("C3", 0), ("C3b", 0), ("C3c", 1), ("C4", 0)):
+        d = N.build_desc(L.lower(context(synth.QUERIES[cfg])))
+        assert lib.hi_pp_rule(ct.byref(d)) == ok, cfg
+
+
+@pytest.mark.parametrize("vmax", [10, 100])
+@pytest.mark.parametrize("name", sorted(SHAPES))
+def test_shapes_vs_oracle(name, vmax):
+    q = HEAD + SHAPES[name]
+    b = small_batch(20_000, 40, vmax, 4, seed=sum(name.encode()) + vmax)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, [b])
+    assert len(want) > 0
+    assert_same(got, want)
+
+
+@pytest.mark.parametrize("name", ["count13", "c3c", "and_next", "count_or"])
+def test_multi_push_carry(name):
+    q = HEAD + SHAPES[name]
+    b = small_batch(30_000, 25, 100, 4, seed=7)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(b, [1, 5000, 5001, 17_777, 29_000]))
+    assert_same(got, want)
+
+
+def test_unpartitioned():
+    q = HEAD + UNPART
+    b = small_batch(20_000, 1, 100, 2, seed=3)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(b, [7000]))
+    assert len(want) > 0
+    assert_same(got, want)
+
+
+def _going_back(q):
+    a = small_batch(10_000, 20, 100, 4, seed=11)
+    b = small_batch(10_000, 20, 100, 4, seed=12, start=10_000, t0=-40)   # starts 40 ms before a's end
+    b.key[:] = a.key[:10_000]
+    b.cols[1][:] = b.key
+    return Batch(20_000, 0, np.concatenate([a.ts, b.ts]), np.zeros(20_000, np.int32), np.concatenate([a.key, b.key]),
+                 [np.concatenate([x, y]) for x, y in zip(a.cols, b.cols)], [None] * 4)
+
+
+@pytest.mark.parametrize("name", ["next3", "and_next", "or"])
+def test_timestamps_going_back_leave_the_route(name):
+    """A push whose timestamps go back (per key) ends the route for count-free queries: the carried rows are replayed
+    silently through the per-key machine, which then continues -- output identical to the oracle on the stream."""
+    q = HEAD + SHAPES[name]
+    both = _going_back(q)
+    assert both.ts[10_000] < both.ts[9_999]
+    want = run_engine(OracleEngine, q, [both])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(both, [10_000, 15_000]))
+    assert len(want) > 0
+    assert_same(got, want)
+
+
+def test_timestamps_going_back_with_a_count_state():
+    """With a count state the carried rows cannot rebuild partials parked in it for longer than `within` (they never
+    expire, CountPreStateProcessor.java:53-93, and would be live again once time goes back): SG_EORDER, as the closed
+    forms do; the per-key machine (partial_lanes = -1) takes such streams."""
+    q = HEAD + SHAPES["c3c"]
+    both = _going_back(q)
+    with pytest.raises(RuntimeError, match="-5"):
+        run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(both, [10_000, 15_000]))
+    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=False), q, split(both, [10_000, 15_000])),
+                run_engine(OracleEngine, q, [both]))
+
+
+def test_c3c_config_slice():
+    q = synth.QUERIES["C3c"]
+    g = synth.generate("C3c", 0, 100_000, keys=500, rate=100)
+    b = Batch(100_000, 0, g["ts"], np.zeros(100_000, np.int32), dense_first_seen(g["key"]),
+              [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(b, [33_333, 66_666]))
+    assert_same(got, want)
+
+
+# ---- the HIP route through the C-ABI
+@pytest.mark.gpu
+@pytest.mark.parametrize("vmax", [10, 100])
+@pytest.mark.parametrize("name", sorted(SHAPES))
+def test_gpu_shapes(name, vmax):
+    from siddhi_amd._native import GpuEngine
+    q = HEAD + SHAPES[name]
+    b = small_batch(20_000, 40, vmax, 4, seed=sum(name.encode()) + vmax)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(b, [6_000, 6_001]))
+    assert_same(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_unpartitioned_and_order_fallback():
+    from siddhi_amd._native import GpuEngine, SgError
+    q = HEAD + UNPART
+    b = small_batch(20_000, 1, 100, 2, seed=3)
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(b, [7000])),
+                run_engine(OracleEngine, q, [b]))
+    q = HEAD + SHAPES["and_next"]
+    both = _going_back(q)
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(both, [10_000, 15_000])),
+                run_engine(OracleEngine, q, [both]))
+    q = HEAD + SHAPES["c3c"]
+    both = _going_back(q)
+    with pytest.raises(SgError):
+        run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(both, [10_000, 15_000]))
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=-1), q,
+                           split(both, [10_000, 15_000])),
+                run_engine(OracleEngine, q, [both]))
+
+
+@pytest.mark.gpu
+def test_gpu_c3c_slice_both_routes():
+    from siddhi_amd._native import GpuEngine
+    q = synth.QUERIES["C3c"]
+    g = synth.generate("C3c", 0, 200_000, keys=500, rate=100)
+    b = Batch(200_000, 0, g["ts"], np.zeros(200_000, np.int32), dense_first_seen(g["key"]),
+              [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
+    want = run_engine(OracleEngine, q, [b])
+    assert_same(run_engine(GpuEngine, q, split(b, [50_000, 123_457])), want)
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, partial_lanes=-1), q, [b]), want)
