@@ -18,7 +18,7 @@
 // records that history (`hist`) and the match records carry it as a tie-break key; a stable radix sort by
 // (trigger row, visit slot, history) restores the reference's delivery order exactly.
 //
-// State kept per lane (registers / scratch): each state's slot (row) or count chain, list membership bits for the
+// State kept per lane (LDS on the GPU): each state's slot (row) or count chain, list membership bits for the
 // pending (l0) and newAndEvery (l1) lists, the partial's timestamp, the per-state processor flags and the history.
 // Every method restates the KeyMachine method of interp.h with the same name (which cites its reference method).
 #pragma once
@@ -30,17 +30,74 @@
 #define SG_HD __host__ __device__
 #endif
 
+#define PP_MAX_S 8         // states of the query
 #define PP_MAX_CHAIN 16   // count-chain entries over all count states of the query
 #define PP_MAX_HIST 4     // insertions recorded (elements after the start state)
+#define PP_MAX_TERMS 4    // conjunctive compare terms of a filter evaluated without the VM
+
+// A filter that is a conjunction of `operand CMP operand` terms (operands: attribute or constant) is evaluated directly;
+// anything else runs on the postfix VM (sg_device.h).  Same semantics: sg_cmp per term, AND of the results.
+struct PpOperand {
+  int32_t kind;      // SG_OP_VAR or SG_OP_CONST
+  int32_t state, idx, slot, type;
+  int64_t bits;
+};
+struct PpTerm {
+  PpOperand l, r;
+  int32_t op, dom;
+};
 
 struct SgPpRule {
   int32_t ok;
   int32_t start;                      // the start state
   int32_t recv;                       // the single (multi) receiver
   int32_t n_hist;                     // tie components of an emission (= elements after the start)
-  int32_t coff[SG_MAX_STATES];        // count state -> offset of its chain in PpLane.chain
-  int32_t visit_rank[SG_MAX_STATES];  // state -> its slot in the receiver's visit order
+  uint32_t local_mask;                // states whose filter reads only the arriving event (precomputed bits)
+  int32_t coff[PP_MAX_S];             // count state -> offset of its chain in PpLane.chain
+  int32_t visit_rank[PP_MAX_S];       // state -> its slot in the receiver's visit order
+  int32_t nterm[PP_MAX_S];            // -1: the VM evaluates the state's filter
+  PpTerm term[PP_MAX_S][PP_MAX_TERMS];
 };
+
+// Parse a postfix filter into conjunctive compare terms (t1 t2 AND t3 AND ...); false if it has another form.
+SG_HD inline bool pp_operand(const int64_t* c, int len, int& pc, PpOperand& o) {
+  if (pc < len && c[pc] == SG_OP_VAR && pc + 5 <= len) {
+    o.kind = SG_OP_VAR;
+    o.state = (int32_t)c[pc + 1];
+    o.idx = (int32_t)c[pc + 2];
+    o.slot = (int32_t)c[pc + 3];
+    o.type = (int32_t)c[pc + 4];
+    o.bits = 0;
+    pc += 5;
+    return true;
+  }
+  if (pc < len && c[pc] == SG_OP_CONST && pc + 3 <= len) {
+    o.kind = SG_OP_CONST;
+    o.state = o.idx = o.slot = 0;
+    o.type = (int32_t)c[pc + 1];
+    o.bits = c[pc + 2];
+    pc += 3;
+    return true;
+  }
+  return false;
+}
+SG_HD inline int pp_terms(const int64_t* c, int len, PpTerm* t) {
+  int pc = 0, n = 0;
+  while (pc < len) {
+    if (n >= PP_MAX_TERMS) return -1;
+    if (!pp_operand(c, len, pc, t[n].l) || !pp_operand(c, len, pc, t[n].r)) return -1;
+    if (pc + 3 > len || c[pc] != SG_OP_CMP) return -1;
+    t[n].op = (int32_t)c[pc + 1];
+    t[n].dom = (int32_t)c[pc + 2];
+    pc += 3;
+    ++n;
+    if (n > 1) {
+      if (pc >= len || c[pc] != SG_OP_AND) return -1;
+      pc += 1;
+    }
+  }
+  return n;
+}
 
 // Which queries may run as partial lanes (checked at lowering-independent level, on the flat descriptor).
 SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
@@ -49,8 +106,9 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   r.start = -1;
   r.recv = -1;
   r.n_hist = 0;
-  for (int s = 0; s < SG_MAX_STATES; ++s) { r.coff[s] = -1; r.visit_rank[s] = -1; }
-  if (d.type != 0 || d.within < 0 || d.n_states < 2 || d.n_sched != 0) return r;
+  r.local_mask = 0;
+  for (int s = 0; s < PP_MAX_S; ++s) { r.coff[s] = -1; r.visit_rank[s] = -1; r.nterm[s] = -1; }
+  if (d.type != 0 || d.within < 0 || d.n_states < 2 || d.n_states > PP_MAX_S || d.n_sched != 0) return r;
   int nrecv = 0;
   for (int s = 0; s < SG_MAX_STREAMS; ++s)
     if (d.recv_of_stream[s] >= 0) { ++nrecv; r.recv = d.recv_of_stream[s]; }
@@ -62,6 +120,8 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   for (int s = 0; s < d.n_states; ++s) {
     const sg_state_desc& x = d.states[s];
     if (r.visit_rank[s] < 0) return r;
+    if (x.local) r.local_mask |= 1u << s;
+    else r.nterm[s] = pp_terms(d.code + x.prog_off, x.prog_len, r.term[s]);
     if (x.kind != SG_K_STREAM && x.kind != SG_K_COUNT && x.kind != SG_K_LOGICAL) return r;
     if (x.callback >= 0) return r;
     if (x.is_start) {
@@ -86,8 +146,8 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   return r;
 }
 
-// Tie key of an emission: bit 63 set for partial lanes (0: the carried-state machine, ordered by its own sequence),
-// then the history newest first, 31 bits per component, two components per word.
+// Tie key of an emission: the insertion history newest first, 31 bits per component (row << 4 | visit slot), two
+// components per word (bit 63 is always set).  Rows only need to be in arrival order within one key.
 SG_HD inline uint32_t pp_tkey(int64_t row, int rank) { return (uint32_t)(((uint64_t)row << 4) | (uint32_t)(rank & 15)); }
 
 // Src interface: int64_t ts(int64_t row); SgVal read(int64_t row, int ret_slot, int type);
@@ -97,8 +157,8 @@ struct PpLane {
   const sg_nfa_desc* d;
   const SgPpRule* ru;
   Src* src;
-  int32_t slot[SG_MAX_STATES];
-  int32_t clen[SG_MAX_STATES];
+  int32_t slot[PP_MAX_S];
+  int32_t clen[PP_MAX_S];
   int32_t chain[PP_MAX_CHAIN];
   uint32_t l0, l1;
   uint32_t f_changed, f_returned, f_success;
@@ -116,13 +176,13 @@ struct PpLane {
 
   // does the start state's armed partial accept this row (its filter, evaluated with e1 bound to the row)?
   SG_HD bool start_ok(int64_t row) {
-    for (int s = 0; s < SG_MAX_STATES; ++s) { slot[s] = -1; clen[s] = 0; }
+    for (int s = 0; s < PP_MAX_S; ++s) { slot[s] = -1; clen[s] = 0; }
     slot[ru->start] = (int32_t)row;
     cur_row = row;
     return filter(ru->start);
   }
   SG_HD void start(int64_t row) {   // the armed start partial takes e1 = row (process_and_return of the start state)
-    for (int s = 0; s < SG_MAX_STATES; ++s) { slot[s] = -1; clen[s] = 0; }
+    for (int s = 0; s < PP_MAX_S; ++s) { slot[s] = -1; clen[s] = 0; }
     l0 = l1 = 0;
     f_changed = f_returned = f_success = 0;
     nh = 0;
@@ -170,9 +230,24 @@ struct PpLane {
       return m->src->read(r, slotk, type);
     }
   };
+  SG_HD SgVal operand(const PpOperand& o) {
+    if (o.kind == SG_OP_CONST) return sg_val_from_bits(o.bits, o.type, 0);
+    Reader rd{this};
+    return rd.read(o.state, o.idx, o.slot, o.type);
+  }
   SG_HD bool filter(int s) {
-    const int b = src->lbit(s, cur_row);
-    if (b >= 0) return b != 0;
+    if ((ru->local_mask >> s) & 1u) {
+      const int b = src->lbit(s, cur_row);
+      if (b >= 0) return b != 0;
+    }
+    const int nt = ru->nterm[s];
+    if (nt >= 0) {
+      for (int i = 0; i < nt; ++i) {
+        const PpTerm& t = ru->term[s][i];
+        if (!sg_cmp(t.op, t.dom, operand(t.l), operand(t.r))) return false;
+      }
+      return true;
+    }
     Reader rd{this};
     return sg_eval(d->code + st(s).prog_off, st(s).prog_len, rd);
   }

@@ -136,20 +136,25 @@ struct PpArgs {
   int32_t any_bits;
 };
 
+// Key-ordered packed rows (position q = the q-th row of the key partition): what a lane reads at every step, so the
+// 64 lanes of a wave (consecutive start rows of one key) read neighbouring addresses.
+struct PpPacked {
+  int64_t* ts;
+  void* val[SG_MAX_RET];        // retained slot k: 4- or 8-byte bit patterns
+  int32_t wide[SG_MAX_RET];
+  uint32_t* nul;                // null mask over retained slots (nullptr: no nulls in this push)
+  uint32_t* lb;                 // condition bits of the event-local filters (rule.local_mask)
+};
+
 struct PpSrc {
-  const PpArgs* a;
-  const SgCols* bc;
-  const SgCols* cc;
-  const DevDesc* d;
-  __device__ int64_t ts(int64_t c) const { return c < a->nc ? a->cts[c] : a->bts[c - a->nc]; }
-  __device__ SgVal read(int64_t c, int slotk, int type) const {
-    const int col = d->ret_col[slotk];
-    return c < a->nc ? sg_read_col(*cc, col, type, c) : sg_read_col(*bc, col, type, c - a->nc);
+  const PpPacked* P;
+  __device__ int64_t ts(int64_t q) const { return P->ts[q]; }
+  __device__ SgVal read(int64_t q, int slotk, int type) const {
+    const int null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
+    const int64_t bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
+    return sg_val_from_bits(bits, type, null);
   }
-  __device__ int lbit(int s, int64_t c) const {
-    if (c < a->nc || !a->lbits[s]) return -1;
-    return (int)mask_bit(a->lbits[s], (uint64_t)(c - a->nc));
-  }
+  __device__ int lbit(int s, int64_t q) const { return (int)((P->lb[q] >> s) & 1u); }
 };
 
 __global__ void k_pp_route(PpArgs a, const DevDesc* __restrict__ dd, int partitioned, uint32_t sentinel,
@@ -205,23 +210,80 @@ struct PpOut {
 
 __device__ __forceinline__ uint64_t pp_index(const PpArgs& a, int64_t r) { return a.index ? a.index[r] : a.base_index + (uint64_t)r; }
 
-__global__ void __launch_bounds__(256) k_pp_lanes(PpArgs a, SgCols bc, SgCols cc, const DevDesc* __restrict__ ddg,
-                                                  const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ skey,
-                                                  const uint32_t* __restrict__ sid, const uint32_t* __restrict__ end,
-                                                  uint32_t sentinel, PpOut o) {
+// pack: key-ordered rows (ts, retained values, nulls, event-local condition bits) and the start-row flags
+__global__ void __launch_bounds__(256) k_pp_pack(PpArgs a, SgCols bc, SgCols cc, const DevDesc* dd,
+                                                 uint32_t local_mask, int start, const uint32_t* __restrict__ skey,
+                                                 const uint32_t* __restrict__ sid, uint32_t sentinel, PpPacked P,
+                                                 uint32_t* __restrict__ flag) {
+  __shared__ SgCols colsl[2];
   __shared__ DevDesc dl;
-  __shared__ SgPpRule rl;
-  __shared__ SgCols bcl, ccl;
-  __shared__ PpArgs al;
   {
     const uint32_t* s1 = (const uint32_t*)&bc;
     const uint32_t* s2 = (const uint32_t*)&cc;
-    const uint32_t* s3 = (const uint32_t*)&a;
     for (uint32_t i = threadIdx.x; i < sizeof(SgCols) / 4; i += blockDim.x) {
-      ((uint32_t*)&bcl)[i] = s1[i];
-      ((uint32_t*)&ccl)[i] = s2[i];
+      ((uint32_t*)&colsl[0])[i] = s1[i];
+      ((uint32_t*)&colsl[1])[i] = s2[i];
     }
-    for (uint32_t i = threadIdx.x; i < sizeof(PpArgs) / 4; i += blockDim.x) ((uint32_t*)&al)[i] = s3[i];
+    const uint32_t* src = (const uint32_t*)dd;
+    for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) ((uint32_t*)&dl)[i] = src[i];
+    __syncthreads();
+  }
+  dd = &dl;
+  const int64_t m = a.nc + a.n;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= m) return;
+  if (skey[q] == sentinel) { flag[q] = 0; return; }
+  const int64_t c = sid[q];
+  const bool carried = c < a.nc;
+  const int64_t r = carried ? c : c - a.nc;
+  const SgCols& cols = colsl[carried ? 1 : 0];
+  P.ts[q] = carried ? a.cts[r] : a.bts[r];
+  uint32_t nm = 0;
+  for (int k = 0; k < dd->n_ret; ++k) {
+    const SgVal v = sg_read_col(cols, dd->ret_col[k], dd->ret_type[k], r);
+    if (v.null) nm |= 1u << k;
+    const int64_t bits = sg_val_bits(v);
+    if (P.wide[k]) ((int64_t*)P.val[k])[q] = bits;
+    else ((int32_t*)P.val[k])[q] = (int32_t)bits;
+  }
+  if (P.nul) P.nul[q] = nm;
+  uint32_t lb = 0;
+  for (int s = 0; s < dd->n_states; ++s) {
+    if (!((local_mask >> s) & 1u)) continue;
+    const sg_state_desc& x = dd->states[s];
+    bool ok;
+    if (x.prog_len <= 0) ok = true;
+    else if (!carried && a.lbits[s]) ok = mask_bit(a.lbits[s], (uint64_t)r) != 0;
+    else {
+      RowReader rd{&cols, dd->ret_col, r};
+      ok = sg_eval(dd->code + x.prog_off, x.prog_len, rd);
+    }
+    if (ok) lb |= 1u << s;
+  }
+  P.lb[q] = lb;
+  flag[q] = (lb >> start) & 1u;
+}
+
+__global__ void k_pp_compact(int64_t m, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
+                             uint32_t* __restrict__ cand) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < m && flag[q]) cand[pos[q]] = (uint32_t)q;
+}
+
+constexpr int PP_BLOCK = 256;
+constexpr int64_t PP_WAVE_CANDS = 2048;   // start rows per wave
+__global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
+                                                       const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ cand,
+                                                       int64_t ncand, const uint32_t* __restrict__ skey,
+                                                       const uint32_t* __restrict__ sid, const uint32_t* __restrict__ end,
+                                                       PpOut o) {
+  __shared__ DevDesc dl;
+  __shared__ SgPpRule rl;
+  __shared__ PpPacked pl;
+  __shared__ PpLane<PpSrc> lanes[PP_BLOCK];
+  {
+    const uint32_t* s3 = (const uint32_t*)&P;
+    for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];
     const uint32_t* src = (const uint32_t*)ddg;
     uint32_t* dst = (uint32_t*)&dl;
     for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) dst[i] = src[i];
@@ -231,52 +293,87 @@ __global__ void __launch_bounds__(256) k_pp_lanes(PpArgs a, SgCols bc, SgCols cc
     __syncthreads();
   }
   const DevDesc* dd = &dl;
-  const int64_t m = a.nc + a.n;
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= m) return;
-  const uint32_t k = skey[p];
-  if (k == sentinel) return;
-  PpSrc src{&al, &bcl, &ccl, dd};
-  PpLane<PpSrc> L;
+  // each wave owns PP_WAVE_CANDS consecutive start rows; a lane whose partial is finished takes the next one, so the
+  // wave never waits on its longest partial (ballot + popcount hand-out, no atomics)
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t lo = wave * PP_WAVE_CANDS;
+  const int64_t hi = lo + PP_WAVE_CANDS < ncand ? lo + PP_WAVE_CANDS : ncand;
+  if (lo >= ncand) return;
+  PpSrc src{&pl};
+  PpLane<PpSrc>& L = lanes[threadIdx.x];
   L.d = dd;
   L.ru = &rl;
   L.src = &src;
-  const int64_t c0 = sid[p];
-  if (!L.start_ok(c0)) return;
-  L.start(c0);
-  const int64_t e = end[k];
-  for (int64_t q = p + 1; q < e; ++q) {
-    const int64_t c = sid[q];
-    if (src.ts(c) - L.e1_ts > dd->within) break;   // expired everywhere it can still emit (sg_pp_rule)
-    const int em = L.step(c);
-    if (L.overflow) { atomicCAS(o.fail, 0, SG_EUNSUPPORTED); return; }
-    if (em >= 0 && c >= a.nc) {
-      const unsigned long long w = atomicAdd(o.count, 1ull);
-      const int64_t r = c - a.nc;
-      o.k1[w] = ((uint64_t)r << 8) | (uint32_t)em;
-      L.tie(o.th[w], o.tl[w]);
-      char* rec = o.rec + (size_t)w * (size_t)o.rstride;
-      uint64_t* h64 = (uint64_t*)rec;
-      h64[0] = pp_index(a, r);
-      h64[1] = (uint64_t)L.pts;
-      uint32_t* h32 = (uint32_t*)(rec + 16);
-      h32[0] = k;
-      h32[1] = (1u << 24) | (uint32_t)em;
-      uint32_t nm = 0;
-      int64_t* vals = (int64_t*)(rec + 32);
-      for (int s = 0; s < dd->n_select; ++s) {
-        const int64_t ev = L.get_event(dd->sel_state[s], dd->sel_index[s]);
-        const int rs = dd->sel_ret[s];
-        SgVal v;
-        if (ev < 0) { nm |= 1u << s; vals[s] = 0; continue; }
-        v = src.read(ev, rs, dd->ret_type[rs]);
-        if (v.null) { nm |= 1u << s; vals[s] = 0; continue; }
-        vals[s] = sg_val_bits(v);
+  const int64_t within = dd->within;
+  int64_t nxt = lo + 64;   // wave-uniform
+  int64_t i = lo + lane;
+  bool active = i < hi;
+  int64_t q = 0, e = 0;
+  uint32_t k = 0;
+  if (active) {
+    const int64_t p = cand[i];
+    k = skey[p];
+    L.start(p);
+    q = p + 1;
+    e = end[k];
+  }
+  const uint64_t lt = (1ull << lane) - 1ull;
+  while (__ballot(active)) {
+    bool done = false;
+    if (active) {
+      if (q >= e || src.ts(q) - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
+        done = true;
+      } else {
+        const int em = L.step(q);
+        if (L.overflow) atomicCAS(o.fail, 0, SG_EUNSUPPORTED);
+        if (em >= 0) {
+          const int64_t c = sid[q];
+          if (c >= a.nc) {
+            const unsigned long long w = atomicAdd(o.count, 1ull);
+            const int64_t r = c - a.nc;
+            o.k1[w] = ((uint64_t)r << 8) | (uint32_t)em;
+            L.tie(o.th[w], o.tl[w]);
+            char* rec = o.rec + (size_t)w * (size_t)o.rstride;
+            uint64_t* h64 = (uint64_t*)rec;
+            h64[0] = pp_index(a, r);
+            h64[1] = (uint64_t)L.pts;
+            uint32_t* h32 = (uint32_t*)(rec + 16);
+            h32[0] = k;
+            h32[1] = (1u << 24) | (uint32_t)em;
+            uint32_t nm = 0;
+            int64_t* vals = (int64_t*)(rec + 32);
+            for (int s = 0; s < dd->n_select; ++s) {
+              const int64_t ev = L.get_event(dd->sel_state[s], dd->sel_index[s]);
+              const int rs = dd->sel_ret[s];
+              if (ev < 0) { nm |= 1u << s; vals[s] = 0; continue; }
+              const SgVal v = src.read(ev, rs, dd->ret_type[rs]);
+              if (v.null) { nm |= 1u << s; vals[s] = 0; continue; }
+              vals[s] = sg_val_bits(v);
+            }
+            h32[2] = nm;
+            h32[3] = 0;
+          }
+        }
+        ++q;
+        done = L.dead() || L.overflow;
       }
-      h32[2] = nm;
-      h32[3] = 0;
     }
-    if (L.dead()) break;
+    const uint64_t dm = __ballot(done);
+    if (dm) {
+      if (done) {
+        i = nxt + __popcll(dm & lt);
+        active = i < hi;
+        if (active) {
+          const int64_t p = cand[i];
+          k = skey[p];
+          L.start(p);
+          q = p + 1;
+          e = end[k];
+        }
+      }
+      nxt += __popcll(dm);
+    }
   }
 }
 
@@ -473,10 +570,45 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     }
     if (any) h->kend();
   }
+  // ---- key-ordered packed rows, start rows
+  PpPacked P;
+  memset(&P, 0, sizeof(P));
+  bool any_nul = false;
+  for (int k = 0; k < d.n_ret; ++k) {
+    const int c = d.ret_col[k];
+    any_nul |= bv.cols.nul[c] != nullptr || (nc > 0 && cc.nul[c] != nullptr);
+  }
+  P.ts = (int64_t*)h->ws.get("pp_qts", 8 * m, st);
+  for (int k = 0; k < d.n_ret; ++k) {
+    P.wide[k] = (d.ret_type[k] == SG_T_LONG || d.ret_type[k] == SG_T_DOUBLE) ? 1 : 0;
+    P.val[k] = h->ws.get("pp_qv" + std::to_string(k), (P.wide[k] ? 8 : 4) * m, st);
+  }
+  P.nul = any_nul ? (uint32_t*)h->ws.get("pp_qnul", 4 * m, st) : nullptr;
+  P.lb = (uint32_t*)h->ws.get("pp_qlb", 4 * m, st);
+  uint32_t* flag = (uint32_t*)h->ws.get("pp_flag", 4 * (m + 1), st);
+  uint32_t* fpos = (uint32_t*)h->ws.get("pp_fpos", 4 * (m + 1), st);
+  uint32_t* cand = (uint32_t*)h->ws.get("pp_cand", 4 * (m + 1), st);
+  h->kbeg("pack");
+  if (m) hipLaunchKernelGGL(k_pp_pack, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->rule.local_mask, ps->rule.start,
+                            skeys, sids, sentinel, P, flag);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemsetAsync(flag + m, 0, 4, st));
+  {
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, flag, fpos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("pp_fscan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, flag, fpos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
+  }
+  if (m) hipLaunchKernelGGL(k_pp_compact, grd, blk, 0, st, m, flag, fpos, cand);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  uint32_t ncand = 0;
+  HIPCHK(hipMemcpyAsync(&ncand, fpos + m, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   // ---- partial lanes
   const int nsel = d.n_select;
   const int32_t rstride = 32 + 8 * nsel;
-  const int64_t cap = std::max<int64_t>(m, 1);   // a partial completes at most once (sg_pp_rule)
+  const int64_t cap = std::max<int64_t>(ncand, 1);   // a partial completes at most once (sg_pp_rule)
   PpOut o;
   o.rec = (char*)h->ws.get("pp_rec", (size_t)cap * rstride, st);
   o.k1 = (uint64_t*)h->ws.get("pp_k1", 8 * cap, st);
@@ -487,8 +619,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   o.rstride = rstride;
   HIPCHK(hipMemsetAsync(o.count, 0, 8, st));
   h->kbeg("partial_lanes");
-  if (m)
-    hipLaunchKernelGGL(k_pp_lanes, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->drule, skeys, sids, end, sentinel, o);
+  if (ncand)
+    hipLaunchKernelGGL(k_pp_lanes, dim3((unsigned)((ncand + PP_WAVE_CANDS * (PP_BLOCK / 64) - 1) / (PP_WAVE_CANDS * (PP_BLOCK / 64)))),
+                       dim3(PP_BLOCK), 0, st, a, P,
+                       h->ddesc, ps->drule, cand, (int64_t)ncand, skeys, sids, end, o);
   HIPCHK(hipGetLastError());
   h->kend();
   h->mark(3);
