@@ -152,19 +152,24 @@ SG_HD inline uint32_t pp_tkey(int64_t row, int rank) { return (uint32_t)(((uint6
 
 // Src interface: int64_t ts(int64_t row); SgVal read(int64_t row, int ret_slot, int type);
 //                int lbit(int state, int64_t row) -> 0/1, or -1 when the state's filter must be evaluated.
+// The dynamically indexed part of a lane's state (LDS on the GPU); the rest stays in registers.
+struct PpArrays {
+  int32_t slot[PP_MAX_S];
+  int32_t chain[PP_MAX_CHAIN];
+  uint32_t hist[PP_MAX_HIST];
+  int8_t clen[PP_MAX_S];
+};
+
 template <class Src>
 struct PpLane {
   const sg_nfa_desc* d;
   const SgPpRule* ru;
-  Src* src;
-  int32_t slot[PP_MAX_S];
-  int32_t clen[PP_MAX_S];
-  int32_t chain[PP_MAX_CHAIN];
+  Src src;
+  PpArrays* A;
   uint32_t l0, l1;
   uint32_t f_changed, f_returned, f_success;
   int64_t pts;
   int64_t e1_ts;
-  uint32_t hist[PP_MAX_HIST];
   int32_t nh;
   int32_t overflow;
   // current row
@@ -176,33 +181,33 @@ struct PpLane {
 
   // does the start state's armed partial accept this row (its filter, evaluated with e1 bound to the row)?
   SG_HD bool start_ok(int64_t row) {
-    for (int s = 0; s < PP_MAX_S; ++s) { slot[s] = -1; clen[s] = 0; }
-    slot[ru->start] = (int32_t)row;
+    for (int s = 0; s < PP_MAX_S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
+    A->slot[ru->start] = (int32_t)row;
     cur_row = row;
     return filter(ru->start);
   }
   SG_HD void start(int64_t row) {   // the armed start partial takes e1 = row (process_and_return of the start state)
-    for (int s = 0; s < PP_MAX_S; ++s) { slot[s] = -1; clen[s] = 0; }
+    for (int s = 0; s < PP_MAX_S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
     l0 = l1 = 0;
     f_changed = f_returned = f_success = 0;
     nh = 0;
     overflow = 0;
     cur_row = row;
     cur_rank = ru->visit_rank[ru->start];
-    slot[ru->start] = (int32_t)row;
-    e1_ts = src->ts(row);
+    A->slot[ru->start] = (int32_t)row;
+    e1_ts = src.ts(row);
     stream_post(ru->start);   // the `every` clone it also makes stays behind in the start state's lists
   }
 
   // ---- event access (KeyMachine::get_event): row of (state, index in chain) or -1
   SG_HD int64_t get_event(int s, int idx) {
     if (st(s).kind != SG_K_COUNT) {
-      if (slot[s] < 0) return -1;
-      return (idx == 0 || idx == -1) ? slot[s] : -1;
+      if (A->slot[s] < 0) return -1;
+      return (idx == 0 || idx == -1) ? A->slot[s] : -1;
     }
-    const int n = clen[s];
+    const int n = A->clen[s];
     if (n == 0) return -1;
-    const int32_t* c = chain + ru->coff[s];
+    const int32_t* c = A->chain + ru->coff[s];
     int k;
     if (idx >= 0) k = idx;
     else if (idx == -1) k = n - 1;
@@ -212,8 +217,8 @@ struct PpLane {
     return c[k];
   }
   SG_HD int64_t slot_ts(int s) {
-    int64_t r = st(s).kind == SG_K_COUNT ? (clen[s] ? chain[ru->coff[s]] : -1) : slot[s];
-    return src->ts(r);
+    int64_t r = st(s).kind == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
+    return src.ts(r);
   }
   struct Reader {
     PpLane* m;
@@ -227,7 +232,7 @@ struct PpLane {
         v.null = 1;
         return v;
       }
-      return m->src->read(r, slotk, type);
+      return m->src.read(r, slotk, type);
     }
   };
   SG_HD SgVal operand(const PpOperand& o) {
@@ -237,7 +242,7 @@ struct PpLane {
   }
   SG_HD bool filter(int s) {
     if ((ru->local_mask >> s) & 1u) {
-      const int b = src->lbit(s, cur_row);
+      const int b = src.lbit(s, cur_row);
       if (b >= 0) return b != 0;
     }
     const int nt = ru->nterm[s];
@@ -262,9 +267,9 @@ struct PpLane {
   }
   SG_HD void count_post(int s) {
     const sg_state_desc& x = st(s);
-    const int n = clen[s];
+    const int n = A->clen[s];
     f_success |= bit(s);
-    pts = src->ts(chain[ru->coff[s] + n - 1]);
+    pts = src.ts(A->chain[ru->coff[s] + n - 1]);
     if (n >= x.min_count) {
       if (n == x.min_count && x.next_state >= 0) add_state(x.next_state);   // count_min_reached (no selector)
       if (n == x.max_count) f_changed |= bit(s);
@@ -273,7 +278,7 @@ struct PpLane {
   SG_HD void logical_post(int s) {
     const sg_state_desc& x = st(s);
     if (x.logical_type == 0) {
-      if (slot[x.partner] >= 0) stream_post(s);
+      if (A->slot[x.partner] >= 0) stream_post(s);
       else f_changed |= bit(s);
     } else {
       stream_post(s);
@@ -281,7 +286,7 @@ struct PpLane {
   }
   SG_HD void add_state(int s) {
     const sg_state_desc& x = st(s);
-    if (nh < PP_MAX_HIST) hist[nh++] = pp_tkey(cur_row, cur_rank);
+    if (nh < PP_MAX_HIST) A->hist[nh++] = pp_tkey(cur_row, cur_rank);
     else overflow = 1;
     l1 |= bit(s);
     if (x.kind == SG_K_LOGICAL) l1 |= bit(x.partner);
@@ -300,7 +305,7 @@ struct PpLane {
     const uint32_t moved = l1;
     l0 |= moved;
     l1 = 0;
-    const int64_t t = src->ts(row);
+    const int64_t t = src.ts(row);
     int emitted = -1;
     for (int k = 0; k < rv.n; ++k) {
       const int s = rv.pres[rv.n - 1 - k];
@@ -313,17 +318,17 @@ struct PpLane {
           l0 &= ~bit(s);
           continue;
         }
-        if (clen[s] >= st(s).max_count) { overflow = 1; return -1; }
-        chain[ru->coff[s] + clen[s]++] = (int32_t)row;
+        if (A->clen[s] >= st(s).max_count) { overflow = 1; return -1; }
+        A->chain[ru->coff[s] + A->clen[s]++] = (int32_t)row;
         f_success &= ~bit(s);
         f_changed &= ~bit(s);
         if (filter(s)) count_post(s);
         if (f_changed & bit(s)) remove = true;
-        if (!(f_success & bit(s))) --clen[s];
+        if (!(f_success & bit(s))) --A->clen[s];
       } else {
         if (is_expired(t)) { l0 &= ~bit(s); continue; }
-        if (x.kind == SG_K_LOGICAL && x.logical_type == 1 && slot[x.partner] >= 0) { l0 &= ~bit(s); continue; }
-        slot[s] = (int32_t)row;
+        if (x.kind == SG_K_LOGICAL && x.logical_type == 1 && A->slot[x.partner] >= 0) { l0 &= ~bit(s); continue; }
+        A->slot[s] = (int32_t)row;
         f_changed &= ~bit(s);
         if (filter(s)) {
           if (x.kind == SG_K_LOGICAL) logical_post(s);
@@ -335,19 +340,19 @@ struct PpLane {
           else overflow = 1;
         }
         if (f_changed & bit(s)) remove = true;
-        else slot[s] = -1;
+        else A->slot[s] = -1;
       }
       if (remove) l0 &= ~bit(s);
     }
     return emitted;
   }
-  SG_HD bool get_any(int s) { return st(s).kind == SG_K_COUNT ? clen[s] > 0 : slot[s] >= 0; }
+  SG_HD bool get_any(int s) { return st(s).kind == SG_K_COUNT ? A->clen[s] > 0 : A->slot[s] >= 0; }
   SG_HD bool dead() const { return (l0 | l1) == 0; }
 
   // tie words of an emission (bit 63: partial lane)
   SG_HD void tie(uint64_t& hi, uint64_t& lo) const {
     uint32_t c[PP_MAX_HIST] = {0, 0, 0, 0};
-    for (int i = 0; i < nh; ++i) c[i] = hist[nh - 1 - i] & 0x7FFFFFFFu;
+    for (int i = 0; i < nh; ++i) c[i] = A->hist[nh - 1 - i] & 0x7FFFFFFFu;
     hi = (1ull << 63) | ((uint64_t)c[0] << 31) | c[1];
     lo = ((uint64_t)c[2] << 31) | c[3];
   }

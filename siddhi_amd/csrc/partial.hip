@@ -206,6 +206,7 @@ struct PpOut {
   unsigned long long* count;
   int32_t* fail;
   int32_t rstride;
+  uint64_t k1_none;           // k1 of a start row without a match (above every (row << 8 | slot) of this push)
 };
 
 __device__ __forceinline__ uint64_t pp_index(const PpArgs& a, int64_t r) { return a.index ? a.index[r] : a.base_index + (uint64_t)r; }
@@ -280,7 +281,7 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
   __shared__ DevDesc dl;
   __shared__ SgPpRule rl;
   __shared__ PpPacked pl;
-  __shared__ PpLane<PpSrc> lanes[PP_BLOCK];
+  __shared__ PpArrays lanes[PP_BLOCK];
   {
     const uint32_t* s3 = (const uint32_t*)&P;
     for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];
@@ -301,10 +302,11 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
   const int64_t hi = lo + PP_WAVE_CANDS < ncand ? lo + PP_WAVE_CANDS : ncand;
   if (lo >= ncand) return;
   PpSrc src{&pl};
-  PpLane<PpSrc>& L = lanes[threadIdx.x];
+  PpLane<PpSrc> L;
   L.d = dd;
   L.ru = &rl;
-  L.src = &src;
+  L.src = src;
+  L.A = &lanes[threadIdx.x];
   const int64_t within = dd->within;
   int64_t nxt = lo + 64;   // wave-uniform
   int64_t i = lo + lane;
@@ -319,6 +321,8 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
     e = end[k];
   }
   const uint64_t lt = (1ull << lane) - 1ull;
+  bool emitted = false;
+  uint32_t nemit = 0;
   while (__ballot(active)) {
     bool done = false;
     if (active) {
@@ -330,7 +334,9 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
         if (em >= 0) {
           const int64_t c = sid[q];
           if (c >= a.nc) {
-            const unsigned long long w = atomicAdd(o.count, 1ull);
+            // a partial completes at most once (sg_pp_rule): its match record goes to its start row's slot
+            const int64_t w = i;
+            emitted = true;
             const int64_t r = c - a.nc;
             o.k1[w] = ((uint64_t)r << 8) | (uint32_t)em;
             L.tie(o.th[w], o.tl[w]);
@@ -362,6 +368,9 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
     const uint64_t dm = __ballot(done);
     if (dm) {
       if (done) {
+        if (emitted) ++nemit;
+        else o.k1[i] = o.k1_none;   // no match: sorts behind every match
+        emitted = false;
         i = nxt + __popcll(dm & lt);
         active = i < hi;
         if (active) {
@@ -375,6 +384,8 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
       nxt += __popcll(dm);
     }
   }
+  for (int off = 32; off > 0; off >>= 1) nemit += __shfl_down(nemit, off, 64);
+  if (lane == 0 && nemit) atomicAdd(o.count, (unsigned long long)nemit);
 }
 
 __global__ void k_pp_iota(int64_t n, uint32_t* __restrict__ x) {
@@ -617,6 +628,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   o.count = (unsigned long long*)h->ws.get("pp_count", 8, st);
   o.fail = err + 1;
   o.rstride = rstride;
+  int rb = 1;
+  while ((1ll << rb) < n + 1) ++rb;
+  const int k1_bits = std::min(64, rb + 8);
+  o.k1_none = k1_bits >= 64 ? ~0ull : (1ull << k1_bits) - 1;
   HIPCHK(hipMemsetAsync(o.count, 0, 8, st));
   h->kbeg("partial_lanes");
   if (ncand)
@@ -634,7 +649,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   if (fail) throw SgError(fail, "partial lane capacity exceeded (query outside the route's shape)");
   // ---- delivery order: LSD stable sorts (tie low word, tie high word, then trigger row and visit slot)
   if (total) {
-    const int64_t T = (int64_t)total;
+    const int64_t T = (int64_t)ncand;   // one slot per start row; rows without a match sort behind (k1 = ~0)
     const dim3 g2((unsigned)((T + 255) / 256));
     uint32_t* ia = (uint32_t*)h->ws.get("pp_ia", 4 * T, st);
     uint32_t* ib = (uint32_t*)h->ws.get("pp_ib", 4 * T, st);
@@ -655,15 +670,15 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     sort_pairs64(h, "hi", ka, kb2, ia, ib, T, 64);
     std::swap(ia, ib);
     hipLaunchKernelGGL(k_pp_take, g2, blk, 0, st, T, o.k1, ia, ka);
-    int rb = 1;
-    while ((1ll << rb) < n) ++rb;
-    sort_pairs64(h, "k1", ka, kb2, ia, ib, T, std::min(64, rb + 8));
+    sort_pairs64(h, "k1", ka, kb2, ia, ib, T, k1_bits);
     std::swap(ia, ib);
-    char* out = h->out.reserve(T, nsel, st);
-    hipLaunchKernelGGL(k_pp_gather, g2, blk, 0, st, T, o.rec, ia, rstride, out + (size_t)h->out.n * rstride);
+    const int64_t M = (int64_t)total;
+    char* out = h->out.reserve(M, nsel, st);
+    hipLaunchKernelGGL(k_pp_gather, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, o.rec, ia, rstride,
+                       out + (size_t)h->out.n * rstride);
     HIPCHK(hipGetLastError());
     h->kend();
-    h->out.n += T;
+    h->out.n += M;
   }
   // ---- carry
   if (!h->opt.no_carry && m) {

@@ -132,9 +132,11 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
     const auto& rows = own[k];
     for (size_t p = 0; p < rows.size(); ++p) {
       PpLane<HostPpSrc> L;
+      PpArrays arr;
       L.d = &d;
       L.ru = &ru;
-      L.src = &src;
+      L.src = src;
+      L.A = &arr;
       if (!L.start_ok(rows[p])) continue;
       L.start(rows[p]);
       for (size_t q = p + 1; q < rows.size(); ++q) {
