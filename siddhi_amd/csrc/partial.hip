@@ -205,6 +205,8 @@ struct PpOut {
   uint64_t* tl;
   unsigned long long* count;
   int32_t* fail;
+  uint32_t* jp;               // sorted position of the trigger row
+  uint32_t* maxoff;           // largest (trigger position - start position) of a match
   int32_t rstride;
   uint64_t k1_none;           // k1 of a start row without a match (above every (row << 8 | slot) of this push)
 };
@@ -311,18 +313,19 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
   int64_t nxt = lo + 64;   // wave-uniform
   int64_t i = lo + lane;
   bool active = i < hi;
-  int64_t q = 0, e = 0;
+  int64_t q = 0, e = 0, p0 = 0;
   uint32_t k = 0;
   if (active) {
     const int64_t p = cand[i];
     k = skey[p];
     L.start(p);
     q = p + 1;
+    p0 = p;
     e = end[k];
   }
   const uint64_t lt = (1ull << lane) - 1ull;
   bool emitted = false;
-  uint32_t nemit = 0;
+  uint32_t nemit = 0, maxoff = 0;
   while (__ballot(active)) {
     bool done = false;
     if (active) {
@@ -340,6 +343,9 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
             const int64_t r = c - a.nc;
             o.k1[w] = ((uint64_t)r << 8) | (uint32_t)em;
             L.tie(o.th[w], o.tl[w]);
+            o.jp[w] = (uint32_t)q;
+            const uint32_t off = (uint32_t)(q - p0);
+            maxoff = off > maxoff ? off : maxoff;
             char* rec = o.rec + (size_t)w * (size_t)o.rstride;
             uint64_t* h64 = (uint64_t*)rec;
             h64[0] = pp_index(a, r);
@@ -378,14 +384,43 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
           k = skey[p];
           L.start(p);
           q = p + 1;
+          p0 = p;
           e = end[k];
         }
       }
       nxt += __popcll(dm);
     }
   }
-  for (int off = 32; off > 0; off >>= 1) nemit += __shfl_down(nemit, off, 64);
-  if (lane == 0 && nemit) atomicAdd(o.count, (unsigned long long)nemit);
+  for (int off = 32; off > 0; off >>= 1) {
+    nemit += __shfl_down(nemit, off, 64);
+    const uint32_t x = __shfl_down(maxoff, off, 64);
+    maxoff = x > maxoff ? x : maxoff;
+  }
+  if (lane == 0 && nemit) {
+    atomicAdd(o.count, (unsigned long long)nemit);
+    atomicMax(o.maxoff, maxoff);
+  }
+}
+
+// One 64-bit delivery key per match when it fits: (trigger row, visit slot), then the insertion history as offsets
+// back from the trigger's position (a later insertion = a smaller offset), newest first.
+__global__ void k_pp_key(int64_t n, const uint64_t* __restrict__ k1, const uint64_t* __restrict__ th,
+                         const uint64_t* __restrict__ tl, const uint32_t* __restrict__ jp, uint64_t k1_none, int n_hist,
+                         uint32_t maxoff, int ob, uint64_t none, uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  idx[i] = (uint32_t)i;
+  const uint64_t a = k1[i];
+  if (a == k1_none) { key[i] = none; return; }
+  uint64_t x = ((a >> 8) << 4) | (a & 15u);
+  const uint32_t J = jp[i];
+  for (int j = 0; j < n_hist; ++j) {
+    const uint64_t w = j < 2 ? th[i] : tl[i];
+    const uint32_t c = (uint32_t)((j & 1) ? (w & 0x7FFFFFFFu) : ((w >> 31) & 0x7FFFFFFFu));
+    const uint32_t off = J - (c >> 4);
+    x = (x << (ob + 4)) | ((uint64_t)(maxoff - off) << 4) | (c & 15u);
+  }
+  key[i] = x;
 }
 
 __global__ void k_pp_iota(int64_t n, uint32_t* __restrict__ x) {
@@ -625,14 +660,16 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   o.k1 = (uint64_t*)h->ws.get("pp_k1", 8 * cap, st);
   o.th = (uint64_t*)h->ws.get("pp_th", 8 * cap, st);
   o.tl = (uint64_t*)h->ws.get("pp_tl", 8 * cap, st);
-  o.count = (unsigned long long*)h->ws.get("pp_count", 8, st);
+  o.count = (unsigned long long*)h->ws.get("pp_count", 16, st);
+  o.maxoff = (uint32_t*)(o.count + 1);
+  o.jp = (uint32_t*)h->ws.get("pp_jp", 4 * cap, st);
   o.fail = err + 1;
   o.rstride = rstride;
   int rb = 1;
   while ((1ll << rb) < n + 1) ++rb;
   const int k1_bits = std::min(64, rb + 8);
   o.k1_none = k1_bits >= 64 ? ~0ull : (1ull << k1_bits) - 1;
-  HIPCHK(hipMemsetAsync(o.count, 0, 8, st));
+  HIPCHK(hipMemsetAsync(o.count, 0, 16, st));
   h->kbeg("partial_lanes");
   if (ncand)
     hipLaunchKernelGGL(k_pp_lanes, dim3((unsigned)((ncand + PP_WAVE_CANDS * (PP_BLOCK / 64) - 1) / (PP_WAVE_CANDS * (PP_BLOCK / 64)))),
@@ -642,8 +679,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   h->kend();
   h->mark(3);
   unsigned long long total = 0;
+  uint32_t hmaxoff = 0;
   int32_t fail = 0;
   HIPCHK(hipMemcpyAsync(&total, o.count, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&hmaxoff, o.maxoff, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&fail, o.fail, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (fail) throw SgError(fail, "partial lane capacity exceeded (query outside the route's shape)");
@@ -656,6 +695,16 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     uint64_t* ka = (uint64_t*)h->ws.get("pp_ka", 8 * T, st);
     uint64_t* kb2 = (uint64_t*)h->ws.get("pp_kb", 8 * T, st);
     h->kbeg("match_order");
+    int ob = 1;
+    while ((1ull << ob) <= (uint64_t)hmaxoff) ++ob;
+    const int need = rb + 4 + ps->rule.n_hist * (ob + 4);
+    if (need <= 63) {   // one radix sort over a single composed key
+      const uint64_t none = (1ull << need) - 1;
+      hipLaunchKernelGGL(k_pp_key, g2, blk, 0, st, T, o.k1, o.th, o.tl, o.jp, o.k1_none, ps->rule.n_hist, hmaxoff, ob,
+                         none, ka, ia);
+      sort_pairs64(h, "one", ka, kb2, ia, ib, T, need);
+      std::swap(ia, ib);
+    } else {
     hipLaunchKernelGGL(k_pp_iota, g2, blk, 0, st, T, ia);
     int tb = 1;
     while ((1ll << tb) < m) ++tb;
@@ -672,6 +721,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     hipLaunchKernelGGL(k_pp_take, g2, blk, 0, st, T, o.k1, ia, ka);
     sort_pairs64(h, "k1", ka, kb2, ia, ib, T, k1_bits);
     std::swap(ia, ib);
+    }
     const int64_t M = (int64_t)total;
     char* out = h->out.reserve(M, nsel, st);
     hipLaunchKernelGGL(k_pp_gather, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, o.rec, ia, rstride,

@@ -185,6 +185,17 @@ def test_gpu_unpartitioned_and_order_fallback():
 
 
 @pytest.mark.gpu
+def test_gpu_long_history_sort_path():
+    """Matches whose insertion history does not fit one 64-bit delivery key (long windows, three insertions) are
+    ordered by the multi-pass stable sort instead."""
+    from siddhi_amd._native import GpuEngine
+    q = HEAD + ("@info(name='q') from every e1=S[v>80] -> e2=S[v>e1.v] -> e3=S[w>e1.w] -> e4=S[v<e1.v] within 1 hour "
+                "select e1.id as i1, e2.id as i2, e3.id as i3, e4.id as i4 insert into M;")
+    b = small_batch(40_000, 1, 100, 4, seed=5)
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, [b]), run_engine(OracleEngine, q, [b]))
+
+
+@pytest.mark.gpu
 def test_gpu_c3c_slice_both_routes():
     from siddhi_amd._native import GpuEngine
     q = synth.QUERIES["C3c"]
