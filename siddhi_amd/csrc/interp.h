@@ -987,10 +987,6 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t em
 //   at that row (StreamPreStateProcessor.isExpired, C/query/input/stream/state/
 //   StreamPreStateProcessor.java:102-113) and can neither advance nor emit again, so the rows with
 //   ts >= ts(first) - T rebuild every live partial;
-//   single-stream sequences whose start states re-arm with `every` and whose counts are bounded: every
-//   event resets the partials that did not advance on it (StateStreamRuntime.resetAndUpdate,
-//   C/query/input/stream/state/StateStreamRuntime.java:96-99), so a live partial is at most
-//   sum(max count or 1) events old.
 // Absence (timers on the global clock) is never chunked.
 struct SgChunkRule {
   int kind;            // 0 none, 1 time horizon, 2 event horizon
@@ -1023,21 +1019,10 @@ SG_HD inline SgChunkRule sg_chunk_rule(const sg_nfa_desc& d) {
     r.within = d.within;
     return r;
   }
-  int recv = 0;
-  for (int s = 0; s < SG_MAX_STREAMS; ++s) if (d.recv_of_stream[s] >= 0) ++recv;
-  if (recv != 1) return r;
-  int64_t h = 0;
-  for (int s = 0; s < d.n_states; ++s) {
-    const sg_state_desc& x = d.states[s];
-    if (x.kind == SG_K_COUNT) {
-      if (x.max_count < 0 || x.max_count > 4096) return r;
-      h += x.max_count;
-    } else {
-      h += 1;
-    }
-  }
-  r.kind = 2;
-  r.events = h;
+  // Sequences are never cut: a partial lives at most sum(max counts) events, but addState admits one partial per
+  // newAndEvery list (StreamPreStateProcessor.addState :203-216), so whether a partial exists can depend on an older
+  // one that occupied the list, and that on an older one still -- the state is not a function of a bounded suffix
+  // (tests/test_partial_lanes.py::test_sequence_state_is_not_a_bounded_suffix).
   return r;
 }
 // First own row a unit starting at own row p0 (> 0) must replay from; ts_at(i) = timestamp of own row i.

@@ -11,6 +11,7 @@
 #include "../../siddhi_amd/csrc/sg_device.h"
 #include "../../siddhi_amd/csrc/interp.h"
 #include "../../siddhi_amd/csrc/chain.h"
+#include "../../siddhi_amd/csrc/seq.h"
 
 struct HiHandle {
   sg_nfa_desc d;
@@ -24,6 +25,7 @@ struct HiHandle {
   int pp_active = 1;
   struct CRow { int64_t ts; int32_t key; int64_t vals[SG_MAX_RET]; int32_t nullmask; };
   std::vector<CRow> carried;
+  std::vector<SeqState> seq_state;   // sequence lanes: per key
 };
 
 struct HostRows {
@@ -202,9 +204,115 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
   return 1;
 }
 
+// sequence-lane push (partial.hip's sequence route restated on the host): one compact machine per key, resumed from the
+// key's carried state over its carried rows (the last H) + this push's rows; returns 0 when the machine overflows
+struct HostSeqSrc {
+  HostPpSrc base_src;
+  const std::vector<int64_t>* rows;   // combined ids of this key's rows
+  int64_t ts(int64_t pos) const { return base_src.ts((*rows)[pos]); }
+  SgVal read(int64_t pos, int slotk, int type) const { return base_src.read((*rows)[pos], slotk, type); }
+  int lbit(int, int64_t) const { return -1; }
+};
+
+static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std::vector<uint64_t>& k1) {
+  const sg_nfa_desc& d = h->d;
+  const SgSeqRule ru = sg_seq_rule(d);
+  const int64_t n = b->n;
+  const int64_t nc = (int64_t)h->carried.size();
+  int kmax = 0;
+  for (auto& r : h->carried) kmax = std::max(kmax, r.key + 1);
+  for (int64_t i = 0; i < n; ++i) if (d.partitioned && b->key && b->key[i] >= 0) kmax = std::max(kmax, b->key[i] + 1);
+  std::vector<std::vector<int64_t>> own((size_t)std::max(kmax, 1));
+  for (int64_t c = 0; c < nc; ++c) own[d.partitioned ? h->carried[c].key : 0].push_back(c);
+  std::vector<int64_t> ncar(own.size(), 0);
+  for (size_t k = 0; k < own.size(); ++k) ncar[k] = (int64_t)own[k].size();
+  for (int64_t i = 0; i < n; ++i) {
+    int s = b->stream ? b->stream[i] : 0;
+    if (s < 0 || d.recv_of_stream[s] < 0) continue;
+    int k = d.partitioned ? (b->key ? b->key[i] : -1) : 0;
+    if (k < 0) continue;
+    own[k].push_back(nc + i);
+  }
+  if (h->seq_state.size() < own.size()) h->seq_state.resize(own.size());
+  std::vector<SeqState> next_state = h->seq_state;
+  HostPpSrc src{b, &d, &h->carried, nc};
+  const int rstride = 32 + 8 * d.n_select;
+  const int64_t H = ru.horizon;
+  std::vector<HiHandle::CRow> next;
+  for (size_t k = 0; k < own.size(); ++k) {
+    const auto& rows = own[k];
+    const int64_t nk = (int64_t)rows.size();
+    if (!nk) continue;
+    SeqState& st = next_state[k];
+    SeqMachine<HostSeqSrc> m;
+    m.d = &d;
+    m.ru = &ru;
+    m.src = HostSeqSrc{src, &rows};
+    m.M = &st;
+    m.failed = 0;
+    m.f_changed = m.f_returned = m.f_success = 0;
+    if (ncar[k] == 0) m.reset_runtime();
+    uint32_t seq = 0;
+    int64_t crow = -1;
+    auto emit = [&](SeqMachine<HostSeqSrc>& mm, int p, int grp) {
+      const int64_t r = crow;
+      k1.push_back(((uint64_t)r << 16) | seq++);
+      const size_t o = recs.size();
+      recs.resize(o + rstride);
+      char* rec = recs.data() + o;
+      uint64_t trig = b->index ? b->index[r] : b->base_index + (uint64_t)r;
+      memcpy(rec, &trig, 8);
+      const int64_t pp = mm.dec(mm.M->P[p].pts);
+      int64_t pts = pp >= 0 ? mm.src.ts(pp) : -1;
+      memcpy(rec + 8, &pts, 8);
+      uint32_t h32[4] = {(uint32_t)k, (1u << 24) | (uint32_t)grp, 0, 0};
+      for (int s = 0; s < d.n_select; ++s) {
+        int64_t v = 0;
+        const int64_t ev = mm.get_event(p, d.sel_state[s], d.sel_index[s]);
+        if (ev < 0) h32[2] |= 1u << s;
+        else {
+          SgVal x = mm.src.read(ev, d.sel_ret[s], d.ret_type[d.sel_ret[s]]);
+          if (x.null) h32[2] |= 1u << s; else v = sg_val_bits(x);
+        }
+        memcpy(rec + 32 + 8 * s, &v, 8);
+      }
+      memcpy(rec + 16, h32, 16);
+    };
+    for (int64_t q = ncar[k]; q < nk; ++q) {
+      crow = rows[q] - nc;
+      seq = 0;
+      m.receive(q, emit);
+      if (m.failed) return 0;
+    }
+    // carry: the last H rows and the state re-expressed over them
+    const int64_t from = nk > H ? nk - H : 0;
+    m.rebase(nk - 1, from);
+    for (int64_t q = from; q < nk; ++q) {
+      const int64_t c = rows[q];
+      HiHandle::CRow cr;
+      memset(&cr, 0, sizeof(cr));
+      if (c < nc) cr = h->carried[c];
+      else {
+        cr.ts = src.ts(c);
+        cr.key = (int32_t)k;
+        for (int j = 0; j < d.n_ret; ++j) {
+          int null = 0;
+          cr.vals[j] = read_bits(b, &d, j, c - nc, &null);
+          if (null) cr.nullmask |= 1 << j;
+        }
+      }
+      next.push_back(cr);
+    }
+  }
+  h->seq_state.swap(next_state);
+  h->carried.swap(next);
+  return 1;
+}
+
 extern "C" {
 
 void hi_set_pp(HiHandle* h, int on) { h->pp = on; }
+int hi_seq_rule(const sg_nfa_desc* d) { return sg_seq_rule(*d).ok; }
 int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
 
 HiHandle* hi_open(const sg_nfa_desc* d, int P, int E, int C, int L) {
@@ -227,7 +335,26 @@ int hi_chunk_rule(const sg_nfa_desc* d, int64_t* horizon) {
 static int machine_push(HiHandle* h, const sg_batch* b, bool silent);
 
 int hi_push(HiHandle* h, const sg_batch* b) {
-  if (h->pp && h->pp_active && sg_pp_rule(h->d).ok) {
+  if (h->pp && h->pp_active && sg_seq_rule(h->d).ok) {
+    std::vector<char> recs;
+    std::vector<uint64_t> k1;
+    const std::vector<HiHandle::CRow> before = h->carried;
+    const std::vector<SeqState> before_st = h->seq_state;
+    if (seq_push(h, b, recs, k1)) {
+      const int rstride = 32 + 8 * h->d.n_select;
+      std::vector<size_t> idx(k1.size());
+      for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+      std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return k1[x] < k1[y]; });
+      for (size_t i : idx) h->out.emplace_back(recs.begin() + i * rstride, recs.begin() + (i + 1) * rstride);
+      return 0;
+    }
+    // a key outgrew the compact machine: only a fresh stream can move to the per-key machine exactly
+    if (!before.empty()) { h->err = SG_ECAPACITY; return SG_ECAPACITY; }
+    h->carried = before;
+    h->seq_state = before_st;
+  }
+  if (h->pp && h->pp_active && (sg_pp_rule(h->d).ok || sg_seq_rule(h->d).ok)) {
+   if (sg_pp_rule(h->d).ok) {
     std::vector<char> recs;
     std::vector<uint64_t> k1, th, tl;
     const int rc = pp_push(h, b, recs, k1, th, tl);
@@ -245,12 +372,14 @@ int hi_push(HiHandle* h, const sg_batch* b) {
       for (size_t i : idx) h->out.emplace_back(recs.begin() + i * rstride, recs.begin() + (i + 1) * rstride);
       return 0;
     }
+   }
     // leave the route: replay the carried rows through the machine without emitting
     h->pp_active = 0;
     const size_t nc = h->carried.size();
     if (nc) {
       std::vector<int64_t> ts(nc), colv[SG_MAX_COLS];
-      std::vector<int32_t> key(nc), stream(nc, h->d.receivers[sg_pp_rule(h->d).recv].stream);
+      const int recv = sg_pp_rule(h->d).ok ? sg_pp_rule(h->d).recv : sg_seq_rule(h->d).recv;
+      std::vector<int32_t> key(nc), stream(nc, h->d.receivers[recv].stream);
       std::vector<uint8_t> nul[SG_MAX_COLS];
       const void* cols[SG_MAX_COLS] = {};
       const uint8_t* nuls[SG_MAX_COLS] = {};

@@ -16,7 +16,8 @@ def _load():
     global _lib
     if _lib is None:
         srcs = [os.path.join(HERE, "harness.cpp"), os.path.join(ROOT, "siddhi_amd", "csrc", "interp.h"),
-                os.path.join(ROOT, "siddhi_amd", "csrc", "sg_device.h"), os.path.join(ROOT, "siddhi_amd", "csrc", "chain.h")]
+                os.path.join(ROOT, "siddhi_amd", "csrc", "sg_device.h"), os.path.join(ROOT, "siddhi_amd", "csrc", "chain.h"),
+                os.path.join(ROOT, "siddhi_amd", "csrc", "seq.h")]
         if not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(s) for s in srcs):
             os.makedirs(os.path.dirname(LIB), exist_ok=True)
             subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, srcs[0]], check=True)
@@ -34,6 +35,8 @@ def _load():
         lib.hi_set_pp.argtypes = [P, ct.c_int]
         lib.hi_pp_rule.restype = ct.c_int
         lib.hi_pp_rule.argtypes = [P]
+        lib.hi_seq_rule.restype = ct.c_int
+        lib.hi_seq_rule.argtypes = [P]
         _lib = lib
     return _lib
 

@@ -43,6 +43,21 @@ SHAPES = {
                            "within 70 milliseconds select e1.id as i1, e2.id as i2, e3.id as i3, e3.v as v3 "
                            "insert into M; end;",
 }
+SEQ_SHAPES = {
+    "seq_next": PART + "from every e1=S[v>50], e2=S[v>e1.v] select e1.id as i1, e2.id as i2 insert into M; end;",
+    "seq_count": PART + "from every e1=S[v>30], e2=S[v>=e1.v]<1:4>, e3=S[v<e2[0].v] "
+                        "select e1.id as i1, e2[0].id as a, e2[last].id as z, e3.id as i3 insert into M; end;",
+    "seq_c3b": PART + "from every e1=S[v>50], e2=S[v>e1.v]<1:5>, e3=S[v<e1.v] or e4=S[w<e1.w] "
+                      "select e1.id as i1, e2[0].id as a, e2[last].id as z, e3.id as i3, e4.id as i4 insert into M; end;",
+    "seq_and": PART + "from every e1=S[v>50], e2=S[v>e1.v] and e3=S[w<e1.w] "
+                      "select e1.id as i1, e2.id as i2, e3.id as i3 insert into M; end;",
+    "seq_or_next": PART + "from every e1=S[v>50], e2=S[v>e1.v] or e3=S[w<e1.w], e4=S[v>=e1.v] "
+                          "select e1.id as i1, e2.id as i2, e3.id as i3, e4.id as i4 insert into M; end;",
+    "seq_last_ref": PART + "from every e1=S[v>40], e2=S[v>=e1.v]<1:3>, e3=S[v<e2[last].v and w>e1.w] "
+                           "select e1.id as i1, e2[last].id as z, e3.id as i3 insert into M; end;",
+}
+UNPART_SEQ = ("@info(name='q') from every e1=S[v>50], e2=S[v>e1.v]<1:3>, e3=S[w<e1.w] "
+              "select e1.id as i1, e2[last].id as z, e3.id as i3 insert into M;")
 UNPART = ("@info(name='q') from every e1=S[v>50] -> e2=S[v>e1.v]<1:3> -> e3=S[w<e1.w] within 15 milliseconds "
           "select e1.id as i1, e2[last].id as z, e3.id as i3 insert into M;")
 
@@ -139,6 +154,57 @@ def test_timestamps_going_back_with_a_count_state():
         run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(both, [10_000, 15_000]))
     assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=False), q, split(both, [10_000, 15_000])),
                 run_engine(OracleEngine, q, [both]))
+
+
+def test_seq_rule_covers_the_shapes():
+    import ctypes as ct
+    lib = _load()
+    for name, q in SEQ_SHAPES.items():
+        d = N.build_desc(L.lower(context(HEAD + q)))
+        assert lib.hi_seq_rule(ct.byref(d)) == 1, name
+    for cfg, ok in (("C3", 0), ("C3b", 1), ("C3c", 0), ("C2", 0)):
+        d = N.build_desc(L.lower(context(synth.QUERIES[cfg])))
+        assert lib.hi_seq_rule(ct.byref(d)) == ok, cfg
+
+
+@pytest.mark.parametrize("vmax", [10, 100])
+@pytest.mark.parametrize("name", sorted(SEQ_SHAPES))
+def test_seq_shapes_vs_oracle(name, vmax):
+    q = HEAD + SEQ_SHAPES[name]
+    b = small_batch(12_000, 30, vmax, 4, seed=sum(name.encode()) + vmax)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(b, [3000, 3001, 3003, 9000]))
+    assert len(want) > 0
+    assert_same(got, want)
+
+
+def test_sequence_state_is_not_a_bounded_suffix():
+    """Why sequences are never cut into units: on this stream, rebuilding a key's state from the H = 5 events before a
+    row (a partial's longest life) gives the wrong partial at trigger 739 -- an older partial occupying e2's
+    newAndEvery list had kept the newer one out (StreamPreStateProcessor.addState :203-216), and that older one existed
+    only because of events further back."""
+    q = HEAD + SEQ_SHAPES["seq_last_ref"]
+    b = small_batch(12_000, 30, 10, 4, seed=sum(b"seq_last_ref") + 10)
+    want = run_engine(OracleEngine, q, [b])
+    k = b.key[739]
+    rows = np.nonzero(b.key == k)[0]
+    rows = rows[rows <= 739]
+    tail = rows[-6:]                      # the trigger and the 5 events of its key before it
+    sub = Batch(len(tail), 0, b.ts[tail], b.stream[tail], b.key[tail], [c[tail] for c in b.cols], [None] * 4,
+                index=tail.astype(np.uint64))
+    got_tail = run_engine(OracleEngine, q, [sub])
+    w = want.vals[want.trigger == 739]
+    g = got_tail.vals[got_tail.trigger == 739]
+    assert len(w) == 1 and len(g) == 1 and w[0][0] == 657 and g[0][0] == 700
+
+
+def test_seq_unpartitioned():
+    q = HEAD + UNPART_SEQ
+    b = small_batch(20_000, 1, 100, 2, seed=3)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(b, [7000]))
+    assert len(want) > 0
+    assert_same(got, want)
 
 
 def test_c3c_config_slice():
