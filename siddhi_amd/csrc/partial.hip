@@ -21,6 +21,8 @@
 // back a partial parked in a count state longer than `within` could still complete, and the carried rows do not hold
 // it -- such a push fails with SG_EORDER, like the closed forms (open the handle with partial_lanes = -1 for streams
 // whose timestamps go back).
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -32,6 +34,7 @@
 #include "sg_engine.h"
 #include "interp.h"
 #include "chain.h"
+#include "seq.h"
 #include "pred.h"
 
 #define HIPCHK(x)                                                                                   \
@@ -50,8 +53,15 @@ struct PpRows {
 };
 
 struct PartialState {
+  int mode = 1;         // 1: partial lanes (patterns, chain.h), 2: sequence lanes (seq.h)
   SgPpRule rule;
   SgPpRule* drule = nullptr;
+  SgSeqRule srule;
+  SgSeqRule* dsrule = nullptr;
+  SeqState* kst = nullptr;      // sequence lanes: per-key machine state (zero = no runtime yet)
+  int64_t kst_keys = 0;
+  int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
+  int64_t last_reruns = 0;      // sequence units rerun from their predecessor's end state in the last push
   int used_col[SG_MAX_COLS] = {};
   int col_bytes[SG_MAX_COLS] = {};
   PpRows rows[2];       // carried rows (cur) and the next push's (double buffer)
@@ -88,9 +98,19 @@ static void rows_reserve(PartialState* ps, PpRows& r, int64_t need) {
 
 PartialState* sg_partial_new(const sg_nfa_desc& d) {
   SgPpRule ru = sg_pp_rule(d);
-  if (!ru.ok) return nullptr;
+  SgSeqRule sr = sg_seq_rule(d);
+  if (!ru.ok && !sr.ok) return nullptr;
   PartialState* ps = new PartialState();
+  ps->mode = ru.ok ? 1 : 2;
   ps->rule = ru;
+  ps->srule = sr;
+  if (ps->mode == 2) {
+    ps->rule.local_mask = sr.local_mask;
+    ps->rule.start = sr.start;
+    ps->rule.recv = sr.recv;
+    if (hipMalloc(&ps->dsrule, sizeof(SgSeqRule)) != hipSuccess) { delete ps; throw SgError(SG_EHIP, "hipMalloc rule"); }
+    hipMemcpy(ps->dsrule, &ps->srule, sizeof(SgSeqRule), hipMemcpyHostToDevice);
+  }
   for (int s = 0; s < d.n_states; ++s) ps->has_count |= d.states[s].kind == SG_K_COUNT;
   for (int k = 0; k < d.n_ret; ++k) {
     const int c = d.ret_col[k];
@@ -107,6 +127,8 @@ void sg_partial_free(PartialState* ps) {
   rows_free(ps->rows[0]);
   rows_free(ps->rows[1]);
   if (ps->drule) hipFree(ps->drule);
+  if (ps->dsrule) hipFree(ps->dsrule);
+  if (ps->kst) hipFree(ps->kst);
   delete ps;
 }
 
@@ -114,6 +136,8 @@ void sg_partial_reset(PartialState* ps) {
   if (!ps) return;
   ps->rows[0].n = ps->rows[1].n = 0;
   ps->active = 1;
+  ps->seq_pushes = 0;
+  if (ps->kst) hipMemset(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys);
 }
 
 int sg_partial_active(const PartialState* ps) { return ps && ps->active; }
@@ -526,6 +550,442 @@ static void sort_pairs64(SgHandle* h, const char* tag, uint64_t* k_in, uint64_t*
   HIPCHK(rocprim::radix_sort_pairs(tmp, tb, k_in, k_out, v_in, v_out, (size_t)n, 0, end_bit, st));
 }
 
+// ---- sequence lanes (seq.h): one lane per key resumes the key's compact machine over its rows ----------------------
+struct SeqSrcD {
+  const PpPacked* P;
+  int64_t base;
+  __device__ int64_t ts(int64_t pos) const { return P->ts[base + pos]; }
+  __device__ SgVal read(int64_t pos, int slotk, int type) const {
+    const int64_t q = base + pos;
+    const int null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
+    const int64_t bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
+    return sg_val_from_bits(bits, type, null);
+  }
+  __device__ int lbit(int s, int64_t pos) const { return (int)((P->lb[base + pos] >> s) & 1u); }
+};
+
+struct SqOut {
+  char* rec;
+  uint64_t* k1;               // (trigger row << 16) | emission index within the row
+  unsigned long long* reserved;
+  unsigned long long* count;
+  int32_t* fail;
+  int64_t cap;
+  int32_t rstride;
+  uint64_t k1_none;
+};
+
+constexpr int SQ_BLOCK = 64;
+constexpr int SQ_CHUNK = 16;   // match slots a lane reserves at a time
+
+// Units (key, c): the key's new rows [s0, s1) = [beg + ncar + c R, ...).  Unit 0 starts from the key's carried state;
+// unit c > 0 from a guess -- a zeroed state warmed up over the W rows before it -- verified afterwards.
+struct SqPlan {
+  const uint32_t* beg;
+  const uint32_t* end;
+  const uint32_t* ncar;       // carried rows at the start of each key's positions
+  const uint32_t* uoff;       // key -> first unit
+  const uint32_t* umap;       // unit -> key
+  int64_t R, W;
+  int64_t nunits;
+  SeqState* kst;              // per key (carried)
+  SeqState* ust;              // per unit: start state
+  SeqState* uen;              // per unit: end state
+  unsigned long long* reruns;
+};
+
+__global__ void k_sq_ucount(int64_t kb, const uint32_t* __restrict__ beg, const uint32_t* __restrict__ end,
+                            const uint32_t* __restrict__ sid, int64_t nc, int64_t R, uint32_t* __restrict__ ncar,
+                            uint32_t* __restrict__ nu) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > kb) return;
+  if (k == kb) { nu[k] = 0; return; }
+  const int64_t b0 = beg[k], e0 = end[k];
+  int64_t c = 0;
+  while (b0 + c < e0 && (int64_t)sid[b0 + c] < nc) ++c;
+  ncar[k] = (uint32_t)c;
+  const int64_t own = e0 > b0 ? e0 - b0 - c : 0;
+  nu[k] = (uint32_t)((own + R - 1) / R);
+}
+
+__global__ void k_sq_umap(int64_t kb, const uint32_t* __restrict__ uoff, uint32_t* __restrict__ umap) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= kb) return;
+  for (uint32_t u = uoff[k]; u < uoff[k + 1]; ++u) umap[u] = (uint32_t)k;
+}
+
+__device__ __forceinline__ void sq_copy(SeqState* __restrict__ dst, const SeqState* __restrict__ src) {
+  const uint32_t* s = (const uint32_t*)src;
+  uint32_t* d = (uint32_t*)dst;
+  for (uint32_t i = 0; i < sizeof(SeqState) / 4; ++i) d[i] = s[i];
+}
+__device__ __forceinline__ void sq_zero(SeqState* dst) {
+  uint32_t* d = (uint32_t*)dst;
+  for (uint32_t i = 0; i < sizeof(SeqState) / 4; ++i) d[i] = 0;
+}
+
+struct SqEmit {   // match writer of the emitting pass
+  const PpArgs* a;
+  const DevDesc* dd;
+  const uint32_t* sid;
+  SqOut o;
+  int64_t slot, slot_end, r;
+  uint32_t key, seq, nemit;
+  __device__ void operator()(SeqMachine<SeqSrcD>& mm, int p, int grp) {
+    if (slot == slot_end) {
+      slot = (int64_t)atomicAdd(o.reserved, (unsigned long long)SQ_CHUNK);
+      slot_end = slot + SQ_CHUNK;
+      if (slot_end > o.cap) { mm.fail(5); slot = slot_end; return; }
+    }
+    const int64_t w = slot++;
+    ++nemit;
+    o.k1[w] = ((uint64_t)r << 16) | seq++;
+    char* rec = o.rec + (size_t)w * (size_t)o.rstride;
+    uint64_t* h64 = (uint64_t*)rec;
+    h64[0] = pp_index(*a, r);
+    const int64_t pp = mm.dec(mm.M->P[p].pts);
+    h64[1] = (uint64_t)(pp >= 0 ? mm.src.ts(pp) : -1);
+    uint32_t* h32 = (uint32_t*)(rec + 16);
+    h32[0] = key;
+    h32[1] = (1u << 24) | (uint32_t)grp;
+    uint32_t nm = 0;
+    int64_t* vals = (int64_t*)(rec + 32);
+    for (int s = 0; s < dd->n_select; ++s) {
+      const int64_t ev = mm.get_event(p, dd->sel_state[s], dd->sel_index[s]);
+      const int rs = dd->sel_ret[s];
+      if (ev < 0) { nm |= 1u << s; vals[s] = 0; continue; }
+      const SgVal v = mm.src.read(ev, rs, dd->ret_type[rs]);
+      if (v.null) { nm |= 1u << s; vals[s] = 0; continue; }
+      vals[s] = sg_val_bits(v);
+    }
+    h32[2] = nm;
+    h32[3] = 0;
+  }
+};
+struct SqNoEmit {
+  __device__ void operator()(SeqMachine<SeqSrcD>&, int, int) {}
+};
+
+// rows [q0, q1) of a key whose positions start at b0; emit != null: the emitting pass
+template <class E>
+__device__ __forceinline__ void sq_run(SeqMachine<SeqSrcD>& m, int64_t b0, int64_t q0, int64_t q1, E& emit,
+                                       const uint32_t* __restrict__ sid, int64_t nc, int64_t* rcur, uint32_t* seq) {
+  m.begin();
+  for (int64_t q = q0; q < q1 && !m.failed; ++q) {
+    if (rcur) *rcur = (int64_t)sid[q] - nc;
+    if (seq) *seq = 0;
+    m.receive(q - b0, emit);
+  }
+  m.finish();
+}
+
+#define SQ_KERNEL_PROLOGUE                                                                                     \
+  __shared__ DevDesc dl;                                                                                       \
+  __shared__ SgSeqRule rl;                                                                                     \
+  __shared__ PpPacked pl;                                                                                      \
+  __shared__ SeqState lanes[SQ_BLOCK];                                                                         \
+  {                                                                                                            \
+    const uint32_t* s3 = (const uint32_t*)&P;                                                                  \
+    for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];    \
+    const uint32_t* src = (const uint32_t*)ddg;                                                                \
+    for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) ((uint32_t*)&dl)[i] = src[i];    \
+    const uint32_t* rs = (const uint32_t*)rug;                                                                 \
+    for (uint32_t i = threadIdx.x; i < sizeof(SgSeqRule) / 4; i += blockDim.x) ((uint32_t*)&rl)[i] = rs[i];   \
+    __syncthreads();                                                                                           \
+  }
+
+// pass A: every unit's (guessed) start state and the end state it leads to
+__global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
+                                                      const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
+                                                      SqPlan pl_, int32_t* __restrict__ fail) {
+  SQ_KERNEL_PROLOGUE
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= pl_.nunits) return;
+  const uint32_t k = pl_.umap[u];
+  const int64_t c = u - pl_.uoff[k];
+  const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
+  const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
+  SeqState& M = lanes[threadIdx.x];
+  SeqMachine<SeqSrcD> m;
+  m.d = &dl;
+  m.ru = &rl;
+  m.src = SeqSrcD{&pl, b0};
+  m.M = &M;
+  m.cur = 0;
+  SqNoEmit ne;
+  if (c == 0) {
+    sq_copy(&M, pl_.kst + k);
+  } else {
+    sq_zero(&M);
+    const int64_t w0 = s0 - pl_.W > b0 ? s0 - pl_.W : b0;
+    sq_run(m, b0, w0, s0, ne, sid, a.nc, nullptr, nullptr);
+  }
+  sq_copy(pl_.ust + u, &M);
+  sq_run(m, b0, s0, s1, ne, sid, a.nc, nullptr, nullptr);
+  if (m.failed) atomicCAS(fail, 0, m.failed);
+  sq_copy(pl_.uen + u, &M);
+}
+
+// pass B: per key, in unit order, a unit whose guessed start differs from its predecessor's end is rerun from that end
+__global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
+                                                     const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
+                                                     SqPlan pl_, int64_t kb, int32_t* __restrict__ fail) {
+  SQ_KERNEL_PROLOGUE
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= kb) return;
+  const uint32_t u0 = pl_.uoff[k], u1 = pl_.uoff[k + 1];
+  if (u1 - u0 < 2) return;
+  const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
+  SeqState& M = lanes[threadIdx.x];
+  SeqMachine<SeqSrcD> m;
+  m.d = &dl;
+  m.ru = &rl;
+  m.src = SeqSrcD{&pl, b0};
+  m.M = &M;
+  m.cur = 0;
+  SqNoEmit ne;
+  uint32_t reruns = 0;
+  for (uint32_t u = u0 + 1; u < u1; ++u) {
+    if (sg_seq_equiv(pl_.ust[u], pl_.uen[u - 1], dl, rl)) continue;
+    ++reruns;
+    const int64_t c = u - u0;
+    const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
+    sq_copy(&M, pl_.uen + (u - 1));
+    sq_copy(pl_.ust + u, &M);
+    sq_run(m, b0, s0, s1, ne, sid, a.nc, nullptr, nullptr);
+    if (m.failed) { atomicCAS(fail, 0, m.failed); return; }
+    sq_copy(pl_.uen + u, &M);
+  }
+  if (reruns) atomicAdd(pl_.reruns, (unsigned long long)reruns);
+}
+
+// pass C: every unit from its verified start, emitting; the key's last unit leaves the state to carry
+__global__ void __launch_bounds__(SQ_BLOCK) k_sq_emit(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
+                                                      const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
+                                                      SqPlan pl_, SqOut o) {
+  SQ_KERNEL_PROLOGUE
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= pl_.nunits) return;
+  const uint32_t k = pl_.umap[u];
+  const int64_t c = u - pl_.uoff[k];
+  const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
+  const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
+  SeqState& M = lanes[threadIdx.x];
+  SeqMachine<SeqSrcD> m;
+  m.d = &dl;
+  m.ru = &rl;
+  m.src = SeqSrcD{&pl, b0};
+  m.M = &M;
+  m.cur = 0;
+  sq_copy(&M, pl_.ust + u);
+  SqEmit em;
+  em.a = &a;
+  em.dd = &dl;
+  em.sid = sid;
+  em.o = o;
+  em.slot = em.slot_end = 0;
+  em.key = k;
+  em.nemit = 0;
+  em.seq = 0;
+  em.r = 0;
+  sq_run(m, b0, s0, s1, em, sid, a.nc, &em.r, &em.seq);
+  for (int64_t q = em.slot; q < em.slot_end && q < o.cap; ++q) o.k1[q] = o.k1_none;
+  if (em.nemit) atomicAdd(o.count, (unsigned long long)em.nemit);
+  if (m.failed) { atomicCAS(o.fail, 0, m.failed); return; }
+  if (u + 1 == (int64_t)pl_.uoff[k + 1]) {
+    const int64_t nk = e0 - b0;
+    m.rebase(nk - 1, nk > rl.horizon ? nk - rl.horizon : 0);
+    sq_copy(pl_.kst + k, &M);
+  }
+}
+
+// carry for sequence lanes: the last H rows of every key
+__global__ void k_seq_keep(int64_t m, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ end, uint32_t sentinel,
+                           int64_t H, uint32_t* __restrict__ keep) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= m) return;
+  const uint32_t k = skey[p];
+  keep[p] = (k != sentinel && p >= (int64_t)end[k] - H) ? 1u : 0u;
+}
+
+static void carry_rows(SgHandle* h, PartialState* ps, const BatchView& bv, const PpArgs& a, int64_t m,
+                       const uint32_t* skeys, const uint32_t* sids, uint32_t* keep);
+
+static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t n, uint32_t kb, const PpArgs& a,
+                          const PpPacked& P, const uint32_t* skeys, const uint32_t* sids, const uint32_t* beg,
+                          const uint32_t* end, uint32_t sentinel) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  const int64_t m = a.nc + a.n;
+  const dim3 blk(256), grd((unsigned)((m + 255) / 256));
+  // per-key machine states (grown with the key bound; new keys start zeroed = no runtime yet)
+  if ((int64_t)kb > ps->kst_keys) {
+    const int64_t nk = std::max<int64_t>((int64_t)kb, ps->kst_keys * 3 / 2);
+    SeqState* ns = nullptr;
+    if (hipMalloc(&ns, sizeof(SeqState) * (size_t)nk) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
+    HIPCHK(hipMemsetAsync(ns, 0, sizeof(SeqState) * (size_t)nk, st));
+    if (ps->kst) {
+      HIPCHK(hipMemcpyAsync(ns, ps->kst, sizeof(SeqState) * (size_t)ps->kst_keys, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+      hipFree(ps->kst);
+    }
+    ps->kst = ns;
+    ps->kst_keys = nk;
+  }
+  const int nsel = d.n_select;
+  const int32_t rstride = 32 + 8 * nsel;
+  const int64_t cap = n + (int64_t)SQ_CHUNK * (int64_t)kb + 65536;
+  SqOut o;
+  o.rec = (char*)h->ws.get("sq_rec", (size_t)cap * rstride, st);
+  o.k1 = (uint64_t*)h->ws.get("sq_k1", 8 * cap, st);
+  o.reserved = (unsigned long long*)h->ws.get("sq_cnt", 64, st);
+  o.count = o.reserved + 1;
+  o.fail = (int32_t*)(o.reserved + 2);
+  o.cap = cap;
+  o.rstride = rstride;
+  int rb = 1;
+  while ((1ll << rb) < n + 1) ++rb;
+  const int k1_bits = std::min(64, rb + 16);
+  o.k1_none = k1_bits >= 64 ? ~0ull : (1ull << k1_bits) - 1;
+  HIPCHK(hipMemsetAsync(o.reserved, 0, 64, st));
+  // ---- unit plan
+  SqPlan pl_;
+  const int64_t H = ps->srule.horizon;
+  pl_.R = std::max<int64_t>(64, (n + 262143) / 262144);
+  if (h->opt.chunk_rows > 0) pl_.R = h->opt.chunk_rows;
+  pl_.W = std::max<int64_t>(4 * H, 16);
+  uint32_t* ncar = (uint32_t*)h->ws.get("sq_ncar", 4 * ((size_t)kb + 1), st);
+  uint32_t* nu = (uint32_t*)h->ws.get("sq_nu", 4 * ((size_t)kb + 1), st);
+  uint32_t* uoff = (uint32_t*)h->ws.get("sq_uoff", 4 * ((size_t)kb + 1), st);
+  const dim3 gk((unsigned)((kb + 1 + 255) / 256));
+  h->kbeg("sequence_units");
+  hipLaunchKernelGGL(k_sq_ucount, gk, blk, 0, st, (int64_t)kb, beg, end, sids, a.nc, pl_.R, ncar, nu);
+  {
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, nu, uoff, (uint32_t)0, (size_t)kb + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("sq_uscan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, nu, uoff, (uint32_t)0, (size_t)kb + 1, rocprim::plus<uint32_t>(), st));
+  }
+  uint32_t U = 0;
+  HIPCHK(hipMemcpyAsync(&U, uoff + kb, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint32_t* umap = (uint32_t*)h->ws.get("sq_umap", 4 * ((size_t)U + 1), st);
+  hipLaunchKernelGGL(k_sq_umap, dim3((unsigned)((kb + 255) / 256)), blk, 0, st, (int64_t)kb, uoff, umap);
+  pl_.beg = beg;
+  pl_.end = end;
+  pl_.ncar = ncar;
+  pl_.uoff = uoff;
+  pl_.umap = umap;
+  pl_.nunits = U;
+  pl_.kst = ps->kst;
+  pl_.ust = (SeqState*)h->ws.get("sq_ust", sizeof(SeqState) * ((size_t)U + 1), st);
+  pl_.uen = (SeqState*)h->ws.get("sq_uen", sizeof(SeqState) * ((size_t)U + 1), st);
+  pl_.reruns = o.reserved + 3;
+  h->kend();
+  const dim3 gu((unsigned)((U + SQ_BLOCK - 1) / SQ_BLOCK)), gq((unsigned)((kb + SQ_BLOCK - 1) / SQ_BLOCK));
+  h->kbeg("sequence_spec");
+  if (U) hipLaunchKernelGGL(k_sq_spec, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o.fail);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  h->kbeg("sequence_fix");
+  if (U) hipLaunchKernelGGL(k_sq_fix, gq, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, (int64_t)kb, o.fail);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  h->kbeg("sequence_lanes");
+  if (U) hipLaunchKernelGGL(k_sq_emit, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  h->mark(3);
+  unsigned long long cnt[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(cnt, o.reserved, 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  ps->last_reruns = (int64_t)cnt[3];
+  const int32_t fail = (int32_t)(cnt[2] & 0xffffffffu);
+  if (fail) {
+    if (getenv("SG_DEBUG_SEQ")) fprintf(stderr, "sequence lanes failed: reason %d\n", fail);
+    if (ps->seq_pushes == 0 && a.nc == 0) {   // nothing carried yet: the per-key machine can take the stream exactly
+      HIPCHK(hipMemsetAsync(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys, st));
+      return 0;
+    }
+    throw SgError(SG_ECAPACITY, "sequence machine capacity exceeded (reason " + std::to_string(fail) +
+                                    ": 1 partials, 2 list, 3 returned, 4 chain, 5 match buffer)");
+  }
+  const int64_t R = std::min<int64_t>((int64_t)cnt[0], cap), total = (int64_t)cnt[1];
+  if (total) {
+    const dim3 g2((unsigned)((R + 255) / 256));
+    uint32_t* ia = (uint32_t*)h->ws.get("sq_ia", 4 * R, st);
+    uint32_t* ib = (uint32_t*)h->ws.get("sq_ib", 4 * R, st);
+    uint64_t* kb2 = (uint64_t*)h->ws.get("sq_kb", 8 * R, st);
+    h->kbeg("match_order");
+    hipLaunchKernelGGL(k_pp_iota, g2, blk, 0, st, R, ia);
+    size_t tb = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, o.k1, kb2, ia, ib, (size_t)R, 0, k1_bits, st));
+    void* tmp = h->ws.get("sq_sorttmp", tb, st);
+    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, o.k1, kb2, ia, ib, (size_t)R, 0, k1_bits, st));
+    char* out = h->out.reserve(total, nsel, st);
+    hipLaunchKernelGGL(k_pp_gather, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total, o.rec, ib, rstride,
+                       out + (size_t)h->out.n * rstride);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->out.n += total;
+  }
+  if (!h->opt.no_carry && m) {
+    uint32_t* keep = (uint32_t*)h->ws.get("pp_keep", 4 * (m + 1), st);
+    hipLaunchKernelGGL(k_seq_keep, grd, blk, 0, st, m, skeys, end, sentinel, (int64_t)ps->srule.horizon, keep);
+    carry_rows(h, ps, bv, a, m, skeys, sids, keep);
+  } else if (h->opt.no_carry) {
+    HIPCHK(hipMemsetAsync(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys, st));
+  }
+  ps->seq_pushes++;
+  h->mark(4);
+  h->last_events = n;
+  h->last_spilled = 0;
+  h->last_matches = total;
+  return 1;
+}
+
+static void carry_rows(SgHandle* h, PartialState* ps, const BatchView& bv, const PpArgs& a, int64_t m,
+                       const uint32_t* skeys, const uint32_t* sids, uint32_t* keep) {
+  {
+    const sg_nfa_desc& d = h->desc;
+    hipStream_t st = h->stream;
+    const dim3 blk(256), grd((unsigned)((m + 255) / 256));
+    const PpRows& cr = ps->rows[ps->cur];
+    h->kbeg("carry");
+    uint32_t* pos = (uint32_t*)h->ws.get("pp_pos", 4 * (m + 1), st);
+    HIPCHK(hipMemsetAsync(keep + m, 0, 4, st));
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, keep, pos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("pp_scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, keep, pos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t nn = 0;
+    HIPCHK(hipMemcpyAsync(&nn, pos + m, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    PpRows& nr = ps->rows[1 - ps->cur];
+    rows_reserve(ps, nr, nn);
+    PpCopyCols c2;
+    memset(&c2, 0, sizeof(c2));
+    c2.ncols = d.n_cols;
+    for (int j = 0; j < d.n_cols; ++j) {
+      if (!ps->used_col[j]) continue;
+      c2.bsrc[j] = bv.cols.col[j];
+      c2.bnul[j] = bv.cols.nul[j];
+      c2.csrc[j] = cr.col[j];
+      c2.cnul[j] = cr.nul[j];
+      c2.dst[j] = nr.col[j];
+      c2.dnul[j] = nr.nul[j];
+      c2.bytes[j] = ps->col_bytes[j];
+    }
+    hipLaunchKernelGGL(k_pp_carry, grd, blk, 0, st, m, a, skeys, sids, keep, pos, c2, nr.ts, nr.key);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    nr.n = nn;
+    ps->rows[ps->cur].n = 0;
+    ps->cur = 1 - ps->cur;
+    h->kend();
+  }
+}
+
 // Returns 1 when the push ran on partial lanes, 0 when it breaks the route's precondition (nothing was changed).
 int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t n, uint32_t kb) {
   const sg_nfa_desc& d = h->desc;
@@ -533,7 +993,11 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   const PpRows& cr = ps->rows[ps->cur];
   const int64_t nc = h->opt.no_carry ? 0 : cr.n;
   const int64_t m = nc + n;
-  if (m >= ((int64_t)1 << 27)) return 0;   // tie components hold a combined row in 27 bits
+  if (ps->mode == 1 && m >= ((int64_t)1 << 27)) {   // tie components hold a combined row in 27 bits
+    if (ps->has_count && nc > 0)
+      throw SgError(SG_ECAPACITY, "partial-lane route: push at most 2^27 rows at a time (carried rows included)");
+    return 0;
+  }
   PpArgs a;
   memset(&a, 0, sizeof(a));
   a.nc = nc;
@@ -581,7 +1045,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (herr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-    if (herr & 1) {
+    if ((herr & 1) && ps->mode == 1) {
       if (ps->has_count && nc > 0)
         throw SgError(SG_EORDER, "partial-lane route requires non-decreasing timestamps per key once a count state holds "
                                  "partials (open the handle with partial_lanes = -1 for such streams)");
@@ -638,6 +1102,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   if (m) hipLaunchKernelGGL(k_pp_pack, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->rule.local_mask, ps->rule.start,
                             skeys, sids, sentinel, P, flag);
   HIPCHK(hipGetLastError());
+  if (ps->mode == 2) {
+    h->kend();
+    return seq_lanes_push(h, ps, bv, n, kb, a, P, skeys, sids, beg, end, sentinel);
+  }
   HIPCHK(hipMemsetAsync(flag + m, 0, 4, st));
   {
     size_t tb = 0;
@@ -732,40 +1200,9 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   }
   // ---- carry
   if (!h->opt.no_carry && m) {
-    h->kbeg("carry");
     uint32_t* keep = (uint32_t*)h->ws.get("pp_keep", 4 * (m + 1), st);
-    uint32_t* pos = (uint32_t*)h->ws.get("pp_pos", 4 * (m + 1), st);
     hipLaunchKernelGGL(k_pp_keep, grd, blk, 0, st, m, a, skeys, sids, end, sentinel, (int64_t)d.within, keep);
-    HIPCHK(hipMemsetAsync(keep + m, 0, 4, st));
-    size_t tb = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, tb, keep, pos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
-    void* tmp = h->ws.get("pp_scan_tmp", tb, st);
-    HIPCHK(rocprim::exclusive_scan(tmp, tb, keep, pos, (uint32_t)0, (size_t)m + 1, rocprim::plus<uint32_t>(), st));
-    uint32_t nn = 0;
-    HIPCHK(hipMemcpyAsync(&nn, pos + m, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    PpRows& nr = ps->rows[1 - ps->cur];
-    rows_reserve(ps, nr, nn);
-    PpCopyCols c2;
-    memset(&c2, 0, sizeof(c2));
-    c2.ncols = d.n_cols;
-    for (int j = 0; j < d.n_cols; ++j) {
-      if (!ps->used_col[j]) continue;
-      c2.bsrc[j] = bv.cols.col[j];
-      c2.bnul[j] = bv.cols.nul[j];
-      c2.csrc[j] = cr.col[j];
-      c2.cnul[j] = cr.nul[j];
-      c2.dst[j] = nr.col[j];
-      c2.dnul[j] = nr.nul[j];
-      c2.bytes[j] = ps->col_bytes[j];
-    }
-    hipLaunchKernelGGL(k_pp_carry, grd, blk, 0, st, m, a, skeys, sids, keep, pos, c2, nr.ts, nr.key);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(st));
-    nr.n = nn;
-    ps->rows[ps->cur].n = 0;
-    ps->cur = 1 - ps->cur;
-    h->kend();
+    carry_rows(h, ps, bv, a, m, skeys, sids, keep);
   }
   h->mark(4);
   h->last_events = n;
@@ -779,6 +1216,12 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
 // newAndEveryStateEventList, C/query/input/stream/state/StreamPreStateProcessor.java:352-367) and the latest timestamp.
 void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
   const PpRows& r = ps->rows[ps->cur];
+  w.pod((int32_t)ps->mode);
+  if (ps->mode == 2) {   // sequence lanes: the per-key machine states as well (seq.h SeqState, positions over the rows)
+    w.pod(ps->kst_keys);
+    w.pod(ps->seq_pushes);
+    if (ps->kst_keys) w.dev(ps->kst, sizeof(SeqState) * (size_t)ps->kst_keys, h->stream);
+  }
   w.pod(r.n);
   if (!r.n) return;
   w.dev(r.ts, 8 * r.n, h->stream);
@@ -792,6 +1235,21 @@ void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
 
 void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& rd) {
   sg_partial_reset(ps);
+  if (rd.pod<int32_t>() != ps->mode) throw SgError(SG_EINVAL, "snapshot: lane route differs");
+  if (ps->mode == 2) {
+    const int64_t keys = rd.pod<int64_t>();
+    const int64_t pushes = rd.pod<int64_t>();
+    if (keys < 0 || keys > ((int64_t)1 << 31)) throw SgError(SG_EINVAL, "snapshot: bad sequence state count");
+    if (keys > ps->kst_keys) {
+      if (ps->kst) hipFree(ps->kst);
+      ps->kst = nullptr;
+      if (hipMalloc(&ps->kst, sizeof(SeqState) * (size_t)keys) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
+      ps->kst_keys = keys;
+    }
+    if (ps->kst_keys) HIPCHK(hipMemset(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys));
+    if (keys) rd.dev(ps->kst, sizeof(SeqState) * (size_t)keys, h->stream);
+    ps->seq_pushes = pushes;
+  }
   const int64_t n = rd.pod<int64_t>();
   if (n < 0 || n >= ((int64_t)1 << 31)) throw SgError(SG_EINVAL, "snapshot: bad carried row count");
   PpRows& r = ps->rows[ps->cur];

@@ -106,6 +106,7 @@ struct SeqState {
   uint32_t free_mask;   // pool entries free for allocation in this event
   uint32_t h_init;      // per-state processor flags (KeyMachine H_* words)
   uint32_t created;
+  uint32_t fch, fret, fsuc;   // H_CHANGED / H_RETURNED / H_SUCCESS bits between runs (registers while running)
 };
 
 // Src: int64_t ts(int64_t pos); SgVal read(int64_t pos, int ret_slot, int type); int lbit(int s, int64_t pos) (-1: VM)
@@ -122,8 +123,19 @@ struct SeqMachine {
 
   SG_HD const sg_state_desc& st(int s) const { return d->states[s]; }
   SG_HD static uint32_t bit(int s) { return 1u << s; }
-  SG_HD void fail() { failed = 1; }
+  SG_HD void fail(int why = 1) { if (!failed) failed = why; }   // 1 pool, 2 list, 3 returned, 4 chain, 5 output
 
+  SG_HD void begin() {   // a run resumes the state's processor flags
+    f_changed = M->fch;
+    f_returned = M->fret;
+    f_success = M->fsuc;
+    failed = 0;
+  }
+  SG_HD void finish() {
+    M->fch = f_changed;
+    M->fret = f_returned;
+    M->fsuc = f_success;
+  }
   SG_HD void reset_runtime() {
     M->created = 0;
     M->h_init = 0;
@@ -143,7 +155,7 @@ struct SeqMachine {
   }
   SG_HD int alloc() {
     const uint32_t f = M->free_mask;
-    if (!f) { fail(); return 0; }
+    if (!f) { fail(1); return 0; }
     int p = 0;
     while (!((f >> p) & 1u)) ++p;
     M->free_mask &= ~(1u << p);
@@ -166,7 +178,7 @@ struct SeqMachine {
   // ---- lists
   SG_HD int llen(int s, int w) const { return M->llen_[s][w]; }
   SG_HD void ladd(int s, int w, int p) {
-    if (M->llen_[s][w] >= PQ_MAX_L) { fail(); return; }
+    if (M->llen_[s][w] >= PQ_MAX_L) { fail(2); return; }
     M->list[s][w][M->llen_[s][w]++] = (int8_t)p;
   }
   SG_HD void lclear(int s, int w) { M->llen_[s][w] = 0; }
@@ -327,14 +339,14 @@ struct SeqMachine {
       bool remove = false;
       if (x.kind == SG_K_COUNT) {
         if ((s + 1 < d->n_states && has_event(p, s + 1)) || (s + 2 < d->n_states && has_event(p, s + 2))) continue;
-        if (y.clen[s] >= x.max_count) { fail(); break; }
+        if (y.clen[s] >= x.max_count) { fail(4); break; }
         y.chain[ru->coff[s] + y.clen[s]++] = enc(cur);
         f_success &= ~bit(s);
         f_changed &= ~bit(s);
         if (filter(s, p)) count_post(s, p);
         if ((f_returned >> last) & 1u) {
           f_returned &= ~bit(last);
-          if (nret < PQ_MAX_RET) ret[nret++] = p; else fail();
+          if (nret < PQ_MAX_RET) ret[nret++] = p; else fail(3);
         }
         if ((f_changed >> s) & 1u) remove = true;
         if (!((f_success >> s) & 1u)) {
@@ -351,7 +363,7 @@ struct SeqMachine {
         }
         if ((f_returned >> last) & 1u) {
           f_returned &= ~bit(last);
-          if (nret < PQ_MAX_RET) ret[nret++] = p; else fail();
+          if (nret < PQ_MAX_RET) ret[nret++] = p; else fail(3);
         }
         if ((f_changed >> s) & 1u) remove = true;
         else {
@@ -382,8 +394,8 @@ struct SeqMachine {
   template <class Emit>
   SG_HD void receive(int64_t pos, Emit& emit) {
     cur = pos;
-    if (!M->created) create_runtime();
     recompute_free();
+    if (!M->created) create_runtime();
     for (int k = 0; k < d->n_reset && !failed; ++k) reset_state(d->reset_ops[k]);
     for (int k = 0; k < d->n_update && !failed; ++k) update_state(d->update_ops[k]);
     const sg_receiver_desc& rv = d->receivers[ru->recv];
@@ -396,3 +408,39 @@ struct SeqMachine {
     }
   }
 };
+
+// Two machine states are the same runtime when their lists hold equal partials in equal order with the same sharing
+// (pool slots may differ) and the same pending H_RETURNED bits.  Positions are compared encoded (absolute & 0x7FFF).
+// Not compared, because nothing reads them before writing them: H_CHANGED / H_SUCCESS (cleared before every filter),
+// H_INIT (only read for start states without `every`, outside sg_seq_rule).
+SG_HD inline bool sg_seq_equiv(const SeqState& A, const SeqState& B, const sg_nfa_desc& d, const SgSeqRule& ru) {
+  if (A.created != B.created || A.fret != B.fret) return false;
+  int8_t a2b[PQ_MAX_P], b2a[PQ_MAX_P];
+  for (int p = 0; p < PQ_MAX_P; ++p) { a2b[p] = -1; b2a[p] = -1; }
+  for (int s = 0; s < d.n_states; ++s)
+    for (int w = 0; w < 2; ++w) {
+      if (A.llen_[s][w] != B.llen_[s][w]) return false;
+      for (int i = 0; i < A.llen_[s][w]; ++i) {
+        const int pa = A.list[s][w][i], pb = B.list[s][w][i];
+        if (a2b[pa] >= 0 || b2a[pb] >= 0) {
+          if (a2b[pa] != pb || b2a[pb] != pa) return false;
+          continue;
+        }
+        a2b[pa] = (int8_t)pb;
+        b2a[pb] = (int8_t)pa;
+        const SeqPartial& x = A.P[pa];
+        const SeqPartial& y = B.P[pb];
+        if (x.pts != y.pts) return false;
+        for (int t = 0; t < d.n_states; ++t) {
+          if (d.states[t].kind == SG_K_COUNT) {
+            if (x.clen[t] != y.clen[t]) return false;
+            for (int c = 0; c < x.clen[t]; ++c)
+              if (x.chain[ru.coff[t] + c] != y.chain[ru.coff[t] + c]) return false;
+          } else if (x.slot[t] != y.slot[t]) {
+            return false;
+          }
+        }
+      }
+    }
+  return true;
+}

@@ -26,6 +26,7 @@ struct HiHandle {
   struct CRow { int64_t ts; int32_t key; int64_t vals[SG_MAX_RET]; int32_t nullmask; };
   std::vector<CRow> carried;
   std::vector<SeqState> seq_state;   // sequence lanes: per key
+  int64_t spec_rows = 0, spec_warm = 0, spec_reruns = 0;   // speculative units (0: one run per key)
 };
 
 struct HostRows {
@@ -251,7 +252,7 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
     m.M = &st;
     m.failed = 0;
     m.f_changed = m.f_returned = m.f_success = 0;
-    if (ncar[k] == 0) m.reset_runtime();
+    if (ncar[k] == 0) { memset(&st, 0, sizeof(st)); next_state[k] = st; }   // a key without state starts zeroed
     uint32_t seq = 0;
     int64_t crow = -1;
     auto emit = [&](SeqMachine<HostSeqSrc>& mm, int p, int grp) {
@@ -278,11 +279,53 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
       }
       memcpy(rec + 16, h32, 16);
     };
-    for (int64_t q = ncar[k]; q < nk; ++q) {
-      crow = rows[q] - nc;
-      seq = 0;
-      m.receive(q, emit);
-      if (m.failed) return 0;
+    auto noemit = [&](SeqMachine<HostSeqSrc>&, int, int) {};
+    // run rows [a, b) from the state in `st` (the machine's M), emitting or not
+    auto run = [&](int64_t a, int64_t b2, bool emitting) {
+      m.begin();
+      for (int64_t q = a; q < b2 && !m.failed; ++q) {
+        crow = rows[q] - nc;
+        seq = 0;
+        if (emitting) m.receive(q, emit);
+        else m.receive(q, noemit);
+      }
+      m.finish();
+      return !m.failed;
+    };
+    const int64_t R = h->spec_rows;
+    if (R <= 0 || nk - ncar[k] <= R) {
+      if (!run(ncar[k], nk, true)) return 0;
+    } else {
+      // speculative units (partial.hip's scheme): unit c > 0 starts from a zeroed state warmed up over the W rows before
+      // it; a unit whose warmed-up start differs from its predecessor's end is rerun from that end; then every unit
+      // runs again from its verified start, emitting
+      const int64_t U = (nk - ncar[k] + R - 1) / R;
+      std::vector<SeqState> start((size_t)U), fin((size_t)U);
+      for (int64_t c = 0; c < U; ++c) {
+        const int64_t s0 = ncar[k] + c * R, s1 = std::min(nk, s0 + R);
+        if (c == 0) st = next_state[k];
+        else {
+          memset(&st, 0, sizeof(st));
+          if (!run(std::max<int64_t>(0, s0 - h->spec_warm), s0, false)) return 0;
+        }
+        start[c] = st;
+        if (!run(s0, s1, false)) return 0;
+        fin[c] = st;
+      }
+      for (int64_t c = 1; c < U; ++c) {
+        if (sg_seq_equiv(start[c], fin[c - 1], d, ru)) continue;
+        ++h->spec_reruns;
+        const int64_t s0 = ncar[k] + c * R, s1 = std::min(nk, s0 + R);
+        start[c] = fin[c - 1];
+        st = start[c];
+        if (!run(s0, s1, false)) return 0;
+        fin[c] = st;
+      }
+      for (int64_t c = 0; c < U; ++c) {
+        const int64_t s0 = ncar[k] + c * R, s1 = std::min(nk, s0 + R);
+        st = start[c];
+        if (!run(s0, s1, true)) return 0;
+      }
     }
     // carry: the last H rows and the state re-expressed over them
     const int64_t from = nk > H ? nk - H : 0;
@@ -312,6 +355,8 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
 extern "C" {
 
 void hi_set_pp(HiHandle* h, int on) { h->pp = on; }
+void hi_set_spec(HiHandle* h, int64_t rows, int64_t warm) { h->spec_rows = rows; h->spec_warm = warm; }
+int64_t hi_spec_reruns(HiHandle* h) { return h->spec_reruns; }
 int hi_seq_rule(const sg_nfa_desc* d) { return sg_seq_rule(*d).ok; }
 int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
 

@@ -37,12 +37,15 @@ def _load():
         lib.hi_pp_rule.argtypes = [P]
         lib.hi_seq_rule.restype = ct.c_int
         lib.hi_seq_rule.argtypes = [P]
+        lib.hi_set_spec.argtypes = [P, ct.c_int64, ct.c_int64]
+        lib.hi_spec_reruns.restype = ct.c_int64
+        lib.hi_spec_reruns.argtypes = [P]
         _lib = lib
     return _lib
 
 
 class HostInterpEngine:
-    def __init__(self, ctx, pool=256, chunk_rows=0, pp=True):
+    def __init__(self, ctx, pool=256, chunk_rows=0, pp=True, spec=(0, 0)):
         from siddhi_amd import lowering as L
         from siddhi_amd import _native as N
         self.lib = _load()
@@ -53,6 +56,7 @@ class HostInterpEngine:
         self.h = self.lib.hi_open(ct.byref(self.desc), pool, pool, pool, pool)
         self.lib.hi_set_chunk(self.h, chunk_rows)
         self.lib.hi_set_pp(self.h, 1 if pp else 0)   # partial lanes (chain.h) where sg_pp_rule allows, as the GPU
+        self.lib.hi_set_spec(self.h, spec[0], spec[1])   # sequence lanes: speculative units of spec[0] rows, spec[1] warm-up
 
     def push(self, b):
         keep = []
@@ -88,6 +92,9 @@ class HostInterpEngine:
         for k in range(self.nsel):
             vnull[:, k] = (vn >> np.uint32(k)) & np.uint32(1)
         return Outputs(tr, ts, ky, gr, vals[:, :self.nsel], vnull)
+
+    def reruns(self):
+        return self.lib.hi_spec_reruns(self.h)
 
     def close(self):
         if self.h:

@@ -57,7 +57,7 @@ def _workers():
     ("C2", 100_000_000, 10_000, 1_000, 48_942_666, 0),     # BASELINE configs[1], the bench workload
     ("C2", 100_000_000, 10_000, 1_000, 48_942_666, 1),     # same, radix-sort partition path
     ("C5", 100_000_000, 1_000_000, 10_000, 38_852_524, 0),  # C5 per-GPU slice (1M keys)
-    ("C3b", 100_000_000, 10_000, 1_000, 10_159_775, 0),    # general machine at 100M events
+    ("C3b", 100_000_000, 10_000, 1_000, 10_159_774, 0),    # sequence lanes at 100M events
     ("C3c", 100_000_000, 10_000, 1_000, 47_100_761, 0),    # general machine: counts, and, within
 ], ids=["C2", "C2-radix", "C5", "C3b", "C3c"])
 def test_full_size_all_rows(cfg, n, keys, rate, expect, sort):

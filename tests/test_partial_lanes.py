@@ -271,3 +271,42 @@ def test_gpu_c3c_slice_both_routes():
     want = run_engine(OracleEngine, q, [b])
     assert_same(run_engine(GpuEngine, q, split(b, [50_000, 123_457])), want)
     assert_same(run_engine(lambda ctx: GpuEngine(ctx, partial_lanes=-1), q, [b]), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vmax", [10, 100])
+@pytest.mark.parametrize("name", sorted(SEQ_SHAPES))
+def test_gpu_seq_shapes(name, vmax):
+    from siddhi_amd._native import GpuEngine
+    q = HEAD + SEQ_SHAPES[name]
+    b = small_batch(12_000, 30, vmax, 4, seed=sum(name.encode()) + vmax)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(GpuEngine, q, split(b, [3000, 3001, 3003, 9000]))
+    assert_same(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_seq_unpartitioned_and_c3b():
+    from siddhi_amd._native import GpuEngine
+    q = HEAD + UNPART_SEQ
+    b = small_batch(20_000, 1, 100, 2, seed=3)
+    assert_same(run_engine(GpuEngine, q, split(b, [7000])), run_engine(OracleEngine, q, [b]))
+    q = synth.QUERIES["C3b"]
+    g = synth.generate("C3b", 0, 200_000, keys=500, rate=100)
+    b = Batch(200_000, 0, g["ts"], np.zeros(200_000, np.int32), dense_first_seen(g["key"]),
+              [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
+    want = run_engine(OracleEngine, q, [b])
+    assert_same(run_engine(GpuEngine, q, split(b, [50_000, 123_457])), want)
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, partial_lanes=-1), q, [b]), want)
+
+
+@pytest.mark.parametrize("spec", [(3, 0), (5, 2), (16, 8), (64, 40)])
+@pytest.mark.parametrize("name", sorted(SEQ_SHAPES))
+def test_seq_speculative_units(name, spec):
+    """Speculative units: a warmed-up guess of each unit's start state, verified against its predecessor's end state
+    (sg_seq_equiv) and rerun from it when they differ -- exact for any warm-up, even none."""
+    q = HEAD + SEQ_SHAPES[name]
+    b = small_batch(12_000, 30, 10, 4, seed=sum(name.encode()) + 10)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True, spec=spec), q, split(b, [3000, 3001, 9000]))
+    assert_same(got, want)
