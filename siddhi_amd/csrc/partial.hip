@@ -567,6 +567,9 @@ struct SeqSrcD {
 struct SqOut {
   char* rec;
   uint64_t* k1;               // (trigger row << 16) | emission index within the row
+  uint32_t* runit;            // unit that wrote the slot (| 0x80000000 when written by a rerun)
+  uint32_t* rerun;            // per unit: 1 = its speculative matches are void
+  unsigned long long* dropped;
   unsigned long long* reserved;
   unsigned long long* count;
   int32_t* fail;
@@ -630,7 +633,7 @@ struct SqEmit {   // match writer of the emitting pass
   const uint32_t* sid;
   SqOut o;
   int64_t slot, slot_end, r;
-  uint32_t key, seq, nemit;
+  uint32_t key, seq, nemit, unit;
   __device__ void operator()(SeqMachine<SeqSrcD>& mm, int p, int grp) {
     if (slot == slot_end) {
       slot = (int64_t)atomicAdd(o.reserved, (unsigned long long)SQ_CHUNK);
@@ -640,6 +643,7 @@ struct SqEmit {   // match writer of the emitting pass
     const int64_t w = slot++;
     ++nemit;
     o.k1[w] = ((uint64_t)r << 16) | seq++;
+    o.runit[w] = unit;
     char* rec = o.rec + (size_t)w * (size_t)o.rstride;
     uint64_t* h64 = (uint64_t*)rec;
     h64[0] = pp_index(*a, r);
@@ -694,10 +698,10 @@ __device__ __forceinline__ void sq_run(SeqMachine<SeqSrcD>& m, int64_t b0, int64
     __syncthreads();                                                                                           \
   }
 
-// pass A: every unit's (guessed) start state and the end state it leads to
+// pass A: every unit from its (guessed) start state, emitting; its start and end states are kept for the check
 __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                       const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
-                                                      SqPlan pl_, int32_t* __restrict__ fail) {
+                                                      SqPlan pl_, SqOut o) {
   SQ_KERNEL_PROLOGUE
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= pl_.nunits) return;
@@ -721,63 +725,6 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
     sq_run(m, b0, w0, s0, ne, sid, a.nc, nullptr, nullptr);
   }
   sq_copy(pl_.ust + u, &M);
-  sq_run(m, b0, s0, s1, ne, sid, a.nc, nullptr, nullptr);
-  if (m.failed) atomicCAS(fail, 0, m.failed);
-  sq_copy(pl_.uen + u, &M);
-}
-
-// pass B: per key, in unit order, a unit whose guessed start differs from its predecessor's end is rerun from that end
-__global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
-                                                     const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
-                                                     SqPlan pl_, int64_t kb, int32_t* __restrict__ fail) {
-  SQ_KERNEL_PROLOGUE
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= kb) return;
-  const uint32_t u0 = pl_.uoff[k], u1 = pl_.uoff[k + 1];
-  if (u1 - u0 < 2) return;
-  const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
-  SeqState& M = lanes[threadIdx.x];
-  SeqMachine<SeqSrcD> m;
-  m.d = &dl;
-  m.ru = &rl;
-  m.src = SeqSrcD{&pl, b0};
-  m.M = &M;
-  m.cur = 0;
-  SqNoEmit ne;
-  uint32_t reruns = 0;
-  for (uint32_t u = u0 + 1; u < u1; ++u) {
-    if (sg_seq_equiv(pl_.ust[u], pl_.uen[u - 1], dl, rl)) continue;
-    ++reruns;
-    const int64_t c = u - u0;
-    const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
-    sq_copy(&M, pl_.uen + (u - 1));
-    sq_copy(pl_.ust + u, &M);
-    sq_run(m, b0, s0, s1, ne, sid, a.nc, nullptr, nullptr);
-    if (m.failed) { atomicCAS(fail, 0, m.failed); return; }
-    sq_copy(pl_.uen + u, &M);
-  }
-  if (reruns) atomicAdd(pl_.reruns, (unsigned long long)reruns);
-}
-
-// pass C: every unit from its verified start, emitting; the key's last unit leaves the state to carry
-__global__ void __launch_bounds__(SQ_BLOCK) k_sq_emit(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
-                                                      const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
-                                                      SqPlan pl_, SqOut o) {
-  SQ_KERNEL_PROLOGUE
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= pl_.nunits) return;
-  const uint32_t k = pl_.umap[u];
-  const int64_t c = u - pl_.uoff[k];
-  const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
-  const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
-  SeqState& M = lanes[threadIdx.x];
-  SeqMachine<SeqSrcD> m;
-  m.d = &dl;
-  m.ru = &rl;
-  m.src = SeqSrcD{&pl, b0};
-  m.M = &M;
-  m.cur = 0;
-  sq_copy(&M, pl_.ust + u);
   SqEmit em;
   em.a = &a;
   em.dd = &dl;
@@ -788,14 +735,72 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_emit(PpArgs a, PpPacked P, cons
   em.nemit = 0;
   em.seq = 0;
   em.r = 0;
+  em.unit = (uint32_t)u;
   sq_run(m, b0, s0, s1, em, sid, a.nc, &em.r, &em.seq);
   for (int64_t q = em.slot; q < em.slot_end && q < o.cap; ++q) o.k1[q] = o.k1_none;
   if (em.nemit) atomicAdd(o.count, (unsigned long long)em.nemit);
-  if (m.failed) { atomicCAS(o.fail, 0, m.failed); return; }
-  if (u + 1 == (int64_t)pl_.uoff[k + 1]) {
-    const int64_t nk = e0 - b0;
-    m.rebase(nk - 1, nk > rl.horizon ? nk - rl.horizon : 0);
-    sq_copy(pl_.kst + k, &M);
+  if (m.failed) atomicCAS(o.fail, 0, m.failed);
+  sq_copy(pl_.uen + u, &M);
+}
+
+// pass B: per key, in unit order, a unit whose guessed start differs from its predecessor's end is rerun from that end
+// (emitting again; its speculative matches are voided); then the key's final state is kept for the next push
+__global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
+                                                     const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
+                                                     SqPlan pl_, int64_t kb, SqOut o) {
+  SQ_KERNEL_PROLOGUE
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= kb) return;
+  const uint32_t u0 = pl_.uoff[k], u1 = pl_.uoff[k + 1];
+  if (u1 == u0) return;
+  const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
+  SeqState& M = lanes[threadIdx.x];
+  SeqMachine<SeqSrcD> m;
+  m.d = &dl;
+  m.ru = &rl;
+  m.src = SeqSrcD{&pl, b0};
+  m.M = &M;
+  m.cur = 0;
+  SqEmit em;
+  em.a = &a;
+  em.dd = &dl;
+  em.sid = sid;
+  em.o = o;
+  em.slot = em.slot_end = 0;
+  em.key = (uint32_t)k;
+  em.nemit = 0;
+  em.seq = 0;
+  em.r = 0;
+  uint32_t reruns = 0;
+  for (uint32_t u = u0 + 1; u < u1; ++u) {
+    if (sg_seq_equiv(pl_.ust[u], pl_.uen[u - 1], dl, rl)) continue;
+    ++reruns;
+    o.rerun[u] = 1;
+    em.unit = u | 0x80000000u;
+    const int64_t c = u - u0;
+    const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
+    sq_copy(&M, pl_.uen + (u - 1));
+    sq_run(m, b0, s0, s1, em, sid, a.nc, &em.r, &em.seq);
+    if (m.failed) { atomicCAS(o.fail, 0, m.failed); return; }
+    sq_copy(pl_.uen + u, &M);
+  }
+  for (int64_t q = em.slot; q < em.slot_end && q < o.cap; ++q) o.k1[q] = o.k1_none;
+  if (em.nemit) atomicAdd(o.count, (unsigned long long)em.nemit);
+  if (reruns) atomicAdd(pl_.reruns, (unsigned long long)reruns);
+  sq_copy(&M, pl_.uen + (u1 - 1));
+  const int64_t nk = e0 - b0;
+  m.rebase(nk - 1, nk > rl.horizon ? nk - rl.horizon : 0);
+  sq_copy(pl_.kst + k, &M);
+}
+
+// void the speculative matches of rerun units
+__global__ void k_sq_drop(int64_t n, SqOut o) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n || o.k1[w] == o.k1_none) return;
+  const uint32_t u = o.runit[w];
+  if (!(u & 0x80000000u) && o.rerun[u]) {
+    o.k1[w] = o.k1_none;
+    atomicAdd(o.dropped, 1ull);
   }
 }
 
@@ -834,10 +839,8 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   }
   const int nsel = d.n_select;
   const int32_t rstride = 32 + 8 * nsel;
-  const int64_t cap = n + (int64_t)SQ_CHUNK * (int64_t)kb + 65536;
+  int64_t cap = 0;   // set with the unit plan
   SqOut o;
-  o.rec = (char*)h->ws.get("sq_rec", (size_t)cap * rstride, st);
-  o.k1 = (uint64_t*)h->ws.get("sq_k1", 8 * cap, st);
   o.reserved = (unsigned long long*)h->ws.get("sq_cnt", 64, st);
   o.count = o.reserved + 1;
   o.fail = (int32_t*)(o.reserved + 2);
@@ -882,23 +885,34 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   pl_.uen = (SeqState*)h->ws.get("sq_uen", sizeof(SeqState) * ((size_t)U + 1), st);
   pl_.reruns = o.reserved + 3;
   h->kend();
+  cap = n + (int64_t)SQ_CHUNK * ((int64_t)U + (int64_t)kb) + 65536;
+  o.cap = cap;
+  o.rec = (char*)h->ws.get("sq_rec", (size_t)cap * rstride, st);
+  o.k1 = (uint64_t*)h->ws.get("sq_k1", 8 * cap, st);
   const dim3 gu((unsigned)((U + SQ_BLOCK - 1) / SQ_BLOCK)), gq((unsigned)((kb + SQ_BLOCK - 1) / SQ_BLOCK));
-  h->kbeg("sequence_spec");
-  if (U) hipLaunchKernelGGL(k_sq_spec, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o.fail);
+  o.runit = (uint32_t*)h->ws.get("sq_runit", 4 * (size_t)cap, st);
+  o.rerun = (uint32_t*)h->ws.get("sq_rerun", 4 * ((size_t)U + 1), st);
+  o.dropped = o.reserved + 4;
+  HIPCHK(hipMemsetAsync(o.rerun, 0, 4 * ((size_t)U + 1), st));
+  h->kbeg("sequence_lanes");
+  if (U) hipLaunchKernelGGL(k_sq_spec, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
   HIPCHK(hipGetLastError());
   h->kend();
   h->kbeg("sequence_fix");
-  if (U) hipLaunchKernelGGL(k_sq_fix, gq, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, (int64_t)kb, o.fail);
+  if (U) hipLaunchKernelGGL(k_sq_fix, gq, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, (int64_t)kb, o);
   HIPCHK(hipGetLastError());
   h->kend();
-  h->kbeg("sequence_lanes");
-  if (U) hipLaunchKernelGGL(k_sq_emit, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
-  HIPCHK(hipGetLastError());
-  h->kend();
-  h->mark(3);
-  unsigned long long cnt[4] = {0, 0, 0, 0};
-  HIPCHK(hipMemcpyAsync(cnt, o.reserved, 32, hipMemcpyDeviceToHost, st));
+  unsigned long long cnt[5] = {0, 0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(cnt, o.reserved, 40, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (cnt[3]) {   // some units were rerun: void their speculative matches
+    const int64_t Rz = std::min<int64_t>((int64_t)cnt[0], cap);
+    hipLaunchKernelGGL(k_sq_drop, dim3((unsigned)((Rz + 255) / 256)), blk, 0, st, Rz, o);
+    HIPCHK(hipMemcpyAsync(&cnt[4], o.dropped, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  h->mark(3);
+  cnt[1] -= cnt[4];
   ps->last_reruns = (int64_t)cnt[3];
   const int32_t fail = (int32_t)(cnt[2] & 0xffffffffu);
   if (fail) {
