@@ -23,6 +23,7 @@
 // Every method restates the KeyMachine method of interp.h with the same name (which cites its reference method).
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #include "../../include/siddhi_gpu.h"
 
@@ -45,6 +46,7 @@ struct PpOperand {
 struct PpTerm {
   PpOperand l, r;
   int32_t op, dom;
+  int32_t fast;      // 1: both operands INT/LONG in the integral domain, 2: both FLOAT in the float domain, 0: SgVal path
 };
 
 struct SgPpRule {
@@ -89,6 +91,11 @@ SG_HD inline int pp_terms(const int64_t* c, int len, PpTerm* t) {
     if (pc + 3 > len || c[pc] != SG_OP_CMP) return -1;
     t[n].op = (int32_t)c[pc + 1];
     t[n].dom = (int32_t)c[pc + 2];
+    {
+      const int lt = t[n].l.type, rt = t[n].r.type;
+      const bool li = lt == SG_T_INT || lt == SG_T_LONG, ri = rt == SG_T_INT || rt == SG_T_LONG;
+      t[n].fast = (t[n].dom == 0 && li && ri) ? 1 : (t[n].dom == 1 && lt == SG_T_FLOAT && rt == SG_T_FLOAT) ? 2 : 0;
+    }
     pc += 3;
     ++n;
     if (n > 1) {
@@ -146,11 +153,40 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   return r;
 }
 
+SG_HD inline bool pp_cmp_i(int op, int64_t a, int64_t b) {
+  switch (op) {
+    case 0: return a == b;
+    case 1: return a != b;
+    case 2: return a > b;
+    case 3: return a >= b;
+    case 4: return a < b;
+    default: return a <= b;
+  }
+}
+SG_HD inline bool pp_cmp_f(int op, float a, float b) {
+  switch (op) {
+    case 0: return a == b;
+    case 1: return a != b;
+    case 2: return a > b;
+    case 3: return a >= b;
+    case 4: return a < b;
+    default: return a <= b;
+  }
+}
+SG_HD inline float pp_f32(int64_t bits) {
+  const uint32_t u = (uint32_t)bits;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
 // Tie key of an emission: the insertion history newest first, 31 bits per component (row << 4 | visit slot), two
 // components per word (bit 63 is always set).  Rows only need to be in arrival order within one key.
 SG_HD inline uint32_t pp_tkey(int64_t row, int rank) { return (uint32_t)(((uint64_t)row << 4) | (uint32_t)(rank & 15)); }
 
 // Src interface: int64_t ts(int64_t row); SgVal read(int64_t row, int ret_slot, int type);
+//                void read_bits(int64_t row, int ret_slot, int type, int64_t& bits, int& null) (INT sign-extended,
+//                FLOAT as its 32-bit pattern -- the bit layout of sg_val_bits);
 //                int lbit(int state, int64_t row) -> 0/1, or -1 when the state's filter must be evaluated.
 // The dynamically indexed part of a lane's state (LDS on the GPU); the rest stays in registers.
 struct PpArrays {
@@ -173,20 +209,20 @@ struct PpLane {
   int32_t nh;
   int32_t overflow;
   // current row
-  int64_t cur_row;
+  int32_t cur_row;
   int cur_rank;
 
   SG_HD const sg_state_desc& st(int s) const { return d->states[s]; }
   SG_HD static uint32_t bit(int s) { return 1u << s; }
 
   // does the start state's armed partial accept this row (its filter, evaluated with e1 bound to the row)?
-  SG_HD bool start_ok(int64_t row) {
+  SG_HD bool start_ok(int32_t row) {
     for (int s = 0; s < PP_MAX_S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
     A->slot[ru->start] = (int32_t)row;
     cur_row = row;
     return filter(ru->start);
   }
-  SG_HD void start(int64_t row) {   // the armed start partial takes e1 = row (process_and_return of the start state)
+  SG_HD void start(int32_t row) {   // the armed start partial takes e1 = row (process_and_return of the start state)
     for (int s = 0; s < PP_MAX_S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
     l0 = l1 = 0;
     f_changed = f_returned = f_success = 0;
@@ -200,7 +236,7 @@ struct PpLane {
   }
 
   // ---- event access (KeyMachine::get_event): row of (state, index in chain) or -1
-  SG_HD int64_t get_event(int s, int idx) {
+  SG_HD int32_t get_event(int s, int idx) {
     if (st(s).kind != SG_K_COUNT) {
       if (A->slot[s] < 0) return -1;
       return (idx == 0 || idx == -1) ? A->slot[s] : -1;
@@ -217,13 +253,13 @@ struct PpLane {
     return c[k];
   }
   SG_HD int64_t slot_ts(int s) {
-    int64_t r = st(s).kind == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
+    int32_t r = st(s).kind == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
     return src.ts(r);
   }
   struct Reader {
     PpLane* m;
     SG_HD SgVal read(int s, int idx, int slotk, int type) {
-      const int64_t r = m->get_event(s, idx);
+      const int32_t r = m->get_event(s, idx);
       if (r < 0) {
         SgVal v;
         v.type = type;
@@ -235,6 +271,16 @@ struct PpLane {
       return m->src.read(r, slotk, type);
     }
   };
+  SG_HD void operand_bits(const PpOperand& o, int64_t& bits, int& null) {
+    if (o.kind == SG_OP_CONST) {
+      bits = o.bits;
+      null = 0;
+      return;
+    }
+    const int32_t r = get_event(o.state, o.idx);
+    if (r < 0) { bits = 0; null = 1; return; }
+    src.read_bits(r, o.slot, o.type, bits, null);
+  }
   SG_HD SgVal operand(const PpOperand& o) {
     if (o.kind == SG_OP_CONST) return sg_val_from_bits(o.bits, o.type, 0);
     Reader rd{this};
@@ -249,6 +295,21 @@ struct PpLane {
     if (nt >= 0) {
       for (int i = 0; i < nt; ++i) {
         const PpTerm& t = ru->term[s][i];
+        if (t.fast) {   // same result as sg_cmp on the two values, without building SgVals
+          int64_t a, b;
+          int na, nb;
+          operand_bits(t.l, a, na);
+          operand_bits(t.r, b, nb);
+          if (na || nb) {
+            if (t.op != 1) return false;
+            continue;
+          }
+          bool ok;
+          if (t.fast == 1) ok = pp_cmp_i(t.op, a, b);
+          else ok = pp_cmp_f(t.op, pp_f32(a), pp_f32(b));
+          if (!ok) return false;
+          continue;
+        }
         if (!sg_cmp(t.op, t.dom, operand(t.l), operand(t.r))) return false;
       }
       return true;
@@ -299,7 +360,7 @@ struct PpLane {
 
   // ---- one row: updateState of every state, then the states in visit order (KeyMachine::receive)
   // Returns the visit slot that emitted (one emission per row at most: the partial leaves the emitting state), or -1.
-  SG_HD int step(int64_t row) {
+  SG_HD int step(int32_t row) {
     cur_row = row;
     const sg_receiver_desc& rv = d->receivers[ru->recv];
     const uint32_t moved = l1;

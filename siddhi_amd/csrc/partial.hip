@@ -179,6 +179,10 @@ struct PpSrc {
     return sg_val_from_bits(bits, type, null);
   }
   __device__ int lbit(int s, int64_t q) const { return (int)((P->lb[q] >> s) & 1u); }
+  __device__ void read_bits(int64_t q, int slotk, int type, int64_t& bits, int& null) const {
+    null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
+    bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
+  }
 };
 
 __global__ void k_pp_route(PpArgs a, const DevDesc* __restrict__ dd, int partitioned, uint32_t sentinel,
@@ -562,6 +566,11 @@ struct SeqSrcD {
     return sg_val_from_bits(bits, type, null);
   }
   __device__ int lbit(int s, int64_t pos) const { return (int)((P->lb[base + pos] >> s) & 1u); }
+  __device__ void read_bits(int64_t pos, int slotk, int type, int64_t& bits, int& null) const {
+    const int64_t q = base + pos;
+    null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
+    bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
+  }
 };
 
 struct SqOut {
@@ -683,16 +692,16 @@ __device__ __forceinline__ void sq_run(SeqMachine<SeqSrcD>& m, int64_t b0, int64
   m.finish();
 }
 
+// The descriptor stays in global memory (L1-resident: every lane reads the same few hundred bytes of it); LDS holds
+// the lanes' machine states, so more waves fit per CU.
 #define SQ_KERNEL_PROLOGUE                                                                                     \
-  __shared__ DevDesc dl;                                                                                       \
+  const DevDesc& dl = *ddg;                                                                                    \
   __shared__ SgSeqRule rl;                                                                                     \
   __shared__ PpPacked pl;                                                                                      \
   __shared__ SeqState lanes[SQ_BLOCK];                                                                         \
   {                                                                                                            \
     const uint32_t* s3 = (const uint32_t*)&P;                                                                  \
     for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];    \
-    const uint32_t* src = (const uint32_t*)ddg;                                                                \
-    for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) ((uint32_t*)&dl)[i] = src[i];    \
     const uint32_t* rs = (const uint32_t*)rug;                                                                 \
     for (uint32_t i = threadIdx.x; i < sizeof(SgSeqRule) / 4; i += blockDim.x) ((uint32_t*)&rl)[i] = rs[i];   \
     __syncthreads();                                                                                           \

@@ -28,7 +28,7 @@
 #endif
 
 #define PQ_MAX_S 6
-#define PQ_MAX_P 8        // partials alive at once (pool)
+#define PQ_MAX_P 6        // partials alive at once (pool)
 #define PQ_MAX_L 4        // entries per pending / newAndEvery list
 #define PQ_MAX_CHAIN 12   // count-chain entries per partial over all count states
 #define PQ_MAX_RET 8      // partials one state returns for one event
@@ -226,6 +226,16 @@ struct SeqMachine {
       return m->src.read(r, slotk, type);
     }
   };
+  SG_HD void operand_bits(int p, const PpOperand& o, int64_t& bits, int& null) {
+    if (o.kind == SG_OP_CONST) {
+      bits = o.bits;
+      null = 0;
+      return;
+    }
+    const int64_t r = get_event(p, o.state, o.idx);
+    if (r < 0) { bits = 0; null = 1; return; }
+    src.read_bits(r, o.slot, o.type, bits, null);
+  }
   SG_HD bool filter(int s, int p) {
     if ((ru->local_mask >> s) & 1u) {
       const int b = src.lbit(s, cur);
@@ -236,6 +246,18 @@ struct SeqMachine {
     if (nt >= 0) {
       for (int i = 0; i < nt; ++i) {
         const PpTerm& t = ru->term[s][i];
+        if (t.fast) {   // same result as sg_cmp on the two values, without building SgVals
+          int64_t a, b;
+          int na, nb;
+          operand_bits(p, t.l, a, na);
+          operand_bits(p, t.r, b, nb);
+          if (na || nb) {
+            if (t.op != 1) return false;
+            continue;
+          }
+          if (!(t.fast == 1 ? pp_cmp_i(t.op, a, b) : pp_cmp_f(t.op, pp_f32(a), pp_f32(b)))) return false;
+          continue;
+        }
         const SgVal l = t.l.kind == SG_OP_CONST ? sg_val_from_bits(t.l.bits, t.l.type, 0) : rd.read(t.l.state, t.l.idx, t.l.slot, t.l.type);
         const SgVal r = t.r.kind == SG_OP_CONST ? sg_val_from_bits(t.r.bits, t.r.type, 0) : rd.read(t.r.state, t.r.idx, t.r.slot, t.r.type);
         if (!sg_cmp(t.op, t.dom, l, r)) return false;

@@ -5,6 +5,7 @@
 #define SG_HD
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -27,6 +28,7 @@ struct HiHandle {
   std::vector<CRow> carried;
   std::vector<SeqState> seq_state;   // sequence lanes: per key
   int64_t spec_rows = 0, spec_warm = 0, spec_reruns = 0;   // speculative units (0: one run per key)
+  int64_t pp_steps = 0, pp_lanes = 0;                      // partial lanes: rows stepped, lanes started
 };
 
 struct HostRows {
@@ -69,7 +71,7 @@ struct HostRows {
   }
 };
 
-static int64_t read_bits(const sg_batch* b, const sg_nfa_desc* d, int k, int64_t r, int* null) {
+static int64_t read_bits_col(const sg_batch* b, const sg_nfa_desc* d, int k, int64_t r, int* null) {
   int c = d->ret_col[k];
   int t = d->ret_type[k];
   *null = (b->nulls && b->nulls[c] && b->nulls[c][r]) ? 1 : 0;
@@ -98,11 +100,20 @@ struct HostPpSrc {
       null = ((*c)[x].nullmask >> slotk) & 1;
       bits = (*c)[x].vals[slotk];
     } else {
-      bits = read_bits(b, d, slotk, x - nc, &null);
+      bits = read_bits_col(b, d, slotk, x - nc, &null);
     }
     return sg_val_from_bits(bits, type, null);
   }
   int lbit(int, int64_t) const { return -1; }
+  void read_bits(int64_t x, int slotk, int type, int64_t& bits, int& null) const {
+    if (x < nc) {
+      null = ((*c)[x].nullmask >> slotk) & 1;
+      bits = (*c)[x].vals[slotk];
+    } else {
+      bits = read_bits_col(b, d, slotk, x - nc, &null);
+    }
+    if (type == SG_T_INT) bits = (int64_t)(int32_t)bits;
+  }
 };
 
 // partial-lane push (partial.hip restated on the host); returns 0 when the push breaks the route's precondition
@@ -142,10 +153,12 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
       L.A = &arr;
       if (!L.start_ok(rows[p])) continue;
       L.start(rows[p]);
+      ++h->pp_lanes;
       for (size_t q = p + 1; q < rows.size(); ++q) {
         const int64_t c = rows[q];
         if (src.ts(c) - L.e1_ts > d.within) break;
         const int em = L.step(c);
+        ++h->pp_steps;
         if (L.overflow) return -1;
         if (em >= 0 && c >= nc) {
           const int64_t r = c - nc;
@@ -194,7 +207,7 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
       else {
         for (int j = 0; j < d.n_ret; ++j) {
           int null = 0;
-          cr.vals[j] = read_bits(b, &d, j, c - nc, &null);
+          cr.vals[j] = read_bits_col(b, &d, j, c - nc, &null);
           if (null) cr.nullmask |= 1 << j;
         }
       }
@@ -213,6 +226,9 @@ struct HostSeqSrc {
   int64_t ts(int64_t pos) const { return base_src.ts((*rows)[pos]); }
   SgVal read(int64_t pos, int slotk, int type) const { return base_src.read((*rows)[pos], slotk, type); }
   int lbit(int, int64_t) const { return -1; }
+  void read_bits(int64_t pos, int slotk, int type, int64_t& bits, int& null) const {
+    base_src.read_bits((*rows)[pos], slotk, type, bits, null);
+  }
 };
 
 static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std::vector<uint64_t>& k1) {
@@ -289,6 +305,7 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
         if (emitting) m.receive(q, emit);
         else m.receive(q, noemit);
       }
+      if (m.failed && getenv("SG_DEBUG_SEQ")) fprintf(stderr, "seq machine failed: %d\n", m.failed);
       m.finish();
       return !m.failed;
     };
@@ -340,7 +357,7 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
         cr.key = (int32_t)k;
         for (int j = 0; j < d.n_ret; ++j) {
           int null = 0;
-          cr.vals[j] = read_bits(b, &d, j, c - nc, &null);
+          cr.vals[j] = read_bits_col(b, &d, j, c - nc, &null);
           if (null) cr.nullmask |= 1 << j;
         }
       }
@@ -357,6 +374,7 @@ extern "C" {
 void hi_set_pp(HiHandle* h, int on) { h->pp = on; }
 void hi_set_spec(HiHandle* h, int64_t rows, int64_t warm) { h->spec_rows = rows; h->spec_warm = warm; }
 int64_t hi_spec_reruns(HiHandle* h) { return h->spec_reruns; }
+int64_t hi_pp_steps(HiHandle* h, int64_t* lanes) { *lanes = h->pp_lanes; return h->pp_steps; }
 int hi_seq_rule(const sg_nfa_desc* d) { return sg_seq_rule(*d).ok; }
 int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
 
