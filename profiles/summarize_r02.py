@@ -67,7 +67,7 @@ def main(d, cfg, pushes):
                              "bytes_per_push": byt.get(m, 0.0) / pushes}
     sys.path.insert(0, ROOT)
     import bench   # noqa: E402  (source hash of the measured tree)
-    out["source_hash"] = bench.source_hash()
+    out["source_hash"] = bench.source_hash(cfg)
     try:
         out["git_head"] = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
                                          text=True).stdout.strip() or None
