@@ -62,6 +62,9 @@ struct PartialState {
   int64_t kst_keys = 0;
   int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
   int64_t last_reruns = 0;      // sequence units rerun from their predecessor's end state in the last push
+  int nulls_seen = 0;           // a push had null flags in a column the query reads (carried rows may hold nulls)
+  int8_t hot[SG_MAX_RET];       // record sort: slot -> word of the 16-B record (-1: gathered), see rec_plan
+  int rec_ok = 0;
   int used_col[SG_MAX_COLS] = {};
   int col_bytes[SG_MAX_COLS] = {};
   PpRows rows[2];       // carried rows (cur) and the next push's (double buffer)
@@ -117,6 +120,35 @@ PartialState* sg_partial_new(const sg_nfa_desc& d) {
     ps->used_col[c] = 1;
     ps->col_bytes[c] = (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE) ? 8 : 4;
   }
+  // Record sort (see k_pp_rec): the retained slots the non-local filters read must fit two 32-bit words; partial
+  // lanes carry the timestamp in the record instead of condition bits, so only the start state may be event-local.
+  {
+    for (int k = 0; k < SG_MAX_RET; ++k) ps->hot[k] = -1;
+    int words = 0;
+    bool fits = true;
+    for (int k = 0; k < d.n_ret && fits; ++k) {
+      bool used = false;
+      for (int s2 = 0; s2 < d.n_states && !used; ++s2) {
+        const sg_state_desc& x = d.states[s2];
+        if (x.local) continue;
+        for (int pc = 0; pc < x.prog_len;) {
+          const int64_t op = d.code[x.prog_off + pc];
+          if (op == SG_OP_VAR) { if (d.code[x.prog_off + pc + 3] == k) used = true; pc += 5; }
+          else if (op == SG_OP_CONST || op == SG_OP_CMP || op == SG_OP_MATH) pc += 3;
+          else pc += 1;
+        }
+      }
+      if (!used) continue;
+      const bool wide = d.ret_type[k] == SG_T_LONG || d.ret_type[k] == SG_T_DOUBLE;
+      if (words + (wide ? 2 : 1) > 2) { fits = false; break; }
+      ps->hot[k] = (int8_t)(wide ? 2 : words);
+      words += wide ? 2 : 1;
+    }
+    uint32_t local_mask = 0;
+    for (int s2 = 0; s2 < d.n_states; ++s2) if (d.states[s2].local) local_mask |= 1u << s2;
+    const int start = ps->mode == 1 ? ru.start : sr.start;
+    ps->rec_ok = fits && (ps->mode == 2 || (local_mask & ~(1u << start)) == 0);
+  }
   if (hipMalloc(&ps->drule, sizeof(SgPpRule)) != hipSuccess) { delete ps; throw SgError(SG_EHIP, "hipMalloc rule"); }
   hipMemcpy(ps->drule, &ps->rule, sizeof(SgPpRule), hipMemcpyHostToDevice);
   return ps;
@@ -163,12 +195,30 @@ struct PpArgs {
 // Key-ordered packed rows (position q = the q-th row of the key partition): what a lane reads at every step, so the
 // 64 lanes of a wave (consecutive start rows of one key) read neighbouring addresses.
 struct PpPacked {
-  int64_t* ts;
-  void* val[SG_MAX_RET];        // retained slot k: 4- or 8-byte bit patterns
+  int64_t* ts;                  // (nullptr: read through sid, lazy -- sequence lanes only need it for matches)
+  void* val[SG_MAX_RET];        // retained slot k: 4- or 8-byte bit patterns (nullptr: lazy, read through sid)
   int32_t wide[SG_MAX_RET];
   uint32_t* nul;                // null mask over retained slots (nullptr: no nulls in this push)
   uint32_t* lb;                 // condition bits of the event-local filters (rule.local_mask)
+  // lazy reads: the row's own column through the combined row id (carried rows first)
+  const uint32_t* sid;
+  int64_t nc;
+  const int64_t* bts;
+  const int64_t* cts;
+  const void* bcol[SG_MAX_RET];
+  const void* ccol[SG_MAX_RET];
 };
+__device__ __forceinline__ int64_t pp_lazy_ts(const PpPacked* P, int64_t q) {
+  const int64_t c = P->sid[q];
+  return c < P->nc ? P->cts[c] : P->bts[c - P->nc];
+}
+__device__ __forceinline__ int64_t pp_lazy_bits(const PpPacked* P, int64_t q, int k) {
+  const int64_t c = P->sid[q];
+  const bool cr = c < P->nc;
+  const void* col = cr ? P->ccol[k] : P->bcol[k];
+  const int64_t r = cr ? c : c - P->nc;
+  return P->wide[k] ? ((const int64_t*)col)[r] : (int64_t)((const int32_t*)col)[r];
+}
 
 struct PpSrc {
   const PpPacked* P;
@@ -210,17 +260,160 @@ __global__ void k_pp_route(PpArgs a, const DevDesc* __restrict__ dd, int partiti
   orow[i] = (uint32_t)i;
 }
 
+// ---- record sort: the rows' per-step fields travel through the key sort as one 16-byte record, so the key-ordered
+// rows come out of the sort instead of a gather over the whole batch.  Record: {combined row (| start flag << 31 for
+// partial lanes), timestamp - tbase (partial lanes) or event-local condition bits (sequence lanes), hot word 0,
+// hot word 1}.
+struct alignas(16) PpRec { uint32_t w[4]; };
+
+struct RecArgs {
+  int32_t mode, start, partitioned;
+  uint32_t sentinel;
+  int64_t tbase;
+  int8_t hot[SG_MAX_RET];
+};
+
+__global__ void __launch_bounds__(256) k_pp_rec(PpArgs a, SgCols bc, SgCols cc, const DevDesc* dd, RecArgs ra,
+                                                uint32_t* __restrict__ okey, PpRec* __restrict__ orec,
+                                                int32_t* __restrict__ err) {
+  __shared__ SgCols colsl[2];
+  __shared__ DevDesc dl;
+  {
+    const uint32_t* s1 = (const uint32_t*)&bc;
+    const uint32_t* s2 = (const uint32_t*)&cc;
+    for (uint32_t i = threadIdx.x; i < sizeof(SgCols) / 4; i += blockDim.x) {
+      ((uint32_t*)&colsl[0])[i] = s1[i];
+      ((uint32_t*)&colsl[1])[i] = s2[i];
+    }
+    const uint32_t* src = (const uint32_t*)dd;
+    for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) ((uint32_t*)&dl)[i] = src[i];
+    __syncthreads();
+  }
+  dd = &dl;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nc + a.n) return;
+  const bool carried = i < a.nc;
+  const int64_t r = carried ? i : i - a.nc;
+  uint32_t k = ra.sentinel;
+  if (carried) {
+    k = ra.partitioned ? (uint32_t)a.ckey[r] : 0u;
+  } else {
+    const int s = a.stream ? a.stream[r] : 0;
+    if (s >= 0 && s < SG_MAX_STREAMS && dd->recv_of_stream[s] >= 0) {
+      if (!ra.partitioned) k = 0;
+      else {
+        const int32_t kk = a.bkey ? a.bkey[r] : -1;
+        if (kk >= 0) {
+          if ((uint32_t)kk >= ra.sentinel) atomicOr(err, 2);
+          else k = (uint32_t)kk;
+        }
+      }
+    }
+  }
+  okey[i] = k;
+  PpRec rec;
+  rec.w[0] = (uint32_t)i;
+  rec.w[1] = rec.w[2] = rec.w[3] = 0;
+  if (k != ra.sentinel) {
+    const SgCols& cols = colsl[carried ? 1 : 0];
+    uint32_t lb = 0;
+    for (int s = 0; s < dd->n_states; ++s) {
+      const sg_state_desc& x = dd->states[s];
+      if (!x.local || (ra.mode == 1 && s != ra.start)) continue;
+      bool ok;
+      if (x.prog_len <= 0) ok = true;
+      else if (!carried && a.lbits[s]) ok = mask_bit(a.lbits[s], (uint64_t)r) != 0;
+      else {
+        RowReader rd{&cols, dd->ret_col, r};
+        ok = sg_eval(dd->code + x.prog_off, x.prog_len, rd);
+      }
+      if (ok) lb |= 1u << s;
+    }
+    if (ra.mode == 1) {
+      rec.w[0] |= ((lb >> ra.start) & 1u) << 31;
+      const int64_t dt = (carried ? a.cts[r] : a.bts[r]) - ra.tbase;
+      if (dt != (int64_t)(int32_t)dt) atomicOr(err, 4);
+      rec.w[1] = (uint32_t)(int32_t)dt;
+    } else {
+      rec.w[1] = lb;
+    }
+    for (int q = 0; q < dd->n_ret; ++q) {
+      const int hw = ra.hot[q];
+      if (hw < 0) continue;
+      const int64_t bits = sg_val_bits(sg_read_col(cols, dd->ret_col[q], dd->ret_type[q], r));
+      if (hw == 2) { rec.w[2] = (uint32_t)bits; rec.w[3] = (uint32_t)((uint64_t)bits >> 32); }
+      else rec.w[2 + hw] = (uint32_t)bits;
+    }
+  }
+  orec[i] = rec;
+}
+
+// sorted records -> the key-ordered SoA rows the lanes read (retained slots outside the record are gathered)
+__global__ void __launch_bounds__(256) k_pp_unpack(PpArgs a, SgCols bc, SgCols cc, const DevDesc* dd, RecArgs ra,
+                                                   const uint32_t* __restrict__ skey, const PpRec* __restrict__ srec,
+                                                   PpPacked P, uint32_t* __restrict__ sid, uint32_t* __restrict__ flag) {
+  __shared__ SgCols colsl[2];
+  __shared__ DevDesc dl;
+  {
+    const uint32_t* s1 = (const uint32_t*)&bc;
+    const uint32_t* s2 = (const uint32_t*)&cc;
+    for (uint32_t i = threadIdx.x; i < sizeof(SgCols) / 4; i += blockDim.x) {
+      ((uint32_t*)&colsl[0])[i] = s1[i];
+      ((uint32_t*)&colsl[1])[i] = s2[i];
+    }
+    const uint32_t* src = (const uint32_t*)dd;
+    for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) ((uint32_t*)&dl)[i] = src[i];
+    __syncthreads();
+  }
+  dd = &dl;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nc + a.n) return;
+  const PpRec rec = srec[q];
+  const uint32_t c = rec.w[0] & 0x7FFFFFFFu;
+  sid[q] = c;
+  if (skey[q] == ra.sentinel) { flag[q] = 0; return; }
+  const bool carried = (int64_t)c < a.nc;
+  const int64_t r = carried ? (int64_t)c : (int64_t)c - a.nc;
+  if (ra.mode == 1) {
+    const uint32_t f = rec.w[0] >> 31;
+    P.ts[q] = ra.tbase + (int64_t)(int32_t)rec.w[1];
+    P.lb[q] = f << ra.start;
+    flag[q] = f;
+  } else {
+    P.lb[q] = rec.w[1];
+    flag[q] = (rec.w[1] >> ra.start) & 1u;
+  }
+  const SgCols& cols = colsl[carried ? 1 : 0];
+  for (int k = 0; k < dd->n_ret; ++k) {
+    const int hw = ra.hot[k];
+    if (!P.val[k]) continue;   // lazy slot
+    int64_t bits;
+    if (hw == 2) bits = (int64_t)(((uint64_t)rec.w[3] << 32) | rec.w[2]);
+    else if (hw >= 0) bits = (int64_t)(int32_t)rec.w[2 + hw];
+    else bits = sg_val_bits(sg_read_col(cols, dd->ret_col[k], dd->ret_type[k], r));
+    if (P.wide[k]) ((int64_t*)P.val[k])[q] = bits;
+    else ((int32_t*)P.val[k])[q] = (int32_t)bits;
+  }
+}
+
 __global__ void k_pp_segments(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
-                              uint32_t sentinel, uint32_t* __restrict__ beg, uint32_t* __restrict__ end,
-                              int32_t* __restrict__ err) {
+                              const int64_t* __restrict__ qts, int check_order, uint32_t sentinel,
+                              uint32_t* __restrict__ beg, uint32_t* __restrict__ end, int32_t* __restrict__ err) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= m) return;
   const uint32_t k = skey[p];
   if (k == sentinel) return;
   if (p == 0 || skey[p - 1] != k) beg[k] = (uint32_t)p;
-  else {
-    const int64_t c0 = sid[p - 1], c1 = sid[p];
-    const int64_t t0 = c0 < a.nc ? a.cts[c0] : a.bts[c0 - a.nc], t1 = c1 < a.nc ? a.cts[c1] : a.bts[c1 - a.nc];
+  else if (check_order) {
+    int64_t t0, t1;
+    if (qts) {
+      t0 = qts[p - 1];
+      t1 = qts[p];
+    } else {
+      const int64_t c0 = sid[p - 1], c1 = sid[p];
+      t0 = c0 < a.nc ? a.cts[c0] : a.bts[c0 - a.nc];
+      t1 = c1 < a.nc ? a.cts[c1] : a.bts[c1 - a.nc];
+    }
     if (t0 > t1) atomicOr(err, 1);
   }
   if (p == m - 1 || skey[p + 1] != k) end[k] = (uint32_t)p + 1;
@@ -381,17 +574,12 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
             uint32_t* h32 = (uint32_t*)(rec + 16);
             h32[0] = k;
             h32[1] = (1u << 24) | (uint32_t)em;
-            uint32_t nm = 0;
-            int64_t* vals = (int64_t*)(rec + 32);
+            int64_t* vals = (int64_t*)(rec + 32);   // positions: k_sq_resolve reads the values after ordering
             for (int s = 0; s < dd->n_select; ++s) {
               const int64_t ev = L.get_event(dd->sel_state[s], dd->sel_index[s]);
-              const int rs = dd->sel_ret[s];
-              if (ev < 0) { nm |= 1u << s; vals[s] = 0; continue; }
-              const SgVal v = src.read(ev, rs, dd->ret_type[rs]);
-              if (v.null) { nm |= 1u << s; vals[s] = 0; continue; }
-              vals[s] = sg_val_bits(v);
+              vals[s] = ev < 0 ? -1 : ev;
             }
-            h32[2] = nm;
+            h32[2] = 0;
             h32[3] = 0;
           }
         }
@@ -558,19 +746,20 @@ static void sort_pairs64(SgHandle* h, const char* tag, uint64_t* k_in, uint64_t*
 struct SeqSrcD {
   const PpPacked* P;
   int64_t base;
-  __device__ int64_t ts(int64_t pos) const { return P->ts[base + pos]; }
-  __device__ SgVal read(int64_t pos, int slotk, int type) const {
-    const int64_t q = base + pos;
-    const int null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
-    const int64_t bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
-    return sg_val_from_bits(bits, type, null);
-  }
-  __device__ int lbit(int s, int64_t pos) const { return (int)((P->lb[base + pos] >> s) & 1u); }
+  __device__ int64_t ts(int64_t pos) const { return P->ts ? P->ts[base + pos] : pp_lazy_ts(P, base + pos); }
   __device__ void read_bits(int64_t pos, int slotk, int type, int64_t& bits, int& null) const {
     const int64_t q = base + pos;
     null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
+    if (!P->val[slotk]) { bits = pp_lazy_bits(P, q, slotk); return; }
     bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
   }
+  __device__ SgVal read(int64_t pos, int slotk, int type) const {
+    int64_t bits;
+    int null;
+    read_bits(pos, slotk, type, bits, null);
+    return sg_val_from_bits(bits, type, null);
+  }
+  __device__ int lbit(int s, int64_t pos) const { return (int)((P->lb[base + pos] >> s) & 1u); }
 };
 
 struct SqOut {
@@ -655,23 +844,20 @@ struct SqEmit {   // match writer of the emitting pass
     o.runit[w] = unit;
     char* rec = o.rec + (size_t)w * (size_t)o.rstride;
     uint64_t* h64 = (uint64_t*)rec;
+    // positions only: k_sq_resolve turns them into timestamps and values once the matches are in delivery order
+    // (one thread per match instead of dependent reads in the lane's critical path)
     h64[0] = pp_index(*a, r);
     const int64_t pp = mm.dec(mm.M->P[p].pts);
-    h64[1] = (uint64_t)(pp >= 0 ? mm.src.ts(pp) : -1);
+    h64[1] = (uint64_t)(pp >= 0 ? mm.src.base + pp : -1);
     uint32_t* h32 = (uint32_t*)(rec + 16);
     h32[0] = key;
     h32[1] = (1u << 24) | (uint32_t)grp;
-    uint32_t nm = 0;
     int64_t* vals = (int64_t*)(rec + 32);
     for (int s = 0; s < dd->n_select; ++s) {
       const int64_t ev = mm.get_event(p, dd->sel_state[s], dd->sel_index[s]);
-      const int rs = dd->sel_ret[s];
-      if (ev < 0) { nm |= 1u << s; vals[s] = 0; continue; }
-      const SgVal v = mm.src.read(ev, rs, dd->ret_type[rs]);
-      if (v.null) { nm |= 1u << s; vals[s] = 0; continue; }
-      vals[s] = sg_val_bits(v);
+      vals[s] = ev < 0 ? -1 : mm.src.base + ev;
     }
-    h32[2] = nm;
+    h32[2] = 0;
     h32[3] = 0;
   }
 };
@@ -813,6 +999,30 @@ __global__ void k_sq_drop(int64_t n, SqOut o) {
   }
 }
 
+// match records in delivery order: key-ordered positions -> timestamp and projected values (SelectiveStateEventPopulator)
+__global__ void k_sq_resolve(int64_t n, char* __restrict__ out, int32_t stride, PpPacked P, const DevDesc* __restrict__ dd,
+                             int resolve_ts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  char* rec = out + (size_t)i * stride;
+  int64_t* h64 = (int64_t*)rec;
+  if (resolve_ts) {
+    const int64_t tp = h64[1];
+    h64[1] = tp >= 0 ? (P.ts ? P.ts[tp] : pp_lazy_ts(&P, tp)) : -1;
+  }
+  uint32_t nm = 0;
+  int64_t* vals = (int64_t*)(rec + 32);
+  for (int s = 0; s < dd->n_select; ++s) {
+    const int64_t q = vals[s];
+    const int rs = dd->sel_ret[s];
+    if (q < 0 || (P.nul && ((P.nul[q] >> rs) & 1u))) { nm |= 1u << s; vals[s] = 0; continue; }
+    int64_t bits = P.val[rs] ? (P.wide[rs] ? ((const int64_t*)P.val[rs])[q] : (int64_t)((const int32_t*)P.val[rs])[q])
+                             : pp_lazy_bits(&P, q, rs);
+    vals[s] = sg_val_bits(sg_val_from_bits(bits, dd->ret_type[rs], 0));
+  }
+  ((uint32_t*)(rec + 16))[2] = nm;
+}
+
 // carry for sequence lanes: the last H rows of every key
 __global__ void k_seq_keep(int64_t m, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ end, uint32_t sentinel,
                            int64_t H, uint32_t* __restrict__ keep) {
@@ -949,6 +1159,9 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
     hipLaunchKernelGGL(k_pp_gather, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total, o.rec, ib, rstride,
                        out + (size_t)h->out.n * rstride);
     HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_sq_resolve, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total,
+                       out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, 1);
+    HIPCHK(hipGetLastError());
     h->kend();
     h->out.n += total;
   }
@@ -1038,44 +1251,11 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   const uint32_t sentinel = kb;
   const dim3 blk(256), grd((unsigned)((m + 255) / 256));
   uint32_t* keys = (uint32_t*)h->ws.get("pp_keys", 4 * m, st);
-  uint32_t* ids = (uint32_t*)h->ws.get("pp_ids", 4 * m, st);
   uint32_t* skeys = (uint32_t*)h->ws.get("pp_skeys", 4 * m, st);
   uint32_t* sids = (uint32_t*)h->ws.get("pp_sids", 4 * m, st);
   int32_t* err = (int32_t*)h->ws.get("pp_err", 8, st);
   HIPCHK(hipMemsetAsync(err, 0, 8, st));
   h->mark(0);
-  h->kbeg("route");
-  hipLaunchKernelGGL(k_pp_route, grd, blk, 0, st, a, h->ddesc, d.partitioned, sentinel, keys, ids, err);
-  HIPCHK(hipGetLastError());
-  h->kend();
-  h->mark(1);
-  h->kbeg("key_sort");
-  {
-    size_t tb = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, ids, sids, (size_t)m, 0, end_bit, st));
-    void* tmp = h->ws.get("pp_sort_tmp", tb, st);
-    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, ids, sids, (size_t)m, 0, end_bit, st));
-  }
-  uint32_t* beg = (uint32_t*)h->ws.get("pp_beg", 4 * (size_t)kb, st);
-  uint32_t* end = (uint32_t*)h->ws.get("pp_end", 4 * (size_t)kb, st);
-  HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
-  HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
-  if (m) hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, sentinel, beg, end, err);
-  HIPCHK(hipGetLastError());
-  h->kend();
-  {
-    int32_t herr = 0;
-    HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (herr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-    if ((herr & 1) && ps->mode == 1) {
-      if (ps->has_count && nc > 0)
-        throw SgError(SG_EORDER, "partial-lane route requires non-decreasing timestamps per key once a count state holds "
-                                 "partials (open the handle with partial_lanes = -1 for such streams)");
-      return 0;
-    }
-  }
-  h->mark(2);
   // ---- predicate-evaluation pass over the batch rows
   for (int s = 0; s < SG_MAX_STATES; ++s) a.lbits[s] = nullptr;
   {
@@ -1103,14 +1283,14 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     }
     if (any) h->kend();
   }
-  // ---- key-ordered packed rows, start rows
+  h->mark(1);
+  // ---- the key-ordered rows the lanes read
+  bool batch_nul = false;
+  for (int k = 0; k < d.n_ret; ++k) batch_nul |= bv.cols.nul[d.ret_col[k]] != nullptr;
+  if (batch_nul) ps->nulls_seen = 1;
+  const bool any_nul = batch_nul || (nc > 0 && ps->nulls_seen);
   PpPacked P;
   memset(&P, 0, sizeof(P));
-  bool any_nul = false;
-  for (int k = 0; k < d.n_ret; ++k) {
-    const int c = d.ret_col[k];
-    any_nul |= bv.cols.nul[c] != nullptr || (nc > 0 && cc.nul[c] != nullptr);
-  }
   P.ts = (int64_t*)h->ws.get("pp_qts", 8 * m, st);
   for (int k = 0; k < d.n_ret; ++k) {
     P.wide[k] = (d.ret_type[k] == SG_T_LONG || d.ret_type[k] == SG_T_DOUBLE) ? 1 : 0;
@@ -1118,17 +1298,110 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   }
   P.nul = any_nul ? (uint32_t*)h->ws.get("pp_qnul", 4 * m, st) : nullptr;
   P.lb = (uint32_t*)h->ws.get("pp_qlb", 4 * m, st);
+  P.sid = sids;
+  P.nc = nc;
+  P.bts = bv.ts;
+  P.cts = cr.ts;
+  for (int k = 0; k < d.n_ret; ++k) {
+    P.bcol[k] = bv.cols.col[d.ret_col[k]];
+    P.ccol[k] = cc.col[d.ret_col[k]];
+  }
   uint32_t* flag = (uint32_t*)h->ws.get("pp_flag", 4 * (m + 1), st);
   uint32_t* fpos = (uint32_t*)h->ws.get("pp_fpos", 4 * (m + 1), st);
   uint32_t* cand = (uint32_t*)h->ws.get("pp_cand", 4 * (m + 1), st);
-  h->kbeg("pack");
-  if (m) hipLaunchKernelGGL(k_pp_pack, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->rule.local_mask, ps->rule.start,
-                            skeys, sids, sentinel, P, flag);
-  HIPCHK(hipGetLastError());
-  if (ps->mode == 2) {
+  uint32_t* beg = (uint32_t*)h->ws.get("pp_beg", 4 * (size_t)kb, st);
+  uint32_t* end = (uint32_t*)h->ws.get("pp_end", 4 * (size_t)kb, st);
+  bool rec_mode = ps->rec_ok && !any_nul && m > 0;
+  if (rec_mode) {
+    // record sort: one 16-B record per row through the key sort, unpacked into the SoA rows (no batch-wide gather)
+    RecArgs ra;
+    memset(&ra, 0, sizeof(ra));
+    ra.mode = ps->mode;
+    ra.start = ps->rule.start;
+    ra.partitioned = d.partitioned;
+    ra.sentinel = sentinel;
+    for (int k = 0; k < SG_MAX_RET; ++k) ra.hot[k] = ps->hot[k];
+    int64_t t0 = 0;
+    HIPCHK(hipMemcpyAsync(&t0, n ? bv.ts : cr.ts, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ra.tbase = t0;
+    PpRec* recs = (PpRec*)h->ws.get("pp_recs", sizeof(PpRec) * m, st);
+    PpRec* srecs = (PpRec*)h->ws.get("pp_srecs", sizeof(PpRec) * m, st);
+    h->kbeg("route");
+    hipLaunchKernelGGL(k_pp_rec, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ra, keys, recs, err);
+    HIPCHK(hipGetLastError());
     h->kend();
-    return seq_lanes_push(h, ps, bv, n, kb, a, P, skeys, sids, beg, end, sentinel);
+    h->kbeg("key_sort");
+    {
+      size_t tb = 0;
+      HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, recs, srecs, (size_t)m, 0, end_bit, st));
+      void* tmp = h->ws.get("pp_rsort_tmp", tb, st);
+      HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, recs, srecs, (size_t)m, 0, end_bit, st));
+    }
+    h->kend();
+    int32_t herr = 0;
+    HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (herr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+    if (herr & 4) {   // a timestamp more than 2^31 ms from the push's first: the gather path carries full timestamps
+      rec_mode = false;
+      HIPCHK(hipMemsetAsync(err, 0, 8, st));
+    } else {
+      if (ps->mode == 2) {   // sequence lanes read timestamps and the other slots only for matches: lazily
+        P.ts = nullptr;
+        for (int k = 0; k < d.n_ret; ++k) if (ps->hot[k] < 0) P.val[k] = nullptr;
+      }
+      h->kbeg("pack");
+      hipLaunchKernelGGL(k_pp_unpack, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ra, skeys, srecs, P, sids, flag);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
+      HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
+      hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, P.ts, ps->mode == 1 ? 1 : 0, sentinel, beg,
+                         end, err);
+      HIPCHK(hipGetLastError());
+      h->kend();
+    }
   }
+  if (!rec_mode) {
+    uint32_t* ids = (uint32_t*)h->ws.get("pp_ids", 4 * m, st);
+    h->kbeg("route");
+    hipLaunchKernelGGL(k_pp_route, grd, blk, 0, st, a, h->ddesc, d.partitioned, sentinel, keys, ids, err);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->kbeg("key_sort");
+    {
+      size_t tb = 0;
+      HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, ids, sids, (size_t)m, 0, end_bit, st));
+      void* tmp = h->ws.get("pp_sort_tmp", tb, st);
+      HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, ids, sids, (size_t)m, 0, end_bit, st));
+    }
+    HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
+    HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
+    if (m) hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, (const int64_t*)nullptr,
+                              ps->mode == 1 ? 1 : 0, sentinel, beg, end, err);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->kbeg("pack");
+    if (m) hipLaunchKernelGGL(k_pp_pack, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->rule.local_mask, ps->rule.start,
+                              skeys, sids, sentinel, P, flag);
+    HIPCHK(hipGetLastError());
+    h->kend();
+  }
+  {
+    int32_t herr = 0;
+    HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (herr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+    if ((herr & 1) && ps->mode == 1) {
+      if (ps->has_count && nc > 0)
+        throw SgError(SG_EORDER, "partial-lane route requires non-decreasing timestamps per key once a count state holds "
+                                 "partials (open the handle with partial_lanes = -1 for such streams)");
+      return 0;
+    }
+  }
+  h->mark(2);
+  if (ps->mode == 2) return seq_lanes_push(h, ps, bv, n, kb, a, P, skeys, sids, beg, end, sentinel);
+  h->kbeg("start_rows");
   HIPCHK(hipMemsetAsync(flag + m, 0, 4, st));
   {
     size_t tb = 0;
@@ -1218,6 +1491,9 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     hipLaunchKernelGGL(k_pp_gather, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, o.rec, ia, rstride,
                        out + (size_t)h->out.n * rstride);
     HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_sq_resolve, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, out + (size_t)h->out.n * rstride,
+                       rstride, P, h->ddesc, 0);
+    HIPCHK(hipGetLastError());
     h->kend();
     h->out.n += M;
   }
@@ -1258,6 +1534,7 @@ void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
 
 void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& rd) {
   sg_partial_reset(ps);
+  ps->nulls_seen = 1;   // the restored rows may hold nulls
   if (rd.pod<int32_t>() != ps->mode) throw SgError(SG_EINVAL, "snapshot: lane route differs");
   if (ps->mode == 2) {
     const int64_t keys = rd.pod<int64_t>();
