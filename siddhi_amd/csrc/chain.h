@@ -205,6 +205,7 @@ struct PpLane {
   uint32_t l0, l1;
   uint32_t f_changed, f_returned, f_success;
   int64_t pts;
+  int32_t pts_pos;   // the row whose timestamp pts is
   int64_t e1_ts;
   int32_t nh;
   int32_t overflow;
@@ -322,6 +323,7 @@ struct PpLane {
   SG_HD void stream_post(int s) {
     const sg_state_desc& x = st(s);
     f_changed |= bit(s);
+    pts_pos = st(s).kind == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
     pts = slot_ts(s);
     if (x.has_selector) f_returned |= bit(s);
     if (x.next_state >= 0) add_state(x.next_state);
@@ -330,7 +332,8 @@ struct PpLane {
     const sg_state_desc& x = st(s);
     const int n = A->clen[s];
     f_success |= bit(s);
-    pts = src.ts(A->chain[ru->coff[s] + n - 1]);
+    pts_pos = A->chain[ru->coff[s] + n - 1];
+    pts = src.ts(pts_pos);
     if (n >= x.min_count) {
       if (n == x.min_count && x.next_state >= 0) add_state(x.next_state);   // count_min_reached (no selector)
       if (n == x.max_count) f_changed |= bit(s);

@@ -567,20 +567,12 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
             o.jp[w] = (uint32_t)q;
             const uint32_t off = (uint32_t)(q - p0);
             maxoff = off > maxoff ? off : maxoff;
-            char* rec = o.rec + (size_t)w * (size_t)o.rstride;
-            uint64_t* h64 = (uint64_t*)rec;
-            h64[0] = pp_index(a, r);
-            h64[1] = (uint64_t)L.pts;
-            uint32_t* h32 = (uint32_t*)(rec + 16);
-            h32[0] = k;
-            h32[1] = (1u << 24) | (uint32_t)em;
-            int64_t* vals = (int64_t*)(rec + 32);   // positions: k_sq_resolve reads the values after ordering
-            for (int s = 0; s < dd->n_select; ++s) {
-              const int64_t ev = L.get_event(dd->sel_state[s], dd->sel_index[s]);
-              vals[s] = ev < 0 ? -1 : ev;
-            }
-            h32[2] = 0;
-            h32[3] = 0;
+            uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);   // compact: positions (k_em_out)
+            em32[0] = (uint32_t)q;
+            em32[1] = k;
+            em32[2] = (1u << 24) | (uint32_t)em;
+            em32[3] = (uint32_t)L.pts_pos;
+            for (int s = 0; s < dd->n_select; ++s) em32[4 + s] = (uint32_t)L.get_event(dd->sel_state[s], dd->sel_index[s]);
           }
         }
         ++q;
@@ -842,23 +834,18 @@ struct SqEmit {   // match writer of the emitting pass
     ++nemit;
     o.k1[w] = ((uint64_t)r << 16) | seq++;
     o.runit[w] = unit;
-    char* rec = o.rec + (size_t)w * (size_t)o.rstride;
-    uint64_t* h64 = (uint64_t*)rec;
-    // positions only: k_sq_resolve turns them into timestamps and values once the matches are in delivery order
-    // (one thread per match instead of dependent reads in the lane's critical path)
-    h64[0] = pp_index(*a, r);
+    // positions only: k_em_out turns them into the match record once the matches are in delivery order (one thread
+    // per match instead of dependent reads in the lane's critical path)
+    uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);
     const int64_t pp = mm.dec(mm.M->P[p].pts);
-    h64[1] = (uint64_t)(pp >= 0 ? mm.src.base + pp : -1);
-    uint32_t* h32 = (uint32_t*)(rec + 16);
-    h32[0] = key;
-    h32[1] = (1u << 24) | (uint32_t)grp;
-    int64_t* vals = (int64_t*)(rec + 32);
+    em32[0] = (uint32_t)(mm.src.base + mm.cur);
+    em32[1] = key;
+    em32[2] = (1u << 24) | (uint32_t)grp;
+    em32[3] = (uint32_t)(pp >= 0 ? mm.src.base + pp : -1);
     for (int s = 0; s < dd->n_select; ++s) {
       const int64_t ev = mm.get_event(p, dd->sel_state[s], dd->sel_index[s]);
-      vals[s] = ev < 0 ? -1 : mm.src.base + ev;
+      em32[4 + s] = (uint32_t)(ev < 0 ? -1 : mm.src.base + ev);
     }
-    h32[2] = 0;
-    h32[3] = 0;
   }
 };
 struct SqNoEmit {
@@ -999,28 +986,36 @@ __global__ void k_sq_drop(int64_t n, SqOut o) {
   }
 }
 
-// match records in delivery order: key-ordered positions -> timestamp and projected values (SelectiveStateEventPopulator)
-__global__ void k_sq_resolve(int64_t n, char* __restrict__ out, int32_t stride, PpPacked P, const DevDesc* __restrict__ dd,
-                             int resolve_ts) {
+// Match records in delivery order (QuerySelector.processNoGroupBy + SelectiveStateEventPopulator,
+// C/query/selector/QuerySelector.java:125-163): the lanes' compact records {trigger position, key, group, position of
+// the timestamp row, position per select slot} -> {trigger index, ts, key, group, null mask, values}.
+__global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char* __restrict__ em, int32_t estride,
+                         char* __restrict__ out, int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
+                         const uint64_t* __restrict__ index, uint64_t base_index) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  char* rec = out + (size_t)i * stride;
+  const uint32_t* e = (const uint32_t*)(em + (size_t)idx[i] * estride);
+  char* rec = out + (size_t)i * ostride;
   int64_t* h64 = (int64_t*)rec;
-  if (resolve_ts) {
-    const int64_t tp = h64[1];
-    h64[1] = tp >= 0 ? (P.ts ? P.ts[tp] : pp_lazy_ts(&P, tp)) : -1;
-  }
+  const int64_t r = (int64_t)P.sid[e[0]] - P.nc;
+  h64[0] = (int64_t)(index ? index[r] : base_index + (uint64_t)r);
+  const int32_t tp = (int32_t)e[3];
+  h64[1] = tp >= 0 ? (P.ts ? P.ts[tp] : pp_lazy_ts(&P, tp)) : -1;
+  uint32_t* h32 = (uint32_t*)(rec + 16);
+  h32[0] = e[1];
+  h32[1] = e[2];
   uint32_t nm = 0;
   int64_t* vals = (int64_t*)(rec + 32);
   for (int s = 0; s < dd->n_select; ++s) {
-    const int64_t q = vals[s];
+    const int32_t q = (int32_t)e[4 + s];
     const int rs = dd->sel_ret[s];
     if (q < 0 || (P.nul && ((P.nul[q] >> rs) & 1u))) { nm |= 1u << s; vals[s] = 0; continue; }
-    int64_t bits = P.val[rs] ? (P.wide[rs] ? ((const int64_t*)P.val[rs])[q] : (int64_t)((const int32_t*)P.val[rs])[q])
-                             : pp_lazy_bits(&P, q, rs);
+    const int64_t bits = P.val[rs] ? (P.wide[rs] ? ((const int64_t*)P.val[rs])[q] : (int64_t)((const int32_t*)P.val[rs])[q])
+                                   : pp_lazy_bits(&P, q, rs);
     vals[s] = sg_val_bits(sg_val_from_bits(bits, dd->ret_type[rs], 0));
   }
-  ((uint32_t*)(rec + 16))[2] = nm;
+  h32[2] = nm;
+  h32[3] = 0;
 }
 
 // carry for sequence lanes: the last H rows of every key
@@ -1064,7 +1059,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   o.count = o.reserved + 1;
   o.fail = (int32_t*)(o.reserved + 2);
   o.cap = cap;
-  o.rstride = rstride;
+  o.rstride = 16 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
   int rb = 1;
   while ((1ll << rb) < n + 1) ++rb;
   const int k1_bits = std::min(64, rb + 16);
@@ -1156,11 +1151,8 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
     void* tmp = h->ws.get("sq_sorttmp", tb, st);
     HIPCHK(rocprim::radix_sort_pairs(tmp, tb, o.k1, kb2, ia, ib, (size_t)R, 0, k1_bits, st));
     char* out = h->out.reserve(total, nsel, st);
-    hipLaunchKernelGGL(k_pp_gather, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total, o.rec, ib, rstride,
-                       out + (size_t)h->out.n * rstride);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_sq_resolve, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total,
-                       out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, 1);
+    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total, ib, o.rec, o.rstride,
+                       out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());
     h->kend();
     h->out.n += total;
@@ -1428,7 +1420,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   o.maxoff = (uint32_t*)(o.count + 1);
   o.jp = (uint32_t*)h->ws.get("pp_jp", 4 * cap, st);
   o.fail = err + 1;
-  o.rstride = rstride;
+  o.rstride = 16 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
   int rb = 1;
   while ((1ll << rb) < n + 1) ++rb;
   const int k1_bits = std::min(64, rb + 8);
@@ -1488,11 +1480,8 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     }
     const int64_t M = (int64_t)total;
     char* out = h->out.reserve(M, nsel, st);
-    hipLaunchKernelGGL(k_pp_gather, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, o.rec, ia, rstride,
-                       out + (size_t)h->out.n * rstride);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_sq_resolve, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, out + (size_t)h->out.n * rstride,
-                       rstride, P, h->ddesc, 0);
+    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, ia, o.rec, o.rstride,
+                       out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());
     h->kend();
     h->out.n += M;
