@@ -290,62 +290,64 @@ __global__ void __launch_bounds__(256) k_pp_rec(PpArgs a, SgCols bc, SgCols cc, 
     __syncthreads();
   }
   dd = &dl;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.nc + a.n) return;
-  const bool carried = i < a.nc;
-  const int64_t r = carried ? i : i - a.nc;
-  uint32_t k = ra.sentinel;
-  if (carried) {
-    k = ra.partitioned ? (uint32_t)a.ckey[r] : 0u;
-  } else {
-    const int s = a.stream ? a.stream[r] : 0;
-    if (s >= 0 && s < SG_MAX_STREAMS && dd->recv_of_stream[s] >= 0) {
-      if (!ra.partitioned) k = 0;
-      else {
-        const int32_t kk = a.bkey ? a.bkey[r] : -1;
-        if (kk >= 0) {
-          if ((uint32_t)kk >= ra.sentinel) atomicOr(err, 2);
-          else k = (uint32_t)kk;
+  // grid-stride: a few thousand blocks each stage the descriptors once and walk many rows
+  const int64_t m_ = a.nc + a.n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m_; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool carried = i < a.nc;
+    const int64_t r = carried ? i : i - a.nc;
+    uint32_t k = ra.sentinel;
+    if (carried) {
+      k = ra.partitioned ? (uint32_t)a.ckey[r] : 0u;
+    } else {
+      const int s = a.stream ? a.stream[r] : 0;
+      if (s >= 0 && s < SG_MAX_STREAMS && dd->recv_of_stream[s] >= 0) {
+        if (!ra.partitioned) k = 0;
+        else {
+          const int32_t kk = a.bkey ? a.bkey[r] : -1;
+          if (kk >= 0) {
+            if ((uint32_t)kk >= ra.sentinel) atomicOr(err, 2);
+            else k = (uint32_t)kk;
+          }
         }
       }
     }
-  }
-  okey[i] = k;
-  PpRec rec;
-  rec.w[0] = (uint32_t)i;
-  rec.w[1] = rec.w[2] = rec.w[3] = 0;
-  if (k != ra.sentinel) {
-    const SgCols& cols = colsl[carried ? 1 : 0];
-    uint32_t lb = 0;
-    for (int s = 0; s < dd->n_states; ++s) {
-      const sg_state_desc& x = dd->states[s];
-      if (!x.local || (ra.mode == 1 && s != ra.start)) continue;
-      bool ok;
-      if (x.prog_len <= 0) ok = true;
-      else if (!carried && a.lbits[s]) ok = mask_bit(a.lbits[s], (uint64_t)r) != 0;
-      else {
-        RowReader rd{&cols, dd->ret_col, r};
-        ok = sg_eval(dd->code + x.prog_off, x.prog_len, rd);
+    okey[i] = k;
+    PpRec rec;
+    rec.w[0] = (uint32_t)i;
+    rec.w[1] = rec.w[2] = rec.w[3] = 0;
+    if (k != ra.sentinel) {
+      const SgCols& cols = colsl[carried ? 1 : 0];
+      uint32_t lb = 0;
+      for (int s = 0; s < dd->n_states; ++s) {
+        const sg_state_desc& x = dd->states[s];
+        if (!x.local || (ra.mode == 1 && s != ra.start)) continue;
+        bool ok;
+        if (x.prog_len <= 0) ok = true;
+        else if (!carried && a.lbits[s]) ok = mask_bit(a.lbits[s], (uint64_t)r) != 0;
+        else {
+          RowReader rd{&cols, dd->ret_col, r};
+          ok = sg_eval(dd->code + x.prog_off, x.prog_len, rd);
+        }
+        if (ok) lb |= 1u << s;
       }
-      if (ok) lb |= 1u << s;
+      if (ra.mode == 1) {
+        rec.w[0] |= ((lb >> ra.start) & 1u) << 31;
+        const int64_t dt = (carried ? a.cts[r] : a.bts[r]) - ra.tbase;
+        if (dt != (int64_t)(int32_t)dt) atomicOr(err, 4);
+        rec.w[1] = (uint32_t)(int32_t)dt;
+      } else {
+        rec.w[1] = lb;
+      }
+      for (int q = 0; q < dd->n_ret; ++q) {
+        const int hw = ra.hot[q];
+        if (hw < 0) continue;
+        const int64_t bits = sg_val_bits(sg_read_col(cols, dd->ret_col[q], dd->ret_type[q], r));
+        if (hw == 2) { rec.w[2] = (uint32_t)bits; rec.w[3] = (uint32_t)((uint64_t)bits >> 32); }
+        else rec.w[2 + hw] = (uint32_t)bits;
+      }
     }
-    if (ra.mode == 1) {
-      rec.w[0] |= ((lb >> ra.start) & 1u) << 31;
-      const int64_t dt = (carried ? a.cts[r] : a.bts[r]) - ra.tbase;
-      if (dt != (int64_t)(int32_t)dt) atomicOr(err, 4);
-      rec.w[1] = (uint32_t)(int32_t)dt;
-    } else {
-      rec.w[1] = lb;
-    }
-    for (int q = 0; q < dd->n_ret; ++q) {
-      const int hw = ra.hot[q];
-      if (hw < 0) continue;
-      const int64_t bits = sg_val_bits(sg_read_col(cols, dd->ret_col[q], dd->ret_type[q], r));
-      if (hw == 2) { rec.w[2] = (uint32_t)bits; rec.w[3] = (uint32_t)((uint64_t)bits >> 32); }
-      else rec.w[2 + hw] = (uint32_t)bits;
-    }
+    orec[i] = rec;
   }
-  orec[i] = rec;
 }
 
 // sorted records -> the key-ordered SoA rows the lanes read (retained slots outside the record are gathered)
@@ -366,33 +368,35 @@ __global__ void __launch_bounds__(256) k_pp_unpack(PpArgs a, SgCols bc, SgCols c
     __syncthreads();
   }
   dd = &dl;
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= a.nc + a.n) return;
-  const PpRec rec = srec[q];
-  const uint32_t c = rec.w[0] & 0x7FFFFFFFu;
-  sid[q] = c;
-  if (skey[q] == ra.sentinel) { flag[q] = 0; return; }
-  const bool carried = (int64_t)c < a.nc;
-  const int64_t r = carried ? (int64_t)c : (int64_t)c - a.nc;
-  if (ra.mode == 1) {
-    const uint32_t f = rec.w[0] >> 31;
-    P.ts[q] = ra.tbase + (int64_t)(int32_t)rec.w[1];
-    P.lb[q] = f << ra.start;
-    flag[q] = f;
-  } else {
-    P.lb[q] = rec.w[1];
-    flag[q] = (rec.w[1] >> ra.start) & 1u;
-  }
-  const SgCols& cols = colsl[carried ? 1 : 0];
-  for (int k = 0; k < dd->n_ret; ++k) {
-    const int hw = ra.hot[k];
-    if (!P.val[k]) continue;   // lazy slot
-    int64_t bits;
-    if (hw == 2) bits = (int64_t)(((uint64_t)rec.w[3] << 32) | rec.w[2]);
-    else if (hw >= 0) bits = (int64_t)(int32_t)rec.w[2 + hw];
-    else bits = sg_val_bits(sg_read_col(cols, dd->ret_col[k], dd->ret_type[k], r));
-    if (P.wide[k]) ((int64_t*)P.val[k])[q] = bits;
-    else ((int32_t*)P.val[k])[q] = (int32_t)bits;
+  // grid-stride: a few thousand blocks each stage the descriptors once and walk many rows
+  const int64_t m_ = a.nc + a.n;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m_; q += (int64_t)gridDim.x * blockDim.x) {
+    const PpRec rec = srec[q];
+    const uint32_t c = rec.w[0] & 0x7FFFFFFFu;
+    sid[q] = c;
+    if (skey[q] == ra.sentinel) { flag[q] = 0; continue; }
+    const bool carried = (int64_t)c < a.nc;
+    const int64_t r = carried ? (int64_t)c : (int64_t)c - a.nc;
+    if (ra.mode == 1) {
+      const uint32_t f = rec.w[0] >> 31;
+      P.ts[q] = ra.tbase + (int64_t)(int32_t)rec.w[1];
+      P.lb[q] = f << ra.start;
+      flag[q] = f;
+    } else {
+      P.lb[q] = rec.w[1];
+      flag[q] = (rec.w[1] >> ra.start) & 1u;
+    }
+    const SgCols& cols = colsl[carried ? 1 : 0];
+    for (int k = 0; k < dd->n_ret; ++k) {
+      const int hw = ra.hot[k];
+      if (!P.val[k]) continue;   // lazy slot
+      int64_t bits;
+      if (hw == 2) bits = (int64_t)(((uint64_t)rec.w[3] << 32) | rec.w[2]);
+      else if (hw >= 0) bits = (int64_t)(int32_t)rec.w[2 + hw];
+      else bits = sg_val_bits(sg_read_col(cols, dd->ret_col[k], dd->ret_type[k], r));
+      if (P.wide[k]) ((int64_t*)P.val[k])[q] = bits;
+      else ((int32_t*)P.val[k])[q] = (int32_t)bits;
+    }
   }
 }
 
@@ -453,39 +457,40 @@ __global__ void __launch_bounds__(256) k_pp_pack(PpArgs a, SgCols bc, SgCols cc,
     __syncthreads();
   }
   dd = &dl;
-  const int64_t m = a.nc + a.n;
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= m) return;
-  if (skey[q] == sentinel) { flag[q] = 0; return; }
-  const int64_t c = sid[q];
-  const bool carried = c < a.nc;
-  const int64_t r = carried ? c : c - a.nc;
-  const SgCols& cols = colsl[carried ? 1 : 0];
-  P.ts[q] = carried ? a.cts[r] : a.bts[r];
-  uint32_t nm = 0;
-  for (int k = 0; k < dd->n_ret; ++k) {
-    const SgVal v = sg_read_col(cols, dd->ret_col[k], dd->ret_type[k], r);
-    if (v.null) nm |= 1u << k;
-    const int64_t bits = sg_val_bits(v);
-    if (P.wide[k]) ((int64_t*)P.val[k])[q] = bits;
-    else ((int32_t*)P.val[k])[q] = (int32_t)bits;
-  }
-  if (P.nul) P.nul[q] = nm;
-  uint32_t lb = 0;
-  for (int s = 0; s < dd->n_states; ++s) {
-    if (!((local_mask >> s) & 1u)) continue;
-    const sg_state_desc& x = dd->states[s];
-    bool ok;
-    if (x.prog_len <= 0) ok = true;
-    else if (!carried && a.lbits[s]) ok = mask_bit(a.lbits[s], (uint64_t)r) != 0;
-    else {
-      RowReader rd{&cols, dd->ret_col, r};
-      ok = sg_eval(dd->code + x.prog_off, x.prog_len, rd);
+  // grid-stride: a few thousand blocks each stage the descriptors once and walk many rows
+  const int64_t m_ = a.nc + a.n;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m_; q += (int64_t)gridDim.x * blockDim.x) {
+    if (skey[q] == sentinel) { flag[q] = 0; continue; }
+    const int64_t c = sid[q];
+    const bool carried = c < a.nc;
+    const int64_t r = carried ? c : c - a.nc;
+    const SgCols& cols = colsl[carried ? 1 : 0];
+    P.ts[q] = carried ? a.cts[r] : a.bts[r];
+    uint32_t nm = 0;
+    for (int k = 0; k < dd->n_ret; ++k) {
+      const SgVal v = sg_read_col(cols, dd->ret_col[k], dd->ret_type[k], r);
+      if (v.null) nm |= 1u << k;
+      const int64_t bits = sg_val_bits(v);
+      if (P.wide[k]) ((int64_t*)P.val[k])[q] = bits;
+      else ((int32_t*)P.val[k])[q] = (int32_t)bits;
     }
-    if (ok) lb |= 1u << s;
+    if (P.nul) P.nul[q] = nm;
+    uint32_t lb = 0;
+    for (int s = 0; s < dd->n_states; ++s) {
+      if (!((local_mask >> s) & 1u)) continue;
+      const sg_state_desc& x = dd->states[s];
+      bool ok;
+      if (x.prog_len <= 0) ok = true;
+      else if (!carried && a.lbits[s]) ok = mask_bit(a.lbits[s], (uint64_t)r) != 0;
+      else {
+        RowReader rd{&cols, dd->ret_col, r};
+        ok = sg_eval(dd->code + x.prog_off, x.prog_len, rd);
+      }
+      if (ok) lb |= 1u << s;
+    }
+    P.lb[q] = lb;
+    flag[q] = (lb >> start) & 1u;
   }
-  P.lb[q] = lb;
-  flag[q] = (lb >> start) & 1u;
 }
 
 __global__ void k_pp_compact(int64_t m, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
@@ -569,10 +574,11 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
             maxoff = off > maxoff ? off : maxoff;
             uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);   // compact: positions (k_em_out)
             em32[0] = (uint32_t)q;
-            em32[1] = k;
-            em32[2] = (1u << 24) | (uint32_t)em;
-            em32[3] = (uint32_t)L.pts_pos;
-            for (int s = 0; s < dd->n_select; ++s) em32[4 + s] = (uint32_t)L.get_event(dd->sel_state[s], dd->sel_index[s]);
+            em32[1] = (uint32_t)c;
+            em32[2] = k;
+            em32[3] = (1u << 24) | (uint32_t)em;
+            em32[4] = (uint32_t)L.pts_pos;
+            for (int s = 0; s < dd->n_select; ++s) em32[5 + s] = (uint32_t)L.get_event(dd->sel_state[s], dd->sel_index[s]);
           }
         }
         ++q;
@@ -839,12 +845,13 @@ struct SqEmit {   // match writer of the emitting pass
     uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);
     const int64_t pp = mm.dec(mm.M->P[p].pts);
     em32[0] = (uint32_t)(mm.src.base + mm.cur);
-    em32[1] = key;
-    em32[2] = (1u << 24) | (uint32_t)grp;
-    em32[3] = (uint32_t)(pp >= 0 ? mm.src.base + pp : -1);
+    em32[1] = (uint32_t)(r + a->nc);
+    em32[2] = key;
+    em32[3] = (1u << 24) | (uint32_t)grp;
+    em32[4] = (uint32_t)(pp >= 0 ? mm.src.base + pp : -1);
     for (int s = 0; s < dd->n_select; ++s) {
       const int64_t ev = mm.get_event(p, dd->sel_state[s], dd->sel_index[s]);
-      em32[4 + s] = (uint32_t)(ev < 0 ? -1 : mm.src.base + ev);
+      em32[5 + s] = (uint32_t)(ev < 0 ? -1 : mm.src.base + ev);
     }
   }
 };
@@ -997,22 +1004,35 @@ __global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char
   const uint32_t* e = (const uint32_t*)(em + (size_t)idx[i] * estride);
   char* rec = out + (size_t)i * ostride;
   int64_t* h64 = (int64_t*)rec;
-  const int64_t r = (int64_t)P.sid[e[0]] - P.nc;
+  // in delivery order the trigger rows ascend, so the trigger row's own columns are read nearly coalesced straight
+  // from the batch; other rows go through the key-sorted position (sid), and a row selected twice is read once
+  const uint32_t tq = e[0];
+  const int64_t r = (int64_t)e[1] - P.nc;
   h64[0] = (int64_t)(index ? index[r] : base_index + (uint64_t)r);
-  const int32_t tp = (int32_t)e[3];
-  h64[1] = tp >= 0 ? (P.ts ? P.ts[tp] : pp_lazy_ts(&P, tp)) : -1;
+  const int32_t tp = (int32_t)e[4];
+  h64[1] = tp < 0 ? -1 : P.ts ? P.ts[tp] : (uint32_t)tp == tq ? P.bts[r] : pp_lazy_ts(&P, tp);
   uint32_t* h32 = (uint32_t*)(rec + 16);
-  h32[0] = e[1];
-  h32[1] = e[2];
+  h32[0] = e[2];
+  h32[1] = e[3];
   uint32_t nm = 0;
   int64_t* vals = (int64_t*)(rec + 32);
-  for (int s = 0; s < dd->n_select; ++s) {
-    const int32_t q = (int32_t)e[4 + s];
+  const int ns = dd->n_select;
+  int32_t pq = -1;
+  int prs = -1;
+  int64_t pv = 0;
+  for (int s = 0; s < ns; ++s) {
+    const int32_t q = (int32_t)e[5 + s];
     const int rs = dd->sel_ret[s];
     if (q < 0 || (P.nul && ((P.nul[q] >> rs) & 1u))) { nm |= 1u << s; vals[s] = 0; continue; }
-    const int64_t bits = P.val[rs] ? (P.wide[rs] ? ((const int64_t*)P.val[rs])[q] : (int64_t)((const int32_t*)P.val[rs])[q])
-                                   : pp_lazy_bits(&P, q, rs);
-    vals[s] = sg_val_bits(sg_val_from_bits(bits, dd->ret_type[rs], 0));
+    if (q == pq && rs == prs) { vals[s] = pv; continue; }   // e.g. e2[0] and e2[last] of a one-event count
+    int64_t bits;
+    if ((uint32_t)q == tq && !P.val[rs]) bits = P.wide[rs] ? ((const int64_t*)P.bcol[rs])[r] : (int64_t)((const int32_t*)P.bcol[rs])[r];
+    else if (P.val[rs]) bits = P.wide[rs] ? ((const int64_t*)P.val[rs])[q] : (int64_t)((const int32_t*)P.val[rs])[q];
+    else bits = pp_lazy_bits(&P, q, rs);
+    pv = sg_val_bits(sg_val_from_bits(bits, dd->ret_type[rs], 0));
+    pq = q;
+    prs = rs;
+    vals[s] = pv;
   }
   h32[2] = nm;
   h32[3] = 0;
@@ -1059,7 +1079,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   o.count = o.reserved + 1;
   o.fail = (int32_t*)(o.reserved + 2);
   o.cap = cap;
-  o.rstride = 16 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
+  o.rstride = 20 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
   int rb = 1;
   while ((1ll << rb) < n + 1) ++rb;
   const int k1_bits = std::min(64, rb + 16);
@@ -1242,6 +1262,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   while ((1ull << end_bit) <= (uint64_t)kb) ++end_bit;
   const uint32_t sentinel = kb;
   const dim3 blk(256), grd((unsigned)((m + 255) / 256));
+  const dim3 grs((unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 4096)));
   uint32_t* keys = (uint32_t*)h->ws.get("pp_keys", 4 * m, st);
   uint32_t* skeys = (uint32_t*)h->ws.get("pp_skeys", 4 * m, st);
   uint32_t* sids = (uint32_t*)h->ws.get("pp_sids", 4 * m, st);
@@ -1320,7 +1341,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     PpRec* recs = (PpRec*)h->ws.get("pp_recs", sizeof(PpRec) * m, st);
     PpRec* srecs = (PpRec*)h->ws.get("pp_srecs", sizeof(PpRec) * m, st);
     h->kbeg("route");
-    hipLaunchKernelGGL(k_pp_rec, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ra, keys, recs, err);
+    hipLaunchKernelGGL(k_pp_rec, grs, blk, 0, st, a, bv.cols, cc, h->ddesc, ra, keys, recs, err);
     HIPCHK(hipGetLastError());
     h->kend();
     h->kbeg("key_sort");
@@ -1344,7 +1365,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
         for (int k = 0; k < d.n_ret; ++k) if (ps->hot[k] < 0) P.val[k] = nullptr;
       }
       h->kbeg("pack");
-      hipLaunchKernelGGL(k_pp_unpack, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ra, skeys, srecs, P, sids, flag);
+      hipLaunchKernelGGL(k_pp_unpack, grs, blk, 0, st, a, bv.cols, cc, h->ddesc, ra, skeys, srecs, P, sids, flag);
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
       HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
@@ -1374,7 +1395,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     HIPCHK(hipGetLastError());
     h->kend();
     h->kbeg("pack");
-    if (m) hipLaunchKernelGGL(k_pp_pack, grd, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->rule.local_mask, ps->rule.start,
+    if (m) hipLaunchKernelGGL(k_pp_pack, grs, blk, 0, st, a, bv.cols, cc, h->ddesc, ps->rule.local_mask, ps->rule.start,
                               skeys, sids, sentinel, P, flag);
     HIPCHK(hipGetLastError());
     h->kend();
@@ -1420,7 +1441,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   o.maxoff = (uint32_t*)(o.count + 1);
   o.jp = (uint32_t*)h->ws.get("pp_jp", 4 * cap, st);
   o.fail = err + 1;
-  o.rstride = 16 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
+  o.rstride = 20 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
   int rb = 1;
   while ((1ll << rb) < n + 1) ++rb;
   const int k1_bits = std::min(64, rb + 8);
