@@ -17,6 +17,9 @@ Two rates, both in the one JSON line rank 0 prints:
               pinned host memory, overlapped) -> every match tuple in host memory.  PCIe-bound; never `value`.
 Multi-GPU (one process per GPU, torchrun): weak scaling, rank r owns the disjoint key range [r*K, (r+1)*K) with
 its own stream; no data-path collective (keys never interact); times are max over ranks.
+  c5_stream   (BASELINE configs[4], beside `value`): ONE 1B-event, 1M-key C5 stream split by key hash across the
+              N ranks (strong scaling: the same stream at every N), each rank pushing its share in 100M-row batches
+              with state carried between them; value = 1e9 events / max-over-ranks time.
 
 roofline: the dominant kernel of the `value` step (largest HIP-event time, recorded on the launch stream by the
 engine, sg_timing.kernel_ms) against the §8d algorithmic bytes of the whole path (16.125 B/event + 36 B/match),
@@ -267,6 +270,84 @@ def whole_node(cfg, rank, n, keys, rate, steps, dev, threads, parts=4):
             "router_threads": threads, "parts": parts}
 
 
+def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
+    """BASELINE configs[4] as it is worded: ONE 1B-event, 1M-key C5 stream sharded by key hash across the node's
+    ranks (strong scaling: the stream is the same at every N).  Every rank generates the global stream in HBM chunk
+    by chunk and keeps the rows of the keys it owns (siddhi_amd/router.py shard_of_torch: mix64(key) mod N, the host
+    router's assignment, computed on the GPU), with its own dense key ids and the rows' global event indices; it then
+    pushes its share as consecutive batches of `push_rows` (state carried between pushes).  Time = max over ranks;
+    value = the whole stream's events / that time.  Merging the ranks' match streams (router.merge) is host work
+    outside this number; tests/test_multigpu.py checks the merged output against the oracle."""
+    from siddhi_amd import router
+    _, n_total, keys, rate = synth.CONFIGS["C5"]
+    total = total or n_total
+    shard, local, counts = router.shard_tables_torch(keys, ws, dev)
+    parts = {"ts": [], "key": [], "id": [], "price": [], "gidx": []}
+    gen = 100_000_000
+    for start in range(0, total, gen):
+        g = synth.generate_torch("C5", start, min(gen, total - start), dev, keys=keys, rate=rate)
+        gk = g["key"].long()
+        sel = torch.nonzero(shard[gk] == rank).squeeze(1)
+        parts["ts"].append(g["ts"][sel])
+        parts["key"].append(local[gk[sel]])
+        parts["id"].append(g["id"][sel])
+        parts["price"].append(g["price"][sel])
+        parts["gidx"].append(sel + start)
+        del g, gk, sel
+    cat = {k: torch.cat(v) for k, v in parts.items()}
+    del parts
+    n = cat["ts"].numel()
+    h, nfa = make_handle("C5", no_carry=0)
+    keep, batches = [], []
+    for lo in range(0, n, push_rows):
+        hi = min(n, lo + push_rows)
+        cp = [cat["id"].data_ptr() + 8 * lo, cat["key"].data_ptr() + 4 * lo, cat["price"].data_ptr() + 4 * lo]
+        batches.append(N.make_batch(hi - lo, int(cat["gidx"][lo].item()), cat["ts"].data_ptr() + 8 * lo, 0,
+                                    cat["key"].data_ptr() + 4 * lo, cp, [0, 0, 0], 1, counts[rank], keep,
+                                    index=cat["gidx"].data_ptr() + 8 * lo))
+    stream = torch.cuda.current_stream()
+    h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
+
+    def step():
+        h.reset()
+        m = 0
+        for b in batches:
+            h.push(b)
+            m += h.timing().matches
+        return m
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        matches = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tot = torch.tensor([el, float(matches), float(n)], device=dev, dtype=torch.float64)
+    if ws > 1:
+        import torch.distributed as dist
+        mx = tot[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        tot[0] = mx[0]
+    h.close()
+    del cat, batches
+    torch.cuda.empty_cache()
+    el, matches, rows = (float(x) for x in tot.tolist())
+    ms = 1000.0 * el / steps
+    return {"workload": "C5 (BASELINE configs[4]): " + synth.QUERIES["C5"], "events": total, "keys": keys,
+            "rate_events_per_ms": rate, "n_gpus": ws, "scaling": "strong", "steps": steps,
+            "ms_per_step": round(ms, 3), "value": round(total / (ms * 1e-3), 1), "unit": "events/s",
+            "matches": int(matches), "rows_routed": int(rows), "push_rows": push_rows,
+            "sharding": "mix64(key) mod N on the GPU (router.shard_of_torch), per-rank dense ids, global indices kept",
+            "data": "synthetic, generated in HBM; inputs resident before the timed region"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -280,6 +361,10 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16, help="processes for the key-sharded CPU baseline")
     ap.add_argument("--whole-node-steps", type=int, default=3, help="steps of the §8d whole-node rate (0: skip)")
     ap.add_argument("--router-threads", type=int, default=16)
+    ap.add_argument("--c5-stream-steps", type=int, default=2,
+                    help="steps of the 1B-event C5 stream sharded by key hash across the ranks (0: skip)")
+    ap.add_argument("--c5-events", type=int, default=0, help="events of the C5 stream (default 1e9)")
+    ap.add_argument("--c5-push-rows", type=int, default=100_000_000)
     ap.add_argument("--pmc", default=DEFAULT_PMC, help="rocprofv3 PMC summary of this command (profiles/collect_r02.sh)")
     args = ap.parse_args()
 
@@ -360,6 +445,12 @@ def main():
             wn["unit"] = "events/s"
             wn["definition"] = ("SURVEY.md §8d: raw host columns -> native router (first-seen dense keys) -> pinned "
                                 "chunked H2D -> kernels -> GPU-transposed SoA match columns in pinned host memory")
+    c5 = None
+    if args.c5_stream_steps > 0:
+        try:
+            c5 = c5_stream(rank, ws, dev, args.c5_stream_steps, 1, args.c5_events, args.c5_push_rows)
+        except Exception as e:   # report, never fake
+            c5 = {"error": str(e)}
     if rank != 0:
         return
     ms_step = elapsed * 1000.0 / args.steps
@@ -423,6 +514,7 @@ def main():
                    "keys_per_gpu": keys, "rate_events_per_ms": rate, "matches_per_gpu_per_step": int(matches),
                    "spilled_units": int(spilled), "parallelism": f"key-sharded x{ws} (no collective)"},
         "whole_node": wn,
+        "c5_stream": c5,
         "roofline": roof,
         "cpu_baseline": cpu,
         "source_hash": source_hash(cfg),

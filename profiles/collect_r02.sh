@@ -8,7 +8,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=$1; cfg=$2; shift 2
 mkdir -p "$out"
-args="--config $cfg --steps 2 --warmup 1 --no-cpu --whole-node-steps 0 $*"
+args="--config $cfg --steps 2 --warmup 1 --no-cpu --whole-node-steps 0 --c5-stream-steps 0 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
   python3 -u bench.py $args > "$out/trace.log" 2>&1 || { echo "trace failed"; tail -5 "$out/trace.log"; exit 1; }
 i=0

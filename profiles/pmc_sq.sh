@@ -13,8 +13,8 @@ for g in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
          "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $g --kernel-include-regex "$rx" --output-format csv -d "$out/pass$i" -o run -- \
-    python3 -u bench.py --steps 1 --warmup 1 --no-cpu "$@" > "$out/pass$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$out/pass$i.log"; exit 1; }
+    python3 -u bench.py --steps 1 --warmup 1 --no-cpu --c5-stream-steps 0 "$@" > "$out/pass$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$out/pass$i.log"; exit 1; }
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
-  python3 -u bench.py --steps 2 --warmup 1 --no-cpu "$@" > "$out/trace.log" 2>&1 || { echo "trace failed"; exit 1; }
+  python3 -u bench.py --steps 2 --warmup 1 --no-cpu --c5-stream-steps 0 "$@" > "$out/trace.log" 2>&1 || { echo "trace failed"; exit 1; }
 echo done

@@ -999,10 +999,14 @@ __global__ void k_sq_drop(int64_t n, SqOut o) {
 __global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char* __restrict__ em, int32_t estride,
                          char* __restrict__ out, int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
                          const uint64_t* __restrict__ index, uint64_t base_index) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  // records are assembled in LDS and leave the block as one contiguous copy
+  extern __shared__ __align__(16) char em_lds[];
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + threadIdx.x;
+  const int64_t nb = n - i0 < (int64_t)blockDim.x ? n - i0 : (int64_t)blockDim.x;
+  if (i < n) {
   const uint32_t* e = (const uint32_t*)(em + (size_t)idx[i] * estride);
-  char* rec = out + (size_t)i * ostride;
+  char* rec = em_lds + (size_t)threadIdx.x * ostride;
   int64_t* h64 = (int64_t*)rec;
   // in delivery order the trigger rows ascend, so the trigger row's own columns are read nearly coalesced straight
   // from the batch; other rows go through the key-sorted position (sid), and a row selected twice is read once
@@ -1036,6 +1040,12 @@ __global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char
   }
   h32[2] = nm;
   h32[3] = 0;
+  }
+  __syncthreads();
+  const uint2* src = (const uint2*)em_lds;   // records are 8-byte multiples, the output only 8-byte aligned
+  uint2* dst = (uint2*)(out + (size_t)i0 * ostride);
+  const int64_t words = nb * ostride / 8;
+  for (int64_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = src[w];
 }
 
 // carry for sequence lanes: the last H rows of every key
@@ -1171,7 +1181,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
     void* tmp = h->ws.get("sq_sorttmp", tb, st);
     HIPCHK(rocprim::radix_sort_pairs(tmp, tb, o.k1, kb2, ia, ib, (size_t)R, 0, k1_bits, st));
     char* out = h->out.reserve(total, nsel, st);
-    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total, ib, o.rec, o.rstride,
+    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((total + 255) / 256)), blk, 256 * rstride, st, total, ib, o.rec, o.rstride,
                        out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());
     h->kend();
@@ -1501,7 +1511,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     }
     const int64_t M = (int64_t)total;
     char* out = h->out.reserve(M, nsel, st);
-    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, ia, o.rec, o.rstride,
+    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((M + 255) / 256)), blk, 256 * rstride, st, M, ia, o.rec, o.rstride,
                        out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());
     h->kend();

@@ -89,3 +89,44 @@ def merge(parts):
     phase = (cat.group >> np.uint32(24)).astype(np.uint64)
     order = np.lexsort((np.arange(len(cat)), cat.key.astype(np.int64), phase, cat.trigger))
     return Outputs(*[getattr(cat, f)[order] for f in ("trigger", "ts", "key", "group", "vals", "vnull")])
+
+
+# ---- on-device sharding (bench.py's C5 stream mode): the same mix64 assignment computed in HBM with torch int64
+# arithmetic (wrapping multiply, logical shifts by masking), so a 1B-event stream is split without crossing PCIe.
+def _lsr(z, k):
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def _s64(u):
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def mix64_torch(k):
+    z = k.to(dtype=__import__("torch").int64) + _s64(0x9E3779B97F4A7C15)
+    z = (z ^ _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _lsr(z, 27)) * _s64(0x94D049BB133111EB)
+    return z ^ _lsr(z, 31)
+
+
+def shard_of_torch(keys, world: int):
+    """shard_of on a torch tensor of dense key ids (unsigned 64-bit modulo of the int64 bit pattern)."""
+    import torch
+    z = mix64_torch(torch.clamp(keys.to(torch.int64), min=0))
+    hi, lo = _lsr(z, 32), z & 0xFFFFFFFF
+    return (((hi % world) * ((1 << 32) % world) + lo % world) % world).to(torch.int32)
+
+
+def shard_tables_torch(n_keys: int, world: int, device):
+    """Per key id 0..n_keys-1: owning rank and its dense id inside that rank (ascending key order), plus the number
+    of keys each rank owns."""
+    import torch
+    k = torch.arange(n_keys, device=device)
+    s = shard_of_torch(k, world)
+    local = torch.empty(n_keys, dtype=torch.int32, device=device)
+    counts = []
+    for r in range(world):
+        m = s == r
+        c = int(m.sum().item())
+        local[m] = torch.arange(c, dtype=torch.int32, device=device)
+        counts.append(c)
+    return s, local, counts

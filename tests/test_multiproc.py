@@ -95,3 +95,17 @@ def test_shards_are_disjoint_and_cover():
     assert (total == 1).all()
     frac = [o.mean() for o in owners]
     assert max(frac) - min(frac) < 0.02
+
+
+def test_device_shard_matches_host_router():
+    """bench.py's C5 stream mode shards on the GPU with router.shard_of_torch: same owner as the host function, and
+    the per-rank dense ids cover 0..count-1 exactly once."""
+    import torch
+    from siddhi_amd import router
+    k = np.arange(200_000, dtype=np.int32)
+    for world in (1, 2, 3, 8):
+        assert (router.shard_of(k, world) == router.shard_of_torch(torch.from_numpy(k), world).numpy()).all()
+        s, local, counts = router.shard_tables_torch(5_000, world, "cpu")
+        assert sum(counts) == 5_000
+        for r in range(world):
+            assert sorted(local[s == r].tolist()) == list(range(counts[r]))
