@@ -281,21 +281,7 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
     from siddhi_amd import router
     _, n_total, keys, rate = synth.CONFIGS["C5"]
     total = total or n_total
-    shard, local, counts = router.shard_tables_torch(keys, ws, dev)
-    parts = {"ts": [], "key": [], "id": [], "price": [], "gidx": []}
-    gen = 100_000_000
-    for start in range(0, total, gen):
-        g = synth.generate_torch("C5", start, min(gen, total - start), dev, keys=keys, rate=rate)
-        gk = g["key"].long()
-        sel = torch.nonzero(shard[gk] == rank).squeeze(1)
-        parts["ts"].append(g["ts"][sel])
-        parts["key"].append(local[gk[sel]])
-        parts["id"].append(g["id"][sel])
-        parts["price"].append(g["price"][sel])
-        parts["gidx"].append(sel + start)
-        del g, gk, sel
-    cat = {k: torch.cat(v) for k, v in parts.items()}
-    del parts
+    cat, key_bound, _ = router.shard_stream_torch("C5", rank, ws, total, keys, rate, dev)
     n = cat["ts"].numel()
     h, nfa = make_handle("C5", no_carry=0)
     keep, batches = [], []
@@ -303,7 +289,7 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
         hi = min(n, lo + push_rows)
         cp = [cat["id"].data_ptr() + 8 * lo, cat["key"].data_ptr() + 4 * lo, cat["price"].data_ptr() + 4 * lo]
         batches.append(N.make_batch(hi - lo, int(cat["gidx"][lo].item()), cat["ts"].data_ptr() + 8 * lo, 0,
-                                    cat["key"].data_ptr() + 4 * lo, cp, [0, 0, 0], 1, counts[rank], keep,
+                                    cat["key"].data_ptr() + 4 * lo, cp, [0, 0, 0], 1, key_bound, keep,
                                     index=cat["gidx"].data_ptr() + 8 * lo))
     stream = torch.cuda.current_stream()
     h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))

@@ -130,3 +130,26 @@ def shard_tables_torch(n_keys: int, world: int, device):
         local[m] = torch.arange(c, dtype=torch.int32, device=device)
         counts.append(c)
     return s, local, counts
+
+
+def shard_stream_torch(cfg: str, rank: int, world: int, total: int, keys: int, rate: int, device, gen=100_000_000):
+    """This rank's rows of the synthetic stream `cfg` (siddhi_amd/synth.py, generated in HBM chunk by chunk): the rows
+    whose key mix64-hashes to `rank`, with per-rank dense key ids (ascending key order), their global event indices,
+    and the local -> global key table.  Returns (columns dict: ts, key, id, price, gidx), key_bound, l2g."""
+    import torch
+    from . import synth
+    shard, local, counts = shard_tables_torch(keys, world, device)
+    parts = {"ts": [], "key": [], "id": [], "price": [], "gidx": []}
+    for start in range(0, total, gen):
+        g = synth.generate_torch(cfg, start, min(gen, total - start), device, keys=keys, rate=rate)
+        gk = g["key"].long()
+        sel = torch.nonzero(shard[gk] == rank).squeeze(1)
+        parts["ts"].append(g["ts"][sel])
+        parts["key"].append(local[gk[sel]])
+        parts["id"].append(g["id"][sel])
+        parts["price"].append(g["price"][sel])
+        parts["gidx"].append(sel + start)
+        del g, gk, sel
+    cols = {k: torch.cat(v) for k, v in parts.items()}
+    l2g = torch.nonzero(shard == rank).squeeze(1).to(torch.int32)   # ascending key order = local id order
+    return cols, counts[rank], l2g

@@ -88,3 +88,57 @@ def test_two_ranks_router_merge_on_gpu(tmp_path, cfg, n, keys, rate):
     want = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
     assert len(want) > 0
     assert_same(merged, want)
+
+
+@pytest.mark.timeout(300)
+def test_device_sharded_stream_matches_oracle():
+    """bench.py's c5_stream data path at a small size: the stream generated in HBM, split on the GPU by mix64(key)
+    mod 3 (router.shard_stream_torch: per-rank dense ids, global event indices), each rank's share pushed as several
+    batches with state carried, the three ranks (run one after another on cuda:0) merged -- equal to the oracle."""
+    import torch
+    from oracle import OracleEngine
+    from parity_util import assert_same, context, dense_first_seen, run_engine
+    from siddhi_amd import _native as N
+    from siddhi_amd import lowering as L
+    from siddhi_amd import router, synth
+    from siddhi_amd.runtime import Batch, Outputs
+    cfg, total, keys, rate, world, push = "C5", 400_000, 5_000, 1_000, 3, 70_000
+    dev = torch.device("cuda", 0)
+    nfa = L.lower(context(synth.QUERIES[cfg]))
+    nsel = len(nfa.select)
+    g = synth.generate_torch(cfg, 0, total, dev, keys=keys, rate=rate)
+    raw = g["key"].to(torch.int32).cpu().numpy()
+    dense = dense_first_seen(raw)
+    to_dense = np.zeros(keys, np.int32)
+    to_dense[raw] = dense
+    parts = []
+    for rank in range(world):
+        cols, kb, l2g = router.shard_stream_torch(cfg, rank, world, total, keys, rate, dev, gen=150_000)
+        n = cols["ts"].numel()
+        h = N.Handle(N.build_desc(nfa), device=0, options=N.sg_options())
+        keep, outs = [], []
+        for lo in range(0, n, push):
+            hi = min(n, lo + push)
+            cp = [cols["id"].data_ptr() + 8 * lo, cols["key"].data_ptr() + 4 * lo, cols["price"].data_ptr() + 4 * lo]
+            b = N.make_batch(hi - lo, int(cols["gidx"][lo].item()), cols["ts"].data_ptr() + 8 * lo, 0,
+                             cols["key"].data_ptr() + 4 * lo, cp, [0, 0, 0], 1, kb, keep,
+                             index=cols["gidx"].data_ptr() + 8 * lo)
+            h.push(b)
+            tr, ts, ky, gr, vals, vn = h.poll(nsel)
+            vnull = np.zeros((len(tr), nsel), np.uint8)
+            for k in range(nsel):
+                vnull[:, k] = (vn >> np.uint32(k)) & np.uint32(1)
+            outs.append(Outputs(tr, ts, ky, gr, vals, vnull))
+        h.close()
+        torch.cuda.synchronize()
+        out = Outputs(*[np.concatenate([getattr(o, f) for o in outs]) for f in
+                        ("trigger", "ts", "key", "group", "vals", "vnull")])
+        l2g_h = l2g.cpu().numpy()
+        out.key = to_dense[l2g_h[out.key]].astype(out.key.dtype)
+        parts.append(out)
+    got = router.merge(parts)
+    b = Batch(total, 0, g["ts"].cpu().numpy(), np.zeros(total, np.int32), dense,
+              [g["id"].cpu().numpy(), raw, g["price"].cpu().numpy()], [None] * 3)
+    want = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
+    assert len(want) > 1000
+    assert_same(got, want)
