@@ -58,7 +58,9 @@ struct PartialState {
   SgPpRule* drule = nullptr;
   SgSeqRule srule;
   SgSeqRule* dsrule = nullptr;
-  SeqState* kst = nullptr;      // sequence lanes: per-key machine state (zero = no runtime yet)
+  void* kst = nullptr;          // sequence lanes: per-key machine state SeqStateT<G> (zero = no runtime yet)
+  int sq_small = 0;             // the query fits seq.h's small state geometry (SqSmall)
+  size_t sq_bytes = sizeof(SeqState);
   int64_t kst_keys = 0;
   int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
   int64_t last_reruns = 0;      // sequence units rerun from their predecessor's end state in the last push
@@ -111,6 +113,8 @@ PartialState* sg_partial_new(const sg_nfa_desc& d) {
     ps->rule.local_mask = sr.local_mask;
     ps->rule.start = sr.start;
     ps->rule.recv = sr.recv;
+    ps->sq_small = sg_seq_small(sr, d) ? 1 : 0;
+    ps->sq_bytes = ps->sq_small ? sizeof(SeqStateT<SqSmall>) : sizeof(SeqState);
     if (hipMalloc(&ps->dsrule, sizeof(SgSeqRule)) != hipSuccess) { delete ps; throw SgError(SG_EHIP, "hipMalloc rule"); }
     hipMemcpy(ps->dsrule, &ps->srule, sizeof(SgSeqRule), hipMemcpyHostToDevice);
   }
@@ -169,7 +173,7 @@ void sg_partial_reset(PartialState* ps) {
   ps->rows[0].n = ps->rows[1].n = 0;
   ps->active = 1;
   ps->seq_pushes = 0;
-  if (ps->kst) hipMemset(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys);
+  if (ps->kst) hipMemset(ps->kst, 0, ps->sq_bytes * (size_t)ps->kst_keys);
 }
 
 int sg_partial_active(const PartialState* ps) { return ps && ps->active; }
@@ -787,9 +791,9 @@ struct SqPlan {
   const uint32_t* umap;       // unit -> key
   int64_t R, W;
   int64_t nunits;
-  SeqState* kst;              // per key (carried)
-  SeqState* ust;              // per unit: start state
-  SeqState* uen;              // per unit: end state
+  void* kst;                  // per key (carried), SeqStateT<G>
+  void* ust;                  // per unit: start state
+  void* uen;                  // per unit: end state
   unsigned long long* reruns;
 };
 
@@ -813,14 +817,17 @@ __global__ void k_sq_umap(int64_t kb, const uint32_t* __restrict__ uoff, uint32_
   for (uint32_t u = uoff[k]; u < uoff[k + 1]; ++u) umap[u] = (uint32_t)k;
 }
 
-__device__ __forceinline__ void sq_copy(SeqState* __restrict__ dst, const SeqState* __restrict__ src) {
+template <class T>
+__device__ __forceinline__ void sq_copy(T* __restrict__ dst, const T* __restrict__ src) {
+  static_assert(sizeof(T) % 4 == 0, "state words");
   const uint32_t* s = (const uint32_t*)src;
   uint32_t* d = (uint32_t*)dst;
-  for (uint32_t i = 0; i < sizeof(SeqState) / 4; ++i) d[i] = s[i];
+  for (uint32_t i = 0; i < sizeof(T) / 4; ++i) d[i] = s[i];
 }
-__device__ __forceinline__ void sq_zero(SeqState* dst) {
+template <class T>
+__device__ __forceinline__ void sq_zero(T* dst) {
   uint32_t* d = (uint32_t*)dst;
-  for (uint32_t i = 0; i < sizeof(SeqState) / 4; ++i) d[i] = 0;
+  for (uint32_t i = 0; i < sizeof(T) / 4; ++i) d[i] = 0;
 }
 
 struct SqEmit {   // match writer of the emitting pass
@@ -830,7 +837,8 @@ struct SqEmit {   // match writer of the emitting pass
   SqOut o;
   int64_t slot, slot_end, r;
   uint32_t key, seq, nemit, unit;
-  __device__ void operator()(SeqMachine<SeqSrcD>& mm, int p, int grp) {
+  template <class Mach>
+  __device__ void operator()(Mach& mm, int p, int grp) {
     if (slot == slot_end) {
       slot = (int64_t)atomicAdd(o.reserved, (unsigned long long)SQ_CHUNK);
       slot_end = slot + SQ_CHUNK;
@@ -856,12 +864,13 @@ struct SqEmit {   // match writer of the emitting pass
   }
 };
 struct SqNoEmit {
-  __device__ void operator()(SeqMachine<SeqSrcD>&, int, int) {}
+  template <class Mach>
+  __device__ void operator()(Mach&, int, int) {}
 };
 
 // rows [q0, q1) of a key whose positions start at b0; emit != null: the emitting pass
-template <class E>
-__device__ __forceinline__ void sq_run(SeqMachine<SeqSrcD>& m, int64_t b0, int64_t q0, int64_t q1, E& emit,
+template <class E, class Mach>
+__device__ __forceinline__ void sq_run(Mach& m, int64_t b0, int64_t q0, int64_t q1, E& emit,
                                        const uint32_t* __restrict__ sid, int64_t nc, int64_t* rcur, uint32_t* seq) {
   m.begin();
   for (int64_t q = q0; q < q1 && !m.failed; ++q) {
@@ -878,7 +887,7 @@ __device__ __forceinline__ void sq_run(SeqMachine<SeqSrcD>& m, int64_t b0, int64
   const DevDesc& dl = *ddg;                                                                                    \
   __shared__ SgSeqRule rl;                                                                                     \
   __shared__ PpPacked pl;                                                                                      \
-  __shared__ SeqState lanes[SQ_BLOCK];                                                                         \
+  __shared__ SeqStateT<G> lanes[SQ_BLOCK];                                                                         \
   {                                                                                                            \
     const uint32_t* s3 = (const uint32_t*)&P;                                                                  \
     for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];    \
@@ -888,6 +897,7 @@ __device__ __forceinline__ void sq_run(SeqMachine<SeqSrcD>& m, int64_t b0, int64
   }
 
 // pass A: every unit from its (guessed) start state, emitting; its start and end states are kept for the check
+template <class G>
 __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                       const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
                                                       SqPlan pl_, SqOut o) {
@@ -898,8 +908,8 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
   const int64_t c = u - pl_.uoff[k];
   const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
   const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
-  SeqState& M = lanes[threadIdx.x];
-  SeqMachine<SeqSrcD> m;
+  SeqStateT<G>& M = lanes[threadIdx.x];
+  SeqMachine<SeqSrcD, G> m;
   m.d = &dl;
   m.ru = &rl;
   m.src = SeqSrcD{&pl, b0};
@@ -907,13 +917,13 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
   m.cur = 0;
   SqNoEmit ne;
   if (c == 0) {
-    sq_copy(&M, pl_.kst + k);
+    sq_copy(&M, (const SeqStateT<G>*)pl_.kst + k);
   } else {
     sq_zero(&M);
     const int64_t w0 = s0 - pl_.W > b0 ? s0 - pl_.W : b0;
     sq_run(m, b0, w0, s0, ne, sid, a.nc, nullptr, nullptr);
   }
-  sq_copy(pl_.ust + u, &M);
+  sq_copy((SeqStateT<G>*)pl_.ust + u, &M);
   SqEmit em;
   em.a = &a;
   em.dd = &dl;
@@ -929,11 +939,12 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
   for (int64_t q = em.slot; q < em.slot_end && q < o.cap; ++q) o.k1[q] = o.k1_none;
   if (em.nemit) atomicAdd(o.count, (unsigned long long)em.nemit);
   if (m.failed) atomicCAS(o.fail, 0, m.failed);
-  sq_copy(pl_.uen + u, &M);
+  sq_copy((SeqStateT<G>*)pl_.uen + u, &M);
 }
 
 // pass B: per key, in unit order, a unit whose guessed start differs from its predecessor's end is rerun from that end
 // (emitting again; its speculative matches are voided); then the key's final state is kept for the next push
+template <class G>
 __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                      const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
                                                      SqPlan pl_, int64_t kb, SqOut o) {
@@ -943,8 +954,8 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const
   const uint32_t u0 = pl_.uoff[k], u1 = pl_.uoff[k + 1];
   if (u1 == u0) return;
   const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
-  SeqState& M = lanes[threadIdx.x];
-  SeqMachine<SeqSrcD> m;
+  SeqStateT<G>& M = lanes[threadIdx.x];
+  SeqMachine<SeqSrcD, G> m;
   m.d = &dl;
   m.ru = &rl;
   m.src = SeqSrcD{&pl, b0};
@@ -962,24 +973,24 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const
   em.r = 0;
   uint32_t reruns = 0;
   for (uint32_t u = u0 + 1; u < u1; ++u) {
-    if (sg_seq_equiv(pl_.ust[u], pl_.uen[u - 1], dl, rl)) continue;
+    if (sg_seq_equiv(((const SeqStateT<G>*)pl_.ust)[u], ((const SeqStateT<G>*)pl_.uen)[u - 1], dl, rl)) continue;
     ++reruns;
     o.rerun[u] = 1;
     em.unit = u | 0x80000000u;
     const int64_t c = u - u0;
     const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
-    sq_copy(&M, pl_.uen + (u - 1));
+    sq_copy(&M, (const SeqStateT<G>*)pl_.uen + (u - 1));
     sq_run(m, b0, s0, s1, em, sid, a.nc, &em.r, &em.seq);
     if (m.failed) { atomicCAS(o.fail, 0, m.failed); return; }
-    sq_copy(pl_.uen + u, &M);
+    sq_copy((SeqStateT<G>*)pl_.uen + u, &M);
   }
   for (int64_t q = em.slot; q < em.slot_end && q < o.cap; ++q) o.k1[q] = o.k1_none;
   if (em.nemit) atomicAdd(o.count, (unsigned long long)em.nemit);
   if (reruns) atomicAdd(pl_.reruns, (unsigned long long)reruns);
-  sq_copy(&M, pl_.uen + (u1 - 1));
+  sq_copy(&M, (const SeqStateT<G>*)pl_.uen + (u1 - 1));
   const int64_t nk = e0 - b0;
   m.rebase(nk - 1, nk > rl.horizon ? nk - rl.horizon : 0);
-  sq_copy(pl_.kst + k, &M);
+  sq_copy((SeqStateT<G>*)pl_.kst + k, &M);
 }
 
 // void the speculative matches of rerun units
@@ -1070,11 +1081,11 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   // per-key machine states (grown with the key bound; new keys start zeroed = no runtime yet)
   if ((int64_t)kb > ps->kst_keys) {
     const int64_t nk = std::max<int64_t>((int64_t)kb, ps->kst_keys * 3 / 2);
-    SeqState* ns = nullptr;
-    if (hipMalloc(&ns, sizeof(SeqState) * (size_t)nk) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
-    HIPCHK(hipMemsetAsync(ns, 0, sizeof(SeqState) * (size_t)nk, st));
+    void* ns = nullptr;
+    if (hipMalloc(&ns, ps->sq_bytes * (size_t)nk) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
+    HIPCHK(hipMemsetAsync(ns, 0, ps->sq_bytes * (size_t)nk, st));
     if (ps->kst) {
-      HIPCHK(hipMemcpyAsync(ns, ps->kst, sizeof(SeqState) * (size_t)ps->kst_keys, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(ns, ps->kst, ps->sq_bytes * (size_t)ps->kst_keys, hipMemcpyDeviceToDevice, st));
       HIPCHK(hipStreamSynchronize(st));
       hipFree(ps->kst);
     }
@@ -1125,8 +1136,8 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   pl_.umap = umap;
   pl_.nunits = U;
   pl_.kst = ps->kst;
-  pl_.ust = (SeqState*)h->ws.get("sq_ust", sizeof(SeqState) * ((size_t)U + 1), st);
-  pl_.uen = (SeqState*)h->ws.get("sq_uen", sizeof(SeqState) * ((size_t)U + 1), st);
+  pl_.ust = h->ws.get("sq_ust", ps->sq_bytes * ((size_t)U + 1), st);
+  pl_.uen = h->ws.get("sq_uen", ps->sq_bytes * ((size_t)U + 1), st);
   pl_.reruns = o.reserved + 3;
   h->kend();
   cap = n + (int64_t)SQ_CHUNK * ((int64_t)U + (int64_t)kb) + 65536;
@@ -1139,11 +1150,13 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   o.dropped = o.reserved + 4;
   HIPCHK(hipMemsetAsync(o.rerun, 0, 4 * ((size_t)U + 1), st));
   h->kbeg("sequence_lanes");
-  if (U) hipLaunchKernelGGL(k_sq_spec, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
+  if (U && ps->sq_small) hipLaunchKernelGGL(k_sq_spec<SqSmall>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
+  else if (U) hipLaunchKernelGGL(k_sq_spec<SqBig>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
   HIPCHK(hipGetLastError());
   h->kend();
   h->kbeg("sequence_fix");
-  if (U) hipLaunchKernelGGL(k_sq_fix, gq, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, (int64_t)kb, o);
+  if (U && ps->sq_small) hipLaunchKernelGGL(k_sq_fix<SqSmall>, gq, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, (int64_t)kb, o);
+  else if (U) hipLaunchKernelGGL(k_sq_fix<SqBig>, gq, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, (int64_t)kb, o);
   HIPCHK(hipGetLastError());
   h->kend();
   unsigned long long cnt[5] = {0, 0, 0, 0, 0};
@@ -1162,7 +1175,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   if (fail) {
     if (getenv("SG_DEBUG_SEQ")) fprintf(stderr, "sequence lanes failed: reason %d\n", fail);
     if (ps->seq_pushes == 0 && a.nc == 0) {   // nothing carried yet: the per-key machine can take the stream exactly
-      HIPCHK(hipMemsetAsync(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys, st));
+      HIPCHK(hipMemsetAsync(ps->kst, 0, ps->sq_bytes * (size_t)ps->kst_keys, st));
       return 0;
     }
     throw SgError(SG_ECAPACITY, "sequence machine capacity exceeded (reason " + std::to_string(fail) +
@@ -1192,7 +1205,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
     hipLaunchKernelGGL(k_seq_keep, grd, blk, 0, st, m, skeys, end, sentinel, (int64_t)ps->srule.horizon, keep);
     carry_rows(h, ps, bv, a, m, skeys, sids, keep);
   } else if (h->opt.no_carry) {
-    HIPCHK(hipMemsetAsync(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys, st));
+    HIPCHK(hipMemsetAsync(ps->kst, 0, ps->sq_bytes * (size_t)ps->kst_keys, st));
   }
   ps->seq_pushes++;
   h->mark(4);
@@ -1539,7 +1552,7 @@ void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
   if (ps->mode == 2) {   // sequence lanes: the per-key machine states as well (seq.h SeqState, positions over the rows)
     w.pod(ps->kst_keys);
     w.pod(ps->seq_pushes);
-    if (ps->kst_keys) w.dev(ps->kst, sizeof(SeqState) * (size_t)ps->kst_keys, h->stream);
+    if (ps->kst_keys) w.dev(ps->kst, ps->sq_bytes * (size_t)ps->kst_keys, h->stream);
   }
   w.pod(r.n);
   if (!r.n) return;
@@ -1563,11 +1576,11 @@ void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& rd) {
     if (keys > ps->kst_keys) {
       if (ps->kst) hipFree(ps->kst);
       ps->kst = nullptr;
-      if (hipMalloc(&ps->kst, sizeof(SeqState) * (size_t)keys) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
+      if (hipMalloc(&ps->kst, ps->sq_bytes * (size_t)keys) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
       ps->kst_keys = keys;
     }
-    if (ps->kst_keys) HIPCHK(hipMemset(ps->kst, 0, sizeof(SeqState) * (size_t)ps->kst_keys));
-    if (keys) rd.dev(ps->kst, sizeof(SeqState) * (size_t)keys, h->stream);
+    if (ps->kst_keys) HIPCHK(hipMemset(ps->kst, 0, ps->sq_bytes * (size_t)ps->kst_keys));
+    if (keys) rd.dev(ps->kst, ps->sq_bytes * (size_t)keys, h->stream);
     ps->seq_pushes = pushes;
   }
   const int64_t n = rd.pod<int64_t>();

@@ -93,30 +93,49 @@ SG_HD inline SgSeqRule sg_seq_rule(const sg_nfa_desc& d) {
   return r;
 }
 
-struct SeqPartial {
-  int16_t slot[PQ_MAX_S];         // stream / logical: row position or -1
-  int16_t chain[PQ_MAX_CHAIN];    // count chains (positions), inline: no two partials share one in this family
-  int8_t clen[PQ_MAX_S];
+// State geometry: S states, CH count-chain entries per partial.  A lane's state lives in LDS, so its size sets how
+// many lanes a CU holds; queries that fit the small geometry (C3's family: <= 4 states, <= 6 chain entries) run with
+// ~220-byte states instead of ~350 (sg_seq_small).
+template <int S_, int CH_>
+struct SqGeo {
+  static constexpr int S = S_;
+  static constexpr int CH = CH_;
+};
+using SqBig = SqGeo<PQ_MAX_S, PQ_MAX_CHAIN>;
+using SqSmall = SqGeo<4, 6>;
+
+template <class G>
+struct SeqPartialT {
+  int16_t slot[G::S];             // stream / logical: row position or -1
+  int16_t chain[G::CH];           // count chains (positions), inline: no two partials share one in this family
+  int8_t clen[G::S];
   int16_t pts;                    // position whose timestamp is the partial's (StateEvent.timestamp), -1: none
 };
-struct SeqState {
-  SeqPartial P[PQ_MAX_P];
-  int8_t list[PQ_MAX_S][2][PQ_MAX_L];
-  int8_t llen_[PQ_MAX_S][2];
+template <class G>
+struct SeqStateT {
+  SeqPartialT<G> P[PQ_MAX_P];
+  int8_t list[G::S][2][PQ_MAX_L];
+  int8_t llen_[G::S][2];
   uint32_t free_mask;   // pool entries free for allocation in this event
   uint32_t h_init;      // per-state processor flags (KeyMachine H_* words)
   uint32_t created;
   uint32_t fch, fret, fsuc;   // H_CHANGED / H_RETURNED / H_SUCCESS bits between runs (registers while running)
 };
+using SeqPartial = SeqPartialT<SqBig>;
+using SeqState = SeqStateT<SqBig>;
+
+SG_HD inline bool sg_seq_small(const SgSeqRule& r, const sg_nfa_desc& d) {
+  return r.ok && d.n_states <= SqSmall::S && r.chain <= SqSmall::CH;
+}
 
 // Src: int64_t ts(int64_t pos); SgVal read(int64_t pos, int ret_slot, int type); int lbit(int s, int64_t pos) (-1: VM)
 // Sink: void emit(int group, int64_t pts, ...) receives the machine itself (see SeqMachine::emit)
-template <class Src>
+template <class Src, class G = SqBig>
 struct SeqMachine {
   const sg_nfa_desc* d;
   const SgSeqRule* ru;
   Src src;
-  SeqState* M;
+  SeqStateT<G>* M;
   int64_t cur;            // position of the current row
   int failed;
   uint32_t f_changed, f_returned, f_success;
@@ -139,7 +158,7 @@ struct SeqMachine {
   SG_HD void reset_runtime() {
     M->created = 0;
     M->h_init = 0;
-    for (int s = 0; s < PQ_MAX_S; ++s) { M->llen_[s][0] = 0; M->llen_[s][1] = 0; }
+    for (int s = 0; s < G::S; ++s) { M->llen_[s][0] = 0; M->llen_[s][1] = 0; }
     M->free_mask = (1u << PQ_MAX_P) - 1u;
     f_changed = f_returned = f_success = 0;
     failed = 0;
@@ -163,9 +182,9 @@ struct SeqMachine {
   }
   SG_HD int new_partial() {
     const int p = alloc();
-    SeqPartial& x = M->P[p];
+    SeqPartialT<G>& x = M->P[p];
     x.pts = -1;
-    for (int s = 0; s < PQ_MAX_S; ++s) { x.slot[s] = -1; x.clen[s] = 0; }
+    for (int s = 0; s < G::S; ++s) { x.slot[s] = -1; x.clen[s] = 0; }
     return p;
   }
   SG_HD int clone_partial(int q) {   // shallow clone; chains are never shared here (sg_seq_rule), so copy them
@@ -185,7 +204,7 @@ struct SeqMachine {
 
   // ---- events
   SG_HD int64_t get_event(int p, int s, int idx) {
-    const SeqPartial& x = M->P[p];
+    const SeqPartialT<G>& x = M->P[p];
     if (st(s).kind != SG_K_COUNT) {
       if (x.slot[s] < 0) return -1;
       return (idx == 0 || idx == -1) ? dec(x.slot[s]) : -1;
@@ -203,11 +222,11 @@ struct SeqMachine {
   SG_HD int16_t enc(int64_t pos) const { return (int16_t)(pos & 0x7FFF); }
   SG_HD int64_t dec(int x) const { return x < 0 ? -1 : cur - (int64_t)(((uint32_t)(cur & 0x7FFF) - (uint32_t)x) & 0x7FFFu); }
   SG_HD bool has_event(int p, int s) {
-    const SeqPartial& x = M->P[p];
+    const SeqPartialT<G>& x = M->P[p];
     return st(s).kind == SG_K_COUNT ? x.clen[s] > 0 : x.slot[s] >= 0;
   }
   SG_HD int slot_pos(int p, int s) {
-    const SeqPartial& x = M->P[p];
+    const SeqPartialT<G>& x = M->P[p];
     return st(s).kind == SG_K_COUNT ? x.chain[ru->coff[s]] : x.slot[s];
   }
   struct Reader {
@@ -278,7 +297,7 @@ struct SeqMachine {
   }
   SG_HD void count_post(int s, int p) {
     const sg_state_desc& x = st(s);
-    SeqPartial& y = M->P[p];
+    SeqPartialT<G>& y = M->P[p];
     const int n = y.clen[s];
     f_success |= bit(s);
     y.pts = y.chain[ru->coff[s] + n - 1];
@@ -357,7 +376,7 @@ struct SeqMachine {
     const int last = x.this_last;
     for (int r = 0; r < n && !failed; ++r) {
       const int p = M->list[s][0][r];
-      SeqPartial& y = M->P[p];
+      SeqPartialT<G>& y = M->P[p];
       bool remove = false;
       if (x.kind == SG_K_COUNT) {
         if ((s + 1 < d->n_states && has_event(p, s + 1)) || (s + 2 < d->n_states && has_event(p, s + 2))) continue;
@@ -404,10 +423,10 @@ struct SeqMachine {
   SG_HD void rebase(int64_t last, int64_t from) {
     cur = last;
     for (int p = 0; p < PQ_MAX_P; ++p) {
-      SeqPartial& x = M->P[p];
-      for (int s = 0; s < PQ_MAX_S; ++s)
+      SeqPartialT<G>& x = M->P[p];
+      for (int s = 0; s < G::S; ++s)
         if (x.slot[s] >= 0) x.slot[s] = enc(dec(x.slot[s]) - from);
-      for (int c = 0; c < PQ_MAX_CHAIN; ++c) x.chain[c] = enc(dec(x.chain[c]) - from);
+      for (int c = 0; c < G::CH; ++c) x.chain[c] = enc(dec(x.chain[c]) - from);
       if (x.pts >= 0) x.pts = enc(dec(x.pts) - from);
     }
   }
@@ -435,7 +454,8 @@ struct SeqMachine {
 // (pool slots may differ) and the same pending H_RETURNED bits.  Positions are compared encoded (absolute & 0x7FFF).
 // Not compared, because nothing reads them before writing them: H_CHANGED / H_SUCCESS (cleared before every filter),
 // H_INIT (only read for start states without `every`, outside sg_seq_rule).
-SG_HD inline bool sg_seq_equiv(const SeqState& A, const SeqState& B, const sg_nfa_desc& d, const SgSeqRule& ru) {
+template <class G>
+SG_HD inline bool sg_seq_equiv(const SeqStateT<G>& A, const SeqStateT<G>& B, const sg_nfa_desc& d, const SgSeqRule& ru) {
   if (A.created != B.created || A.fret != B.fret) return false;
   int8_t a2b[PQ_MAX_P], b2a[PQ_MAX_P];
   for (int p = 0; p < PQ_MAX_P; ++p) { a2b[p] = -1; b2a[p] = -1; }
@@ -450,8 +470,8 @@ SG_HD inline bool sg_seq_equiv(const SeqState& A, const SeqState& B, const sg_nf
         }
         a2b[pa] = (int8_t)pb;
         b2a[pb] = (int8_t)pa;
-        const SeqPartial& x = A.P[pa];
-        const SeqPartial& y = B.P[pb];
+        const SeqPartialT<G>& x = A.P[pa];
+        const SeqPartialT<G>& y = B.P[pb];
         if (x.pts != y.pts) return false;
         for (int t = 0; t < d.n_states; ++t) {
           if (d.states[t].kind == SG_K_COUNT) {

@@ -26,7 +26,8 @@ struct HiHandle {
   int pp_active = 1;
   struct CRow { int64_t ts; int32_t key; int64_t vals[SG_MAX_RET]; int32_t nullmask; };
   std::vector<CRow> carried;
-  std::vector<SeqState> seq_state;   // sequence lanes: per key
+  std::vector<SeqState> seq_state;   // sequence lanes: per key (partial.hip's geometry choice: big ...)
+  std::vector<SeqStateT<SqSmall>> seq_state_s;   // (... or small, sg_seq_small)
   int64_t spec_rows = 0, spec_warm = 0, spec_reruns = 0;   // speculative units (0: one run per key)
   int64_t pp_steps = 0, pp_lanes = 0;                      // partial lanes: rows stepped, lanes started
 };
@@ -231,7 +232,9 @@ struct HostSeqSrc {
   }
 };
 
-static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std::vector<uint64_t>& k1) {
+template <class G>
+static int seq_push(HiHandle* h, std::vector<SeqStateT<G>>& states, const sg_batch* b, std::vector<char>& recs,
+                    std::vector<uint64_t>& k1) {
   const sg_nfa_desc& d = h->d;
   const SgSeqRule ru = sg_seq_rule(d);
   const int64_t n = b->n;
@@ -250,8 +253,8 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
     if (k < 0) continue;
     own[k].push_back(nc + i);
   }
-  if (h->seq_state.size() < own.size()) h->seq_state.resize(own.size());
-  std::vector<SeqState> next_state = h->seq_state;
+  if (states.size() < own.size()) states.resize(own.size());
+  std::vector<SeqStateT<G>> next_state = states;
   HostPpSrc src{b, &d, &h->carried, nc};
   const int rstride = 32 + 8 * d.n_select;
   const int64_t H = ru.horizon;
@@ -260,8 +263,8 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
     const auto& rows = own[k];
     const int64_t nk = (int64_t)rows.size();
     if (!nk) continue;
-    SeqState& st = next_state[k];
-    SeqMachine<HostSeqSrc> m;
+    SeqStateT<G>& st = next_state[k];
+    SeqMachine<HostSeqSrc, G> m;
     m.d = &d;
     m.ru = &ru;
     m.src = HostSeqSrc{src, &rows};
@@ -271,7 +274,7 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
     if (ncar[k] == 0) { memset(&st, 0, sizeof(st)); next_state[k] = st; }   // a key without state starts zeroed
     uint32_t seq = 0;
     int64_t crow = -1;
-    auto emit = [&](SeqMachine<HostSeqSrc>& mm, int p, int grp) {
+    auto emit = [&](SeqMachine<HostSeqSrc, G>& mm, int p, int grp) {
       const int64_t r = crow;
       k1.push_back(((uint64_t)r << 16) | seq++);
       const size_t o = recs.size();
@@ -295,7 +298,7 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
       }
       memcpy(rec + 16, h32, 16);
     };
-    auto noemit = [&](SeqMachine<HostSeqSrc>&, int, int) {};
+    auto noemit = [&](SeqMachine<HostSeqSrc, G>&, int, int) {};
     // run rows [a, b) from the state in `st` (the machine's M), emitting or not
     auto run = [&](int64_t a, int64_t b2, bool emitting) {
       m.begin();
@@ -317,7 +320,7 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
       // it; a unit whose warmed-up start differs from its predecessor's end is rerun from that end; then every unit
       // runs again from its verified start, emitting
       const int64_t U = (nk - ncar[k] + R - 1) / R;
-      std::vector<SeqState> start((size_t)U), fin((size_t)U);
+      std::vector<SeqStateT<G>> start((size_t)U), fin((size_t)U);
       for (int64_t c = 0; c < U; ++c) {
         const int64_t s0 = ncar[k] + c * R, s1 = std::min(nk, s0 + R);
         if (c == 0) st = next_state[k];
@@ -364,7 +367,7 @@ static int seq_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std
       next.push_back(cr);
     }
   }
-  h->seq_state.swap(next_state);
+  states.swap(next_state);
   h->carried.swap(next);
   return 1;
 }
@@ -403,7 +406,9 @@ int hi_push(HiHandle* h, const sg_batch* b) {
     std::vector<uint64_t> k1;
     const std::vector<HiHandle::CRow> before = h->carried;
     const std::vector<SeqState> before_st = h->seq_state;
-    if (seq_push(h, b, recs, k1)) {
+    const std::vector<SeqStateT<SqSmall>> before_s = h->seq_state_s;
+    const bool small = sg_seq_small(sg_seq_rule(h->d), h->d);
+    if (small ? seq_push(h, h->seq_state_s, b, recs, k1) : seq_push(h, h->seq_state, b, recs, k1)) {
       const int rstride = 32 + 8 * h->d.n_select;
       std::vector<size_t> idx(k1.size());
       for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
@@ -415,6 +420,7 @@ int hi_push(HiHandle* h, const sg_batch* b) {
     if (!before.empty()) { h->err = SG_ECAPACITY; return SG_ECAPACITY; }
     h->carried = before;
     h->seq_state = before_st;
+    h->seq_state_s = before_s;
   }
   if (h->pp && h->pp_active && (sg_pp_rule(h->d).ok || sg_seq_rule(h->d).ok)) {
    if (sg_pp_rule(h->d).ok) {
