@@ -188,20 +188,40 @@ SG_HD inline uint32_t pp_tkey(int64_t row, int rank) { return (uint32_t)(((uint6
 //                void read_bits(int64_t row, int ret_slot, int type, int64_t& bits, int& null) (INT sign-extended,
 //                FLOAT as its 32-bit pattern -- the bit layout of sg_val_bits);
 //                int lbit(int state, int64_t row) -> 0/1, or -1 when the state's filter must be evaluated.
-// The dynamically indexed part of a lane's state (LDS on the GPU); the rest stays in registers.
-struct PpArrays {
-  int32_t slot[PP_MAX_S];
-  int32_t chain[PP_MAX_CHAIN];
-  uint32_t hist[PP_MAX_HIST];
-  int8_t clen[PP_MAX_S];
+// The dynamically indexed part of a lane's state (LDS on the GPU); the rest stays in registers.  Its geometry (S states,
+// CH chain entries) sets how many lanes a CU holds: queries of C3's family (<= 4 states, <= 6 chain entries,
+// sg_pp_small) run with 60-byte arrays instead of 120.
+template <int S_, int CH_>
+struct PpGeo {
+  static constexpr int S = S_;
+  static constexpr int CH = CH_;
 };
+using PpBig = PpGeo<PP_MAX_S, PP_MAX_CHAIN>;
+using PpSmall = PpGeo<4, 6>;
 
-template <class Src>
+template <class G>
+struct PpArraysT {
+  int32_t slot[G::S];
+  int32_t chain[G::CH];
+  uint32_t hist[PP_MAX_HIST];
+  int8_t clen[G::S];
+};
+using PpArrays = PpArraysT<PpBig>;
+
+SG_HD inline bool sg_pp_small(const SgPpRule& r, const sg_nfa_desc& d) {
+  if (!r.ok || d.n_states > PpSmall::S) return false;
+  int chain = 0;
+  for (int s = 0; s < d.n_states; ++s)
+    if (d.states[s].kind == SG_K_COUNT) chain += d.states[s].max_count;
+  return chain <= PpSmall::CH;
+}
+
+template <class Src, class G = PpBig>
 struct PpLane {
   const sg_nfa_desc* d;
   const SgPpRule* ru;
   Src src;
-  PpArrays* A;
+  PpArraysT<G>* A;
   uint32_t l0, l1;
   uint32_t f_changed, f_returned, f_success;
   int64_t pts;
@@ -218,13 +238,13 @@ struct PpLane {
 
   // does the start state's armed partial accept this row (its filter, evaluated with e1 bound to the row)?
   SG_HD bool start_ok(int32_t row) {
-    for (int s = 0; s < PP_MAX_S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
+    for (int s = 0; s < G::S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
     A->slot[ru->start] = (int32_t)row;
     cur_row = row;
     return filter(ru->start);
   }
   SG_HD void start(int32_t row) {   // the armed start partial takes e1 = row (process_and_return of the start state)
-    for (int s = 0; s < PP_MAX_S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
+    for (int s = 0; s < G::S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
     l0 = l1 = 0;
     f_changed = f_returned = f_success = 0;
     nh = 0;

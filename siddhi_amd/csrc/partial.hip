@@ -60,6 +60,7 @@ struct PartialState {
   SgSeqRule* dsrule = nullptr;
   void* kst = nullptr;          // sequence lanes: per-key machine state SeqStateT<G> (zero = no runtime yet)
   int sq_small = 0;             // the query fits seq.h's small state geometry (SqSmall)
+  int pp_small = 0;             // the query fits chain.h's small lane geometry (PpSmall)
   size_t sq_bytes = sizeof(SeqState);
   int64_t kst_keys = 0;
   int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
@@ -109,6 +110,7 @@ PartialState* sg_partial_new(const sg_nfa_desc& d) {
   ps->mode = ru.ok ? 1 : 2;
   ps->rule = ru;
   ps->srule = sr;
+  ps->pp_small = sg_pp_small(ru, d) ? 1 : 0;
   if (ps->mode == 2) {
     ps->rule.local_mask = sr.local_mask;
     ps->rule.start = sr.start;
@@ -505,6 +507,7 @@ __global__ void k_pp_compact(int64_t m, const uint32_t* __restrict__ flag, const
 
 constexpr int PP_BLOCK = 256;
 constexpr int64_t PP_WAVE_CANDS = 2048;   // start rows per wave
+template <class G>
 __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                        const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ cand,
                                                        int64_t ncand, const uint32_t* __restrict__ skey,
@@ -513,7 +516,7 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
   __shared__ DevDesc dl;
   __shared__ SgPpRule rl;
   __shared__ PpPacked pl;
-  __shared__ PpArrays lanes[PP_BLOCK];
+  __shared__ PpArraysT<G> lanes[PP_BLOCK];
   {
     const uint32_t* s3 = (const uint32_t*)&P;
     for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];
@@ -534,7 +537,7 @@ __global__ void __launch_bounds__(PP_BLOCK) k_pp_lanes(PpArgs a, PpPacked P, con
   const int64_t hi = lo + PP_WAVE_CANDS < ncand ? lo + PP_WAVE_CANDS : ncand;
   if (lo >= ncand) return;
   PpSrc src{&pl};
-  PpLane<PpSrc> L;
+  PpLane<PpSrc, G> L;
   L.d = dd;
   L.ru = &rl;
   L.src = src;
@@ -1471,10 +1474,15 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   o.k1_none = k1_bits >= 64 ? ~0ull : (1ull << k1_bits) - 1;
   HIPCHK(hipMemsetAsync(o.count, 0, 16, st));
   h->kbeg("partial_lanes");
-  if (ncand)
-    hipLaunchKernelGGL(k_pp_lanes, dim3((unsigned)((ncand + PP_WAVE_CANDS * (PP_BLOCK / 64) - 1) / (PP_WAVE_CANDS * (PP_BLOCK / 64)))),
-                       dim3(PP_BLOCK), 0, st, a, P,
-                       h->ddesc, ps->drule, cand, (int64_t)ncand, skeys, sids, end, o);
+  if (ncand) {
+    const dim3 gl((unsigned)((ncand + PP_WAVE_CANDS * (PP_BLOCK / 64) - 1) / (PP_WAVE_CANDS * (PP_BLOCK / 64))));
+    if (ps->pp_small)
+      hipLaunchKernelGGL(k_pp_lanes<PpSmall>, gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand, (int64_t)ncand,
+                         skeys, sids, end, o);
+    else
+      hipLaunchKernelGGL(k_pp_lanes<PpBig>, gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand, (int64_t)ncand,
+                         skeys, sids, end, o);
+  }
   HIPCHK(hipGetLastError());
   h->kend();
   h->mark(3);

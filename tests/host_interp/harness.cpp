@@ -118,6 +118,7 @@ struct HostPpSrc {
 };
 
 // partial-lane push (partial.hip restated on the host); returns 0 when the push breaks the route's precondition
+template <class G>
 static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std::vector<uint64_t>& k1,
                    std::vector<uint64_t>& th, std::vector<uint64_t>& tl) {
   const sg_nfa_desc& d = h->d;
@@ -146,8 +147,8 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
   for (size_t k = 0; k < own.size(); ++k) {
     const auto& rows = own[k];
     for (size_t p = 0; p < rows.size(); ++p) {
-      PpLane<HostPpSrc> L;
-      PpArrays arr;
+      PpLane<HostPpSrc, G> L;
+      PpArraysT<G> arr;
       L.d = &d;
       L.ru = &ru;
       L.src = src;
@@ -426,7 +427,8 @@ int hi_push(HiHandle* h, const sg_batch* b) {
    if (sg_pp_rule(h->d).ok) {
     std::vector<char> recs;
     std::vector<uint64_t> k1, th, tl;
-    const int rc = pp_push(h, b, recs, k1, th, tl);
+    const int rc = sg_pp_small(sg_pp_rule(h->d), h->d) ? pp_push<PpSmall>(h, b, recs, k1, th, tl)
+                                                       : pp_push<PpBig>(h, b, recs, k1, th, tl);
     if (rc == -2) { h->err = SG_EORDER; return SG_EORDER; }
     if (rc < 0) { h->err = SG_EUNSUPPORTED; return SG_EUNSUPPORTED; }
     if (rc == 1) {
