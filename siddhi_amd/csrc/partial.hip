@@ -508,27 +508,25 @@ __global__ void k_pp_compact(int64_t m, const uint32_t* __restrict__ flag, const
 constexpr int PP_BLOCK = 256;
 constexpr int64_t PP_WAVE_CANDS = 2048;   // start rows per wave
 template <class G>
-__global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 5 : 1) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
+__global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 6 : 4) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                        const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ cand,
                                                        int64_t ncand, const uint32_t* __restrict__ skey,
                                                        const uint32_t* __restrict__ sid, const uint32_t* __restrict__ end,
                                                        PpOut o) {
-  __shared__ DevDesc dl;
+  // the descriptor (9.6 KB) stays in global memory (cache-resident: every lane reads the same few hundred bytes of
+  // it), so LDS holds more lanes
   __shared__ SgPpRule rl;
   __shared__ PpPacked pl;
   __shared__ PpArraysT<G> lanes[PP_BLOCK];
   {
     const uint32_t* s3 = (const uint32_t*)&P;
     for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];
-    const uint32_t* src = (const uint32_t*)ddg;
-    uint32_t* dst = (uint32_t*)&dl;
-    for (uint32_t i = threadIdx.x; i < sizeof(DevDesc) / 4; i += blockDim.x) dst[i] = src[i];
     const uint32_t* rs = (const uint32_t*)rug;
     uint32_t* rd = (uint32_t*)&rl;
     for (uint32_t i = threadIdx.x; i < sizeof(SgPpRule) / 4; i += blockDim.x) rd[i] = rs[i];
     __syncthreads();
   }
-  const DevDesc* dd = &dl;
+  const DevDesc* dd = ddg;
   // each wave owns PP_WAVE_CANDS consecutive start rows; a lane whose partial is finished takes the next one, so the
   // wave never waits on its longest partial (ballot + popcount hand-out, no atomics)
   const int lane = threadIdx.x & 63;
