@@ -1005,23 +1005,15 @@ __global__ void k_sq_drop(int64_t n, SqOut o) {
   }
 }
 
-// Match records in delivery order (QuerySelector.processNoGroupBy + SelectiveStateEventPopulator,
-// C/query/selector/QuerySelector.java:125-163): the lanes' compact records {trigger position, key, group, position of
-// the timestamp row, position per select slot} -> {trigger index, ts, key, group, null mask, values}.
-__global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char* __restrict__ em, int32_t estride,
-                         char* __restrict__ out, int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
-                         const uint64_t* __restrict__ index, uint64_t base_index) {
-  // records are assembled in LDS and leave the block as one contiguous copy
-  extern __shared__ __align__(16) char em_lds[];
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t i = i0 + threadIdx.x;
-  const int64_t nb = n - i0 < (int64_t)blockDim.x ? n - i0 : (int64_t)blockDim.x;
-  if (i < n) {
-  const uint32_t* e = (const uint32_t*)(em + (size_t)idx[i] * estride);
-  char* rec = em_lds + (size_t)threadIdx.x * ostride;
+// Compact emission records {trigger position, trigger combined row, key, group, timestamp row position, position per
+// select slot} -> match records {trigger index, ts, key, group, null mask, values}.
+// one match record from its compact emission record e
+__device__ __forceinline__ void em_build(const uint32_t* __restrict__ e, char* rec, const PpPacked& P,
+                                         const DevDesc* __restrict__ dd, const uint64_t* __restrict__ index,
+                                         uint64_t base_index) {
   int64_t* h64 = (int64_t*)rec;
-  // in delivery order the trigger rows ascend, so the trigger row's own columns are read nearly coalesced straight
-  // from the batch; other rows go through the key-sorted position (sid), and a row selected twice is read once
+  // the trigger row's own columns are read straight from the batch where the slot is lazy; other rows go through
+  // their key-sorted position, and a row selected twice in a row is read once
   const uint32_t tq = e[0];
   const int64_t r = (int64_t)e[1] - P.nc;
   h64[0] = (int64_t)(index ? index[r] : base_index + (uint64_t)r);
@@ -1052,12 +1044,43 @@ __global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char
   }
   h32[2] = nm;
   h32[3] = 0;
-  }
+}
+
+// Match records in delivery order (QuerySelector.processNoGroupBy + SelectiveStateEventPopulator,
+// C/query/selector/QuerySelector.java:125-163), gathering the compact records by the sorted order idx: each block's
+// records are assembled in LDS and leave as one contiguous copy (sequence lanes: their rows are read lazily anyway)
+__global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char* __restrict__ em, int32_t estride,
+                         char* __restrict__ out, int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
+                         const uint64_t* __restrict__ index, uint64_t base_index) {
+  extern __shared__ __align__(16) char em_lds[];
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + threadIdx.x;
+  const int64_t nb = n - i0 < (int64_t)blockDim.x ? n - i0 : (int64_t)blockDim.x;
+  if (i < n) em_build((const uint32_t*)(em + (size_t)idx[i] * estride), em_lds + (size_t)threadIdx.x * ostride, P, dd,
+                      index, base_index);
   __syncthreads();
   const uint2* src = (const uint2*)em_lds;   // records are 8-byte multiples, the output only 8-byte aligned
   uint2* dst = (uint2*)(out + (size_t)i0 * ostride);
   const int64_t words = nb * ostride / 8;
   for (int64_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = src[w];
+}
+
+// delivery position of every slot (slots without a match keep ~0)
+__global__ void k_em_dest(int64_t n, const uint32_t* __restrict__ idx, uint32_t* __restrict__ dest) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dest[idx[i]] = (uint32_t)i;
+}
+
+// Partial lanes: slot order is start-row order, i.e. key-ordered, so walking the slots reads the compact records and
+// the packed rows they point at nearly coalesced; each record is then written to its delivery position
+__global__ void k_em_scatter(int64_t T, const uint32_t* __restrict__ dest, const char* __restrict__ em, int32_t estride,
+                             char* __restrict__ out, int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
+                             const uint64_t* __restrict__ index, uint64_t base_index) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= T) return;
+  const uint32_t d = dest[w];
+  if (d == 0xFFFFFFFFu) return;
+  em_build((const uint32_t*)(em + (size_t)w * estride), out + (size_t)d * ostride, P, dd, index, base_index);
 }
 
 // carry for sequence lanes: the last H rows of every key
@@ -1530,8 +1553,11 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     }
     const int64_t M = (int64_t)total;
     char* out = h->out.reserve(M, nsel, st);
-    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((M + 255) / 256)), blk, 256 * rstride, st, M, ia, o.rec, o.rstride,
-                       out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
+    uint32_t* dest = (uint32_t*)h->ws.get("pp_dest", 4 * (size_t)(T + 1), st);
+    HIPCHK(hipMemsetAsync(dest, 0xFF, 4 * (size_t)T, st));
+    hipLaunchKernelGGL(k_em_dest, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, ia, dest);
+    hipLaunchKernelGGL(k_em_scatter, g2, blk, 0, st, T, dest, o.rec, o.rstride, out + (size_t)h->out.n * rstride, rstride,
+                       P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());
     h->kend();
     h->out.n += M;
