@@ -1019,9 +1019,8 @@ __device__ __forceinline__ void em_build(const uint32_t* __restrict__ e, char* r
   h64[0] = (int64_t)(index ? index[r] : base_index + (uint64_t)r);
   const int32_t tp = (int32_t)e[4];
   h64[1] = tp < 0 ? -1 : P.ts ? P.ts[tp] : (uint32_t)tp == tq ? P.bts[r] : pp_lazy_ts(&P, tp);
-  uint32_t* h32 = (uint32_t*)(rec + 16);
-  h32[0] = e[2];
-  h32[1] = e[3];
+  uint64_t* h2 = (uint64_t*)(rec + 16);   // {key, group} and {null mask, 0} as two 8-byte stores
+  h2[0] = (uint64_t)e[2] | ((uint64_t)e[3] << 32);
   uint32_t nm = 0;
   int64_t* vals = (int64_t*)(rec + 32);
   const int ns = dd->n_select;
@@ -1042,8 +1041,7 @@ __device__ __forceinline__ void em_build(const uint32_t* __restrict__ e, char* r
     prs = rs;
     vals[s] = pv;
   }
-  h32[2] = nm;
-  h32[3] = 0;
+  h2[1] = (uint64_t)nm;
 }
 
 // Match records in delivery order (QuerySelector.processNoGroupBy + SelectiveStateEventPopulator,
