@@ -508,7 +508,7 @@ __global__ void k_pp_compact(int64_t m, const uint32_t* __restrict__ flag, const
 constexpr int PP_BLOCK = 256;
 constexpr int64_t PP_WAVE_CANDS = 2048;   // start rows per wave
 template <class G>
-__global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 7 : 4) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
+__global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                        const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ cand,
                                                        int64_t ncand, const uint32_t* __restrict__ skey,
                                                        const uint32_t* __restrict__ sid, const uint32_t* __restrict__ end,
