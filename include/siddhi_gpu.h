@@ -283,6 +283,55 @@ int sg_router_open(int n_shards, int threads, sg_router** out);
 int sg_router_route(sg_router* r, int64_t n, const int64_t* raw, int32_t* dense, int32_t* shard, int32_t* local);
 int sg_router_keys(const sg_router* r, int64_t* n_keys, int32_t shard, int64_t* shard_keys);
 int sg_router_close(sg_router* r);
+/* The router's per-shard id table: dense_of_local[l] = node-wide dense id of shard `shard`'s key l (cap entries). */
+int sg_router_dense_ids(const sg_router* r, int32_t shard, int32_t* dense_of_local, int64_t cap);
+/* Merge match runs (each already in delivery order) into the node's delivery order by (trigger, phase = group >> 24,
+ * dense key), ties in run order: out_src[i] = index of the i-th merged row in the concatenation of the runs.
+ * group / key (and their entries) may be NULL (treated as 0).  SG_EORDER if a run is not ordered by trigger.
+ * Replaces the single ordered stream QueryCallback.receive sees on one host (C/query/output/callback/
+ * QueryCallback.java:52-85) for key-sharded engines. */
+int sg_merge_order(int n_runs, const int64_t* run_len, const uint64_t* const* trigger, const uint32_t* const* group,
+                   const int32_t* const* key, int threads, int64_t* out_src);
+
+/* ---- Node pipeline: one host process drives the node's GPUs for one partitioned query ----------------------------
+ * Replaces PartitionStreamReceiver.receive(Event[]) (C/partition/PartitionStreamReceiver.java:177-221) feeding the
+ * per-key cloned runtimes (C/partition/PartitionRuntime.java:255-308) and the ordered delivery to QueryCallback
+ * (C/query/output/callback/QueryCallback.java:52-85).  A host batch of raw rows goes in; the node routes each row by
+ * its raw partition-key value (first-seen dense ids, shard = mix64(id) mod n_gpus), streams every shard's rows to its
+ * GPU in chunks (H2D, kernels and D2H of consecutive chunks overlapped; state carried between chunks and pushes),
+ * and merges the shards' matches into the reference's delivery order.  Unpartitioned queries run on one GPU
+ * (replicas only).  A node is single-threaded like a handle; it starts one thread per GPU internally. */
+#define SG_NODE_MAX_GPUS 16
+typedef struct sg_node sg_node;
+typedef struct sg_node_batch {
+  int64_t n;
+  uint64_t base_index;          /* global event index of row 0; consecutive pushes continue the index */
+  const int64_t* ts;
+  const int32_t* stream;        /* optional stream index per row; -1 = clock-only row (reaches every shard) */
+  const int64_t* raw_key;       /* raw 64-bit partition-key value per row (integers, float bits, dictionary ids) */
+  const void* const* cols;      /* [n_cols] typed host columns (NULL entries: not read by the query) */
+  const uint8_t* const* nulls;  /* optional [n_cols] null flags */
+} sg_node_batch;
+typedef struct sg_node_stats {  /* of the last sg_node_push */
+  double total_ms;              /* wall time of the pipeline (routing .. last merged row) */
+  double reserve_ms;            /* buffer sizing before the pipeline (zero once sizes are stable) */
+  double route_ms, merge_ms;    /* host thread-pool time spent routing / merging */
+  double gpu_ms[SG_NODE_MAX_GPUS];   /* per GPU: compute-thread busy time */
+  int64_t rows, matches, chunks, chunk_rows, h2d_bytes, d2h_bytes;
+  int64_t shard_rows[SG_NODE_MAX_GPUS];   /* rows each GPU has received since open/reset */
+} sg_node_stats;
+/* chunk_rows 0: 25M rows per chunk; host_threads 0: all hardware threads. */
+int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const sg_options* opt, int host_threads,
+                 int64_t chunk_rows, sg_node** out);
+/* Push a batch; its matches (node delivery order) go to out rows [0, *n).  out->trigger is required; other NULL
+ * arrays are skipped.  SG_ECAPACITY if more than cap matches: the node must then be reset. */
+int sg_node_push(sg_node* nd, const sg_node_batch* b, const sg_match_columns* out, int64_t cap, int64_t* n);
+int sg_node_reset(sg_node* nd);   /* new stream: forget keys and per-key state */
+int sg_node_stats_get(const sg_node* nd, sg_node_stats* st);
+int sg_node_keys(const sg_node* nd, int64_t* n_keys);
+int sg_node_close(sg_node* nd);
+const char* sg_node_last_error(const sg_node* nd);
+
 /* Pinned host memory for batch columns (the ingress then copies asynchronously at full PCIe rate). */
 int sg_host_alloc(size_t bytes, void** p);
 int sg_host_free(void* p);

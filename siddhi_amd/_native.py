@@ -19,7 +19,9 @@ SG_ABI_VERSION = 2
 SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
            "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version",
            "sg_snapshot", "sg_restore", "sg_host_alloc", "sg_host_free", "sg_poll_columns", "sg_push_deliver",
-           "sg_router_open", "sg_router_route", "sg_router_keys", "sg_router_close"]
+           "sg_router_open", "sg_router_route", "sg_router_keys", "sg_router_close", "sg_router_dense_ids",
+           "sg_merge_order", "sg_node_open", "sg_node_push", "sg_node_reset", "sg_node_stats_get", "sg_node_keys",
+           "sg_node_close", "sg_node_last_error"]
 
 I32, I64, U64 = ct.c_int32, ct.c_int64, ct.c_uint64
 
@@ -77,6 +79,21 @@ class sg_matches(ct.Structure):
 class sg_match_columns(ct.Structure):
     _fields_ = [("trigger", ct.c_void_p), ("ts", ct.c_void_p), ("key", ct.c_void_p), ("group", ct.c_void_p),
                 ("cols", ct.c_void_p * SG_MAX_SELECT), ("nulls", ct.c_void_p * SG_MAX_SELECT)]
+
+
+SG_NODE_MAX_GPUS = 16
+
+
+class sg_node_batch(ct.Structure):
+    _fields_ = [("n", I64), ("base_index", U64), ("ts", ct.c_void_p), ("stream", ct.c_void_p),
+                ("raw_key", ct.c_void_p), ("cols", ct.c_void_p), ("nulls", ct.c_void_p)]
+
+
+class sg_node_stats(ct.Structure):
+    _fields_ = [("total_ms", ct.c_double), ("reserve_ms", ct.c_double), ("route_ms", ct.c_double),
+                ("merge_ms", ct.c_double), ("gpu_ms", ct.c_double * SG_NODE_MAX_GPUS),
+                ("rows", I64), ("matches", I64), ("chunks", I64), ("chunk_rows", I64), ("h2d_bytes", I64),
+                ("d2h_bytes", I64), ("shard_rows", I64 * SG_NODE_MAX_GPUS)]
 
 
 class sg_match_records(ct.Structure):
@@ -137,6 +154,16 @@ def load_library(path: str = LIB_PATH):
         lib.sg_router_route.argtypes = [P, I64, P, P, P, P]
         lib.sg_router_keys.argtypes = [P, ct.POINTER(I64), I32, ct.POINTER(I64)]
         lib.sg_router_close.argtypes = [P]
+        lib.sg_router_dense_ids.argtypes = [P, I32, P, I64]
+        lib.sg_merge_order.argtypes = [ct.c_int, P, P, P, P, ct.c_int, P]
+        lib.sg_node_open.argtypes = [ct.c_int, P, P, P, ct.c_int, I64, ct.POINTER(P)]
+        lib.sg_node_push.argtypes = [P, P, P, I64, ct.POINTER(I64)]
+        lib.sg_node_reset.argtypes = [P]
+        lib.sg_node_stats_get.argtypes = [P, P]
+        lib.sg_node_keys.argtypes = [P, ct.POINTER(I64)]
+        lib.sg_node_close.argtypes = [P]
+        lib.sg_node_last_error.argtypes = [P]
+        lib.sg_node_last_error.restype = ct.c_char_p
         lib.sg_last_error.argtypes = [P]
         lib.sg_last_error.restype = ct.c_char_p
         lib.sg_version.restype = ct.c_char_p
@@ -396,6 +423,89 @@ class Router:
             self.close()
         except Exception:
             pass
+
+
+def merge_order(triggers, groups=None, keys=None, threads: int = 16) -> np.ndarray:
+    """sg_merge_order: the node's delivery order of several match runs (each in delivery order) as indices into
+    their concatenation -- by (trigger, phase, dense key), ties in run order."""
+    lib = load_library()
+    n = len(triggers)
+    tr = [np.ascontiguousarray(t, np.uint64) for t in triggers]
+    gr = None if groups is None else [np.ascontiguousarray(g, np.uint32) for g in groups]
+    ky = None if keys is None else [np.ascontiguousarray(k, np.int32) for k in keys]
+    lens = np.array([len(t) for t in tr], np.int64)
+    P = ct.c_void_p
+    ptrs = lambda arrs: None if arrs is None else ct.cast((P * max(n, 1))(*[a.ctypes.data for a in arrs]), P)  # noqa
+    out = np.zeros(int(lens.sum()), np.int64)
+    rc = lib.sg_merge_order(n, lens.ctypes.data, ptrs(tr), ptrs(gr), ptrs(ky), threads, out.ctypes.data)
+    if rc != 0:
+        raise SgError(rc, "sg_merge_order failed")
+    return out
+
+
+class Node:
+    """The node pipeline (sg_node_*): raw host rows -> native router -> every GPU of the node (one thread each,
+    chunks with H2D / kernels / D2H overlapped) -> merged matches in delivery order."""
+
+    def __init__(self, desc: sg_nfa_desc, n_gpus: int = 1, devices=None, options: sg_options = None,
+                 threads: int = 16, chunk_rows: int = 0):
+        self.lib = load_library()
+        self.n = ct.c_void_p()
+        self.desc = desc
+        self.opts = options if options is not None else sg_options()
+        devs = (ct.c_int * n_gpus)(*(devices if devices is not None else range(n_gpus)))
+        rc = self.lib.sg_node_open(n_gpus, devs, ct.byref(desc), ct.byref(self.opts), threads, chunk_rows,
+                                   ct.byref(self.n))
+        if rc != 0:
+            raise SgError(rc, "sg_node_open failed")
+
+    def check(self, rc):
+        if rc != 0:
+            raise SgError(rc, self.lib.sg_node_last_error(self.n).decode())
+
+    def push(self, b: sg_node_batch, cols: "sg_match_columns", cap: int) -> int:
+        n = I64()
+        self.check(self.lib.sg_node_push(self.n, ct.byref(b), ct.byref(cols), int(cap), ct.byref(n)))
+        return n.value
+
+    def stats(self) -> dict:
+        st = sg_node_stats()
+        self.check(self.lib.sg_node_stats_get(self.n, ct.byref(st)))
+        g = int(self.desc_gpus) if hasattr(self, "desc_gpus") else SG_NODE_MAX_GPUS
+        return {"total_ms": st.total_ms, "reserve_ms": st.reserve_ms, "route_ms": st.route_ms,
+                "merge_ms": st.merge_ms, "gpu_ms": [st.gpu_ms[k] for k in range(g)], "rows": st.rows,
+                "matches": st.matches, "chunks": st.chunks, "chunk_rows": st.chunk_rows, "h2d_bytes": st.h2d_bytes,
+                "d2h_bytes": st.d2h_bytes, "shard_rows": [st.shard_rows[k] for k in range(g)]}
+
+    def keys(self) -> int:
+        n = I64()
+        self.check(self.lib.sg_node_keys(self.n, ct.byref(n)))
+        return n.value
+
+    def reset(self):
+        self.check(self.lib.sg_node_reset(self.n))
+
+    def close(self):
+        if self.n:
+            self.lib.sg_node_close(self.n)
+            self.n = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_node_batch(n, base_index, ts, stream, raw_key, cols, nulls, keep):
+    """Assemble an sg_node_batch from raw host pointers (ints; 0 = absent)."""
+    ncol = len(cols)
+    carr = (ct.c_void_p * max(ncol, 1))(*[(c if c else None) for c in cols])
+    narr = (ct.c_void_p * max(ncol, 1))(*[(x if x else None) for x in nulls])
+    keep += [carr, narr]
+    has_nul = any(bool(x) for x in nulls)
+    return sg_node_batch(n, base_index, ts or None, stream or None, raw_key or None, ct.cast(carr, ct.c_void_p),
+                         ct.cast(narr, ct.c_void_p) if has_nul else None)
 
 
 class PinnedArray:

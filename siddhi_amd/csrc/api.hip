@@ -22,7 +22,7 @@ struct sg_handle {
   SgHandle h;
 };
 
-static int col_width(int type) { return (type == SG_T_LONG || type == SG_T_DOUBLE) ? 8 : 4; }
+int sg_col_width(int type) { return (type == SG_T_LONG || type == SG_T_DOUBLE) ? 8 : 4; }
 static int out_cols(const sg_nfa_desc& d) { return d.n_out > 0 ? d.n_out : d.n_select; }
 
 // ---- select expressions (QuerySelector.processNoGroupBy over math executors,
@@ -164,7 +164,7 @@ static void validate(const sg_nfa_desc* d) {
 }
 
 // One push of rows already in HBM: the engine route, then the select pass.
-static void push_view(SgHandle& h, BatchView& bv, int64_t n) {
+void sg_push_view(SgHandle& h, BatchView& bv, int64_t n) {
   const sg_nfa_desc& d = h.desc;
   for (int r = 0; r < d.n_ret; ++r)
     if (!bv.cols.col[d.ret_col[r]]) throw SgError(SG_EINVAL, "batch is missing a column the query reads");
@@ -206,17 +206,7 @@ static std::string slot_name(const char* what, int c, int slot) {
   return nm;
 }
 
-// Device buffers of one ingress slot (resolved on the calling thread: the workspace map is not thread-safe).
-struct SlotPtrs {
-  void* ts = nullptr;
-  void* stream = nullptr;
-  void* key = nullptr;
-  void* index = nullptr;
-  void* col[SG_MAX_COLS] = {};
-  void* nul[SG_MAX_COLS] = {};
-};
-
-static SlotPtrs reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int slot) {
+SlotPtrs sg_reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int slot) {
   const sg_nfa_desc& d = h.desc;
   SlotPtrs p;
   p.ts = h.ws.get(slot_name("ts", 0, slot), 8 * rows, h.stream);
@@ -225,7 +215,7 @@ static SlotPtrs reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int s
   if (b->index) p.index = h.ws.get(slot_name("index", 0, slot), 8 * rows, h.stream);
   for (int c = 0; c < d.n_cols; ++c) {
     if (b->cols && b->cols[c])
-      p.col[c] = h.ws.get(slot_name("col", c, slot), (size_t)col_width(d.col_type[c]) * rows, h.stream);
+      p.col[c] = h.ws.get(slot_name("col", c, slot), (size_t)sg_col_width(d.col_type[c]) * rows, h.stream);
     if (b->nulls && b->nulls[c]) p.nul[c] = h.ws.get(slot_name("nul", c, slot), rows, h.stream);
   }
   return p;
@@ -233,7 +223,7 @@ static SlotPtrs reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int s
 
 // Copy rows [lo, lo + cnt) of a host batch into a slot on stream `st`; returns the device view.  Touches no
 // handle state besides the descriptor, so it may run on a helper thread.
-static BatchView upload_to(const sg_nfa_desc& d, const SlotPtrs& p, const sg_batch* b, int64_t lo, int64_t cnt,
+BatchView sg_upload_to(const sg_nfa_desc& d, const SlotPtrs& p, const sg_batch* b, int64_t lo, int64_t cnt,
                            hipStream_t st) {
   BatchView bv;
   bv.n = cnt;
@@ -250,14 +240,14 @@ static BatchView upload_to(const sg_nfa_desc& d, const SlotPtrs& p, const sg_bat
   bv.key = (const int32_t*)up(p.key, b->key, 4);
   bv.index = (const uint64_t*)up(p.index, b->index, 8);
   for (int c = 0; c < d.n_cols; ++c) {
-    bv.cols.col[c] = b->cols ? up(p.col[c], b->cols[c], (size_t)col_width(d.col_type[c])) : nullptr;
+    bv.cols.col[c] = b->cols ? up(p.col[c], b->cols[c], (size_t)sg_col_width(d.col_type[c])) : nullptr;
     bv.cols.nul[c] = (const uint8_t*)(b->nulls ? up(p.nul[c], b->nulls[c], 1) : nullptr);
   }
   return bv;
 }
 
 static BatchView upload(SgHandle& h, const sg_batch* b, int64_t lo, int64_t cnt, int slot, hipStream_t st) {
-  return upload_to(h.desc, reserve_slot(h, b, cnt, slot), b, lo, cnt, st);
+  return sg_upload_to(h.desc, sg_reserve_slot(h, b, cnt, slot), b, lo, cnt, st);
 }
 
 struct ChunkHook {
@@ -291,12 +281,7 @@ static BatchView device_view(const sg_nfa_desc& d, const sg_batch* b) {
 // QueryCallback.java:52-85, as typed columns).  The pending AoS records are transposed on the GPU into a staging
 // buffer of columns; the columns are copied to the caller on a D2H stream, double-buffered so one chunk's copy
 // overlaps the next chunk's kernels.
-struct ColLayout {   // staging layout for `cap` rows
-  int ns;
-  int32_t width[SG_MAX_SELECT];
-  size_t off_trig, off_ts, off_key, off_grp, off_col[SG_MAX_SELECT], off_nul[SG_MAX_SELECT], bytes;
-};
-static ColLayout col_layout(const sg_nfa_desc& d, int64_t cap) {
+ColLayout sg_col_layout(const sg_nfa_desc& d, int64_t cap) {
   ColLayout L;
   L.ns = out_cols(d);
   size_t o = 0;
@@ -307,7 +292,7 @@ static ColLayout col_layout(const sg_nfa_desc& d, int64_t cap) {
   L.off_grp = take(4);
   for (int k = 0; k < L.ns; ++k) {
     const int t = d.n_out > 0 ? d.out_type[k] : d.sel_type[k];
-    L.width[k] = col_width(t);
+    L.width[k] = sg_col_width(t);
     L.off_col[k] = take((size_t)L.width[k]);
   }
   for (int k = 0; k < L.ns; ++k) L.off_nul[k] = take(1);
@@ -337,6 +322,12 @@ __global__ void __launch_bounds__(256) k_to_columns(int64_t n, const char* __res
   }
 }
 
+void sg_launch_to_columns(int64_t n, const char* rec, int stride, const ColLayout& L, char* stage, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_to_columns, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, rec, stride, L, stage);
+  HIPCHK(hipGetLastError());
+}
+
 __global__ void __launch_bounds__(256) k_to_matches(int64_t n, const char* __restrict__ rec, int stride, int ns,
                                                     uint64_t* __restrict__ trig, int64_t* __restrict__ ts,
                                                     int32_t* __restrict__ key, uint32_t* __restrict__ grp,
@@ -352,7 +343,7 @@ __global__ void __launch_bounds__(256) k_to_matches(int64_t n, const char* __res
   for (int k = 0; k < ns; ++k) vals[(size_t)i * ns + k] = ((const int64_t*)(r + 32))[k];
 }
 
-static void egress_init(SgHandle& h) {
+void sg_egress_init(SgHandle& h) {
   if (h.eg.d2h) return;
   HIPCHK(hipStreamCreateWithFlags(&h.eg.d2h, hipStreamNonBlocking));
   for (int k = 0; k < 2; ++k) {
@@ -368,9 +359,9 @@ static int64_t deliver_pending(SgHandle& h, const sg_match_columns* out, int64_t
   OutStore& o = h.out;
   const int64_t k = std::min<int64_t>(cap, o.n);
   if (k <= 0) return 0;
-  egress_init(h);
+  sg_egress_init(h);
   const sg_nfa_desc& d = h.desc;
-  const ColLayout L = col_layout(d, k);
+  const ColLayout L = sg_col_layout(d, k);
   if (h.eg.cap[slot] < (int64_t)L.bytes) {   // grow: wait until this slot's last copy has read it
     HIPCHK(hipEventSynchronize(h.eg.done[slot]));
     if (h.eg.stage[slot]) HIPCHK(hipFree(h.eg.stage[slot]));
@@ -430,7 +421,7 @@ static void ingest_host(SgHandle& h, const sg_batch* b, ChunkHook* after) {
   const int64_t nch = (n + C - 1) / C;
   if (nch == 1) {
     BatchView bv = upload(h, b, 0, n, 0, h.stream);
-    push_view(h, bv, n);
+    sg_push_view(h, bv, n);
     if (after) after->chunk_done();
     return;
   }
@@ -442,8 +433,8 @@ static void ingest_host(SgHandle& h, const sg_batch* b, ChunkHook* after) {
     }
   }
   SlotPtrs slots[2];
-  for (int s = 0; s < 2; ++s) slots[s] = reserve_slot(h, b, C, s);   // no workspace growth inside the pipeline
-  BatchView cur = upload_to(d, slots[0], b, 0, C, h.copy_stream);
+  for (int s = 0; s < 2; ++s) slots[s] = sg_reserve_slot(h, b, C, s);   // no workspace growth inside the pipeline
+  BatchView cur = sg_upload_to(d, slots[0], b, 0, C, h.copy_stream);
   HIPCHK(hipEventRecord(h.ev_copied[0], h.copy_stream));
   // The next chunk's copies are issued from a helper thread: a large hipMemcpyAsync can hold the calling
   // thread, which would otherwise delay this chunk's kernels (measured).
@@ -458,7 +449,7 @@ static void ingest_host(SgHandle& h, const sg_batch* b, ChunkHook* after) {
       copier = std::thread([&, s, lo] {
         try {
           if (hipSetDevice(h.device) != hipSuccess) { copy_rc = hipErrorInvalidDevice; return; }
-          next = upload_to(d, slots[s], b, lo + C, std::min(C, n - lo - C), h.copy_stream);
+          next = sg_upload_to(d, slots[s], b, lo + C, std::min(C, n - lo - C), h.copy_stream);
           copy_rc = hipEventRecord(h.ev_copied[s], h.copy_stream);
         } catch (...) {
           copy_rc = hipErrorUnknown;
@@ -467,7 +458,7 @@ static void ingest_host(SgHandle& h, const sg_batch* b, ChunkHook* after) {
     }
     try {
       HIPCHK(hipStreamWaitEvent(h.stream, h.ev_copied[k & 1], 0));
-      push_view(h, cur, cnt);
+      sg_push_view(h, cur, cnt);
       HIPCHK(hipEventRecord(h.ev_consumed[k & 1], h.stream));
       if (after) after->chunk_done();
     } catch (...) {
@@ -537,7 +528,7 @@ int sg_push(sg_handle* hh, const sg_batch* b) {
     check_batch(b);
     if (b->on_device) {
       BatchView bv = device_view(d, b);
-      push_view(h, bv, n);
+      sg_push_view(h, bv, n);
       return;
     }
     ingest_host(h, b, nullptr);
@@ -597,7 +588,7 @@ int sg_poll(sg_handle* hh, sg_matches* out, int64_t cap, int64_t* n) {
     if (k > 0) {
       // the sg_matches layout is built on the GPU (header fields split into columns, values row-major as in the
       // records), then copied field by field: no host-side transpose
-      egress_init(h);
+      sg_egress_init(h);
       const int ns = out_cols(h.desc);
       const size_t need = (size_t)k * (8 + 8 + 4 + 4 + 4) + (size_t)k * 8 * ns + 1024;
       if (h.eg.cap[0] < (int64_t)need) {
@@ -658,7 +649,7 @@ int sg_push_deliver(sg_handle* hh, const sg_batch* b, const sg_match_columns* ou
         check_batch(b);
         if (b->on_device) {
           BatchView bv = device_view(h.desc, b);
-          push_view(h, bv, b->n);
+          sg_push_view(h, bv, b->n);
           dh.chunk_done();
         } else {
           ingest_host(h, b, &dh);

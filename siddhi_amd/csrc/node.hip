@@ -1,0 +1,1028 @@
+// Node pipeline (sg_node_*): one host process drives every GPU of the node for one partitioned query.
+//
+// The reference runs a partitioned query in one JVM: PartitionStreamReceiver.receive looks each event's key up and
+// hands it to that key's cloned runtime (C/partition/PartitionStreamReceiver.java:80-281, PartitionRuntime.java:
+// 255-308); the matches reach QueryCallback.receive in one ordered stream (C/query/output/callback/
+// QueryCallback.java:52-85).  Here the same contract is met by a pipeline over chunks of the host batch:
+//
+//   route    host thread pool: raw partition-key values -> first-seen dense ids -> shard (GPU) + per-shard id
+//            (router.h); with G > 1 every chunk's rows are scattered, in arrival order, into per-shard pinned
+//            staging (two passes: count per shard, then place), keeping each row's global event index on the host
+//   upload   one copy thread per GPU: the shard's rows of chunk j go to HBM while chunk j-1 computes
+//   compute  one thread per GPU: sg_push_view over the chunk (state carried between chunks = one stream)
+//   deliver  the same thread: the chunk's matches are transposed on the GPU into SoA columns and copied back into
+//            the shard's pinned ring while the next chunk computes
+//   merge    (G > 1) host thread pool: chunk j's shard streams merged into the node's delivery order by (global
+//            trigger, phase, global dense key) -- every trigger's matches come from its key's shard, so the merge
+//            is a k-way interleave by trigger; G = 1: the GPU delivers straight into the caller's columns.
+//
+// Every stage of chunk j overlaps the other stages of chunks j-1 and j+1 (ring depth NODE_RING on the host,
+// two device slots per GPU); no stage blocks another except through those rings.  A handle (sg_handle) is
+// single-threaded: each is only ever driven by its shard's compute thread (and its copy thread's stream).
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "router.h"
+#include "sg_engine.h"
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) throw SgError(SG_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct sg_handle {   // (api.hip's definition)
+  SgHandle h;
+};
+
+namespace {
+
+const int NODE_RING = 3;   // host route/staging slots (chunk j reuses slot j % 3 once chunk j-3 is uploaded+merged)
+const int MAX_GPUS = 16;
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Fixed thread pool: parallel_for(n, fn) runs fn(0..n-1) on the workers and the caller and returns when all are
+// done.  Several coordinator threads may submit at once (their tasks interleave).
+struct Pool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::function<void()>> q;
+  bool stop = false;
+  explicit Pool(int n) {
+    for (int i = 0; i < n; ++i)
+      th.emplace_back([this] {
+        while (true) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || !q.empty(); });
+            if (stop && q.empty()) return;
+            f = std::move(q.back());
+            q.pop_back();
+          }
+          f();
+        }
+      });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  template <class F>
+  void parallel_for(int n, F&& fn) {
+    if (n <= 0) return;
+    std::atomic<int> left(n);
+    std::mutex dm;
+    std::condition_variable dcv;
+    std::exception_ptr err;
+    auto task = [&](int i) {
+      try {
+        fn(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(dm);
+        if (!err) err = std::current_exception();
+      }
+      if (left.fetch_sub(1) == 1) {
+        std::lock_guard<std::mutex> lk(dm);
+        dcv.notify_all();
+      }
+    };
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (int i = n - 1; i >= 1; --i) q.push_back([&task, i] { task(i); });
+    }
+    cv.notify_all();
+    task(0);
+    // help with queued work while waiting (a submitter never idles behind its own tasks)
+    while (left.load() > 0) {
+      std::function<void()> f;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!q.empty()) {
+          f = std::move(q.back());
+          q.pop_back();
+        }
+      }
+      if (f) {
+        f();
+        continue;
+      }
+      std::unique_lock<std::mutex> lk(dm);
+      dcv.wait_for(lk, std::chrono::milliseconds(1), [&] { return left.load() == 0; });
+    }
+    if (err) std::rethrow_exception(err);
+  }
+};
+
+// Pinned host buffer (hipHostMalloc), grow-only.
+struct Pinned {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipHostMalloc(&p, b ? b : 1, hipHostMallocDefault) != hipSuccess) throw SgError(SG_EHIP, "hipHostMalloc (node)");
+    bytes = b;
+  }
+  ~Pinned() {
+    if (p) hipHostFree(p);
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+}  // namespace
+
+// One shard's rows of one chunk, in arrival order (host staging, G > 1).
+struct NodeStage {
+  Pinned ts, key, stream, gidx;
+  Pinned col[SG_MAX_COLS], nul[SG_MAX_COLS];
+};
+
+// One shard's delivered matches (pinned ring of M rows, G > 1).
+struct NodeRing {
+  int64_t M = 0;
+  Pinned trig, ts, key, grp;
+  Pinned col[SG_MAX_SELECT], nul[SG_MAX_SELECT];
+};
+
+struct sg_node {
+  int G = 1;
+  int dev[MAX_GPUS] = {};
+  sg_nfa_desc desc;
+  sg_options opt;
+  sg_handle* h[MAX_GPUS] = {};
+  sg_router* router = nullptr;
+  int threads = 16;
+  int64_t chunk_rows = 0;
+  Pool* pool = nullptr;
+  std::string err;
+  sg_node_stats st;
+  int64_t local_rows[MAX_GPUS] = {};   // rows each shard has seen (its local event index space)
+  int64_t next_index = 0;
+  bool broken = false;
+  // per-GPU device-side ingress slots and copy stream
+  hipStream_t cp[MAX_GPUS] = {};
+  hipEvent_t ev_copied[MAX_GPUS][2] = {}, ev_used[MAX_GPUS][2] = {};
+  SlotPtrs dslot[MAX_GPUS][2];       // device ingress slots (resolved once, before the pipeline's threads start)
+  // host staging: route slot per chunk (G = 1: the routed key column; G > 1: per-shard rows)
+  Pinned keyslot[NODE_RING];
+  std::vector<int32_t> dense_tmp[NODE_RING];
+  NodeStage stage[NODE_RING][MAX_GPUS];
+  NodeRing ring[MAX_GPUS];
+};
+
+namespace {
+
+// What every shard delivers: the caller's columns plus, for the merge, trigger (always) and phase / key when two
+// shards can produce matches for the same trigger (timer passes fan out to every shard).
+struct Want {
+  bool ts, key, grp, col[SG_MAX_SELECT], nul[SG_MAX_SELECT];
+  int ns;
+  int width[SG_MAX_SELECT];
+};
+
+Want want_of(const sg_node& nd, const sg_match_columns* out) {
+  Want w;
+  memset(&w, 0, sizeof(w));
+  const sg_nfa_desc& d = nd.desc;
+  w.ns = d.n_out > 0 ? d.n_out : d.n_select;
+  const bool tie = nd.G > 1 && d.shape != SG_SHAPE_EVERY_NEXT_CMP;
+  w.ts = out->ts != nullptr;
+  w.key = out->key != nullptr || tie;
+  w.grp = out->group != nullptr || tie;
+  for (int k = 0; k < w.ns; ++k) {
+    w.col[k] = out->cols[k] != nullptr;
+    w.nul[k] = out->nulls[k] != nullptr;
+    w.width[k] = sg_col_width(d.n_out > 0 ? d.out_type[k] : d.sel_type[k]);
+  }
+  return w;
+}
+
+// Pipeline state of one sg_node_push call.
+struct Run {
+  sg_node& nd;
+  const sg_node_batch& b;
+  const sg_match_columns* out;
+  int64_t cap;
+  Want w;
+  int64_t nch = 0, C = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool failed = false;
+  int fail_code = 0;
+  std::string fail_msg;
+  int64_t routed = 0;                        // chunks routed (staging complete)
+  int64_t uploaded[MAX_GPUS] = {};           // chunks whose H2D completed, per shard
+  int64_t issued[MAX_GPUS] = {};             // chunks whose H2D was issued (ev_copied recorded)
+  int64_t used[MAX_GPUS] = {};               // chunks whose compute was issued (ev_used recorded)
+  int64_t delivered[MAX_GPUS] = {};          // chunks whose matches are in host memory
+  int64_t merged = 0;                        // chunks merged (G > 1)
+  std::vector<int64_t> dlv_end[MAX_GPUS];    // ring position after chunk j
+  int64_t ring_tail[MAX_GPUS] = {};          // rows of the ring the merge has consumed
+  int64_t out_rows = 0;                      // rows written to the caller's columns
+  // per (chunk, shard): rows, key bound and local index of row 0 (fixed when the chunk is routed)
+  std::vector<int64_t> rows_of, lbase_of;
+  std::vector<int32_t> kb_of;
+  double t_route = 0, t_merge = 0, t_gpu[MAX_GPUS] = {};
+  int64_t h2d_bytes = 0, d2h_bytes = 0;
+
+  Run(sg_node& n, const sg_node_batch& bb, const sg_match_columns* o, int64_t c) : nd(n), b(bb), out(o), cap(c) {}
+
+  void fail(int code, const std::string& m) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!failed) {
+      failed = true;
+      fail_code = code;
+      fail_msg = m;
+    }
+    cv.notify_all();
+  }
+  // wait until pred() or failure; returns false on failure
+  template <class P>
+  bool wait(P pred) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return failed || pred(); });
+    return !failed;
+  }
+  void publish(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      f();
+    }
+    cv.notify_all();
+  }
+  template <class F>
+  void guarded(F&& f) {
+    try {
+      f();
+    } catch (SgError& e) {
+      fail(e.code, e.msg);
+    } catch (std::exception& e) {
+      fail(SG_EINVAL, e.what());
+    }
+  }
+};
+
+int64_t chunk_lo(const Run& r, int64_t j) { return std::min(r.b.n, j * r.C); }
+
+// playback queries with timers (absence states) need every row's clock on every shard
+bool need_clocks(const sg_nfa_desc& d) { return d.playback && d.n_sched > 0; }
+
+// row lo + i starts a new timestamp (the first row of a thread's slice always counts: a repeated clock row at an
+// unchanged time fires nothing)
+inline bool is_clock_point(const Run& r, int64_t lo, int64_t slice_a, int64_t i) {
+  return i == slice_a || r.b.ts[lo + i] != r.b.ts[lo + i - 1];
+}
+
+// ---- route (+ scatter) of chunk j into host slot j % NODE_RING --------------------------------------------------
+void route_chunk(Run& r, int64_t j) {
+  sg_node& nd = r.nd;
+  const sg_nfa_desc& d = nd.desc;
+  const int slot = (int)(j % NODE_RING);
+  const int64_t lo = chunk_lo(r, j), hi = chunk_lo(r, j + 1), n = hi - lo;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, n / 65536 + 1));
+  auto slice = [&](int t, int64_t& a, int64_t& e) {
+    a = n * t / T;
+    e = n * (t + 1) / T;
+  };
+  const int32_t* stream = r.b.stream ? r.b.stream + lo : nullptr;
+  if (!d.partitioned) {   // one runtime: no keys (replicas only, G = 1)
+    int32_t* kd = nd.keyslot[slot].as<int32_t>();
+    nd.pool->parallel_for(T, [&](int t) {
+      int64_t a, e;
+      slice(t, a, e);
+      memset(kd + a, 0, (size_t)(e - a) * 4);
+    });
+    r.rows_of[j] = n;
+    r.kb_of[j] = 1;
+    return;
+  }
+  sg_router* rt = nd.router;
+  const int64_t* raw = r.b.raw_key + lo;
+  int32_t* dense = nd.G == 1 ? nd.keyslot[slot].as<int32_t>() : nd.dense_tmp[slot].data();
+  std::vector<sgr::SliceMiss> miss(T);
+  const int G = nd.G;
+  // playback timers (absence states) fire when the app's clock reaches a row's time, for every key
+  // (TimestampGeneratorImpl.setCurrentTimestamp, C/util/timestamp/TimestampGeneratorImpl.java:106-125): every shard
+  // gets a clock-only row at each new timestamp of a row it does not own, with that row's global index
+  const bool clocks = G > 1 && need_clocks(d);
+  std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(G, 0));
+  // 1. lookups; hits are counted per shard
+  nd.pool->parallel_for(T, [&](int t) {
+    int64_t a, e;
+    slice(t, a, e);
+    sgr::lookup_slice(rt->dict, raw + a, e - a, dense + a, miss[t]);
+    if (stream)   // clock-only rows (stream -1) carry no key: every shard sees them
+      for (int64_t i = a; i < e; ++i)
+        if (stream[i] < 0) dense[i] = -1;
+    if (G > 1) {
+      const int32_t* so = rt->shard_of.data();
+      int64_t* c = cnt[t].data();
+      int64_t bcast = 0;
+      for (int64_t i = a; i < e; ++i) {
+        const int32_t x = dense[i];
+        if (x >= 0) ++c[so[x]];
+        else if (x == -1) ++bcast;
+        if (clocks && x != -1 && is_clock_point(r, lo, a, i)) ++bcast;   // (the owner's share is taken back below)
+      }
+      for (int s = 0; s < G; ++s) c[s] += bcast;
+    }
+  });
+  // 2. new keys, first-seen order
+  std::vector<std::vector<int32_t>> remap(T);
+  bool any = false;
+  for (int t = 0; t < T; ++t) {
+    if (!miss[t].any) continue;
+    any = true;
+    remap[t].resize(miss[t].fresh.size());
+    for (size_t q = 0; q < miss[t].fresh.size(); ++q) remap[t][q] = rt->add_key(miss[t].fresh[q]);
+  }
+  if (any)
+    nd.pool->parallel_for(T, [&](int t) {
+      if (!miss[t].any) return;
+      int64_t a, e;
+      slice(t, a, e);
+      const int32_t* rm = remap[t].data();
+      const int32_t* so = rt->shard_of.data();
+      for (int64_t i = a; i < e; ++i) {
+        const int32_t x = dense[i];
+        if (x >= -1) continue;
+        const int32_t id = rm[-x - 2];
+        dense[i] = id;
+        if (G > 1) ++cnt[t][so[id]];
+      }
+    });
+  if (clocks)   // a clock point was counted for every shard: its owner gets the row itself instead
+    nd.pool->parallel_for(T, [&](int t) {
+      int64_t a, e;
+      slice(t, a, e);
+      const int32_t* so = rt->shard_of.data();
+      for (int64_t i = a; i < e; ++i)
+        if (dense[i] >= 0 && is_clock_point(r, lo, a, i)) --cnt[t][so[dense[i]]];
+    });
+  for (int s = 0; s < G; ++s) r.kb_of[j * G + s] = std::max<int32_t>(1, rt->shard_keys[s]);
+  if (G == 1) {   // dense ids are the shard's ids; clock rows keep -1 (no key)
+    r.rows_of[j] = n;
+    return;
+  }
+  // 3. scatter into per-shard staging, arrival order kept
+  std::vector<std::vector<int64_t>> off(T, std::vector<int64_t>(G, 0));
+  for (int s = 0; s < G; ++s) {
+    int64_t o = 0;
+    for (int t = 0; t < T; ++t) {
+      off[t][s] = o;
+      o += cnt[t][s];
+    }
+    r.rows_of[j * G + s] = o;
+  }
+  const int nc = d.n_cols;
+  int need[SG_MAX_COLS] = {};
+  for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
+  const bool stage_stream = stream != nullptr || clocks;
+  nd.pool->parallel_for(T, [&](int t) {
+    int64_t a, e;
+    slice(t, a, e);
+    const int32_t* so = rt->shard_of.data();
+    const int32_t* lc = rt->local_of.data();
+    int64_t cur[MAX_GPUS];
+    for (int s = 0; s < G; ++s) cur[s] = off[t][s];
+    for (int64_t i = a; i < e; ++i) {
+      const int32_t x = dense[i];
+      const int own = x >= 0 ? so[x] : -1;
+      const bool fan = x < 0 || (clocks && is_clock_point(r, lo, a, i));
+      for (int s = 0; s < G; ++s) {
+        if (s != own && !fan) continue;
+        const bool clock = s != own;   // a clock-only row on a shard that does not own the row
+        NodeStage& S = nd.stage[slot][s];
+        const int64_t p = cur[s]++;
+        S.ts.as<int64_t>()[p] = r.b.ts[lo + i];
+        S.key.as<int32_t>()[p] = clock ? -1 : lc[x];
+        if (stage_stream) S.stream.as<int32_t>()[p] = clock ? -1 : (stream ? stream[i] : 0);
+        S.gidx.as<uint64_t>()[p] = r.b.base_index + (uint64_t)(lo + i);
+        if (clock) {
+          for (int c = 0; c < nc; ++c) {
+            if (!need[c] || !r.b.cols[c]) continue;
+            if (sg_col_width(d.col_type[c]) == 8) S.col[c].as<int64_t>()[p] = 0;
+            else S.col[c].as<int32_t>()[p] = 0;
+            if (r.b.nulls && r.b.nulls[c]) S.nul[c].as<uint8_t>()[p] = 1;
+          }
+          continue;
+        }
+        for (int c = 0; c < nc; ++c) {
+          if (!need[c] || !r.b.cols[c]) continue;
+          if (sg_col_width(d.col_type[c]) == 8) S.col[c].as<int64_t>()[p] = ((const int64_t*)r.b.cols[c])[lo + i];
+          else S.col[c].as<int32_t>()[p] = ((const int32_t*)r.b.cols[c])[lo + i];
+          if (r.b.nulls && r.b.nulls[c]) S.nul[c].as<uint8_t>()[p] = r.b.nulls[c][lo + i];
+        }
+      }
+    }
+  });
+}
+
+// The sg_batch of shard s's rows of chunk j (host memory).
+sg_batch shard_batch(Run& r, int64_t j, int s, const void** cols, const uint8_t** nuls) {
+  sg_node& nd = r.nd;
+  const sg_nfa_desc& d = nd.desc;
+  const int slot = (int)(j % NODE_RING);
+  sg_batch sb;
+  memset(&sb, 0, sizeof(sb));
+  sb.on_device = 0;
+  sb.key_bound = r.kb_of[j * nd.G + s];
+  sb.n = r.rows_of[j * nd.G + s];
+  int need[SG_MAX_COLS] = {};
+  for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
+  if (nd.G == 1) {
+    const int64_t lo = chunk_lo(r, j);
+    sb.base_index = r.b.base_index + (uint64_t)lo;
+    sb.ts = r.b.ts + lo;
+    sb.stream = r.b.stream ? r.b.stream + lo : nullptr;
+    sb.key = nd.keyslot[slot].as<int32_t>();
+    bool nul = false;
+    for (int c = 0; c < d.n_cols; ++c) {
+      cols[c] = (need[c] && r.b.cols[c]) ? (const char*)r.b.cols[c] + (size_t)sg_col_width(d.col_type[c]) * lo : nullptr;
+      nuls[c] = (need[c] && r.b.nulls && r.b.nulls[c]) ? r.b.nulls[c] + lo : nullptr;
+      nul |= nuls[c] != nullptr;
+    }
+    sb.cols = cols;
+    sb.nulls = nul ? nuls : nullptr;
+    return sb;
+  }
+  NodeStage& S = nd.stage[slot][s];
+  sb.base_index = (uint64_t)r.lbase_of[j * nd.G + s];   // local index space: the host maps triggers back through gidx
+  sb.ts = S.ts.as<int64_t>();
+  sb.stream = (r.b.stream || need_clocks(d)) ? S.stream.as<int32_t>() : nullptr;
+  sb.key = S.key.as<int32_t>();
+  bool nul = false;
+  for (int c = 0; c < d.n_cols; ++c) {
+    cols[c] = (need[c] && r.b.cols[c]) ? S.col[c].p : nullptr;
+    nuls[c] = (need[c] && r.b.nulls && r.b.nulls[c]) ? S.nul[c].as<uint8_t>() : nullptr;
+    nul |= nuls[c] != nullptr;
+  }
+  sb.cols = cols;
+  sb.nulls = nul ? nuls : nullptr;
+  return sb;
+}
+
+// ---- per-GPU copy thread: H2D of shard s's rows, two device slots ------------------------------------------------
+void copy_loop(Run& r, int s) {
+  sg_node& nd = r.nd;
+  r.guarded([&] {
+    HIPCHK(hipSetDevice(nd.dev[s]));
+    for (int64_t j = 0; j < r.nch; ++j) {
+      if (!r.wait([&] { return r.routed > j && (j < 2 || r.used[s] >= j - 1); })) return;
+      const int ds = (int)(j & 1);
+      if (j >= 2) HIPCHK(hipStreamWaitEvent(nd.cp[s], nd.ev_used[s][ds], 0));   // device slot free again
+      const void* cols[SG_MAX_COLS];
+      const uint8_t* nuls[SG_MAX_COLS];
+      sg_batch sb = shard_batch(r, j, s, cols, nuls);
+      // (the slot's buffers were reserved for a whole chunk before the pipeline started: no workspace-map access
+      // from this thread)
+      if (sb.n > 0) sg_upload_to(nd.desc, nd.dslot[s][ds], &sb, 0, sb.n, nd.cp[s]);
+      HIPCHK(hipEventRecord(nd.ev_copied[s][ds], nd.cp[s]));
+      r.publish([&] { r.issued[s] = j + 1; });
+      HIPCHK(hipEventSynchronize(nd.ev_copied[s][ds]));
+      int64_t bytes = 8 * sb.n + (sb.stream ? 4 * sb.n : 0) + 4 * sb.n;
+      for (int c = 0; c < nd.desc.n_cols; ++c) {
+        if (sb.cols[c]) bytes += (int64_t)sg_col_width(nd.desc.col_type[c]) * sb.n;
+        if (sb.nulls && sb.nulls[c]) bytes += sb.n;
+      }
+      r.publish([&] { r.uploaded[s] = j + 1; r.h2d_bytes += bytes; });
+    }
+  });
+}
+
+// ---- per-GPU compute + deliver thread --------------------------------------------------------------------------
+struct Dst {   // where delivered rows go: the caller's columns (G = 1) or the shard's ring (G > 1)
+  uint64_t* trig;
+  int64_t* ts;
+  int32_t* key;
+  uint32_t* grp;
+  void* col[SG_MAX_SELECT];
+  uint8_t* nul[SG_MAX_SELECT];
+  int64_t M;   // ring size (rows wrap at M); G = 1: no wrap
+};
+
+// transpose all pending matches of h into staging slot es and copy them to dst rows [pos, pos + k) (mod M)
+void deliver(Run& r, SgHandle& h, const Dst& dst, int64_t pos, int64_t k, int es) {
+  const sg_nfa_desc& d = h.desc;
+  const Want& w = r.w;
+  sg_egress_init(h);
+  const ColLayout L = sg_col_layout(d, k);
+  if (h.eg.cap[es] < (int64_t)L.bytes) {
+    HIPCHK(hipEventSynchronize(h.eg.done[es]));
+    if (h.eg.stage[es]) HIPCHK(hipFree(h.eg.stage[es]));
+    h.eg.stage[es] = nullptr;
+    const size_t want = L.bytes + L.bytes / 2;
+    HIPCHK(hipMalloc(&h.eg.stage[es], want));
+    h.eg.cap[es] = (int64_t)want;
+  }
+  char* st = h.eg.stage[es];
+  HIPCHK(hipStreamWaitEvent(h.stream, h.eg.done[es], 0));
+  sg_launch_to_columns(k, h.out.rec, h.out.stride, L, st, h.stream);
+  HIPCHK(hipEventRecord(h.eg.ready[es], h.stream));
+  h.out.n = 0;   // all consumed (the next push writes after the transpose in stream order)
+  HIPCHK(hipStreamWaitEvent(h.eg.d2h, h.eg.ready[es], 0));
+  int64_t bytes = 0;
+  auto cp = [&](void* base, size_t off, size_t width) {
+    if (!base) return;
+    const int64_t p = dst.M ? pos % dst.M : pos;
+    const int64_t first = dst.M ? std::min<int64_t>(k, dst.M - p) : k;
+    HIPCHK(hipMemcpyAsync((char*)base + width * (size_t)p, st + off, width * (size_t)first, hipMemcpyDeviceToHost, h.eg.d2h));
+    if (first < k)
+      HIPCHK(hipMemcpyAsync(base, st + off + width * (size_t)first, width * (size_t)(k - first), hipMemcpyDeviceToHost,
+                            h.eg.d2h));
+    bytes += (int64_t)(width * (size_t)k);
+  };
+  cp(dst.trig, L.off_trig, 8);
+  if (w.ts) cp(dst.ts, L.off_ts, 8);
+  if (w.key) cp(dst.key, L.off_key, 4);
+  if (w.grp) cp(dst.grp, L.off_grp, 4);
+  for (int c = 0; c < w.ns; ++c) {
+    if (w.col[c]) cp(dst.col[c], L.off_col[c], (size_t)L.width[c]);
+    if (w.nul[c]) cp(dst.nul[c], L.off_nul[c], 1);
+  }
+  HIPCHK(hipEventRecord(h.eg.done[es], h.eg.d2h));
+  std::lock_guard<std::mutex> lk(r.mu);
+  r.d2h_bytes += bytes;
+}
+
+void gpu_loop(Run& r, int s) {
+  sg_node& nd = r.nd;
+  SgHandle& h = nd.h[s]->h;
+  r.guarded([&] {
+    HIPCHK(hipSetDevice(nd.dev[s]));
+    Dst dst;
+    memset(&dst, 0, sizeof(dst));
+    if (nd.G == 1) {
+      dst.trig = r.out->trigger;
+      dst.ts = r.out->ts;
+      dst.key = r.out->key;
+      dst.grp = r.out->group;
+      for (int c = 0; c < r.w.ns; ++c) { dst.col[c] = r.out->cols[c]; dst.nul[c] = r.out->nulls[c]; }
+      dst.M = 0;
+    } else {
+      NodeRing& R = nd.ring[s];
+      dst.trig = R.trig.as<uint64_t>();
+      dst.ts = R.ts.as<int64_t>();
+      dst.key = R.key.as<int32_t>();
+      dst.grp = R.grp.as<uint32_t>();
+      for (int c = 0; c < r.w.ns; ++c) { dst.col[c] = R.col[c].p; dst.nul[c] = R.nul[c].as<uint8_t>(); }
+      dst.M = R.M;
+    }
+    int64_t pos = 0;
+    int es = 0;
+    for (int64_t j = 0; j < r.nch; ++j) {
+      if (!r.wait([&] { return r.issued[s] > j; })) return;
+      const double t0 = now_ms();
+      const int ds = (int)(j & 1);
+      HIPCHK(hipStreamWaitEvent(h.stream, nd.ev_copied[s][ds], 0));
+      const void* cols[SG_MAX_COLS];
+      const uint8_t* nuls[SG_MAX_COLS];
+      sg_batch sb = shard_batch(r, j, s, cols, nuls);
+      int64_t k = 0;
+      if (sb.n > 0) {
+        // the device view of the slot the copy thread filled
+        BatchView bv;
+        memset(&bv, 0, sizeof(bv));
+        bv.n = sb.n;
+        bv.base_index = sb.base_index;
+        bv.key_bound = sb.key_bound;
+        const SlotPtrs& sp = nd.dslot[s][ds];
+        bv.ts = (const int64_t*)sp.ts;
+        bv.stream = sb.stream ? (const int32_t*)sp.stream : nullptr;
+        bv.key = (const int32_t*)sp.key;
+        bv.index = nullptr;
+        for (int c = 0; c < nd.desc.n_cols; ++c) {
+          bv.cols.col[c] = sb.cols[c] ? sp.col[c] : nullptr;
+          bv.cols.nul[c] = (sb.nulls && sb.nulls[c]) ? (const uint8_t*)sp.nul[c] : nullptr;
+        }
+        sg_push_view(h, bv, sb.n);
+        k = h.out.n;
+      }
+      HIPCHK(hipEventRecord(nd.ev_used[s][ds], h.stream));
+      r.publish([&] { r.used[s] = j + 1; });
+      // the previous chunk's matches have landed: hand them to the merge before waiting for ring space
+      if (j > 0) {
+        HIPCHK(hipEventSynchronize(h.eg.done[es ^ 1]));
+        r.publish([&] { r.delivered[s] = j; });
+      }
+      if (k > 0) {
+        if (nd.G == 1) {
+          if (pos + k > r.cap) throw SgError(SG_ECAPACITY, "node: more matches than the output capacity");
+        } else {
+          if (k > dst.M) throw SgError(SG_ECAPACITY, "node: one chunk's matches exceed the shard ring");
+          if (!r.wait([&] { return pos + k - r.ring_tail[s] <= dst.M; })) return;
+        }
+        deliver(r, h, dst, pos, k, es);
+        pos += k;
+        es ^= 1;
+      }
+      r.publish([&] { r.dlv_end[s][j] = pos; });
+      std::lock_guard<std::mutex> lk(r.mu);
+      r.t_gpu[s] += now_ms() - t0;
+    }
+    if (h.eg.d2h) HIPCHK(hipStreamSynchronize(h.eg.d2h));
+    r.publish([&] {
+      r.delivered[s] = r.nch;
+      if (nd.G == 1) r.out_rows = pos;
+    });
+  });
+}
+
+// ---- merge of chunk j (G > 1) ------------------------------------------------------------------------------------
+void merge_chunk(Run& r, int64_t j) {
+  sg_node& nd = r.nd;
+  const int G = nd.G;
+  const int slot = (int)(j % NODE_RING);
+  const Want& w = r.w;
+  int64_t a[MAX_GPUS], e[MAX_GPUS], total = 0;
+  for (int s = 0; s < G; ++s) {
+    a[s] = j ? r.dlv_end[s][j - 1] : 0;
+    e[s] = r.dlv_end[s][j];
+    total += e[s] - a[s];
+  }
+  if (r.out_rows + total > r.cap) throw SgError(SG_ECAPACITY, "node: more matches than the output capacity");
+  if (total == 0) return;
+  // global trigger of ring row p of shard s (its chunk-j local trigger mapped through the staged global indices)
+  auto gtrig = [&](int s, int64_t p) -> uint64_t {
+    const NodeRing& R = nd.ring[s];
+    const uint64_t lt = R.trig.as<uint64_t>()[p % R.M];
+    return nd.stage[slot][s].gidx.as<uint64_t>()[lt - (uint64_t)r.lbase_of[j * G + s]];
+  };
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, total / 131072 + 1));
+  const int64_t lo = chunk_lo(r, j), hi = chunk_lo(r, j + 1);
+  std::vector<std::vector<int64_t>> cut(T + 1, std::vector<int64_t>(G));
+  for (int t = 0; t <= T; ++t)
+    for (int s = 0; s < G; ++s) {
+      if (t == 0) { cut[t][s] = a[s]; continue; }
+      if (t == T) { cut[t][s] = e[s]; continue; }
+      const uint64_t bound = r.b.base_index + (uint64_t)(lo + (hi - lo) * t / T);
+      int64_t x = a[s], y = e[s];
+      while (x < y) {
+        const int64_t m = x + (y - x) / 2;
+        if (gtrig(s, m) < bound) x = m + 1;
+        else y = m;
+      }
+      cut[t][s] = x;
+    }
+  std::vector<int64_t> o0(T + 1, r.out_rows);
+  for (int t = 0; t < T; ++t) {
+    int64_t c = 0;
+    for (int s = 0; s < G; ++s) c += cut[t + 1][s] - cut[t][s];
+    o0[t + 1] = o0[t] + c;
+  }
+  const sg_router* rt = nd.router;
+  nd.pool->parallel_for(T, [&](int t) {
+    int64_t cur[MAX_GPUS], end[MAX_GPUS];
+    uint64_t head[MAX_GPUS];
+    for (int s = 0; s < G; ++s) {
+      cur[s] = cut[t][s];
+      end[s] = cut[t + 1][s];
+      head[s] = cur[s] < end[s] ? gtrig(s, cur[s]) : ~0ull;
+    }
+    auto gkey = [&](int s, int64_t p) -> int64_t {
+      const int32_t lk = nd.ring[s].key.as<int32_t>()[p % nd.ring[s].M];
+      return lk >= 0 ? (int64_t)rt->l2d[s][lk] : -1;
+    };
+    for (int64_t o = o0[t]; o < o0[t + 1]; ++o) {
+      int best = -1;
+      for (int s = 0; s < G; ++s) {
+        if (cur[s] >= end[s]) continue;
+        if (best < 0 || head[s] < head[best]) { best = s; continue; }
+        if (head[s] == head[best] && w.grp) {   // same trigger on two shards: a clock pass -> (phase, key)
+          const NodeRing& A = nd.ring[s];
+          const NodeRing& B = nd.ring[best];
+          const uint32_t pa = A.grp.as<uint32_t>()[cur[s] % A.M] >> 24, pb = B.grp.as<uint32_t>()[cur[best] % B.M] >> 24;
+          if (pa < pb || (pa == pb && gkey(s, cur[s]) < gkey(best, cur[best]))) best = s;
+        }
+      }
+      const int s = best;
+      const NodeRing& R = nd.ring[s];
+      const int64_t p = cur[s] % R.M;
+      if (r.out->trigger) r.out->trigger[o] = head[s];
+      if (r.out->ts) r.out->ts[o] = R.ts.as<int64_t>()[p];
+      if (r.out->key) r.out->key[o] = (int32_t)gkey(s, cur[s]);
+      if (r.out->group) r.out->group[o] = R.grp.as<uint32_t>()[p];
+      for (int c = 0; c < w.ns; ++c) {
+        if (w.col[c]) {
+          if (w.width[c] == 8) ((int64_t*)r.out->cols[c])[o] = R.col[c].as<int64_t>()[p];
+          else ((int32_t*)r.out->cols[c])[o] = R.col[c].as<int32_t>()[p];
+        }
+        if (w.nul[c]) r.out->nulls[c][o] = R.nul[c].as<uint8_t>()[p];
+      }
+      ++cur[s];
+      head[s] = cur[s] < end[s] ? gtrig(s, cur[s]) : ~0ull;
+    }
+  });
+  r.out_rows += total;
+}
+
+void merge_loop(Run& r) {
+  sg_node& nd = r.nd;
+  r.guarded([&] {
+    for (int64_t j = 0; j < r.nch; ++j) {
+      if (!r.wait([&] {
+            for (int s = 0; s < nd.G; ++s)
+              if (r.delivered[s] <= j) return false;
+            return true;
+          }))
+        return;
+      const double t0 = now_ms();
+      merge_chunk(r, j);
+      r.publish([&] {
+        for (int s = 0; s < nd.G; ++s) r.ring_tail[s] = r.dlv_end[s][j];
+        r.merged = j + 1;
+        r.t_merge += now_ms() - t0;
+      });
+    }
+  });
+}
+
+void reserve_all(Run& r) {
+  sg_node& nd = r.nd;
+  const sg_nfa_desc& d = nd.desc;
+  const int64_t C = r.C;
+  int need[SG_MAX_COLS] = {};
+  for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
+  for (int q = 0; q < NODE_RING; ++q) {
+    if (nd.G == 1) nd.keyslot[q].ensure((size_t)C * 4);
+    else {
+      if ((int64_t)nd.dense_tmp[q].size() < C) nd.dense_tmp[q].resize((size_t)C);
+      for (int s = 0; s < nd.G; ++s) {
+        NodeStage& S = nd.stage[q][s];
+        S.ts.ensure((size_t)C * 8);
+        S.key.ensure((size_t)C * 4);
+        S.gidx.ensure((size_t)C * 8);
+        if (r.b.stream || need_clocks(d)) S.stream.ensure((size_t)C * 4);
+        for (int c = 0; c < d.n_cols; ++c) {
+          if (!need[c] || !r.b.cols[c]) continue;
+          S.col[c].ensure((size_t)C * sg_col_width(d.col_type[c]));
+          if (r.b.nulls && r.b.nulls[c]) S.nul[c].ensure((size_t)C);
+        }
+      }
+    }
+  }
+  // device slots of every GPU, sized for a whole chunk (no workspace growth inside the pipeline)
+  for (int s = 0; s < nd.G; ++s) {
+    SgHandle& h = nd.h[s]->h;
+    HIPCHK(hipSetDevice(nd.dev[s]));
+    sg_batch sb;
+    memset(&sb, 0, sizeof(sb));
+    const void* cols[SG_MAX_COLS] = {};
+    const uint8_t* nuls[SG_MAX_COLS] = {};
+    static const char dummy[1] = {0};
+    sb.ts = (const int64_t*)dummy;
+    sb.key = (const int32_t*)dummy;
+    sb.stream = (r.b.stream || (nd.G > 1 && need_clocks(d))) ? (const int32_t*)dummy : nullptr;
+    bool nul = false;
+    for (int c = 0; c < d.n_cols; ++c) {
+      cols[c] = (need[c] && r.b.cols[c]) ? dummy : nullptr;
+      nuls[c] = (need[c] && r.b.nulls && r.b.nulls[c]) ? (const uint8_t*)dummy : nullptr;
+      nul |= nuls[c] != nullptr;
+    }
+    sb.cols = cols;
+    sb.nulls = nul ? nuls : nullptr;
+    for (int ds = 0; ds < 2; ++ds) nd.dslot[s][ds] = sg_reserve_slot(h, &sb, C, ds);
+    HIPCHK(hipStreamSynchronize(h.stream));
+    sg_egress_init(h);
+  }
+  // shard rings: room for two chunks' worth of matches per shard beyond the share of the output capacity
+  if (nd.G > 1) {
+    const int64_t M = std::max<int64_t>(1024, std::min<int64_t>(r.cap, r.cap / nd.G * 2 + 2 * C));
+    for (int s = 0; s < nd.G; ++s) {
+      NodeRing& R = nd.ring[s];
+      R.M = M;
+      R.trig.ensure((size_t)M * 8);
+      if (r.w.ts) R.ts.ensure((size_t)M * 8);
+      if (r.w.key) R.key.ensure((size_t)M * 4);
+      if (r.w.grp) R.grp.ensure((size_t)M * 4);
+      for (int c = 0; c < r.w.ns; ++c) {
+        if (r.w.col[c]) R.col[c].ensure((size_t)M * r.w.width[c]);
+        if (r.w.nul[c]) R.nul[c].ensure((size_t)M);
+      }
+    }
+  }
+}
+
+void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, int64_t cap, int64_t* n_out) {
+  Run r(nd, b, out, cap);
+  r.w = want_of(nd, out);
+  r.C = nd.chunk_rows > 0 ? nd.chunk_rows : std::max<int64_t>(1, std::min<int64_t>(b.n, (int64_t)25 << 20));
+  if (r.C >= (1ll << 30) - 1) throw SgError(SG_EINVAL, "node chunk too large (max 2^30-2 rows)");
+  r.nch = (b.n + r.C - 1) / r.C;
+  for (int s = 0; s < nd.G; ++s) r.dlv_end[s].assign((size_t)r.nch, 0);
+  r.rows_of.assign((size_t)(r.nch * nd.G), 0);
+  r.lbase_of.assign((size_t)(r.nch * nd.G), 0);
+  r.kb_of.assign((size_t)(r.nch * nd.G), 1);
+  const double t0 = now_ms();
+  reserve_all(r);
+  const double t_res = now_ms() - t0;
+  // local index bases of each shard's rows per chunk are fixed as chunks are routed
+  std::vector<std::thread> th;
+  for (int s = 0; s < nd.G; ++s) {
+    th.emplace_back(copy_loop, std::ref(r), s);
+    th.emplace_back(gpu_loop, std::ref(r), s);
+  }
+  if (nd.G > 1) th.emplace_back(merge_loop, std::ref(r));
+  const double t1 = now_ms();
+  r.guarded([&] {
+    for (int64_t j = 0; j < r.nch; ++j) {
+      // slot j % NODE_RING is free once chunk j - NODE_RING is uploaded everywhere (and merged: its gidx)
+      if (!r.wait([&] {
+            if (j < NODE_RING) return true;
+            for (int s = 0; s < nd.G; ++s)
+              if (r.uploaded[s] <= j - NODE_RING) return false;
+            return nd.G == 1 || r.merged > j - NODE_RING;
+          }))
+        return;
+      const double ta = now_ms();
+      route_chunk(r, j);
+      for (int s = 0; s < nd.G; ++s) {
+        r.lbase_of[j * nd.G + s] = nd.local_rows[s];
+        nd.local_rows[s] += r.rows_of[j * nd.G + s];
+      }
+      r.publish([&] {
+        r.routed = j + 1;
+        r.t_route += now_ms() - ta;
+      });
+    }
+  });
+  for (auto& t : th) t.join();
+  for (int s = 0; s < nd.G; ++s) {
+    hipSetDevice(nd.dev[s]);
+    hipStreamSynchronize(nd.h[s]->h.stream);
+    hipStreamSynchronize(nd.cp[s]);
+    if (nd.h[s]->h.eg.d2h) hipStreamSynchronize(nd.h[s]->h.eg.d2h);
+  }
+  if (r.failed) {
+    nd.broken = true;
+    throw SgError(r.fail_code, r.fail_msg);
+  }
+  const double t2 = now_ms();
+  sg_node_stats& st = nd.st;
+  st.total_ms = t2 - t1;
+  st.reserve_ms = t_res;
+  st.route_ms = r.t_route;
+  st.merge_ms = r.t_merge;
+  for (int s = 0; s < nd.G; ++s) st.gpu_ms[s] = r.t_gpu[s];
+  st.rows = b.n;
+  st.matches = r.out_rows;
+  st.chunks = r.nch;
+  st.chunk_rows = r.C;
+  st.h2d_bytes = r.h2d_bytes;
+  st.d2h_bytes = r.d2h_bytes;
+  for (int s = 0; s < nd.G; ++s) st.shard_rows[s] = nd.local_rows[s];
+  *n_out = r.out_rows;
+}
+
+void close_node(sg_node* nd) {
+  for (int s = 0; s < nd->G; ++s) {
+    hipSetDevice(nd->dev[s]);
+    if (nd->h[s]) sg_close(nd->h[s]);
+    if (nd->cp[s]) hipStreamDestroy(nd->cp[s]);
+    for (int k = 0; k < 2; ++k) {
+      if (nd->ev_copied[s][k]) hipEventDestroy(nd->ev_copied[s][k]);
+      if (nd->ev_used[s][k]) hipEventDestroy(nd->ev_used[s][k]);
+    }
+  }
+  if (nd->router) sg_router_close(nd->router);
+  delete nd->pool;
+  delete nd;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const sg_options* opt, int host_threads,
+                 int64_t chunk_rows, sg_node** out) {
+  if (!out || !nfa || n_gpus < 1 || n_gpus > MAX_GPUS || host_threads < 0 || chunk_rows < 0) return SG_EINVAL;
+  *out = nullptr;
+  if (!nfa->partitioned && n_gpus != 1) return SG_EUNSUPPORTED;   // one runtime: replicas only
+  sg_node* nd = new sg_node();
+  nd->G = n_gpus;
+  nd->desc = *nfa;
+  if (opt) nd->opt = *opt;
+  else memset(&nd->opt, 0, sizeof(nd->opt));
+  nd->opt.no_carry = 0;       // chunks are consecutive pushes of one stream
+  nd->opt.ingress_rows = -1;  // (the node does its own chunking)
+  nd->threads = host_threads ? host_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nd->chunk_rows = chunk_rows;
+  memset(&nd->st, 0, sizeof(nd->st));
+  int rc = SG_OK;
+  for (int s = 0; s < n_gpus && rc == SG_OK; ++s) {
+    nd->dev[s] = devices ? devices[s] : 0;
+    rc = sg_open(nd->dev[s], &nd->desc, &nd->opt, &nd->h[s]);
+    if (rc != SG_OK) {
+      nd->err = nd->h[s] ? sg_last_error(nd->h[s]) : "sg_open failed";
+      break;
+    }
+    if (hipSetDevice(nd->dev[s]) != hipSuccess || hipStreamCreateWithFlags(&nd->cp[s], hipStreamNonBlocking) != hipSuccess) {
+      rc = SG_EHIP;
+      nd->err = "node: stream creation failed";
+      break;
+    }
+    for (int k = 0; k < 2 && rc == SG_OK; ++k)
+      if (hipEventCreateWithFlags(&nd->ev_copied[s][k], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&nd->ev_used[s][k], hipEventDisableTiming) != hipSuccess) {
+        rc = SG_EHIP;
+        nd->err = "node: event creation failed";
+      }
+  }
+  if (rc == SG_OK) rc = sg_router_open(n_gpus, nd->threads, &nd->router);
+  if (rc == SG_OK) nd->pool = new Pool(std::max(0, nd->threads - 1));
+  if (rc != SG_OK) {
+    std::string e = nd->err;
+    close_node(nd);
+    (void)e;
+    return rc;
+  }
+  *out = nd;
+  return SG_OK;
+}
+
+int sg_node_push(sg_node* nd, const sg_node_batch* b, const sg_match_columns* out, int64_t cap, int64_t* n) {
+  if (!nd || !b || !out || cap < 0) return SG_EINVAL;
+  int64_t got = 0;
+  try {
+    if (nd->broken) throw SgError(SG_EINVAL, "node: a failed push left it inconsistent; call sg_node_reset");
+    if (b->n < 0 || (b->n && !b->ts)) throw SgError(SG_EINVAL, "node batch without timestamps");
+    if (nd->desc.partitioned && b->n && !b->raw_key) throw SgError(SG_EINVAL, "partitioned query without raw keys");
+    if (!out->trigger) throw SgError(SG_EINVAL, "node delivery needs the trigger column");
+    if (b->n == 0) {
+      if (n) *n = 0;
+      return SG_OK;
+    }
+    if (b->base_index != (uint64_t)nd->next_index && nd->next_index != 0)
+      throw SgError(SG_EINVAL, "node batches must continue the stream's event index");
+    run_push(*nd, *b, out, cap, &got);
+    nd->next_index = (int64_t)(b->base_index + (uint64_t)b->n);
+  } catch (SgError& e) {
+    nd->err = e.msg;
+    if (n) *n = got;
+    return e.code;
+  } catch (std::exception& e) {
+    nd->err = e.what();
+    nd->broken = true;
+    return SG_EINVAL;
+  }
+  if (n) *n = got;
+  return SG_OK;
+}
+
+int sg_node_reset(sg_node* nd) {
+  if (!nd) return SG_EINVAL;
+  int rc = SG_OK;
+  for (int s = 0; s < nd->G; ++s) {
+    const int x = sg_reset(nd->h[s]);
+    if (x != SG_OK) rc = x;
+    nd->local_rows[s] = 0;
+  }
+  if (nd->router) sg_router_close(nd->router);
+  nd->router = nullptr;
+  const int x = sg_router_open(nd->G, nd->threads, &nd->router);
+  if (x != SG_OK) rc = x;
+  nd->next_index = 0;
+  nd->broken = rc != SG_OK;
+  return rc;
+}
+
+int sg_node_stats_get(const sg_node* nd, sg_node_stats* st) {
+  if (!nd || !st) return SG_EINVAL;
+  *st = nd->st;
+  return SG_OK;
+}
+
+int sg_node_keys(const sg_node* nd, int64_t* n_keys) {
+  if (!nd || !n_keys) return SG_EINVAL;
+  return sg_router_keys(nd->router, n_keys, -1, nullptr);
+}
+
+int sg_node_close(sg_node* nd) {
+  if (!nd) return SG_EINVAL;
+  close_node(nd);
+  return SG_OK;
+}
+
+const char* sg_node_last_error(const sg_node* nd) { return nd ? nd->err.c_str() : "null node"; }
+
+}  // extern "C"

@@ -1,16 +1,20 @@
-// Host partition router (part of libsiddhi_gpu.so; plain C++, no device code).
+// Host partition router and match-stream merge (part of libsiddhi_gpu.so; plain C++, no device code).
 //
-// Replaces the per-event key lookup of PartitionStreamReceiver.receive / PartitionRuntime.cloneIfNotExist
-// (C/partition/PartitionStreamReceiver.java:80-275, C/partition/PartitionRuntime.java:255-308) for SoA
-// batches: raw partition-key values are dictionary-encoded into dense ids in first-seen order -- the order the
-// reference clones per-key runtimes and registers their schedulers in -- and every key is assigned to one shard
-// (GPU) by mix64(dense id) mod n_shards, with a dense id of its own inside the shard (first-seen order there too),
-// so each GPU's key space stays dense.
+// Router: replaces the per-event key lookup of PartitionStreamReceiver.receive / PartitionRuntime.cloneIfNotExist
+// (C/partition/PartitionStreamReceiver.java:80-275, C/partition/PartitionRuntime.java:255-308) for SoA batches:
+// raw partition-key values are dictionary-encoded into dense ids in first-seen order -- the order the reference
+// clones per-key runtimes and registers their schedulers in -- and every key is assigned to one shard (GPU) by
+// mix64(dense id) mod n_shards, with a dense id of its own inside the shard (first-seen order there too), so each
+// GPU's key space stays dense.
 //
-// One call routes a batch with T threads in two parallel passes and one serial merge:
-//   1. each thread numbers the keys of its contiguous slice in first-arrival order (one hash lookup per row);
-//   2. the slices' keys are merged into the dictionary slice by slice (so new ids follow first arrival);
-//   3. each thread maps its slice-local ids to dictionary ids (array lookups).
+// One call routes a batch with T threads:
+//   1. each thread looks its contiguous slice up in the dictionary (read-only, shared); keys it does not hold get
+//      slice-local numbers in first-arrival order -- once a stream's keys have been seen this is the only pass;
+//   2. the slices' new keys are merged into the dictionary slice by slice (so new ids follow first arrival);
+//   3. rows of new keys get their dictionary ids; shard / per-shard ids are array lookups.
+//
+// Merge: the per-GPU match streams (each in delivery order) merged into the node's delivery order by (trigger,
+// phase, key) -- the order QueryCallback.receive sees on one host (C/query/output/callback/QueryCallback.java:52-85).
 #include <stdint.h>
 #include <string.h>
 
@@ -21,83 +25,19 @@
 #include <vector>
 
 #include "../../include/siddhi_gpu.h"
+#include "router.h"
 
 namespace {
 
-inline uint64_t mix64(uint64_t x) {   // splitmix64 step (same as siddhi_amd/router.py mix64)
-  x += 0x9E3779B97F4A7C15ull;
-  x ^= x >> 30;
-  x *= 0xbf58476d1ce4e5b9ull;
-  x ^= x >> 27;
-  x *= 0x94d049bb133111ebull;
-  x ^= x >> 31;
-  return x;
+template <class F>
+void run_threads(int T, F&& f) {
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back(f, t);
+  f(0);
+  for (auto& th : pool) th.join();
 }
 
-// open-addressing map int64 raw key -> int32 value (linear probing, power-of-two capacity, key and value in one
-// 16-byte slot so a probe touches one cache line)
-struct KeyMap {
-  struct Slot {
-    int64_t key;
-    int32_t val;   // -1 = empty
-    int32_t pad;
-  };
-  std::vector<Slot> slots;
-  size_t mask = 0, size = 0;
-  int shift = 64;
-  void init(size_t cap_pow2) {
-    slots.assign(cap_pow2, Slot{0, -1, 0});
-    mask = cap_pow2 - 1;
-    size = 0;
-    shift = 64;
-    for (size_t c = cap_pow2; c > 1; c >>= 1) --shift;
-  }
-  // Fibonacci hashing: one multiply, the top bits index the table
-  size_t home(int64_t k) const { return (size_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> shift) & mask; }
-  void prefetch(int64_t k) const { __builtin_prefetch(&slots[home(k)]); }
-  int32_t find(int64_t k) const {
-    size_t i = home(k);
-    while (true) {
-      const Slot& s = slots[i];
-      if (s.val < 0) return -1;
-      if (s.key == k) return s.val;
-      i = (i + 1) & mask;
-    }
-  }
-  // returns the existing value, or inserts v and returns -1
-  int32_t insert(int64_t k, int32_t v) {
-    if ((size + 1) * 2 > slots.size()) grow();
-    size_t i = home(k);
-    while (true) {
-      Slot& s = slots[i];
-      if (s.val < 0) {
-        s.key = k;
-        s.val = v;
-        ++size;
-        return -1;
-      }
-      if (s.key == k) return s.val;
-      i = (i + 1) & mask;
-    }
-  }
-  void grow() {
-    std::vector<Slot> old;
-    old.swap(slots);
-    init(std::max<size_t>(old.size() * 2, 1024));
-    for (const Slot& s : old)
-      if (s.val >= 0) insert(s.key, s.val);
-  }
-};
-
 }  // namespace
-
-struct sg_router {
-  int n_shards = 1, threads = 1;
-  KeyMap dict;                         // raw -> dense id
-  std::vector<int32_t> shard_of, local_of;
-  std::vector<int32_t> shard_keys;     // keys per shard
-  std::string err;
-};
 
 extern "C" {
 
@@ -109,6 +49,7 @@ int sg_router_open(int n_shards, int threads, sg_router** out) {
   r->threads = threads ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
   r->dict.init(1 << 12);
   r->shard_keys.assign(n_shards, 0);
+  r->l2d = std::vector<sgr::BlockVec>(n_shards);
   *out = r;
   return SG_OK;
 }
@@ -122,74 +63,57 @@ int sg_router_route(sg_router* r, int64_t n, const int64_t* raw, int32_t* dense,
     dense = tmp.data();
   }
   const int T = (int)std::max<int64_t>(1, std::min<int64_t>(r->threads, n / 65536 + 1));
-  std::vector<std::vector<int64_t>> keys_of(T);   // per slice: its distinct keys in first-arrival order
-  std::vector<std::vector<int32_t>> remap(T);     // per slice: slice-local id -> dictionary id
+  std::vector<sgr::SliceMiss> miss(T);
   auto slice = [&](int t, int64_t& lo, int64_t& hi) {
     lo = n * t / T;
     hi = n * (t + 1) / T;
   };
-  // 1. every slice numbers its own keys in first-arrival order (one hash lookup per row; slots of the next 16
-  //    rows are prefetched) and writes those slice-local ids
-  auto pass1 = [&](int t) {
-    int64_t lo, hi;
-    slice(t, lo, hi);
-    KeyMap m;
-    m.init(1 << 12);
-    std::vector<int64_t>& ks = keys_of[t];
-    constexpr int G = 16;
+  // shard / per-shard ids of resolved rows (one pass when every key is known)
+  auto finish = [&](int64_t lo, int64_t hi, bool only_new) {
+    const int32_t* so = r->shard_of.data();
+    const int32_t* lc = r->local_of.data();
     for (int64_t i = lo; i < hi; ++i) {
-      if (i + G < hi) m.prefetch(raw[i + G]);
-      const int64_t k = raw[i];
-      const int32_t nid = (int32_t)ks.size();
-      const int32_t id = m.insert(k, nid);
-      if (id < 0) {
-        ks.push_back(k);
-        dense[i] = nid;
-      } else {
-        dense[i] = id;
-      }
+      const int32_t id = dense[i];
+      if (only_new && id >= 0) continue;
+      if (id < 0) continue;
+      if (shard) shard[i] = so[id];
+      if (local) local[i] = lc[id];
     }
   };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < T; ++t) pool.emplace_back(pass1, t);
-  pass1(0);
-  for (auto& th : pool) th.join();
-  pool.clear();
-  // 2. serial merge, slice by slice: dictionary ids in first-seen order (new keys get the next id, shard
-  //    mix64(id) mod n_shards and the next dense id of that shard)
+  // 1. dictionary lookups (read-only)
+  run_threads(T, [&](int t) {
+    int64_t lo, hi;
+    slice(t, lo, hi);
+    sgr::lookup_slice(r->dict, raw + lo, hi - lo, dense + lo, miss[t]);
+    finish(lo, hi, false);
+  });
+  // 2. serial merge of new keys, slice by slice (first-seen order)
+  std::vector<std::vector<int32_t>> remap(T);
+  bool any = false;
   for (int t = 0; t < T; ++t) {
-    remap[t].resize(keys_of[t].size());
-    for (size_t j = 0; j < keys_of[t].size(); ++j) {
-      const int64_t k = keys_of[t][j];
-      const int32_t id = (int32_t)r->shard_of.size();
-      const int32_t old = r->dict.insert(k, id);
-      if (old >= 0) {
-        remap[t][j] = old;
-        continue;
-      }
-      remap[t][j] = id;
-      const int32_t s = (int32_t)(mix64((uint64_t)id) % (uint64_t)r->n_shards);
-      r->shard_of.push_back(s);
-      r->local_of.push_back(r->shard_keys[s]++);
-    }
+    if (!miss[t].any) continue;
+    any = true;
+    remap[t].resize(miss[t].fresh.size());
+    for (size_t j = 0; j < miss[t].fresh.size(); ++j) remap[t][j] = r->add_key(miss[t].fresh[j]);
   }
-  // 3. slice-local ids -> dictionary ids (and shard / per-shard ids): array lookups only
-  auto pass3 = [&](int t) {
+  if (!any) return SG_OK;
+  // 3. rows of new keys
+  run_threads(T, [&](int t) {
+    if (!miss[t].any) return;
     int64_t lo, hi;
     slice(t, lo, hi);
     const int32_t* rm = remap[t].data();
     const int32_t* so = r->shard_of.data();
     const int32_t* lc = r->local_of.data();
     for (int64_t i = lo; i < hi; ++i) {
-      const int32_t id = rm[dense[i]];
+      const int32_t x = dense[i];
+      if (x >= 0) continue;
+      const int32_t id = rm[-x - 2];
       dense[i] = id;
       if (shard) shard[i] = so[id];
       if (local) local[i] = lc[id];
     }
-  };
-  for (int t = 1; t < T; ++t) pool.emplace_back(pass3, t);
-  pass3(0);
-  for (auto& th : pool) th.join();
+  });
   return SG_OK;
 }
 
@@ -200,8 +124,88 @@ int sg_router_keys(const sg_router* r, int64_t* n_keys, int32_t shard, int64_t* 
   return SG_OK;
 }
 
+int sg_router_dense_ids(const sg_router* r, int32_t shard, int32_t* dense_of_local, int64_t cap) {
+  if (!r || shard < 0 || shard >= r->n_shards || cap < 0) return SG_EINVAL;
+  const sgr::BlockVec& v = r->l2d[shard];
+  if (cap < (int64_t)v.size()) return SG_ECAPACITY;
+  for (size_t i = 0; i < v.size(); ++i) dense_of_local[i] = v[i];
+  return SG_OK;
+}
+
 int sg_router_close(sg_router* r) {
   delete r;
+  return SG_OK;
+}
+
+// K-way merge of match runs (each already in delivery order) into the node's delivery order: by trigger, then
+// phase (group >> 24: a clock pass's timer emissions before the event's own states), then dense key (timer passes
+// fire key by key in registration = first-seen order, C/util/timestamp/TimestampGeneratorImpl.java:106-125);
+// ties keep run order.  out_src[i] = index of the i-th merged row in the concatenation of the runs.  Parallel
+// over trigger ranges: every thread takes the rows whose trigger lies in its range from every run (boundaries by
+// binary search; equal triggers never straddle two threads).
+int sg_merge_order(int n_runs, const int64_t* run_len, const uint64_t* const* trigger, const uint32_t* const* group,
+                   const int32_t* const* key, int threads, int64_t* out_src) {
+  if (n_runs < 0 || (n_runs && (!run_len || !trigger)) || !out_src) return SG_EINVAL;
+  std::vector<int64_t> base(n_runs + 1, 0);
+  for (int r = 0; r < n_runs; ++r) {
+    if (run_len[r] < 0 || (run_len[r] && !trigger[r])) return SG_EINVAL;
+    base[r + 1] = base[r] + run_len[r];
+  }
+  const int64_t total = base[n_runs];
+  if (total == 0) return SG_OK;
+  for (int r = 0; r < n_runs; ++r)   // every run must be ordered by trigger
+    for (int64_t i = 1; i < run_len[r]; ++i)
+      if (trigger[r][i] < trigger[r][i - 1]) return SG_EORDER;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads > 0 ? threads : 1, total / 262144 + 1));
+  // splitters: triggers of the longest run at equal positions
+  int big = 0;
+  for (int r = 1; r < n_runs; ++r) if (run_len[r] > run_len[big]) big = r;
+  std::vector<uint64_t> split(T + 1);
+  split[0] = 0;
+  for (int t = 1; t < T; ++t) split[t] = trigger[big][run_len[big] * t / T];
+  std::vector<std::vector<int64_t>> lo(T + 1, std::vector<int64_t>(n_runs));
+  for (int t = 0; t <= T; ++t)
+    for (int r = 0; r < n_runs; ++r) {
+      if (t == 0) { lo[t][r] = 0; continue; }
+      if (t == T) { lo[t][r] = run_len[r]; continue; }
+      lo[t][r] = std::lower_bound(trigger[r], trigger[r] + run_len[r], split[t]) - trigger[r];
+    }
+  std::vector<int64_t> out0(T + 1, 0);
+  for (int t = 0; t < T; ++t) {
+    int64_t c = 0;
+    for (int r = 0; r < n_runs; ++r) c += std::max<int64_t>(0, lo[t + 1][r] - lo[t][r]);
+    out0[t + 1] = out0[t] + c;
+  }
+  auto less = [&](int ra, int64_t ia, int rb, int64_t ib) {
+    const uint64_t ta = trigger[ra][ia], tb = trigger[rb][ib];
+    if (ta != tb) return ta < tb;
+    const uint32_t pa = group && group[ra] ? group[ra][ia] >> 24 : 0, pb = group && group[rb] ? group[rb][ib] >> 24 : 0;
+    if (pa != pb) return pa < pb;
+    const int32_t ka = key && key[ra] ? key[ra][ia] : 0, kb = key && key[rb] ? key[rb][ib] : 0;
+    if (ka != kb) return ka < kb;
+    return ra < rb;
+  };
+  run_threads(T, [&](int t) {
+    std::vector<int64_t> cur(lo[t]), end(lo[t + 1]);
+    int64_t o = out0[t];
+    while (true) {
+      int best = -1;
+      for (int r = 0; r < n_runs; ++r)
+        if (cur[r] < end[r] && (best < 0 || less(r, cur[r], best, cur[best]))) best = r;
+      if (best < 0) break;
+      // the whole stretch of `best` that stays ahead of every other run's head goes out in one go
+      int64_t i = cur[best];
+      do {
+        out_src[o++] = base[best] + i;
+        ++i;
+        bool ahead = i < end[best];
+        for (int r = 0; ahead && r < n_runs; ++r)
+          if (r != best && cur[r] < end[r] && !less(best, i, r, cur[r])) ahead = false;
+        if (!ahead) break;
+      } while (true);
+      cur[best] = i;
+    }
+  });
   return SG_OK;
 }
 

@@ -186,6 +186,31 @@ void sg_every_absent_restore(SgHandle* h, SnapR& r);
 void sg_general_snapshot(SgHandle* h, SnapW& w);
 void sg_general_restore(SgHandle* h, SnapR& r);
 
+// Ingress / egress building blocks of the C-ABI (api.hip), shared with the node pipeline (node.hip).
+// Device buffers of one ingress slot (resolved on the calling thread: the workspace map is not thread-safe).
+struct SlotPtrs {
+  void* ts = nullptr;
+  void* stream = nullptr;
+  void* key = nullptr;
+  void* index = nullptr;
+  void* col[SG_MAX_COLS] = {};
+  void* nul[SG_MAX_COLS] = {};
+};
+struct ColLayout {   // SoA staging layout of `cap` delivered matches
+  int ns;
+  int32_t width[SG_MAX_SELECT];
+  size_t off_trig, off_ts, off_key, off_grp, off_col[SG_MAX_SELECT], off_nul[SG_MAX_SELECT], bytes;
+};
+int sg_col_width(int type);
+SlotPtrs sg_reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int slot);
+// copy rows [lo, lo + cnt) of a host batch into a slot on stream `st` (touches no handle state: any thread)
+BatchView sg_upload_to(const sg_nfa_desc& d, const SlotPtrs& p, const sg_batch* b, int64_t lo, int64_t cnt,
+                       hipStream_t st);
+void sg_push_view(SgHandle& h, BatchView& bv, int64_t n);   // one push of rows in HBM (engine route + select)
+ColLayout sg_col_layout(const sg_nfa_desc& d, int64_t cap);
+void sg_launch_to_columns(int64_t n, const char* rec, int stride, const ColLayout& L, char* stage, hipStream_t st);
+void sg_egress_init(SgHandle& h);
+
 void sg_run_every_next(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_f32(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_f64(SgHandle* h, const BatchView& bv, int64_t n);

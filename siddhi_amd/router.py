@@ -79,15 +79,16 @@ class RankShard:
         return out
 
 
-def merge(parts):
-    """Merge per-rank Outputs (each already in delivery order) into the node's delivery order."""
+def merge(parts, threads: int = 16):
+    """Merge per-rank Outputs (each already in delivery order) into the node's delivery order: the native k-way
+    merge sg_merge_order (csrc/router.cpp) by (trigger, phase, dense key), ties in rank order."""
+    from ._native import merge_order
     from .runtime import Outputs
     if not parts:
         raise ValueError("nothing to merge")
+    order = merge_order([p.trigger for p in parts], [p.group for p in parts], [p.key for p in parts], threads)
     cat = Outputs(*[np.concatenate([getattr(p, f) for p in parts]) for f in
                     ("trigger", "ts", "key", "group", "vals", "vnull")])
-    phase = (cat.group >> np.uint32(24)).astype(np.uint64)
-    order = np.lexsort((np.arange(len(cat)), cat.key.astype(np.int64), phase, cat.trigger))
     return Outputs(*[getattr(cat, f)[order] for f in ("trigger", "ts", "key", "group", "vals", "vnull")])
 
 

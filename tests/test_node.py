@@ -1,0 +1,139 @@
+"""The node pipeline (sg_node_*, siddhi_amd/csrc/node.hip) against the oracle: raw host rows -> native router
+(first-seen dense ids, shard mix64(id) mod G) -> one thread per GPU with chunked H2D / kernels / D2H -> native merge
+into the node's delivery order (PartitionStreamReceiver.receive(Event[]) feeding per-key runtimes and one ordered
+QueryCallback stream, C/partition/PartitionStreamReceiver.java:177-221, C/partition/PartitionRuntime.java:255-308,
+C/query/output/callback/QueryCallback.java:52-85).  G > 1 runs several shards on cuda:0 (one handle each)."""
+import numpy as np
+import pytest
+
+from oracle import OracleEngine
+from parity_util import assert_same, context, dense_first_seen, run_engine, synth_batch
+from siddhi_amd import synth
+from siddhi_amd.runtime import Batch, Outputs
+
+pytestmark = pytest.mark.gpu
+
+ABSENT_Q = ("@app:playback define stream S (id long, symbol string, v int, w int); "
+            "partition with (symbol of S) begin @info(name='q') "
+            "from every e1=S[v>700] -> not S[v<e1.v] for 30 milliseconds "
+            "select e1.id as i1, e1.v as v1 insert into M; end;")
+
+
+def node_outputs(nfa, sink, n):
+    """Delivered SoA columns -> Outputs (vals as the bit patterns sg_poll reports)."""
+    from siddhi_amd._native import column_dtypes
+    dts = column_dtypes(nfa)
+    vals = np.zeros((n, max(len(dts), 1)), np.int64)
+    vnull = np.zeros((n, max(len(dts), 1)), np.uint8)
+    for k, dt in enumerate(dts):
+        c = sink.cols[k][:n]
+        if np.dtype(dt) == np.float32:
+            vals[:, k] = c.view(np.uint32).astype(np.int64)
+        elif np.dtype(dt).itemsize == 4:
+            vals[:, k] = c.view(np.int32).astype(np.int64)
+        else:
+            vals[:, k] = c.view(np.int64)
+        vnull[:, k] = sink.nulls[k][:n]
+    ns = len(dts)
+    return Outputs(sink.trigger[:n].copy(), sink.ts[:n].copy(), sink.key[:n].copy(), sink.group[:n].copy(),
+                   vals[:, :ns], vnull[:, :ns])
+
+
+def run_node(query, pushes, n_gpus, chunk_rows, raw_of, threads=4, cap=None, pinned=False):
+    """Push host batches (their .key = synthetic key ids, sent as raw 64-bit symbols) through one node."""
+    from siddhi_amd import _native as N
+    nfa = __import__("siddhi_amd.lowering", fromlist=["lower"]).lower(context(query))
+    node = N.Node(N.build_desc(nfa), n_gpus=n_gpus, devices=[0] * n_gpus, threads=threads, chunk_rows=chunk_rows)
+    outs = []
+    for b in pushes:
+        keep = []
+        ts = np.ascontiguousarray(b.ts, np.int64)
+        raw = np.ascontiguousarray(raw_of(b.key), np.int64)
+        st = None if b.stream is None else np.ascontiguousarray(b.stream, np.int32)
+        cols = [np.ascontiguousarray(c) for c in b.cols]
+        nul = [None if x is None else np.ascontiguousarray(x, np.uint8) for x in b.nulls]
+        keep += [ts, raw, st] + cols + nul
+        nb = N.make_node_batch(b.n, b.base_index, ts.ctypes.data, 0 if st is None else st.ctypes.data,
+                               raw.ctypes.data, [c.ctypes.data for c in cols],
+                               [0 if x is None else x.ctypes.data for x in nul], keep)
+        sink = N.ColumnSink(nfa, cap or (4 * b.n + 16), pinned=pinned)
+        got = node.push(nb, sink.struct, sink.cap)
+        outs.append(node_outputs(nfa, sink, got))
+    st = node.stats()
+    node.close()
+    return Outputs(*[np.concatenate([getattr(o, f) for o in outs]) for f in
+                     ("trigger", "ts", "key", "group", "vals", "vnull")]), st
+
+
+def _want(query, b):
+    d = Batch(b.n, b.base_index, b.ts, b.stream, dense_first_seen(b.key), b.cols, b.nulls)
+    return run_engine(OracleEngine, query, [d])
+
+
+def _split(b, cuts):
+    out = []
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        out.append(Batch(hi - lo, b.base_index + lo, b.ts[lo:hi], b.stream[lo:hi], b.key[lo:hi],
+                         [c[lo:hi] for c in b.cols], [None if x is None else x[lo:hi] for x in b.nulls]))
+    return out
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cfg,n,keys,rate,gpus,chunk", [
+    ("C2", 200_000, 1_000, 100, 1, 30_000), ("C2", 200_000, 1_000, 100, 2, 45_000), ("C2", 200_000, 400, 100, 3, 0),
+    ("C5", 300_000, 20_000, 1_000, 2, 70_000), ("C3b", 200_000, 400, 1_000, 2, 50_000),
+    ("C3c", 200_000, 400, 100, 2, 60_000), ("C3c", 150_000, 400, 100, 1, 40_000)])
+def test_node_matches_oracle(cfg, n, keys, rate, gpus, chunk):
+    b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
+    want = _want(synth.QUERIES[cfg], b)
+    assert len(want) > 0
+    got, st = run_node(synth.QUERIES[cfg], [b], gpus, chunk, synth.raw_symbols)
+    assert st["matches"] == len(want)
+    assert sum(st["shard_rows"][:gpus]) == n
+    assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_node_pushes_carry_state(gpus):
+    """Consecutive node pushes are one stream (per-key state and the key dictionary carry over)."""
+    cfg = "C2"
+    b = synth_batch(cfg, 0, 240_000, keys=800, rate=100)
+    want = _want(synth.QUERIES[cfg], b)
+    got, _ = run_node(synth.QUERIES[cfg], _split(b, [0, 50_000, 50_001, 170_000, 240_000]), gpus, 40_000,
+                      synth.raw_symbols)
+    assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+def test_node_pinned_output_and_capacity():
+    from siddhi_amd._native import SgError
+    cfg = "C2"
+    b = synth_batch(cfg, 0, 100_000, keys=500, rate=100)
+    want = _want(synth.QUERIES[cfg], b)
+    got, _ = run_node(synth.QUERIES[cfg], [b], 2, 30_000, synth.raw_symbols, pinned=True)
+    assert_same(got, want)
+    with pytest.raises(SgError) as ei:
+        run_node(synth.QUERIES[cfg], [b], 1, 30_000, synth.raw_symbols, cap=len(want) // 2)
+    assert ei.value.code == -3
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cfg,n", [("C1", 100_000), ("C4", 200_000)])
+def test_node_unpartitioned_single_gpu(cfg, n):
+    b = synth_batch(cfg, 0, n)
+    want = run_engine(OracleEngine, synth.QUERIES[cfg], [b])
+    got, _ = run_node(synth.QUERIES[cfg], [b], 1, 64_000, lambda k: np.zeros(len(k), np.int64))
+    assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus", [1, 2, 3])
+def test_node_partitioned_absence_clock_fanout(gpus):
+    """Playback timers of every key fire on every row's clock: with G > 1 each shard gets clock rows for the rows
+    it does not own, and timer emissions of one clock advance merge across shards by (phase, first-seen key)."""
+    b = synth_batch("C3b", 0, 60_000, keys=200, rate=10)
+    want = _want(ABSENT_Q, b)
+    assert len(want) > 100
+    got, _ = run_node(ABSENT_Q, [b], gpus, 25_000, synth.raw_symbols)
+    assert_same(got, want)
