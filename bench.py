@@ -50,6 +50,27 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 DEFAULT_PMC = os.path.join(ROOT, "profiles", "r02", "c2_pmc.json")
 
 
+def barrier():
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.barrier()
+
+
+def reduce_max(x):
+    if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_sum(x):
+    if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM)
+    return float(t.item())
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -193,81 +214,84 @@ def synth_columns(cfg, rank, n, keys, rate, dev):
     return g, key, cols
 
 
-def whole_node(cfg, rank, n, keys, rate, steps, dev, threads, parts=4):
-    """SURVEY §8d whole-node rate on this rank's stream: raw host columns -> native router -> sg_push_deliver
-    (pinned H2D in chunks, kernels, GPU-transposed SoA match columns D2H into pinned memory, overlapped).  The
-    stream is fed as `parts` consecutive sub-batches (carried state makes that identical to one push): the router
-    encodes part p+1 on host threads while part p is in flight on the GPU."""
-    from concurrent.futures import ThreadPoolExecutor
-    g, key, cols = synth_columns(cfg, rank, n, keys, rate, dev)
+def host_stream(cfg, total, keys, rate, dev, gen_rows=50_000_000):
+    """The config's stream as the host receives it, in pinned memory: ts, the raw 64-bit partition-key value per
+    row (synth.raw_symbols, never a dense id) and the query's typed columns.  Generated in HBM chunk by chunk and
+    copied down (outside any timed region)."""
     keep = []
 
-    def pinned(a, dtype=None):
-        a = np.ascontiguousarray(a if dtype is None else a.astype(dtype))
-        p = N.PinnedArray(len(a), a.dtype)
-        p.array[:] = a
+    def pinned(n, dt):
+        p = N.PinnedArray(n, dt)
         keep.append(p)
         return p.array
-    # host raw columns: the partition attribute arrives as a raw 64-bit symbol value (not a dense id)
-    raw = synth.raw_symbols(key.cpu().numpy())
-    ts_h = pinned(g["ts"].cpu().numpy())
-    col_h = [pinned(c.cpu().numpy()) for c in cols]
-    key_h = pinned(np.zeros(n, np.int32))
-    del g, key, cols
-    partitioned = "partition with" in synth.QUERIES[cfg]
-    bounds = [n * p // parts for p in range(parts + 1)]
-    h, nfa = make_handle(cfg, no_carry=0, ingress_rows=max(1, (bounds[1] - bounds[0] + 1) // 2))
-    sink = N.ColumnSink(nfa, n + 1, pinned=True, fields=("trigger", "ts"), nulls=False)
-    batches = []
-    for p in range(parts):
-        lo, hi = bounds[p], bounds[p + 1]
-        cp = [c.ctypes.data + lo * c.itemsize for c in col_h]
-        if partitioned:
-            cp[1] = 0   # the symbol column itself is never read by the query (only its dense key)
-        b = N.make_batch(hi - lo, rank * n + lo, ts_h.ctypes.data + 8 * lo, 0, key_h.ctypes.data + 4 * lo, cp,
-                         [0] * len(col_h), 0, keys, keep)
-        batches.append(b)
-    cols_struct = sink.struct
-    times, rts, delivered = [], [], 0
-    pool = ThreadPoolExecutor(1)
-    for s in range(steps + 1):
-        h.reset()
-        router = N.Router(1, threads)
+    ts = pinned(total, np.int64)
+    raw = pinned(total, np.int64)
+    if cfg.startswith("C3"):
+        names = [("id", np.int64), (None, np.int32), ("v", np.int32), ("w", np.int32)]
+    else:
+        names = [("id", np.int64), (None, np.int32), ("price", np.float32)]
+    cols = [pinned(total, dt) if nm else None for nm, dt in names]
+    for lo in range(0, total, gen_rows):
+        hi = min(total, lo + gen_rows)
+        g = synth.generate_torch(cfg, lo, hi - lo, dev, keys=keys, rate=rate)
+        ts[lo:hi] = g["ts"].cpu().numpy()
+        raw[lo:hi] = synth.raw_symbols_torch(g["key"]).cpu().numpy()
+        for (nm, _), c in zip(names, cols):
+            if nm:
+                c[lo:hi] = g[nm].cpu().numpy()
+        del g
+    torch.cuda.empty_cache()
+    return ts, raw, cols, keep
 
-        def route(p):
-            if partitioned:
-                router.route(raw[bounds[p]:bounds[p + 1]], key_h[bounds[p]:bounds[p + 1]])
+
+def node_whole(cfg, total, keys, rate, devices, steps, threads, chunk_rows):
+    """SURVEY.md §8d whole-node events/s through the node pipeline (sg_node_*, csrc/node.hip), one host process
+    driving `gpus` GPUs: pinned raw host rows -> native router (first-seen dense ids, shard mix64(id) mod G) ->
+    per-GPU threads (chunked H2D, kernels, GPU-transposed SoA match columns D2H, overlapped across chunks) ->
+    native k-way merge into the node's delivery order -> every match tuple (trigger, ts, projected columns) in
+    pinned host memory.  Routing and merge are inside the timed region; data generation is not."""
+    gpus = len(devices)
+    ts, raw, cols, keep = host_stream(cfg, total, keys, rate, torch.device("cuda", devices[0]))
+    nfa = L.lower(_ctx(cfg))
+    node = N.Node(N.build_desc(nfa), n_gpus=gpus, devices=list(devices), threads=threads, chunk_rows=chunk_rows)
+    nb = N.make_node_batch(total, 0, ts.ctypes.data, 0, raw.ctypes.data, [c.ctypes.data if c is not None else 0
+                                                                         for c in cols], [0] * len(cols), keep)
+    cap = total // 2 + 1_000_000
+    sink = N.ColumnSink(nfa, cap, pinned=True, fields=("trigger", "ts"), nulls=False)
+    times, stats, got = [], [], 0
+    for s in range(steps + 1):
+        node.reset()
         t0 = time.perf_counter()
-        route(0)
-        t1 = time.perf_counter()
-        got = 0
-        for p in range(parts):
-            nxt = pool.submit(route, p + 1) if p + 1 < parts else None
-            # deliver part p's matches right after the ones already written
-            part_out = N.sg_match_columns()
-            part_out.trigger = sink.trigger.ctypes.data + 8 * got
-            part_out.ts = sink.ts.ctypes.data + 8 * got
-            for k, a in enumerate(sink.cols):
-                part_out.cols[k] = a.ctypes.data + a.itemsize * got
-            got += h.push_deliver(batches[p], part_out, sink.cap - got)
-            if nxt is not None:
-                nxt.result()
-        t2 = time.perf_counter()
-        router.close()
-        delivered = got
-        if s:   # the first step warms the pinned paths and workspaces
-            times.append(t2 - t0)
-            rts.append(t1 - t0)
-    pool.shutdown()
-    h.close()
+        got = node.push(nb, sink.struct, cap)
+        dt = time.perf_counter() - t0
+        if s:   # the first push sizes the pinned staging and device slots
+            times.append(dt)
+            stats.append(node.stats())
+    # spot check of the delivered order: triggers never decrease
+    tr = sink.trigger[:got]
+    ordered = bool(np.all(tr[1:] >= tr[:-1])) if got > 1 else True
+    node.close()
     ms = 1000.0 * float(np.mean(times))
-    bytes_in = n * (8 + (4 if partitioned else 0) + sum(np.dtype(c.dtype).itemsize for c in col_h)
-                    - (col_h[1].dtype.itemsize if partitioned else 0))
-    bytes_out = delivered * (8 + 8 + sum(np.dtype(d).itemsize for d in N.column_dtypes(nfa)))
-    del cols_struct
-    return {"ms_per_step": round(ms, 3), "router_first_part_ms": round(1000.0 * float(np.mean(rts)), 3),
-            "matches": int(delivered), "h2d_GB": round(bytes_in / 1e9, 3), "d2h_GB": round(bytes_out / 1e9, 3),
-            "router_threads": threads, "parts": parts}
+    st = stats[-1]
+    del sink, keep, ts, raw, cols
+    return {"workload": f"{cfg}: " + synth.QUERIES[cfg], "events": total, "keys": keys,
+            "rate_events_per_ms": rate, "gpus": gpus, "ms_per_step": round(ms, 2),
+            "value": round(total / (ms * 1e-3), 1), "unit": "events/s", "matches": int(got),
+            "delivery_ordered": ordered, "host_threads": threads, "chunk_rows": int(st["chunk_rows"]),
+            "chunks": int(st["chunks"]), "route_ms": round(st["route_ms"], 1), "merge_ms": round(st["merge_ms"], 1),
+            "gpu_busy_ms": [round(x, 1) for x in st["gpu_ms"][:gpus]],
+            "h2d_GB": round(st["h2d_bytes"] / 1e9, 3), "d2h_GB": round(st["d2h_bytes"] / 1e9, 3),
+            "shard_rows": [int(x) for x in st["shard_rows"][:gpus]],
+            "definition": "SURVEY.md §8d: pinned raw host rows -> native router -> per-GPU chunked H2D / kernels / "
+                          "D2H -> native merge -> every match tuple in host memory (sg_node_push wall time)"}
+
+
+def _ctx(cfg):
+    app = C.parse(synth.QUERIES[cfg])
+    if app.partitions:
+        p = app.partitions[0]
+        return L.make_context(app, p.queries[0], p, {})
+    return L.make_context(app, app.queries[0], None, {})
 
 
 def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
@@ -305,26 +329,17 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    if ws > 1:
-        import torch.distributed as dist
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         matches = step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    tot = torch.tensor([el, float(matches), float(n)], device=dev, dtype=torch.float64)
-    if ws > 1:
-        import torch.distributed as dist
-        mx = tot[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        tot[0] = mx[0]
+    el, matches, rows = reduce_max(el), reduce_sum(matches), reduce_sum(n)
     h.close()
     del cat, batches
     torch.cuda.empty_cache()
-    el, matches, rows = (float(x) for x in tot.tolist())
     ms = 1000.0 * el / steps
     return {"workload": "C5 (BASELINE configs[4]): " + synth.QUERIES["C5"], "events": total, "keys": keys,
             "rate_events_per_ms": rate, "n_gpus": ws, "scaling": "strong", "steps": steps,
@@ -351,15 +366,18 @@ def main():
                     help="steps of the 1B-event C5 stream sharded by key hash across the ranks (0: skip)")
     ap.add_argument("--c5-events", type=int, default=0, help="events of the C5 stream (default 1e9)")
     ap.add_argument("--c5-push-rows", type=int, default=100_000_000)
+    ap.add_argument("--c5-node-steps", type=int, default=2,
+                    help="steps of the 1B-event C5 stream through the node pipeline, rank 0 driving every GPU (0: skip)")
+    ap.add_argument("--node-threads", type=int, default=0, help="host threads of the node pipeline (0: 16 per GPU)")
     ap.add_argument("--pmc", default=DEFAULT_PMC, help="rocprofv3 PMC summary of this command (profiles/collect_r02.sh)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if ws > 1:
+    if ws > 1:   # timing reductions only (no data-path collective): gloo, host tensors
         import torch.distributed as dist
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group("gloo")
     cfg = args.config
     if not args.cpu_sample:
         args.cpu_sample = {"C1": 1_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000,
@@ -384,9 +402,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if ws > 1:
-        import torch.distributed as dist
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     stage = np.zeros(5)
     kern = {}
@@ -403,34 +419,36 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if ws > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        dist.barrier()
+        elapsed = reduce_max(elapsed)
+        barrier()
     stage /= args.steps
     kern = {k: v / args.steps for k, v in kern.items()}
     h.close()
     del g, key, cols
     torch.cuda.empty_cache()
 
-    # ---- whole_node (§8d): host routing + PCIe both ways, per rank, max over ranks
+    # ---- whole_node (§8d) on this rank's stream, its own GPU through the node pipeline (max over ranks)
     wn = None
     if args.whole_node_steps > 0:
         try:
-            wn = whole_node(cfg, rank, n, keys, rate, args.whole_node_steps, dev, args.router_threads)
+            wn = node_whole(cfg, n, keys, rate, [local], args.whole_node_steps, args.router_threads, 0)
         except Exception as e:   # report, never fake
             wn = {"error": str(e)}
         if ws > 1 and "ms_per_step" in wn:
-            import torch.distributed as dist
-            tt = torch.tensor([wn["ms_per_step"]], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            wn["ms_per_step"] = round(float(tt.item()), 3)
-        if "ms_per_step" in wn:
+            wn["ms_per_step"] = round(reduce_max(wn["ms_per_step"]), 2)
             wn["value"] = round(ws * n / (wn["ms_per_step"] * 1e-3), 1)
-            wn["unit"] = "events/s"
-            wn["definition"] = ("SURVEY.md §8d: raw host columns -> native router (first-seen dense keys) -> pinned "
-                                "chunked H2D -> kernels -> GPU-transposed SoA match columns in pinned host memory")
+            wn["scaling"] = "weak (every rank its own stream and GPU)"
+    # ---- c5_whole_node (BASELINE configs[4] as the metric words it): ONE process drives every GPU of the job
+    c5w = None
+    if args.c5_node_steps > 0:
+        if rank == 0:
+            try:
+                thr = args.node_threads or max(16, min(16 * ws, len(os.sched_getaffinity(0))))
+                c5w = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
+                                 synth.CONFIGS["C5"][3], list(range(ws)), args.c5_node_steps, thr, 0)
+            except Exception as e:   # report, never fake
+                c5w = {"error": str(e)}
+        barrier()
     c5 = None
     if args.c5_stream_steps > 0:
         try:
@@ -501,6 +519,7 @@ def main():
                    "spilled_units": int(spilled), "parallelism": f"key-sharded x{ws} (no collective)"},
         "whole_node": wn,
         "c5_stream": c5,
+        "c5_whole_node": c5w,
         "roofline": roof,
         "cpu_baseline": cpu,
         "source_hash": source_hash(cfg),

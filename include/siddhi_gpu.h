@@ -320,7 +320,9 @@ typedef struct sg_node_stats {  /* of the last sg_node_push */
   int64_t rows, matches, chunks, chunk_rows, h2d_bytes, d2h_bytes;
   int64_t shard_rows[SG_NODE_MAX_GPUS];   /* rows each GPU has received since open/reset */
 } sg_node_stats;
-/* chunk_rows 0: 25M rows per chunk; host_threads 0: all hardware threads. */
+/* chunk_rows 0: about 16 chunks per push (4M..25M rows each); host_threads 0: all hardware threads.
+ * Closed-form queries (`every A -> B[..]`): out->ts and B-attribute columns are filled on the host from the
+ * batch's trigger rows instead of being copied back from the GPU (environment SG_NODE_NO_FILL: copy them). */
 int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const sg_options* opt, int host_threads,
                  int64_t chunk_rows, sg_node** out);
 /* Push a batch; its matches (node delivery order) go to out rows [0, *n).  out->trigger is required; other NULL

@@ -24,6 +24,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -179,6 +180,7 @@ struct sg_node {
   int64_t local_rows[MAX_GPUS] = {};   // rows each shard has seen (its local event index space)
   int64_t next_index = 0;
   bool broken = false;
+  bool no_fill = false;              // testing: ship every column back instead of filling trigger-row columns on the host
   // per-GPU device-side ingress slots and copy stream
   hipStream_t cp[MAX_GPUS] = {};
   hipEvent_t ev_copied[MAX_GPUS][2] = {}, ev_used[MAX_GPUS][2] = {};
@@ -193,28 +195,68 @@ struct sg_node {
 namespace {
 
 // What every shard delivers: the caller's columns plus, for the merge, trigger (always) and phase / key when two
-// shards can produce matches for the same trigger (timer passes fan out to every shard).
+// shards can produce matches for the same trigger (timer passes fan out to every shard).  Columns the host can read
+// from the trigger row itself are not shipped back over PCIe at all (`fill`): for the closed form `every A -> B[..]`
+// the output timestamp is the trigger's (StateEvent.timestamp is set by the event that completed the match,
+// C/query/input/stream/state/StreamPostStateProcessor.java:53-72) and every B.attr projection is the trigger row's
+// attribute (QuerySelector.processNoGroupBy, C/query/selector/QuerySelector.java:125-163) -- the host selector copies
+// them from the caller's pinned input columns by global trigger index.
 struct Want {
   bool ts, key, grp, col[SG_MAX_SELECT], nul[SG_MAX_SELECT];
   int ns;
   int width[SG_MAX_SELECT];
+  bool fill_ts;                 // out->ts from the trigger row's ts (host)
+  int fill_col[SG_MAX_SELECT];  // >= 0: out->cols[k] (and nulls[k]) from batch column fill_col[k] at the trigger row
+  bool any_fill;
 };
 
-Want want_of(const sg_node& nd, const sg_match_columns* out) {
+Want want_of(const sg_node& nd, const sg_node_batch& b, const sg_match_columns* out) {
   Want w;
   memset(&w, 0, sizeof(w));
   const sg_nfa_desc& d = nd.desc;
   w.ns = d.n_out > 0 ? d.n_out : d.n_select;
   const bool tie = nd.G > 1 && d.shape != SG_SHAPE_EVERY_NEXT_CMP;
+  const bool closed = d.shape == SG_SHAPE_EVERY_NEXT_CMP && d.n_out == 0 && !nd.no_fill;
+  const int b_state = d.shape_args[1];
   w.ts = out->ts != nullptr;
+  w.fill_ts = closed && w.ts;
+  if (w.fill_ts) w.ts = false;
   w.key = out->key != nullptr || tie;
   w.grp = out->group != nullptr || tie;
   for (int k = 0; k < w.ns; ++k) {
     w.col[k] = out->cols[k] != nullptr;
     w.nul[k] = out->nulls[k] != nullptr;
     w.width[k] = sg_col_width(d.n_out > 0 ? d.out_type[k] : d.sel_type[k]);
+    w.fill_col[k] = -1;
+    if (!closed || (!w.col[k] && !w.nul[k])) continue;
+    const int c = d.ret_col[d.sel_ret[k]];
+    const bool single = d.sel_index[k] == 0 || d.sel_index[k] == -1;
+    if (d.sel_state[k] == b_state && single && d.sel_type[k] == d.col_type[c] && b.cols && b.cols[c] &&
+        true) {
+      w.fill_col[k] = c;
+      w.col[k] = w.nul[k] = false;
+    }
   }
+  w.any_fill = w.fill_ts;
+  for (int k = 0; k < w.ns; ++k) w.any_fill |= w.fill_col[k] >= 0;
   return w;
+}
+
+// Host selector for the trigger-row columns of output rows [o0, o1): trig[] holds their global trigger indices.
+inline void fill_row(const sg_node_batch& b, const sg_nfa_desc& d, const Want& w, const sg_match_columns* out,
+                     int64_t o, uint64_t trig) {
+  const int64_t t = (int64_t)(trig - b.base_index);
+  if (w.fill_ts) out->ts[o] = b.ts[t];
+  for (int k = 0; k < w.ns; ++k) {
+    const int c = w.fill_col[k];
+    if (c < 0) continue;
+    if (out->cols[k]) {
+      if (w.width[k] == 8) ((int64_t*)out->cols[k])[o] = ((const int64_t*)b.cols[c])[t];
+      else ((int32_t*)out->cols[k])[o] = ((const int32_t*)b.cols[c])[t];
+    }
+    if (out->nulls[k]) out->nulls[k][o] = (b.nulls && b.nulls[c]) ? b.nulls[c][t] : 0;
+  }
+  (void)d;
 }
 
 // Pipeline state of one sg_node_push call.
@@ -719,7 +761,8 @@ void merge_chunk(Run& r, int64_t j) {
       const NodeRing& R = nd.ring[s];
       const int64_t p = cur[s] % R.M;
       if (r.out->trigger) r.out->trigger[o] = head[s];
-      if (r.out->ts) r.out->ts[o] = R.ts.as<int64_t>()[p];
+      if (w.ts) r.out->ts[o] = R.ts.as<int64_t>()[p];
+      if (w.any_fill) fill_row(r.b, nd.desc, w, r.out, o, head[s]);
       if (r.out->key) r.out->key[o] = (int32_t)gkey(s, cur[s]);
       if (r.out->group) r.out->group[o] = R.grp.as<uint32_t>()[p];
       for (int c = 0; c < w.ns; ++c) {
@@ -734,6 +777,31 @@ void merge_chunk(Run& r, int64_t j) {
     }
   });
   r.out_rows += total;
+}
+
+// G = 1: the GPU delivers straight into the caller's columns; the trigger-row columns of chunk j are filled in once
+// its triggers have landed (host thread pool, rows in parallel)
+void fill_loop(Run& r) {
+  sg_node& nd = r.nd;
+  r.guarded([&] {
+    for (int64_t j = 0; j < r.nch; ++j) {
+      if (!r.wait([&] { return r.delivered[0] > j; })) return;
+      const int64_t o0 = j ? r.dlv_end[0][j - 1] : 0, o1 = r.dlv_end[0][j];
+      const double t0 = now_ms();
+      const int64_t cnt = o1 - o0;
+      if (cnt > 0) {
+        const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, cnt / 65536 + 1));
+        nd.pool->parallel_for(T, [&](int t) {
+          const int64_t a = o0 + cnt * t / T, e = o0 + cnt * (t + 1) / T;
+          for (int64_t o = a; o < e; ++o) fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o]);
+        });
+      }
+      r.publish([&] {
+        r.merged = j + 1;
+        r.t_merge += now_ms() - t0;
+      });
+    }
+  });
 }
 
 void merge_loop(Run& r) {
@@ -825,8 +893,11 @@ void reserve_all(Run& r) {
 
 void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, int64_t cap, int64_t* n_out) {
   Run r(nd, b, out, cap);
-  r.w = want_of(nd, out);
-  r.C = nd.chunk_rows > 0 ? nd.chunk_rows : std::max<int64_t>(1, std::min<int64_t>(b.n, (int64_t)25 << 20));
+  r.w = want_of(nd, b, out);
+  // default chunks: ~16 per push (short pipeline fill and drain), 4M..25M rows each
+  r.C = nd.chunk_rows > 0 ? nd.chunk_rows
+                          : std::max<int64_t>(1, std::min<int64_t>(b.n, std::max<int64_t>((int64_t)4 << 20,
+                                                                   std::min<int64_t>((int64_t)25 << 20, (b.n + 15) / 16))));
   if (r.C >= (1ll << 30) - 1) throw SgError(SG_EINVAL, "node chunk too large (max 2^30-2 rows)");
   r.nch = (b.n + r.C - 1) / r.C;
   for (int s = 0; s < nd.G; ++s) r.dlv_end[s].assign((size_t)r.nch, 0);
@@ -843,6 +914,7 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
     th.emplace_back(gpu_loop, std::ref(r), s);
   }
   if (nd.G > 1) th.emplace_back(merge_loop, std::ref(r));
+  else if (r.w.any_fill) th.emplace_back(fill_loop, std::ref(r));
   const double t1 = now_ms();
   r.guarded([&] {
     for (int64_t j = 0; j < r.nch; ++j) {
@@ -927,6 +999,7 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
   nd->opt.ingress_rows = -1;  // (the node does its own chunking)
   nd->threads = host_threads ? host_threads : (int)std::max(1u, std::thread::hardware_concurrency());
   nd->chunk_rows = chunk_rows;
+  nd->no_fill = getenv("SG_NODE_NO_FILL") != nullptr;
   memset(&nd->st, 0, sizeof(nd->st));
   int rc = SG_OK;
   for (int s = 0; s < n_gpus && rc == SG_OK; ++s) {

@@ -143,7 +143,26 @@ def generate_torch(cfg: str, start: int, count: int, device, keys: int = None, r
     return out
 
 
+SYMBOL_SALT = 0x5359_4D42_4F4C_0000
+
+
 def raw_symbols(key: np.ndarray) -> np.ndarray:
     """The partition attribute as a host sees it before dictionary encoding: one 64-bit value per symbol
     ("S%07d" % key hashed), for the native router (sg_router_route) to map to first-seen dense ids."""
-    return splitmix64_np(key.astype(np.uint64) ^ np.uint64(0x5359_4D42_4F4C_0000)).view(np.int64)
+    return splitmix64_np(key.astype(np.uint64) ^ np.uint64(SYMBOL_SALT)).view(np.int64)
+
+
+def raw_symbols_torch(key):
+    """raw_symbols computed in HBM (int64 bit patterns; same values as the numpy version)."""
+    import torch
+
+    def s64(u):
+        return u - (1 << 64) if u >= (1 << 63) else u
+
+    def lsr(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+    z = key.to(torch.int64) ^ SYMBOL_SALT
+    z = z + s64(GOLDEN)
+    z = (z ^ lsr(z, 30)) * s64(M1)
+    z = (z ^ lsr(z, 27)) * s64(M2)
+    return z ^ lsr(z, 31)

@@ -137,3 +137,69 @@ def test_node_partitioned_absence_clock_fanout(gpus):
     assert len(want) > 100
     got, _ = run_node(ABSENT_Q, [b], gpus, 25_000, synth.raw_symbols)
     assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_node_ships_every_column_when_fill_is_off(gpus, monkeypatch):
+    """SG_NODE_NO_FILL: the closed form's trigger-row columns (ts, e2.*) come back from the GPU instead of being
+    filled on the host from the batch -- both deliveries are the same rows."""
+    monkeypatch.setenv("SG_NODE_NO_FILL", "1")
+    cfg = "C2"
+    b = synth_batch(cfg, 0, 150_000, keys=600, rate=100)
+    want = _want(synth.QUERIES[cfg], b)
+    got, _ = run_node(synth.QUERIES[cfg], [b], gpus, 40_000, synth.raw_symbols)
+    assert_same(got, want)
+
+
+def _first_seen_ids(keys, K):
+    """Dense first-seen ids of keys in [0, K) without sorting the rows (the first occurrence wins the reversed
+    fancy-index assignment)."""
+    n = len(keys)
+    first = np.full(K, n, np.int64)
+    first[keys[::-1]] = np.arange(n - 1, -1, -1, dtype=np.int64)
+    present = first < n
+    order = np.argsort(first, kind="stable")
+    ids = np.full(K, -1, np.int32)
+    ids[order[:int(present.sum())]] = np.arange(int(present.sum()), dtype=np.int32)
+    return ids[keys]
+
+
+@pytest.mark.timeout(1100)
+def test_node_c5_300m_two_shards_three_pushes():
+    """BASELINE configs[4] through the node pipeline at scale: the first 300M events of the 1M-key C5 stream as
+    three 100M-event node pushes (key dictionary and per-key state carried between them) over two shards on
+    device 0 -- raw symbols routed on the host, chunked H2D / kernels / D2H per shard, native merge -- compared row
+    for row with the oracle run key-sharded over the host cores (parity_util.sharded_oracle)."""
+    import os
+    from parity_util import sharded_oracle
+    cfg = "C5"
+    _, _, K, R = synth.CONFIGS[cfg]
+    n, pushes = 300_000_000, 3
+    g = synth.generate(cfg, 0, n, keys=K, rate=R)
+    raw = synth.raw_symbols(g["key"])
+    cols = [g["id"], None, g["price"]]
+    per = n // pushes
+    from siddhi_amd import _native as N
+    nfa = __import__("siddhi_amd.lowering", fromlist=["lower"]).lower(context(synth.QUERIES[cfg]))
+    node = N.Node(N.build_desc(nfa), n_gpus=2, devices=[0, 0], threads=16, chunk_rows=0)
+    outs = []
+    for p in range(pushes):
+        lo, hi = p * per, (p + 1) * per
+        keep = []
+        nb = N.make_node_batch(hi - lo, lo, g["ts"][lo:].ctypes.data, 0, raw[lo:].ctypes.data,
+                               [cols[0][lo:].ctypes.data, 0, cols[2][lo:].ctypes.data], [0, 0, 0], keep)
+        sink = N.ColumnSink(nfa, per // 2, pinned=False)
+        m = node.push(nb, sink.struct, sink.cap)
+        outs.append(node_outputs(nfa, sink, m))
+        del sink
+    assert node.keys() == K
+    node.close()
+    got = Outputs(*[np.concatenate([getattr(o, f) for o in outs]) for f in
+                    ("trigger", "ts", "key", "group", "vals", "vnull")])
+    del outs, raw
+    dense = _first_seen_ids(g["key"].astype(np.int64), K)
+    b = Batch(n, 0, g["ts"], np.zeros(n, np.int32), dense, [g["id"], g["key"], g["price"]], [None] * 3)
+    want = sharded_oracle(synth.QUERIES[cfg], b, max(2, min(16, os.cpu_count() or 2)))
+    assert len(got) == len(want) > 0
+    assert_same(got, want)
