@@ -329,6 +329,11 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
  * arrays are skipped.  SG_ECAPACITY if more than cap matches: the node must then be reset. */
 int sg_node_push(sg_node* nd, const sg_node_batch* b, const sg_match_columns* out, int64_t cap, int64_t* n);
 int sg_node_reset(sg_node* nd);   /* new stream: forget keys and per-key state */
+/* Where partition keys are dictionary-encoded (first-seen dense ids, PartitionRuntime.cloneIfNotExist,
+ * C/partition/PartitionRuntime.java:255-308): 0 auto (the device unless the query has playback timers), 1 the host
+ * router (sg_router), 2 one dictionary per GPU in HBM (raw keys are uploaded; with several GPUs rows go to shard
+ * mix64(raw) mod n_gpus).  Only before the first push of a stream. */
+int sg_node_set_key_dict(sg_node* nd, int mode);
 int sg_node_stats_get(const sg_node* nd, sg_node_stats* st);
 int sg_node_keys(const sg_node* nd, int64_t* n_keys);
 int sg_node_close(sg_node* nd);

@@ -21,7 +21,7 @@ SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg
            "sg_snapshot", "sg_restore", "sg_host_alloc", "sg_host_free", "sg_poll_columns", "sg_push_deliver",
            "sg_router_open", "sg_router_route", "sg_router_keys", "sg_router_close", "sg_router_dense_ids",
            "sg_merge_order", "sg_node_open", "sg_node_push", "sg_node_reset", "sg_node_stats_get", "sg_node_keys",
-           "sg_node_close", "sg_node_last_error"]
+           "sg_node_close", "sg_node_last_error", "sg_node_set_key_dict"]
 
 I32, I64, U64 = ct.c_int32, ct.c_int64, ct.c_uint64
 
@@ -162,6 +162,7 @@ def load_library(path: str = LIB_PATH):
         lib.sg_node_stats_get.argtypes = [P, P]
         lib.sg_node_keys.argtypes = [P, ct.POINTER(I64)]
         lib.sg_node_close.argtypes = [P]
+        lib.sg_node_set_key_dict.argtypes = [P, ct.c_int]
         lib.sg_node_last_error.argtypes = [P]
         lib.sg_node_last_error.restype = ct.c_char_p
         lib.sg_last_error.argtypes = [P]
@@ -484,6 +485,10 @@ class Node:
 
     def reset(self):
         self.check(self.lib.sg_node_reset(self.n))
+
+    def set_key_dict(self, mode: int):
+        """0 auto, 1 host router, 2 device dictionary (before the first push of a stream)."""
+        self.check(self.lib.sg_node_set_key_dict(self.n, int(mode)))
 
     def close(self):
         if self.n:

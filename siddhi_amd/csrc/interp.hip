@@ -376,6 +376,23 @@ static uint32_t general_key_bound(SgHandle* h, const BatchView& bv, int64_t n) {
 
 static void run_machine(SgHandle* h, const BatchView& bv, int64_t n);
 
+// rows [lo, lo + cnt) of a device batch view
+static BatchView slice_view(const sg_nfa_desc& d, const BatchView& bv, int64_t lo, int64_t cnt) {
+  if (lo == 0 && cnt == bv.n) return bv;
+  BatchView v = bv;
+  v.n = cnt;
+  v.base_index = bv.base_index + (uint64_t)lo;
+  v.ts = bv.ts + lo;
+  if (bv.stream) v.stream = bv.stream + lo;
+  if (bv.key) v.key = bv.key + lo;
+  if (bv.index) v.index = bv.index + lo;
+  for (int c = 0; c < d.n_cols; ++c) {
+    if (bv.cols.col[c]) v.cols.col[c] = (const char*)bv.cols.col[c] + (size_t)sg_col_width(d.col_type[c]) * lo;
+    if (bv.cols.nul[c]) v.cols.nul[c] = bv.cols.nul[c] + lo;
+  }
+  return v;
+}
+
 void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   GeneralState* gs = gstate(h);
   if (!gs->pp_checked) {
@@ -384,7 +401,16 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   if (gs->pp && sg_partial_active(gs->pp) && h->opt.partial_lanes >= 0) {
     const uint32_t kb = general_key_bound(h, bv, n);
-    if (sg_partial_push(h, gs->pp, bv, n, kb)) return;
+    // a push larger than the route's row budget runs as consecutive sub-pushes (carried state makes them one push)
+    int64_t lo = 0;
+    while (lo < n) {
+      const int64_t room = sg_partial_max_rows(h, gs->pp);
+      if (room < 1) throw SgError(SG_ECAPACITY, "partial-lane route: carried rows alone exceed the row budget");
+      const int64_t cnt = std::min(n - lo, room);
+      if (!sg_partial_push(h, gs->pp, slice_view(h->desc, bv, lo, cnt), cnt, kb)) break;
+      lo += cnt;
+    }
+    if (lo == n) return;
     // the stream left the route's precondition (a timestamp went back): rebuild the general machine's per-key runtimes
     // by replaying the carried rows without emitting (they were delivered already), then continue on the machine
     BatchView cv = sg_partial_carried_view(h, gs->pp, (int32_t)kb);
@@ -394,6 +420,8 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
       run_machine(h, cv, cv.n);
       h->out.n = delivered;
     }
+    run_machine(h, slice_view(h->desc, bv, lo, n - lo), n - lo);
+    return;
   }
   run_machine(h, bv, n);
 }

@@ -32,6 +32,7 @@
 #include <thread>
 #include <vector>
 
+#include "keydict.h"
 #include "router.h"
 #include "sg_engine.h"
 
@@ -154,7 +155,7 @@ struct Pinned {
 
 // One shard's rows of one chunk, in arrival order (host staging, G > 1).
 struct NodeStage {
-  Pinned ts, key, stream, gidx;
+  Pinned ts, key, stream, gidx, raw;   // (raw: device-dictionary mode, the key as received)
   Pinned col[SG_MAX_COLS], nul[SG_MAX_COLS];
 };
 
@@ -190,6 +191,14 @@ struct sg_node {
   std::vector<int32_t> dense_tmp[NODE_RING];
   NodeStage stage[NODE_RING][MAX_GPUS];
   NodeRing ring[MAX_GPUS];
+  // key dictionary: the host router (sg_router) or one device dictionary per GPU (keydict.h)
+  int key_dict_mode = 0;             // 0 auto, 1 host, 2 device (sg_node_set_key_dict)
+  int ddict = -1;                    // decided at the first push of a stream: 1 device, 0 host
+  KeyDict kd[MAX_GPUS];
+  int64_t* draw[MAX_GPUS][2] = {};   // device raw-key slots
+  int64_t draw_rows = 0;
+  std::vector<int32_t> l2g[MAX_GPUS];   // G > 1, device mode: shard-local id -> node-wide first-seen id
+  int64_t g_keys = 0;
 };
 
 namespace {
@@ -284,6 +293,10 @@ struct Run {
   // per (chunk, shard): rows, key bound and local index of row 0 (fixed when the chunk is routed)
   std::vector<int64_t> rows_of, lbase_of;
   std::vector<int32_t> kb_of;
+  // device-dictionary mode, per (chunk, shard): the shard's key count before the chunk and the first rows of the
+  // keys the chunk introduced, in id order (G > 1: merged into node-wide first-seen ids)
+  std::vector<int64_t> kbase_of;
+  std::vector<std::vector<uint32_t>> newf_of;
   double t_route = 0, t_merge = 0, t_gpu[MAX_GPUS] = {};
   int64_t h2d_bytes = 0, d2h_bytes = 0;
 
@@ -335,8 +348,86 @@ inline bool is_clock_point(const Run& r, int64_t lo, int64_t slice_a, int64_t i)
   return i == slice_a || r.b.ts[lo + i] != r.b.ts[lo + i - 1];
 }
 
+// ---- device-dictionary mode: no key lookups on the host.  G = 1: nothing to do; G > 1: rows are scattered to
+// shard mix64(raw key) mod G (rows of stream -1 reach every shard), each GPU dictionary-encodes its own keys --
+// first-seen order inside a shard is the node's first-seen order restricted to it.
+void route_chunk_dev(Run& r, int64_t j) {
+  sg_node& nd = r.nd;
+  const sg_nfa_desc& d = nd.desc;
+  const int G = nd.G;
+  const int slot = (int)(j % NODE_RING);
+  const int64_t lo = chunk_lo(r, j), hi = chunk_lo(r, j + 1), n = hi - lo;
+  if (G == 1) {
+    r.rows_of[j] = n;
+    return;
+  }
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, n / 65536 + 1));
+  auto slice = [&](int t, int64_t& a, int64_t& e) {
+    a = n * t / T;
+    e = n * (t + 1) / T;
+  };
+  const int32_t* stream = r.b.stream ? r.b.stream + lo : nullptr;
+  const int64_t* raw = r.b.raw_key + lo;
+  auto shard = [&](int64_t i) -> int {
+    return (stream && stream[i] < 0) ? -1 : (int)(sgr::mix64((uint64_t)raw[i]) % (uint64_t)G);
+  };
+  std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(G, 0));
+  nd.pool->parallel_for(T, [&](int t) {
+    int64_t a, e;
+    slice(t, a, e);
+    int64_t* c = cnt[t].data();
+    int64_t bcast = 0;
+    for (int64_t i = a; i < e; ++i) {
+      const int x = shard(i);
+      if (x >= 0) ++c[x];
+      else ++bcast;
+    }
+    for (int q = 0; q < G; ++q) c[q] += bcast;
+  });
+  std::vector<std::vector<int64_t>> off(T, std::vector<int64_t>(G, 0));
+  for (int q = 0; q < G; ++q) {
+    int64_t o = 0;
+    for (int t = 0; t < T; ++t) {
+      off[t][q] = o;
+      o += cnt[t][q];
+    }
+    r.rows_of[j * G + q] = o;
+  }
+  const int nc = d.n_cols;
+  int need[SG_MAX_COLS] = {};
+  for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
+  nd.pool->parallel_for(T, [&](int t) {
+    int64_t a, e;
+    slice(t, a, e);
+    int64_t cur[MAX_GPUS];
+    for (int q = 0; q < G; ++q) cur[q] = off[t][q];
+    for (int64_t i = a; i < e; ++i) {
+      const int own = shard(i);
+      for (int q = 0; q < G; ++q) {
+        if (own >= 0 && q != own) continue;
+        NodeStage& S = nd.stage[slot][q];
+        const int64_t p = cur[q]++;
+        S.ts.as<int64_t>()[p] = r.b.ts[lo + i];
+        S.raw.as<int64_t>()[p] = raw[i];
+        if (stream) S.stream.as<int32_t>()[p] = stream[i];
+        S.gidx.as<uint64_t>()[p] = r.b.base_index + (uint64_t)(lo + i);
+        for (int c = 0; c < nc; ++c) {
+          if (!need[c] || !r.b.cols[c]) continue;
+          if (sg_col_width(d.col_type[c]) == 8) S.col[c].as<int64_t>()[p] = ((const int64_t*)r.b.cols[c])[lo + i];
+          else S.col[c].as<int32_t>()[p] = ((const int32_t*)r.b.cols[c])[lo + i];
+          if (r.b.nulls && r.b.nulls[c]) S.nul[c].as<uint8_t>()[p] = r.b.nulls[c][lo + i];
+        }
+      }
+    }
+  });
+}
+
 // ---- route (+ scatter) of chunk j into host slot j % NODE_RING --------------------------------------------------
 void route_chunk(Run& r, int64_t j) {
+  if (r.nd.ddict == 1) {
+    route_chunk_dev(r, j);
+    return;
+  }
   sg_node& nd = r.nd;
   const sg_nfa_desc& d = nd.desc;
   const int slot = (int)(j % NODE_RING);
@@ -497,7 +588,7 @@ sg_batch shard_batch(Run& r, int64_t j, int s, const void** cols, const uint8_t*
     sb.base_index = r.b.base_index + (uint64_t)lo;
     sb.ts = r.b.ts + lo;
     sb.stream = r.b.stream ? r.b.stream + lo : nullptr;
-    sb.key = nd.keyslot[slot].as<int32_t>();
+    sb.key = nd.ddict == 1 ? nullptr : nd.keyslot[slot].as<int32_t>();   // (device mode: raw keys go up instead)
     bool nul = false;
     for (int c = 0; c < d.n_cols; ++c) {
       cols[c] = (need[c] && r.b.cols[c]) ? (const char*)r.b.cols[c] + (size_t)sg_col_width(d.col_type[c]) * lo : nullptr;
@@ -512,7 +603,7 @@ sg_batch shard_batch(Run& r, int64_t j, int s, const void** cols, const uint8_t*
   sb.base_index = (uint64_t)r.lbase_of[j * nd.G + s];   // local index space: the host maps triggers back through gidx
   sb.ts = S.ts.as<int64_t>();
   sb.stream = (r.b.stream || need_clocks(d)) ? S.stream.as<int32_t>() : nullptr;
-  sb.key = S.key.as<int32_t>();
+  sb.key = nd.ddict == 1 ? nullptr : S.key.as<int32_t>();
   bool nul = false;
   for (int c = 0; c < d.n_cols; ++c) {
     cols[c] = (need[c] && r.b.cols[c]) ? S.col[c].p : nullptr;
@@ -539,10 +630,14 @@ void copy_loop(Run& r, int s) {
       // (the slot's buffers were reserved for a whole chunk before the pipeline started: no workspace-map access
       // from this thread)
       if (sb.n > 0) sg_upload_to(nd.desc, nd.dslot[s][ds], &sb, 0, sb.n, nd.cp[s]);
+      if (sb.n > 0 && nd.ddict == 1) {
+        const int64_t* rk = nd.G == 1 ? r.b.raw_key + chunk_lo(r, j) : nd.stage[j % NODE_RING][s].raw.as<int64_t>();
+        HIPCHK(hipMemcpyAsync(nd.draw[s][ds], rk, 8 * (size_t)sb.n, hipMemcpyHostToDevice, nd.cp[s]));
+      }
       HIPCHK(hipEventRecord(nd.ev_copied[s][ds], nd.cp[s]));
       r.publish([&] { r.issued[s] = j + 1; });
       HIPCHK(hipEventSynchronize(nd.ev_copied[s][ds]));
-      int64_t bytes = 8 * sb.n + (sb.stream ? 4 * sb.n : 0) + 4 * sb.n;
+      int64_t bytes = 8 * sb.n + (sb.stream ? 4 * sb.n : 0) + (nd.ddict == 1 ? 8 : 4) * sb.n;
       for (int c = 0; c < nd.desc.n_cols; ++c) {
         if (sb.cols[c]) bytes += (int64_t)sg_col_width(nd.desc.col_type[c]) * sb.n;
         if (sb.nulls && sb.nulls[c]) bytes += sb.n;
@@ -653,6 +748,16 @@ void gpu_loop(Run& r, int s) {
         bv.stream = sb.stream ? (const int32_t*)sp.stream : nullptr;
         bv.key = (const int32_t*)sp.key;
         bv.index = nullptr;
+        if (nd.ddict == 1) {   // dictionary-encode the chunk's raw keys on this GPU
+          const int64_t before = nd.kd[s].n_keys;
+          std::vector<uint32_t> nf;
+          kd_resolve(nd.kd[s], nd.draw[s][ds], bv.stream, sb.n, (int32_t*)sp.key, h.stream, nd.G > 1 ? &nf : nullptr);
+          bv.key_bound = (int32_t)std::max<int64_t>(1, nd.kd[s].n_keys);
+          r.publish([&] {
+            r.kbase_of[j * nd.G + s] = before;
+            r.newf_of[j * nd.G + s].swap(nf);
+          });
+        }
         for (int c = 0; c < nd.desc.n_cols; ++c) {
           bv.cols.col[c] = sb.cols[c] ? sp.col[c] : nullptr;
           bv.cols.nul[c] = (sb.nulls && sb.nulls[c]) ? (const uint8_t*)sp.nul[c] : nullptr;
@@ -702,6 +807,24 @@ void merge_chunk(Run& r, int64_t j) {
     e[s] = r.dlv_end[s][j];
     total += e[s] - a[s];
   }
+  if (nd.ddict == 1) {
+    // node-wide first-seen ids of the keys chunk j introduced: every shard's new keys are in first-row order, so a
+    // k-way merge by global first row interleaves them
+    int64_t cur[MAX_GPUS] = {}, m[MAX_GPUS];
+    for (int s = 0; s < G; ++s) {
+      m[s] = (int64_t)r.newf_of[j * G + s].size();
+      if (m[s] > 0) nd.l2g[s].resize((size_t)(r.kbase_of[j * G + s] + m[s]));   // (kbase_of is unset without rows)
+    }
+    auto gfirst = [&](int s, int64_t q) { return nd.stage[slot][s].gidx.as<uint64_t>()[r.newf_of[j * G + s][q]]; };
+    while (true) {
+      int best = -1;
+      for (int s = 0; s < G; ++s)
+        if (cur[s] < m[s] && (best < 0 || gfirst(s, cur[s]) < gfirst(best, cur[best]))) best = s;
+      if (best < 0) break;
+      nd.l2g[best][r.kbase_of[j * G + best] + cur[best]] = (int32_t)nd.g_keys++;
+      ++cur[best];
+    }
+  }
   if (r.out_rows + total > r.cap) throw SgError(SG_ECAPACITY, "node: more matches than the output capacity");
   if (total == 0) return;
   // global trigger of ring row p of shard s (its chunk-j local trigger mapped through the staged global indices)
@@ -743,7 +866,8 @@ void merge_chunk(Run& r, int64_t j) {
     }
     auto gkey = [&](int s, int64_t p) -> int64_t {
       const int32_t lk = nd.ring[s].key.as<int32_t>()[p % nd.ring[s].M];
-      return lk >= 0 ? (int64_t)rt->l2d[s][lk] : -1;
+      if (lk < 0) return -1;
+      return nd.ddict == 1 ? (int64_t)nd.l2g[s][lk] : (int64_t)rt->l2d[s][lk];
     };
     for (int64_t o = o0[t]; o < o0[t + 1]; ++o) {
       int best = -1;
@@ -840,6 +964,7 @@ void reserve_all(Run& r) {
         S.ts.ensure((size_t)C * 8);
         S.key.ensure((size_t)C * 4);
         S.gidx.ensure((size_t)C * 8);
+        if (nd.ddict == 1) S.raw.ensure((size_t)C * 8);
         if (r.b.stream || need_clocks(d)) S.stream.ensure((size_t)C * 4);
         for (int c = 0; c < d.n_cols; ++c) {
           if (!need[c] || !r.b.cols[c]) continue;
@@ -870,9 +995,16 @@ void reserve_all(Run& r) {
     sb.cols = cols;
     sb.nulls = nul ? nuls : nullptr;
     for (int ds = 0; ds < 2; ++ds) nd.dslot[s][ds] = sg_reserve_slot(h, &sb, C, ds);
+    if (nd.ddict == 1 && nd.draw_rows < C)
+      for (int ds = 0; ds < 2; ++ds) {
+        if (nd.draw[s][ds]) HIPCHK(hipFree(nd.draw[s][ds]));
+        nd.draw[s][ds] = nullptr;
+        HIPCHK(hipMalloc((void**)&nd.draw[s][ds], (size_t)C * 8));
+      }
     HIPCHK(hipStreamSynchronize(h.stream));
     sg_egress_init(h);
   }
+  if (nd.ddict == 1) nd.draw_rows = std::max(nd.draw_rows, C);
   // shard rings: room for two chunks' worth of matches per shard beyond the share of the output capacity
   if (nd.G > 1) {
     const int64_t M = std::max<int64_t>(1024, std::min<int64_t>(r.cap, r.cap / nd.G * 2 + 2 * C));
@@ -904,6 +1036,10 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
   r.rows_of.assign((size_t)(r.nch * nd.G), 0);
   r.lbase_of.assign((size_t)(r.nch * nd.G), 0);
   r.kb_of.assign((size_t)(r.nch * nd.G), 1);
+  if (nd.ddict < 0)   // the first push of a stream fixes where keys are encoded
+    nd.ddict = (nd.desc.partitioned && !need_clocks(nd.desc) && nd.key_dict_mode != 1) ? 1 : 0;
+  r.kbase_of.assign((size_t)(r.nch * nd.G), 0);
+  r.newf_of.assign((size_t)(r.nch * nd.G), std::vector<uint32_t>());
   const double t0 = now_ms();
   reserve_all(r);
   const double t_res = now_ms() - t0;
@@ -969,6 +1105,9 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
 void close_node(sg_node* nd) {
   for (int s = 0; s < nd->G; ++s) {
     hipSetDevice(nd->dev[s]);
+    kd_free(nd->kd[s]);
+    for (int k = 0; k < 2; ++k)
+      if (nd->draw[s][k]) hipFree(nd->draw[s][k]);
     if (nd->h[s]) sg_close(nd->h[s]);
     if (nd->cp[s]) hipStreamDestroy(nd->cp[s]);
     for (int k = 0; k < 2; ++k) {
@@ -1069,7 +1208,11 @@ int sg_node_reset(sg_node* nd) {
     const int x = sg_reset(nd->h[s]);
     if (x != SG_OK) rc = x;
     nd->local_rows[s] = 0;
+    kd_reset(nd->kd[s]);
+    nd->l2g[s].clear();
   }
+  nd->g_keys = 0;
+  nd->ddict = -1;
   if (nd->router) sg_router_close(nd->router);
   nd->router = nullptr;
   const int x = sg_router_open(nd->G, nd->threads, &nd->router);
@@ -1087,7 +1230,26 @@ int sg_node_stats_get(const sg_node* nd, sg_node_stats* st) {
 
 int sg_node_keys(const sg_node* nd, int64_t* n_keys) {
   if (!nd || !n_keys) return SG_EINVAL;
+  if (nd->ddict == 1) {
+    *n_keys = 0;
+    for (int s = 0; s < nd->G; ++s) *n_keys += nd->kd[s].n_keys;
+    return SG_OK;
+  }
   return sg_router_keys(nd->router, n_keys, -1, nullptr);
+}
+
+int sg_node_set_key_dict(sg_node* nd, int mode) {
+  if (!nd || mode < 0 || mode > 2) return SG_EINVAL;
+  if (nd->ddict >= 0) {
+    nd->err = "node: the key dictionary is chosen at the first push of a stream (call before it or after sg_node_reset)";
+    return SG_EINVAL;
+  }
+  if (mode == 2 && (!nd->desc.partitioned || need_clocks(nd->desc))) {
+    nd->err = "node: the device dictionary needs a partitioned query without playback timers";
+    return SG_EUNSUPPORTED;
+  }
+  nd->key_dict_mode = mode;
+  return SG_OK;
 }
 
 int sg_node_close(sg_node* nd) {

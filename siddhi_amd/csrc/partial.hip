@@ -1279,6 +1279,16 @@ static void carry_rows(SgHandle* h, PartialState* ps, const BatchView& bv, const
   }
 }
 
+// Rows the next push may carry (carried rows included) before a tie component's 27-bit combined row overflows:
+// larger pushes are cut into sub-pushes by the caller (a stream without carry runs on the machine instead).
+int64_t sg_partial_max_rows(SgHandle* h, PartialState* ps) {
+  if (ps->mode != 1 || h->opt.no_carry) return INT64_MAX;
+  const char* e = getenv("SG_PP_ROW_BUDGET");   // (tests lower the budget through the environment)
+  const int64_t v = e ? atoll(e) : 0;
+  const int64_t lim = v > 0 && v < ((int64_t)1 << 27) ? v : ((int64_t)1 << 27);
+  return lim - 1 - ps->rows[ps->cur].n;
+}
+
 // Returns 1 when the push ran on partial lanes, 0 when it breaks the route's precondition (nothing was changed).
 int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t n, uint32_t kb) {
   const sg_nfa_desc& d = h->desc;

@@ -4,8 +4,8 @@
 // in (StateStreamRuntime.resetAndUpdate, C/query/input/stream/state/StateStreamRuntime.java:96-99), and addState admits
 // one partial per newAndEvery list (StreamPreStateProcessor.addState :203-216, CountPreStateProcessor.addState :109-132,
 // LogicalPreStateProcessor.addState :62-83).  So a key's runtime is a handful of partials, and for sequences whose
-// start state re-arms with `every` it is a function of the key's last H events (H = sum of the states' max counts,
-// interp.h sg_chunk_rule kind 2).  This machine is interp.h's KeyMachine restricted to such sequences (stream, count and
+// start state re-arms with `every` it stays small (its partials reference at most the key's last H events, H = sum of
+// the states' max counts).  This machine is interp.h's KeyMachine restricted to such sequences (stream, count and
 // logical states of one stream, `every` only on the start state) with everything sized to that: partials in a pool of
 // at most PQ_MAX_P entries with their count chains inline, lists of at most PQ_MAX_L entries, events as row positions
 // (the rows stay in HBM, key-ordered) -- a few hundred bytes of LDS per lane instead of a 30 KB HBM arena.
@@ -88,6 +88,12 @@ SG_HD inline SgSeqRule sg_seq_rule(const sg_nfa_desc& d) {
     if (x.kind == SG_K_LOGICAL && (x.partner < 0 || d.states[x.partner].kind != SG_K_LOGICAL)) return r;
   }
   if (starts != 1 || r.chain > PQ_MAX_CHAIN) return r;
+  // pool bound: one partial per non-start element's newAndEvery list, the start state's every-clone, and the one
+  // allocated inside a step before the step's frees (logical partners share their partial: one element)
+  int elements = 0;
+  for (int s = 0; s < d.n_states; ++s)
+    if (!(d.states[s].kind == SG_K_LOGICAL && d.states[s].partner >= 0 && d.states[s].partner < s)) ++elements;
+  if (elements + 1 > PQ_MAX_P) return r;
   r.horizon = h;
   r.ok = 1;
   return r;

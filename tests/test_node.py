@@ -39,11 +39,13 @@ def node_outputs(nfa, sink, n):
                    vals[:, :ns], vnull[:, :ns])
 
 
-def run_node(query, pushes, n_gpus, chunk_rows, raw_of, threads=4, cap=None, pinned=False):
+def run_node(query, pushes, n_gpus, chunk_rows, raw_of, threads=4, cap=None, pinned=False, key_dict=0):
     """Push host batches (their .key = synthetic key ids, sent as raw 64-bit symbols) through one node."""
     from siddhi_amd import _native as N
     nfa = __import__("siddhi_amd.lowering", fromlist=["lower"]).lower(context(query))
     node = N.Node(N.build_desc(nfa), n_gpus=n_gpus, devices=[0] * n_gpus, threads=threads, chunk_rows=chunk_rows)
+    if key_dict:
+        node.set_key_dict(key_dict)
     outs = []
     for b in pushes:
         keep = []
@@ -79,29 +81,49 @@ def _split(b, cuts):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("key_dict", [1, 2], ids=["host-dict", "device-dict"])
 @pytest.mark.parametrize("cfg,n,keys,rate,gpus,chunk", [
     ("C2", 200_000, 1_000, 100, 1, 30_000), ("C2", 200_000, 1_000, 100, 2, 45_000), ("C2", 200_000, 400, 100, 3, 0),
     ("C5", 300_000, 20_000, 1_000, 2, 70_000), ("C3b", 200_000, 400, 1_000, 2, 50_000),
     ("C3c", 200_000, 400, 100, 2, 60_000), ("C3c", 150_000, 400, 100, 1, 40_000)])
-def test_node_matches_oracle(cfg, n, keys, rate, gpus, chunk):
+def test_node_matches_oracle(cfg, n, keys, rate, gpus, chunk, key_dict):
     b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
     want = _want(synth.QUERIES[cfg], b)
     assert len(want) > 0
-    got, st = run_node(synth.QUERIES[cfg], [b], gpus, chunk, synth.raw_symbols)
+    got, st = run_node(synth.QUERIES[cfg], [b], gpus, chunk, synth.raw_symbols, key_dict=key_dict)
     assert st["matches"] == len(want)
     assert sum(st["shard_rows"][:gpus]) == n
     assert_same(got, want)
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("key_dict", [1, 2], ids=["host-dict", "device-dict"])
 @pytest.mark.parametrize("gpus", [1, 2])
-def test_node_pushes_carry_state(gpus):
+def test_node_pushes_carry_state(gpus, key_dict):
     """Consecutive node pushes are one stream (per-key state and the key dictionary carry over)."""
     cfg = "C2"
     b = synth_batch(cfg, 0, 240_000, keys=800, rate=100)
     want = _want(synth.QUERIES[cfg], b)
     got, _ = run_node(synth.QUERIES[cfg], _split(b, [0, 50_000, 50_001, 170_000, 240_000]), gpus, 40_000,
-                      synth.raw_symbols)
+                      synth.raw_symbols, key_dict=key_dict)
+    assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_node_device_dictionary_rebuild_and_sentinel(gpus):
+    """The device dictionary (csrc/keydict.hip) at 2.5M keys: the first 4M-row chunk brings more new keys than half
+    its initial 4M-slot table, so the table is rebuilt 4x larger and the chunk re-probed; one symbol's raw value is
+    the table's empty-slot sentinel (INT64_MIN) and lives in the extra slot.  Keys get first-seen ids node-wide."""
+    cfg = "C2"
+    b = synth_batch(cfg, 0, 8_000_000, keys=3_000_000, rate=10_000)
+    want = _want(synth.QUERIES[cfg], b)
+    assert len(want) > 100_000
+
+    def raw_of(k):
+        r = synth.raw_symbols(k)
+        return np.where(k == k[17], np.iinfo(np.int64).min, r)
+    got, st = run_node(synth.QUERIES[cfg], [b], gpus, 4_000_000, raw_of, threads=8, key_dict=2)
     assert_same(got, want)
 
 

@@ -310,3 +310,38 @@ def test_seq_speculative_units(name, spec):
     want = run_engine(OracleEngine, q, [b])
     got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True, spec=spec), q, split(b, [3000, 3001, 9000]))
     assert_same(got, want)
+
+
+def _long_seq(k):
+    els = ", ".join(f"e{i}=S[v>=0]" for i in range(1, k + 1))
+    return HEAD + PART + f"from every {els} select e1.id as i1, e{k}.id as ik insert into M; end;"
+
+
+@pytest.mark.parametrize("k,ok", [(5, 1), (6, 0)])
+def test_seq_rule_pool_bound_always_matching(k, ok):
+    """Sequence lanes hold at most PQ_MAX_P = 6 partials: one per non-start element's newAndEvery list, the start
+    state's every-clone and one allocated inside a step.  An always-matching k-element sequence fills exactly that, so
+    the rule takes 5 elements and leaves 6 to the per-key machine; both stay exact across pushes."""
+    import ctypes as ct
+    lib = _load()
+    q = _long_seq(k)
+    assert lib.hi_seq_rule(ct.byref(N.build_desc(L.lower(context(q))))) == ok
+    b = small_batch(6_000, 7, 100, 4, seed=5 + k)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(b, [1000, 1001, 3500]))
+    assert len(want) > 1000
+    assert_same(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_pushes_beyond_the_row_budget_are_split(monkeypatch):
+    """Tie components hold a combined row in 27 bits: a push whose rows (carried rows included) pass that budget runs
+    as consecutive sub-pushes on the route instead of failing (budget lowered to 30k rows here), first push included."""
+    from siddhi_amd._native import GpuEngine
+    monkeypatch.setenv("SG_PP_ROW_BUDGET", "30000")   # (rate 10/ms: about 10k rows inside `within 1 sec` are carried)
+    q = synth.QUERIES["C3c"]
+    g = synth.generate("C3c", 0, 200_000, keys=500, rate=10)
+    b = Batch(200_000, 0, g["ts"], np.zeros(200_000, np.int32), dense_first_seen(g["key"]),
+              [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
+    want = run_engine(OracleEngine, q, [b])
+    assert_same(run_engine(GpuEngine, q, split(b, [100_000, 100_007])), want)
