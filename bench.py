@@ -294,6 +294,110 @@ def _ctx(cfg):
     return L.make_context(app, app.queries[0], None, {})
 
 
+# SURVEY.md §8d algorithmic bytes per config: (whole path B/event, B/match, predicate pass B/event)
+#   C1: ts 8 + price 4 + bit; C2/C5: + key 4; 36 B/match (trigger 8, rank 4, ts 8, two slot indices 8+8)
+#   C3b/C3c: ts 8 + key 4 + v 4 + w 4 + bits; 92 B/match (trigger, rank, ts, 4 slots x 8, 5 projected x 8)
+#   C4: ts 8 + id 8 (no local predicate: no predicate pass); 28 B per emission (one slot)
+PATH_BYTES = {"C1": (12.125, 36.0, 4.125), "C2": (16.125, 36.0, 4.125), "C5": (16.125, 36.0, 4.125),
+              "C3b": (20.125, 92.0, 8.125), "C3c": (20.125, 92.0, 8.125), "C3": (20.125, 92.0, 4.125),
+              "C4": (16.0, 28.0, None)}
+
+
+def roofline_of(cfg, n, matches, kern, stage):
+    """`roofline` of one push: the §8d whole-path algorithmic bytes over the dominant kernel's HIP-event time (and
+    over the sum of the push's kernels), plus the predicate-evaluation pass."""
+    per_ev, per_m, pred_b = PATH_BYTES[cfg]
+    path_bytes = per_ev * n + per_m * matches
+    dominant = max(kern, key=kern.get) if kern else None
+    t_dom = kern.get(dominant, 0.0)
+    dom_gbs = path_bytes / (t_dom * 1e-3) / 1e9 if t_dom else 0.0
+    path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9 if stage[4] else 0.0
+    roof = {"bound": "hbm", "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": dominant, "kernel_ms": round(t_dom, 4),
+            "algorithmic_GB_per_launch": round(path_bytes / 1e9, 4),
+            "bytes_definition": "SURVEY.md §8d whole-path algorithmic bytes (%.3f B/event + %.0f B/match) over the "
+                                "dominant kernel's HIP-event time" % (per_ev, per_m),
+            "path": {"achieved": round(path_gbs, 1), "frac": round(path_gbs / HBM_PEAK_GBS, 4),
+                     "kernels_total_ms": round(float(stage[4]), 4)},
+            "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])}}
+    if "pred" in kern and pred_b:
+        pg = pred_b * n / (kern["pred"] * 1e-3) / 1e9
+        roof["pred_eval_pass"] = {"achieved": round(pg, 1), "frac": round(pg / HBM_PEAK_GBS, 4),
+                                  "bytes_per_event": pred_b, "ms": round(kern["pred"], 4)}
+    return roof
+
+
+def measure_push(cfg, rank, n, keys, rate, dev, steps, warmup, sync_ranks=False):
+    """K timed sg_push steps of one batch resident in HBM (fresh state each step), HIP-event kernel times."""
+    g, key, cols = synth_columns(cfg, rank, n, keys, rate, dev)
+    torch.cuda.synchronize()
+    keep = []
+    h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
+    partitioned = "partition with" in synth.QUERIES[cfg]
+    batch = N.make_batch(n, rank * n, g["ts"].data_ptr(), 0, key.data_ptr(), [c.data_ptr() for c in cols],
+                         [0] * len(cols), 1, keys if partitioned else 1, keep)
+    stream = torch.cuda.current_stream()
+    h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
+    tick = int(synth.T0 + (n - 1) // rate + 5001)   # C4: the final Tick fires every remaining timer (SURVEY.md §8d)
+
+    def step():
+        h.reset()
+        h.push(batch)
+        if cfg.startswith("C4"):
+            h.advance_time(tick, rank * n + n)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if sync_ranks:
+        barrier()
+    torch.cuda.synchronize()
+    stage = np.zeros(5)
+    kern = {}
+    matches = spilled = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        t = h.timing()
+        stage += [t.pred_ms, t.partition_ms, t.match_ms, t.output_ms, t.total_ms]
+        for name, ms in t.kernels():
+            kern[name] = kern.get(name, 0.0) + ms
+        matches = h.pending() if cfg.startswith("C4") else t.matches
+        spilled = t.spilled_units
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if sync_ranks:
+        elapsed = reduce_max(elapsed)
+        barrier()
+    h.close()
+    del g, key, cols
+    torch.cuda.empty_cache()
+    return {"elapsed": elapsed, "stage": stage / steps, "kern": {k: v / steps for k, v in kern.items()},
+            "matches": matches, "spilled": spilled}
+
+
+CPU_SAMPLE = {"C1": 1_000_000, "C2": 12_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000, "C5": 3_000_000}
+
+
+def config_line(cfg, dev, steps, warmup, cpu):
+    """One BASELINE config beside the headline: its own push timing, roofline with its own §8d bytes, and the
+    oracle on a bounded sample of the same stream (1 thread)."""
+    _, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
+    n = min(n_cfg, 100_000_000)
+    m = measure_push(cfg, 0, n, keys, rate, dev, steps, warmup)
+    ms = 1000.0 * m["elapsed"] / steps
+    out = {"workload": f"{cfg}: " + synth.QUERIES[cfg], "events": n, "keys": keys, "rate_events_per_ms": rate,
+           "matches": int(m["matches"]), "steps": steps, "ms_per_push": round(ms, 3),
+           "value": round(n / (ms * 1e-3), 1), "unit": "events/s",
+           "roofline": roofline_of(cfg, n, m["matches"], m["kern"], m["stage"])}
+    if cpu:
+        sample = CPU_SAMPLE[cfg] // 4
+        r, nm, dt = cpu_baseline(cfg, sample, keys, rate)
+        out["cpu_baseline"] = {"value": round(r, 1), "unit": "events/s", "cores": 1, "kind": "port",
+                               "sample": f"first {sample} events, oracle single thread, {nm} matches, {dt:.1f}s"}
+    return out
+
+
 def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
     """BASELINE configs[4] as it is worded: ONE 1B-event, 1M-key C5 stream sharded by key hash across the node's
     ranks (strong scaling: the stream is the same at every N).  Every rank generates the global stream in HBM chunk
@@ -369,6 +473,9 @@ def main():
     ap.add_argument("--c5-node-steps", type=int, default=2,
                     help="steps of the 1B-event C5 stream through the node pipeline, rank 0 driving every GPU (0: skip)")
     ap.add_argument("--node-threads", type=int, default=0, help="host threads of the node pipeline (0: 16 per GPU)")
+    ap.add_argument("--other-configs", default="C1,C3b,C3c,C4",
+                    help="BASELINE configs measured beside the headline (one GPU, rank 0; '' to skip)")
+    ap.add_argument("--other-steps", type=int, default=3)
     ap.add_argument("--pmc", default=DEFAULT_PMC, help="rocprofv3 PMC summary of this command (profiles/collect_r02.sh)")
     args = ap.parse_args()
 
@@ -380,52 +487,13 @@ def main():
         dist.init_process_group("gloo")
     cfg = args.config
     if not args.cpu_sample:
-        args.cpu_sample = {"C1": 1_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000,
-                           "C5": 3_000_000}.get(cfg, 12_000_000)
+        args.cpu_sample = CPU_SAMPLE.get(cfg, 12_000_000)
     num, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
     n = args.events or min(n_cfg, 100_000_000)
 
     # ---- value: inputs resident in HBM (each rank's keys are its own dense ids 0..K-1, siddhi_amd/router.py)
-    g, key, cols = synth_columns(cfg, rank, n, keys, rate, dev)
-    torch.cuda.synchronize()
-    keep = []
-    h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
-    batch = N.make_batch(n, rank * n, g["ts"].data_ptr(), 0, key.data_ptr(), [c.data_ptr() for c in cols],
-                         [0] * len(cols), 1, keys, keep)
-    stream = torch.cuda.current_stream()
-    h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
-
-    def step():
-        h.reset()
-        h.push(batch)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    stage = np.zeros(5)
-    kern = {}
-    matches = spilled = 0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        t = h.timing()
-        stage += [t.pred_ms, t.partition_ms, t.match_ms, t.output_ms, t.total_ms]
-        for name, ms in t.kernels():
-            kern[name] = kern.get(name, 0.0) + ms
-        matches = t.matches
-        spilled = t.spilled_units
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if ws > 1:
-        elapsed = reduce_max(elapsed)
-        barrier()
-    stage /= args.steps
-    kern = {k: v / args.steps for k, v in kern.items()}
-    h.close()
-    del g, key, cols
-    torch.cuda.empty_cache()
+    m = measure_push(cfg, rank, n, keys, rate, dev, args.steps, args.warmup, sync_ranks=ws > 1)
+    elapsed, stage, kern, matches, spilled = m["elapsed"], m["stage"], m["kern"], m["matches"], m["spilled"]
 
     # ---- whole_node (§8d) on this rank's stream, its own GPU through the node pipeline (max over ranks)
     wn = None
@@ -460,28 +528,8 @@ def main():
     ms_step = elapsed * 1000.0 / args.steps
     value = ws * n * args.steps / elapsed
 
-    # algorithmic bytes: predicate pass 4.125 B/event (price read + condition bit);
-    # whole path 16.125 B/event (ts 8 + key 4 + price 4 + bit) + 36 B/match (C1: no key, 12.125);
-    # C4 (no local predicate): ts 8 + id 8 B/event + 28 B/emission
-    per_ev, per_m = {"C1": (12.125, 36.0), "C4": (16.0, 28.0)}.get(cfg[:2], (16.125, 36.0))
-    path_bytes = per_ev * n + per_m * matches
-    dominant = max(kern, key=kern.get) if kern else None
-    t_dom = kern.get(dominant, 0.0)
-    dom_gbs = path_bytes / (t_dom * 1e-3) / 1e9 if t_dom else 0.0
-    path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9 if stage[4] else 0.0
-    roof = {"bound": "hbm", "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": dominant, "kernel_ms": round(t_dom, 4),
-            "algorithmic_GB_per_launch": round(path_bytes / 1e9, 4),
-            "bytes_definition": "SURVEY.md §8d whole-path algorithmic bytes (%.3f B/event + %.0f B/match) over the "
-                                "dominant kernel's HIP-event time" % (per_ev, per_m),
-            "path": {"achieved": round(path_gbs, 1), "frac": round(path_gbs / HBM_PEAK_GBS, 4),
-                     "kernels_total_ms": round(float(stage[4]), 4)},
-            "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])}}
-    if "pred" in kern and not cfg.startswith("C4"):
-        pg = 4.125 * n / (kern["pred"] * 1e-3) / 1e9
-        roof["pred_eval_pass"] = {"achieved": round(pg, 1), "frac": round(pg / HBM_PEAK_GBS, 4),
-                                  "bytes_per_event": 4.125, "ms": round(kern["pred"], 4)}
+    roof = roofline_of(cfg, n, matches, kern, stage)
+    dominant = roof["kernel"]
     tr, why = pmc_traffic(args.pmc, cfg, n, dominant)
     if tr is not None:
         roof["traffic"] = tr["dominant_GB"]
@@ -508,6 +556,13 @@ def main():
         except Exception as e:  # report, never fake
             cpu = {"value": None, "unit": "events/s", "cores": 1, "kind": "port", "sample": f"failed: {e}",
                    "nproc": hi["nproc"], "cpu_model": hi["cpu_model"]}
+    others = {}
+    if args.other_configs:
+        for oc in [c for c in args.other_configs.split(",") if c and c != cfg]:
+            try:
+                others[oc] = config_line(oc, dev, args.other_steps, 1, not args.no_cpu)
+            except Exception as e:   # report, never fake
+                others[oc] = {"error": str(e)}
     line = {
         "metric": "events/sec (whole node) for partitioned pattern query at 1/2/4/8 GPUs; % HBM peak",
         "value": round(value, 1), "unit": "events/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
@@ -522,6 +577,7 @@ def main():
         "c5_whole_node": c5w,
         "roofline": roof,
         "cpu_baseline": cpu,
+        "configs": others,
         "source_hash": source_hash(cfg),
     }
     print(json.dumps(line))

@@ -173,6 +173,8 @@ typedef struct sg_options {
   int32_t partial_lanes;    /* general engine, patterns whose partial matches never interact (every e1 -> ... within T
                                over stream / count / logical states of one stream): 0 = one GPU lane per partial
                                match while timestamps never decrease, -1 = always the per-key machine (testing) */
+  int32_t no_direct;        /* closed form: 1 = match records always through the projection kernel instead of being
+                               written by the record walk itself (testing both paths) */
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)
@@ -330,7 +332,8 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
 int sg_node_push(sg_node* nd, const sg_node_batch* b, const sg_match_columns* out, int64_t cap, int64_t* n);
 int sg_node_reset(sg_node* nd);   /* new stream: forget keys and per-key state */
 /* Where partition keys are dictionary-encoded (first-seen dense ids, PartitionRuntime.cloneIfNotExist,
- * C/partition/PartitionRuntime.java:255-308): 0 auto (the device unless the query has playback timers), 1 the host
+ * C/partition/PartitionRuntime.java:255-308): 0 auto (the device when the first push's first 64K rows hold more than
+ * 16K distinct keys and the query has no playback timers, else the host), 1 the host
  * router (sg_router), 2 one dictionary per GPU in HBM (raw keys are uploaded; with several GPUs rows go to shard
  * mix64(raw) mod n_gpus).  Only before the first push of a stream. */
 int sg_node_set_key_dict(sg_node* nd, int mode);

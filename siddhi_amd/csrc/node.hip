@@ -155,7 +155,7 @@ struct Pinned {
 
 // One shard's rows of one chunk, in arrival order (host staging, G > 1).
 struct NodeStage {
-  Pinned ts, key, stream, gidx, raw;   // (raw: device-dictionary mode, the key as received)
+  Pinned ts, ts32, key, stream, gidx, raw;   // (ts32: the chunk's timestamps as 32-bit offsets from its minimum)   // (raw: device-dictionary mode, the key as received)
   Pinned col[SG_MAX_COLS], nul[SG_MAX_COLS];
 };
 
@@ -181,13 +181,17 @@ struct sg_node {
   int64_t local_rows[MAX_GPUS] = {};   // rows each shard has seen (its local event index space)
   int64_t next_index = 0;
   bool broken = false;
-  bool no_fill = false;              // testing: ship every column back instead of filling trigger-row columns on the host
+  bool no_fill = false;
+  bool no_ts32 = false;              // testing: timestamps always travel as 8 bytes              // testing: ship every column back instead of filling trigger-row columns on the host
   // per-GPU device-side ingress slots and copy stream
   hipStream_t cp[MAX_GPUS] = {};
   hipEvent_t ev_copied[MAX_GPUS][2] = {}, ev_used[MAX_GPUS][2] = {};
   SlotPtrs dslot[MAX_GPUS][2];       // device ingress slots (resolved once, before the pipeline's threads start)
   // host staging: route slot per chunk (G = 1: the routed key column; G > 1: per-shard rows)
   Pinned keyslot[NODE_RING];
+  Pinned tsslot[NODE_RING];          // G = 1: the chunk's timestamps as 32-bit offsets
+  int32_t* dts32[MAX_GPUS][2] = {};  // device slots of the 32-bit offsets
+  int64_t dts32_rows = 0;
   std::vector<int32_t> dense_tmp[NODE_RING];
   NodeStage stage[NODE_RING][MAX_GPUS];
   NodeRing ring[MAX_GPUS];
@@ -296,6 +300,9 @@ struct Run {
   // device-dictionary mode, per (chunk, shard): the shard's key count before the chunk and the first rows of the
   // keys the chunk introduced, in id order (G > 1: merged into node-wide first-seen ids)
   std::vector<int64_t> kbase_of;
+  // per chunk: timestamps travel as 32-bit offsets from ts_base_of[j] when the chunk spans less than 2^31 ms
+  std::vector<int64_t> ts_base_of;
+  std::vector<uint8_t> ts32_of;
   std::vector<std::vector<uint32_t>> newf_of;
   double t_route = 0, t_merge = 0, t_gpu[MAX_GPUS] = {};
   int64_t h2d_bytes = 0, d2h_bytes = 0;
@@ -346,6 +353,43 @@ bool need_clocks(const sg_nfa_desc& d) { return d.playback && d.n_sched > 0; }
 // unchanged time fires nothing)
 inline bool is_clock_point(const Run& r, int64_t lo, int64_t slice_a, int64_t i) {
   return i == slice_a || r.b.ts[lo + i] != r.b.ts[lo + i - 1];
+}
+
+// Chunk j's timestamps as 32-bit offsets from its first row's when every row is within 2^31 ms of it (G = 1:
+// written into the host slot in the same pass; G > 1: by the scatter).  Halves the timestamp column's PCIe bytes.
+void ts_prepare(Run& r, int64_t j) {
+  sg_node& nd = r.nd;
+  const int slot = (int)(j % NODE_RING);
+  const int64_t lo = chunk_lo(r, j), hi = chunk_lo(r, j + 1), n = hi - lo;
+  r.ts32_of[j] = 0;
+  if (n <= 0 || nd.no_ts32) return;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, n / 65536 + 1));
+  const int64_t* ts = r.b.ts + lo;
+  const int64_t base = ts[0];
+  int32_t* o = nd.G == 1 ? nd.tsslot[slot].as<int32_t>() : nullptr;
+  std::atomic<bool> wide(false);
+  nd.pool->parallel_for(T, [&](int t) {
+    const int64_t a = n * t / T, e = n * (t + 1) / T;
+    uint64_t bad = 0;
+    if (o) {
+      for (int64_t i = a; i < e; ++i) {
+        const int64_t d = ts[i] - base;
+        bad |= (uint64_t)(d + 0x80000000ll) >> 32;   // nonzero unless INT32_MIN <= d <= INT32_MAX
+        o[i] = (int32_t)d;
+      }
+    } else {
+      for (int64_t i = a; i < e; ++i) bad |= (uint64_t)(ts[i] - base + 0x80000000ll) >> 32;
+    }
+    if (bad) wide = true;
+  });
+  r.ts_base_of[j] = base;
+  r.ts32_of[j] = wide ? 0 : 1;
+}
+
+// staged timestamp of shard row p of chunk j
+inline void put_ts(const Run& r, NodeStage& S, int64_t j, int64_t p, int64_t ts) {
+  if (r.ts32_of[j]) S.ts32.as<int32_t>()[p] = (int32_t)(ts - r.ts_base_of[j]);
+  else S.ts.as<int64_t>()[p] = ts;
 }
 
 // ---- device-dictionary mode: no key lookups on the host.  G = 1: nothing to do; G > 1: rows are scattered to
@@ -407,7 +451,7 @@ void route_chunk_dev(Run& r, int64_t j) {
         if (own >= 0 && q != own) continue;
         NodeStage& S = nd.stage[slot][q];
         const int64_t p = cur[q]++;
-        S.ts.as<int64_t>()[p] = r.b.ts[lo + i];
+        put_ts(r, S, j, p, r.b.ts[lo + i]);
         S.raw.as<int64_t>()[p] = raw[i];
         if (stream) S.stream.as<int32_t>()[p] = stream[i];
         S.gidx.as<uint64_t>()[p] = r.b.base_index + (uint64_t)(lo + i);
@@ -424,6 +468,7 @@ void route_chunk_dev(Run& r, int64_t j) {
 
 // ---- route (+ scatter) of chunk j into host slot j % NODE_RING --------------------------------------------------
 void route_chunk(Run& r, int64_t j) {
+  ts_prepare(r, j);
   if (r.nd.ddict == 1) {
     route_chunk_dev(r, j);
     return;
@@ -547,7 +592,7 @@ void route_chunk(Run& r, int64_t j) {
         const bool clock = s != own;   // a clock-only row on a shard that does not own the row
         NodeStage& S = nd.stage[slot][s];
         const int64_t p = cur[s]++;
-        S.ts.as<int64_t>()[p] = r.b.ts[lo + i];
+        put_ts(r, S, j, p, r.b.ts[lo + i]);
         S.key.as<int32_t>()[p] = clock ? -1 : lc[x];
         if (stage_stream) S.stream.as<int32_t>()[p] = clock ? -1 : (stream ? stream[i] : 0);
         S.gidx.as<uint64_t>()[p] = r.b.base_index + (uint64_t)(lo + i);
@@ -586,7 +631,7 @@ sg_batch shard_batch(Run& r, int64_t j, int s, const void** cols, const uint8_t*
   if (nd.G == 1) {
     const int64_t lo = chunk_lo(r, j);
     sb.base_index = r.b.base_index + (uint64_t)lo;
-    sb.ts = r.b.ts + lo;
+    sb.ts = r.ts32_of[j] ? nullptr : r.b.ts + lo;
     sb.stream = r.b.stream ? r.b.stream + lo : nullptr;
     sb.key = nd.ddict == 1 ? nullptr : nd.keyslot[slot].as<int32_t>();   // (device mode: raw keys go up instead)
     bool nul = false;
@@ -601,7 +646,7 @@ sg_batch shard_batch(Run& r, int64_t j, int s, const void** cols, const uint8_t*
   }
   NodeStage& S = nd.stage[slot][s];
   sb.base_index = (uint64_t)r.lbase_of[j * nd.G + s];   // local index space: the host maps triggers back through gidx
-  sb.ts = S.ts.as<int64_t>();
+  sb.ts = r.ts32_of[j] ? nullptr : S.ts.as<int64_t>();
   sb.stream = (r.b.stream || need_clocks(d)) ? S.stream.as<int32_t>() : nullptr;
   sb.key = nd.ddict == 1 ? nullptr : S.key.as<int32_t>();
   bool nul = false;
@@ -630,6 +675,10 @@ void copy_loop(Run& r, int s) {
       // (the slot's buffers were reserved for a whole chunk before the pipeline started: no workspace-map access
       // from this thread)
       if (sb.n > 0) sg_upload_to(nd.desc, nd.dslot[s][ds], &sb, 0, sb.n, nd.cp[s]);
+      if (sb.n > 0 && r.ts32_of[j]) {
+        const int32_t* t32 = nd.G == 1 ? nd.tsslot[j % NODE_RING].as<int32_t>() : nd.stage[j % NODE_RING][s].ts32.as<int32_t>();
+        HIPCHK(hipMemcpyAsync(nd.dts32[s][ds], t32, 4 * (size_t)sb.n, hipMemcpyHostToDevice, nd.cp[s]));
+      }
       if (sb.n > 0 && nd.ddict == 1) {
         const int64_t* rk = nd.G == 1 ? r.b.raw_key + chunk_lo(r, j) : nd.stage[j % NODE_RING][s].raw.as<int64_t>();
         HIPCHK(hipMemcpyAsync(nd.draw[s][ds], rk, 8 * (size_t)sb.n, hipMemcpyHostToDevice, nd.cp[s]));
@@ -637,7 +686,7 @@ void copy_loop(Run& r, int s) {
       HIPCHK(hipEventRecord(nd.ev_copied[s][ds], nd.cp[s]));
       r.publish([&] { r.issued[s] = j + 1; });
       HIPCHK(hipEventSynchronize(nd.ev_copied[s][ds]));
-      int64_t bytes = 8 * sb.n + (sb.stream ? 4 * sb.n : 0) + (nd.ddict == 1 ? 8 : 4) * sb.n;
+      int64_t bytes = (r.ts32_of[j] ? 4 : 8) * sb.n + (sb.stream ? 4 * sb.n : 0) + (nd.ddict == 1 ? 8 : 4) * sb.n;
       for (int c = 0; c < nd.desc.n_cols; ++c) {
         if (sb.cols[c]) bytes += (int64_t)sg_col_width(nd.desc.col_type[c]) * sb.n;
         if (sb.nulls && sb.nulls[c]) bytes += sb.n;
@@ -648,6 +697,11 @@ void copy_loop(Run& r, int s) {
 }
 
 // ---- per-GPU compute + deliver thread --------------------------------------------------------------------------
+__global__ void k_ts_widen(const int32_t* __restrict__ d, int64_t base, int64_t n, int64_t* __restrict__ ts) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ts[i] = base + (int64_t)d[i];
+}
+
 struct Dst {   // where delivered rows go: the caller's columns (G = 1) or the shard's ring (G > 1)
   uint64_t* trig;
   int64_t* ts;
@@ -748,6 +802,11 @@ void gpu_loop(Run& r, int s) {
         bv.stream = sb.stream ? (const int32_t*)sp.stream : nullptr;
         bv.key = (const int32_t*)sp.key;
         bv.index = nullptr;
+        if (r.ts32_of[j]) {   // widen the 32-bit offsets into the slot's timestamp column
+          hipLaunchKernelGGL(k_ts_widen, dim3((unsigned)std::min<int64_t>((sb.n + 255) / 256, 8192)), dim3(256), 0,
+                             h.stream, (const int32_t*)nd.dts32[s][ds], r.ts_base_of[j], sb.n, (int64_t*)sp.ts);
+          HIPCHK(hipGetLastError());
+        }
         if (nd.ddict == 1) {   // dictionary-encode the chunk's raw keys on this GPU
           const int64_t before = nd.kd[s].n_keys;
           std::vector<uint32_t> nf;
@@ -956,7 +1015,10 @@ void reserve_all(Run& r) {
   int need[SG_MAX_COLS] = {};
   for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
   for (int q = 0; q < NODE_RING; ++q) {
-    if (nd.G == 1) nd.keyslot[q].ensure((size_t)C * 4);
+    if (nd.G == 1) {
+      nd.keyslot[q].ensure((size_t)C * 4);
+      nd.tsslot[q].ensure((size_t)C * 4);
+    }
     else {
       if ((int64_t)nd.dense_tmp[q].size() < C) nd.dense_tmp[q].resize((size_t)C);
       for (int s = 0; s < nd.G; ++s) {
@@ -964,6 +1026,7 @@ void reserve_all(Run& r) {
         S.ts.ensure((size_t)C * 8);
         S.key.ensure((size_t)C * 4);
         S.gidx.ensure((size_t)C * 8);
+        S.ts32.ensure((size_t)C * 4);
         if (nd.ddict == 1) S.raw.ensure((size_t)C * 8);
         if (r.b.stream || need_clocks(d)) S.stream.ensure((size_t)C * 4);
         for (int c = 0; c < d.n_cols; ++c) {
@@ -995,6 +1058,12 @@ void reserve_all(Run& r) {
     sb.cols = cols;
     sb.nulls = nul ? nuls : nullptr;
     for (int ds = 0; ds < 2; ++ds) nd.dslot[s][ds] = sg_reserve_slot(h, &sb, C, ds);
+    if (nd.dts32_rows < C)
+      for (int ds = 0; ds < 2; ++ds) {
+        if (nd.dts32[s][ds]) HIPCHK(hipFree(nd.dts32[s][ds]));
+        nd.dts32[s][ds] = nullptr;
+        HIPCHK(hipMalloc((void**)&nd.dts32[s][ds], (size_t)C * 4));
+      }
     if (nd.ddict == 1 && nd.draw_rows < C)
       for (int ds = 0; ds < 2; ++ds) {
         if (nd.draw[s][ds]) HIPCHK(hipFree(nd.draw[s][ds]));
@@ -1005,6 +1074,7 @@ void reserve_all(Run& r) {
     sg_egress_init(h);
   }
   if (nd.ddict == 1) nd.draw_rows = std::max(nd.draw_rows, C);
+  nd.dts32_rows = std::max(nd.dts32_rows, C);
   // shard rings: room for two chunks' worth of matches per shard beyond the share of the output capacity
   if (nd.G > 1) {
     const int64_t M = std::max<int64_t>(1024, std::min<int64_t>(r.cap, r.cap / nd.G * 2 + 2 * C));
@@ -1023,6 +1093,21 @@ void reserve_all(Run& r) {
   }
 }
 
+// Auto key dictionary: a stream whose first 64K rows hold few distinct keys keeps its dictionary on the host (a
+// cache-resident table; the GPU then receives 4-byte dense ids instead of 8-byte raw keys); many keys (a DRAM-bound
+// table on the host) are encoded on the GPUs.
+bool few_keys(const sg_node_batch& b) {
+  const int64_t m = std::min<int64_t>(b.n, 65536);
+  sgr::KeyMap seen;
+  seen.init(1 << 17);
+  int64_t distinct = 0;
+  for (int64_t i = 0; i < m; ++i) {
+    if (b.stream && b.stream[i] < 0) continue;
+    if (seen.insert(b.raw_key[i], 0) < 0 && ++distinct > 16384) return false;
+  }
+  return true;
+}
+
 void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, int64_t cap, int64_t* n_out) {
   Run r(nd, b, out, cap);
   r.w = want_of(nd, b, out);
@@ -1036,9 +1121,14 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
   r.rows_of.assign((size_t)(r.nch * nd.G), 0);
   r.lbase_of.assign((size_t)(r.nch * nd.G), 0);
   r.kb_of.assign((size_t)(r.nch * nd.G), 1);
-  if (nd.ddict < 0)   // the first push of a stream fixes where keys are encoded
-    nd.ddict = (nd.desc.partitioned && !need_clocks(nd.desc) && nd.key_dict_mode != 1) ? 1 : 0;
+  if (nd.ddict < 0) {   // the first push of a stream fixes where keys are encoded
+    const bool dev_ok = nd.desc.partitioned && !need_clocks(nd.desc);
+    nd.ddict = (dev_ok && nd.key_dict_mode == 2) ? 1 : 0;
+    if (dev_ok && nd.key_dict_mode == 0) nd.ddict = few_keys(b) ? 0 : 1;
+  }
   r.kbase_of.assign((size_t)(r.nch * nd.G), 0);
+  r.ts_base_of.assign((size_t)r.nch, 0);
+  r.ts32_of.assign((size_t)r.nch, 0);
   r.newf_of.assign((size_t)(r.nch * nd.G), std::vector<uint32_t>());
   const double t0 = now_ms();
   reserve_all(r);
@@ -1106,8 +1196,10 @@ void close_node(sg_node* nd) {
   for (int s = 0; s < nd->G; ++s) {
     hipSetDevice(nd->dev[s]);
     kd_free(nd->kd[s]);
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < 2; ++k) {
       if (nd->draw[s][k]) hipFree(nd->draw[s][k]);
+      if (nd->dts32[s][k]) hipFree(nd->dts32[s][k]);
+    }
     if (nd->h[s]) sg_close(nd->h[s]);
     if (nd->cp[s]) hipStreamDestroy(nd->cp[s]);
     for (int k = 0; k < 2; ++k) {
@@ -1139,6 +1231,7 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
   nd->threads = host_threads ? host_threads : (int)std::max(1u, std::thread::hardware_concurrency());
   nd->chunk_rows = chunk_rows;
   nd->no_fill = getenv("SG_NODE_NO_FILL") != nullptr;
+  nd->no_ts32 = getenv("SG_NODE_NO_TS32") != nullptr;
   memset(&nd->st, 0, sizeof(nd->st));
   int rc = SG_OK;
   for (int s = 0; s < n_gpus && rc == SG_OK; ++s) {

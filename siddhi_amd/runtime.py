@@ -164,6 +164,46 @@ def _key_string(v, t):
     return str(v)
 
 
+def _query_streams(query: C.Query) -> set:
+    """Stream ids the query's state elements read."""
+    out = set()
+
+    def walk(el):
+        if isinstance(el, (C.StreamStateElement, C.AbsentStreamStateElement)):
+            out.add(el.stream_id)
+        elif isinstance(el, C.NextStateElement):
+            walk(el.current)
+            walk(el.next)
+        elif isinstance(el, (C.EveryStateElement, C.CountStateElement)):
+            walk(el.inner)
+        elif isinstance(el, C.LogicalStateElement):
+            walk(el.e1)
+            walk(el.e2)
+    walk(query.input.element)
+    return out
+
+
+def _broadcast(b: "Batch", bcast: np.ndarray, keys_before: int) -> "Batch":
+    """Rows of a stream that is not partitioned but read inside a partition reach every partition instance that
+    exists when they arrive (PartitionStreamReceiver.receive with no partition executor -> send(event) to every
+    cached per-key junction, C/partition/PartitionStreamReceiver.java:83-92,277-281): such a row (bcast) becomes one
+    row per key seen before it, all with the row's event index.  The reference visits the instances in its
+    ConcurrentHashMap order; here they come in first-seen key order (the order every other per-trigger tie uses)."""
+    n = b.n
+    seen = np.maximum.accumulate(np.where(bcast, -1, b.key.astype(np.int64)))   # highest id seen so far
+    before = np.maximum(np.concatenate([[keys_before - 1], seen[:-1]]), keys_before - 1) + 1
+    reps = np.where(bcast, before, 1).astype(np.int64)
+    idx = np.repeat(np.arange(n, dtype=np.int64), reps)
+    key = b.key[idx].copy()
+    starts = np.cumsum(reps) - reps
+    within = np.arange(len(idx), dtype=np.int64) - np.repeat(starts, reps)
+    bi = bcast[idx]
+    key[bi] = within[bi].astype(np.int32)
+    index = (np.uint64(b.base_index) + idx.astype(np.uint64)) if b.index is None else b.index[idx]
+    return Batch(len(idx), b.base_index, b.ts[idx], b.stream[idx], key, [c[idx] for c in b.cols],
+                 [None if x is None else x[idx] for x in b.nulls], index=index)
+
+
 class _QueryRuntime:
     def __init__(self, app_rt: "SiddhiAppRuntime", query: C.Query, partition: Optional[C.Partition],
                  engine_factory):
@@ -171,6 +211,12 @@ class _QueryRuntime:
         self.query = query
         self.partition = partition
         self.ctx = L.make_context(app_rt.app, query, partition, app_rt.strings)
+        # streams read inside the partition without a partition key: broadcast to every instance
+        self.global_streams = set()
+        if partition is not None:
+            reads = _query_streams(query)
+            self.global_streams = {i for i, sid in enumerate(self.ctx.stream_ids)
+                                   if sid in reads and self.ctx.key_attr[i] < 0}
         self.sel_types = [self._select_type(oa.expr) for oa in query.select]
         self.engine = engine_factory(self.ctx)
         self.query_callbacks: List[QueryCallback] = []
@@ -401,7 +447,11 @@ class SiddhiAppRuntime:
                 key = self._dense_keys(qi, allcols[self._col_base(stream) + ai], t)
             else:
                 key = np.zeros(n, np.int32) if not q.ctx.partitioned else np.full(n, -1, np.int32)
-            q.engine.push(Batch(n, base, ts, stream_col, key, allcols, nulls))
+            b = Batch(n, base, ts, stream_col, key, allcols, nulls)
+            if stream in q.global_streams:
+                b = _broadcast(b, np.ones(n, bool), len(self.key_dicts[qi]))
+            if b.n:
+                q.engine.push(b)
             self._deliver(q, q.engine.fetch())
 
     def _col_base(self, stream: int) -> int:
@@ -467,8 +517,12 @@ class SiddhiAppRuntime:
                 nulls.append(nul)
         for qi, q in enumerate(self.queries):
             key = np.full(n, -1, dtype=np.int32)
+            bcast = None
             if q.ctx.partitioned:
                 kd = self.key_dicts[qi]
+                keys_before = len(kd)
+                if q.global_streams:
+                    bcast = np.fromiter((r[0] in q.global_streams for r in rows), dtype=bool, count=n)
                 for i, r in enumerate(rows):
                     s = r[0]
                     if s < 0 or q.ctx.key_attr[s] < 0:
@@ -486,7 +540,10 @@ class SiddhiAppRuntime:
             else:
                 key[:] = 0
             b = Batch(n, base, ts, stream, key, cols, nulls)
-            q.engine.push(b)
+            if bcast is not None and bcast.any():
+                b = _broadcast(b, bcast, keys_before)
+            if b.n:
+                q.engine.push(b)
             self._deliver(q, q.engine.fetch())
 
     # -- output

@@ -1,6 +1,7 @@
 """Known-answer tests transcribed from the reference's Java suites (data in tests/golden/ref_kats.json, made by
 tests/golden/make_ref_kats.py).  Each case is the test's action list up to its count assertion -- `send`,
-`sleep` (ms), `wait_in_events` (TestUtil.waitForInEvents, T/TestUtil.java:237-247) -- the rows the test asserts
+`sleep` (ms), `wait_in_events` (TestUtil.waitForInEvents, T/TestUtil.java:237-247), `wait_events`
+(SiddhiTestHelper.waitForEvents, C/util/SiddhiTestHelper.java:49-57) -- the rows the test asserts
 (in order, T/TestUtil.java:124-143, or an inline callback's assertArrayEquals sequence) and the asserted
 in-event count.  Wall-clock tests (clock "wall") run in playback with the clock advanced in 1 ms heartbeats
 (SiddhiAppRuntime.advance_time -> sg_advance_time) through every sleep, starting at 1 ms: an event's timestamp
@@ -41,9 +42,12 @@ REF_KATS = load()
 
 def check(case, rows):
     """The reference test's assertions: in-event count, and the expected rows in order (a prefix when the test
-    lists fewer rows than it counts)."""
+    lists fewer rows than it counts; every row when the test asserts one row inside its per-event loop)."""
     assert len(rows) == case["expect_count"], (len(rows), case["expect_count"], rows)
     exp = case["expect"]
+    if case.get("expect_every"):
+        assert all(r == exp[0] for r in rows), (rows, exp)
+        return
     assert rows[:len(exp)] == exp, (rows, exp)
 
 
@@ -92,5 +96,13 @@ def run_ref_kat(case, engine):
                 rt.flush()
                 if len(rows) == 1:
                     break
+        elif wall and a[0] == "wait_events":   # SiddhiTestHelper.waitForEvents(sleep, expected, count, timeout)
+            _, step, expected, timeout = a
+            rt.flush()
+            waited = 0
+            while len(rows) < expected and waited <= timeout:
+                sleep(step)
+                waited += step
+                rt.flush()
     rt.shutdown()
     return rows, tss

@@ -225,3 +225,20 @@ def test_node_c5_300m_two_shards_three_pushes():
     want = sharded_oracle(synth.QUERIES[cfg], b, max(2, min(16, os.cpu_count() or 2)))
     assert len(got) == len(want) > 0
     assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("ts32", [True, False])
+def test_node_timestamp_offsets_and_wide_chunks(ts32, monkeypatch):
+    """Chunk timestamps travel as 32-bit offsets from the chunk's minimum; a chunk spanning 2^31 ms or more (here a
+    35-day gap in the middle of the stream) ships them as 8 bytes.  SG_NODE_NO_TS32 forces 8 bytes everywhere."""
+    if not ts32:
+        monkeypatch.setenv("SG_NODE_NO_TS32", "1")
+    cfg = "C2"
+    b = synth_batch(cfg, 0, 200_000, keys=700, rate=100)
+    b.ts = b.ts.copy()
+    b.ts[90_000:] += 3_000_000_000
+    want = _want(synth.QUERIES[cfg], b)
+    for gpus in (1, 2):
+        got, _ = run_node(synth.QUERIES[cfg], [b], gpus, 40_000, synth.raw_symbols)
+        assert_same(got, want)
