@@ -175,6 +175,9 @@ typedef struct sg_options {
                                match while timestamps never decrease, -1 = always the per-key machine (testing) */
   int32_t no_direct;        /* closed form: 1 = match records always through the projection kernel instead of being
                                written by the record walk itself (testing both paths) */
+  int32_t no_grow;          /* general machine: 1 = a push that runs out of a key's pool / list / timer capacity or of
+                               emission space fails with SG_ECAPACITY instead of being rolled back and rerun with 4x the
+                               capacity (testing) */
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)

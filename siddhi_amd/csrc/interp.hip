@@ -41,6 +41,7 @@ struct GeneralState {
   PartialState* pp = nullptr; // partial-lane route (partial.hip) while the query and the stream allow it
   int pp_checked = 0;
   int64_t max_ts = INT64_MIN;  // largest timestamp pushed (INT64_MAX once a timestamp went back)
+  int64_t grows = 0;           // capacity growths (pushes rerun with larger pools / lists / emission space)
 };
 
 __global__ void k_route(int64_t n, const int32_t* __restrict__ stream, const int32_t* __restrict__ key,
@@ -320,6 +321,50 @@ __global__ void k_unit_keep(int64_t nkeys, const uint32_t* __restrict__ uoff, co
   }
 }
 
+// A key's runtime moved into a larger arena geometry (capacity growth): lists, pools and timer FIFOs keep their
+// entries at the same indices (pool entries are addressed by index, never by arena offset); the new pool entries
+// are put on the free lists and each timer FIFO is unrolled to start at 0.  One block per key.
+__global__ void k_regeo(int64_t nkeys, const int32_t* __restrict__ old_arena, SgGeo og, int32_t* __restrict__ new_arena,
+                        SgGeo ng) {
+  for (int64_t k = blockIdx.x; k < nkeys; k += gridDim.x) {
+    const int32_t* o = old_arena + (size_t)k * og.key_words;
+    int32_t* a = new_arena + (size_t)k * ng.key_words;
+    const int hw = sg_hdr_words(og.S);
+    for (int w = threadIdx.x; w < hw; w += blockDim.x) a[w] = o[w];
+    for (int l = 0; l < 2 * og.S; ++l)
+      for (int w = threadIdx.x; w <= og.L; w += blockDim.x) a[ng.off_lists + l * (ng.L + 1) + w] = o[og.off_lists + l * (og.L + 1) + w];
+    for (int w = threadIdx.x; w < og.P * og.part_words; w += blockDim.x) a[ng.off_part + w] = o[og.off_part + w];
+    for (int w = threadIdx.x; w < og.E * og.ev_words; w += blockDim.x) a[ng.off_ev + w] = o[og.off_ev + w];
+    for (int w = threadIdx.x; w < og.C * 3; w += blockDim.x) a[ng.off_chain + w] = o[og.off_chain + w];
+    // new pool entries: a chain ending in the old free list, pushed in front of it
+    for (int p = og.P + threadIdx.x; p < ng.P; p += blockDim.x)
+      a[ng.off_part + p * ng.part_words + 2] = p + 1 < ng.P ? p + 1 : o[K_FREE_P];
+    for (int e = og.E + threadIdx.x; e < ng.E; e += blockDim.x)
+      a[ng.off_ev + e * ng.ev_words + 5] = e + 1 < ng.E ? e + 1 : o[K_FREE_E];
+    for (int c = og.C + threadIdx.x; c < ng.C; c += blockDim.x)
+      a[ng.off_chain + c * 3 + 2] = c + 1 < ng.C ? c + 1 : o[K_FREE_C];
+    for (int i = 0; i < og.A; ++i) {
+      const int32_t* oq = o + og.off_timer + i * (2 + 2 * og.Q);
+      int32_t* nq = a + ng.off_timer + i * (2 + 2 * ng.Q);
+      const int32_t head = oq[0], cnt = oq[1];
+      for (int j = threadIdx.x; j < cnt; j += blockDim.x) {
+        const int src = (head + j) % og.Q;
+        nq[2 + 2 * j] = oq[2 + 2 * src];
+        nq[3 + 2 * j] = oq[3 + 2 * src];
+      }
+      if (threadIdx.x == 0) {
+        nq[0] = 0;
+        nq[1] = cnt;
+      }
+    }
+    if (threadIdx.x == 0 && o[K_CREATED]) {
+      if (ng.P > og.P) { a[K_FREE_P] = og.P; a[K_NFREE_P] = o[K_NFREE_P] + (ng.P - og.P); }
+      if (ng.E > og.E) { a[K_FREE_E] = og.E; a[K_NFREE_E] = o[K_NFREE_E] + (ng.E - og.E); }
+      if (ng.C > og.C) { a[K_FREE_C] = og.C; a[K_NFREE_C] = o[K_NFREE_C] + (ng.C - og.C); }
+    }
+  }
+}
+
 __global__ void k_sortkeys(int64_t n, const char* __restrict__ buf, int32_t stride, uint64_t* __restrict__ sk,
                            uint32_t* __restrict__ idx) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -426,6 +471,36 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
   run_machine(h, bv, n);
 }
 
+// Move every key's runtime into geometry ng (larger pools / lists / timer FIFOs).
+static void regeo(SgHandle* h, GeneralState* gs, const SgGeo& ng) {
+  hipStream_t st = h->stream;
+  const SgGeo og = gs->geo;
+  if (gs->arena && gs->keys_alloc > 0) {
+    const size_t bytes = (size_t)gs->keys_alloc * (size_t)ng.key_words * 4;
+    int32_t* na = nullptr;
+    if (hipMalloc(&na, bytes) != hipSuccess)
+      throw SgError(SG_ECAPACITY, "cannot allocate grown per-key NFA arenas (" + std::to_string(bytes >> 20) + " MiB)");
+    HIPCHK(hipMemsetAsync(na, 0, bytes, st));
+    hipLaunchKernelGGL(k_regeo, dim3((unsigned)std::min<int64_t>(gs->keys_alloc, 65535)), dim3(256), 0, st,
+                       gs->keys_alloc, gs->arena, og, na, ng);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    hipFree(gs->arena);
+    gs->arena = na;
+  }
+  gs->geo = ng;
+  HIPCHK(hipMemcpy(gs->dgeo, &gs->geo, sizeof(SgGeo), hipMemcpyHostToDevice));
+}
+
+// the next geometry when a key's pools, lists or timer FIFOs ran out: 4x each (as far as int32 indices allow)
+static bool grown_geo(const sg_nfa_desc& d, const SgGeo& g, SgGeo& ng) {
+  const int64_t lim = (int64_t)1 << 22;
+  if ((int64_t)g.P * 4 > lim && (int64_t)g.L * 4 > lim) return false;
+  auto up = [&](int32_t x) { return (int32_t)std::min<int64_t>(lim, std::max<int64_t>(4, (int64_t)x * 4)); };
+  ng = sg_make_geo(d, up(g.P), up(g.E), up(g.C), up(g.L), up(g.Q));
+  return ng.key_words < ((int64_t)1 << 31);
+}
+
 static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
@@ -487,12 +562,9 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
   // ---- per-key machines
   int32_t stride = sg_emit_stride(d.n_select);
   int64_t cap = n + 65536;
-  char* ebuf = (char*)h->ws.get("g_emit", (size_t)cap * stride, st);
+  char* ebuf = nullptr;
   unsigned long long* ecount = (unsigned long long*)h->ws.get("g_ecount", 16, st);
   int32_t* eover = (int32_t*)h->ws.get("g_eover", 4, st);
-  HIPCHK(hipMemsetAsync(ecount, 0, 8, st));
-  HIPCHK(hipMemsetAsync(eover, 0, 4, st));
-  HIPCHK(hipMemsetAsync(gs->dfail, 0, 4, st));
   int32_t oerr = 0;
   int64_t tfl[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(&oerr, order_err, 4, hipMemcpyDeviceToHost, st));
@@ -547,6 +619,17 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
     }
     if (any) h->kend();
   }
+  // The reference's lists are unbounded (StreamPreStateProcessor.java:58-59): a push that runs out of a key's pool,
+  // list or timer capacity, or out of emission space, is rolled back and rerun with 4x the capacity.
+  unsigned long long total = 0;
+  for (int attempt = 0;; ++attempt) {
+  const size_t pre_bytes = (size_t)kb * (size_t)gs->geo.key_words * 4;
+  int32_t* pre = (int32_t*)h->ws.get("g_pre", std::max<size_t>(pre_bytes, 4), st);
+  if (pre_bytes) HIPCHK(hipMemcpyAsync(pre, gs->arena, pre_bytes, hipMemcpyDeviceToDevice, st));
+  ebuf = (char*)h->ws.get("g_emit", (size_t)cap * stride, st);
+  HIPCHK(hipMemsetAsync(ecount, 0, 8, st));
+  HIPCHK(hipMemsetAsync(eover, 0, 4, st));
+  HIPCHK(hipMemsetAsync(gs->dfail, 0, 4, st));
   SgEmitSink sink;
   sink.buf = ebuf;
   sink.cap = cap;
@@ -614,16 +697,28 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   HIPCHK(hipGetLastError());
   h->mark(3);
-  unsigned long long total = 0;
+  total = 0;
   int32_t over = 0, fcode = 0;
   HIPCHK(hipMemcpyAsync(&total, ecount, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&over, eover, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&fcode, gs->dfail, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  SgGeo ng;
+  const bool grow_pools = fcode == SG_ECAPACITY && !h->opt.no_grow && grown_geo(d, gs->geo, ng);
+  const bool grow_emit = over && !fcode && !h->opt.no_grow && cap < ((int64_t)1 << 31);
+  if ((grow_pools || grow_emit) && attempt < 8) {
+    if (pre_bytes) HIPCHK(hipMemcpyAsync(gs->arena, pre, pre_bytes, hipMemcpyDeviceToDevice, st));   // roll back
+    if (grow_pools) regeo(h, gs, ng);
+    if (grow_emit) cap = std::min<int64_t>((int64_t)1 << 31, cap * 4);
+    ++gs->grows;
+    continue;
+  }
   if (fcode) throw SgError(fcode, fcode == SG_ECAPACITY
                                       ? "per-key pool/list capacity exceeded (raise sg_options pool_* / list_cap)"
                                       : "query shape hits a reference failure path (see DESIGN.md)");
   if (over) throw SgError(SG_ECAPACITY, "match buffer overflow: push smaller batches");
+  break;
+  }
   // ---- order matches by (trigger, timer-before-event, key) keeping per-key emission order
   if (total) {
     uint64_t* sk = (uint64_t*)h->ws.get("g_sk", 8 * total, st);
@@ -723,9 +818,19 @@ void sg_general_restore(SgHandle* h, SnapR& r) {
   }
   SgGeo g = r.pod<SgGeo>();
   const SgGeo& m = gs->geo;
-  if (g.S != m.S || g.R != m.R || g.P != m.P || g.E != m.E || g.C != m.C || g.L != m.L || g.Q != m.Q ||
-      g.A != m.A || g.nsel != m.nsel || g.key_words != m.key_words)
-    throw SgError(SG_EINVAL, "snapshot: per-key arena geometry differs (pool / list options must match)");
+  if (g.S != m.S || g.R != m.R || g.A != m.A || g.nsel != m.nsel)
+    throw SgError(SG_EINVAL, "snapshot: per-key arena geometry differs (another query)");
+  const SgGeo want = sg_make_geo(h->desc, g.P, g.E, g.C, g.L, g.Q);
+  if (want.key_words != g.key_words) throw SgError(SG_EINVAL, "snapshot: inconsistent arena geometry");
+  if (g.key_words != m.key_words || g.P != m.P || g.E != m.E || g.C != m.C || g.L != m.L || g.Q != m.Q) {
+    // the snapshot's runtimes had grown (or this handle's have): adopt the snapshot's geometry
+    HIPCHK(hipStreamSynchronize(st));
+    if (gs->arena) hipFree(gs->arena);
+    gs->arena = nullptr;
+    gs->keys_alloc = 0;
+    gs->geo = g;
+    HIPCHK(hipMemcpy(gs->dgeo, &gs->geo, sizeof(SgGeo), hipMemcpyHostToDevice));
+  }
   if (keys > gs->keys_alloc) {
     size_t bytes = (size_t)keys * (size_t)gs->geo.key_words * 4;
     int32_t* na = nullptr;

@@ -1,0 +1,58 @@
+"""Capacity growth instead of failed pushes.  The reference's pending lists are unbounded LinkedLists
+(C/query/input/stream/state/StreamPreStateProcessor.java:58-59): one key holding tens of thousands of live partial
+matches is a valid stream.  The per-key machine (csrc/interp.hip) starts from fixed pools (256 partials per key);
+a push that runs out of a key's pool, list or timer capacity -- or of emission space -- is rolled back and rerun
+with 4x the capacity, every key's runtime moved into the larger geometry (k_regeo).  Every route must give the
+oracle's rows on a stream with one such skewed key."""
+import numpy as np
+import pytest
+
+from oracle import OracleEngine
+from parity_util import assert_same, run_engine
+from siddhi_amd import synth
+from siddhi_amd.runtime import Batch
+
+pytestmark = pytest.mark.gpu
+
+Q = ("define stream S (id long, symbol string, v int, w int); partition with (symbol of S) begin @info(name='q') "
+     "from every e1=S[v>0] -> e2=S[v > e1.v + 5000] within 1 hour "
+     "select e1.id as i1, e2.id as i2, e1.v as v1 insert into M; end;")
+
+
+def skewed(hot=12_000, cold_keys=50, cold=2_000, seed=3):
+    """Key 0 gets `hot` rows whose partials never complete until one last row completes all of them; other keys
+    get light traffic (some matches of their own)."""
+    rng = np.random.default_rng(seed)
+    n = hot + cold + 1
+    key = np.concatenate([np.zeros(hot, np.int32), rng.integers(1, cold_keys + 1, cold).astype(np.int32),
+                          np.zeros(1, np.int32)])
+    v = np.concatenate([rng.integers(1, 1000, hot), rng.integers(1, 9000, cold), [10_000_000]]).astype(np.int32)
+    order = np.concatenate([rng.permutation(hot + cold), [hot + cold]])
+    key, v = key[order], v[order]
+    ts = (synth.T0 + np.arange(n) // 10).astype(np.int64)
+    ids = np.arange(n, dtype=np.int64)
+    from parity_util import dense_first_seen
+    k = dense_first_seen(key)
+    return Batch(n, 0, ts, np.zeros(n, np.int32), k, [ids, k, v, np.zeros(n, np.int32)], [None] * 4)
+
+
+@pytest.mark.timeout(600)
+def test_skewed_key_every_route():
+    from siddhi_amd._native import GpuEngine
+    b = skewed()
+    want = run_engine(OracleEngine, Q, [b])
+    assert len(want) > 12_000            # the last row completes every partial of the hot key
+    halves = [Batch(h - l, l, b.ts[l:h], b.stream[l:h], b.key[l:h], [c[l:h] for c in b.cols], [None] * 4)
+              for l, h in ((0, 7_000), (7_000, b.n))]
+    for kw in ({}, {"force_general": True, "partial_lanes": -1}):
+        assert_same(run_engine(lambda ctx: GpuEngine(ctx, **kw), Q, [b]), want)
+        assert_same(run_engine(lambda ctx: GpuEngine(ctx, **kw), Q, halves), want)
+
+
+@pytest.mark.timeout(300)
+def test_machine_without_growth_still_reports_capacity():
+    from siddhi_amd._native import GpuEngine, SgError
+    b = skewed(hot=2_000, cold=200)
+    with pytest.raises(SgError) as ei:
+        run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=-1, no_grow=True), Q, [b])
+    assert ei.value.code == -3
