@@ -207,6 +207,8 @@ def synth_columns(cfg, rank, n, keys, rate, dev):
     key = g["key"].to(torch.int32) if "key" in g else torch.zeros(n, dtype=torch.int32, device=dev)
     if cfg.startswith("C4"):     # S(id, seq) rows only (the Tick stream's column is never read)
         cols = [g["id"], g["seq"], torch.zeros(n, dtype=torch.int32, device=dev)]
+    elif cfg.startswith("PP"):   # Stream1 / Stream2 (symbol, price, volume)
+        cols = [key, g["price"], key] * 2
     elif cfg.startswith("C3"):
         cols = [g["id"], key, g["v"], g["w"]]
     else:
@@ -299,6 +301,7 @@ def _ctx(cfg):
 #   C3b/C3c: ts 8 + key 4 + v 4 + w 4 + bits; 92 B/match (trigger, rank, ts, 4 slots x 8, 5 projected x 8)
 #   C4: ts 8 + id 8 (no local predicate: no predicate pass); 28 B per emission (one slot)
 PATH_BYTES = {"C1": (12.125, 36.0, 4.125), "C2": (16.125, 36.0, 4.125), "C5": (16.125, 36.0, 4.125),
+              "PP": (20.125, 36.0, 4.125), "PPe": (20.125, 36.0, 4.125),   # + the stream column (4 B)
               "C3b": (20.125, 92.0, 8.125), "C3c": (20.125, 92.0, 8.125), "C3": (20.125, 92.0, 4.125),
               "C4": (16.0, 28.0, None)}
 
@@ -335,8 +338,8 @@ def measure_push(cfg, rank, n, keys, rate, dev, steps, warmup, sync_ranks=False)
     keep = []
     h, nfa = make_handle(cfg)   # each step is a complete stream: no state carried between steps
     partitioned = "partition with" in synth.QUERIES[cfg]
-    batch = N.make_batch(n, rank * n, g["ts"].data_ptr(), 0, key.data_ptr(), [c.data_ptr() for c in cols],
-                         [0] * len(cols), 1, keys if partitioned else 1, keep)
+    batch = N.make_batch(n, rank * n, g["ts"].data_ptr(), g["stream"].data_ptr() if "stream" in g else 0, key.data_ptr(),
+                         [c.data_ptr() for c in cols], [0] * len(cols), 1, keys if partitioned else 1, keep)
     stream = torch.cuda.current_stream()
     h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
     tick = int(synth.T0 + (n - 1) // rate + 5001)   # C4: the final Tick fires every remaining timer
@@ -376,13 +379,13 @@ def measure_push(cfg, rank, n, keys, rate, dev, steps, warmup, sync_ranks=False)
             "matches": matches, "spilled": spilled}
 
 
-CPU_SAMPLE = {"C1": 1_000_000, "C2": 12_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000, "C5": 3_000_000}
+CPU_SAMPLE = {"PP": 12_000_000, "PPe": 12_000_000, "C1": 1_000_000, "C2": 12_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000, "C5": 3_000_000}
 
 
 def config_line(cfg, dev, steps, warmup, cpu):
     """One BASELINE config beside the headline: its own push timing, roofline with its own §8d bytes, and the
     oracle on a bounded sample of the same stream (1 thread)."""
-    _, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
+    _, n_cfg, keys, rate = synth.CONFIGS[synth._base(cfg)]
     n = min(n_cfg, 100_000_000)
     m = measure_push(cfg, 0, n, keys, rate, dev, steps, warmup)
     ms = 1000.0 * m["elapsed"] / steps
@@ -488,7 +491,7 @@ def main():
     cfg = args.config
     if not args.cpu_sample:
         args.cpu_sample = CPU_SAMPLE.get(cfg, 12_000_000)
-    num, n_cfg, keys, rate = synth.CONFIGS[cfg[:2]]
+    num, n_cfg, keys, rate = synth.CONFIGS[synth._base(cfg)]
     n = args.events or min(n_cfg, 100_000_000)
 
     # ---- value: inputs resident in HBM (each rank's keys are its own dense ids 0..K-1, siddhi_amd/router.py)

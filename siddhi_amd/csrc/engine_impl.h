@@ -2130,7 +2130,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     ms.narrow = (N && sizeof(T) == 4) ? 1 : 0;
     ms.cap = total;
     // direct emission when every select column comes from the pending list or the trigger's own record
-    bool direct = !h->opt.no_direct;
+    bool direct = h->opt.direct_emit != 0;
     for (int s = 0; s < d.n_select && direct; ++s) {
       const int kind = plan.pp.kind[s];
       const bool s2 = plan.pp.src[s] != 0;

@@ -27,6 +27,7 @@
 struct SgGeo {
   int32_t S, R, P, E, C, L, Q, A, nsel;
   int32_t off_lists, off_part, off_ev, off_chain, off_timer;
+  int32_t off_scratch;        // 3 lists' worth of step scratch (partials a state returns / emits / re-arms in one step)
   int32_t part_words, ev_words, list_words;
   int64_t key_words;
 };
@@ -90,6 +91,9 @@ struct KeyMachine {
   SG_HD int32_t* ev(int e) { return a + g->off_ev + e * g->ev_words; }
   SG_HD int32_t* chain(int c) { return a + g->off_chain + c * 3; }
   SG_HD int32_t* tq(int ai) { return a + g->off_timer + ai * (2 + 2 * g->Q); }
+  // step scratch: a state's list can return / emit / re-arm all its partials in one step (the reference collects
+  // them in unbounded chunks), so these buffers are list-sized and grow with the lists
+  SG_HD int32_t* scratch(int i) { return a + g->off_scratch + i * (g->L + 1); }
   SG_HD static int64_t rd64(const int32_t* p) { return (int64_t)(((uint64_t)(uint32_t)p[1] << 32) | (uint32_t)p[0]); }
   SG_HD static void wr64(int32_t* p, int64_t v) { p[0] = (int32_t)(uint32_t)v; p[1] = (int32_t)(uint32_t)((uint64_t)v >> 32); }
   SG_HD int64_t pts(int p) { return rd64(part(p)); }
@@ -584,7 +588,7 @@ struct KeyMachine {
   SG_HD int within_every(int s) { return clone ? -1 : st(s).within_every; }
 
   // ---- processAndReturn; returned partials are appended to ret[]
-  SG_HD int process_and_return(int s, int e, int* ret, int retcap) {
+  SG_HD int process_and_return(int s, int e, int32_t* ret, int retcap) {
     const sg_state_desc& x = st(s);
     if (x.kind == SG_K_ABSENT && !sth(s)[H_ACTIVE]) return 0;
     if (x.kind == SG_K_ALOGICAL) { alogical_process(s, e); return 0; }
@@ -720,7 +724,7 @@ struct KeyMachine {
       update_state(s);
       int32_t* l = list(s, 0);
       int n = l[0], w = 0;
-      int emitted[64];
+      int32_t* emitted = scratch(1);
       int ne = 0;
       for (int r = 0; r < n && !failed; ++r) {
         int p = l[1 + r];
@@ -738,11 +742,11 @@ struct KeyMachine {
         if (passed) {
           const bool partner_bound = slot(p, x.partner) != SG_NIL;
           if (x.logical_type == 0 && partner_bound) {              // AND: partner received but did not send out
-            if (ne < 64) emitted[ne++] = p; else fail(SG_ECAPACITY);
+            if (ne < g->L) emitted[ne++] = p; else fail(SG_ECAPACITY);
           } else if (!partner_bound) {                               // OR: partner not received; AND: let it process
             if (own != SG_NIL) { fail(SG_EUNSUPPORTED); break; }     // (a chained absent slot is not representable)
             slot(p, s) = blank_event();
-            if (x.logical_type == 1) { if (ne < 64) emitted[ne++] = p; else fail(SG_ECAPACITY); }
+            if (x.logical_type == 1) { if (ne < g->L) emitted[ne++] = p; else fail(SG_ECAPACITY); }
           }
           continue;   // removed
         }
@@ -808,22 +812,22 @@ struct KeyMachine {
     move_nae(s);
     int32_t* l = list(s, 0);
     int n = l[0], w = 0;
-    int emitted[64];
+    int32_t* emitted = scratch(1);
     int ne = 0;
-    int reevery[64];
+    int32_t* reevery = scratch(2);
     int nre = 0;
     lst = rd64(sth(s) + H_LST_LO);
     int we = within_every(s);
     for (int r = 0; r < n; ++r) {
       int p = l[1 + r];
       if (is_expired(s, p, current)) {
-        if (we >= 0 && x.next_every != s) { if (nre < 64) reevery[nre++] = p; else fail(SG_ECAPACITY); }
+        if (we >= 0 && x.next_every != s) { if (nre < g->L) reevery[nre++] = p; else fail(SG_ECAPACITY); }
         continue;
       }
       int64_t t = pts(p);
       if ((t == -1 && current >= lst) || (t != -1 && current >= t + x.waiting_time)) {
         set_pts(p, current);
-        if (ne < 64) emitted[ne++] = p; else fail(SG_ECAPACITY);
+        if (ne < g->L) emitted[ne++] = p; else fail(SG_ECAPACITY);
         continue;
       }
       l[1 + w++] = p;
@@ -871,20 +875,21 @@ struct KeyMachine {
     if (ri < 0) return;
     const sg_receiver_desc& r = d->receivers[ri];
     phase = 1;
-    int ret[64];
+    int32_t* ret = scratch(0);
+    const int retcap = g->L;
     if (r.multi) {
       if (d->type == 0) { for (int k = 0; k < r.n; ++k) update_state(r.stab[k]); }
       else reset_and_update();
       for (int k = 0; k < r.n && !failed; ++k) {
         int s = r.pres[r.n - 1 - k];
-        int nr = process_and_return(s, e, ret, 64);
+        int nr = process_and_return(s, e, ret, retcap);
         group = (uint32_t)k;
         if (r.selector) for (int i = 0; i < nr; ++i) emit(ret[i]);
       }
     } else {
       if (d->type == 0) update_state(r.stab[0]);
       else reset_and_update();
-      int nr = process_and_return(r.pres[0], e, ret, 64);
+      int nr = process_and_return(r.pres[0], e, ret, retcap);
       for (int i = 0; i < nr; ++i) {
         group = 0x800000u | (uint32_t)i;
         if (r.selector) emit(ret[i]);
@@ -901,6 +906,22 @@ struct KeyMachine {
     x[4] = row.nullmask;
     for (int k = 0; k < g->R; ++k) wr64(x + 6 + 2 * k, row.vals[k]);
     return e;
+  }
+  // A PATTERN without `every` and without absence never gets a new partial once its first one has left the start
+  // state (StreamPreStateProcessor.init arms a start state only once unless an every re-arms it, :157-166): when every
+  // list is empty the runtime has ended, and the key's remaining rows change nothing.
+  SG_HD bool can_end() {
+    if (d->type != 0 || d->n_sched != 0) return false;
+    for (int s = 0; s < g->S; ++s)
+      if (st(s).next_every >= 0 || st(s).within_every >= 0 || st(s).kind == SG_K_ABSENT || st(s).kind == SG_K_ALOGICAL)
+        return false;
+    return true;
+  }
+  SG_HD bool ended() {
+    if (!hdr()[K_CREATED]) return false;
+    for (int s = 0; s < g->S; ++s)
+      if (list(s, 0)[0] || list(s, 1)[0]) return false;
+    return true;
   }
   SG_HD int64_t pos() { return rd64(hdr() + K_POS_LO); }
   SG_HD void set_pos(int64_t v) { wr64(hdr() + K_POS_LO, v); }
@@ -928,7 +949,9 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t em
   int64_t nown = rows.n_own();
   int64_t nrows = rows.n_rows();
   int64_t i = 0;
+  const bool can_end = m.can_end();
   while (!m.failed) {
+    if (can_end && m.ended()) break;   // (no timers either: nothing left to fire)
     int64_t lev = (i < nown) ? rows.own_local(i) : nrows;
     // earliest timer trigger of this key's schedulers
     int64_t ltim = nrows;
@@ -1065,6 +1088,8 @@ inline SgGeo sg_make_geo(const sg_nfa_desc& d, int P, int E, int C, int L, int Q
   off += C * 3;
   g.off_timer = off;
   off += g.A * (2 + 2 * Q);
+  g.off_scratch = off;
+  off += 3 * (L + 1);
   off = (off + 3) & ~3;
   g.key_words = off;
   return g;

@@ -18,9 +18,16 @@ def _load():
         srcs = [os.path.join(HERE, "harness.cpp"), os.path.join(ROOT, "siddhi_amd", "csrc", "interp.h"),
                 os.path.join(ROOT, "siddhi_amd", "csrc", "sg_device.h"), os.path.join(ROOT, "siddhi_amd", "csrc", "chain.h"),
                 os.path.join(ROOT, "siddhi_amd", "csrc", "seq.h")]
-        if not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(s) for s in srcs):
+        stale = lambda: not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(s) for s in srcs)  # noqa
+        if stale():
+            import fcntl
             os.makedirs(os.path.dirname(LIB), exist_ok=True)
-            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, srcs[0]], check=True)
+            with open(LIB + ".lock", "w") as lk:   # parallel test workers: one builds, the others wait for it
+                fcntl.flock(lk, fcntl.LOCK_EX)
+                if stale():
+                    tmp = f"{LIB}.{os.getpid()}.tmp"
+                    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", tmp, srcs[0]], check=True)
+                    os.replace(tmp, LIB)
         lib = ct.CDLL(LIB)
         P = ct.c_void_p
         lib.hi_open.restype = P

@@ -23,6 +23,9 @@ def synth_batch(cfg, start, count, keys=None, rate=None):
     if cfg.startswith("C4"):
         cols = [g["id"], g["seq"], np.zeros(n, np.int32)]       # S(id, seq), Tick(x)
         return Batch(n, start, g["ts"], np.zeros(n, np.int32), np.zeros(n, np.int32), cols, [None] * 3)
+    if cfg.startswith("PP"):   # Stream1 / Stream2 (symbol, price, volume): one column set per stream
+        cols = [g["key"], g["price"], g["key"]] * 2
+        return Batch(n, start, g["ts"], g["stream"], g["key"].astype(np.int32), cols, [None] * len(cols))
     if cfg.startswith("C3"):
         cols = [g["id"], g["key"], g["v"], g["w"]]
     else:

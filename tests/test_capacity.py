@@ -36,17 +36,33 @@ def skewed(hot=12_000, cold_keys=50, cold=2_000, seed=3):
     return Batch(n, 0, ts, np.zeros(n, np.int32), k, [ids, k, v, np.zeros(n, np.int32)], [None] * 4)
 
 
-@pytest.mark.timeout(600)
-def test_skewed_key_every_route():
+def _halves(b, cut):
+    return [Batch(h - l, l, b.ts[l:h], b.stream[l:h], b.key[l:h], [c[l:h] for c in b.cols], [None] * 4)
+            for l, h in ((0, cut), (cut, b.n))]
+
+
+@pytest.mark.timeout(300)
+def test_skewed_key_partial_lanes():
+    """20k live partials on one key: partial lanes run one lane per partial (no per-key pool)."""
     from siddhi_amd._native import GpuEngine
-    b = skewed()
+    b = skewed(hot=20_000)
     want = run_engine(OracleEngine, Q, [b])
-    assert len(want) > 12_000            # the last row completes every partial of the hot key
-    halves = [Batch(h - l, l, b.ts[l:h], b.stream[l:h], b.key[l:h], [c[l:h] for c in b.cols], [None] * 4)
-              for l, h in ((0, 7_000), (7_000, b.n))]
-    for kw in ({}, {"force_general": True, "partial_lanes": -1}):
-        assert_same(run_engine(lambda ctx: GpuEngine(ctx, **kw), Q, [b]), want)
-        assert_same(run_engine(lambda ctx: GpuEngine(ctx, **kw), Q, halves), want)
+    assert len(want) > 20_000            # the last row completes every partial of the hot key
+    assert_same(run_engine(GpuEngine, Q, [b]), want)
+    assert_same(run_engine(GpuEngine, Q, _halves(b, 11_000)), want)
+
+
+@pytest.mark.timeout(300)
+def test_skewed_key_machine_grows():
+    """3000 live partials on one key through the per-key machine (pools of 256 partials and lists of 256 entries at
+    first): the push is rolled back and rerun with 4x capacity until it fits -- in one push and across two."""
+    from siddhi_amd._native import GpuEngine
+    b = skewed(hot=3_000, cold=1_000)
+    want = run_engine(OracleEngine, Q, [b])
+    assert len(want) > 3_000
+    eng = lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=-1)   # noqa: E731
+    assert_same(run_engine(eng, Q, [b]), want)
+    assert_same(run_engine(eng, Q, _halves(b, 1_700)), want)
 
 
 @pytest.mark.timeout(300)

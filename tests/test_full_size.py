@@ -25,7 +25,9 @@ def _gpu_full(cfg, n, keys, rate, sort=0):
     dev = torch.device("cuda", 0)
     g = synth.generate_torch(cfg, 0, n, dev, keys=keys, rate=rate)
     key = g["key"].to(torch.int32)
-    if cfg.startswith("C3"):
+    if cfg.startswith("PP"):
+        cols = [key, g["price"], key] * 2
+    elif cfg.startswith("C3"):
         cols = [g["id"], key, g["v"], g["w"]]
     else:
         cols = [g["id"], key, g["price"]]
@@ -35,12 +37,13 @@ def _gpu_full(cfg, n, keys, rate, sort=0):
     opts.partition_sort = sort
     h = N.Handle(N.build_desc(nfa), device=0, options=opts)
     keep = []
-    b = N.make_batch(n, 0, g["ts"].data_ptr(), 0, key.data_ptr(), [c.data_ptr() for c in cols], [0] * len(cols),
-                     1, keys, keep)
+    b = N.make_batch(n, 0, g["ts"].data_ptr(), g["stream"].data_ptr() if "stream" in g else 0, key.data_ptr(),
+                     [c.data_ptr() for c in cols], [0] * len(cols), 1, keys, keep)
     h.push(b)
     tr, ts, ky, gr, vals, vn = h.poll(len(nfa.select))
     h.close()
-    host = {"ts": g["ts"].cpu().numpy(), "key": key.cpu().numpy(), "cols": [c.cpu().numpy() for c in cols]}
+    host = {"ts": g["ts"].cpu().numpy(), "key": key.cpu().numpy(), "cols": [c.cpu().numpy() for c in cols],
+            "stream": g["stream"].cpu().numpy() if "stream" in g else np.zeros(n, np.int32)}
     vnull = np.zeros((len(tr), len(nfa.select)), np.uint8)
     for k in range(len(nfa.select)):
         vnull[:, k] = (vn >> np.uint32(k)) & np.uint32(1)
@@ -64,7 +67,24 @@ def test_full_size_all_rows(cfg, n, keys, rate, expect, sort):
     from parity_util import sharded_oracle
     got, host = _gpu_full(cfg, n, keys, rate, sort)
     assert len(got) == expect                                       # the count bench.py reports
-    b = Batch(n, 0, host["ts"], np.zeros(n, np.int32), host["key"], host["cols"], [None] * len(host["cols"]))
+    b = Batch(n, 0, host["ts"], host["stream"], host["key"], host["cols"], [None] * len(host["cols"]))
+    del host
+    want = sharded_oracle(synth.QUERIES[cfg], b, _workers())
+    assert_same(got, want)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", ["PP", "PPe"])
+def test_full_size_pattern_partition_two_streams(cfg):
+    """PatternPartitionTestCase's two-stream shape (T/query/partition/PatternPartitionTestCase.java:54-64) at C2's
+    scale -- `from e1=Stream1[price>20] -> e2=Stream2[price>e1.price]` under partition with (volume of Stream1,
+    volume of Stream2), 100M events over 10k keys (PP: no `every`, the per-key machine; PPe: `every .. within 1
+    sec`, the two-stream closed form) -- every row against the key-sharded oracle."""
+    from parity_util import sharded_oracle
+    _, n, keys, rate = synth.CONFIGS["PP"]
+    got, host = _gpu_full(cfg, n, keys, rate)
+    assert len(got) > 0
+    b = Batch(n, 0, host["ts"], host["stream"], host["key"], host["cols"], [None] * len(host["cols"]))
     del host
     want = sharded_oracle(synth.QUERIES[cfg], b, _workers())
     assert_same(got, want)

@@ -45,8 +45,15 @@ def _build(name):
     defs, srcs = TARGETS[name]
     deps = DEPS + srcs
     if not os.path.exists(exe) or any(os.path.getmtime(exe) < os.path.getmtime(d) for d in deps):
+        import fcntl
         os.makedirs(BUILD, exist_ok=True)
-        subprocess.run(["g++"] + FLAGS + defs + [os.path.join(SAN, "driver.cpp")] + srcs + ["-o", exe], check=True)
+        with open(exe + ".lock", "w") as lk:   # parallel test workers: one builds, the others wait for it
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            if not os.path.exists(exe) or any(os.path.getmtime(exe) < os.path.getmtime(d) for d in deps):
+                tmp = f"{exe}.{os.getpid()}.tmp"
+                subprocess.run(["g++"] + FLAGS + defs + [os.path.join(SAN, "driver.cpp")] + srcs + ["-o", tmp],
+                               check=True)
+                os.replace(tmp, exe)
     return exe
 
 

@@ -74,11 +74,11 @@ class _Spy:
     spilled = []
     ring_cap = 0
     walker_only = False
-    no_direct = False
+    no_direct = True
 
     def __init__(self, ctx):
         from siddhi_amd._native import GpuEngine
-        self.e = GpuEngine(ctx, ring_cap=_Spy.ring_cap, walker_only=_Spy.walker_only, no_direct=_Spy.no_direct)
+        self.e = GpuEngine(ctx, ring_cap=_Spy.ring_cap, walker_only=_Spy.walker_only, direct_emit=not _Spy.no_direct)
 
     def push(self, b):
         self.e.push(b)
@@ -91,7 +91,7 @@ class _Spy:
         self.e.close()
 
 
-def check(app, batches, min_matches=1, expect_spill=None, ring_cap=0, walker_only=False, no_direct=False):
+def check(app, batches, min_matches=1, expect_spill=None, ring_cap=0, walker_only=False, no_direct=True):
     assert shape_of(app) == L.SHAPE_EVERY_NEXT_CMP, "case must exercise the closed-form walker"
     want = run_engine(OracleEngine, app, batches)
     _Spy.spilled = []
@@ -268,9 +268,9 @@ def test_unpartitioned_search_longer_than_limit():
 @pytest.mark.parametrize("no_direct", [False, True], ids=["direct", "projected"])
 @pytest.mark.parametrize("case", ["stack", "list", "spill", "carry", "nulls", "wide", "ints"])
 def test_direct_emission_and_projection_agree(case, no_direct):
-    """The record walk writes the final match records itself when every select column is e1's pending-list payload /
-    value or the trigger's own value / payload (MatchSink::put_rec); otherwise (and with no_direct) k_project builds
-    them from 16-byte intermediates.  Both against the oracle."""
+    """With direct_emit the record walk writes the final match records itself when every select column is e1's
+    pending-list payload / value or the trigger's own value / payload (MatchSink::put_rec); by default (and for other
+    selects) k_project builds them from 16-byte intermediates.  Both against the oracle."""
     if case == "stack":
         app = q_part("price > e1.price")
         check(app, [make_batch(app, 50_000, seed=31, keys=120, rate=20, values=PRICE_TIES)], no_direct=no_direct)
