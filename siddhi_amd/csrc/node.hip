@@ -203,6 +203,17 @@ struct sg_node {
   int64_t draw_rows = 0;
   std::vector<int32_t> l2g[MAX_GPUS];   // G > 1, device mode: shard-local id -> node-wide first-seen id
   int64_t g_keys = 0;
+  // Row tags (one GPU, closed form): the e1 attribute the query only projects (e.g. `e1.id`) never crosses PCIe --
+  // the GPU carries each row's event index mod 2^32 in its place (generated in HBM) and the host selector reads the
+  // attribute of the e1 row the tag names from the caller's columns, or, for rows of earlier pushes the engine still
+  // holds, from `hist` (kept at each push's end for exactly the carried rows' range).
+  int tag_col = -1;
+  bool tag_sel[SG_MAX_SELECT] = {};
+  sg_nfa_desc edesc;                 // what the engine runs (the tag column as INT)
+  Pinned tagbuf;
+  int64_t hist_lo = 0, hist_n = 0;
+  std::vector<int64_t> hist;
+  std::vector<uint8_t> hist_nul;
 };
 
 namespace {
@@ -216,6 +227,7 @@ namespace {
 // them from the caller's pinned input columns by global trigger index.
 struct Want {
   bool ts, key, grp, col[SG_MAX_SELECT], nul[SG_MAX_SELECT];
+  bool tag[SG_MAX_SELECT];      // e1.<tag column>: the GPU delivers the row tag (node tagbuf), the host the value
   int ns;
   int width[SG_MAX_SELECT];
   bool fill_ts;                 // out->ts from the trigger row's ts (host)
@@ -250,15 +262,45 @@ Want want_of(const sg_node& nd, const sg_node_batch& b, const sg_match_columns* 
       w.col[k] = w.nul[k] = false;
     }
   }
+  for (int k = 0; k < w.ns; ++k)
+    if (nd.tag_sel[k] && (w.col[k] || w.nul[k])) {
+      w.tag[k] = true;
+      w.col[k] = true;   // (D2H of the tag into tagbuf)
+      w.nul[k] = false;
+    }
   w.any_fill = w.fill_ts;
-  for (int k = 0; k < w.ns; ++k) w.any_fill |= w.fill_col[k] >= 0;
+  for (int k = 0; k < w.ns; ++k) w.any_fill |= w.fill_col[k] >= 0 || w.tag[k];
   return w;
 }
 
 // Host selector for the trigger-row columns of output rows [o0, o1): trig[] holds their global trigger indices.
 inline void fill_row(const sg_node_batch& b, const sg_nfa_desc& d, const Want& w, const sg_match_columns* out,
-                     int64_t o, uint64_t trig) {
+                     int64_t o, uint64_t trig, const sg_node* nd = nullptr) {
   const int64_t t = (int64_t)(trig - b.base_index);
+  if (nd && nd->tag_col >= 0) {   // e1's projected attribute through its row tag
+    const int c = nd->tag_col;
+    const int wc = sg_col_width(d.col_type[c]);
+    for (int k = 0; k < w.ns; ++k) {
+      if (!w.tag[k]) continue;
+      const uint32_t tag = nd->tagbuf.as<uint32_t>()[o];
+      const uint64_t g = trig - (uint64_t)(uint32_t)((uint32_t)trig - tag);   // e1 is at most 2^32 - 1 rows back
+      int64_t v = 0;
+      uint8_t nul = 0;
+      if (g >= b.base_index) {
+        const int64_t r = (int64_t)(g - b.base_index);
+        v = wc == 8 ? ((const int64_t*)b.cols[c])[r] : (int64_t)((const int32_t*)b.cols[c])[r];
+        nul = (b.nulls && b.nulls[c]) ? b.nulls[c][r] : 0;
+      } else if ((int64_t)g >= nd->hist_lo && (int64_t)g < nd->hist_lo + nd->hist_n) {
+        v = nd->hist[(size_t)((int64_t)g - nd->hist_lo)];
+        nul = nd->hist_nul.empty() ? 0 : nd->hist_nul[(size_t)((int64_t)g - nd->hist_lo)];
+      }
+      if (out->cols[k]) {
+        if (w.width[k] == 8) ((int64_t*)out->cols[k])[o] = v;
+        else ((int32_t*)out->cols[k])[o] = (int32_t)v;
+      }
+      if (out->nulls[k]) out->nulls[k][o] = nul;
+    }
+  }
   if (w.fill_ts) out->ts[o] = b.ts[t];
   for (int k = 0; k < w.ns; ++k) {
     const int c = w.fill_col[k];
@@ -638,6 +680,7 @@ sg_batch shard_batch(Run& r, int64_t j, int s, const void** cols, const uint8_t*
     for (int c = 0; c < d.n_cols; ++c) {
       cols[c] = (need[c] && r.b.cols[c]) ? (const char*)r.b.cols[c] + (size_t)sg_col_width(d.col_type[c]) * lo : nullptr;
       nuls[c] = (need[c] && r.b.nulls && r.b.nulls[c]) ? r.b.nulls[c] + lo : nullptr;
+      if (c == nd.tag_col) cols[c] = nuls[c] = nullptr;   // (tags are made in HBM)
       nul |= nuls[c] != nullptr;
     }
     sb.cols = cols;
@@ -697,6 +740,11 @@ void copy_loop(Run& r, int s) {
 }
 
 // ---- per-GPU compute + deliver thread --------------------------------------------------------------------------
+__global__ void k_row_tags(uint32_t base, int64_t n, uint32_t* __restrict__ tag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    tag[i] = base + (uint32_t)i;
+}
+
 __global__ void k_ts_widen(const int32_t* __restrict__ d, int64_t base, int64_t n, int64_t* __restrict__ ts) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     ts[i] = base + (int64_t)d[i];
@@ -768,7 +816,10 @@ void gpu_loop(Run& r, int s) {
       dst.ts = r.out->ts;
       dst.key = r.out->key;
       dst.grp = r.out->group;
-      for (int c = 0; c < r.w.ns; ++c) { dst.col[c] = r.out->cols[c]; dst.nul[c] = r.out->nulls[c]; }
+      for (int c = 0; c < r.w.ns; ++c) {
+        dst.col[c] = r.w.tag[c] ? nd.tagbuf.p : r.out->cols[c];
+        dst.nul[c] = r.w.tag[c] ? nullptr : r.out->nulls[c];
+      }
       dst.M = 0;
     } else {
       NodeRing& R = nd.ring[s];
@@ -802,6 +853,13 @@ void gpu_loop(Run& r, int s) {
         bv.stream = sb.stream ? (const int32_t*)sp.stream : nullptr;
         bv.key = (const int32_t*)sp.key;
         bv.index = nullptr;
+        if (nd.tag_col >= 0) {   // row tags: event index mod 2^32, in place of the projected-only column
+          bv.cols.col[nd.tag_col] = sp.col[nd.tag_col];
+          bv.cols.nul[nd.tag_col] = nullptr;
+          hipLaunchKernelGGL(k_row_tags, dim3((unsigned)std::min<int64_t>((sb.n + 255) / 256, 8192)), dim3(256), 0,
+                             h.stream, (uint32_t)(sb.base_index), sb.n, (uint32_t*)sp.col[nd.tag_col]);
+          HIPCHK(hipGetLastError());
+        }
         if (r.ts32_of[j]) {   // widen the 32-bit offsets into the slot's timestamp column
           hipLaunchKernelGGL(k_ts_widen, dim3((unsigned)std::min<int64_t>((sb.n + 255) / 256, 8192)), dim3(256), 0,
                              h.stream, (const int32_t*)nd.dts32[s][ds], r.ts_base_of[j], sb.n, (int64_t*)sp.ts);
@@ -976,7 +1034,7 @@ void fill_loop(Run& r) {
         const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, cnt / 65536 + 1));
         nd.pool->parallel_for(T, [&](int t) {
           const int64_t a = o0 + cnt * t / T, e = o0 + cnt * (t + 1) / T;
-          for (int64_t o = a; o < e; ++o) fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o]);
+          for (int64_t o = a; o < e; ++o) fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o], &nd);
         });
       }
       r.publish([&] {
@@ -1074,6 +1132,7 @@ void reserve_all(Run& r) {
     sg_egress_init(h);
   }
   if (nd.ddict == 1) nd.draw_rows = std::max(nd.draw_rows, C);
+  if (nd.tag_col >= 0) nd.tagbuf.ensure((size_t)std::max<int64_t>(r.cap, 1) * 4);
   nd.dts32_rows = std::max(nd.dts32_rows, C);
   // shard rings: room for two chunks' worth of matches per shard beyond the share of the output capacity
   if (nd.G > 1) {
@@ -1092,6 +1151,8 @@ void reserve_all(Run& r) {
     }
   }
 }
+
+void keep_history(sg_node& nd, const sg_node_batch& b);
 
 // Auto key dictionary: a stream whose first 64K rows hold few distinct keys keeps its dictionary on the host (a
 // cache-resident table; the GPU then receives 4-byte dense ids instead of 8-byte raw keys); many keys (a DRAM-bound
@@ -1175,6 +1236,7 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
     nd.broken = true;
     throw SgError(r.fail_code, r.fail_msg);
   }
+  if (nd.tag_col >= 0) keep_history(nd, b);
   const double t2 = now_ms();
   sg_node_stats& st = nd.st;
   st.total_ms = t2 - t1;
@@ -1212,6 +1274,87 @@ void close_node(sg_node* nd) {
   delete nd;
 }
 
+// The tag column of a closed-form query: the one batch column e1 contributes to the select besides the compared value
+// (LONG / INT), read by no predicate -- or -1.
+int tag_column(const sg_nfa_desc& d) {
+  if (d.shape != SG_SHAPE_EVERY_NEXT_CMP || d.n_out != 0) return -1;
+  const int a_state = d.shape_args[0];
+  const int val_a = d.ret_col[d.shape_args[4]], val_b = d.ret_col[d.shape_args[3]];
+  int c = -1;
+  for (int k = 0; k < d.n_select; ++k) {
+    if (d.sel_state[k] != a_state) continue;
+    const int col = d.ret_col[d.sel_ret[k]];
+    if (col == val_a) continue;
+    if (d.sel_index[k] != 0 && d.sel_index[k] != -1) return -1;
+    if (c >= 0 && c != col) return -1;
+    c = col;
+  }
+  if (c < 0 || c == val_b || (d.col_type[c] != SG_T_LONG && d.col_type[c] != SG_T_INT)) return -1;
+  auto reads = [&](int off, int len) {   // does a postfix program read column c?
+    for (int pc = off; pc < off + len;) {
+      const int64_t op = d.code[pc];
+      if (op == SG_OP_VAR) {
+        if (d.ret_col[d.code[pc + 3]] == c) return true;
+        pc += 5;
+      } else if (op == SG_OP_CONST || op == SG_OP_CMP || op == SG_OP_MATH) {
+        pc += 3;
+      } else {
+        pc += 1;
+      }
+    }
+    return false;
+  };
+  for (int s = 0; s < d.n_states; ++s)
+    if (reads(d.states[s].prog_off, d.states[s].prog_len)) return -1;
+  if (reads(d.shape_prog_off, d.shape_prog_len)) return -1;
+  return c;
+}
+
+// After a push: keep the tag column's values of the rows the engine still carries (the only earlier rows a later
+// match can name as e1): [push_end - lag, push_end) from the caller's columns and the previous history.
+void keep_history(sg_node& nd, const sg_node_batch& b) {
+  const int c = nd.tag_col;
+  const int64_t end = (int64_t)(b.base_index + (uint64_t)b.n);
+  HIPCHK(hipSetDevice(nd.dev[0]));
+  const int64_t lag = sg_every_next_carry_max_lag(&nd.h[0]->h, c, (uint32_t)end);
+  if (lag <= 0) {
+    nd.hist_n = 0;
+    return;
+  }
+  const int64_t lo = end - lag;
+  std::vector<int64_t> h((size_t)lag);
+  std::vector<uint8_t> hn;
+  const bool nul = (b.nulls && b.nulls[c]) || !nd.hist_nul.empty();
+  if (nul) hn.assign((size_t)lag, 0);
+  const int wc = sg_col_width(nd.desc.col_type[c]);
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, lag / 65536 + 1));
+  bool miss = false;
+  nd.pool->parallel_for(T, [&](int t) {
+    const int64_t a = lo + lag * t / T, e = lo + lag * (t + 1) / T;
+    for (int64_t g = a; g < e; ++g) {
+      int64_t v = 0;
+      uint8_t u = 0;
+      if (g >= (int64_t)b.base_index) {
+        const int64_t r = g - (int64_t)b.base_index;
+        v = wc == 8 ? ((const int64_t*)b.cols[c])[r] : (int64_t)((const int32_t*)b.cols[c])[r];
+        u = (b.nulls && b.nulls[c]) ? b.nulls[c][r] : 0;
+      } else if (g >= nd.hist_lo && g < nd.hist_lo + nd.hist_n) {
+        v = nd.hist[(size_t)(g - nd.hist_lo)];
+        u = nd.hist_nul.empty() ? 0 : nd.hist_nul[(size_t)(g - nd.hist_lo)];
+      } else {
+        miss = true;
+      }
+      h[(size_t)(g - lo)] = v;
+      if (nul) hn[(size_t)(g - lo)] = u;
+    }
+  });
+  if (miss) throw SgError(SG_EINVAL, "internal: a carried row is older than the node's tag history");
+  nd.hist.swap(h);
+  nd.hist_nul.swap(hn);
+  nd.hist_lo = lo;
+  nd.hist_n = lag;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1232,11 +1375,26 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
   nd->chunk_rows = chunk_rows;
   nd->no_fill = getenv("SG_NODE_NO_FILL") != nullptr;
   nd->no_ts32 = getenv("SG_NODE_NO_TS32") != nullptr;
+  nd->edesc = nd->desc;
+  if (n_gpus == 1 && !nd->no_fill && !getenv("SG_NODE_NO_TAG")) {
+    nd->tag_col = tag_column(nd->desc);
+    if (nd->tag_col >= 0) {
+      const int c = nd->tag_col;
+      nd->edesc.col_type[c] = SG_T_INT;
+      for (int k = 0; k < nd->desc.n_ret; ++k)
+        if (nd->desc.ret_col[k] == c) nd->edesc.ret_type[k] = SG_T_INT;
+      for (int k = 0; k < nd->desc.n_select; ++k)
+        if (nd->desc.ret_col[nd->desc.sel_ret[k]] == c) {
+          nd->edesc.sel_type[k] = SG_T_INT;
+          nd->tag_sel[k] = nd->desc.sel_state[k] == nd->desc.shape_args[0];
+        }
+    }
+  }
   memset(&nd->st, 0, sizeof(nd->st));
   int rc = SG_OK;
   for (int s = 0; s < n_gpus && rc == SG_OK; ++s) {
     nd->dev[s] = devices ? devices[s] : 0;
-    rc = sg_open(nd->dev[s], &nd->desc, &nd->opt, &nd->h[s]);
+    rc = sg_open(nd->dev[s], &nd->edesc, &nd->opt, &nd->h[s]);
     if (rc != SG_OK) {
       nd->err = nd->h[s] ? sg_last_error(nd->h[s]) : "sg_open failed";
       break;
@@ -1306,6 +1464,9 @@ int sg_node_reset(sg_node* nd) {
   }
   nd->g_keys = 0;
   nd->ddict = -1;
+  nd->hist_n = 0;
+  nd->hist.clear();
+  nd->hist_nul.clear();
   if (nd->router) sg_router_close(nd->router);
   nd->router = nullptr;
   const int x = sg_router_open(nd->G, nd->threads, &nd->router);

@@ -217,6 +217,7 @@ void sg_every_next_f64(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_i32(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_i64(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_reset(SgHandle* h);
+int64_t sg_every_next_carry_max_lag(SgHandle* h, int col, uint32_t ref);
 void sg_every_next_release(SgHandle* h);
 void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n);

@@ -242,3 +242,26 @@ def test_node_timestamp_offsets_and_wide_chunks(ts32, monkeypatch):
     for gpus in (1, 2):
         got, _ = run_node(synth.QUERIES[cfg], [b], gpus, 40_000, synth.raw_symbols)
         assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("tags", [True, False])
+def test_node_row_tags_reach_back_across_pushes(tags, monkeypatch):
+    """One GPU, closed form: `e1.id` (projected only) travels as the row's event index mod 2^32 and the host reads the
+    id of the e1 row it names -- from the caller's columns, or for rows of earlier pushes the engine still carries,
+    from the node's history.  Key X is quiet from row 1000 to row 80000 (10..800 ms), so its early rows are carried
+    through four pushes and complete matches in the fifth.  SG_NODE_NO_TAG ships the column instead."""
+    if not tags:
+        monkeypatch.setenv("SG_NODE_NO_TAG", "1")
+    cfg = "C2"
+    b = synth_batch(cfg, 0, 160_000, keys=600, rate=100)
+    b.key = b.key.copy()
+    x = b.key[3]
+    quiet = np.arange(1000, 80_000)
+    b.key[quiet[b.key[quiet] == x]] = (x + 1) % 600
+    b.cols[1] = b.key
+    want = _want(synth.QUERIES[cfg], b)
+    assert np.any((want.trigger >= 80_000) & (want.vals[:, 0] < 1000))   # e1 rows from the first push, matched in the fifth
+    got, _ = run_node(synth.QUERIES[cfg], _split(b, [0, 20_000, 40_000, 60_000, 80_000, 160_000]), 1, 30_000,
+                      synth.raw_symbols)
+    assert_same(got, want)
