@@ -173,9 +173,6 @@ typedef struct sg_options {
   int32_t partial_lanes;    /* general engine, patterns whose partial matches never interact (every e1 -> ... within T
                                over stream / count / logical states of one stream): 0 = one GPU lane per partial
                                match while timestamps never decrease, -1 = always the per-key machine (testing) */
-  int32_t direct_emit;      /* closed form: 1 = the record walk writes the final match records itself instead of
-                               16-byte intermediates for the projection kernel (measured slower on C2: scattered
-                               64-byte stores from divergent lanes; kept for testing both paths) */
   int32_t no_grow;          /* general machine: 1 = a push that runs out of a key's pool / list / timer capacity or of
                                emission space fails with SG_ECAPACITY instead of being rolled back and rerun with 4x the
                                capacity (testing) */

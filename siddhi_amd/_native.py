@@ -62,7 +62,7 @@ class sg_options(ct.Structure):
     _fields_ = [("max_batch", I64), ("pool_partials", I32), ("pool_events", I32), ("pool_chain", I32),
                 ("list_cap", I32), ("force_general", I32), ("no_carry", I32), ("ring_cap", I32),
                 ("chunk_rows", I32), ("walker_only", I32), ("ingress_rows", I32),
-                ("partition_sort", I32), ("partial_lanes", I32), ("direct_emit", I32), ("no_grow", I32)]
+                ("partition_sort", I32), ("partial_lanes", I32), ("no_grow", I32)]
 
 
 class sg_batch(ct.Structure):
@@ -549,8 +549,7 @@ class GpuEngine:
 
     def __init__(self, ctx: L.QueryContext, device: int = 0, force_general: bool = False, pool: int = 0,
                  no_carry: bool = False, ring_cap: int = 0, chunk_rows: int = 0, walker_only: bool = False,
-                 ingress_rows: int = 0, partition_sort: int = 0, partial_lanes: int = 0, direct_emit: bool = False,
-                 no_grow: bool = False):
+                 ingress_rows: int = 0, partition_sort: int = 0, partial_lanes: int = 0, no_grow: bool = False):
         self.ctx = ctx
         self.nfa = L.lower(ctx)
         self.desc = build_desc(self.nfa)
@@ -563,7 +562,6 @@ class GpuEngine:
         opts.ingress_rows = ingress_rows
         opts.partition_sort = partition_sort
         opts.partial_lanes = partial_lanes
-        opts.direct_emit = 1 if direct_emit else 0
         opts.no_grow = 1 if no_grow else 0
         if pool:
             opts.pool_partials = opts.pool_events = opts.pool_chain = opts.list_cap = pool

@@ -635,57 +635,11 @@ struct MRec {
 struct MRec16 {
   uint32_t r1, r2, v1, p1;
 };
-// Per-trigger parts of a directly emitted match record (see MatchSink::put_rec).
-struct TrigRec {
-  uint64_t trig;
-  int64_t ts;
-  uint32_t key;
-  int64_t v2, p2;
-};
-
 struct MatchSink {
   void* rec;
   int32_t narrow;
   uint32_t cap;               // slots allocated (a slot beyond it trips the internal guard)
   uint32_t* err;
-  // Direct emission (out != null): when every select column is e1's payload / compared value or the trigger's
-  // compared value / payload, the record walk writes the final match records itself -- full 64-byte lines at their
-  // delivery slots -- and k_project (with the intermediates it reads back) is skipped.
-  char* out;
-  int32_t stride, n_select, multi, b_slot;
-  int64_t out_base;
-  uint64_t base_index;
-  const uint64_t* index;
-  const int64_t* ts0;         // narrow records: timestamp of virtual row 0 (record times are offsets from it)
-  int64_t nc;
-  int8_t src[SG_MAX_SELECT];  // select column from: 0 e1 payload, 1 e1 value, 2 trigger value, 3 trigger payload
-  __device__ __forceinline__ void put_rec(uint32_t slot, uint32_t rank, int64_t v1, int64_t p1, const TrigRec& t) const {
-    if (slot >= cap) { atomicOr(err, 8u); return; }
-    int64_t w[4 + SG_MAX_SELECT];
-    w[0] = (int64_t)t.trig;
-    w[1] = t.ts;
-    w[2] = (int64_t)((uint64_t)t.key | ((uint64_t)((1u << 24) | (multi ? (uint32_t)b_slot : (0x800000u | rank))) << 32));
-    w[3] = 0;
-#pragma unroll
-    for (int s = 0; s < SG_MAX_SELECT; ++s) {
-      if (s >= n_select) break;
-      const int c = src[s];
-      w[4 + s] = c == 0 ? p1 : c == 1 ? v1 : c == 2 ? t.v2 : t.p2;
-    }
-    char* o = out + (size_t)(out_base + slot) * stride;
-    if ((stride & 15) == 0) {
-      typedef long long L2 __attribute__((ext_vector_type(2)));
-      for (int q = 0; q < 2 + SG_MAX_SELECT / 2; ++q) {
-        if (2 * q >= 4 + n_select) break;
-        L2 x;
-        x.x = w[2 * q];
-        x.y = w[2 * q + 1];
-        *(L2*)(o + 16 * q) = x;
-      }
-    } else {
-      for (int q = 0; q < 4 + n_select; ++q) ((int64_t*)o)[q] = w[q];
-    }
-  }
   __device__ __forceinline__ void put(uint32_t slot, uint32_t r1, uint32_t r2, int64_t v1, int64_t p1) const {
     if (slot >= cap) { atomicOr(err, 8u); return; }
     if (narrow) {
@@ -940,7 +894,6 @@ struct Walker {
   bool bad = false;
   bool oob = false;           // internal guard: a row outside the batch (never expected)
   bool overflow = false;
-  uint32_t key = 0;           // the unit's partition key (direct emission)
   uint32_t ew = 0xffffffffu, ebits = 0;   // count pass: emit bitmap word being built
   __device__ __forceinline__ void set_within(int64_t w) {
     within = BIG ? (TT)w : (TT)(w > 0x7fffffffll ? 0x7fffffffll : w);   // a wider window never expires in-unit
@@ -1001,16 +954,6 @@ struct Walker {
     const uint32_t r = rc.rowf & ROW_MASK;
     const bool live = !is_nan_val<T>(x);
     uint32_t m = 0;
-    TrigRec tr;
-    if (WRITE && em.out && (f & F_CONS) && live && in_chunk && r >= v.nc) {   // the trigger's part of direct records
-      const uint64_t b = r - (uint64_t)v.nc;
-      tr.trig = em.index ? em.index[b] : em.base_index + b;
-      tr.ts = (em.ts0 ? *em.ts0 : 0) + rc.t();
-      tr.key = key;
-      tr.v2 = val_bits<T>(x);
-      tr.p2 = 0;
-      if (payload) tr.p2 = (R::has_pay && a.pay_in_rec) ? rc.p(v.pfloat) : v_payload(v, r);
-    }
     if ((f & F_CONS) && live) {
       if (a.stack_mode) {
         // monotone stack: the completed partials are exactly a suffix, delivered oldest first
@@ -1025,12 +968,8 @@ struct Walker {
           }
         }
         if (WRITE && in_chunk && r >= v.nc) {
-          if (em.out) {
-            for (uint32_t q = 0; q < m; ++q) em.put_rec(ofs + q, q, val_bits<T>(L.gv(top + q)), L.gpay(top + q), tr);
-          } else {
-            for (uint32_t q = 0; q < m; ++q)
-              em.put(ofs + q, L.grow(top + q), r, val_bits<T>(L.gv(top + q)), L.gpay(top + q));
-          }
+          for (uint32_t q = 0; q < m; ++q)
+            em.put(ofs + q, L.grow(top + q), r, val_bits<T>(L.gv(top + q)), L.gpay(top + q));
         }
       } else {
         const bool emit = in_chunk && (r >= v.nc);
@@ -1038,10 +977,7 @@ struct Walker {
         for (uint32_t s = head; s != top; ++s) {
           T e = L.gv(s);
           if (cmp_sel<OP, T>(a.op, x, e)) {
-            if (WRITE && emit) {
-              if (em.out) em.put_rec(ofs + m, m, val_bits<T>(e), L.gpay(s), tr);
-              else em.put(ofs + m, L.grow(s), r, val_bits<T>(e), L.gpay(s));
-            }
+            if (WRITE && emit) em.put(ofs + m, L.grow(s), r, val_bits<T>(e), L.gpay(s));
             ++m;
           } else {
             if (wr != s) L.put(wr, e, BIG ? (int64_t)at(s) : L.base + (int64_t)at(s), L.grow(s), L.gpay(s));
@@ -1114,7 +1050,6 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
     if (BIG != (ovf != 0)) return;
   }
   Walker<T, WRITE, BIG> W;
-  W.key = part ? k : 0u;
   if (BIG) hbm_planes<T, BIG>(W.L, big, ovf - 1, a.big_cap);
   else lds_planes<T, BIG>(W.L, lds, WRITE, a.lp);
   W.L.pzero = v.pfloat;
@@ -1311,7 +1246,6 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
   lds_planes<T, false>(Wk.L, lds, WRITE, a.lp);
   Wk.L.pzero = v.pfloat;
   const uint32_t k = u % a.K;
-  Wk.key = a.partitioned ? k : 0u;
   const uint32_t sb = active ? seg_b[k] : 0;
   const int64_t tw = active ? src.ts(w) : 0;
   Wk.L.base = tw;
@@ -2129,32 +2063,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     // narrow match records when the value type is 4 bytes and every payload fits 32 bits (narrow walker records)
     ms.narrow = (N && sizeof(T) == 4) ? 1 : 0;
     ms.cap = total;
-    // direct emission when every select column comes from the pending list or the trigger's own record
-    bool direct = h->opt.direct_emit != 0;
-    for (int s = 0; s < d.n_select && direct; ++s) {
-      const int kind = plan.pp.kind[s];
-      const bool s2 = plan.pp.src[s] != 0;
-      if (kind == 0 && !s2) ms.src[s] = 0;
-      else if (kind == 1 && !s2) ms.src[s] = 1;
-      else if (kind == 1 && s2 && same_col) ms.src[s] = 2;
-      else if (kind == 3 && s2 && plan.pcol >= 0 && plan.pp.col[s] == plan.pcol && !es->nul_seen[plan.pcol]) ms.src[s] = 3;
-      else direct = false;
-    }
-    if (direct) {
-      ms.out = out;
-      ms.stride = wa.stride;
-      ms.n_select = d.n_select;
-      ms.multi = wa.multi;
-      ms.b_slot = wa.b_slot;
-      ms.out_base = wa.out_base;
-      ms.base_index = bv.base_index;
-      ms.index = bv.index;
-      ms.ts0 = N ? (nc ? cs.ts : bv.ts) : nullptr;
-      ms.nc = nc;
-      ms.rec = nullptr;
-    } else {
-      ms.rec = h->ws.get("mrec", (ms.narrow ? sizeof(MRec16) : sizeof(MRec)) * std::max<uint32_t>(total, 1), st);
-    }
+    ms.rec = h->ws.get("mrec", (ms.narrow ? sizeof(MRec16) : sizeof(MRec)) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
     h->kbeg("walk_record");
     launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, ms,
@@ -2165,7 +2074,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
                          emap, wst, big, carry_q0, carry_n);
       HIPCHK(hipGetLastError());
     }
-    if (total && !ms.out) {
+    if (total) {
       h->kbeg("project");
       hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)),
                          dim3(256), (size_t)256 * wa.stride, st, wa, v, plan.pp, bv.cols, cc, ms, off, (int64_t)total, out);

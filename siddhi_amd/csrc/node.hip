@@ -854,8 +854,6 @@ void gpu_loop(Run& r, int s) {
         bv.key = (const int32_t*)sp.key;
         bv.index = nullptr;
         if (nd.tag_col >= 0) {   // row tags: event index mod 2^32, in place of the projected-only column
-          bv.cols.col[nd.tag_col] = sp.col[nd.tag_col];
-          bv.cols.nul[nd.tag_col] = nullptr;
           hipLaunchKernelGGL(k_row_tags, dim3((unsigned)std::min<int64_t>((sb.n + 255) / 256, 8192)), dim3(256), 0,
                              h.stream, (uint32_t)(sb.base_index), sb.n, (uint32_t*)sp.col[nd.tag_col]);
           HIPCHK(hipGetLastError());
@@ -876,8 +874,8 @@ void gpu_loop(Run& r, int s) {
           });
         }
         for (int c = 0; c < nd.desc.n_cols; ++c) {
-          bv.cols.col[c] = sb.cols[c] ? sp.col[c] : nullptr;
-          bv.cols.nul[c] = (sb.nulls && sb.nulls[c]) ? (const uint8_t*)sp.nul[c] : nullptr;
+          bv.cols.col[c] = (sb.cols[c] || c == nd.tag_col) ? sp.col[c] : nullptr;
+          bv.cols.nul[c] = (sb.nulls && sb.nulls[c] && c != nd.tag_col) ? (const uint8_t*)sp.nul[c] : nullptr;
         }
         sg_push_view(h, bv, sb.n);
         k = h.out.n;

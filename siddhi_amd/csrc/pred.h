@@ -133,6 +133,71 @@ __global__ void __launch_bounds__(256) k_pred_simple(int64_t n, D c, const V* __
     if (lane < 4) cand_m[g * 4 + lane] = mine;
   }
 }
+// simple with a stream column (several streams, e.g. `e1=Stream1[price>20] -> e2=Stream2[..]`): A's bit also needs
+// the row's stream to be A's, and B's consumers are exactly the rows of B's stream (B has no local conjunct and its
+// compared value no nulls) -- the stream column is streamed with 16-B loads as well
+template <class V, class D, int OP>
+__global__ void __launch_bounds__(256) k_pred_simple_s(int64_t n, D c, const V* __restrict__ col,
+                                                       const uint8_t* __restrict__ nul, const int32_t* __restrict__ stream,
+                                                       int32_t sa, int32_t sb, uint64_t* __restrict__ cand_m,
+                                                       uint64_t* __restrict__ cons_m) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ntiles = (n + 255) >> 8;
+  const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (g >= ntiles) return;
+  typedef V V4 __attribute__((ext_vector_type(4)));
+  typedef int32_t I4 __attribute__((ext_vector_type(4)));
+  const int64_t i = g * 256 + lane * 4;
+  V4 x;
+  I4 t;
+  if (i + 4 <= n) {
+    x = __builtin_nontemporal_load((const V4*)(col + i));
+    t = __builtin_nontemporal_load((const I4*)(stream + i));
+  } else {
+    x.x = i + 0 < n ? col[i + 0] : V(0);
+    x.y = i + 1 < n ? col[i + 1] : V(0);
+    x.z = i + 2 < n ? col[i + 2] : V(0);
+    x.w = i + 3 < n ? col[i + 3] : V(0);
+    t.x = i + 0 < n ? stream[i + 0] : -1;
+    t.y = i + 1 < n ? stream[i + 1] : -1;
+    t.z = i + 2 < n ? stream[i + 2] : -1;
+    t.w = i + 3 < n ? stream[i + 3] : -1;
+  }
+  const V xs[4] = {x.x, x.y, x.z, x.w};
+  const int32_t ts[4] = {t.x, t.y, t.z, t.w};
+  uint64_t ma = 0, mb = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    bool ok = (i + s < n) && ts[s] == sa && cmp_op<OP, D>((D)xs[s], c);
+    if (nul && ok) ok = !nul[i + s];
+    const uint64_t a = __ballot(ok);
+    const uint64_t b = __ballot((i + s < n) && ts[s] == sb);
+    if (lane == s) { ma = a; mb = b; }
+  }
+  if (lane < 4) {
+    cand_m[g * 4 + lane] = ma;
+    cons_m[g * 4 + lane] = mb;
+  }
+}
+
+template <class V, class D>
+static void launch_pred_simple_s(int op, int64_t n, D c, const V* col, const uint8_t* nul, const int32_t* stream,
+                                 int sa, int sb, uint64_t* cand_m, uint64_t* cons_m, hipStream_t st) {
+  const int64_t ntiles = (n + 255) >> 8;
+  const dim3 grd((unsigned)std::max<int64_t>(1, (ntiles + 3) / 4)), blk(256);
+#define SG_PRED_S(OPV) hipLaunchKernelGGL((k_pred_simple_s<V, D, OPV>), grd, blk, 0, st, n, c, col, nul, stream, sa, sb, \
+                                          cand_m, cons_m)
+  switch (op) {
+    case 0: SG_PRED_S(0); break;
+    case 1: SG_PRED_S(1); break;
+    case 2: SG_PRED_S(2); break;
+    case 3: SG_PRED_S(3); break;
+    case 4: SG_PRED_S(4); break;
+    default: SG_PRED_S(5); break;
+  }
+#undef SG_PRED_S
+}
+
 template <class V, class D>
 static void launch_pred_simple(int op, int64_t n, D c, const V* col, const uint8_t* nul, uint64_t* cand_m,
                                hipStream_t st) {
@@ -194,6 +259,23 @@ static void launch_pred(const sg_nfa_desc& d, const PredArgs& pa, const int32_t*
   bool simple = pa.cons_all && !stream && pa.s_a == 0 && simple_prog(d, pa.prog_a_off, pa.prog_a_len, sp) &&
                 (pa.val_col_a < 0 || sp.s_col == pa.val_col_a) && (((uintptr_t)cols.col[sp.s_col]) & 15) == 0;
   const dim3 blk(256);
+  // several streams: the same pass with the stream column when B's consumers are just B's stream's rows
+  if (!simple && stream && cons_m && pa.prog_b_len == 0 && pa.val_col_b >= 0 && !cols.nul[pa.val_col_b] &&
+      simple_prog(d, pa.prog_a_off, pa.prog_a_len, sp) && (pa.val_col_a < 0 || sp.s_col == pa.val_col_a) &&
+      (((uintptr_t)cols.col[sp.s_col]) & 15) == 0 && (((uintptr_t)stream) & 15) == 0 && sp.s_dom != 0 &&
+      sp.s_type == SG_T_FLOAT) {
+    SgVal cv = sg_val_from_bits_host(sp.s_cbits, sp.s_ctype);
+    const float* colp = (const float*)cols.col[sp.s_col];
+    const uint8_t* nul = cols.nul[sp.s_col];
+    if (sp.s_dom == 1) {
+      float c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? (float)cv.d : (float)cv.i;
+      launch_pred_simple_s<float, float>(sp.s_op, n, c, colp, nul, stream, pa.s_a, pa.s_b, cand_m, cons_m, st);
+    } else {
+      double c = (sp.s_ctype == SG_T_FLOAT || sp.s_ctype == SG_T_DOUBLE) ? cv.d : (double)cv.i;
+      launch_pred_simple_s<float, double>(sp.s_op, n, c, colp, nul, stream, pa.s_a, pa.s_b, cand_m, cons_m, st);
+    }
+    return;
+  }
   if (simple) {
     // constant in the compare domain (sg_cmp: 0 integral, 1 f32, 2 f64)
     SgVal cv = sg_val_from_bits_host(sp.s_cbits, sp.s_ctype);

@@ -74,11 +74,10 @@ class _Spy:
     spilled = []
     ring_cap = 0
     walker_only = False
-    no_direct = True
 
     def __init__(self, ctx):
         from siddhi_amd._native import GpuEngine
-        self.e = GpuEngine(ctx, ring_cap=_Spy.ring_cap, walker_only=_Spy.walker_only, direct_emit=not _Spy.no_direct)
+        self.e = GpuEngine(ctx, ring_cap=_Spy.ring_cap, walker_only=_Spy.walker_only)
 
     def push(self, b):
         self.e.push(b)
@@ -91,13 +90,12 @@ class _Spy:
         self.e.close()
 
 
-def check(app, batches, min_matches=1, expect_spill=None, ring_cap=0, walker_only=False, no_direct=True):
+def check(app, batches, min_matches=1, expect_spill=None, ring_cap=0, walker_only=False):
     assert shape_of(app) == L.SHAPE_EVERY_NEXT_CMP, "case must exercise the closed-form walker"
     want = run_engine(OracleEngine, app, batches)
     _Spy.spilled = []
     _Spy.ring_cap = ring_cap
     _Spy.walker_only = walker_only
-    _Spy.no_direct = no_direct
     got = run_engine(_Spy, app, batches)
     assert len(want) >= min_matches
     assert_same(got, want)
@@ -264,42 +262,3 @@ def test_unpartitioned_search_longer_than_limit():
     b = make_batch(app, n, seed=23, rate=10, values={"price": falling})
     check(app, [b])
 
-
-@pytest.mark.parametrize("no_direct", [False, True], ids=["direct", "projected"])
-@pytest.mark.parametrize("case", ["stack", "list", "spill", "carry", "nulls", "wide", "ints"])
-def test_direct_emission_and_projection_agree(case, no_direct):
-    """With direct_emit the record walk writes the final match records itself when every select column is e1's
-    pending-list payload / value or the trigger's own value / payload (MatchSink::put_rec); by default (and for other
-    selects) k_project builds them from 16-byte intermediates.  Both against the oracle."""
-    if case == "stack":
-        app = q_part("price > e1.price")
-        check(app, [make_batch(app, 50_000, seed=31, keys=120, rate=20, values=PRICE_TIES)], no_direct=no_direct)
-    elif case == "list":
-        app = q_part("price > e1.price and volume > 300", sel="e2.price as p2, e1.id as i1, e2.id as i2")
-        check(app, [make_batch(app, 50_000, seed=32, keys=120, rate=20, values=PRICE_TIES)], no_direct=no_direct)
-    elif case == "spill":
-        falling = lambda r, n: np.where((np.arange(n) // 3) % 120 < 90, 40.0 - ((np.arange(n) // 3) % 120) * 0.2,
-                                        r.random(n) * 40)
-        app = q_part("price > e1.price")
-        b = make_batch(app, 40_000, seed=33, keys=3, rate=40, values={"price": falling})
-        check(app, [b], expect_spill=True, ring_cap=16, no_direct=no_direct)
-    elif case == "carry":
-        app = q_part("price >= e1.price", sel="e1.price as p1, e2.id as i2, e1.id as i1")
-        b = make_batch(app, 60_000, seed=34, keys=300, rate=30, values=PRICE_TIES)
-        check(app, split(b, [20_000, 20_001, 41_000]), no_direct=no_direct)
-    elif case == "nulls":
-        app = q_part("price > e1.price", sel="e1.id as i1, e2.id as i2, e1.volume as v1, e2.volume as v2")
-        b = make_batch(app, 40_000, seed=35, keys=100, rate=20, values={"price": lambda r, n: r.random(n) * 40},
-                       null_frac={"price": 0.05, "volume": 0.1, "id": 0.1})
-        check(app, [b], no_direct=no_direct)
-    elif case == "wide":
-        app = q_part("price > e1.price")
-        b = make_batch(app, 40_000, seed=36, keys=100, rate=20,
-                       values={"price": lambda r, n: r.random(n) * 40, "id": lambda r, n: (1 << 40) + np.arange(n)})
-        check(app, [b], no_direct=no_direct)
-    else:
-        app = (f"define stream S (id long, symbol string, v int, price float); " + PART +
-               f"from every e1=S[v>500] -> e2=S[v<e1.v] within 1 sec "
-               f"select e2.v as v2, e1.id as i1, e1.v as v1, e2.id as i2 insert into M; end;")
-        b = make_batch(app, 50_000, seed=37, keys=200, rate=30, values={"v": lambda r, n: r.integers(0, 1000, n)})
-        check(app, [b], no_direct=no_direct)
