@@ -246,7 +246,7 @@ def host_stream(cfg, total, keys, rate, dev, gen_rows=50_000_000):
     return ts, raw, cols, keep
 
 
-def node_whole(cfg, total, keys, rate, devices, steps, threads, chunk_rows):
+def node_whole(cfg, total, keys, rate, devices, steps, threads, chunk_rows, key_dict=0):
     """SURVEY.md §8d whole-node events/s through the node pipeline (sg_node_*, csrc/node.hip), one host process
     driving `gpus` GPUs: pinned raw host rows -> native router (first-seen dense ids, shard mix64(id) mod G) ->
     per-GPU threads (chunked H2D, kernels, GPU-transposed SoA match columns D2H, overlapped across chunks) ->
@@ -263,6 +263,8 @@ def node_whole(cfg, total, keys, rate, devices, steps, threads, chunk_rows):
     times, stats, got = [], [], 0
     for s in range(steps + 1):
         node.reset()
+        if key_dict:
+            node.set_key_dict(key_dict)
         t0 = time.perf_counter()
         got = node.push(nb, sink.struct, cap)
         dt = time.perf_counter() - t0
@@ -481,6 +483,8 @@ def main():
     ap.add_argument("--c5-push-rows", type=int, default=100_000_000)
     ap.add_argument("--c5-node-steps", type=int, default=2,
                     help="steps of the 1B-event C5 stream through the node pipeline, rank 0 driving every GPU (0: skip)")
+    ap.add_argument("--c5-node-devices", default="", help="devices of the c5_whole_node pipeline (default: one per rank)")
+    ap.add_argument("--node-key-dict", type=int, default=0, help="whole_node key dictionary: 0 auto, 1 host, 2 GPU")
     ap.add_argument("--node-threads", type=int, default=0, help="host threads of the node pipeline (0: 16 per GPU)")
     ap.add_argument("--other-configs", default="C1,C3b,C3c,C4",
                     help="BASELINE configs measured beside the headline (one GPU, rank 0; '' to skip)")
@@ -508,7 +512,8 @@ def main():
     wn = None
     if args.whole_node_steps > 0:
         try:
-            wn = node_whole(cfg, n, keys, rate, [local], args.whole_node_steps, args.router_threads, 0)
+            wn = node_whole(cfg, n, keys, rate, [local], args.whole_node_steps, args.router_threads, 0,
+                            args.node_key_dict)
         except Exception as e:   # report, never fake
             wn = {"error": str(e)}
         if ws > 1 and "ms_per_step" in wn:
@@ -521,8 +526,9 @@ def main():
         if rank == 0:
             try:
                 thr = args.node_threads or max(16, min(16 * ws, len(os.sched_getaffinity(0))))
+                devs = [int(x) for x in args.c5_node_devices.split(",")] if args.c5_node_devices else list(range(ws))
                 c5w = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
-                                 synth.CONFIGS["C5"][3], list(range(ws)), args.c5_node_steps, thr, 0)
+                                 synth.CONFIGS["C5"][3], devs, args.c5_node_steps, thr, 0)
             except Exception as e:   # report, never fake
                 c5w = {"error": str(e)}
         barrier()

@@ -208,6 +208,7 @@ struct sg_node {
   // attribute of the e1 row the tag names from the caller's columns, or, for rows of earlier pushes the engine still
   // holds, from `hist` (kept at each push's end for exactly the carried rows' range).
   int tag_col = -1;
+  int tag_cand = -1;                 // the query's tag column if it has one (tag_col: in use for this stream)
   bool tag_sel[SG_MAX_SELECT] = {};
   sg_nfa_desc edesc;                 // what the engine runs (the tag column as INT)
   Pinned tagbuf;
@@ -1032,7 +1033,19 @@ void fill_loop(Run& r) {
         const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, cnt / 65536 + 1));
         nd.pool->parallel_for(T, [&](int t) {
           const int64_t a = o0 + cnt * t / T, e = o0 + cnt * (t + 1) / T;
-          for (int64_t o = a; o < e; ++o) fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o], &nd);
+          const int tc = nd.tag_col;
+          const bool pf = tc >= 0 && r.b.cols[tc];
+          const int wc = pf ? sg_col_width(nd.desc.col_type[tc]) : 8;
+          const uint32_t* tags = nd.tagbuf.as<uint32_t>();
+          constexpr int64_t D = 32;   // e1 rows are scattered over the last `within`: keep 32 of their lines in flight
+          for (int64_t o = a; o < e; ++o) {
+            if (pf && o + D < e) {
+              const uint64_t tr = r.out->trigger[o + D];
+              const uint64_t g = tr - (uint64_t)(uint32_t)((uint32_t)tr - tags[o + D]);
+              if (g >= r.b.base_index) __builtin_prefetch((const char*)r.b.cols[tc] + (size_t)wc * (g - r.b.base_index));
+            }
+            fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o], &nd);
+          }
         });
       }
       r.publish([&] {
@@ -1152,6 +1165,36 @@ void reserve_all(Run& r) {
 
 void keep_history(sg_node& nd, const sg_node_batch& b);
 
+// Switch the row tags on or off for a new stream: the GPU handles are reopened with the tag column as INT (or as the
+// query declares it).
+void set_tags(sg_node& nd, bool on) {
+  if ((nd.tag_col >= 0) == on) return;
+  const sg_nfa_desc* dd = &nd.desc;
+  nd.edesc = nd.desc;
+  for (int k = 0; k < SG_MAX_SELECT; ++k) nd.tag_sel[k] = false;
+  if (on) {
+    const int c = nd.tag_cand;
+    nd.edesc.col_type[c] = SG_T_INT;
+    for (int k = 0; k < nd.desc.n_ret; ++k)
+      if (nd.desc.ret_col[k] == c) nd.edesc.ret_type[k] = SG_T_INT;
+    for (int k = 0; k < nd.desc.n_select; ++k)
+      if (nd.desc.ret_col[nd.desc.sel_ret[k]] == c) {
+        nd.edesc.sel_type[k] = SG_T_INT;
+        nd.tag_sel[k] = nd.desc.sel_state[k] == nd.desc.shape_args[0];
+      }
+    dd = &nd.edesc;
+  }
+  for (int s = 0; s < nd.G; ++s) {
+    HIPCHK(hipSetDevice(nd.dev[s]));
+    if (nd.h[s]) sg_close(nd.h[s]);
+    nd.h[s] = nullptr;
+    const int rc = sg_open(nd.dev[s], dd, &nd.opt, &nd.h[s]);
+    if (rc != SG_OK) throw SgError(rc, "node: reopening the GPU handle failed");
+  }
+  nd.tag_col = on ? nd.tag_cand : -1;
+  nd.hist_n = 0;
+}
+
 // Auto key dictionary: a stream whose first 64K rows hold few distinct keys keeps its dictionary on the host (a
 // cache-resident table; the GPU then receives 4-byte dense ids instead of 8-byte raw keys); many keys (a DRAM-bound
 // table on the host) are encoded on the GPUs.
@@ -1168,6 +1211,16 @@ bool few_keys(const sg_node_batch& b) {
 }
 
 void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, int64_t cap, int64_t* n_out) {
+  if (nd.ddict < 0) {   // the first push of a stream fixes where keys are encoded, and whether rows carry tags
+    const bool dev_ok = nd.desc.partitioned && !need_clocks(nd.desc);
+    nd.ddict = (dev_ok && nd.key_dict_mode == 2) ? 1 : 0;
+    if (dev_ok && nd.key_dict_mode == 0) nd.ddict = few_keys(b) ? 0 : 1;
+    // tags save PCIe bytes at the price of host selector work (random e1 reads): opt-in, SG_NODE_TAGS=1
+    const char* e = getenv("SG_NODE_TAGS");
+    const bool want = nd.tag_cand >= 0 && e && e[0] == '1';   // (measured: the host's e1 gathers cost more than
+                                                               // the PCIe bytes they save on this pool's hosts)
+    set_tags(nd, want);
+  }
   Run r(nd, b, out, cap);
   r.w = want_of(nd, b, out);
   // default chunks: ~16 per push (short pipeline fill and drain), 4M..25M rows each
@@ -1180,11 +1233,6 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
   r.rows_of.assign((size_t)(r.nch * nd.G), 0);
   r.lbase_of.assign((size_t)(r.nch * nd.G), 0);
   r.kb_of.assign((size_t)(r.nch * nd.G), 1);
-  if (nd.ddict < 0) {   // the first push of a stream fixes where keys are encoded
-    const bool dev_ok = nd.desc.partitioned && !need_clocks(nd.desc);
-    nd.ddict = (dev_ok && nd.key_dict_mode == 2) ? 1 : 0;
-    if (dev_ok && nd.key_dict_mode == 0) nd.ddict = few_keys(b) ? 0 : 1;
-  }
   r.kbase_of.assign((size_t)(r.nch * nd.G), 0);
   r.ts_base_of.assign((size_t)r.nch, 0);
   r.ts32_of.assign((size_t)r.nch, 0);
@@ -1374,25 +1422,12 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
   nd->no_fill = getenv("SG_NODE_NO_FILL") != nullptr;
   nd->no_ts32 = getenv("SG_NODE_NO_TS32") != nullptr;
   nd->edesc = nd->desc;
-  if (n_gpus == 1 && !nd->no_fill && !getenv("SG_NODE_NO_TAG")) {
-    nd->tag_col = tag_column(nd->desc);
-    if (nd->tag_col >= 0) {
-      const int c = nd->tag_col;
-      nd->edesc.col_type[c] = SG_T_INT;
-      for (int k = 0; k < nd->desc.n_ret; ++k)
-        if (nd->desc.ret_col[k] == c) nd->edesc.ret_type[k] = SG_T_INT;
-      for (int k = 0; k < nd->desc.n_select; ++k)
-        if (nd->desc.ret_col[nd->desc.sel_ret[k]] == c) {
-          nd->edesc.sel_type[k] = SG_T_INT;
-          nd->tag_sel[k] = nd->desc.sel_state[k] == nd->desc.shape_args[0];
-        }
-    }
-  }
+  nd->tag_cand = (n_gpus == 1 && !nd->no_fill) ? tag_column(nd->desc) : -1;
   memset(&nd->st, 0, sizeof(nd->st));
   int rc = SG_OK;
   for (int s = 0; s < n_gpus && rc == SG_OK; ++s) {
     nd->dev[s] = devices ? devices[s] : 0;
-    rc = sg_open(nd->dev[s], &nd->edesc, &nd->opt, &nd->h[s]);
+    rc = sg_open(nd->dev[s], &nd->desc, &nd->opt, &nd->h[s]);
     if (rc != SG_OK) {
       nd->err = nd->h[s] ? sg_last_error(nd->h[s]) : "sg_open failed";
       break;

@@ -250,9 +250,8 @@ def test_node_row_tags_reach_back_across_pushes(tags, monkeypatch):
     """One GPU, closed form: `e1.id` (projected only) travels as the row's event index mod 2^32 and the host reads the
     id of the e1 row it names -- from the caller's columns, or for rows of earlier pushes the engine still carries,
     from the node's history.  Key X is quiet from row 1000 to row 80000 (10..800 ms), so its early rows are carried
-    through four pushes and complete matches in the fifth.  SG_NODE_NO_TAG ships the column instead."""
-    if not tags:
-        monkeypatch.setenv("SG_NODE_NO_TAG", "1")
+    through four pushes and complete matches in the fifth.  SG_NODE_TAGS=0 ships the column instead."""
+    monkeypatch.setenv("SG_NODE_TAGS", "1" if tags else "0")
     cfg = "C2"
     b = synth_batch(cfg, 0, 160_000, keys=600, rate=100)
     b.key = b.key.copy()
