@@ -24,7 +24,7 @@ its own stream; no data-path collective (keys never interact); t
 roofline: the dominant kernel of the `value` step (largest HIP-event time, recorded on the launch stream by the
 engine, sg_timing.kernel_ms) against the §8d algorithmic bytes of the whole path (16.125 B/event + 36 B/match),
 plus the predicate pass (4.125 B/event) and the end-to-end path; `traffic` comes from a rocprofv3 PMC summary of
-this same command (profiles/collect_r02.sh) and is only used when its source hash matches the tree.
+this same command (profiles/collect_r03.sh) and is only used when its source hash matches the tree.
 """
 import argparse
 import hashlib
@@ -47,7 +47,8 @@ from siddhi_amd import lowering as L          # noqa: E402
 from siddhi_amd import synth                  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-DEFAULT_PMC = os.path.join(ROOT, "profiles", "r02", "c2_pmc.json")
+PMC_DIR = os.path.join(ROOT, "profiles", "r03")
+DEFAULT_PMC = os.path.join(PMC_DIR, "C2_pmc.json")
 
 
 def barrier():
@@ -79,6 +80,7 @@ def dist_env():
 
 
 # sources of the engine routes that do not run the closed-form walker (C1/C2/C5): their edits leave a C2 profile valid
+NODE_ONLY = ("node.hip", "keydict.hip", "keydict.h", "router.cpp")
 OTHER_ROUTES = ("absent.hip", "interp.hip", "interp.h", "partial.hip", "chain.h", "seq.h", "router.cpp")
 
 
@@ -90,6 +92,7 @@ def source_hash(cfg="C2"):
     for d, exts in ((os.path.join(ROOT, "siddhi_amd", "csrc"), (".hip", ".h", ".cpp")),
                     (os.path.join(ROOT, "include"), (".h",))):
         files += sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(exts))
+    files = [f for f in files if os.path.basename(f) not in NODE_ONLY]   # not on the per-push path measured here
     if cfg in ("C1", "C2", "C5"):
         files = [f for f in files if os.path.basename(f) not in OTHER_ROUTES]
     files.append(os.path.join(ROOT, "siddhi_amd", "lowering.py"))
@@ -191,7 +194,7 @@ def pmc_traffic(path, cfg, n, dominant):
     except OSError:
         return None, "no PMC summary at %s" % os.path.relpath(path, ROOT)
     if prof.get("source_hash") != source_hash(cfg):
-        return None, "stale PMC summary (source hash %s != tree %s): rerun profiles/collect_r02.sh" % (
+        return None, "stale PMC summary (source hash %s != tree %s): rerun profiles/collect_r03.sh" % (
             prof.get("source_hash"), source_hash(cfg))
     if prof.get("workload") != cfg or prof.get("events") != n:
         return None, "PMC summary is for %s/%s events" % (prof.get("workload"), prof.get("events"))
@@ -200,6 +203,18 @@ def pmc_traffic(path, cfg, n, dominant):
     path_tot = sum(v["bytes_per_push"] for v in prof["kernels"].values())
     return {"dominant_GB": dom, "path_GB": round(path_tot / 1e9, 4),
             "source": os.path.relpath(path, ROOT), "collected_at_head": prof.get("git_head")}, None
+
+
+def attach_traffic(roof, path, cfg, n):
+    tr, why = pmc_traffic(path, cfg, n, roof["kernel"])
+    if tr is not None:
+        roof["traffic"] = tr["dominant_GB"]
+        roof["traffic_unit"] = "GB per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)"
+        roof["path_traffic_GB"] = tr["path_GB"]
+        roof["traffic_source"] = tr["source"]
+    else:
+        roof["traffic_note"] = why
+    return roof
 
 
 def synth_columns(cfg, rank, n, keys, rate, dev):
@@ -400,7 +415,8 @@ def config_line(cfg, dev, steps, warmup, cpu):
     out = {"workload": f"{cfg}: " + synth.QUERIES[cfg], "events": n, "keys": keys, "rate_events_per_ms": rate,
            "matches": int(m["matches"]), "steps": steps, "ms_per_push": round(ms, 3),
            "value": round(n / (ms * 1e-3), 1), "unit": "events/s",
-           "roofline": roofline_of(cfg, n, m["matches"], m["kern"], m["stage"])}
+           "roofline": attach_traffic(roofline_of(cfg, n, m["matches"], m["kern"], m["stage"]),
+                                      os.path.join(PMC_DIR, cfg + "_pmc.json"), cfg, n)}
     if cpu:
         sample = CPU_SAMPLE[cfg] // 4
         r, nm, dt = cpu_baseline(cfg, sample, keys, rate)
@@ -489,7 +505,7 @@ def main():
     ap.add_argument("--other-configs", default="C1,C3b,C3c,C4",
                     help="BASELINE configs measured beside the headline (one GPU, rank 0; '' to skip)")
     ap.add_argument("--other-steps", type=int, default=3)
-    ap.add_argument("--pmc", default=DEFAULT_PMC, help="rocprofv3 PMC summary of this command (profiles/collect_r02.sh)")
+    ap.add_argument("--pmc", default=DEFAULT_PMC, help="rocprofv3 PMC summary of this command (profiles/collect_r03.sh)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -545,14 +561,7 @@ def main():
 
     roof = roofline_of(cfg, n, matches, kern, stage)
     dominant = roof["kernel"]
-    tr, why = pmc_traffic(args.pmc, cfg, n, dominant)
-    if tr is not None:
-        roof["traffic"] = tr["dominant_GB"]
-        roof["traffic_unit"] = "GB per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)"
-        roof["path_traffic_GB"] = tr["path_GB"]
-        roof["traffic_source"] = tr["source"]
-    else:
-        roof["traffic_note"] = why
+    attach_traffic(roof, args.pmc, cfg, n)
     cpu = None
     if not args.no_cpu:
         hi = host_info()

@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 MARKS = [   # kernel name pattern -> engine mark (siddhi_amd/csrc: h->kbeg names)
+    (r"k_sq_spec", "sequence_lanes"), (r"k_sq_fix", "sequence_fix"), (r"k_pp_lanes", "partial_lanes"),
     (r"k_pred_simple|k_pred\b", "pred"), (r"k_pack\b", "pack"), (r"onesweep", "key_sort"),
     (r"k_part1_hist", "part_hist"), (r"k_part2_hist", "part_hist2"), (r"k_part1<", "part_group"),
     (r"k_part2<|k_part_segs", "part_key"),
