@@ -353,6 +353,18 @@ void sg_egress_init(SgHandle& h) {
   }
 }
 
+// Staging slot `slot` holds at least `bytes` (grown only after its last copy has read it: hipFree synchronises the
+// device, so sg_push_deliver sizes both slots before its chunk pipeline starts).
+static void stage_reserve(SgHandle& h, int slot, int64_t bytes) {
+  if (h.eg.cap[slot] >= bytes) return;
+  HIPCHK(hipEventSynchronize(h.eg.done[slot]));
+  if (h.eg.stage[slot]) HIPCHK(hipFree(h.eg.stage[slot]));
+  h.eg.stage[slot] = nullptr;
+  const size_t want = (size_t)bytes + (size_t)bytes / 4;
+  HIPCHK(hipMalloc(&h.eg.stage[slot], want));
+  h.eg.cap[slot] = (int64_t)want;
+}
+
 // Deliver up to `cap` pending matches into out (rows [row0, row0 + k)) through staging slot `slot`; returns k.
 // The copies are left in flight on the D2H stream (the caller synchronises it before returning to its caller).
 static int64_t deliver_pending(SgHandle& h, const sg_match_columns* out, int64_t row0, int64_t cap, int slot) {
@@ -362,14 +374,7 @@ static int64_t deliver_pending(SgHandle& h, const sg_match_columns* out, int64_t
   sg_egress_init(h);
   const sg_nfa_desc& d = h.desc;
   const ColLayout L = sg_col_layout(d, k);
-  if (h.eg.cap[slot] < (int64_t)L.bytes) {   // grow: wait until this slot's last copy has read it
-    HIPCHK(hipEventSynchronize(h.eg.done[slot]));
-    if (h.eg.stage[slot]) HIPCHK(hipFree(h.eg.stage[slot]));
-    h.eg.stage[slot] = nullptr;
-    const size_t want = L.bytes + L.bytes / 4;
-    HIPCHK(hipMalloc(&h.eg.stage[slot], want));
-    h.eg.cap[slot] = (int64_t)want;
-  }
+  stage_reserve(h, slot, (int64_t)L.bytes);
   char* st = h.eg.stage[slot];
   HIPCHK(hipStreamWaitEvent(h.stream, h.eg.done[slot], 0));   // slot free again
   hipLaunchKernelGGL(k_to_columns, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, h.stream, k, (const char*)o.rec,
@@ -599,6 +604,7 @@ int sg_poll(sg_handle* hh, sg_matches* out, int64_t cap, int64_t* n) {
         h.eg.cap[0] = (int64_t)(need + need / 4);
       }
       char* st = h.eg.stage[0];
+      HIPCHK(hipStreamWaitEvent(h.stream, h.eg.done[0], 0));   // the slot's last column copy has read it
       uint64_t* trig = (uint64_t*)st;
       int64_t* ts = (int64_t*)(trig + k);
       int64_t* vals = ts + k;
@@ -643,6 +649,17 @@ int sg_push_deliver(sg_handle* hh, const sg_batch* b, const sg_match_columns* ou
   int rc = guard(hh, [&] {
     HIPCHK(hipSetDevice(h.device));
     DeliverHook dh(h, out, cap);
+    {
+      // size both staging slots for the largest delivery this call expects (pending matches, or one match per row of
+      // the batch), so the chunk pipeline below does not allocate
+      sg_egress_init(h);
+      const int64_t expect = std::min<int64_t>(cap, std::max<int64_t>(h.out.n, b->n));
+      if (expect > 0) {
+        const int64_t bytes = (int64_t)sg_col_layout(h.desc, expect).bytes;
+        stage_reserve(h, 0, bytes);
+        stage_reserve(h, 1, bytes);
+      }
+    }
     try {
       dh.chunk_done();   // matches pending before this batch come first
       if (b->n > 0) {

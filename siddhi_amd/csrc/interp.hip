@@ -805,6 +805,10 @@ void sg_general_restore(SgHandle* h, SnapR& r) {
     if (!gs->pp || h->opt.partial_lanes < 0) throw SgError(SG_EINVAL, "snapshot: taken on the partial-lane route");
     sg_partial_restore(h, gs->pp, r);
     gs->max_ts = max_ts;
+    // the machine's per-key runtimes from before the restore (a fallback taken earlier) are stale: a later fallback
+    // rebuilds them from the restored carried rows alone
+    if (gs->arena) HIPCHK(hipMemsetAsync(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4, st));
+    HIPCHK(hipStreamSynchronize(st));
     return;
   }
   if (gs->pp) sg_partial_deactivate(gs->pp);

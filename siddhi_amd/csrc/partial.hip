@@ -560,10 +560,11 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   while (__ballot(active)) {
     bool done = false;
     if (active) {
-      if (q >= e || src.ts(q) - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
+      const int64_t tq = q < e ? src.ts(q) : 0;
+      if (q >= e || tq - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
         done = true;
       } else {
-        const int em = L.step(q);
+        const int em = L.step(q, tq);
         if (L.overflow) atomicCAS(o.fail, 0, SG_EUNSUPPORTED);
         if (em >= 0) {
           const int64_t c = sid[q];
