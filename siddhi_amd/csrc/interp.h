@@ -18,6 +18,10 @@
 
 #include "../../include/siddhi_gpu.h"
 
+#ifndef SG_GLOBAL
+#define SG_GLOBAL   // (sg_device.h: the global address space on the GPU, nothing on the host)
+#endif
+
 #ifndef SG_HD
 #define SG_HD __host__ __device__
 #endif
@@ -66,7 +70,7 @@ struct SgEmitSink {     // where emissions go (device: atomic bump buffer; host:
 struct KeyMachine {
   const sg_nfa_desc* d;
   const SgGeo* g;
-  int32_t* a;           // this key's arena
+  SG_GLOBAL int32_t* a;   // this key's arena (global-address-space pointer: plain global loads, not flat ones)
   int32_t key;
   int clone;            // partition clones never get withinEvery (cloneProperties, StreamPreStateProcessor.java:190-200)
   SgEmitSink sink;
@@ -84,21 +88,21 @@ struct KeyMachine {
   const uint64_t* const* lbits = nullptr;
 
   // ---------------------------------------------------------------- raw accessors
-  SG_HD int32_t* hdr() { return a; }
-  SG_HD int32_t* sth(int s) { return a + K_HDR_FIXED + s * H_STATE_WORDS; }
-  SG_HD int32_t* list(int s, int which) { return a + g->off_lists + (s * 2 + which) * (g->L + 1); }
-  SG_HD int32_t* part(int p) { return a + g->off_part + p * g->part_words; }
-  SG_HD int32_t* ev(int e) { return a + g->off_ev + e * g->ev_words; }
-  SG_HD int32_t* chain(int c) { return a + g->off_chain + c * 3; }
-  SG_HD int32_t* tq(int ai) { return a + g->off_timer + ai * (2 + 2 * g->Q); }
+  SG_HD SG_GLOBAL int32_t* hdr() { return a; }
+  SG_HD SG_GLOBAL int32_t* sth(int s) { return a + K_HDR_FIXED + s * H_STATE_WORDS; }
+  SG_HD SG_GLOBAL int32_t* list(int s, int which) { return a + g->off_lists + (s * 2 + which) * (g->L + 1); }
+  SG_HD SG_GLOBAL int32_t* part(int p) { return a + g->off_part + p * g->part_words; }
+  SG_HD SG_GLOBAL int32_t* ev(int e) { return a + g->off_ev + e * g->ev_words; }
+  SG_HD SG_GLOBAL int32_t* chain(int c) { return a + g->off_chain + c * 3; }
+  SG_HD SG_GLOBAL int32_t* tq(int ai) { return a + g->off_timer + ai * (2 + 2 * g->Q); }
   // step scratch: a state's list can return / emit / re-arm all its partials in one step (the reference collects
   // them in unbounded chunks), so these buffers are list-sized and grow with the lists
-  SG_HD int32_t* scratch(int i) { return a + g->off_scratch + i * (g->L + 1); }
-  SG_HD static int64_t rd64(const int32_t* p) { return (int64_t)(((uint64_t)(uint32_t)p[1] << 32) | (uint32_t)p[0]); }
-  SG_HD static void wr64(int32_t* p, int64_t v) { p[0] = (int32_t)(uint32_t)v; p[1] = (int32_t)(uint32_t)((uint64_t)v >> 32); }
+  SG_HD SG_GLOBAL int32_t* scratch(int i) { return a + g->off_scratch + i * (g->L + 1); }
+  SG_HD static int64_t rd64(const SG_GLOBAL int32_t* p) { return (int64_t)(((uint64_t)(uint32_t)p[1] << 32) | (uint32_t)p[0]); }
+  SG_HD static void wr64(SG_GLOBAL int32_t* p, int64_t v) { p[0] = (int32_t)(uint32_t)v; p[1] = (int32_t)(uint32_t)((uint64_t)v >> 32); }
   SG_HD int64_t pts(int p) { return rd64(part(p)); }
   SG_HD void set_pts(int p, int64_t t) { wr64(part(p), t); }
-  SG_HD int32_t& slot(int p, int s) { return part(p)[3 + s]; }
+  SG_HD SG_GLOBAL int32_t& slot(int p, int s) { return part(p)[3 + s]; }
   SG_HD int64_t ets(int e) { return rd64(ev(e)); }
   SG_HD const sg_state_desc& st(int s) { return d->states[s]; }
 
@@ -108,7 +112,7 @@ struct KeyMachine {
 
   // ---------------------------------------------------------------- pools
   SG_HD void format() {
-    int32_t* h = hdr();
+    SG_GLOBAL int32_t* h = hdr();
     for (int i = 0; i < (int)g->key_words && i < sg_hdr_words(g->S); ++i) h[i] = 0;
     for (int s = 0; s < g->S; ++s) { list(s, 0)[0] = 0; list(s, 1)[0] = 0; sth(s)[H_ACTIVE] = 1; }
     for (int p = 0; p < g->P; ++p) part(p)[2] = (p + 1 < g->P) ? p + 1 : SG_NIL;
@@ -125,7 +129,7 @@ struct KeyMachine {
     wr64(h + K_POS_LO, -1);
   }
   SG_HD int alloc_part() {
-    int32_t* h = hdr();
+    SG_GLOBAL int32_t* h = hdr();
     int p = h[K_FREE_P];
     if (p == SG_NIL) { fail(SG_ECAPACITY); return 0; }
     h[K_FREE_P] = part(p)[2];
@@ -134,7 +138,7 @@ struct KeyMachine {
     return p;
   }
   SG_HD int alloc_ev() {
-    int32_t* h = hdr();
+    SG_GLOBAL int32_t* h = hdr();
     int e = h[K_FREE_E];
     if (e == SG_NIL) { fail(SG_ECAPACITY); return 0; }
     h[K_FREE_E] = ev(e)[5];
@@ -143,7 +147,7 @@ struct KeyMachine {
     return e;
   }
   SG_HD int alloc_chain(int e) {
-    int32_t* h = hdr();
+    SG_GLOBAL int32_t* h = hdr();
     int c = h[K_FREE_C];
     if (c == SG_NIL) { fail(SG_ECAPACITY); return 0; }
     h[K_FREE_C] = chain(c)[2];
@@ -181,7 +185,7 @@ struct KeyMachine {
     for (int c = 0; c < g->C; ++c) if (chain(c)[2] == -3) chain(c)[2] = -2;
     for (int s = 0; s < g->S; ++s)
       for (int w = 0; w < 2; ++w) {
-        int32_t* l = list(s, w);
+        SG_GLOBAL int32_t* l = list(s, w);
         for (int i = 0; i < l[0]; ++i) {
           int p = l[1 + i];
           if (part(p)[2] == -3) continue;
@@ -194,7 +198,7 @@ struct KeyMachine {
           }
         }
       }
-    int32_t* h = hdr();
+    SG_GLOBAL int32_t* h = hdr();
     h[K_FREE_P] = SG_NIL; h[K_NFREE_P] = 0;
     for (int p = g->P - 1; p >= 0; --p) {
       if (part(p)[2] == -3) { part(p)[2] = -2; continue; }
@@ -214,7 +218,7 @@ struct KeyMachine {
   SG_HD void maybe_gc() {
     int listed = 0;
     for (int s = 0; s < g->S; ++s) listed += list(s, 0)[0] + list(s, 1)[0];
-    int32_t* h = hdr();
+    SG_GLOBAL int32_t* h = hdr();
     int need_p = 2 * listed + 2 * g->S + 4, need_c = listed + 4, need_e = 4 + (g->A ? listed : 0);
     if (h[K_NFREE_P] < need_p || h[K_NFREE_C] < need_c || h[K_NFREE_E] < need_e) {
       gc();
@@ -225,7 +229,7 @@ struct KeyMachine {
   // ---------------------------------------------------------------- lists (LinkedList<StateEvent>)
   SG_HD int llen(int s, int w) { return list(s, w)[0]; }
   SG_HD void ladd(int s, int w, int p) {
-    int32_t* l = list(s, w);
+    SG_GLOBAL int32_t* l = list(s, w);
     if (l[0] >= g->L) { fail(SG_ECAPACITY); return; }
     l[1 + l[0]] = p;
     l[0]++;
@@ -301,7 +305,7 @@ struct KeyMachine {
   SG_HD bool filter(int s, int p) {
     if (lbits && lbits[s]) {   // (pred.h interleaved layout)
       const uint64_t r = (uint64_t)trig_local;
-      return ((lbits[s][(r >> 8) * 4 + (r & 3)] >> ((r >> 2) & 63)) & 1u) != 0;
+      return ((((const SG_GLOBAL uint64_t*)lbits[s])[(r >> 8) * 4 + (r & 3)] >> ((r >> 2) & 63)) & 1u) != 0;
     }
     PReader rd{this, p};
     return sg_eval(d->code + st(s).prog_off, st(s).prog_len, rd);
@@ -525,7 +529,7 @@ struct KeyMachine {
     if (x.kind == SG_K_LOGICAL || x.kind == SG_K_ALOGICAL) move_nae(x.partner);
   }
   SG_HD void move_nae(int s) {
-    int32_t* n = list(s, 1);
+    SG_GLOBAL int32_t* n = list(s, 1);
     for (int i = 0; i < n[0]; ++i) ladd(s, 0, n[1 + i]);
     n[0] = 0;
   }
@@ -588,12 +592,12 @@ struct KeyMachine {
   SG_HD int within_every(int s) { return clone ? -1 : st(s).within_every; }
 
   // ---- processAndReturn; returned partials are appended to ret[]
-  SG_HD int process_and_return(int s, int e, int32_t* ret, int retcap) {
+  SG_HD int process_and_return(int s, int e, SG_GLOBAL int32_t* ret, int retcap) {
     const sg_state_desc& x = st(s);
     if (x.kind == SG_K_ABSENT && !sth(s)[H_ACTIVE]) return 0;
     if (x.kind == SG_K_ALOGICAL) { alogical_process(s, e); return 0; }
     int nret = 0;
-    int32_t* l = list(s, 0);
+    SG_GLOBAL int32_t* l = list(s, 0);
     int n = l[0];
     int w = 0;
     int64_t t = ets(e);
@@ -651,7 +655,7 @@ struct KeyMachine {
   SG_HD void alogical_process(int s, int e) {
     const sg_state_desc& x = st(s);
     if (!sth(s)[H_ACTIVE]) return;
-    int32_t* l = list(s, 0);
+    SG_GLOBAL int32_t* l = list(s, 0);
     int n = l[0], w = 0;
     const int64_t t = ets(e);
     for (int r = 0; r < n && !failed; ++r) {
@@ -689,7 +693,7 @@ struct KeyMachine {
     if (!failed) l[0] = w;
   }
   SG_HD void list_remove_first(int s, int which, int p) {   // LinkedList.remove(Object)
-    int32_t* l = list(s, which);
+    SG_GLOBAL int32_t* l = list(s, which);
     for (int i = 0; i < l[0]; ++i)
       if (l[1 + i] == p) {
         for (int j = i + 1; j < l[0]; ++j) l[j] = l[1 + j];
@@ -701,7 +705,7 @@ struct KeyMachine {
   SG_HD int blank_event() {
     int e = alloc_ev();
     if (failed) return 0;
-    int32_t* x = ev(e);
+    SG_GLOBAL int32_t* x = ev(e);
     wr64(x, -1);
     wr64(x + 2, 0);
     x[4] = -1;
@@ -722,9 +726,9 @@ struct KeyMachine {
         reset_state(s);
       }
       update_state(s);
-      int32_t* l = list(s, 0);
+      SG_GLOBAL int32_t* l = list(s, 0);
       int n = l[0], w = 0;
-      int32_t* emitted = scratch(1);
+      SG_GLOBAL int32_t* emitted = scratch(1);
       int ne = 0;
       for (int r = 0; r < n && !failed; ++r) {
         int p = l[1 + r];
@@ -780,7 +784,7 @@ struct KeyMachine {
     return 0;
   }
   SG_HD void tq_push(int s, int64_t t) {   // scheduler.notifyAt(t)
-    int32_t* q = tq(absent_index(s));
+    SG_GLOBAL int32_t* q = tq(absent_index(s));
     if (q[1] >= g->Q) { fail(SG_ECAPACITY); return; }
     int pos = (q[0] + q[1]) % g->Q;
     wr64(q + 2 + 2 * pos, t);
@@ -792,8 +796,8 @@ struct KeyMachine {
   }
   SG_HD void absent_update_last_arrival(int s, int64_t ts) { absent_schedule(s, ts + st(s).waiting_time); }
   SG_HD bool tq_empty(int ai) { return tq(ai)[1] == 0; }
-  SG_HD int64_t tq_head(int ai) { int32_t* q = tq(ai); return rd64(q + 2 + 2 * q[0]); }
-  SG_HD void tq_pop(int ai) { int32_t* q = tq(ai); q[0] = (q[0] + 1) % g->Q; q[1]--; }
+  SG_HD int64_t tq_head(int ai) { SG_GLOBAL int32_t* q = tq(ai); return rd64(q + 2 + 2 * q[0]); }
+  SG_HD void tq_pop(int ai) { SG_GLOBAL int32_t* q = tq(ai); q[0] = (q[0] + 1) % g->Q; q[1]--; }
 
   // AbsentStreamPreStateProcessor.process(ComplexEventChunk) :140-210 for one TIMER event at currentTime
   SG_HD void absent_timer(int s, int64_t current) {
@@ -810,11 +814,11 @@ struct KeyMachine {
       reset_state(s);
     }
     move_nae(s);
-    int32_t* l = list(s, 0);
+    SG_GLOBAL int32_t* l = list(s, 0);
     int n = l[0], w = 0;
-    int32_t* emitted = scratch(1);
+    SG_GLOBAL int32_t* emitted = scratch(1);
     int ne = 0;
-    int32_t* reevery = scratch(2);
+    SG_GLOBAL int32_t* reevery = scratch(2);
     int nre = 0;
     lst = rd64(sth(s) + H_LST_LO);
     int we = within_every(s);
@@ -875,7 +879,7 @@ struct KeyMachine {
     if (ri < 0) return;
     const sg_receiver_desc& r = d->receivers[ri];
     phase = 1;
-    int32_t* ret = scratch(0);
+    SG_GLOBAL int32_t* ret = scratch(0);
     const int retcap = g->L;
     if (r.multi) {
       if (d->type == 0) { for (int k = 0; k < r.n; ++k) update_state(r.stab[k]); }
@@ -900,7 +904,7 @@ struct KeyMachine {
   SG_HD int copy_row(const SgRow& row) {
     int e = alloc_ev();
     if (failed) return 0;
-    int32_t* x = ev(e);
+    SG_GLOBAL int32_t* x = ev(e);
     wr64(x, row.ts);
     wr64(x + 2, (int64_t)row.index);
     x[4] = row.nullmask;

@@ -89,7 +89,7 @@ struct DevRows {
   const DevDesc* d;
   uint64_t base;
   const uint64_t* index;
-  __device__ uint64_t index_of(int64_t r) { return index ? index[r] : base + (uint64_t)r; }
+  __device__ uint64_t index_of(int64_t r) { return index ? gptr<uint64_t>(index)[r] : base + (uint64_t)r; }
   __device__ int64_t first_after(int64_t pos) {
     if (!index) {
       int64_t p = pos - (int64_t)base + 1;
@@ -98,29 +98,29 @@ struct DevRows {
     int64_t lo = 0, hi = n;
     while (lo < hi) {
       int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)index[mid] <= pos) lo = mid + 1;
+      if ((int64_t)gptr<uint64_t>(index)[mid] <= pos) lo = mid + 1;
       else hi = mid;
     }
     return lo;
   }
   __device__ int64_t n_own() { return nown; }
-  __device__ int64_t own_local(int64_t i) { return (int64_t)rows[i]; }
+  __device__ int64_t own_local(int64_t i) { return (int64_t)gptr<uint32_t>(rows)[i]; }
   __device__ int64_t n_rows() { return n; }
-  __device__ int64_t ts_at(int64_t r) { return ts[r]; }
-  __device__ int64_t ts_(int64_t r) { return ts[r]; }
+  __device__ int64_t ts_at(int64_t r) { return gptr<int64_t>(ts)[r]; }
+  __device__ int64_t ts_(int64_t r) { return gptr<int64_t>(ts)[r]; }
   __device__ int64_t find_ge(int64_t from, int64_t v) {
     int64_t lo = from, hi = n;
     while (lo < hi) {
       int64_t mid = (lo + hi) >> 1;
-      if (ts[mid] < v) lo = mid + 1;
+      if (gptr<int64_t>(ts)[mid] < v) lo = mid + 1;
       else hi = mid;
     }
     return lo;
   }
   __device__ void fill(int64_t r, SgRow& row) {
-    row.ts = ts[r];
+    row.ts = gptr<int64_t>(ts)[r];
     row.index = index_of(r);
-    row.stream = stream ? stream[r] : 0;
+    row.stream = stream ? gptr<int32_t>(stream)[r] : 0;
     row.nullmask = 0;
     for (int k = 0; k < d->n_ret; ++k) {
       SgVal v = sg_read_col(*cols, d->ret_col[k], d->ret_type[k], r);
@@ -131,7 +131,7 @@ struct DevRows {
 };
 // sg_run_key calls rows.ts(r)
 struct DevRowsTs : DevRows {
-  __device__ int64_t ts(int64_t r) { return DevRows::ts[r]; }
+  __device__ int64_t ts(int64_t r) { return gptr<int64_t>(DevRows::ts)[r]; }
 };
 
 // The descriptor (programs, state tables: ~9.6 KB) and the arena geometry are read hundreds of times per event;
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDes
   KeyMachine m;
   m.d = dd;
   m.g = geo;
-  m.a = ar;
+  m.a = (SG_GLOBAL int32_t*)ar;
   m.key = (int32_t)k;
   m.clone = a.clone;
   m.sink = sink;
@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(64) k_nfa_units(NfaArgs a, UnitArgs ua, SgCols
   KeyMachine m;
   m.d = dd;
   m.g = geo;
-  m.a = ar;
+  m.a = (SG_GLOBAL int32_t*)ar;
   m.key = (int32_t)k;
   m.clone = a.clone;
   m.sink = sink;

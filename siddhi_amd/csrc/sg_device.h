@@ -15,9 +15,16 @@
 #include "sg_host_shim.h"
 #else
 #include <hip/hip_runtime.h>
+#define SG_GLOBAL __attribute__((address_space(1)))
 #endif
 #include <stdint.h>
 #include "../../include/siddhi_gpu.h"
+
+// Column and packed-row reads go through global-address-space pointers: a generic pointer read out of a struct (a
+// kernel-argument view, a descriptor) would make every access a flat load, which also waits on the LDS traffic of
+// the same wave.
+template <class T>
+__device__ __forceinline__ const SG_GLOBAL T* gptr(const void* p) { return (const SG_GLOBAL T*)p; }
 
 struct SgVal {
   int64_t i;
@@ -36,13 +43,13 @@ __device__ __forceinline__ SgVal sg_read_col(const SgCols& c, int col, int type,
   v.type = type;
   v.i = 0;
   v.d = 0.0;
-  v.null = (c.nul[col] != nullptr && c.nul[col][row]) ? 1 : 0;
+  v.null = (c.nul[col] != nullptr && gptr<uint8_t>(c.nul[col])[row]) ? 1 : 0;
   if (v.null) return v;
   switch (type) {
-    case SG_T_LONG: v.i = ((const int64_t*)c.col[col])[row]; break;
-    case SG_T_FLOAT: v.d = (double)((const float*)c.col[col])[row]; break;
-    case SG_T_DOUBLE: v.d = ((const double*)c.col[col])[row]; break;
-    default: v.i = ((const int32_t*)c.col[col])[row]; break;
+    case SG_T_LONG: v.i = gptr<int64_t>(c.col[col])[row]; break;
+    case SG_T_FLOAT: v.d = (double)gptr<float>(c.col[col])[row]; break;
+    case SG_T_DOUBLE: v.d = gptr<double>(c.col[col])[row]; break;
+    default: v.i = gptr<int32_t>(c.col[col])[row]; break;
   }
   return v;
 }

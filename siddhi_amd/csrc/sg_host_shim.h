@@ -7,6 +7,7 @@
 #define __host__
 #define __device__
 #define __forceinline__ inline
+#define SG_GLOBAL
 static inline unsigned int __float_as_uint(float f) { unsigned int u; memcpy(&u, &f, 4); return u; }
 static inline float __uint_as_float(unsigned int u) { float f; memcpy(&f, &u, 4); return f; }
 static inline long long __double_as_longlong(double d) { long long u; memcpy(&u, &d, 8); return u; }
