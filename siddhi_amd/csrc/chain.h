@@ -41,22 +41,8 @@
 struct PpOperand {
   int32_t kind;      // SG_OP_VAR or SG_OP_CONST
   int32_t state, idx, slot, type;
-  int32_t at;        // where a VAR's event is (pp_classify): 0 through the lane's slots, 1 the row being processed,
-                     // 2 the partial's start row (partial lanes: value cached in registers at start, index cidx)
-  int32_t cidx;
   int64_t bits;
 };
-#define PP_MAX_CACHE 4    // start-row attribute values a partial lane keeps in registers
-
-// Where a term operand of state s's filter finds its event.  The filter of state s runs after s has bound the arriving
-// row (stream / logical: slot = row; count: the row appended to the chain), so `s.x` and `s[last].x` are that row's
-// attributes -- read without going through the lane's slots.
-SG_HD inline void pp_classify(PpOperand& o, int s, const sg_state_desc& x) {
-  o.at = 0;
-  o.cidx = -1;
-  if (o.kind != SG_OP_VAR || o.state != s) return;
-  if (x.kind == SG_K_COUNT ? o.idx == -1 : (o.idx == 0 || o.idx == -1)) o.at = 1;
-}
 struct PpTerm {
   PpOperand l, r;
   int32_t op, dom;
@@ -73,22 +59,7 @@ struct SgPpRule {
   int32_t visit_rank[PP_MAX_S];       // state -> its slot in the receiver's visit order
   int32_t nterm[PP_MAX_S];            // -1: the VM evaluates the state's filter
   PpTerm term[PP_MAX_S][PP_MAX_TERMS];
-  int32_t ncache;                     // start-row attributes the terms read (PpOperand.at == 2)
-  int32_t cslot[PP_MAX_CACHE], ctype[PP_MAX_CACHE];
 };
-
-// Start-row operands of the partial lanes' terms: the start state's slot is bound once (PpLane::start) and never
-// changes, so its attributes are read once per partial into registers instead of once per step.
-SG_HD inline void pp_cache_start(PpOperand& o, int start, SgPpRule& r) {
-  if (o.kind != SG_OP_VAR || o.at != 0 || o.state != start || !(o.idx == 0 || o.idx == -1)) return;
-  for (int i = 0; i < r.ncache; ++i)
-    if (r.cslot[i] == o.slot && r.ctype[i] == o.type) { o.at = 2; o.cidx = i; return; }
-  if (r.ncache >= PP_MAX_CACHE) return;
-  r.cslot[r.ncache] = o.slot;
-  r.ctype[r.ncache] = o.type;
-  o.at = 2;
-  o.cidx = r.ncache++;
-}
 
 // Parse a postfix filter into conjunctive compare terms (t1 t2 AND t3 AND ...); false if it has another form.
 SG_HD inline bool pp_operand(const int64_t* c, int len, int& pc, PpOperand& o) {
@@ -98,8 +69,6 @@ SG_HD inline bool pp_operand(const int64_t* c, int len, int& pc, PpOperand& o) {
     o.idx = (int32_t)c[pc + 2];
     o.slot = (int32_t)c[pc + 3];
     o.type = (int32_t)c[pc + 4];
-    o.at = 0;
-    o.cidx = -1;
     o.bits = 0;
     pc += 5;
     return true;
@@ -107,8 +76,6 @@ SG_HD inline bool pp_operand(const int64_t* c, int len, int& pc, PpOperand& o) {
   if (pc < len && c[pc] == SG_OP_CONST && pc + 3 <= len) {
     o.kind = SG_OP_CONST;
     o.state = o.idx = o.slot = 0;
-    o.at = 0;
-    o.cidx = -1;
     o.type = (int32_t)c[pc + 1];
     o.bits = c[pc + 2];
     pc += 3;
@@ -147,8 +114,6 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   r.recv = -1;
   r.n_hist = 0;
   r.local_mask = 0;
-  r.ncache = 0;
-  for (int i = 0; i < PP_MAX_CACHE; ++i) { r.cslot[i] = -1; r.ctype[i] = 0; }
   for (int s = 0; s < PP_MAX_S; ++s) { r.coff[s] = -1; r.visit_rank[s] = -1; r.nterm[s] = -1; }
   if (d.type != 0 || d.within < 0 || d.n_states < 2 || d.n_states > PP_MAX_S || d.n_sched != 0) return r;
   int nrecv = 0;
@@ -183,14 +148,6 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
     if (x.kind != SG_K_LOGICAL || s < x.partner) ++elems;
   }
   if (starts != 1 || d.n_start != 1 || chain > PP_MAX_CHAIN || elems > PP_MAX_HIST) return r;
-  for (int s = 0; s < d.n_states; ++s)
-    for (int i = 0; i < r.nterm[s]; ++i) {
-      PpTerm& t = r.term[s][i];
-      pp_classify(t.l, s, d.states[s]);
-      pp_classify(t.r, s, d.states[s]);
-      pp_cache_start(t.l, r.start, r);
-      pp_cache_start(t.r, r.start, r);
-    }
   r.n_hist = elems;
   r.ok = 1;
   return r;
@@ -275,17 +232,6 @@ struct PpLane {
   // current row
   int32_t cur_row;
   int cur_rank;
-  // start-row attributes the terms read (SgPpRule.cslot), in registers
-  int64_t cv[PP_MAX_CACHE];
-  uint32_t cnull;
-  SG_HD int64_t cached(int i) const {   // (constant indices only: the array stays in registers)
-    switch (i) {
-      case 0: return cv[0];
-      case 1: return cv[1];
-      case 2: return cv[2];
-      default: return cv[3];
-    }
-  }
 
   SG_HD const sg_state_desc& st(int s) const { return d->states[s]; }
   SG_HD static uint32_t bit(int s) { return 1u << s; }
@@ -307,16 +253,6 @@ struct PpLane {
     cur_rank = ru->visit_rank[ru->start];
     A->slot[ru->start] = (int32_t)row;
     e1_ts = src.ts(row);
-    cnull = 0;
-#pragma unroll
-    for (int i = 0; i < PP_MAX_CACHE; ++i) {
-      cv[i] = 0;
-      if (i < ru->ncache) {
-        int nl = 0;
-        src.read_bits(row, ru->cslot[i], ru->ctype[i], cv[i], nl);
-        cnull |= (uint32_t)nl << i;
-      }
-    }
     stream_post(ru->start);   // the `every` clone it also makes stays behind in the start state's lists
   }
 
@@ -360,15 +296,6 @@ struct PpLane {
     if (o.kind == SG_OP_CONST) {
       bits = o.bits;
       null = 0;
-      return;
-    }
-    if (o.at == 1) {   // the row being processed (pp_classify)
-      src.read_bits(cur_row, o.slot, o.type, bits, null);
-      return;
-    }
-    if (o.at == 2) {   // the start row, cached at start
-      bits = cached(o.cidx);
-      null = (int)((cnull >> o.cidx) & 1u);
       return;
     }
     const int32_t r = get_event(o.state, o.idx);
@@ -456,13 +383,13 @@ struct PpLane {
 
   // ---- one row: updateState of every state, then the states in visit order (KeyMachine::receive)
   // Returns the visit slot that emitted (one emission per row at most: the partial leaves the emitting state), or -1.
-  SG_HD int step(int32_t row) { return step(row, src.ts(row)); }
-  SG_HD int step(int32_t row, int64_t t) {   // t: the row's timestamp (the caller's expiry check already read it)
+  SG_HD int step(int32_t row) {
     cur_row = row;
     const sg_receiver_desc& rv = d->receivers[ru->recv];
     const uint32_t moved = l1;
     l0 |= moved;
     l1 = 0;
+    const int64_t t = src.ts(row);
     int emitted = -1;
     for (int k = 0; k < rv.n; ++k) {
       const int s = rv.pres[rv.n - 1 - k];

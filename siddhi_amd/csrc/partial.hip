@@ -214,32 +214,30 @@ struct PpPacked {
   const void* bcol[SG_MAX_RET];
   const void* ccol[SG_MAX_RET];
 };
-// (packed-row reads: global-address-space pointers, gptr in sg_device.h)
 __device__ __forceinline__ int64_t pp_lazy_ts(const PpPacked* P, int64_t q) {
-  const int64_t c = gptr<uint32_t>(P->sid)[q];
-  return c < P->nc ? gptr<int64_t>(P->cts)[c] : gptr<int64_t>(P->bts)[c - P->nc];
+  const int64_t c = P->sid[q];
+  return c < P->nc ? P->cts[c] : P->bts[c - P->nc];
 }
 __device__ __forceinline__ int64_t pp_lazy_bits(const PpPacked* P, int64_t q, int k) {
-  const int64_t c = gptr<uint32_t>(P->sid)[q];
+  const int64_t c = P->sid[q];
   const bool cr = c < P->nc;
   const void* col = cr ? P->ccol[k] : P->bcol[k];
   const int64_t r = cr ? c : c - P->nc;
-  return P->wide[k] ? gptr<int64_t>(col)[r] : (int64_t)gptr<int32_t>(col)[r];
+  return P->wide[k] ? ((const int64_t*)col)[r] : (int64_t)((const int32_t*)col)[r];
 }
 
 struct PpSrc {
   const PpPacked* P;
-  __device__ int64_t ts(int64_t q) const { return gptr<int64_t>(P->ts)[q]; }
+  __device__ int64_t ts(int64_t q) const { return P->ts[q]; }
   __device__ SgVal read(int64_t q, int slotk, int type) const {
-    int64_t bits;
-    int null;
-    read_bits(q, slotk, type, bits, null);
+    const int null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
+    const int64_t bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
     return sg_val_from_bits(bits, type, null);
   }
-  __device__ int lbit(int s, int64_t q) const { return (int)((gptr<uint32_t>(P->lb)[q] >> s) & 1u); }
+  __device__ int lbit(int s, int64_t q) const { return (int)((P->lb[q] >> s) & 1u); }
   __device__ void read_bits(int64_t q, int slotk, int type, int64_t& bits, int& null) const {
-    null = P->nul ? (int)((gptr<uint32_t>(P->nul)[q] >> slotk) & 1u) : 0;
-    bits = P->wide[slotk] ? gptr<int64_t>(P->val[slotk])[q] : (int64_t)gptr<int32_t>(P->val[slotk])[q];
+    null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
+    bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
   }
 };
 
@@ -518,8 +516,11 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   // the descriptor (9.6 KB) stays in global memory (cache-resident: every lane reads the same few hundred bytes of
   // it), so LDS holds more lanes
   __shared__ SgPpRule rl;
+  __shared__ PpPacked pl;
   __shared__ PpArraysT<G> lanes[PP_BLOCK];
   {
+    const uint32_t* s3 = (const uint32_t*)&P;
+    for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];
     const uint32_t* rs = (const uint32_t*)rug;
     uint32_t* rd = (uint32_t*)&rl;
     for (uint32_t i = threadIdx.x; i < sizeof(SgPpRule) / 4; i += blockDim.x) rd[i] = rs[i];
@@ -533,7 +534,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   const int64_t lo = wave * PP_WAVE_CANDS;
   const int64_t hi = lo + PP_WAVE_CANDS < ncand ? lo + PP_WAVE_CANDS : ncand;
   if (lo >= ncand) return;
-  PpSrc src{&P};   // (kernel-argument copy: scalar loads, no LDS round trip)
+  PpSrc src{&pl};
   PpLane<PpSrc, G> L;
   L.d = dd;
   L.ru = &rl;
@@ -559,11 +560,10 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   while (__ballot(active)) {
     bool done = false;
     if (active) {
-      const int64_t tq = q < e ? src.ts(q) : 0;
-      if (q >= e || tq - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
+      if (q >= e || src.ts(q) - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
         done = true;
       } else {
-        const int em = L.step(q, tq);
+        const int em = L.step(q);
         if (L.overflow) atomicCAS(o.fail, 0, SG_EUNSUPPORTED);
         if (em >= 0) {
           const int64_t c = sid[q];
@@ -746,15 +746,15 @@ static void sort_pairs64(SgHandle* h, const char* tag, uint64_t* k_in, uint64_t*
 }
 
 // ---- sequence lanes (seq.h): one lane per key resumes the key's compact machine over its rows ----------------------
-struct SeqSrcD {   // (global-address-space reads, as PpSrc)
+struct SeqSrcD {
   const PpPacked* P;
   int64_t base;
-  __device__ int64_t ts(int64_t pos) const { return P->ts ? gptr<int64_t>(P->ts)[base + pos] : pp_lazy_ts(P, base + pos); }
+  __device__ int64_t ts(int64_t pos) const { return P->ts ? P->ts[base + pos] : pp_lazy_ts(P, base + pos); }
   __device__ void read_bits(int64_t pos, int slotk, int type, int64_t& bits, int& null) const {
     const int64_t q = base + pos;
-    null = P->nul ? (int)((gptr<uint32_t>(P->nul)[q] >> slotk) & 1u) : 0;
+    null = P->nul ? (int)((P->nul[q] >> slotk) & 1u) : 0;
     if (!P->val[slotk]) { bits = pp_lazy_bits(P, q, slotk); return; }
-    bits = P->wide[slotk] ? gptr<int64_t>(P->val[slotk])[q] : (int64_t)gptr<int32_t>(P->val[slotk])[q];
+    bits = P->wide[slotk] ? ((const int64_t*)P->val[slotk])[q] : (int64_t)((const int32_t*)P->val[slotk])[q];
   }
   __device__ SgVal read(int64_t pos, int slotk, int type) const {
     int64_t bits;
@@ -762,7 +762,7 @@ struct SeqSrcD {   // (global-address-space reads, as PpSrc)
     read_bits(pos, slotk, type, bits, null);
     return sg_val_from_bits(bits, type, null);
   }
-  __device__ int lbit(int s, int64_t pos) const { return (int)((gptr<uint32_t>(P->lb)[base + pos] >> s) & 1u); }
+  __device__ int lbit(int s, int64_t pos) const { return (int)((P->lb[base + pos] >> s) & 1u); }
 };
 
 struct SqOut {
@@ -887,8 +887,11 @@ __device__ __forceinline__ void sq_run(Mach& m, int64_t b0, int64_t q0, int64_t 
 #define SQ_KERNEL_PROLOGUE                                                                                     \
   const DevDesc& dl = *ddg;                                                                                    \
   __shared__ SgSeqRule rl;                                                                                     \
+  __shared__ PpPacked pl;                                                                                      \
   __shared__ SeqStateT<G> lanes[SQ_BLOCK];                                                                         \
   {                                                                                                            \
+    const uint32_t* s3 = (const uint32_t*)&P;                                                                  \
+    for (uint32_t i = threadIdx.x; i < sizeof(PpPacked) / 4; i += blockDim.x) ((uint32_t*)&pl)[i] = s3[i];    \
     const uint32_t* rs = (const uint32_t*)rug;                                                                 \
     for (uint32_t i = threadIdx.x; i < sizeof(SgSeqRule) / 4; i += blockDim.x) ((uint32_t*)&rl)[i] = rs[i];   \
     __syncthreads();                                                                                           \
@@ -910,7 +913,7 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
   SeqMachine<SeqSrcD, G> m;
   m.d = &dl;
   m.ru = &rl;
-  m.src = SeqSrcD{&P, b0};
+  m.src = SeqSrcD{&pl, b0};
   m.M = &M;
   m.cur = 0;
   SqNoEmit ne;
@@ -956,7 +959,7 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const
   SeqMachine<SeqSrcD, G> m;
   m.d = &dl;
   m.ru = &rl;
-  m.src = SeqSrcD{&P, b0};
+  m.src = SeqSrcD{&pl, b0};
   m.M = &M;
   m.cur = 0;
   SqEmit em;

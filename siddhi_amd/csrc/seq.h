@@ -88,11 +88,6 @@ SG_HD inline SgSeqRule sg_seq_rule(const sg_nfa_desc& d) {
     if (x.kind == SG_K_LOGICAL && (x.partner < 0 || d.states[x.partner].kind != SG_K_LOGICAL)) return r;
   }
   if (starts != 1 || r.chain > PQ_MAX_CHAIN) return r;
-  for (int s = 0; s < d.n_states; ++s)
-    for (int i = 0; i < r.nterm[s]; ++i) {
-      pp_classify(r.term[s][i].l, s, d.states[s]);
-      pp_classify(r.term[s][i].r, s, d.states[s]);
-    }
   // pool bound: one partial per non-start element's newAndEvery list, the start state's every-clone, and the one
   // allocated inside a step before the step's frees (logical partners share their partial: one element)
   int elements = 0;
@@ -260,10 +255,6 @@ struct SeqMachine {
     if (o.kind == SG_OP_CONST) {
       bits = o.bits;
       null = 0;
-      return;
-    }
-    if (o.at == 1) {   // the row being processed (pp_classify)
-      src.read_bits(cur, o.slot, o.type, bits, null);
       return;
     }
     const int64_t r = get_event(p, o.state, o.idx);
