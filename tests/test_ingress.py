@@ -27,7 +27,7 @@ def _c4_batch(n, ids):
     ("C1", 200_000, 1, 1, 30_000, {}),
     ("C3b", 200_000, 500, 1_000, 45_000, {}),
     ("C3c", 100_000, 500, 100, 33_333, {}),
-    ("C4", 200_000, 10_000, 1, 40_000, {}),
+    ("C4", 60_000, 10_000, 1, 14_000, {}),
 ], ids=["C2", "C2-ragged", "C1", "C3b", "C3c", "C4"])
 def test_chunked_ingress_parity(cfg, n, keys, rate, chunk, kw):
     from siddhi_amd._native import GpuEngine

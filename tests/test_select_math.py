@@ -233,7 +233,7 @@ def test_gpu_having_edge_values():
     ("C2", 100_000, 500, 100, {"force_general": True}),
     ("C1", 200_000, 1, 1, {}),
     ("C3b", 200_000, 500, 1_000, {}),
-    ("C4", 100_000, 10_000, 1, {}),
+    ("C4", 30_000, 10_000, 1, {}),
 ], ids=["C2", "C2-general", "C1", "C3b", "C4"])
 def test_gpu_having_parity(cfg, n, keys, rate, kw):
     from siddhi_amd._native import GpuEngine
@@ -285,7 +285,7 @@ def test_gpu_select_arithmetic_parity(cfg, n, keys, rate, kw):
 @pytest.mark.gpu
 def test_gpu_select_arithmetic_absence():
     from siddhi_amd._native import GpuEngine
-    n = 100_000
+    n = 30_000
     b = synth_batch("C4", 0, n, keys=10_000, rate=1)
     ts = np.append(b.ts, b.ts[-1] + 5001)
     st = np.append(b.stream, np.int32(1)).astype(np.int32)

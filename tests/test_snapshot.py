@@ -82,7 +82,7 @@ def test_snapshot_restore_continues_stream(cfg, n, keys, rate, kw, splits):
 
 
 @gpu
-@pytest.mark.parametrize("kw,n", [({}, 200_000), ({"force_general": True, "pool": 16384}, 4_000)],
+@pytest.mark.parametrize("kw,n", [({}, 60_000), ({"force_general": True, "pool": 16384}, 4_000)],
                          ids=["closed-form", "general"])
 def test_snapshot_restore_absence(kw, n):
     """C4: the pending partials and their timers survive a restore; the final Tick fires them."""
