@@ -218,6 +218,13 @@ class _QueryRuntime:
             self.global_streams = {i for i, sid in enumerate(self.ctx.stream_ids)
                                    if sid in reads and self.ctx.key_attr[i] < 0}
         self.sel_types = [self._select_type(oa.expr) for oa in query.select]
+        # the query is checked (types, references) when the app is created, whichever engine runs it
+        # (SiddhiAppRuntime creation -> ExpressionParser throws SiddhiAppCreationException, C/util/parser/
+        # ExpressionParser.java: parseCompare for a compare the executors do not support)
+        try:
+            L.lower(self.ctx)
+        except L.LoweringError as x:
+            raise SiddhiAppCreationException(str(x)) from x
         self.engine = engine_factory(self.ctx)
         self.query_callbacks: List[QueryCallback] = []
 
