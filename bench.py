@@ -315,11 +315,13 @@ def _ctx(cfg):
 
 # SURVEY.md §8d algorithmic bytes per config: (whole path B/event, B/match, predicate pass B/event)
 #   C1: ts 8 + price 4 + bit; C2/C5: + key 4; 36 B/match (trigger 8, rank 4, ts 8, two slot indices 8+8)
-#   C3b/C3c: ts 8 + key 4 + v 4 + w 4 + bits; 92 B/match (trigger, rank, ts, 4 slots x 8, 5 projected x 8)
+#   C3b/C3c: ts 8 + key 4 + v 4 + w 4 + bits; 92 B/match (trigger, rank, ts, 4 slots x 8, 5 projected x 8); the
+#            predicate pass reads only v (e1's filter is the one event-local filter): 4.125 B/event, as its PMC
+#            FETCH+WRITE shows (profiles/r03/C3b_pmc.json: 412.6 MB per 100M events)
 #   C4: ts 8 + id 8 (no local predicate: no predicate pass); 28 B per emission (one slot)
 PATH_BYTES = {"C1": (12.125, 36.0, 4.125), "C2": (16.125, 36.0, 4.125), "C5": (16.125, 36.0, 4.125),
               "PP": (20.125, 36.0, 4.125), "PPe": (20.125, 36.0, 4.125),   # + the stream column (4 B)
-              "C3b": (20.125, 92.0, 8.125), "C3c": (20.125, 92.0, 8.125), "C3": (20.125, 92.0, 4.125),
+              "C3b": (20.125, 92.0, 4.125), "C3c": (20.125, 92.0, 4.125), "C3": (20.125, 92.0, 4.125),
               "C4": (16.0, 28.0, None)}
 
 
