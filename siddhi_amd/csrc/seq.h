@@ -4,8 +4,8 @@
 // in (StateStreamRuntime.resetAndUpdate, C/query/input/stream/state/StateStreamRuntime.java:96-99), and addState admits
 // one partial per newAndEvery list (StreamPreStateProcessor.addState :203-216, CountPreStateProcessor.addState :109-132,
 // LogicalPreStateProcessor.addState :62-83).  So a key's runtime is a handful of partials, and for sequences whose
-// start state re-arms with `every` it stays small (its partials reference at most the key's last H events, H = sum of
-// the states' max counts).  This machine is interp.h's KeyMachine restricted to such sequences (stream, count and
+// start state re-arms with `every` it stays small: each live partial references only events among the key's last H
+// rows (H = sum of the states' max counts) -- which partials are live, though, depends on the whole history (below).  This machine is interp.h's KeyMachine restricted to such sequences (stream, count and
 // logical states of one stream, `every` only on the start state) with everything sized to that: partials in a pool of
 // at most PQ_MAX_P entries with their count chains inline, lists of at most PQ_MAX_L entries, events as row positions
 // (the rows stay in HBM, key-ordered) -- a few hundred bytes of LDS per lane instead of a 30 KB HBM arena.
