@@ -336,8 +336,8 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
 int sg_node_push(sg_node* nd, const sg_node_batch* b, const sg_match_columns* out, int64_t cap, int64_t* n);
 int sg_node_reset(sg_node* nd);   /* new stream: forget keys and per-key state */
 /* Where partition keys are dictionary-encoded (first-seen dense ids, PartitionRuntime.cloneIfNotExist,
- * C/partition/PartitionRuntime.java:255-308): 0 auto (the device when the first push's first 64K rows hold more than
- * 16K distinct keys and the query has no playback timers, else the host), 1 the host
+ * C/partition/PartitionRuntime.java:255-308): 0 auto (the device whenever the query has no playback timers, else
+ * the host), 1 the host
  * router (sg_router), 2 one dictionary per GPU in HBM (raw keys are uploaded; with several GPUs rows go to shard
  * mix64(raw) mod n_gpus).  Only before the first push of a stream. */
 int sg_node_set_key_dict(sg_node* nd, int mode);

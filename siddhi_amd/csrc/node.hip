@@ -1195,26 +1195,14 @@ void set_tags(sg_node& nd, bool on) {
   nd.hist_n = 0;
 }
 
-// Auto key dictionary: a stream whose first 64K rows hold few distinct keys keeps its dictionary on the host (a
-// cache-resident table; the GPU then receives 4-byte dense ids instead of 8-byte raw keys); many keys (a DRAM-bound
-// table on the host) are encoded on the GPUs.
-bool few_keys(const sg_node_batch& b) {
-  const int64_t m = std::min<int64_t>(b.n, 65536);
-  sgr::KeyMap seen;
-  seen.init(1 << 17);
-  int64_t distinct = 0;
-  for (int64_t i = 0; i < m; ++i) {
-    if (b.stream && b.stream[i] < 0) continue;
-    if (seen.insert(b.raw_key[i], 0) < 0 && ++distinct > 16384) return false;
-  }
-  return true;
-}
-
+// Auto key dictionary: keys are encoded on the GPUs whenever the query allows it (partitioned, no playback clocks).
+// Measured on C2 (100M events, 10k keys, one GPU, profiles/r03/whole_node_*_dict.log): the host router's lookups were
+// the pipeline's bound (route 50 ms of 58.7 ms per push) even with a cache-resident table, while raw 8-byte keys cost
+// only 0.4 GB more H2D (route 13 ms, 48.8 ms per push); with 1M keys (C5) the host table is DRAM-bound as well.
 void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, int64_t cap, int64_t* n_out) {
   if (nd.ddict < 0) {   // the first push of a stream fixes where keys are encoded, and whether rows carry tags
     const bool dev_ok = nd.desc.partitioned && !need_clocks(nd.desc);
-    nd.ddict = (dev_ok && nd.key_dict_mode == 2) ? 1 : 0;
-    if (dev_ok && nd.key_dict_mode == 0) nd.ddict = few_keys(b) ? 0 : 1;
+    nd.ddict = (dev_ok && nd.key_dict_mode != 1) ? 1 : 0;
     // tags save PCIe bytes at the price of host selector work (random e1 reads): opt-in, SG_NODE_TAGS=1
     const char* e = getenv("SG_NODE_TAGS");
     const bool want = nd.tag_cand >= 0 && e && e[0] == '1';   // (measured: the host's e1 gathers cost more than
