@@ -153,6 +153,20 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   return r;
 }
 
+// Carry window of the partial-lane route: per key, the rows with ts >= last ts - window survive into the next push
+// and rebuild every partial that can still match (`within` of the key's last row).  A query with a count state
+// carries one more `within` of rows (pp_regress_tol): count states never expire partials (CountPreStateProcessor.
+// processAndReturn, C/query/input/stream/state/CountPreStateProcessor.java:53-93), so a push whose time goes BACK can
+// revive a partial parked in a count state after it left `within`.  When a key's time goes back by at most the
+// tolerance below its last carried row, the per-key machine rebuilt from these rows takes over exactly: every partial
+// it lacks started before last - within - tol and stays expired for every row at or after last - tol
+// (StreamPreStateProcessor.isExpired compares |ts - e1.ts| with `within`).  A deeper regression is SG_EORDER.
+SG_HD inline int64_t pp_regress_tol(const sg_nfa_desc& d, bool has_count) { return has_count ? d.within : 0; }
+SG_HD inline int64_t pp_carry_window(const sg_nfa_desc& d, bool has_count) {
+  const int64_t tol = pp_regress_tol(d, has_count);
+  return d.within > INT64_MAX / 4 || tol > INT64_MAX / 4 ? d.within : d.within + tol;
+}
+
 SG_HD inline bool pp_cmp_i(int op, int64_t a, int64_t b) {
   switch (op) {
     case 0: return a == b;

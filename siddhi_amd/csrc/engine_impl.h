@@ -292,7 +292,10 @@ static __global__ void __launch_bounds__(256) k_bounds(const uint32_t* __restric
 // as whole lines.  Pass 1 reads the raw columns and builds the walker records on the way (no pack pass);
 // pass 2 reads pass 1's records and 1-byte in-group keys.  The per-key segments are read off the last
 // pass's offsets (no bounds pass).  Same result as the radix sort: per key its rows in arrival order.
-static const int PT_PER = 8;                 // rows per thread per sub-tile
+#ifndef SG_PT_PER
+#define SG_PT_PER 8
+#endif
+static const int PT_PER = SG_PT_PER;         // rows per thread per sub-tile
 static const int PT_ROWS = 256 * PT_PER;   // rows per LDS-staged sub-tile (2048: 4 workgroups per CU)
 static const int PT_D = 256;       // digit values per pass (8 bits)
 

@@ -14,13 +14,14 @@
 //                      written with its sort key (trigger row, visit slot) and its insertion history (tie key)
 //   5. match order     stable radix sorts: tie words, then (trigger, visit slot) -> the reference's delivery order;
 //                      k_pp_gather writes the match records
-//   6. carry           per key, the rows with ts >= last ts - within become the next push's carried rows
+//   6. carry           per key, the rows with ts >= last ts - window become the next push's carried rows (window =
+//                      within, plus one more `within` for queries with a count state: chain.h pp_carry_window)
 // A push that breaks the ordering precondition leaves this route: the carried rows are handed back so the caller can
-// replay them through the general machine (interp.hip) and continue there.  That replay is exact unless the query has a
-// count state: CountPreStateProcessor never expires a partial (CountPreStateProcessor.java:53-93), so with time going
-// back a partial parked in a count state longer than `within` could still complete, and the carried rows do not hold
-// it -- such a push fails with SG_EORDER, like the closed forms (open the handle with partial_lanes = -1 for streams
-// whose timestamps go back).
+// replay them through the general machine (interp.hip) and continue there.  With a count state that replay is exact only
+// for a regression of at most `within` below the key's last carried row: CountPreStateProcessor never expires a partial
+// (CountPreStateProcessor.java:53-93), so time going back further could revive a partial parked in a count state that
+// the carried rows do not hold -- such a push fails with SG_EORDER, like the closed forms (open the handle with
+// partial_lanes = -1 for streams whose timestamps may go back that far).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -406,25 +407,42 @@ __global__ void __launch_bounds__(256) k_pp_unpack(PpArgs a, SgCols bc, SgCols c
   }
 }
 
+// err bit 1: a key's timestamps go back somewhere; bit 8: by more than `tol` below the key's last carried row (the
+// regression the per-key machine cannot take over exactly, pp_regress_tol).  check_order 0: no check.
 __global__ void k_pp_segments(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
-                              const int64_t* __restrict__ qts, int check_order, uint32_t sentinel,
+                              const int64_t* __restrict__ qts, int check_order, int64_t tol, uint32_t sentinel,
                               uint32_t* __restrict__ beg, uint32_t* __restrict__ end, int32_t* __restrict__ err) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= m) return;
   const uint32_t k = skey[p];
   if (k == sentinel) return;
+  auto ts_at = [&](int64_t q) -> int64_t {
+    if (qts) return qts[q];
+    const int64_t c = sid[q];
+    return c < a.nc ? a.cts[c] : a.bts[c - a.nc];
+  };
   if (p == 0 || skey[p - 1] != k) beg[k] = (uint32_t)p;
   else if (check_order) {
-    int64_t t0, t1;
-    if (qts) {
-      t0 = qts[p - 1];
-      t1 = qts[p];
-    } else {
-      const int64_t c0 = sid[p - 1], c1 = sid[p];
-      t0 = c0 < a.nc ? a.cts[c0] : a.bts[c0 - a.nc];
-      t1 = c1 < a.nc ? a.cts[c1] : a.bts[c1 - a.nc];
+    const int64_t t1 = ts_at(p);
+    if (ts_at(p - 1) > t1) {   // (rare: searched, not precomputed)
+      int32_t f = 1;
+      if (check_order == 2) {
+        int64_t lo = 0, hi = p;   // the key's first position
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (skey[mid] < k) lo = mid + 1; else hi = mid;
+        }
+        if ((int64_t)sid[lo] < a.nc) {   // carried rows (they come first): the key's last one
+          int64_t l2 = lo, h2 = p;
+          while (l2 < h2) {
+            const int64_t mid = (l2 + h2) >> 1;
+            if ((int64_t)sid[mid] < a.nc) l2 = mid + 1; else h2 = mid;
+          }
+          if (t1 < ts_at(l2 - 1) - tol) f |= 8;
+        }
+      }
+      atomicOr(err, f);
     }
-    if (t0 > t1) atomicOr(err, 1);
   }
   if (p == m - 1 || skey[p + 1] != k) end[k] = (uint32_t)p + 1;
 }
@@ -1301,6 +1319,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
       throw SgError(SG_ECAPACITY, "partial-lane route: push at most 2^27 rows at a time (carried rows included)");
     return 0;
   }
+  // the route's ordering precondition (k_pp_segments): 1 detect a key's time going back, 2 also whether it went back
+  // deeper than the regression tolerance below the key's carried rows (count states with carried rows only)
+  const int order_check = ps->mode == 1 ? ((ps->has_count && nc > 0) ? 2 : 1) : 0;
+  const int64_t tol = pp_regress_tol(d, ps->has_count != 0);
   PpArgs a;
   memset(&a, 0, sizeof(a));
   a.nc = nc;
@@ -1424,7 +1446,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
       HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
-      hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, P.ts, ps->mode == 1 ? 1 : 0, sentinel, beg,
+      hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, P.ts, order_check, tol, sentinel, beg,
                          end, err);
       HIPCHK(hipGetLastError());
       h->kend();
@@ -1446,7 +1468,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
     HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
     if (m) hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, (const int64_t*)nullptr,
-                              ps->mode == 1 ? 1 : 0, sentinel, beg, end, err);
+                              order_check, tol, sentinel, beg, end, err);
     HIPCHK(hipGetLastError());
     h->kend();
     h->kbeg("pack");
@@ -1461,10 +1483,11 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     HIPCHK(hipStreamSynchronize(st));
     if (herr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
     if ((herr & 1) && ps->mode == 1) {
-      if (ps->has_count && nc > 0)
-        throw SgError(SG_EORDER, "partial-lane route requires non-decreasing timestamps per key once a count state holds "
-                                 "partials (open the handle with partial_lanes = -1 for such streams)");
-      return 0;
+      if (herr & 8)
+        throw SgError(SG_EORDER, "partial-lane route: a key's time went back by more than `within` below its carried "
+                                 "rows while a count state may hold partials (open the handle with partial_lanes = -1 "
+                                 "for such streams)");
+      return 0;   // the per-key machine, rebuilt from the carried rows, takes over exactly
     }
   }
   h->mark(2);
@@ -1573,7 +1596,8 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   // ---- carry
   if (!h->opt.no_carry && m) {
     uint32_t* keep = (uint32_t*)h->ws.get("pp_keep", 4 * (m + 1), st);
-    hipLaunchKernelGGL(k_pp_keep, grd, blk, 0, st, m, a, skeys, sids, end, sentinel, (int64_t)d.within, keep);
+    hipLaunchKernelGGL(k_pp_keep, grd, blk, 0, st, m, a, skeys, sids, end, sentinel,
+                       ps->mode == 1 ? pp_carry_window(d, ps->has_count) : (int64_t)d.within, keep);
     carry_rows(h, ps, bv, a, m, skeys, sids, keep);
   }
   h->mark(4);

@@ -140,9 +140,23 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
   HostPpSrc src{b, &d, &h->carried, nc};
   bool has_count = false;
   for (int s = 0; s < d.n_states; ++s) has_count |= d.states[s].kind == SG_K_COUNT;
-  for (const auto& rows : own)   // the route's precondition: a key's timestamps never decrease (also across pushes)
-    for (size_t p = 1; p < rows.size(); ++p)
-      if (src.ts(rows[p - 1]) > src.ts(rows[p])) return (has_count && nc > 0) ? -2 : 0;
+  // the route's precondition: a key's timestamps never decrease (also across pushes).  A push that breaks it goes to
+  // the per-key machine rebuilt from the carried rows -- exactly, unless a count state's partial older than the carry
+  // window could be revived (a regression deeper than pp_regress_tol below the key's last carried row): SG_EORDER
+  {
+    const int64_t tol = pp_regress_tol(d, has_count);
+    bool regress = false, deep = false;
+    for (const auto& rows : own) {
+      int64_t last_car = INT64_MIN;   // the key's last carried row's ts (carried rows come first)
+      for (size_t p = 0; p < rows.size() && rows[p] < nc; ++p) last_car = src.ts(rows[p]);
+      for (size_t p = 1; p < rows.size(); ++p)
+        if (src.ts(rows[p - 1]) > src.ts(rows[p])) {
+          regress = true;
+          if (has_count && last_car != INT64_MIN && src.ts(rows[p]) < last_car - tol) deep = true;
+        }
+    }
+    if (regress) return deep ? -2 : 0;
+  }
   const int rstride = 32 + 8 * d.n_select;
   for (size_t k = 0; k < own.size(); ++k) {
     const auto& rows = own[k];
@@ -193,14 +207,15 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
       }
     }
   }
-  // carry: per key, rows with ts >= last ts - within
+  // carry: per key, rows with ts >= last ts - window (pp_carry_window)
   std::vector<HiHandle::CRow> next;
+  const int64_t window = pp_carry_window(d, has_count);
   for (size_t k = 0; k < own.size(); ++k) {
     const auto& rows = own[k];
     if (rows.empty()) continue;
     const int64_t last = src.ts(rows.back());
     for (int64_t c : rows) {
-      if (src.ts(c) < last - d.within) continue;
+      if (src.ts(c) < last - window) continue;
       HiHandle::CRow cr;
       memset(&cr, 0, sizeof(cr));
       cr.ts = src.ts(c);

@@ -122,9 +122,9 @@ def test_unpartitioned():
     assert_same(got, want)
 
 
-def _going_back(q):
+def _going_back(q, back=40):
     a = small_batch(10_000, 20, 100, 4, seed=11)
-    b = small_batch(10_000, 20, 100, 4, seed=12, start=10_000, t0=-40)   # starts 40 ms before a's end
+    b = small_batch(10_000, 20, 100, 4, seed=12, start=10_000, t0=-back)   # starts `back` ms before a's end
     b.key[:] = a.key[:10_000]
     b.cols[1][:] = b.key
     return Batch(20_000, 0, np.concatenate([a.ts, b.ts]), np.zeros(20_000, np.int32), np.concatenate([a.key, b.key]),
@@ -145,15 +145,22 @@ def test_timestamps_going_back_leave_the_route(name):
 
 
 def test_timestamps_going_back_with_a_count_state():
-    """With a count state the carried rows cannot rebuild partials parked in it for longer than `within` (they never
-    expire, CountPreStateProcessor.java:53-93, and would be live again once time goes back): SG_EORDER, as the closed
-    forms do; the per-key machine (partial_lanes = -1) takes such streams."""
-    q = HEAD + SHAPES["c3c"]
-    both = _going_back(q)
+    """Count states never expire partials (CountPreStateProcessor.java:53-93), so time going back can revive one parked
+    in a count state after it left `within`.  The route carries one extra `within` of rows for such queries
+    (chain.h pp_carry_window): a key whose time goes back by at most `within` below its carried rows continues exactly
+    on the per-key machine rebuilt from them; a deeper regression is SG_EORDER, and the per-key machine from the start
+    (partial_lanes = -1) takes such streams."""
+    q = HEAD + SHAPES["c3c"]   # within 60 ms
+    shallow = _going_back(q, back=40)
+    assert shallow.ts[10_000] < shallow.ts[9_999]
+    want = run_engine(OracleEngine, q, [shallow])
+    assert len(want) > 0
+    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(shallow, [10_000, 15_000])), want)
+    deep = _going_back(q, back=400)
     with pytest.raises(RuntimeError, match="-5"):
-        run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(both, [10_000, 15_000]))
-    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=False), q, split(both, [10_000, 15_000])),
-                run_engine(OracleEngine, q, [both]))
+        run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(deep, [10_000, 15_000]))
+    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=False), q, split(deep, [10_000, 15_000])),
+                run_engine(OracleEngine, q, [deep]))
 
 
 def test_seq_rule_covers_the_shapes():
@@ -241,13 +248,17 @@ def test_gpu_unpartitioned_and_order_fallback():
     both = _going_back(q)
     assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(both, [10_000, 15_000])),
                 run_engine(OracleEngine, q, [both]))
-    q = HEAD + SHAPES["c3c"]
-    both = _going_back(q)
-    with pytest.raises(SgError):
-        run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(both, [10_000, 15_000]))
+    q = HEAD + SHAPES["c3c"]   # count state, within 60 ms: a 40 ms regression continues exactly, 400 ms is SG_EORDER
+    shallow = _going_back(q, back=40)
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(shallow, [10_000, 15_000])),
+                run_engine(OracleEngine, q, [shallow]))
+    deep = _going_back(q, back=400)
+    with pytest.raises(SgError) as ei:
+        run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(deep, [10_000, 15_000]))
+    assert ei.value.code == -5
     assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=-1), q,
-                           split(both, [10_000, 15_000])),
-                run_engine(OracleEngine, q, [both]))
+                           split(deep, [10_000, 15_000])),
+                run_engine(OracleEngine, q, [deep]))
 
 
 @pytest.mark.gpu
