@@ -292,24 +292,31 @@ static __global__ void __launch_bounds__(256) k_bounds(const uint32_t* __restric
 // as whole lines.  Pass 1 reads the raw columns and builds the walker records on the way (no pack pass);
 // pass 2 reads pass 1's records and 1-byte in-group keys.  The per-key segments are read off the last
 // pass's offsets (no bounds pass).  Same result as the radix sort: per key its rows in arrival order.
-#ifndef SG_PT_PER
-#define SG_PT_PER 8
+// Rows per thread per LDS-staged sub-tile, per pass (measured on C2, 100M events / 10k keys: pass 1 -- raw columns in,
+// 16-B records out, 79 key-group digits -- is fastest with 1024-row sub-tiles (more resident workgroups: part_group
+// 1.26 -> 1.04 ms); pass 2 -- records in, 128 in-group digits -- with 4096-row ones (longer runs per digit: part_key
+// 0.90 -> 0.78 ms))
+#ifndef SG_PT1
+#define SG_PT1 4
 #endif
-static const int PT_PER = SG_PT_PER;         // rows per thread per sub-tile
-static const int PT_ROWS = 256 * PT_PER;   // rows per LDS-staged sub-tile (2048: 4 workgroups per CU)
+#ifndef SG_PT2
+#define SG_PT2 16
+#endif
+static const int PT1 = SG_PT1, PT1_ROWS = 256 * SG_PT1;
+static const int PT2 = SG_PT2, PT2_ROWS = 256 * SG_PT2;
 static const int PT_D = 256;       // digit values per pass (8 bits)
 
 struct PartPlan {
   uint32_t K, lb, ng, two;    // keys; pass-2 digit bits (key & (2^lb - 1)); pass-1 digit values (key >> lb); 2 passes?
   uint32_t nb1, nb2;          // bits that tell the digits apart (ballots per 64-row step)
-  uint32_t seg1, ns1;         // rows per pass-1 segment (multiple of PT_ROWS); pass-1 segments
+  uint32_t seg1, ns1;         // rows per pass-1 segment (multiple of PT1_ROWS); pass-1 segments
   uint32_t ts2, nj;           // pass-1 segments per pass-2 segment; pass-2 segments per group
 };
 
-template <class R>
+template <class R, int PT>
 struct PartLds {
-  R stage[PT_ROWS];           // the sub-tile's records, sorted by digit
-  uint16_t tag[PT_ROWS];      // key (pass 1) / in-group key (pass 2) of each staged record
+  R stage[256 * PT];          // the sub-tile's records, sorted by digit
+  uint16_t tag[256 * PT];     // key (pass 1) / in-group key (pass 2) of each staged record
   uint32_t cw[4][PT_D];       // per-wave digit counts, then per-wave slot cursors
   uint32_t ls[PT_D];          // sub-tile start of each digit
   uint32_t tot[PT_D];         // sub-tile count of each digit
@@ -345,8 +352,8 @@ __device__ __forceinline__ void peer_rank(bool valid, uint32_t d, uint32_t nb, u
 }
 
 // digit counts -> per-wave slot cursors and sub-tile digit starts; returns the sub-tile's staged rows
-template <class R>
-__device__ __forceinline__ uint32_t part_cursors(PartLds<R>& L) {
+template <class R, int PT>
+__device__ __forceinline__ uint32_t part_cursors(PartLds<R, PT>& L) {
   const uint32_t t = threadIdx.x;
   const uint32_t c0 = L.cw[0][t], c1 = L.cw[1][t], c2 = L.cw[2][t], c3 = L.cw[3][t];
   const uint32_t tot = c0 + c1 + c2 + c3;
@@ -397,7 +404,7 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
                                                uint8_t* __restrict__ olk, uint32_t* __restrict__ flags) {
   typedef WRec<T, N> R;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  PartLds<R>& L = *(PartLds<R>*)lds_raw;
+  PartLds<R, PT1>& L = *(PartLds<R, PT1>*)lds_raw;
   const uint32_t j = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t lmask = (1u << pp.lb) - 1u;
   if (t < pp.ng) L.run[t] = o1[(size_t)t * pp.ns1 + j];
@@ -406,13 +413,13 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
   uint32_t bad = 0;
   // the sub-tile's loads, all issued before the first use (one memory latency per sub-tile)
   auto load = [&](int64_t base, uint32_t* tg, R* rc) {
-    const uint32_t rows = (uint32_t)((re - base < PT_ROWS) ? re - base : PT_ROWS);
+    const uint32_t rows = (uint32_t)((re - base < PT1_ROWS) ? re - base : PT1_ROWS);
     if (base >= (int64_t)pk.v.nc) {
       // batch rows only: branch-free loads (rows past the end re-read the last row and are dropped)
       const uint32_t b0 = (uint32_t)(base - pk.v.nc), last = rows - 1;
 #pragma unroll
-      for (int s = 0; s < PT_PER; ++s) {
-        const uint32_t i = w * (PT_PER * 64) + s * 64 + lane;
+      for (int s = 0; s < PT1; ++s) {
+        const uint32_t i = w * (PT1 * 64) + s * 64 + lane;
         const uint32_t b = b0 + (i < rows ? i : last);
         const uint32_t k = (uint32_t)pk.v.key[b];
         uint32_t bd = 0;
@@ -422,8 +429,8 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
       }
     } else {
 #pragma unroll
-      for (int s = 0; s < PT_PER; ++s) {
-        const uint32_t i = w * (PT_PER * 64) + s * 64 + lane;
+      for (int s = 0; s < PT1; ++s) {
+        const uint32_t i = w * (PT1 * 64) + s * 64 + lane;
         const uint32_t r = (uint32_t)(base + i);
         const uint32_t k = i < rows ? kf(r) : 0xffffffffu;
         tg[s] = k < pp.K ? k : 0xffffffffu;
@@ -441,20 +448,20 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
       }
     }
   };
-  uint32_t tg[PT_PER], tn[PT_PER];
-  R rc[PT_PER], rn[PT_PER];
+  uint32_t tg[PT1], tn[PT1];
+  R rc[PT1], rn[PT1];
   if (rb < re) load(rb, tg, rc);
-  for (int64_t base = rb; base < re; base += PT_ROWS) {
+  for (int64_t base = rb; base < re; base += PT1_ROWS) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < PT_PER; ++s)
+    for (int s = 0; s < PT1; ++s)
       if (tg[s] != 0xffffffffu) atomicAdd(&L.cw[w][tg[s] >> pp.lb], 1u);
     __syncthreads();
     const uint32_t staged = part_cursors(L);
 #pragma unroll
-    for (int s = 0; s < PT_PER; ++s) {
+    for (int s = 0; s < PT1; ++s) {
       const bool valid = tg[s] != 0xffffffffu;
       const uint32_t d = valid ? tg[s] >> pp.lb : 0u;
       uint32_t rank, cnt;
@@ -466,7 +473,7 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
         L.tag[slot] = (uint16_t)tg[s];
       }
     }
-    if (base + PT_ROWS < re) load(base + PT_ROWS, tn, rn);   // next sub-tile in flight during the write-out
+    if (base + PT1_ROWS < re) load(base + PT1_ROWS, tn, rn);   // next sub-tile in flight during the write-out
     __syncthreads();
     for (uint32_t q = t; q < staged; q += 256) {
       const uint32_t k = L.tag[q], d = k >> pp.lb;
@@ -478,7 +485,7 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
     __syncthreads();
     L.run[t] += L.tot[t];
 #pragma unroll
-    for (int s = 0; s < PT_PER; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
+    for (int s = 0; s < PT1; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
   }
   if (bad) atomicOr(flags, bad);
 }
@@ -519,37 +526,37 @@ __global__ void __launch_bounds__(256) k_part2(PartPlan pp, const uint32_t* __re
                                                const R* __restrict__ grec, const uint8_t* __restrict__ glk,
                                                R* __restrict__ srec, uint32_t cap, uint32_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  PartLds<R>& L = *(PartLds<R>*)lds_raw;
+  PartLds<R, PT2>& L = *(PartLds<R, PT2>*)lds_raw;
   const uint32_t g = blockIdx.x / pp.nj, jj = blockIdx.x % pp.nj;
   const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
   if (t < (1u << pp.lb)) L.run[t] = o2[(size_t)((g << pp.lb) + t) * pp.nj + jj];
   uint32_t lo, hi;
   part2_range(pp, o1, g, jj, lo, hi);
   auto load = [&](uint32_t base, uint32_t* tg, R* rc) {
-    const uint32_t rows = (hi - base < (uint32_t)PT_ROWS) ? hi - base : (uint32_t)PT_ROWS;
+    const uint32_t rows = (hi - base < (uint32_t)PT2_ROWS) ? hi - base : (uint32_t)PT2_ROWS;
 #pragma unroll
-    for (int s = 0; s < PT_PER; ++s) {
-      const uint32_t i = w * (PT_PER * 64) + s * 64 + lane;
+    for (int s = 0; s < PT2; ++s) {
+      const uint32_t i = w * (PT2 * 64) + s * 64 + lane;
       const uint32_t p = base + (i < rows ? i : rows - 1);   // (clamped: branch-free loads)
       const uint32_t lk = glk[p];
       rc[s] = grec[p];
       tg[s] = i < rows ? lk : 0xffffffffu;
     }
   };
-  uint32_t tg[PT_PER], tn[PT_PER];
-  R rc[PT_PER], rn[PT_PER];
+  uint32_t tg[PT2], tn[PT2];
+  R rc[PT2], rn[PT2];
   if (lo < hi) load(lo, tg, rc);
-  for (uint32_t base = lo; base < hi; base += PT_ROWS) {
+  for (uint32_t base = lo; base < hi; base += PT2_ROWS) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < PT_PER; ++s)
+    for (int s = 0; s < PT2; ++s)
       if (tg[s] != 0xffffffffu) atomicAdd(&L.cw[w][tg[s]], 1u);
     __syncthreads();
     const uint32_t staged = part_cursors(L);
 #pragma unroll
-    for (int s = 0; s < PT_PER; ++s) {
+    for (int s = 0; s < PT2; ++s) {
       const bool valid = tg[s] != 0xffffffffu;
       const uint32_t d = valid ? tg[s] : 0u;
       uint32_t rank, cnt;
@@ -561,7 +568,7 @@ __global__ void __launch_bounds__(256) k_part2(PartPlan pp, const uint32_t* __re
         L.tag[slot] = (uint16_t)d;
       }
     }
-    if (hi - base > (uint32_t)PT_ROWS) load(base + PT_ROWS, tn, rn);   // next sub-tile in flight during the write-out
+    if (hi - base > (uint32_t)PT2_ROWS) load(base + PT2_ROWS, tn, rn);   // next sub-tile in flight during the write-out
     __syncthreads();
     for (uint32_t q = t; q < staged; q += 256) {
       const uint32_t d = L.tag[q];
@@ -572,7 +579,7 @@ __global__ void __launch_bounds__(256) k_part2(PartPlan pp, const uint32_t* __re
     __syncthreads();
     L.run[t] += L.tot[t];
 #pragma unroll
-    for (int s = 0; s < PT_PER; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
+    for (int s = 0; s < PT2; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
   }
 }
 
@@ -607,8 +614,8 @@ static PartPlan part_plan(uint32_t K, int64_t nt) {
   p.nb1 = nbits(p.ng);
   p.nb2 = p.lb;
   // >= ~2048 pass-1 segments when the batch allows (8 workgroups per CU), at most 32 sub-tiles each
-  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(32, nt / ((int64_t)PT_ROWS * 2048)));
-  p.seg1 = (uint32_t)(PT_ROWS * sub);
+  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(32, nt / ((int64_t)PT1_ROWS * 2048)));
+  p.seg1 = (uint32_t)(PT1_ROWS * sub);
   p.ns1 = (uint32_t)std::max<int64_t>(1, (nt + p.seg1 - 1) / p.seg1);
   // pass-2 segments of ~8192 rows of one group
   p.ts2 = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(p.ns1, (int64_t)8192 * p.ng / p.seg1));
@@ -1815,11 +1822,11 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     uint32_t* h1 = (uint32_t*)h->ws.get("part_h1", sizeof(uint32_t) * n1, st);
     uint32_t* o1 = (uint32_t*)h->ws.get("part_o1", sizeof(uint32_t) * n1, st);
     R* srec = (R*)h->ws.get("srec", sizeof(R) * nt, st);
-    const size_t lds = std::max(sizeof(PartLds<R>), sizeof(PartLds<PtRaw<R>>));
-    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     typedef PtRaw<R> RW;
     static_assert(sizeof(RW) == sizeof(R), "raw record layout");
-    HIPCHK(hipFuncSetAttribute((const void*)k_part2<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const size_t lds1 = sizeof(PartLds<R, PT1>), lds2 = sizeof(PartLds<RW, PT2>);
+    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+    HIPCHK(hipFuncSetAttribute((const void*)k_part2<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
     h->kbeg("part_hist");
     HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pp, nt, h1, pk_flags);
@@ -1831,7 +1838,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     h->kend();
     if (!pp.two) {
       h->kbeg("part_scatter");
-      hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds, st, src.pk, kf, pp, nt, o1, srec, (uint8_t*)nullptr,
+      hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds1, st, src.pk, kf, pp, nt, o1, srec, (uint8_t*)nullptr,
                          pk_flags);
       HIPCHK(hipGetLastError());
       h->kend();
@@ -1843,7 +1850,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       uint32_t* h2 = (uint32_t*)h->ws.get("part_h2", sizeof(uint32_t) * n2, st);
       uint32_t* o2 = (uint32_t*)h->ws.get("part_o2", sizeof(uint32_t) * n2, st);
       h->kbeg("part_group");
-      hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds, st, src.pk, kf, pp, nt, o1, grec, glk, pk_flags);
+      hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds1, st, src.pk, kf, pp, nt, o1, grec, glk, pk_flags);
       HIPCHK(hipGetLastError());
       h->kend();
       h->kbeg("part_hist2");
@@ -1856,7 +1863,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       HIPCHK(rocprim::exclusive_scan(tmp, tb, h2, o2, (uint32_t)0, n2, rocprim::plus<uint32_t>(), st));
       h->kend();
       h->kbeg("part_key");
-      hipLaunchKernelGGL((k_part2<RW>), dim3(pp.ng * pp.nj), dim3(256), lds, st, pp, o1, o2, (const RW*)grec, glk, (RW*)srec,
+      hipLaunchKernelGGL((k_part2<RW>), dim3(pp.ng * pp.nj), dim3(256), lds2, st, pp, o1, o2, (const RW*)grec, glk, (RW*)srec,
                          (uint32_t)nt, pk_flags);
       HIPCHK(hipGetLastError());
       h->kend();
