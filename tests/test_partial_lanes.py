@@ -261,6 +261,38 @@ def test_gpu_unpartitioned_and_order_fallback():
                 run_engine(OracleEngine, q, [deep]))
 
 
+def _two_stream_going_back(back):
+    """S and T rows (same attributes) of 20 keys; the second half starts `back` ms before the first half's end."""
+    b = _going_back(None, back=back)
+    rng = np.random.default_rng(21)
+    st = rng.integers(0, 2, b.n).astype(np.int32)
+    cols = []
+    for s in (0, 1):   # one column per (stream, attribute): the other stream's rows read as zeros
+        cols += [np.where(st == s, c, 0).astype(c.dtype) for c in b.cols]
+    return Batch(b.n, 0, b.ts, st, b.key, cols, [None] * len(cols))
+
+
+@pytest.mark.gpu
+def test_gpu_machine_count_state_time_going_back():
+    """A two-stream count pattern (outside the lane routes: the per-key machine, cut into time-horizon units while
+    time moves forward).  A cut runtime lacks the partials parked in the count state since before the unit horizon,
+    which time going back would revive: the push that goes back is SG_EORDER on a default handle, and a handle opened
+    with partial_lanes = -1 (never cut for count states) matches the oracle."""
+    from siddhi_amd._native import GpuEngine, SgError
+    q = ("define stream S (id long, symbol string, v int, w int); define stream T (id long, symbol string, v int, w int); "
+         "partition with (symbol of S, symbol of T) begin @info(name='q') "
+         "from every e1=S[v>50] -> e2=T[v>e1.v]<2:5> -> e3=S[v<e1.v] within 60 milliseconds "
+         "select e1.id as i1, e2[0].id as a, e2[last].id as z, e3.id as i3 insert into M; end;")
+    b = _two_stream_going_back(400)
+    parts = split(b, [10_000, 15_000])
+    with pytest.raises(SgError) as ei:
+        run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, parts)
+    assert ei.value.code == -5
+    want = run_engine(OracleEngine, q, [b])
+    assert len(want) > 0
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=-1), q, parts), want)
+
+
 @pytest.mark.gpu
 def test_gpu_long_history_sort_path():
     """Matches whose insertion history does not fit one 64-bit delivery key (long windows, three insertions) are
