@@ -900,6 +900,23 @@ struct KeyMachine {
       }
     }
   }
+  // A PATTERN row on a stream whose receiver visits only states with empty lists changes nothing: updateState moves
+  // nothing and processAndReturn walks nothing (MultiProcessStreamReceiver.receive :271-309).  Without absence (no
+  // timers on the playback clock) such a row is skipped before its event is even copied -- e.g. the Stream1 rows after
+  // a non-`every` e1 of PatternPartitionTestCase's shape has bound.
+  SG_HD bool lists_empty(int s) {
+    if (list(s, 0)[0] || list(s, 1)[0]) return false;
+    const sg_state_desc& x = st(s);
+    return !(x.kind == SG_K_LOGICAL && x.partner >= 0 && (list(x.partner, 0)[0] || list(x.partner, 1)[0]));
+  }
+  SG_HD bool stream_idle(int stream) {
+    const int ri = d->recv_of_stream[stream];
+    if (ri < 0) return true;
+    const sg_receiver_desc& r = d->receivers[ri];
+    for (int k = 0; k < r.n; ++k)
+      if (!lists_empty(r.stab[k]) || !lists_empty(r.pres[k])) return false;
+    return true;
+  }
   // store one row's retained values in the event pool
   SG_HD int copy_row(const SgRow& row) {
     int e = alloc_ev();
@@ -954,6 +971,7 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t em
   int64_t nrows = rows.n_rows();
   int64_t i = 0;
   const bool can_end = m.can_end();
+  const bool skip_idle = m.d->type == 0 && m.d->n_sched == 0 && A == 0;
   while (!m.failed) {
     if (can_end && m.ended()) break;   // (no timers either: nothing left to fire)
     int64_t lev = (i < nown) ? rows.own_local(i) : nrows;
@@ -988,6 +1006,11 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t em
       if (ltim < lev) continue;
     }
     if (i >= nown) break;
+    if (skip_idle && m.hdr()[K_CREATED] && m.stream_idle(rows.stream_at(lev))) {   // (stream_idle)
+      m.set_pos((int64_t)rows.index_of(lev));
+      ++i;
+      continue;
+    }
     SgRow row;
     rows.fill(lev, row);
     m.now = row.ts;

@@ -112,6 +112,7 @@ struct DevRows {
   }
   __device__ int64_t n_own() { return nown; }
   __device__ int64_t own_local(int64_t i) { return (int64_t)gptr<uint32_t>(rows)[i]; }
+  __device__ int stream_at(int64_t r) { return stream ? gptr<int32_t>(stream)[r] : 0; }
   __device__ int64_t n_rows() { return n; }
   __device__ int64_t ts_at(int64_t r) { return gptr<int64_t>(ts)[r]; }
   __device__ int64_t ts_(int64_t r) { return gptr<int64_t>(ts)[r]; }

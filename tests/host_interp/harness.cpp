@@ -43,6 +43,7 @@ struct HostRows {
   }
   int64_t n_own() { return (int64_t)own->size(); }
   int64_t own_local(int64_t i) { return (*own)[i]; }
+  int stream_at(int64_t r) { return b->stream ? b->stream[r] : 0; }
   int64_t n_rows() { return b->n; }
   int64_t ts(int64_t r) { return b->ts[r]; }
   int64_t find_ge(int64_t from, int64_t v) {
