@@ -172,7 +172,9 @@ typedef struct sg_options {
                                (rocPRIM radix sort above), 1 = always the radix sort (testing both paths) */
   int32_t partial_lanes;    /* general engine, patterns whose partial matches never interact (every e1 -> ... within T
                                over stream / count / logical states of one stream): 0 = one GPU lane per partial
-                               match while timestamps never decrease, -1 = always the per-key machine (testing) */
+                               match while timestamps never decrease, -1 = always the per-key machine (testing);
+                               1 / 2 = lanes, matches ordered by the trigger-row sort plus in-place tie runs / by the
+                               three LSD radix sorts even where one composed key would do (testing every order path) */
   int32_t no_grow;          /* general machine: 1 = a push that runs out of a key's pool / list / timer capacity or of
                                emission space fails with SG_ECAPACITY instead of being rolled back and rerun with 4x the
                                capacity (testing) */

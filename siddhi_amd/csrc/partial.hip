@@ -660,6 +660,36 @@ __global__ void k_pp_key(int64_t n, const uint64_t* __restrict__ k1, const uint6
   key[i] = x;
 }
 
+// After the stable sort by k1, the matches of one (trigger row, visit slot) sit together in start-row order: order each
+// such run by its insertion history (th, then tl) in place -- what the two LSD tie sorts over all T slots would give,
+// for the cost of the runs alone.  A run longer than max_run sets *over and the caller takes the LSD sorts.
+__global__ void k_pp_ties(int64_t m, const uint64_t* __restrict__ key, uint32_t* __restrict__ idx,
+                          const uint64_t* __restrict__ th, const uint64_t* __restrict__ tl, uint64_t tl_mask, int max_run,
+                          int32_t* __restrict__ over) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t k = key[i];
+  if (i > 0 && key[i - 1] == k) return;   // not the head of its run
+  int64_t e = i + 1;
+  while (e < m && key[e] == k) {
+    if (e - i >= max_run) { atomicOr(over, 1); return; }
+    ++e;
+  }
+  for (int64_t a = i + 1; a < e; ++a) {   // stable insertion sort: equal histories keep start-row order
+    const uint32_t v = idx[a];
+    const uint64_t hv = th[v], lv = tl[v] & tl_mask;
+    int64_t b = a;
+    while (b > i) {
+      const uint32_t u = idx[b - 1];
+      const uint64_t hu = th[u], lu = tl[u] & tl_mask;
+      if (hu < hv || (hu == hv && lu <= lv)) break;
+      idx[b] = u;
+      --b;
+    }
+    idx[b] = v;
+  }
+}
+
 __global__ void k_pp_iota(int64_t n, uint32_t* __restrict__ x) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = (uint32_t)i;
@@ -1558,19 +1588,37 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     int ob = 1;
     while ((1ull << ob) <= (uint64_t)hmaxoff) ++ob;
     const int need = rb + 4 + ps->rule.n_hist * (ob + 4);
-    if (need <= 63) {   // one radix sort over a single composed key
+    const int order_path = h->opt.partial_lanes;   // 1 / 2: tie runs / LSD sorts even where one key fits (testing)
+    if (need <= 63 && order_path == 0) {   // one radix sort over a single composed key
       const uint64_t none = (1ull << need) - 1;
       hipLaunchKernelGGL(k_pp_key, g2, blk, 0, st, T, o.k1, o.th, o.tl, o.jp, o.k1_none, ps->rule.n_hist, hmaxoff, ob,
                          none, ka, ia);
       sort_pairs64(h, "one", ka, kb2, ia, ib, T, need);
       std::swap(ia, ib);
     } else {
-    hipLaunchKernelGGL(k_pp_iota, g2, blk, 0, st, T, ia);
     int tb = 1;
     while ((1ll << tb) < m) ++tb;
     const int comp_bits = tb + 4;   // one history component: combined row << 4 | visit slot
+    const int eb = std::min(64, 31 + comp_bits);
+    // k1 first, then the tie runs in place (k_pp_ties); the three LSD sorts only when a run is too long
+    int32_t hover = 1;
+    if (order_path != 2) {
+      int32_t* over = (int32_t*)h->ws.get("pp_over", 4, st);
+      HIPCHK(hipMemsetAsync(over, 0, 4, st));
+      hipLaunchKernelGGL(k_pp_iota, g2, blk, 0, st, T, ia);
+      sort_pairs64(h, "k1", o.k1, kb2, ia, ib, T, k1_bits);
+      const uint64_t tl_mask = ps->rule.n_hist <= 2 ? 0ull : (eb >= 64 ? ~0ull : (1ull << eb) - 1);
+      hipLaunchKernelGGL(k_pp_ties, dim3((unsigned)((total + 255) / 256)), blk, 0, st, (int64_t)total, kb2, ib, o.th,
+                         o.tl, tl_mask, 256, over);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(&hover, over, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    if (!hover) {
+      std::swap(ia, ib);
+    } else {
+    hipLaunchKernelGGL(k_pp_iota, g2, blk, 0, st, T, ia);
     if (ps->rule.n_hist > 2) {
-      const int eb = std::min(64, 31 + comp_bits);
       hipLaunchKernelGGL(k_pp_take, g2, blk, 0, st, T, o.tl, ia, ka);
       sort_pairs64(h, "lo", ka, kb2, ia, ib, T, eb);
       std::swap(ia, ib);
@@ -1581,6 +1629,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     hipLaunchKernelGGL(k_pp_take, g2, blk, 0, st, T, o.k1, ia, ka);
     sort_pairs64(h, "k1", ka, kb2, ia, ib, T, k1_bits);
     std::swap(ia, ib);
+    }
     }
     const int64_t M = (int64_t)total;
     char* out = h->out.reserve(M, nsel, st);

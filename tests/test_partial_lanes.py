@@ -238,6 +238,20 @@ def test_gpu_shapes(name, vmax):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("name", sorted(SHAPES))
+def test_gpu_shapes_every_order_path(name, order):
+    """Delivery order by the trigger-row sort plus in-place tie runs (1) and by the three LSD sorts (2), forced where
+    one composed key would fit: both give the oracle's order."""
+    from siddhi_amd._native import GpuEngine
+    q = HEAD + SHAPES[name]
+    b = small_batch(20_000, 40, 10, 4, seed=sum(name.encode()) + 7)
+    want = run_engine(OracleEngine, q, [b])
+    got = run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=order), q, split(b, [6_000, 6_001]))
+    assert_same(got, want)
+
+
+@pytest.mark.gpu
 def test_gpu_unpartitioned_and_order_fallback():
     from siddhi_amd._native import GpuEngine, SgError
     q = HEAD + UNPART
@@ -294,14 +308,19 @@ def test_gpu_machine_count_state_time_going_back():
 
 
 @pytest.mark.gpu
-def test_gpu_long_history_sort_path():
+@pytest.mark.parametrize("keys", [1, 200])
+def test_gpu_long_history_sort_path(keys):
     """Matches whose insertion history does not fit one 64-bit delivery key (long windows, three insertions) are
-    ordered by the multi-pass stable sort instead."""
+    ordered by the trigger-row sort and in-place tie runs; one key makes runs of more than 256 matches, which take
+    the three LSD sorts instead."""
     from siddhi_amd._native import GpuEngine
     q = HEAD + ("@info(name='q') from every e1=S[v>80] -> e2=S[v>e1.v] -> e3=S[w>e1.w] -> e4=S[v<e1.v] within 1 hour "
                 "select e1.id as i1, e2.id as i2, e3.id as i3, e4.id as i4 insert into M;")
-    b = small_batch(40_000, 1, 100, 4, seed=5)
-    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, [b]), run_engine(OracleEngine, q, [b]))
+    b = small_batch(40_000, keys, 100, 4, seed=5)
+    want = run_engine(OracleEngine, q, [b])
+    assert len(want) > 0
+    for order in (0, 1, 2):
+        assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=order), q, [b]), want)
 
 
 @pytest.mark.gpu
@@ -313,7 +332,8 @@ def test_gpu_c3c_slice_both_routes():
               [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
     want = run_engine(OracleEngine, q, [b])
     assert_same(run_engine(GpuEngine, q, split(b, [50_000, 123_457])), want)
-    assert_same(run_engine(lambda ctx: GpuEngine(ctx, partial_lanes=-1), q, [b]), want)
+    for order in (-1, 1, 2):
+        assert_same(run_engine(lambda ctx: GpuEngine(ctx, partial_lanes=order), q, [b]), want)
 
 
 @pytest.mark.gpu
