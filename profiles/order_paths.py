@@ -12,13 +12,23 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-from parity_util import context   # noqa: E402
+from parity_util import context, dense_first_seen   # noqa: E402
+from siddhi_amd import synth   # noqa: E402
 from siddhi_amd._native import GpuEngine   # noqa: E402
-from test_partial_lanes import small_batch   # noqa: E402
+from siddhi_amd.runtime import Batch   # noqa: E402
 
 Q = ("define stream S (id long, symbol string, v int, w int); partition with (symbol of S) begin @info(name='q') "
      "from every e1=S[v>80] -> e2=S[v>e1.v] -> e3=S[w>e1.w] -> e4=S[v<e1.v] within 1 hour "
      "select e1.id as i1, e2.id as i2, e3.id as i3, e4.id as i4 insert into M; end;")
+
+
+def small_batch(n, keys, vmax, rate, seed):   # the shape of tests/test_partial_lanes.py's batches
+    rng = np.random.default_rng(seed)
+    ts = (synth.T0 + np.arange(n) // rate).astype(np.int64)
+    key = dense_first_seen(rng.integers(0, keys, n).astype(np.int64)).astype(np.int32)
+    v = rng.integers(0, vmax, n).astype(np.int32)
+    w = rng.integers(0, vmax, n).astype(np.int32)
+    return Batch(n, 0, ts, np.zeros(n, np.int32), key, [np.arange(n, dtype=np.int64), key, v, w], [None] * 4)
 
 
 def main(n=int(os.environ.get("ORDER_ROWS", 20_000_000)), keys=4000, reps=3):
