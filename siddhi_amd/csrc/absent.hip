@@ -247,6 +247,41 @@ __global__ void k_abs_kill(AbsArgs a, const K* __restrict__ skeys, const uint32_
   }
 }
 
+// 4a'. kill, fast shape (every batch row kills, every sorted row is a candidate; non-sorted rows carry the sentinel
+//      key): the first killer after p is almost always p + 1, so its key, row and timestamp come from the next lane
+//      instead of a second random read of the row arrays; only a carried neighbour (not a killer) makes the lane search
+template <class K>
+__global__ void __launch_bounds__(256) k_abs_kill_fast(AbsArgs a, const K* __restrict__ skeys,
+                                                       const uint32_t* __restrict__ sid, K sentinel,
+                                                       const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
+                                                       uint8_t* __restrict__ dead) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x; p0 < a.nt; p0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = p0 + threadIdx.x;
+    const bool in = p < a.nt;
+    const uint32_t v = in ? sid[p] : 0u;
+    const K kp = in ? skeys[p] : sentinel;
+    const bool live = kp != sentinel;
+    const int64_t tv = live ? vts(a, ts, c_dl, v) : 0;
+    const int64_t t1 = __shfl_down(tv, 1, 64);
+    const uint32_t v1 = __shfl_down(v, 1, 64);
+    const K k1 = __shfl_down(kp, 1, 64);
+    if (!live) continue;
+    int64_t tq = 0;
+    bool found = false;
+    int64_t x = p + 1;
+    if (lane < 63 && x < a.nt) {
+      if (k1 != kp) continue;   // no later row with this value
+      if (v1 >= (uint32_t)a.nc) { tq = t1; found = true; }
+      else ++x;                 // a carried row: search on
+    }
+    if (!found)
+      for (; x < a.nt && skeys[x] == kp; ++x)
+        if (sid[x] >= (uint32_t)a.nc) { tq = ts[sid[x] - a.nc]; found = true; break; }
+    if (found && tq < tv + a.W) dead[v] = 1;
+  }
+}
+
 // 4b. per candidate: trigger row (first row with ts >= deadline) or pending; packed counts for the scan
 __global__ void k_abs_decide(AbsArgs a, const uint8_t* __restrict__ role, const uint8_t* __restrict__ dead,
                              const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
@@ -386,7 +421,10 @@ void sort_and_kill(SgHandle* h, const AbsArgs& a, uint64_t omin, int bits, const
     tmp = h->ws.get("abs_scan_tmp", tb, st);
     HIPCHK(rocprim::inclusive_scan(tmp, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
   }
-  hipLaunchKernelGGL((k_abs_kill<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, role, nks, ts, c_dl, dead);
+  if (a.fast && bits < 64)   // below 64 bits the sentinel lies above every value key
+    hipLaunchKernelGGL((k_abs_kill_fast<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, sentinel, ts, c_dl, dead);
+  else
+    hipLaunchKernelGGL((k_abs_kill<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, role, nks, ts, c_dl, dead);
   HIPCHK(hipGetLastError());
 }
 
