@@ -282,45 +282,24 @@ __global__ void __launch_bounds__(256) k_abs_kill_fast(AbsArgs a, const K* __res
   }
 }
 
-// 4b. per candidate: trigger row (first row with ts >= deadline) or pending; packed counts for the scan.
-//     Timestamps are non-decreasing here (checked before this pass), so in a block of batch rows the deadlines are
-//     too: two lanes find the triggers of the block's first and last deadlines over the whole push, and every lane
-//     then searches only between them (the full-range search stays for blocks holding carried partials).
-__device__ __forceinline__ int64_t ts_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, int64_t d) {
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (ts[mid] < d) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-__global__ void __launch_bounds__(256) k_abs_decide(AbsArgs a, const uint8_t* __restrict__ role,
-                                                    const uint8_t* __restrict__ dead, const int64_t* __restrict__ ts,
-                                                    const int64_t* __restrict__ c_dl, uint32_t* __restrict__ trig,
-                                                    uint64_t* __restrict__ cnt) {
-  __shared__ int64_t span[2];
-  for (int64_t v0 = (int64_t)blockIdx.x * blockDim.x; v0 < a.nt; v0 += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t v = v0 + threadIdx.x;
-    const bool narrow = v0 >= a.nc;   // batch rows only
-    if (narrow && threadIdx.x < 2) {
-      const int64_t vl = (v0 + blockDim.x < a.nt ? v0 + blockDim.x : a.nt) - 1;
-      const int64_t d = ts[(threadIdx.x ? vl : v0) - a.nc] + a.W;
-      span[threadIdx.x] = ts_lower_bound(ts, v0 - a.nc + 1, a.n, d);   // W > 0: the trigger follows the row
-    }
-    __syncthreads();
-    if (v < a.nt) {
-      uint64_t c = 0;
-      uint32_t t = NONE;
-      if ((role[v] & R_CAND) && !dead[v]) {
-        const int64_t d = vts(a, ts, c_dl, (uint32_t)v) + a.W;
-        const int64_t lo = narrow ? ts_lower_bound(ts, span[0], span[1], d)
-                                  : ts_lower_bound(ts, v < a.nc ? 0 : v - a.nc + 1, a.n, d);
-        if (lo < a.n) { t = (uint32_t)lo; c = 1; } else { c = 1ull << 32; }
+// 4b. per candidate: trigger row (first row with ts >= deadline) or pending; packed counts for the scan
+__global__ void k_abs_decide(AbsArgs a, const uint8_t* __restrict__ role, const uint8_t* __restrict__ dead,
+                             const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
+                             uint32_t* __restrict__ trig, uint64_t* __restrict__ cnt) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.nt; v += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t c = 0;
+    uint32_t t = NONE;
+    if ((role[v] & R_CAND) && !dead[v]) {
+      const int64_t d = vts(a, ts, c_dl, (uint32_t)v) + a.W;
+      int64_t lo = v < a.nc ? 0 : v - a.nc + 1, hi = a.n;   // W > 0: the trigger follows the row
+      while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (ts[mid] < d) lo = mid + 1; else hi = mid;
       }
-      trig[v] = t;
-      cnt[v] = c;
+      if (lo < a.n) { t = (uint32_t)lo; c = 1; } else { c = 1ull << 32; }
     }
-    __syncthreads();   // span is rewritten by the next block of rows
+    trig[v] = t;
+    cnt[v] = c;
   }
 }
 
