@@ -45,7 +45,9 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 2
+/* Checked on every sg_nfa_desc and written into every snapshot.  3: sg_options.no_grow; the general route's
+   snapshots carry SgGeo with off_scratch (version-2 snapshots and bindings are refused). */
+#define SG_ABI_VERSION 3
 
 #define SG_MAX_STATES 16
 #define SG_MAX_STREAMS 16

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SIDDHI_GPU_LIB") or os.path.join(HERE, "libsiddhi_gpu.so")   # override: experiments
 
 SG_MAX_STATES, SG_MAX_STREAMS, SG_MAX_SELECT, SG_MAX_RET, SG_MAX_COLS, SG_MAX_CODE = 16, 16, 32, 16, 64, 512
-SG_ABI_VERSION = 2
+SG_ABI_VERSION = 3
 
 SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
            "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version",
@@ -123,6 +123,24 @@ class SgError(RuntimeError):
         self.code = code
 
 
+def _one_hip_runtime():
+    """Make the process's HIP runtime the one torch brings, before libsiddhi_gpu.so is loaded.
+
+    torch's wheel ships its own libamdhip64 / libhsa-runtime64 (same sonames as /opt/rocm's).  Loaded first, torch's
+    copies satisfy libsiddhi_gpu.so's dependencies by soname and the process has one HIP runtime.  Loaded the other
+    way round (this library first, torch later) the dynamic linker maps BOTH runtimes and both HSA runtimes into the
+    process, each opening the GPU on its own: after hundreds of engine handles had been opened and closed on the first
+    one, torch's later initialisation found "No HIP GPUs are available" (r03 GPU suite).  A host without torch (the
+    JNI binding) has one runtime anyway."""
+    import sys
+    if "torch" in sys.modules:
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_library(path: str = LIB_PATH):
     """Load libsiddhi_gpu.so; raises if it is not built (no silent fallback)."""
     global _lib
@@ -130,6 +148,7 @@ def load_library(path: str = LIB_PATH):
         if not os.path.exists(path):
             raise RuntimeError(f"libsiddhi_gpu.so not built at {path}: run `make -C siddhi_amd/csrc` "
                                "or __graft_entry__.build()")
+        _one_hip_runtime()
         lib = ct.CDLL(path)
         P = ct.c_void_p
         lib.sg_open.argtypes = [ct.c_int, P, P, ct.POINTER(P)]

@@ -255,6 +255,9 @@ __global__ void __launch_bounds__(256) k_abs_kill_fast(AbsArgs a, const K* __res
                                                        const uint32_t* __restrict__ sid, K sentinel,
                                                        const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
                                                        uint8_t* __restrict__ dead) {
+#if defined(__AMDGCN_WAVEFRONT_SIZE)
+  static_assert(__AMDGCN_WAVEFRONT_SIZE == 64, "k_abs_kill_fast reads lane + 1 by a 64-wide shuffle (CDNA wave64)");
+#endif
   const int lane = threadIdx.x & 63;
   for (int64_t p0 = (int64_t)blockIdx.x * blockDim.x; p0 < a.nt; p0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = p0 + threadIdx.x;

@@ -355,7 +355,7 @@ void sg_egress_init(SgHandle& h) {
 
 // Staging slot `slot` holds at least `bytes` (grown only after its last copy has read it: hipFree synchronises the
 // device, so sg_push_deliver sizes both slots before its chunk pipeline starts).
-static void stage_reserve(SgHandle& h, int slot, int64_t bytes) {
+void sg_stage_reserve(SgHandle& h, int slot, int64_t bytes) {
   if (h.eg.cap[slot] >= bytes) return;
   HIPCHK(hipEventSynchronize(h.eg.done[slot]));
   if (h.eg.stage[slot]) HIPCHK(hipFree(h.eg.stage[slot]));
@@ -374,7 +374,7 @@ static int64_t deliver_pending(SgHandle& h, const sg_match_columns* out, int64_t
   sg_egress_init(h);
   const sg_nfa_desc& d = h.desc;
   const ColLayout L = sg_col_layout(d, k);
-  stage_reserve(h, slot, (int64_t)L.bytes);
+  sg_stage_reserve(h, slot, (int64_t)L.bytes);
   char* st = h.eg.stage[slot];
   HIPCHK(hipStreamWaitEvent(h.stream, h.eg.done[slot], 0));   // slot free again
   hipLaunchKernelGGL(k_to_columns, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, h.stream, k, (const char*)o.rec,
@@ -656,8 +656,8 @@ int sg_push_deliver(sg_handle* hh, const sg_batch* b, const sg_match_columns* ou
       const int64_t expect = std::min<int64_t>(cap, std::max<int64_t>(h.out.n, b->n));
       if (expect > 0) {
         const int64_t bytes = (int64_t)sg_col_layout(h.desc, expect).bytes;
-        stage_reserve(h, 0, bytes);
-        stage_reserve(h, 1, bytes);
+        sg_stage_reserve(h, 0, bytes);
+        sg_stage_reserve(h, 1, bytes);
       }
     }
     try {

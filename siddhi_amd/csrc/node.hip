@@ -87,33 +87,44 @@ struct Pool {
     cv.notify_all();
     for (auto& t : th) t.join();
   }
+  // Completion state of one parallel_for, shared by the submitter and every queued closure: the worker that finishes
+  // the last task decrements and notifies under the mutex, and the closures own the state, so the submitter may
+  // return (and its stack frame die) the moment it observes left == 0.
+  struct Join {
+    std::mutex m;
+    std::condition_variable cv;
+    int left = 0;
+    std::exception_ptr err;
+  };
   template <class F>
   void parallel_for(int n, F&& fn) {
     if (n <= 0) return;
-    std::atomic<int> left(n);
-    std::mutex dm;
-    std::condition_variable dcv;
-    std::exception_ptr err;
-    auto task = [&](int i) {
+    auto js = std::make_shared<Join>();
+    js->left = n;
+    // `fn` is only touched before this task's decrement, while the submitter is still waiting for it
+    auto run = [js, &fn](int i) {
+      std::exception_ptr e;
       try {
         fn(i);
       } catch (...) {
-        std::lock_guard<std::mutex> lk(dm);
-        if (!err) err = std::current_exception();
+        e = std::current_exception();
       }
-      if (left.fetch_sub(1) == 1) {
-        std::lock_guard<std::mutex> lk(dm);
-        dcv.notify_all();
-      }
+      std::lock_guard<std::mutex> lk(js->m);
+      if (e && !js->err) js->err = e;
+      if (--js->left == 0) js->cv.notify_all();
     };
     {
       std::lock_guard<std::mutex> lk(mu);
-      for (int i = n - 1; i >= 1; --i) q.push_back([&task, i] { task(i); });
+      for (int i = n - 1; i >= 1; --i) q.push_back([run, i] { run(i); });
     }
     cv.notify_all();
-    task(0);
+    run(0);
     // help with queued work while waiting (a submitter never idles behind its own tasks)
-    while (left.load() > 0) {
+    while (true) {
+      {
+        std::lock_guard<std::mutex> lk(js->m);
+        if (js->left == 0) break;
+      }
       std::function<void()> f;
       {
         std::lock_guard<std::mutex> lk(mu);
@@ -126,10 +137,10 @@ struct Pool {
         f();
         continue;
       }
-      std::unique_lock<std::mutex> lk(dm);
-      dcv.wait_for(lk, std::chrono::milliseconds(1), [&] { return left.load() == 0; });
+      std::unique_lock<std::mutex> lk(js->m);
+      js->cv.wait_for(lk, std::chrono::milliseconds(1), [&] { return js->left == 0; });
     }
-    if (err) std::rethrow_exception(err);
+    if (js->err) std::rethrow_exception(js->err);
   }
 };
 
@@ -767,14 +778,9 @@ void deliver(Run& r, SgHandle& h, const Dst& dst, int64_t pos, int64_t k, int es
   const Want& w = r.w;
   sg_egress_init(h);
   const ColLayout L = sg_col_layout(d, k);
-  if (h.eg.cap[es] < (int64_t)L.bytes) {
-    HIPCHK(hipEventSynchronize(h.eg.done[es]));
-    if (h.eg.stage[es]) HIPCHK(hipFree(h.eg.stage[es]));
-    h.eg.stage[es] = nullptr;
-    const size_t want = L.bytes + L.bytes / 2;
-    HIPCHK(hipMalloc(&h.eg.stage[es], want));
-    h.eg.cap[es] = (int64_t)want;
-  }
+  // (reserve_all sized both slots for a chunk's worth of matches; a larger chunk output grows the slot here, which
+  // synchronises the device once)
+  sg_stage_reserve(h, es, (int64_t)L.bytes);
   char* st = h.eg.stage[es];
   HIPCHK(hipStreamWaitEvent(h.stream, h.eg.done[es], 0));
   sg_launch_to_columns(k, h.out.rec, h.out.stride, L, st, h.stream);
@@ -1141,6 +1147,11 @@ void reserve_all(Run& r) {
       }
     HIPCHK(hipStreamSynchronize(h.stream));
     sg_egress_init(h);
+    // egress slots for one chunk's matches (the closed forms emit at most one match per e1 row, the lane routes rarely
+    // more): no hipFree / hipMalloc -- a device-wide synchronisation -- inside the pipeline for such chunks
+    const int64_t eb = (int64_t)sg_col_layout(h.desc, std::max<int64_t>(1, std::min<int64_t>(C, r.cap))).bytes;
+    sg_stage_reserve(h, 0, eb);
+    sg_stage_reserve(h, 1, eb);
   }
   if (nd.ddict == 1) nd.draw_rows = std::max(nd.draw_rows, C);
   if (nd.tag_col >= 0) nd.tagbuf.ensure((size_t)std::max<int64_t>(r.cap, 1) * 4);

@@ -208,6 +208,8 @@ BatchView sg_upload_to(const sg_nfa_desc& d, const SlotPtrs& p, const sg_batch* 
                        hipStream_t st);
 void sg_push_view(SgHandle& h, BatchView& bv, int64_t n);   // one push of rows in HBM (engine route + select)
 ColLayout sg_col_layout(const sg_nfa_desc& d, int64_t cap);
+// egress staging slot `slot` of h holds at least `bytes` (grows after the slot's last copy has read it; api.hip)
+void sg_stage_reserve(SgHandle& h, int slot, int64_t bytes);
 void sg_launch_to_columns(int64_t n, const char* rec, int stride, const ColLayout& L, char* stage, hipStream_t st);
 void sg_egress_init(SgHandle& h);
 
