@@ -83,6 +83,7 @@ extern "C" {
 #define SG_SHAPE_GENERAL 0
 #define SG_SHAPE_EVERY_NEXT_CMP 1    /* every A[l] -> B[l' and B.x OP A.x] within T */
 #define SG_SHAPE_EVERY_ABSENT_EQ 2   /* every A[l] -> not B[l' and B.x == A.x] for T  (playback) */
+#define SG_SHAPE_NEXT_CMP_ONCE 3     /* A[l] -> B[l' and B.x OP A.x] (within T), no `every`: one match per key */
 
 /* postfix predicate program opcodes; words are int64 */
 #define SG_OP_VAR 1     /* VAR state index_in_chain retained_slot type */

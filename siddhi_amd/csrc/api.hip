@@ -181,6 +181,9 @@ void sg_push_view(SgHandle& h, BatchView& bv, int64_t n) {
       case SG_SHAPE_EVERY_ABSENT_EQ:
         sg_run_every_absent(&h, bv, n);
         break;
+      case SG_SHAPE_NEXT_CMP_ONCE:
+        sg_run_once(&h, bv, n);
+        break;
       default:
         sg_run_general(&h, bv, n);
     }
@@ -707,6 +710,7 @@ int sg_reset(sg_handle* hh) {
     sg_every_next_reset(&h);
     sg_every_absent_reset(&h);
     sg_general_reset(&h);
+    sg_once_reset(&h);
   });
 }
 
@@ -762,6 +766,7 @@ int sg_close(sg_handle* hh) {
   sg_every_next_release(&h);
   sg_every_absent_release(&h);
   sg_general_release(&h);
+  sg_once_release(&h);
   h.ws.release();
   h.out.release();
   h.stage.release();
@@ -849,6 +854,7 @@ int sg_snapshot(sg_handle* hh, void* buf, size_t cap, size_t* size) {
       case 1: sg_every_next_snapshot(&h, w); break;
       case 2: sg_general_snapshot(&h, w); break;
       case 3: sg_every_absent_snapshot(&h, w); break;
+      case 4: sg_once_snapshot(&h, w); break;
       default: break;
     }
     *size = w.b.size();
@@ -877,16 +883,18 @@ int sg_restore(sg_handle* hh, const void* buf, size_t size) {
     if (r.pod<uint64_t>() != query_fingerprint(h)) throw SgError(SG_EINVAL, "snapshot was taken for another query");
     const int64_t pushes = r.pod<int64_t>();
     const uint32_t kb = r.pod<uint32_t>();
-    if (kind < 0 || kind > 3 || (h.state_kind && kind && h.state_kind != kind))
+    if (kind < 0 || kind > 4 || (h.state_kind && kind && h.state_kind != kind))
       throw SgError(SG_EINVAL, "snapshot engine kind does not match the handle");
     h.out.n = 0;
     sg_every_next_reset(&h);
     sg_every_absent_reset(&h);
     sg_general_reset(&h);
+    sg_once_reset(&h);
     switch (kind) {
       case 1: sg_every_next_restore(&h, r); break;
       case 2: sg_general_restore(&h, r); break;
       case 3: sg_every_absent_restore(&h, r); break;
+      case 4: sg_once_restore(&h, r); break;
       default: break;
     }
     if (r.p != r.e) throw SgError(SG_EINVAL, "trailing bytes in snapshot");

@@ -60,12 +60,16 @@ struct PartialState {
   SgSeqRule srule;
   SgSeqRule* dsrule = nullptr;
   void* kst = nullptr;          // sequence lanes: per-key machine state SeqStateT<G> (zero = no runtime yet)
+  void* kst_out = nullptr;      // the push's end states (swapped into kst when the push succeeds: a push that runs
+                                // out of match space is rerun from kst with more space, StreamPreStateProcessor's
+                                // lists being unbounded, C/query/input/stream/state/StreamPreStateProcessor.java:57-58)
   int sq_small = 0;             // the query fits seq.h's small state geometry (SqSmall)
   int pp_small = 0;             // the query fits chain.h's small lane geometry (PpSmall)
   size_t sq_bytes = sizeof(SeqState);
   int64_t kst_keys = 0;
   int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
   int64_t last_reruns = 0;      // sequence units rerun from their predecessor's end state in the last push
+  int64_t sq_cap_hint = 0;      // match space the last push that outgrew its default needed
   int nulls_seen = 0;           // a push had null flags in a column the query reads (carried rows may hold nulls)
   int8_t hot[SG_MAX_RET];       // record sort: slot -> word of the 16-B record (-1: gathered), see rec_plan
   int rec_ok = 0;
@@ -168,6 +172,7 @@ void sg_partial_free(PartialState* ps) {
   if (ps->drule) hipFree(ps->drule);
   if (ps->dsrule) hipFree(ps->dsrule);
   if (ps->kst) hipFree(ps->kst);
+  if (ps->kst_out) hipFree(ps->kst_out);
   delete ps;
 }
 
@@ -840,7 +845,8 @@ struct SqPlan {
   const uint32_t* umap;       // unit -> key
   int64_t R, W;
   int64_t nunits;
-  void* kst;                  // per key (carried), SeqStateT<G>
+  void* kst;                  // per key (carried), SeqStateT<G>: the states the push starts from (read only)
+  void* kst_out;              // per key: the states the push ends in
   void* ust;                  // per unit: start state
   void* uen;                  // per unit: end state
   unsigned long long* reruns;
@@ -1001,7 +1007,10 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= kb) return;
   const uint32_t u0 = pl_.uoff[k], u1 = pl_.uoff[k + 1];
-  if (u1 == u0) return;
+  if (u1 == u0) {   // no rows this push: the key's state carries over unchanged
+    sq_copy((SeqStateT<G>*)pl_.kst_out + k, (const SeqStateT<G>*)pl_.kst + k);
+    return;
+  }
   const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
   SeqStateT<G>& M = lanes[threadIdx.x];
   SeqMachine<SeqSrcD, G> m;
@@ -1039,7 +1048,7 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const
   sq_copy(&M, (const SeqStateT<G>*)pl_.uen + (u1 - 1));
   const int64_t nk = e0 - b0;
   m.rebase(nk - 1, nk > rl.horizon ? nk - rl.horizon : 0);
-  sq_copy((SeqStateT<G>*)pl_.kst + k, &M);
+  sq_copy((SeqStateT<G>*)pl_.kst_out + k, &M);
 }
 
 // void the speculative matches of rerun units
@@ -1149,17 +1158,24 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   const int64_t m = a.nc + a.n;
   const dim3 blk(256), grd((unsigned)((m + 255) / 256));
   // per-key machine states (grown with the key bound; new keys start zeroed = no runtime yet)
-  if ((int64_t)kb > ps->kst_keys) {
+  if ((int64_t)kb > ps->kst_keys || !ps->kst_out) {
     const int64_t nk = std::max<int64_t>((int64_t)kb, ps->kst_keys * 3 / 2);
     void* ns = nullptr;
-    if (hipMalloc(&ns, ps->sq_bytes * (size_t)nk) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
+    void* no = nullptr;
+    if (hipMalloc(&ns, ps->sq_bytes * (size_t)nk) != hipSuccess || hipMalloc(&no, ps->sq_bytes * (size_t)nk) != hipSuccess) {
+      if (ns) hipFree(ns);
+      throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
+    }
     HIPCHK(hipMemsetAsync(ns, 0, ps->sq_bytes * (size_t)nk, st));
+    HIPCHK(hipMemsetAsync(no, 0, ps->sq_bytes * (size_t)nk, st));
     if (ps->kst) {
       HIPCHK(hipMemcpyAsync(ns, ps->kst, ps->sq_bytes * (size_t)ps->kst_keys, hipMemcpyDeviceToDevice, st));
       HIPCHK(hipStreamSynchronize(st));
       hipFree(ps->kst);
     }
+    if (ps->kst_out) hipFree(ps->kst_out);
     ps->kst = ns;
+    ps->kst_out = no;
     ps->kst_keys = nk;
   }
   const int nsel = d.n_select;
@@ -1206,19 +1222,31 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   pl_.umap = umap;
   pl_.nunits = U;
   pl_.kst = ps->kst;
+  pl_.kst_out = ps->kst_out;
   pl_.ust = h->ws.get("sq_ust", ps->sq_bytes * ((size_t)U + 1), st);
   pl_.uen = h->ws.get("sq_uen", ps->sq_bytes * ((size_t)U + 1), st);
   pl_.reruns = o.reserved + 3;
   h->kend();
+  // match space: every lane reserves SQ_CHUNK slots at a time; a push whose matches outgrow it is rerun from the
+  // unchanged start states (kst) with four times the space -- the reference's lists are unbounded
   cap = n + (int64_t)SQ_CHUNK * ((int64_t)U + (int64_t)kb) + 65536;
+  if (ps->sq_cap_hint > cap) cap = ps->sq_cap_hint;
+  if (const char* e = getenv("SG_SQ_MATCH_CAP")) {   // (tests start from a tiny match space to exercise the regrowth)
+    const int64_t v = atoll(e);
+    if (v > 0) cap = std::max<int64_t>(v, SQ_CHUNK);
+  }
+  const dim3 gu((unsigned)((U + SQ_BLOCK - 1) / SQ_BLOCK)), gq((unsigned)((kb + SQ_BLOCK - 1) / SQ_BLOCK));
+  unsigned long long cnt[5] = {0, 0, 0, 0, 0};
+  int32_t fail = 0;
+  for (int attempt = 0;; ++attempt) {
   o.cap = cap;
   o.rec = (char*)h->ws.get("sq_rec", (size_t)cap * rstride, st);
   o.k1 = (uint64_t*)h->ws.get("sq_k1", 8 * cap, st);
-  const dim3 gu((unsigned)((U + SQ_BLOCK - 1) / SQ_BLOCK)), gq((unsigned)((kb + SQ_BLOCK - 1) / SQ_BLOCK));
   o.runit = (uint32_t*)h->ws.get("sq_runit", 4 * (size_t)cap, st);
   o.rerun = (uint32_t*)h->ws.get("sq_rerun", 4 * ((size_t)U + 1), st);
   o.dropped = o.reserved + 4;
   HIPCHK(hipMemsetAsync(o.rerun, 0, 4 * ((size_t)U + 1), st));
+  if (attempt) HIPCHK(hipMemsetAsync(o.reserved, 0, 64, st));
   h->kbeg("sequence_lanes");
   if (U && ps->sq_small) hipLaunchKernelGGL(k_sq_spec<SqSmall>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
   else if (U) hipLaunchKernelGGL(k_sq_spec<SqBig>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
@@ -1229,9 +1257,19 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   else if (U) hipLaunchKernelGGL(k_sq_fix<SqBig>, gq, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, (int64_t)kb, o);
   HIPCHK(hipGetLastError());
   h->kend();
-  unsigned long long cnt[5] = {0, 0, 0, 0, 0};
+  // keys past this push's key bound keep their states as well
+  if (ps->kst_keys > (int64_t)kb)
+    HIPCHK(hipMemcpyAsync((char*)ps->kst_out + ps->sq_bytes * (size_t)kb, (const char*)ps->kst + ps->sq_bytes * (size_t)kb,
+                          ps->sq_bytes * (size_t)(ps->kst_keys - (int64_t)kb), hipMemcpyDeviceToDevice, st));
   HIPCHK(hipMemcpyAsync(cnt, o.reserved, 40, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  fail = (int32_t)(cnt[2] & 0xffffffffu);
+  if (fail != 5) break;
+  const int64_t grown = std::max<int64_t>(4 * cap, (int64_t)std::min<unsigned long long>(cnt[0], (1ull << 40)) + cap);
+  if (getenv("SG_DEBUG_SEQ")) fprintf(stderr, "sequence lanes: match space %lld -> %lld\n", (long long)cap, (long long)grown);
+  cap = grown;
+  ps->sq_cap_hint = cap;
+  }
   if (cnt[3]) {   // some units were rerun: void their speculative matches
     const int64_t Rz = std::min<int64_t>((int64_t)cnt[0], cap);
     hipLaunchKernelGGL(k_sq_drop, dim3((unsigned)((Rz + 255) / 256)), blk, 0, st, Rz, o);
@@ -1241,7 +1279,6 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   h->mark(3);
   cnt[1] -= cnt[4];
   ps->last_reruns = (int64_t)cnt[3];
-  const int32_t fail = (int32_t)(cnt[2] & 0xffffffffu);
   if (fail) {
     if (getenv("SG_DEBUG_SEQ")) fprintf(stderr, "sequence lanes failed: reason %d\n", fail);
     if (ps->seq_pushes == 0 && a.nc == 0) {   // nothing carried yet: the per-key machine can take the stream exactly
@@ -1249,8 +1286,9 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
       return 0;
     }
     throw SgError(SG_ECAPACITY, "sequence machine capacity exceeded (reason " + std::to_string(fail) +
-                                    ": 1 partials, 2 list, 3 returned, 4 chain, 5 match buffer)");
+                                    ": 1 partials, 2 list, 3 returned, 4 chain)");
   }
+  std::swap(ps->kst, ps->kst_out);   // the push's end states become the carried states
   const int64_t R = std::min<int64_t>((int64_t)cnt[0], cap), total = (int64_t)cnt[1];
   if (total) {
     const dim3 g2((unsigned)((R + 255) / 256));
@@ -1688,8 +1726,11 @@ void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& rd) {
     if (keys < 0 || keys > ((int64_t)1 << 31)) throw SgError(SG_EINVAL, "snapshot: bad sequence state count");
     if (keys > ps->kst_keys) {
       if (ps->kst) hipFree(ps->kst);
-      ps->kst = nullptr;
-      if (hipMalloc(&ps->kst, ps->sq_bytes * (size_t)keys) != hipSuccess) throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
+      if (ps->kst_out) hipFree(ps->kst_out);
+      ps->kst = ps->kst_out = nullptr;
+      if (hipMalloc(&ps->kst, ps->sq_bytes * (size_t)keys) != hipSuccess ||
+          hipMalloc(&ps->kst_out, ps->sq_bytes * (size_t)keys) != hipSuccess)
+        throw SgError(SG_ECAPACITY, "hipMalloc sequence states");
       ps->kst_keys = keys;
     }
     if (ps->kst_keys) HIPCHK(hipMemset(ps->kst, 0, ps->sq_bytes * (size_t)ps->kst_keys));

@@ -113,7 +113,7 @@ struct SgHandle {
   uint64_t snap_gen = ~0ull;
   uint32_t key_bound_seen = 0;
   void* state = nullptr;      // per-shape persistent state (interp / absent)
-  int state_kind = 0;         // 1 every->next closed form, 2 general machine, 3 absence closed form
+  int state_kind = 0;         // 1 every->next closed form, 2 general machine, 3 absence closed form, 4 once closed form
   int split_out = 0;          // 1: output stage timed from ev[5] (host work between ev[3] and ev[5])
   int extra_marks = 0;        // 1: ev[6]..ev[7] hold an extra match-stage interval (overflow re-pass)
   void mark(int k) { hipEventRecord(ev[k], stream); }
@@ -222,6 +222,12 @@ void sg_every_next_reset(SgHandle* h);
 int64_t sg_every_next_carry_max_lag(SgHandle* h, int col, uint32_t ref);
 void sg_every_next_release(SgHandle* h);
 void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n);
+// SG_SHAPE_NEXT_CMP_ONCE (once.hip): state_kind 4
+void sg_run_once(SgHandle* h, const BatchView& bv, int64_t n);
+void sg_once_reset(SgHandle* h);
+void sg_once_release(SgHandle* h);
+void sg_once_snapshot(SgHandle* h, SnapW& w);
+void sg_once_restore(SgHandle* h, SnapR& r);
 void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_absent_reset(SgHandle* h);
 void sg_every_absent_release(SgHandle* h);

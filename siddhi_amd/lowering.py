@@ -197,7 +197,7 @@ def column_layout(ctx: QueryContext) -> List[Tuple[int, int, str]]:
 # Flat NFA lowering for the HIP engine
 # ==============================================================================================
 K_STREAM, K_COUNT, K_LOGICAL, K_ABSENT, K_ALOGICAL = 0, 1, 2, 3, 4
-SHAPE_GENERAL, SHAPE_EVERY_NEXT_CMP, SHAPE_EVERY_ABSENT_EQ = 0, 1, 2
+SHAPE_GENERAL, SHAPE_EVERY_NEXT_CMP, SHAPE_EVERY_ABSENT_EQ, SHAPE_NEXT_CMP_ONCE = 0, 1, 2, 3
 
 # postfix predicate opcodes (shared with siddhi_amd/csrc/nfa_desc.h)
 OP_VAR, OP_CONST, OP_CMP, OP_AND, OP_OR, OP_NOT, OP_ISNULL, OP_MATH = 1, 2, 3, 4, 5, 6, 7, 8
@@ -638,10 +638,63 @@ def _and_words(b: "_FlatBuilder", exprs, cur: int) -> list:
     return words
 
 
+def _cross_compare(B, a: int, bb: int, b: "_FlatBuilder"):
+    """B's filter as (local conjuncts) and (B.x OP A.x) on one numeric attribute type: (op, lr, rr, local
+    conjuncts) with lr = B's side, rr = A's side, or None."""
+    conj = []
+
+    def flat_and(e):
+        if isinstance(e, C.And):
+            flat_and(e.left)
+            flat_and(e.right)
+        else:
+            conj.append(e)
+    for f_ in B.filters:
+        flat_and(f_)
+    cross = [c for c in conj if not b.compile_expr(c, bb)[2]]
+    if len(cross) != 1 or not isinstance(cross[0], C.Compare) or cross[0].op not in (">", ">=", "<", "<="):
+        return None
+    c = cross[0]
+    l_, r_ = c.left, c.right
+    op = c.op
+    if not (isinstance(l_, C.Var) and isinstance(r_, C.Var)):
+        return None
+    lr = b.resolve(l_, bb, False)
+    rr = b.resolve(r_, bb, False)
+    if lr[0] == a and rr[0] == bb:   # e1.x OP x  -> flip to x OP' e1.x
+        lr, rr = rr, lr
+        op = {">": "<", ">=": "<=", "<": ">", "<=": ">="}[op]
+    if not (lr[0] == bb and lr[1] == CURRENT and rr[0] == a and rr[1] in (CURRENT, 0)):
+        return None
+    if lr[3] != rr[3] or lr[3] not in ("INT", "LONG", "FLOAT", "DOUBLE"):
+        return None
+    return op, lr, rr, [x for x in conj if x is not c]
+
+
 def _classify(nfa: FlatNFA, root, b: _FlatBuilder):
     """Detect closed-form shapes."""
     st = nfa.states
-    if nfa.type != 0 or root[0] != "N" or root[1][0] != "E" or root[1][1][0] != "S" or root[2][0] != "S":
+    if nfa.type != 0 or root[0] != "N" or root[2][0] != "S":
+        return
+    if root[1][0] == "S":
+        # A[l] -> B[l' and B.x OP A.x] (within T) without `every`: one e1 per key, then its first completing B row
+        # (csrc/once.hip; PatternPartitionTestCase.java:54-64)
+        a, bb = root[1][1], root[2][1]
+        A, B = st[a], st[bb]
+        if A.kind != K_STREAM or not A.local or A.next_every != -1 or A.next_state != bb or not A.is_start:
+            return
+        if B.kind != K_STREAM or not B.has_selector or B.next_state != -1 or B.next_every != -1 or nfa.sched:
+            return
+        x = _cross_compare(B, a, bb, b)
+        if x is None:
+            return
+        op, lr, rr, local_b = x
+        nfa.shape = SHAPE_NEXT_CMP_ONCE
+        nfa.shape_args = [a, bb, {">": 2, ">=": 3, "<": 4, "<=": 5}[op], b.ret_slot(B.stream, lr[2]),
+                          b.ret_slot(A.stream, rr[2]), TYPE_CODE[lr[3]], len(local_b), 0]
+        nfa.shape_prog = _and_words(b, local_b, bb)
+        return
+    if root[1][0] != "E" or root[1][1][0] != "S":
         return
     a, bb = root[1][1][1], root[2][1]
     A, B = st[a], st[bb]
@@ -649,36 +702,12 @@ def _classify(nfa: FlatNFA, root, b: _FlatBuilder):
         return
     if B.kind == K_STREAM and B.has_selector and B.next_state == -1 and B.next_every == -1 and nfa.within != -1:
         # B filter: (local conjuncts) and (B.x OP A.x) ; same attribute, numeric
-        conj = []
-
-        def flat_and(e):
-            if isinstance(e, C.And):
-                flat_and(e.left)
-                flat_and(e.right)
-            else:
-                conj.append(e)
-        for f_ in B.filters:
-            flat_and(f_)
-        cross = [c for c in conj if not b.compile_expr(c, bb)[2]]
-        if len(cross) != 1 or not isinstance(cross[0], C.Compare) or cross[0].op not in (">", ">=", "<", "<="):
+        x = _cross_compare(B, a, bb, b)
+        if x is None:
             return
-        c = cross[0]
-        l_, r_ = c.left, c.right
-        op = c.op
-        if not (isinstance(l_, C.Var) and isinstance(r_, C.Var)):
-            return
-        lr = b.resolve(l_, bb, False)
-        rr = b.resolve(r_, bb, False)
-        if lr[0] == a and rr[0] == bb:   # e1.x OP x  -> flip to x OP' e1.x
-            lr, rr = rr, lr
-            op = {">": "<", ">=": "<=", "<": ">", "<=": ">="}[op]
-        if not (lr[0] == bb and lr[1] == CURRENT and rr[0] == a and rr[1] in (CURRENT, 0)):
-            return
-        if lr[3] != rr[3] or lr[3] not in ("INT", "LONG", "FLOAT", "DOUBLE"):
-            return
+        op, lr, rr, local_b = x
         if A.stream == B.stream and lr[2] != rr[2]:
             return   # one value per packed record: same-stream shapes must compare one attribute
-        local_b = [x for x in conj if x is not c]
         nfa.shape = SHAPE_EVERY_NEXT_CMP
         slot_b = b.ret_slot(B.stream, lr[2])
         slot_a = b.ret_slot(A.stream, rr[2])
