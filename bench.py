@@ -47,8 +47,7 @@ from siddhi_amd import lowering as L          # noqa: E402
 from siddhi_amd import synth                  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_DIR = os.path.join(ROOT, "profiles", "r03")
-DEFAULT_PMC = os.path.join(PMC_DIR, "C2_pmc.json")
+PMC_DIR = os.path.join(ROOT, "profiles", "r04")
 
 
 def barrier():
@@ -324,24 +323,49 @@ PATH_BYTES = {"C1": (12.125, 36.0, 4.125), "C2": (16.125, 36.0, 4.125), "C5": (1
               "C3b": (20.125, 92.0, 4.125), "C3c": (20.125, 92.0, 4.125), "C3": (20.125, 92.0, 4.125),
               "C4": (16.0, 28.0, None)}
 
+# Each kernel's OWN algorithmic bytes (B/event, B/match) on the closed-form path of C2/C5 (16-B walker records
+# {dts, row|flags, price, id}; match records of 64 B = 32-B header + 4 projected values; e1's compact record 16 B):
+#   pred         price 4 read + condition bit 0.125 written
+#   part_hist    key 4 read
+#   part_group   ts 8 + key 4 + price 4 + id 8 + bit 0.125 read; record 16 + in-group key 1 written
+#   fgw_walk     record 16 + in-group key 1 read, count word 4 written; 16 B compact record per match written
+#   fgw_project  count word 4 read; per match: compact record 16 read, trigger's ts 8 + key 4 + id 8 + price 4
+#                read, 64 B record written
+#   (sorted-walker pipeline, used when the fused walk declines a push)
+#   part_key     record 16 + key 1 read, record 16 written;  units/tile_transpose  record 16 read + 16 written
+#   walk_count   record 16 read, count 4 written per match;   walk_record  record 16 read, 16 B per match written
+#   project      16 B intermediate + 24 B trigger row read, 64 B record written per match
+#   key_sort     rocPRIM onesweep over 16-B records + 4-B keys, 3 passes (C5's 1M keys), read + write
+KERNEL_BYTES = {"pred": (4.125, 0.0), "part_hist": (4.0, 0.0), "part_group": (41.125, 0.0),
+                "fgw_walk": (21.0, 16.0), "fgw_project": (4.0, 104.0), "part_key": (33.0, 0.0),
+                "tile_transpose": (32.0, 0.0), "walk_count": (16.0, 4.0), "walk_record": (16.0, 16.0),
+                "project": (0.0, 104.0), "key_sort": (120.0, 0.0), "pack": (44.125, 0.0),
+                "nge_search": (12.125, 8.0), "once_match": (16.125, 0.0)}
+
 
 def roofline_of(cfg, n, matches, kern, stage):
-    """`roofline` of one push: the §8d whole-path algorithmic bytes over the dominant kernel's HIP-event time (and
-    over the sum of the push's kernels), plus the predicate-evaluation pass."""
+    """`roofline` of one push: the dominant kernel's OWN algorithmic bytes (KERNEL_BYTES) over its HIP-event time;
+    `path` = SURVEY.md §8d whole-path bytes over the sum of the push's kernels; the predicate-evaluation pass."""
     per_ev, per_m, pred_b = PATH_BYTES[cfg]
     path_bytes = per_ev * n + per_m * matches
     dominant = max(kern, key=kern.get) if kern else None
     t_dom = kern.get(dominant, 0.0)
-    dom_gbs = path_bytes / (t_dom * 1e-3) / 1e9 if t_dom else 0.0
+    if dominant in KERNEL_BYTES:
+        ke, km = KERNEL_BYTES[dominant]
+        dom_bytes = ke * n + km * matches
+        dom_def = "%s's own algorithmic bytes: %.3f B/event + %.0f B/match (bench.py KERNEL_BYTES)" % (dominant, ke, km)
+    else:   # (lane / machine kernels: their bytes are the path's)
+        dom_bytes = path_bytes
+        dom_def = "SURVEY.md §8d whole-path bytes (%.3f B/event + %.0f B/match): no per-kernel model" % (per_ev, per_m)
+    dom_gbs = dom_bytes / (t_dom * 1e-3) / 1e9 if t_dom else 0.0
     path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9 if stage[4] else 0.0
     roof = {"bound": "hbm", "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": dominant, "kernel_ms": round(t_dom, 4),
-            "algorithmic_GB_per_launch": round(path_bytes / 1e9, 4),
-            "bytes_definition": "SURVEY.md §8d whole-path algorithmic bytes (%.3f B/event + %.0f B/match) over the "
-                                "dominant kernel's HIP-event time" % (per_ev, per_m),
+            "algorithmic_GB_per_launch": round(dom_bytes / 1e9, 4), "bytes_definition": dom_def,
             "path": {"achieved": round(path_gbs, 1), "frac": round(path_gbs / HBM_PEAK_GBS, 4),
-                     "kernels_total_ms": round(float(stage[4]), 4)},
+                     "kernels_total_ms": round(float(stage[4]), 4), "algorithmic_GB": round(path_bytes / 1e9, 4),
+                     "bytes_definition": "SURVEY.md §8d: %.3f B/event + %.0f B/match" % (per_ev, per_m)},
             "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])}}
     if "pred" in kern and pred_b:
         pg = pred_b * n / (kern["pred"] * 1e-3) / 1e9
@@ -434,7 +458,8 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
     router's assignment, computed on the GPU), with its own dense key ids and the rows' global event indices; it then
     pushes its share as consecutive batches of `push_rows` (state carried between pushes).  Time = max over ranks;
     value = the whole stream's events / that time.  Merging the ranks' match streams (router.merge) is host work
-    outside this number; tests/test_multigpu.py checks the merged output against the oracle."""
+    outside this number; tests/test_multigpu.py checks the merged output against the oracle.  Kernel times (HIP events
+    on the launch stream, summed over a step's pushes) give the roofline of rank 0's share."""
     from siddhi_amd import router
     _, n_total, keys, rate = synth.CONFIGS["C5"]
     total = total or n_total
@@ -450,13 +475,20 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
                                     index=cat["gidx"].data_ptr() + 8 * lo))
     stream = torch.cuda.current_stream()
     h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
+    stage = np.zeros(5)
+    kern = {}
 
-    def step():
+    def step(record=False):
         h.reset()
         m = 0
         for b in batches:
             h.push(b)
-            m += h.timing().matches
+            t = h.timing()
+            m += t.matches
+            if record:
+                stage[:] += [t.pred_ms, t.partition_ms, t.match_ms, t.output_ms, t.total_ms]
+                for name, ms in t.kernels():
+                    kern[name] = kern.get(name, 0.0) + ms
         return m
 
     for _ in range(warmup):
@@ -466,48 +498,66 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        matches = step()
+        matches = step(record=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    el, matches, rows = reduce_max(el), reduce_sum(matches), reduce_sum(n)
+    el, all_matches, rows = reduce_max(el), reduce_sum(matches), reduce_sum(n)
     h.close()
     del cat, batches
     torch.cuda.empty_cache()
     ms = 1000.0 * el / steps
+    roof = roofline_of("C5", n, matches, {k: v / steps for k, v in kern.items()}, stage / steps)
+    roof["scope"] = "rank 0's share of the stream: %d events in %d pushes of <= %d rows, %d matches" % (
+        n, len(range(0, n, push_rows)), push_rows, matches)
     return {"workload": "C5 (BASELINE configs[4]): " + synth.QUERIES["C5"], "events": total, "keys": keys,
             "rate_events_per_ms": rate, "n_gpus": ws, "scaling": "strong", "steps": steps,
             "ms_per_step": round(ms, 3), "value": round(total / (ms * 1e-3), 1), "unit": "events/s",
-            "matches": int(matches), "rows_routed": int(rows), "push_rows": push_rows,
+            "matches": int(all_matches), "rows_routed": int(rows), "push_rows": push_rows,
             "sharding": "mix64(key) mod N on the GPU (router.shard_of_torch), per-rank dense ids, global indices kept",
-            "data": "synthetic, generated in HBM; inputs resident before the timed region"}
+            "data": "synthetic, generated in HBM; inputs resident before the timed region", "roofline": roof}
+
+
+def pcie_peak(dev, mib=1024, reps=5):
+    """Pinned host -> HBM copy rate of one large hipMemcpy on this box (the whole-node path's PCIe ceiling)."""
+    src = torch.empty(mib << 20, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(mib << 20, dtype=torch.uint8, device=dev)
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    del src, dst
+    return (mib << 20) / best / 1e9
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2")
-    ap.add_argument("--events", type=int, default=0, help="events per GPU per step (default: config size, max 1e8)")
+    ap.add_argument("--steps", type=int, default=5, help="timed steps of the headline (one step = the whole C5 stream)")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C5", help="headline: C5 (BASELINE configs[4], the metric's config) or a "
+                                                   "single-push config (C2, C3b, ...)")
+    ap.add_argument("--events", type=int, default=0, help="single-push headline: events per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="events for the CPU baseline (default per config: ~5-20 s of oracle work)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16, help="processes for the key-sharded CPU baseline")
-    ap.add_argument("--whole-node-steps", type=int, default=3, help="steps of the §8d whole-node rate (0: skip)")
-    ap.add_argument("--router-threads", type=int, default=16)
-    ap.add_argument("--c5-stream-steps", type=int, default=2,
-                    help="steps of the 1B-event C5 stream sharded by key hash across the ranks (0: skip)")
     ap.add_argument("--c5-events", type=int, default=0, help="events of the C5 stream (default 1e9)")
     ap.add_argument("--c5-push-rows", type=int, default=100_000_000)
     ap.add_argument("--c5-node-steps", type=int, default=2,
                     help="steps of the 1B-event C5 stream through the node pipeline, rank 0 driving every GPU (0: skip)")
-    ap.add_argument("--c5-node-devices", default="", help="devices of the c5_whole_node pipeline (default: one per rank)")
-    ap.add_argument("--node-key-dict", type=int, default=0, help="whole_node key dictionary: 0 auto, 1 host, 2 GPU")
+    ap.add_argument("--c5-node-devices", default="", help="devices of the whole-node pipeline (default: one per rank)")
+    ap.add_argument("--node-shards", default="2,4,8",
+                    help="N = 1 only: the whole-node pipeline with G shards mapped onto device 0, one step each -- the "
+                         "host stages (route, merge) of a G-GPU node measured on one GPU ('' to skip)")
     ap.add_argument("--node-threads", type=int, default=0, help="host threads of the node pipeline (0: 16 per GPU)")
-    ap.add_argument("--other-configs", default="C1,C3b,C3c,C4",
+    ap.add_argument("--other-configs", default="C2,C1,C3b,C3c,C4,PP",
                     help="BASELINE configs measured beside the headline (one GPU, rank 0; '' to skip)")
     ap.add_argument("--other-steps", type=int, default=3)
-    ap.add_argument("--pmc", default=DEFAULT_PMC, help="rocprofv3 PMC summary of this command (profiles/collect_r03.sh)")
+    ap.add_argument("--pmc", default="", help="rocprofv3 PMC summary of this command (default profiles/r04/<cfg>_pmc.json)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -520,25 +570,33 @@ def main():
     if not args.cpu_sample:
         args.cpu_sample = CPU_SAMPLE.get(cfg, 12_000_000)
     num, n_cfg, keys, rate = synth.CONFIGS[synth._base(cfg)]
-    n = args.events or min(n_cfg, 100_000_000)
 
-    # ---- value: inputs resident in HBM (each rank's keys are its own dense ids 0..K-1, siddhi_amd/router.py)
-    m = measure_push(cfg, rank, n, keys, rate, dev, args.steps, args.warmup, sync_ranks=ws > 1)
-    elapsed, stage, kern, matches, spilled = m["elapsed"], m["stage"], m["kern"], m["matches"], m["spilled"]
-
-    # ---- whole_node (§8d) on this rank's stream, its own GPU through the node pipeline (max over ranks)
-    wn = None
-    if args.whole_node_steps > 0:
-        try:
-            wn = node_whole(cfg, n, keys, rate, [local], args.whole_node_steps, args.router_threads, 0,
-                            args.node_key_dict)
-        except Exception as e:   # report, never fake
-            wn = {"error": str(e)}
-        if ws > 1 and "ms_per_step" in wn:
-            wn["ms_per_step"] = round(reduce_max(wn["ms_per_step"]), 2)
-            wn["value"] = round(ws * n / (wn["ms_per_step"] * 1e-3), 1)
-            wn["scaling"] = "weak (every rank its own stream and GPU)"
-    # ---- c5_whole_node (BASELINE configs[4] as the metric words it): ONE process drives every GPU of the job
+    if cfg == "C5":
+        # ---- value: the metric's config, inputs resident in HBM: ONE 1B-event, 1M-key stream sharded by key hash
+        # over the ranks (strong scaling), pushed in 100M-row batches with carried state
+        head = c5_stream(rank, ws, dev, args.steps, args.warmup, args.c5_events, args.c5_push_rows)
+        value, ms_step = head["value"], head["ms_per_step"]
+        roof = head.pop("roofline")
+        n, matches = head["events"], head["matches"]
+        scaling = "strong"
+        conf = {"workload": head["workload"], "events_per_step": head["events"], "keys": keys, "rate_events_per_ms": rate,
+                "matches_per_step": head["matches"], "push_rows": head["push_rows"],
+                "parallelism": f"key-sharded x{ws} (mix64(key) mod N, no collective)"}
+        pmc_cfg = "C5"
+    else:
+        n = args.events or min(n_cfg, 100_000_000)
+        m = measure_push(cfg, rank, n, keys, rate, dev, args.steps, args.warmup, sync_ranks=ws > 1)
+        ms_step = m["elapsed"] * 1000.0 / args.steps
+        value = ws * n * args.steps / m["elapsed"]
+        matches = m["matches"]
+        roof = roofline_of(cfg, n, matches, m["kern"], m["stage"])
+        scaling = "weak"
+        conf = {"workload": f"{cfg}: " + synth.QUERIES[cfg], "events_per_gpu_per_step": n, "keys_per_gpu": keys,
+                "rate_events_per_ms": rate, "matches_per_gpu_per_step": int(matches),
+                "spilled_units": int(m["spilled"]), "parallelism": f"key-sharded x{ws} (no collective)"}
+        pmc_cfg = cfg
+    # ---- whole node: the same 1B-event C5 stream from pinned host memory through the node pipeline,
+    # rank 0 driving every GPU of the job; PCIe-bound, reported beside `value` (never `value`)
     c5w = None
     if args.c5_node_steps > 0:
         if rank == 0:
@@ -547,36 +605,48 @@ def main():
                 devs = [int(x) for x in args.c5_node_devices.split(",")] if args.c5_node_devices else list(range(ws))
                 c5w = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
                                  synth.CONFIGS["C5"][3], devs, args.c5_node_steps, thr, 0)
+                pk = pcie_peak(dev)
+                h2d_rate = c5w["h2d_GB"] / (c5w["ms_per_step"] * 1e-3)
+                c5w["pcie"] = {"h2d_GBs": round(h2d_rate, 1), "peak_h2d_GBs": round(pk, 1),
+                               "pcie_frac": round(h2d_rate / pk / max(1, len(devs)), 4),
+                               "peak_definition": "one 1 GiB pinned -> HBM copy on this box (best of 5), per GPU"}
+                shards = [int(x) for x in args.node_shards.split(",") if x] if (ws == 1 and args.node_shards) else []
+                if shards:
+                    table = [{"G": 1, "ms_per_step": c5w["ms_per_step"], "route_ms": c5w["route_ms"],
+                              "merge_ms": c5w["merge_ms"], "h2d_GB": c5w["h2d_GB"], "d2h_GB": c5w["d2h_GB"],
+                              "gpu_busy_ms": c5w["gpu_busy_ms"]}]
+                    for G in shards:
+                        r = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
+                                       synth.CONFIGS["C5"][3], [local] * G, 1, thr, 0)
+                        table.append({"G": G, "ms_per_step": r["ms_per_step"], "route_ms": r["route_ms"],
+                                      "merge_ms": r["merge_ms"], "h2d_GB": r["h2d_GB"], "d2h_GB": r["d2h_GB"],
+                                      "gpu_busy_ms": r["gpu_busy_ms"], "shard_rows": r["shard_rows"]})
+                    c5w["node_shards_on_one_gpu"] = {
+                        "host_threads": thr, "rows": table,
+                        "note": "G shards (one sg_handle each) mapped onto device 0: route_ms / merge_ms are the host "
+                                "stages a G-GPU node runs (scatter to per-shard pinned staging, k-way merge), with "
+                                "this box's %d host threads; GPU time is serialised on one device" % thr}
             except Exception as e:   # report, never fake
                 c5w = {"error": str(e)}
         barrier()
-    c5 = None
-    if args.c5_stream_steps > 0:
-        try:
-            c5 = c5_stream(rank, ws, dev, args.c5_stream_steps, 1, args.c5_events, args.c5_push_rows)
-        except Exception as e:   # report, never fake
-            c5 = {"error": str(e)}
     if rank != 0:
         return
-    ms_step = elapsed * 1000.0 / args.steps
-    value = ws * n * args.steps / elapsed
-
-    roof = roofline_of(cfg, n, matches, kern, stage)
-    dominant = roof["kernel"]
-    attach_traffic(roof, args.pmc, cfg, n)
+    attach_traffic(roof, args.pmc or os.path.join(PMC_DIR, pmc_cfg + "_pmc.json"), pmc_cfg,
+                   n if pmc_cfg != "C5" else roof_events(roof))
     cpu = None
     if not args.no_cpu:
         hi = host_info()
         try:
-            r, nm, dt = cpu_baseline(cfg, args.cpu_sample, keys, rate)
+            ccfg = cfg
+            r, nm, dt = cpu_baseline(ccfg, args.cpu_sample, keys, rate)
             cpu = {"value": round(r, 1), "unit": "events/s", "cores": 1, "kind": "port",
                    "nproc": hi["nproc"], "cpu_model": hi["cpu_model"],
-                   "sample": f"first {args.cpu_sample} events of {cfg} ({keys} keys, {rate}/ms), oracle C++ "
+                   "sample": f"first {args.cpu_sample} events of {ccfg} ({keys} keys, {rate}/ms), oracle C++ "
                              f"restatement of the reference state processors, single thread, {nm} matches, {dt:.1f}s"}
             wk = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-            partitioned = cfg[:2] in ("C2", "C3", "C5")   # C1 / C4 are single runtimes
+            partitioned = ccfg[:2] in ("C2", "C3", "C5")   # C1 / C4 are single runtimes
             if partitioned and wk > 1:
-                r2, nm2, dt2 = cpu_baseline_multicore(cfg, args.cpu_sample, keys, rate, wk)
+                r2, nm2, dt2 = cpu_baseline_multicore(ccfg, args.cpu_sample, keys, rate, wk)
                 cpu["multi_core"] = {"value": round(r2, 1), "cores": wk,
                                      "sample": f"same rows key-sharded over {wk} processes, {nm2} matches, {dt2:.1f}s"}
         except Exception as e:  # report, never fake
@@ -592,21 +662,25 @@ def main():
     line = {
         "metric": "events/sec (whole node) for partitioned pattern query at 1/2/4/8 GPUs; % HBM peak",
         "value": round(value, 1), "unit": "events/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
         "dtype": "f32", "data": "synthetic (SplitMix64 generator, SURVEY.md §8d), inputs resident in HBM; matches "
                                "projected in HBM (zero-copy sg_device_records)",
-        "config": {"workload": f"{cfg}: " + synth.QUERIES[cfg], "events_per_gpu_per_step": n,
-                   "keys_per_gpu": keys, "rate_events_per_ms": rate, "matches_per_gpu_per_step": int(matches),
-                   "spilled_units": int(spilled), "parallelism": f"key-sharded x{ws} (no collective)"},
-        "whole_node": wn,
-        "c5_stream": c5,
-        "c5_whole_node": c5w,
+        "config": conf,
+        "whole_node": c5w,
         "roofline": roof,
         "cpu_baseline": cpu,
         "configs": others,
-        "source_hash": source_hash(cfg),
+        "source_hash": source_hash(pmc_cfg),
     }
     print(json.dumps(line))
+
+
+def roof_events(roof):
+    """events of the push the roofline was taken on (C5: rank 0's share of the stream, a multiple of 1e8 rows)"""
+    try:
+        return int(roof["scope"].split()[4])
+    except Exception:
+        return 0
 
 
 if __name__ == "__main__":

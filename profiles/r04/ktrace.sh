@@ -4,7 +4,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=$1; cfg=$2; shift 2
 d="$out/$cfg"; mkdir -p "$d"
-args="--config $cfg --steps 2 --warmup 1 --no-cpu --other-configs= --whole-node-steps 0 --c5-stream-steps 0 --c5-node-steps 0 $*"
+args="--config $cfg --steps 2 --warmup 1 --no-cpu --other-configs= --c5-node-steps 0 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/trace" -o run -- \
   python3 -u bench.py $args > "$d/trace.log" 2>&1 || { echo "$cfg trace failed"; tail -5 "$d/trace.log"; exit 1; }
 f=$(find "$d/trace" -name "run_kernel_stats.csv" | head -1)

@@ -313,10 +313,10 @@ struct PartPlan {
   uint32_t ts2, nj;           // pass-1 segments per pass-2 segment; pass-2 segments per group
 };
 
-template <class R, int PT>
+template <class R, int PT, class TG = uint16_t>
 struct PartLds {
   R stage[256 * PT];          // the sub-tile's records, sorted by digit
-  uint16_t tag[256 * PT];     // key (pass 1) / in-group key (pass 2) of each staged record
+  TG tag[256 * PT];           // key (pass 1) / in-group key (pass 2) of each staged record
   uint32_t cw[4][PT_D];       // per-wave digit counts, then per-wave slot cursors
   uint32_t ls[PT_D];          // sub-tile start of each digit
   uint32_t tot[PT_D];         // sub-tile count of each digit
@@ -352,8 +352,8 @@ __device__ __forceinline__ void peer_rank(bool valid, uint32_t d, uint32_t nb, u
 }
 
 // digit counts -> per-wave slot cursors and sub-tile digit starts; returns the sub-tile's staged rows
-template <class R, int PT>
-__device__ __forceinline__ uint32_t part_cursors(PartLds<R, PT>& L) {
+template <class R, int PT, class TG>
+__device__ __forceinline__ uint32_t part_cursors(PartLds<R, PT, TG>& L) {
   const uint32_t t = threadIdx.x;
   const uint32_t c0 = L.cw[0][t], c1 = L.cw[1][t], c2 = L.cw[2][t], c3 = L.cw[3][t];
   const uint32_t tot = c0 + c1 + c2 + c3;
@@ -397,14 +397,15 @@ static __global__ void __launch_bounds__(256) k_part1_hist(KeyOf kf, PartPlan pp
   if (bad) atomicOr(flags, bad);
 }
 
-// pass-1 scatter: records of segment j, grouped (two passes) or final (one pass)
-template <class T, bool N>
+// pass-1 scatter: records of segment j, grouped (two passes) or final (one pass).  TG holds a staged record's key
+// (32 bits beyond 65536 keys), LK its in-group key.
+template <class T, bool N, class TG = uint16_t, class LK = uint8_t>
 __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPlan pp, int64_t nt,
                                                const uint32_t* __restrict__ o1, WRec<T, N>* __restrict__ orec,
-                                               uint8_t* __restrict__ olk, uint32_t* __restrict__ flags) {
+                                               LK* __restrict__ olk, uint32_t* __restrict__ flags) {
   typedef WRec<T, N> R;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  PartLds<R, PT1>& L = *(PartLds<R, PT1>*)lds_raw;
+  PartLds<R, PT1, TG>& L = *(PartLds<R, PT1, TG>*)lds_raw;
   const uint32_t j = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t lmask = (1u << pp.lb) - 1u;
   if (t < pp.ng) L.run[t] = o1[(size_t)t * pp.ns1 + j];
@@ -470,7 +471,7 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
         const uint32_t slot = L.cw[w][d] + rank;
         if (rank == 0) L.cw[w][d] = slot + cnt;
         L.stage[slot] = rc[s];
-        L.tag[slot] = (uint16_t)tg[s];
+        L.tag[slot] = (TG)tg[s];
       }
     }
     if (base + PT1_ROWS < re) load(base + PT1_ROWS, tn, rn);   // next sub-tile in flight during the write-out
@@ -480,7 +481,7 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
       const uint32_t dst = L.run[d] + q - L.ls[d];
       if ((int64_t)dst >= nt) { bad |= PK_INTERNAL; continue; }
       orec[dst] = L.stage[q];
-      if (olk) olk[dst] = (uint8_t)(k & lmask);
+      if (olk) olk[dst] = (LK)(k & lmask);
     }
     __syncthreads();
     L.run[t] += L.tot[t];
@@ -1716,6 +1717,293 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   return true;
 }
 
+#include "fgw.h"
+
+template <class T, int KG, int CAP>
+static void launch_fgw(int op, unsigned grid, size_t lds, hipStream_t st, const FgwArgs& A, const PtU4* grec,
+                       const uint8_t* glk, const FgwSeg* segs, uint32_t* gm32, PtU4* comp, uint32_t* cst, uint32_t* cend,
+                       uint32_t* kcnt, uint32_t* kent, uint32_t* fl) {
+#define SG_FGW(OPV)                                                                                                   \
+  HIPCHK(hipFuncSetAttribute((const void*)k_fgw<T, KG, CAP, OPV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+  hipLaunchKernelGGL((k_fgw<T, KG, CAP, OPV>), dim3(grid), dim3(256), lds, st, A, grec, glk, segs, gm32, comp, cst, cend,  \
+                     kcnt, kent, fl)
+  switch (op) {
+    case 2: SG_FGW(2); break;
+    case 3: SG_FGW(3); break;
+    case 4: SG_FGW(4); break;
+    default: SG_FGW(5); break;
+  }
+#undef SG_FGW
+  HIPCHK(hipGetLastError());
+}
+
+// The fused group walk (fgw.h) for one push.  Returns 1 when the push is done, 0 when a precondition failed on the
+// GPU (nothing was changed: the caller runs the sorted-walker pipeline), -1 when narrow records cannot represent the
+// push (the caller falls back to wide records).
+template <class T>
+static int run_fgw(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& plan, const Virt& v, const SgCols& cc,
+                   uint32_t kb, int cap, const WalkArgs& wa0, EveryNextState* es) {
+  typedef WRec<T, true> R;
+  static_assert(sizeof(R) == 16, "narrow record");
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  const int64_t nc = v.nc, nt = nc + n;
+  const int KG = cap <= 16 ? 256 : (cap <= 32 ? 128 : 64);
+  uint32_t lb = 0;
+  while ((1u << lb) < (uint32_t)KG) ++lb;
+  const uint32_t ng = (kb + KG - 1) / KG;
+  // ---- plan: part1 with digit = key >> lb, segments of <= 8192 rows (projection chunks)
+  PartPlan pp;
+  memset(&pp, 0, sizeof(pp));
+  pp.K = kb;
+  pp.lb = lb;
+  pp.ng = ng;
+  pp.two = 1;
+  uint32_t nb1 = 0;
+  while ((1u << nb1) < ng) ++nb1;
+  pp.nb1 = nb1;
+  pp.nb2 = lb;
+  // (part1 segments are the projection chunks: <= 65536 rows, ~2048 of them when the batch allows)
+  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(FGW_CHUNK / PT1_ROWS, nt / ((int64_t)PT1_ROWS * 2048)));
+  pp.seg1 = (uint32_t)(PT1_ROWS * sub);
+  pp.ns1 = (uint32_t)std::max<int64_t>(1, (nt + pp.seg1 - 1) / pp.seg1);
+  KeyOf kf{bv.key, es->carry[es->cur].key, (uint32_t)nc};
+  const size_t n1 = (size_t)pp.ng * pp.ns1 + 1;
+  uint32_t* pk_flags = (uint32_t*)h->ws.get("pack_flags", sizeof(uint32_t), st);
+  HIPCHK(hipMemsetAsync(pk_flags, 0, sizeof(uint32_t), st));
+  uint32_t* h1 = (uint32_t*)h->ws.get("part_h1", sizeof(uint32_t) * n1, st);
+  uint32_t* o1 = (uint32_t*)h->ws.get("part_o1", sizeof(uint32_t) * n1, st);
+  R* grec = (R*)h->ws.get("grec", sizeof(R) * nt, st);
+  uint8_t* glk = (uint8_t*)h->ws.get("glk", nt, st);
+  PackFn<T, true> pk;
+  pk.v = v;
+  size_t tb = 0;
+  void* tmp = nullptr;
+  auto scan_u32 = [&](const uint32_t* in, uint32_t* outp, size_t cnt, const char* tmpname) {
+    size_t b = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, b, in, outp, (uint32_t)0, cnt, rocprim::plus<uint32_t>(), st));
+    void* tp = h->ws.get(tmpname, b, st);
+    HIPCHK(rocprim::exclusive_scan(tp, b, in, outp, (uint32_t)0, cnt, rocprim::plus<uint32_t>(), st));
+  };
+  if (ng <= 256) {
+    const size_t lds1 = sizeof(PartLds<R, PT1>);
+    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+    h->kbeg("part_hist");
+    HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pp, nt, h1, pk_flags);
+    HIPCHK(hipGetLastError());
+    scan_u32(h1, o1, n1, "part_scan_tmp");
+    h->kend();
+    h->kbeg("part_group");
+    hipLaunchKernelGGL((k_part1<T, true>), dim3(pp.ns1), dim3(256), lds1, st, pk, kf, pp, nt, o1, grec, glk, pk_flags);
+    HIPCHK(hipGetLastError());
+    h->kend();
+  } else {
+    // two passes: supergroups of 2^lbs groups (<= 256 of them), then groups inside each supergroup
+    uint32_t lbs = 0;
+    while ((ng >> lbs) > 256u || ((ng + (1u << lbs) - 1) >> lbs) > 256u) ++lbs;
+    PartPlan pa2 = pp;
+    pa2.lb = lb + lbs;
+    pa2.ng = (kb + (1u << pa2.lb) - 1) >> pa2.lb;
+    uint32_t nbA = 0;
+    while ((1u << nbA) < pa2.ng) ++nbA;
+    pa2.nb1 = nbA;
+    const size_t nA = (size_t)pa2.ng * pp.ns1 + 1;
+    uint32_t* hA = (uint32_t*)h->ws.get("part_hA", sizeof(uint32_t) * nA, st);
+    uint32_t* oA = (uint32_t*)h->ws.get("part_oA", sizeof(uint32_t) * nA, st);
+    R* grecA = (R*)h->ws.get("grecA", sizeof(R) * nt, st);
+    uint16_t* glkA = (uint16_t*)h->ws.get("glkA", 2 * nt, st);
+    h->kbeg("part_hist");
+    HIPCHK(hipMemsetAsync(hA + nA - 1, 0, sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pa2, nt, hA, pk_flags);
+    hipLaunchKernelGGL(k_hist_wide, dim3(pp.ns1), dim3(256), 0, st, kf, kb, lb, ng, pp.seg1, pp.ns1, nt, h1, pk_flags);
+    HIPCHK(hipGetLastError());
+    scan_u32(hA, oA, nA, "part_scan_tmpA");
+    scan_u32(h1, o1, n1, "part_scan_tmp");
+    h->kend();
+    h->kbeg("part_group");
+    const size_t ldsA = sizeof(PartLds<R, PT1, uint32_t>);
+    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, true, uint32_t, uint16_t>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsA));
+    hipLaunchKernelGGL((k_part1<T, true, uint32_t, uint16_t>), dim3(pp.ns1), dim3(256), ldsA, st, pk, kf, pa2, nt, oA,
+                       grecA, glkA, pk_flags);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->kbeg("part_split");
+    Part1bArgs B;
+    B.lb = lb;
+    B.lbs = lbs;
+    B.ns1 = pp.ns1;
+    const int64_t per_sg = std::max<int64_t>(1, nt / pa2.ng);
+    B.nsb = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, per_sg / 32768));
+    B.tsb = (pp.ns1 + B.nsb - 1) / B.nsb;
+    B.nsb = (pp.ns1 + B.tsb - 1) / B.tsb;
+    B.oa = oA;
+    B.o1 = o1;
+    const size_t ldsB = sizeof(Part1bLds<16>);
+    HIPCHK(hipFuncSetAttribute((const void*)k_part1b<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsB));
+    hipLaunchKernelGGL((k_part1b<16>), dim3(pa2.ng * B.nsb), dim3(256), ldsB, st, B, (const PtU4*)grecA, glkA,
+                       (PtU4*)grec, glk, (uint32_t)nt, pk_flags);
+    HIPCHK(hipGetLastError());
+    h->kend();
+  }
+  uint32_t pkf = 0;
+  HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (pkf & PK_KEY_RANGE) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+  if (pkf & PK_INTERNAL) throw SgError(SG_EINVAL, "internal: key partition offsets out of range");
+  if (pkf & PK_TS_RANGE) return -1;
+  if (pkf & PK_PAY_RANGE) return 0;   // (payloads wider than 32 bits: the sorted walker gathers them by row)
+  h->mark(2);
+  // ---- walk segments
+  FgwArgs A;
+  memset(&A, 0, sizeof(A));
+  A.nc = nc;
+  A.within = (int32_t)std::min<int64_t>(d.within, 0x7fffffffll);
+  A.op = wa0.op;
+  A.stack_mode = wa0.stack_mode;
+  A.K = ng * (uint32_t)KG;   // (padded: carry scratch is indexed by dense key)
+  A.lb = lb;
+  A.ng = ng;
+  A.ns1 = pp.ns1;
+  A.seg1 = pp.seg1;
+  A.cap = (uint32_t)cap;
+  A.o1 = o1;
+  const uint32_t nsw = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, (1024 + ng - 1) / ng));
+  A.nsw = nsw;
+  A.tsw = (pp.ns1 + nsw - 1) / nsw;
+  const uint32_t nw = ng * nsw;
+  FgwSeg* segs = (FgwSeg*)h->ws.get("fgw_segs", sizeof(FgwSeg) * nw, st);
+  uint32_t* caps = (uint32_t*)h->ws.get("fgw_caps", sizeof(uint32_t) * (nw + 1), st);
+  uint32_t* cofs = (uint32_t*)h->ws.get("fgw_cofs", sizeof(uint32_t) * (nw + 1), st);
+  h->kbeg("fgw_plan");
+  HIPCHK(hipMemsetAsync(caps + nw, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL(k_fgw_plan, dim3((nw + 255) / 256), dim3(256), 0, st, A, (const PtU4*)grec, segs, caps);
+  HIPCHK(hipGetLastError());
+  tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, caps, cofs, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
+  tmp = h->ws.get("fgw_scan_tmp", tb, st);
+  HIPCHK(rocprim::exclusive_scan(tmp, tb, caps, cofs, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
+  hipLaunchKernelGGL(k_fgw_cb, dim3((nw + 255) / 256), dim3(256), 0, st, nw, cofs, segs);
+  HIPCHK(hipGetLastError());
+  uint32_t ccap = 0;
+  HIPCHK(hipMemcpyAsync(&ccap, cofs + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  h->kend();
+  uint32_t* gm32 = (uint32_t*)h->ws.get("fgw_gm32", sizeof(uint32_t) * nt, st);
+  PtU4* comp = (PtU4*)h->ws.get("fgw_comp", sizeof(PtU4) * std::max<uint32_t>(ccap, 1), st);
+  uint32_t* cst = (uint32_t*)h->ws.get("fgw_cst", sizeof(uint32_t) * n1, st);
+  uint32_t* cend = (uint32_t*)h->ws.get("fgw_cend", sizeof(uint32_t) * n1, st);
+  uint32_t* ctot = (uint32_t*)h->ws.get("fgw_ctot", sizeof(uint32_t) * (pp.ns1 + 1), st);
+  uint32_t* cbase = (uint32_t*)h->ws.get("fgw_cbase", sizeof(uint32_t) * (pp.ns1 + 1), st);
+  const bool carry = !h->opt.no_carry;
+  const size_t kslots = (size_t)nsw * A.K;
+  uint32_t* kcnt = carry ? (uint32_t*)h->ws.get("fgw_kcnt", sizeof(uint32_t) * kslots, st) : nullptr;
+  uint32_t* kent = carry ? (uint32_t*)h->ws.get("fgw_kent", sizeof(uint32_t) * kslots * (cap + 1), st) : nullptr;
+  uint32_t* fl = (uint32_t*)h->ws.get("fgw_flags", sizeof(uint32_t), st);
+  HIPCHK(hipMemsetAsync(fl, 0, sizeof(uint32_t), st));
+  if (carry) HIPCHK(hipMemsetAsync(kcnt, 0xff, sizeof(uint32_t) * kslots, st));
+  h->kbeg("fgw_walk");
+  const int op = wa0.op;
+  if (KG == 256) {
+    launch_fgw<T, 256, 16>(op, nw, sizeof(FgwLds<T, 256, 16>), st, A, (const PtU4*)grec, glk, segs, gm32, comp, cst, cend,
+                           kcnt, kent, fl);
+  } else if (KG == 128) {
+    launch_fgw<T, 128, 32>(op, nw, sizeof(FgwLds<T, 128, 32>), st, A, (const PtU4*)grec, glk, segs, gm32, comp, cst, cend,
+                           kcnt, kent, fl);
+  } else {
+    launch_fgw<T, 64, 64>(op, nw, sizeof(FgwLds<T, 64, 64>), st, A, (const PtU4*)grec, glk, segs, gm32, comp, cst, cend,
+                          kcnt, kent, fl);
+  }
+  h->kend();
+  uint32_t hfl = 0;
+  HIPCHK(hipMemcpyAsync(&hfl, fl, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (hfl & FGW_F_INTERNAL) throw SgError(SG_EINVAL, "internal: fused group walk guard tripped");
+  if (hfl) {
+    if (getenv("SG_DEBUG_FGW")) fprintf(stderr, "fused group walk declined (flags %u)\n", hfl);
+    return 0;
+  }
+  h->mark(3);
+  h->kbeg("fgw_scan");
+  hipLaunchKernelGGL(k_fgw_ctot, dim3(pp.ns1 + 1), dim3(256), 0, st, A, cst, cend, ctot);
+  HIPCHK(hipGetLastError());
+  tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, ctot, cbase, (uint32_t)0, (size_t)pp.ns1 + 1, rocprim::plus<uint32_t>(), st));
+  tmp = h->ws.get("fgw_scan_tmp2", tb, st);
+  HIPCHK(rocprim::exclusive_scan(tmp, tb, ctot, cbase, (uint32_t)0, (size_t)pp.ns1 + 1, rocprim::plus<uint32_t>(), st));
+  uint32_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, cbase + pp.ns1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  h->kend();
+  h->split_out = 1;
+  h->extra_marks = 0;
+  WalkArgs wa = wa0;
+  char* out = h->out.reserve(total, d.n_select, st);
+  wa.out_base = h->out.n;
+  h->mark(5);
+  if (total) {
+    h->kbeg("fgw_project");
+    const size_t ldsp = sizeof(FgwProjLds);
+    uint32_t* gcur = (uint32_t*)h->ws.get("fgw_gcur", sizeof(uint32_t) * (size_t)pp.ns1 * ng, st);
+    uint32_t* gsrc = (uint32_t*)h->ws.get("fgw_gsrc", sizeof(uint32_t) * (size_t)pp.ns1 * ng, st);
+    hipLaunchKernelGGL((k_fgw_proj<T>), dim3(pp.ns1), dim3(256), ldsp, st, A, wa, v, plan.pp, bv.cols, cc, gm32,
+                       (const PtU4*)comp, cst, cbase, gcur, gsrc, out, fl);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    HIPCHK(hipMemcpyAsync(&hfl, fl, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (hfl & FGW_F_INTERNAL) throw SgError(SG_EINVAL, "internal: fused group projection guard tripped");
+  }
+  h->out.n += total;
+  h->mark(4);
+  // ---- carry into the next push
+  if (carry) {
+    h->kbeg("carry");
+    const uint32_t Kp = A.K;
+    uint32_t* cn = (uint32_t*)h->ws.get("fgw_ccnt", sizeof(uint32_t) * (Kp + 1), st);
+    uint32_t* coff = (uint32_t*)h->ws.get("fgw_coff", sizeof(uint32_t) * (Kp + 1), st);
+    uint32_t* cseg = (uint32_t*)h->ws.get("fgw_cseg", sizeof(uint32_t) * (Kp + 1), st);
+    hipLaunchKernelGGL(k_fgw_carry_count, dim3((Kp + 1 + 255) / 256), dim3(256), 0, st, Kp, nsw, kcnt, cn, cseg);
+    HIPCHK(hipGetLastError());
+    tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cn, coff, (uint32_t)0, (size_t)Kp + 1, rocprim::plus<uint32_t>(), st));
+    tmp = h->ws.get("fgw_carry_scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, cn, coff, (uint32_t)0, (size_t)Kp + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t ncar = 0;
+    HIPCHK(hipMemcpyAsync(&ncar, coff + Kp, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    CarrySet& cs = es->carry[es->cur];
+    CarrySet& nx = es->carry[es->cur ^ 1];
+    nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
+    int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
+    int32_t hw[SG_MAX_COLS];
+    for (int c = 0; c < SG_MAX_COLS; ++c)
+      hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
+    HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
+    CarryBufs cb;
+    memset(&cb, 0, sizeof(cb));
+    cb.ts = nx.ts;
+    cb.key = nx.key;
+    cb.flags = nx.flags;
+    for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
+    if (ncar)
+      hipLaunchKernelGGL((k_fgw_carry_copy<T>), dim3((Kp + 255) / 256), dim3(256), 0, st, v, Kp, (uint32_t)(cap + 1), cseg,
+                         coff, kent, d.n_cols, widths, bv.cols, cc, cb);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    nx.n = ncar;
+    cs.n = 0;
+    es->cur ^= 1;
+    h->kend();
+  }
+  h->last_events = n;
+  h->last_matches = total;
+  h->last_spilled = 0;
+  return 1;
+}
+
 template <class T, bool N>
 static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan plan) {
   const sg_nfa_desc& d = h->desc;
@@ -1814,6 +2102,40 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
   seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
   const dim3 pgrd((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32));
+  // fused group walk (fgw.h): no key-sorted copy, one walk, arrival-ordered projection
+  if constexpr (N && sizeof(T) == 4) {
+    static const bool fgw_off = getenv("SG_NO_FGW") != nullptr;   // (experiments: the sorted-walker pipeline)
+    if (d.partitioned && h->opt.partition_sort == 0 && !h->opt.walker_only && !fgw_off && n > 0) {
+      int64_t tfl[2] = {0, 0};
+      HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const int64_t win = window_rows(kb, nt, d.within, tfl[1] - tfl[0]);
+      const int cap = h->opt.ring_cap > 0 ? h->opt.ring_cap : pick_cap(win);
+      const int KG = cap <= 16 ? 256 : (cap <= 32 ? 128 : 64);
+      if (cap <= 64 && (kb + KG - 1) / KG <= 4096u) {
+        WalkArgs w0;
+        memset(&w0, 0, sizeof(w0));
+        w0.partitioned = 1;
+        w0.op = op;
+        w0.stack_mode = ((val_col_a == val_col_b) && (pa.s_a == pa.s_b) && pa.prog_b_len == 0) ? 1 : 0;
+        w0.base_index = bv.base_index;
+        w0.index = bv.index;
+        const int rbx = d.recv_of_stream[d.states[b_state].stream];
+        w0.multi = d.receivers[rbx].multi;
+        if (w0.multi) {
+          const sg_receiver_desc& r = d.receivers[rbx];
+          for (int q = 0; q < r.n; ++q)
+            if (r.pres[r.n - 1 - q] == b_state) w0.b_slot = q;   // eventSequence = reversed init order
+        }
+        w0.n_select = d.n_select;
+        w0.stride = 32 + 8 * d.n_select;
+        const int rr = run_fgw<T>(h, bv, n, plan, v, cc, kb, cap, w0, es);
+        if (rr == 1) return true;
+        if (rr == -1) return false;
+      }
+    }
+  }
   const bool lds_part = d.partitioned && kb <= 65536u && h->opt.partition_sort == 0;
   if (lds_part) {
     const PartPlan pp = part_plan(kb, nt);
