@@ -1764,7 +1764,9 @@ static int run_fgw(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& 
   pp.nb1 = nb1;
   pp.nb2 = lb;
   // (part1 segments are the projection chunks: <= 65536 rows, ~2048 of them when the batch allows)
-  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(FGW_CHUNK / PT1_ROWS, nt / ((int64_t)PT1_ROWS * 2048)));
+  // 8192-row chunks (one LDS pass in the projection) unless the (group, chunk) tables would pass 4M entries
+  const int64_t cmax = (int64_t)ng * ((nt + FGW_SUB - 1) / FGW_SUB) <= ((int64_t)4 << 20) ? FGW_SUB : FGW_CHUNK;
+  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(cmax / PT1_ROWS, nt / ((int64_t)PT1_ROWS * 2048)));
   pp.seg1 = (uint32_t)(PT1_ROWS * sub);
   pp.ns1 = (uint32_t)std::max<int64_t>(1, (nt + pp.seg1 - 1) / pp.seg1);
   KeyOf kf{bv.key, es->carry[es->cur].key, (uint32_t)nc};
@@ -1870,7 +1872,8 @@ static int run_fgw(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& 
   A.seg1 = pp.seg1;
   A.cap = (uint32_t)cap;
   A.o1 = o1;
-  const uint32_t nsw = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, (1024 + ng - 1) / ng));
+  // one workgroup per CU (LDS): ~2 full rounds of (group, segment) workgroups, fewer segments = less replay
+  const uint32_t nsw = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, 512 / ng));
   A.nsw = nsw;
   A.tsw = (pp.ns1 + nsw - 1) / nsw;
   const uint32_t nw = ng * nsw;
@@ -1945,7 +1948,8 @@ static int run_fgw(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& 
   h->mark(5);
   if (total) {
     h->kbeg("fgw_project");
-    const size_t ldsp = sizeof(FgwProjLds);
+    const size_t ldsp = sizeof(FgwProjLds) + sizeof(uint32_t) * (3 * (size_t)ng + 1);
+    HIPCHK(hipFuncSetAttribute((const void*)k_fgw_proj<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsp));
     uint32_t* gcur = (uint32_t*)h->ws.get("fgw_gcur", sizeof(uint32_t) * (size_t)pp.ns1 * ng, st);
     uint32_t* gsrc = (uint32_t*)h->ws.get("fgw_gsrc", sizeof(uint32_t) * (size_t)pp.ns1 * ng, st);
     hipLaunchKernelGGL((k_fgw_proj<T>), dim3(pp.ns1), dim3(256), ldsp, st, A, wa, v, plan.pp, bv.cols, cc, gm32,

@@ -59,13 +59,16 @@ struct FgwLds {
   uint32_t srow[CAP * KG];
   PtU4 srt[FGW_T];             // the sub-tile's records sorted by in-group key
   uint16_t said[FGW_T];        // arrival-local index of each sorted slot
+  uint16_t sslot[FGW_T];       // sorted slot of each arrival-local index
   uint32_t aux[FGW_T];         // before the walk: dts by arrival index (order check); after: m | emission slot << 16
+                               // by sorted slot
   uint16_t eoff[FGW_T];        // exclusive scan of m over arrival order
   PtU4 ebuf[FGW_EB];           // the sub-tile's match records in walk order
   uint32_t cw[4][256];         // per-wave digit counts, then slot cursors
   uint32_t kb[256], kn[256];   // per in-group key: first sorted slot, rows
   uint32_t wsum[4];
   uint32_t etop, flags, ttot;
+  uint32_t rfirst, rlast;      // arrival rows of the sub-tile's first and last segment rows
 };
 
 template <class T>
@@ -164,8 +167,9 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
       }
       if (bad) atomicOr(&L.flags, FGW_F_ORDER);
     }
+    const int32_t lastt = (int32_t)L.aux[rows - 1];   // (read before the barrier: aux is cleared after it)
     __syncthreads();
-    if (t == 0) prevt = (int32_t)L.aux[rows - 1];
+    prevt = lastt;
 #pragma unroll
     for (int s = 0; s < FGW_PT; ++s) {
       const bool valid = tg[s] != 0xffffffffu;
@@ -175,8 +179,10 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
       if (valid) {
         const uint32_t slot = L.cw[w][d] + rank;
         if (rank == 0) L.cw[w][d] = slot + cnt;
+        const uint32_t ai = w * (FGW_PT * 64) + s * 64 + lane;
         L.srt[slot] = rc[s];
-        L.said[slot] = (uint16_t)(w * (FGW_PT * 64) + s * 64 + lane);
+        L.said[slot] = (uint16_t)ai;
+        L.sslot[ai] = (uint16_t)slot;
       }
     }
     for (uint32_t i = t; i < rows; i += 256) L.aux[i] = 0;
@@ -187,16 +193,20 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
     // ---- walk: lane k steps through its key's rows of the sub-tile
     if (owner) {
       const uint32_t s0 = L.kb[t], s1 = s0 + L.kn[t];
+      // segment rows (which emit) vs replay rows: only the sub-tile that straddles the segment start mixes them
+      const bool seg_all = base >= sg.lo, seg_none = base + rows <= sg.lo;
+      if (s1 > s0 && !seg_none) {
+        const uint32_t pl = base + L.said[s1 - 1];
+        if (pl >= sg.lo) lastpos = pl;
+      }
       for (uint32_t s = s0; s < s1; ++s) {
         const PtU4 q = L.srt[s];
-        const uint32_t a = L.said[s];
-        const uint32_t pos = base + a;
         const uint32_t f = q.y >> 30;
         const uint32_t r = q.y & ROW_MASK;
         const int32_t tt = (int32_t)q.x;
         const T x = fgw_val<T>(q);
-        if (pos >= sg.lo) lastpos = pos;
         if (!f) continue;
+        const bool in_seg = seg_all || (!seg_none && base + L.said[s] >= sg.lo);
         // lazy `within` expiry of the oldest partials (StreamPreStateProcessor.isExpired :102-113)
         if (head != top && (int64_t)tt - hts > A.within) {
           ++head;
@@ -207,7 +217,7 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
           }
         }
         const bool live = !is_nan_val<T>(x);
-        const bool emit = pos >= sg.lo && (int64_t)r >= A.nc;
+        const bool emit = in_seg && (int64_t)r >= A.nc;
         uint32_t m = 0;
         if ((f & F_CONS) && live && head != top) {
           if (A.stack_mode) {
@@ -229,7 +239,7 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
                     e.w = 0;
                     L.ebuf[e0 + u] = e;
                   }
-                  L.aux[a] = m | (e0 << 16);
+                  L.aux[s] = m | (e0 << 16);
                 }
               }
               top -= m;
@@ -271,7 +281,7 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
                 ++wr;
               }
             }
-            if (emit && m && room) L.aux[a] = m | (e0 << 16);
+            if (emit && m && room) L.aux[s] = m | (e0 << 16);
             top = wr;
             if (head != top) {
               hts = L.sdts[(head & cmask) * KG + t];
@@ -303,7 +313,7 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
 #pragma unroll
       for (int q = 0; q < FGW_PT; ++q) {
         const uint32_t a = t * FGW_PT + q;
-        mv[q] = a < rows ? (L.aux[a] & 0xffffu) : 0u;
+        mv[q] = a < rows ? (L.aux[L.sslot[a]] & 0xffffu) : 0u;
         sum += mv[q];
       }
       const uint32_t ex = block_excl_scan256(sum, L.wsum);
@@ -324,19 +334,31 @@ __global__ void __launch_bounds__(256) k_fgw(FgwArgs A, const PtU4* __restrict__
       if (i >= rows) continue;
       const uint32_t pos = base + i;
       if (pos < sg.lo) continue;
-      const uint32_t av = L.aux[i];
+      const uint32_t av = L.aux[L.sslot[i]];
       const uint32_t m = av & 0xffffu;
       const uint32_t r = rc[s].y & ROW_MASK;
       const uint32_t j = r / A.seg1;
       gm32[pos] = (r - j * A.seg1) | (m << 16);
       const uint32_t dst = sg.cb + cur + L.eoff[i];
-      const size_t gj = (size_t)g * A.ns1 + j;
       if (j < j0 || j >= j1) atomicOr(&L.flags, FGW_F_INTERNAL);
-      if (pos == A.o1[gj]) cst[gj] = dst;              // the group's first row of projection chunk j
-      if (pos + 1 == A.o1[gj + 1]) cend[gj] = dst + m;  // ... and its last (group-domain ranges are contiguous)
+      if (pos == max(base, sg.lo)) L.rfirst = r;
+      if (i == rows - 1) L.rlast = r;
       if (m) {
         const uint32_t e0 = av >> 16;
         for (uint32_t u = 0; u < m; ++u) comp[dst + u] = L.ebuf[e0 + u];
+      }
+    }
+    __syncthreads();
+    // projection-chunk bookkeeping: the compact positions where each chunk's rows of this group start and end
+    if (base + rows > sg.lo) {
+      const uint32_t pa = max(base, sg.lo), pe = base + rows;
+      const uint32_t ja = L.rfirst / A.seg1, je = L.rlast / A.seg1;
+      for (uint32_t j = ja + t; j <= je; j += 256) {
+        const size_t gj = (size_t)g * A.ns1 + j;
+        const uint32_t p0 = A.o1[gj], p1 = A.o1[gj + 1];
+        if (p0 >= pa && p0 < pe) cst[gj] = sg.cb + cur + L.eoff[p0 - base];
+        if (p1 > pa && p1 <= pe)
+          cend[gj] = sg.cb + cur + L.eoff[p1 - 1 - base] + (L.aux[L.sslot[p1 - 1 - base]] & 0xffffu);
       }
     }
     cur += L.ttot;
@@ -416,12 +438,17 @@ static __global__ void __launch_bounds__(256) k_fgw_ctot(FgwArgs A, const uint32
 }
 
 // Projection: chunk j = virtual rows [j*seg1, (j+1)*seg1); its matches are output slots [cbase[j], cbase[j+1]).  The
-// chunk is ordered FGW_SUB arrival rows at a time: every group's entries in the chunk are in arrival order, so per
-// sub-chunk each group contributes the next entries from its cursor.
+// chunk is ordered FGW_SUB arrival rows at a time.  Every group's entries in the chunk are in arrival order, so a
+// sub-chunk takes from each group the entries before the sub-chunk's end (found by binary search from the group's
+// cursor); the groups' entry runs are concatenated and split evenly over the threads (contiguous blocks: coalesced
+// count-word reads), a block scan gives every entry its compact-record position, and the counts are placed by arrival
+// index in LDS, scanned, and the records written out contiguously.
 struct FgwProjLds {
   uint32_t cnt[FGW_SUB];        // per arrival index in the sub-chunk: matches (0: none / a row of no group)
   uint32_t src[FGW_SUB];        // per arrival index: first compact record
   uint32_t wsum[4];
+  uint32_t tot;
+  // followed by gst[ng + 1], gnext[ng], gbase[ng] (dynamic)
 };
 
 template <class T>
@@ -435,61 +462,137 @@ __global__ void __launch_bounds__(256) k_fgw_proj(FgwArgs A, WalkArgs a, Virt v,
                                                   char* __restrict__ out, uint32_t* __restrict__ flags_out) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   FgwProjLds& P = *(FgwProjLds*)lds_raw;
+  const uint32_t ng = A.ng;
+  uint32_t* gst = (uint32_t*)(lds_raw + sizeof(FgwProjLds));
+  uint32_t* gnext = gst + ng + 1;
+  uint32_t* gbase = gnext + ng;
   const uint32_t j = blockIdx.x, t = threadIdx.x;
   const int64_t r0 = (int64_t)j * A.seg1;
   const uint32_t rows = (uint32_t)min((int64_t)A.seg1, (int64_t)(v.nc + v.n) - r0);
-  // per group (threads own groups t, t + 256, ...): cursor into its range and its running compact position (the
-  // group's per-chunk state lives in global scratch, one slot per (chunk block, group): gcur / gsrc [j][g])
-  uint32_t* cur = gcur + (size_t)j * A.ng;
-  uint32_t* srcp = gsrc + (size_t)j * A.ng;
-  for (uint32_t g = t; g < A.ng; g += 256) {
+  // per-group cursor and running compact position (global scratch [j][g]: the chunk's own slots)
+  uint32_t* cur = gcur + (size_t)j * ng;
+  uint32_t* srcp = gsrc + (size_t)j * ng;
+  for (uint32_t g = t; g < ng; g += 256) {
     const size_t gj = (size_t)g * A.ns1 + j;
     cur[g] = A.o1[gj];
     srcp[g] = cst[gj];
   }
   uint32_t obase = cbase[j];
+  const bool one = rows <= (uint32_t)FGW_SUB;
   for (uint32_t s0 = 0; s0 < rows; s0 += FGW_SUB) {
     const uint32_t sn = min((uint32_t)FGW_SUB, rows - s0);
     for (uint32_t i = t; i < sn; i += 256) P.cnt[i] = 0;
     __syncthreads();
-    for (uint32_t g = t; g < A.ng; g += 256) {
+    // 1. each group's entries of this sub-chunk: [cur, next)
+    uint32_t mylen = 0;
+    const uint32_t gpt = (ng + 255) / 256;        // groups per thread (contiguous)
+    const uint32_t g0 = min(ng, t * gpt), g1 = min(ng, g0 + gpt);
+    for (uint32_t g = g0; g < g1; ++g) {
       const size_t gj = (size_t)g * A.ns1 + j;
-      const uint32_t e1 = A.o1[gj + 1];
-      uint32_t p = cur[g], sp = srcp[g];
-      while (p < e1) {
-        const uint32_t wv = gm32[p];
-        const uint32_t ai = wv & 0xffffu, m = wv >> 16;
-        if (ai >= s0 + sn) break;
-        if (ai < s0) { atomicOr(flags_out, FGW_F_INTERNAL); break; }
-        P.cnt[ai - s0] = m;
-        P.src[ai - s0] = sp;
-        sp += m;
-        ++p;
+      const uint32_t c = cur[g], e = A.o1[gj + 1];
+      uint32_t nx = e;
+      if (!one) {   // first entry whose arrival index is past the sub-chunk
+        uint32_t lo = c, hi = e;
+        while (lo < hi) {
+          const uint32_t mid = lo + ((hi - lo) >> 1);
+          if ((gm32[mid] & 0xffffu) < s0 + sn) lo = mid + 1; else hi = mid;
+        }
+        nx = lo;
       }
-      cur[g] = p;
-      srcp[g] = sp;
+      gnext[g] = nx;
+      mylen += nx - c;
+    }
+    {
+      const uint32_t ex = block_excl_scan256(mylen, P.wsum);
+      uint32_t run = ex;
+      for (uint32_t g = g0; g < g1; ++g) {
+        gst[g] = run;
+        run += gnext[g] - cur[g];
+      }
+      if (t == 255) gst[ng] = run;
     }
     __syncthreads();
-    // output offsets inside the sub-chunk (arrival order), then the records: one contiguous output range
-    const uint32_t per = (sn + 255) / 256;
-    const uint32_t c0 = min(sn, t * per), c1 = min(sn, c0 + per);
+    const uint32_t E = gst[ng];
+    const uint32_t per = (E + 255) / 256;
+    const uint32_t b0 = min(E, t * per), b1 = min(E, b0 + per);
+    auto group_of = [&](uint32_t e) {
+      uint32_t lo = 0, hi = ng;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (gst[mid] <= e) lo = mid; else hi = mid;
+      }
+      return lo;
+    };
+    // 2. matches of each thread's block, block scan -> prefix of every entry over the concatenation
+    uint32_t sm = 0;
+    {
+      uint32_t g = b0 < b1 ? group_of(b0) : 0;
+      for (uint32_t e = b0; e < b1; ++e) {
+        while (g + 1 < ng && gst[g + 1] <= e) ++g;
+        sm += gm32[cur[g] + (e - gst[g])] >> 16;
+      }
+    }
+    const uint32_t tx = block_excl_scan256(sm, P.wsum);
+    // 3. the thread holding a group's first entry records gbase = (group's compact position) - (prefix there)
+    {
+      uint32_t g = b0 < b1 ? group_of(b0) : 0, run = tx;
+      for (uint32_t e = b0; e < b1; ++e) {
+        while (g + 1 < ng && gst[g + 1] <= e) ++g;
+        if (e == gst[g]) gbase[g] = srcp[g] - run;
+        run += gm32[cur[g] + (e - gst[g])] >> 16;
+      }
+    }
+    __syncthreads();
+    // 4. place counts and compact positions by arrival index; the last entry of a group advances its cursors
+    {
+      uint32_t g = b0 < b1 ? group_of(b0) : 0, run = tx;
+      for (uint32_t e = b0; e < b1; ++e) {
+        while (g + 1 < ng && gst[g + 1] <= e) ++g;
+        const uint32_t wv = gm32[cur[g] + (e - gst[g])];
+        const uint32_t m = wv >> 16, ai = wv & 0xffffu;
+        if (ai < s0 || ai >= s0 + sn) {
+          atomicOr(flags_out, FGW_F_INTERNAL);
+        } else {
+          P.cnt[ai - s0] = m;
+          P.src[ai - s0] = gbase[g] + run;
+        }
+        run += m;
+        if (e + 1 == gst[g + 1]) srcp[g] = gbase[g] + run;   // (the group's running position for the next sub-chunk)
+      }
+    }
+    __syncthreads();
+    for (uint32_t g = g0; g < g1; ++g) cur[g] = gnext[g];
+    // 5. output offsets inside the sub-chunk (arrival order): each thread scans its block, then one lane per trigger,
+    //    lanes on consecutive triggers -- every wave gathers 64 triggers' rows at once and writes their records to
+    //    consecutive output slots
+    const uint32_t per2 = (sn + 255) / 256;
+    const uint32_t c0 = min(sn, t * per2), c1 = min(sn, c0 + per2);
     uint32_t sum = 0;
     for (uint32_t ai = c0; ai < c1; ++ai) sum += P.cnt[ai];
-    uint32_t run = block_excl_scan256(sum, P.wsum) + obase;
+    uint32_t run = block_excl_scan256(sum, P.wsum);
     const uint32_t sub_tot = P.wsum[0] + P.wsum[1] + P.wsum[2] + P.wsum[3];
-    for (uint32_t ai = c0; ai < c1; ++ai) {
+    for (uint32_t ai = c0; ai < c1; ++ai) {   // cnt[ai] <- output offset << 8 | matches (m < 256 checked)
       const uint32_t m = P.cnt[ai];
+      if (m > 255u) atomicOr(flags_out, FGW_F_INTERNAL);
+      P.cnt[ai] = (run << 8) | (m & 255u);
+      run += m;
+    }
+    __syncthreads();
+    for (uint32_t ai = t; ai < sn; ai += 256) {
+      const uint32_t cw = P.cnt[ai];
+      const uint32_t m = cw & 255u;
       if (!m) continue;
+      const uint32_t slot0 = obase + (cw >> 8);
       const int64_t rv = r0 + s0 + ai;           // virtual row of the trigger
       const int64_t b = rv - v.nc;               // batch row
-      if (b < 0) { atomicOr(flags_out, FGW_F_INTERNAL); run += m; continue; }
+      if (b < 0) { atomicOr(flags_out, FGW_F_INTERNAL); continue; }
       const uint32_t key = a.partitioned ? (uint32_t)v.key[b] : 0u;
       const int64_t t2 = v.ts[b];
       const uint64_t trig = a.index ? a.index[b] : a.base_index + (uint64_t)b;
       const uint32_t sb = P.src[ai];
       for (uint32_t u = 0; u < m; ++u) {
         const PtU4 cr = comp[sb + u];
-        int64_t* o = (int64_t*)(out + (size_t)(a.out_base + run + u) * a.stride);
+        int64_t* o = (int64_t*)(out + (size_t)(a.out_base + slot0 + u) * a.stride);
         uint32_t nm = 0;
         for (int s2 = 0; s2 < a.n_select; ++s2) {
           const bool src2 = pp.src[s2] != 0;
@@ -514,7 +617,6 @@ __global__ void __launch_bounds__(256) k_fgw_proj(FgwArgs A, WalkArgs a, Virt v,
         o[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (a.multi ? (uint32_t)a.b_slot : (0x800000u | u))) << 32));
         o[3] = (int64_t)nm;
       }
-      run += m;
     }
     obase += sub_tot;
     __syncthreads();

@@ -101,3 +101,60 @@ def sharded_oracle(query_text, batch, workers):
     cat = [np.concatenate([getattr(o, f) for o in outs]) for f in fields]
     order = np.argsort(cat[0], kind="stable")
     return Outputs(*[c[order] for c in cat])
+
+
+def _carried_worker(conn, query_text):
+    from oracle import OracleEngine
+    eng = OracleEngine(context(query_text))
+    while True:
+        msg = conn.recv()
+        if msg is None:
+            break
+        eng.push(msg)
+        o = eng.fetch()
+        conn.send(o)
+    eng.close()
+    conn.close()
+
+
+class CarriedShardedOracle:
+    """The oracle key-sharded over `workers` long-lived forked processes that keep their engine (and so every key's
+    partial matches) between pushes -- the streaming counterpart of sharded_oracle for a stream pushed in several
+    batches.  Each push is split by key, every shard keeps the rows' global event indices, and a stable merge by
+    trigger index gives the reference's delivery order for that push.  Test infrastructure only."""
+
+    def __init__(self, query_text, workers):
+        import multiprocessing as mp
+        ctx = mp.get_context("fork")
+        self.workers = workers
+        self.conns, self.procs = [], []
+        for _ in range(workers):
+            a, b = ctx.Pipe()
+            p = ctx.Process(target=_carried_worker, args=(b, query_text), daemon=True)
+            p.start()
+            b.close()
+            self.conns.append(a)
+            self.procs.append(p)
+
+    def push(self, batch):
+        for w, conn in enumerate(self.conns):
+            ix = np.nonzero((batch.key % self.workers) == w)[0]
+            idx = batch.index[ix] if batch.index is not None else (np.uint64(batch.base_index) + ix.astype(np.uint64))
+            conn.send(Batch(len(ix), 0, batch.ts[ix], batch.stream[ix], batch.key[ix], [c[ix] for c in batch.cols],
+                            [None if x is None else x[ix] for x in batch.nulls], index=idx))
+        outs = [conn.recv() for conn in self.conns]
+        fields = ("trigger", "ts", "key", "group", "vals", "vnull")
+        cat = [np.concatenate([getattr(o, f) for o in outs]) for f in fields]
+        order = np.argsort(cat[0], kind="stable")
+        return Outputs(*[c[order] for c in cat])
+
+    def close(self):
+        for conn in self.conns:
+            try:
+                conn.send(None)
+            except (BrokenPipeError, OSError):
+                pass
+        for p in self.procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()

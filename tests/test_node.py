@@ -188,43 +188,57 @@ def _first_seen_ids(keys, K):
 
 
 @pytest.mark.timeout(1100)
-def test_node_c5_300m_two_shards_three_pushes():
-    """BASELINE configs[4] through the node pipeline at scale: the first 300M events of the 1M-key C5 stream as
-    three 100M-event node pushes (key dictionary and per-key state carried between them) over two shards on
-    device 0 -- raw symbols routed on the host, chunked H2D / kernels / D2H per shard, native merge -- compared row
-    for row with the oracle run key-sharded over the host cores (parity_util.sharded_oracle)."""
+def test_node_c5_whole_1b_stream_ten_pushes():
+    """BASELINE configs[4] in full: the whole 1B-event, 1M-key C5 stream as ten 100M-event node pushes over two
+    shards on device 0 (raw symbols routed on the host, chunked H2D / kernels / D2H per shard, native merge; key
+    dictionary and per-key partial matches carried between pushes), every delivered row compared with the oracle
+    run key-sharded over the host cores with its engines -- and so its carried state -- kept across the same ten
+    pushes (parity_util.CarriedShardedOracle).  The workers fork before the first push; the rows of each push are
+    regenerated from the deterministic synth stream, so host memory stays at one push."""
     import os
-    from parity_util import sharded_oracle
-    cfg = "C5"
-    _, _, K, R = synth.CONFIGS[cfg]
-    n, pushes = 300_000_000, 3
-    g = synth.generate(cfg, 0, n, keys=K, rate=R)
-    raw = synth.raw_symbols(g["key"])
-    cols = [g["id"], None, g["price"]]
-    per = n // pushes
+    from parity_util import CarriedShardedOracle
     from siddhi_amd import _native as N
-    nfa = __import__("siddhi_amd.lowering", fromlist=["lower"]).lower(context(synth.QUERIES[cfg]))
+    cfg = "C5"
+    _, n, K, R = synth.CONFIGS[cfg]
+    pushes = 10
+    per = n // pushes
+    q = synth.QUERIES[cfg]
+    oracle = CarriedShardedOracle(q, max(2, min(16, os.cpu_count() or 2)))
+    nfa = __import__("siddhi_amd.lowering", fromlist=["lower"]).lower(context(q))
     node = N.Node(N.build_desc(nfa), n_gpus=2, devices=[0, 0], threads=16, chunk_rows=0)
-    outs = []
-    for p in range(pushes):
-        lo, hi = p * per, (p + 1) * per
-        keep = []
-        nb = N.make_node_batch(hi - lo, lo, g["ts"][lo:].ctypes.data, 0, raw[lo:].ctypes.data,
-                               [cols[0][lo:].ctypes.data, 0, cols[2][lo:].ctypes.data], [0, 0, 0], keep)
-        sink = N.ColumnSink(nfa, per // 2, pinned=False)
-        m = node.push(nb, sink.struct, sink.cap)
-        outs.append(node_outputs(nfa, sink, m))
-        del sink
-    assert node.keys() == K
-    node.close()
-    got = Outputs(*[np.concatenate([getattr(o, f) for o in outs]) for f in
-                    ("trigger", "ts", "key", "group", "vals", "vnull")])
-    del outs, raw
-    dense = _first_seen_ids(g["key"].astype(np.int64), K)
-    b = Batch(n, 0, g["ts"], np.zeros(n, np.int32), dense, [g["id"], g["key"], g["price"]], [None] * 3)
-    want = sharded_oracle(synth.QUERIES[cfg], b, max(2, min(16, os.cpu_count() or 2)))
-    assert len(got) == len(want) > 0
-    assert_same(got, want)
+    ids = np.full(K, -1, np.int64)   # first-seen dense id of every raw key so far (the node's dictionary order)
+    nxt, total = 0, 0
+    try:
+        for p in range(pushes):
+            lo = p * per
+            g = synth.generate(cfg, lo, per, keys=K, rate=R)
+            raw = synth.raw_symbols(g["key"])
+            keep = []
+            nb = N.make_node_batch(per, lo, g["ts"].ctypes.data, 0, raw.ctypes.data,
+                                   [g["id"].ctypes.data, 0, g["price"].ctypes.data], [0, 0, 0], keep)
+            sink = N.ColumnSink(nfa, per // 2, pinned=False)
+            m = node.push(nb, sink.struct, sink.cap)
+            got = node_outputs(nfa, sink, m)
+            del sink, raw
+            k64 = g["key"].astype(np.int64)
+            uniq, first = np.unique(k64, return_index=True)
+            new = ids[uniq] < 0
+            order = np.argsort(first[new], kind="stable")
+            ids[uniq[new][order]] = nxt + np.arange(int(new.sum()))
+            nxt += int(new.sum())
+            dense = ids[k64].astype(np.int32)
+            b = Batch(per, lo, g["ts"], np.zeros(per, np.int32), dense, [g["id"], g["key"], g["price"]], [None] * 3)
+            want = oracle.push(b)
+            del g, b, dense, k64
+            assert len(got) == len(want) > 0, (p, len(got), len(want))
+            assert_same(got, want)
+            total += len(got)
+            del got, want
+        assert node.keys() == K == nxt
+    finally:
+        oracle.close()
+        node.close()
+    assert total > 300_000_000   # (399,303,893 in the r03 whole-node bench line)
 
 
 @pytest.mark.timeout(300)
