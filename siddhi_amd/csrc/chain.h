@@ -49,6 +49,43 @@ struct PpTerm {
   int32_t fast;      // 1: both operands INT/LONG in the integral domain, 2: both FLOAT in the float domain, 0: SgVal path
 };
 
+SG_HD inline bool pp_cmp_i(int op, int64_t a, int64_t b) {
+  switch (op) {
+    case 0: return a == b;
+    case 1: return a != b;
+    case 2: return a > b;
+    case 3: return a >= b;
+    case 4: return a < b;
+    default: return a <= b;
+  }
+}
+SG_HD inline bool pp_cmp_f(int op, float a, float b) {
+  switch (op) {
+    case 0: return a == b;
+    case 1: return a != b;
+    case 2: return a > b;
+    case 3: return a >= b;
+    case 4: return a < b;
+    default: return a <= b;
+  }
+}
+SG_HD inline float pp_f32(int64_t bits) {
+  const uint32_t u = (uint32_t)bits;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// Wait skipping: a state whose filter is one fast compare of the arriving row's 4-byte attribute with an operand that
+// stays fixed while the partial waits there (a constant or another state's event).  See PpLane::wait_on.
+struct PpWait {
+  int32_t ok;
+  int32_t slot;      // retained slot of the arriving row's attribute (INT or FLOAT)
+  int32_t op;        // normalized: row OP fixed
+  int32_t fast;      // 1: integral domain, 2: float domain
+  int32_t other;     // the fixed operand: 0 term.r, 1 term.l
+};
+
 struct SgPpRule {
   int32_t ok;
   int32_t start;                      // the start state
@@ -59,6 +96,8 @@ struct SgPpRule {
   int32_t visit_rank[PP_MAX_S];       // state -> its slot in the receiver's visit order
   int32_t nterm[PP_MAX_S];            // -1: the VM evaluates the state's filter
   PpTerm term[PP_MAX_S][PP_MAX_TERMS];
+  PpWait wait[PP_MAX_S];
+  uint32_t wait_slots;                // retained slots some wait term reads (block summaries, partial.hip)
 };
 
 // Parse a postfix filter into conjunctive compare terms (t1 t2 AND t3 AND ...); false if it has another form.
@@ -106,6 +145,82 @@ SG_HD inline int pp_terms(const int64_t* c, int len, PpTerm* t) {
   return n;
 }
 
+// The wait terms of a rule (PpWait): state s (not the start) whose filter is exactly one fast term with one side the
+// arriving row's INT / FLOAT attribute (state s, index CURRENT = -1) and the other a constant or an event of another
+// state.
+SG_HD inline void pp_wait_rule(const sg_nfa_desc& d, SgPpRule& r) {
+  static const int32_t flip[6] = {0, 1, 4, 5, 2, 3};   // a OP b  <=>  b flip(OP) a
+  r.wait_slots = 0;
+  for (int s = 0; s < PP_MAX_S; ++s) r.wait[s].ok = 0;
+  for (int s = 0; s < d.n_states; ++s) {
+    if (s == r.start || r.nterm[s] != 1 || ((r.local_mask >> s) & 1u)) continue;
+    const PpTerm& t = r.term[s][0];
+    if (!t.fast || t.op < 0 || t.op > 5) continue;
+    const int want = t.fast == 1 ? SG_T_INT : SG_T_FLOAT;
+    auto is_row = [&](const PpOperand& o) { return o.kind == SG_OP_VAR && o.state == s && o.idx == -1 && o.type == want; };
+    auto fixed = [&](const PpOperand& o) { return o.kind == SG_OP_CONST || (o.kind == SG_OP_VAR && o.state != s); };
+    PpWait w;
+    w.ok = 0;
+    if (is_row(t.l) && fixed(t.r)) {
+      w.slot = t.l.slot;
+      w.op = t.op;
+      w.other = 0;
+    } else if (is_row(t.r) && fixed(t.l)) {
+      w.slot = t.r.slot;
+      w.op = flip[t.op];
+      w.other = 1;
+    } else {
+      continue;
+    }
+    if (w.slot < 0 || w.slot >= 32 || (t.fast == 2 && w.op == 1)) continue;   // (float `!=`: NaN rows pass it)
+    w.fast = t.fast;
+    w.ok = 1;
+    r.wait[s] = w;
+    r.wait_slots |= 1u << w.slot;
+  }
+}
+
+// Block summaries of a wait attribute: min and max of an orderable 32-bit encoding over 8 key-ordered rows.  FLOAT:
+// -0.0 is encoded as +0.0 (they compare equal) and NaN rows are left out (no compare but `!=` is true for them, and
+// float `!=` never waits).  An empty summary (min > max) holds no row that can pass.
+SG_HD inline uint32_t pp_wenc(uint32_t bits, int fast) {
+  if (fast == 1) return bits ^ 0x80000000u;
+  if (bits == 0x80000000u) bits = 0;
+  return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+}
+SG_HD inline bool pp_wnan(uint32_t bits, int fast) { return fast == 2 && (bits & 0x7fffffffu) > 0x7f800000u; }
+SG_HD inline int64_t pp_wdec_i(uint32_t e) { return (int64_t)(int32_t)(e ^ 0x80000000u); }
+SG_HD inline float pp_wdec_f(uint32_t e) {
+  const uint32_t u = (e & 0x80000000u) ? (e & 0x7fffffffu) : ~e;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+// can a row of the block pass `row OP c`?  (conservative: true unless no value in [min, max] passes)
+SG_HD inline bool pp_may_pass(uint32_t mn, uint32_t mx, int op, int fast, int64_t cbits) {
+  if (mn > mx) return false;
+  if (fast == 1) {
+    const int64_t lo = pp_wdec_i(mn), hi = pp_wdec_i(mx), c = cbits;
+    switch (op) {
+      case 0: return lo <= c && c <= hi;
+      case 1: return !(lo == hi && lo == c);
+      case 2: return hi > c;
+      case 3: return hi >= c;
+      case 4: return lo < c;
+      default: return lo <= c;
+    }
+  }
+  const float lo = pp_wdec_f(mn), hi = pp_wdec_f(mx), c = pp_f32(cbits);   // (c NaN: every compare is false)
+  switch (op) {
+    case 0: return lo <= c && c <= hi;
+    case 2: return hi > c;
+    case 3: return hi >= c;
+    case 4: return lo < c;
+    case 5: return lo <= c;
+    default: return true;
+  }
+}
+
 // Which queries may run as partial lanes (checked at lowering-independent level, on the flat descriptor).
 SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   SgPpRule r;
@@ -150,6 +265,7 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   if (starts != 1 || d.n_start != 1 || chain > PP_MAX_CHAIN || elems > PP_MAX_HIST) return r;
   r.n_hist = elems;
   r.ok = 1;
+  pp_wait_rule(d, r);
   return r;
 }
 
@@ -165,33 +281,6 @@ SG_HD inline int64_t pp_regress_tol(const sg_nfa_desc& d, bool has_count) { retu
 SG_HD inline int64_t pp_carry_window(const sg_nfa_desc& d, bool has_count) {
   const int64_t tol = pp_regress_tol(d, has_count);
   return d.within > INT64_MAX / 4 || tol > INT64_MAX / 4 ? d.within : d.within + tol;
-}
-
-SG_HD inline bool pp_cmp_i(int op, int64_t a, int64_t b) {
-  switch (op) {
-    case 0: return a == b;
-    case 1: return a != b;
-    case 2: return a > b;
-    case 3: return a >= b;
-    case 4: return a < b;
-    default: return a <= b;
-  }
-}
-SG_HD inline bool pp_cmp_f(int op, float a, float b) {
-  switch (op) {
-    case 0: return a == b;
-    case 1: return a != b;
-    case 2: return a > b;
-    case 3: return a >= b;
-    case 4: return a < b;
-    default: return a <= b;
-  }
-}
-SG_HD inline float pp_f32(int64_t bits) {
-  const uint32_t u = (uint32_t)bits;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
 }
 
 // Tie key of an emission: the insertion history newest first, 31 bits per component (row << 4 | visit slot), two
@@ -446,6 +535,37 @@ struct PpLane {
   }
   SG_HD bool get_any(int s) { return st(s).kind == SG_K_COUNT ? A->clen[s] > 0 : A->slot[s] >= 0; }
   SG_HD bool dead() const { return (l0 | l1) == 0; }
+
+  // Wait skipping.  While the partial's only live state s is a stream, count or logical state with a wait term
+  // (PpWait), an arriving row that fails the term changes nothing: step() binds the row (slot or chain append), the
+  // filter fails, and the binding is undone -- no post, no add_state, no emission; the flags it clears are rewritten
+  // before they are next read.  The one other effect, expiry, the caller checks on the row it lands on (a key's
+  // timestamps never decrease on this route, so a skipped row that had expired the partial means the landing row has
+  // too).  Not while the count state's successors hold the partial (step() would drop it from s) or a full chain, nor
+  // for an `or` state whose partner has matched, nor while the fixed operand is null.  Returns whether the partial
+  // waits, with the term `row.slot OP c`.
+  SG_HD bool wait_on(int& slot, int& op, int& fast, int64_t& cbits) {
+    if (l1 != 0 || l0 == 0 || (l0 & (l0 - 1u)) != 0) return false;
+    int s = 0;
+    while (!((l0 >> s) & 1u)) ++s;
+    if (s == ru->start || !ru->wait[s].ok) return false;
+    const sg_state_desc& x = st(s);
+    if (x.kind == SG_K_COUNT) {
+      if ((s + 1 < d->n_states && get_any(s + 1)) || (s + 2 < d->n_states && get_any(s + 2))) return false;
+      if (A->clen[s] >= x.max_count) return false;
+    } else if (x.kind == SG_K_LOGICAL && x.logical_type == 1 && A->slot[x.partner] >= 0) {
+      return false;
+    }
+    const PpWait& w = ru->wait[s];
+    const PpTerm& t = ru->term[s][0];
+    int null = 0;
+    operand_bits(w.other ? t.l : t.r, cbits, null);
+    if (null) return false;
+    slot = w.slot;
+    op = w.op;
+    fast = w.fast;
+    return true;
+  }
 
   // tie words of an emission (bit 63: partial lane)
   SG_HD void tie(uint64_t& hi, uint64_t& lo) const {

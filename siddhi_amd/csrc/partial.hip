@@ -219,6 +219,10 @@ struct PpPacked {
   const int64_t* cts;
   const void* bcol[SG_MAX_RET];
   const void* ccol[SG_MAX_RET];
+  // wait skipping (chain.h PpLane::wait_on): per wait attribute, {min, max} encodings of every 8 key-ordered rows
+  const uint2* wsum;            // nullptr: no skipping in this push (no wait term, or nulls in a column)
+  int64_t wnb;                  // 8-row blocks
+  int8_t wix[SG_MAX_RET];       // retained slot -> summary index
 };
 __device__ __forceinline__ int64_t pp_lazy_ts(const PpPacked* P, int64_t q) {
   const int64_t c = P->sid[q];
@@ -528,6 +532,39 @@ __global__ void k_pp_compact(int64_t m, const uint32_t* __restrict__ flag, const
   if (q < m && flag[q]) cand[pos[q]] = (uint32_t)q;
 }
 
+// Block summaries of the wait attributes (chain.h pp_wenc): one thread per 8 key-ordered rows and attribute.
+__global__ void k_pp_wsum(int64_t m, PpPacked P, uint32_t slots, uint32_t fslots, uint2* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P.wnb) return;
+  const int64_t q0 = b * 8;
+  const int nr = (int)(m - q0 < 8 ? m - q0 : 8);
+  for (int k = 0; k < SG_MAX_RET; ++k) {
+    if (!((slots >> k) & 1u)) continue;
+    const int fast = ((fslots >> k) & 1u) ? 2 : 1;
+    const uint32_t* v = (const uint32_t*)P.val[k] + q0;
+    uint32_t mn = 0xffffffffu, mx = 0;
+    if (nr == 8) {
+      const uint4 a = *(const uint4*)v, c = *(const uint4*)(v + 4);
+      const uint32_t x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (pp_wnan(x[i], fast)) continue;
+        const uint32_t e = pp_wenc(x[i], fast);
+        mn = e < mn ? e : mn;
+        mx = e > mx ? e : mx;
+      }
+    } else {
+      for (int i = 0; i < nr; ++i) {
+        if (pp_wnan(v[i], fast)) continue;
+        const uint32_t e = pp_wenc(v[i], fast);
+        mn = e < mn ? e : mn;
+        mx = e > mx ? e : mx;
+      }
+    }
+    out[(int64_t)P.wix[k] * P.wnb + b] = make_uint2(mn, mx);
+  }
+}
+
 constexpr int PP_BLOCK = 256;
 constexpr int64_t PP_WAVE_CANDS = 2048;   // start rows per wave
 template <class G>
@@ -583,6 +620,20 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   while (__ballot(active)) {
     bool done = false;
     if (active) {
+      // wait skipping: the 8-row blocks in which no row can pass the partial's wait term change nothing
+      // (PpLane::wait_on); at most 16 blocks per step, the row landed on is checked for expiry below
+      int ws, wop, wf;
+      int64_t wc;
+      if (pl.wsum && q < e && L.wait_on(ws, wop, wf, wc)) {
+        const uint2* S = pl.wsum + (int64_t)pl.wix[ws] * pl.wnb;
+        int64_t b = q >> 3;
+        const int64_t be = (e + 7) >> 3;
+        for (int lim = 0; lim < 16 && b < be; ++lim, ++b) {
+          const uint2 mm = S[b];
+          if (pp_may_pass(mm.x, mm.y, wop, wf, wc)) break;
+        }
+        if ((b << 3) > q) q = (b << 3) < e ? (b << 3) : e;
+      }
       if (q >= e || src.ts(q) - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
         done = true;
       } else {
@@ -1593,6 +1644,32 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   const int k1_bits = std::min(64, rb + 8);
   o.k1_none = k1_bits >= 64 ? ~0ull : (1ull << k1_bits) - 1;
   HIPCHK(hipMemsetAsync(o.count, 0, 16, st));
+  // wait-term block summaries (chain.h PpWait): only without nulls (a null row passes `!=`), 4-byte attributes
+  P.wsum = nullptr;
+  if (ps->rule.wait_slots && !P.nul && m > 0 && !getenv("SG_PP_NO_SKIP")) {
+    uint32_t slots = 0, fslots = 0;
+    int nw = 0;
+    for (int k = 0; k < SG_MAX_RET; ++k) P.wix[k] = -1;
+    for (int s = 0; s < d.n_states; ++s) {
+      const PpWait& w = ps->rule.wait[s];
+      if (!w.ok || w.slot >= d.n_ret || P.wide[w.slot] || !P.val[w.slot] || ((slots >> w.slot) & 1u)) continue;
+      slots |= 1u << w.slot;
+      if (w.fast == 2) fslots |= 1u << w.slot;
+      P.wix[w.slot] = (int8_t)nw++;
+    }
+    bool all = true;   // every wait term's attribute summarized (wait_on may return any of them)
+    for (int s = 0; s < d.n_states; ++s)
+      if (ps->rule.wait[s].ok && !((slots >> ps->rule.wait[s].slot) & 1u)) all = false;
+    if (nw && all) {
+      P.wnb = (m + 7) / 8;
+      uint2* ws = (uint2*)h->ws.get("pp_wsum", sizeof(uint2) * (size_t)nw * (size_t)P.wnb, st);
+      P.wsum = ws;
+      h->kbeg("wait_sum");
+      hipLaunchKernelGGL(k_pp_wsum, dim3((unsigned)((P.wnb + 255) / 256)), blk, 0, st, m, P, slots, fslots, ws);
+      HIPCHK(hipGetLastError());
+      h->kend();
+    }
+  }
   h->kbeg("partial_lanes");
   if (ncand) {
     const dim3 gl((unsigned)((ncand + PP_WAVE_CANDS * (PP_BLOCK / 64) - 1) / (PP_WAVE_CANDS * (PP_BLOCK / 64))));

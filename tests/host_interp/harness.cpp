@@ -29,7 +29,7 @@ struct HiHandle {
   std::vector<SeqState> seq_state;   // sequence lanes: per key (partial.hip's geometry choice: big ...)
   std::vector<SeqStateT<SqSmall>> seq_state_s;   // (... or small, sg_seq_small)
   int64_t spec_rows = 0, spec_warm = 0, spec_reruns = 0;   // speculative units (0: one run per key)
-  int64_t pp_steps = 0, pp_lanes = 0;                      // partial lanes: rows stepped, lanes started
+  int64_t pp_steps = 0, pp_lanes = 0, pp_skipped = 0;      // partial lanes: rows stepped, lanes started, rows skipped
 };
 
 struct HostRows {
@@ -174,6 +174,21 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
       for (size_t q = p + 1; q < rows.size(); ++q) {
         const int64_t c = rows[q];
         if (src.ts(c) - L.e1_ts > d.within) break;
+        {   // wait skipping (chain.h PpLane::wait_on): here every row the wait term rejects is skipped, the GPU skips
+            // whole 8-row blocks that cannot pass it
+          int ws, wop, wf;
+          int64_t wc;
+          if (L.wait_on(ws, wop, wf, wc)) {
+            int64_t rb;
+            int rn;
+            src.read_bits(c, ws, wf == 1 ? SG_T_INT : SG_T_FLOAT, rb, rn);
+            const bool pass = rn ? wop == 1 : (wf == 1 ? pp_cmp_i(wop, rb, wc) : pp_cmp_f(wop, pp_f32(rb), pp_f32(wc)));
+            if (!pass) {
+              ++h->pp_skipped;
+              continue;
+            }
+          }
+        }
         const int em = L.step(c);
         ++h->pp_steps;
         if (L.overflow) return -1;
@@ -395,6 +410,7 @@ void hi_set_pp(HiHandle* h, int on) { h->pp = on; }
 void hi_set_spec(HiHandle* h, int64_t rows, int64_t warm) { h->spec_rows = rows; h->spec_warm = warm; }
 int64_t hi_spec_reruns(HiHandle* h) { return h->spec_reruns; }
 int64_t hi_pp_steps(HiHandle* h, int64_t* lanes) { *lanes = h->pp_lanes; return h->pp_steps; }
+int64_t hi_pp_skipped(HiHandle* h) { return h->pp_skipped; }
 int hi_seq_rule(const sg_nfa_desc* d) { return sg_seq_rule(*d).ok; }
 int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
 

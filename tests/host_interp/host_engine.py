@@ -47,6 +47,10 @@ def _load():
         lib.hi_set_spec.argtypes = [P, ct.c_int64, ct.c_int64]
         lib.hi_spec_reruns.restype = ct.c_int64
         lib.hi_spec_reruns.argtypes = [P]
+        lib.hi_pp_skipped.restype = ct.c_int64
+        lib.hi_pp_skipped.argtypes = [P]
+        lib.hi_pp_steps.restype = ct.c_int64
+        lib.hi_pp_steps.argtypes = [P, P]
         _lib = lib
     return _lib
 
@@ -102,6 +106,12 @@ class HostInterpEngine:
 
     def reruns(self):
         return self.lib.hi_spec_reruns(self.h)
+
+    def pp_counts(self):
+        """partial lanes: (rows stepped, rows skipped by wait terms, lanes started)"""
+        lanes = ct.c_int64(0)
+        steps = self.lib.hi_pp_steps(self.h, ct.byref(lanes))
+        return steps, self.lib.hi_pp_skipped(self.h), lanes.value
 
     def close(self):
         if self.h:
