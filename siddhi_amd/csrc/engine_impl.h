@@ -2106,10 +2106,13 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
   seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
   const dim3 pgrd((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32));
-  // fused group walk (fgw.h): no key-sorted copy, one walk, arrival-ordered projection
+  // fused group walk (fgw.h): no key-sorted copy, one walk, arrival-ordered projection.  Opt-in (SG_FGW=1): measured
+  // slower than the sorted-walker pipeline on C2 (k_fgw 7.2 + k_fgw_proj 9.9 ms against 7.6 ms for the whole pipeline,
+  // profiles/r04/C2_fgw_v2_kernel_stats.csv) -- kept, parity-tested, as the base of a later attempt
   if constexpr (N && sizeof(T) == 4) {
-    static const bool fgw_off = getenv("SG_NO_FGW") != nullptr;   // (experiments: the sorted-walker pipeline)
-    if (d.partitioned && h->opt.partition_sort == 0 && !h->opt.walker_only && !fgw_off && n > 0) {
+    const char* fgw_env = getenv("SG_FGW");
+    const bool fgw_on = fgw_env && fgw_env[0] == '1';
+    if (d.partitioned && h->opt.partition_sort == 0 && !h->opt.walker_only && fgw_on && n > 0) {
       int64_t tfl[2] = {0, 0};
       HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, sizeof(int64_t), hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));

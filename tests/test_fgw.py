@@ -58,8 +58,14 @@ def pieces(b, cuts):
     return out
 
 
+@pytest.fixture(autouse=True)
+def fused_walk_on(monkeypatch):
+    """the fused walk is opt-in (SG_FGW=1, read per push): these tests switch it on"""
+    monkeypatch.setenv("SG_FGW", "1")
+
+
 def both(q, batches, **kw):
-    """the route lowering picks (the fused walk where it applies) and the sorted walker, both against the oracle"""
+    """the fused walk (SG_FGW=1) and the sorted walker (partition_sort = 1), both against the oracle"""
     from siddhi_amd._native import GpuEngine
     want = run_engine(OracleEngine, q, batches)
     assert len(want) > 0
