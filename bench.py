@@ -339,7 +339,7 @@ PATH_BYTES = {"C1": (12.125, 36.0, 4.125), "C2": (16.125, 36.0, 4.125), "C5": (1
 KERNEL_BYTES = {"pred": (4.125, 0.0), "part_hist": (4.0, 0.0), "part_group": (41.125, 0.0),
                 "fgw_walk": (21.0, 16.0), "fgw_project": (4.0, 104.0), "part_key": (33.0, 0.0),
                 "tile_transpose": (32.0, 0.0), "walk_count": (16.0, 4.0), "walk_record": (16.0, 16.0),
-                "project": (0.0, 104.0), "key_sort": (120.0, 0.0), "pack": (44.125, 0.0),
+                "project": (0.0, 104.0), "key_sort": (40.0, 0.0), "pack": (44.125, 0.0), "part_split": (35.0, 0.0),
                 "nge_search": (12.125, 8.0), "once_match": (16.125, 0.0)}
 
 

@@ -1365,6 +1365,75 @@ __global__ void k_carry_copy(Src<T, N> src, uint32_t K, uint32_t ncar, const uin
   }
 }
 
+// Carry by arrival order: a virtual row survives into the next push iff its key's last row is within `within` of it
+// (the rows lb_ts finds per key in the record walk: sorted positions [carry_q0, seg_e)).  Those positions mark their
+// arrival rows in a bitmask (one lane per key), a count per 8192-row block and a scan place every survivor, and the
+// survivors are copied in arrival order -- reads of the row columns are near-coalesced (the survivors are mostly the
+// push's last `within` of rows) instead of one random gather per column per row; per-key order stays arrival order,
+// which is all the next push's stable key partition needs.
+template <class T, bool N>
+__global__ void k_carry_mark(Src<T, N> src, uint32_t K, const uint32_t* __restrict__ q0s,
+                             const uint32_t* __restrict__ cn, uint32_t* __restrict__ bits) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const uint32_t q0 = q0s[k], c = cn[k];
+  for (uint32_t i = 0; i < c; ++i) {
+    const uint32_t r = src.row(q0 + i);
+    atomicOr(&bits[r >> 5], 1u << (r & 31));
+  }
+}
+
+static const int CARRY_BLK = 8192;   // rows per block of the survivor count (256 bitmask words)
+
+static __global__ void __launch_bounds__(256) k_carry_bcount(int64_t nt, const uint32_t* __restrict__ bits,
+                                                             uint32_t* __restrict__ bcnt) {
+  __shared__ uint32_t red[4];
+  const int64_t wi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t c = wi * 32 < nt ? (uint32_t)__popc(bits[wi]) : 0u;
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+static __global__ void __launch_bounds__(256) k_carry_gather(Virt v, int64_t nt, const uint32_t* __restrict__ bits,
+                                                             const uint32_t* __restrict__ boff, int n_cols,
+                                                             const int32_t* __restrict__ widths, SgCols bc, SgCols cc,
+                                                             CarryBufs dst) {
+  // 256 consecutive rows per step, one per thread: survivors of a step get consecutive slots (coalesced stores)
+  __shared__ uint32_t wc[2][4];
+  const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
+  uint32_t base_d = boff[blockIdx.x];
+  const int64_t r0 = (int64_t)blockIdx.x * CARRY_BLK;
+  for (int step = 0; step < CARRY_BLK / 256; ++step) {
+    const int64_t r64 = r0 + step * 256 + t;
+    const bool live = r64 < nt && ((bits[r64 >> 5] >> (r64 & 31)) & 1u);
+    const uint64_t m = __ballot(live);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) wc[step & 1][w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t q = 0; q < w; ++q) before += wc[step & 1][q];
+    const uint32_t tot = wc[step & 1][0] + wc[step & 1][1] + wc[step & 1][2] + wc[step & 1][3];
+    if (live) {
+      const uint32_t d = base_d + before + below;
+      const uint32_t r = (uint32_t)r64;
+      dst.ts[d] = v_ts(v, r);
+      dst.key[d] = r < v.nc ? v.c_key[r] : (v.key ? v.key[r - v.nc] : 0);
+      dst.flags[d] = (uint8_t)v_flags(v, r);
+      const SgCols& s = r < v.nc ? cc : bc;
+      const uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
+      for (int c = 0; c < n_cols; ++c) {
+        if (!s.col[c]) continue;
+        if (widths[c] == 8) ((int64_t*)dst.col[c])[d] = ((const int64_t*)s.col[c])[rr];
+        else ((int32_t*)dst.col[c])[d] = ((const int32_t*)s.col[c])[rr];
+        dst.nul[c][d] = s.nul[c] ? s.nul[c][rr] : 0;
+      }
+    }
+    base_d += tot;
+  }
+}
+
 // ----------------------------------------------------------------------------------------------
 struct CarrySet {
   int64_t n = 0, cap = 0;
@@ -1737,6 +1806,76 @@ static void launch_fgw(int op, unsigned grid, size_t lds, hipStream_t st, const 
   HIPCHK(hipGetLastError());
 }
 
+// Pass 1 of the key partition beyond 256 key groups (up to 4096 groups of 2^pp.lb keys, e.g. C5's 1M keys): rows ->
+// narrow walker records grouped by key group, arrival order kept inside a group, in two LDS counting passes --
+// supergroups of 2^lbs groups (<= 256 of them, k_part1 with 32-bit staged keys), then the groups inside each
+// supergroup (k_part1b) straight into the group positions o1[g * ns1 + j] of the per-(group, segment) histogram.
+// Output: grec, glk (in-group key), o1.
+template <class T>
+static void part1_wide(SgHandle* h, const PackFn<T, true>& pk, KeyOf kf, uint32_t kb, int64_t nt, const PartPlan& pp,
+                       uint32_t* h1, uint32_t* o1, WRec<T, true>* grec, uint8_t* glk, uint32_t* pk_flags) {
+  typedef WRec<T, true> R;
+  hipStream_t st = h->stream;
+  const uint32_t lb = pp.lb, ng = pp.ng;
+  const size_t n1 = (size_t)pp.ng * pp.ns1 + 1;
+  auto scan_u32 = [&](const uint32_t* in, uint32_t* outp, size_t cnt, const char* tmpname) {
+    size_t b = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, b, in, outp, (uint32_t)0, cnt, rocprim::plus<uint32_t>(), st));
+    void* tp = h->ws.get(tmpname, b, st);
+    HIPCHK(rocprim::exclusive_scan(tp, b, in, outp, (uint32_t)0, cnt, rocprim::plus<uint32_t>(), st));
+  };
+  {
+    // two passes: supergroups of 2^lbs groups (<= 256 of them), then groups inside each supergroup
+    uint32_t lbs = 0;
+    while ((ng >> lbs) > 256u || ((ng + (1u << lbs) - 1) >> lbs) > 256u) ++lbs;
+    PartPlan pa2 = pp;
+    pa2.lb = lb + lbs;
+    pa2.ng = (kb + (1u << pa2.lb) - 1) >> pa2.lb;
+    uint32_t nbA = 0;
+    while ((1u << nbA) < pa2.ng) ++nbA;
+    pa2.nb1 = nbA;
+    const size_t nA = (size_t)pa2.ng * pp.ns1 + 1;
+    uint32_t* hA = (uint32_t*)h->ws.get("part_hA", sizeof(uint32_t) * nA, st);
+    uint32_t* oA = (uint32_t*)h->ws.get("part_oA", sizeof(uint32_t) * nA, st);
+    R* grecA = (R*)h->ws.get("grecA", sizeof(R) * nt, st);
+    uint16_t* glkA = (uint16_t*)h->ws.get("glkA", 2 * nt, st);
+    h->kbeg("part_hist");
+    HIPCHK(hipMemsetAsync(hA + nA - 1, 0, sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pa2, nt, hA, pk_flags);
+    hipLaunchKernelGGL(k_hist_wide, dim3(pp.ns1), dim3(256), 0, st, kf, kb, lb, ng, pp.seg1, pp.ns1, nt, h1, pk_flags);
+    HIPCHK(hipGetLastError());
+    scan_u32(hA, oA, nA, "part_scan_tmpA");
+    scan_u32(h1, o1, n1, "part_scan_tmp");
+    h->kend();
+    h->kbeg("part_group");
+    const size_t ldsA = sizeof(PartLds<R, PT1, uint32_t>);
+    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, true, uint32_t, uint16_t>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsA));
+    hipLaunchKernelGGL((k_part1<T, true, uint32_t, uint16_t>), dim3(pp.ns1), dim3(256), ldsA, st, pk, kf, pa2, nt, oA,
+                       grecA, glkA, pk_flags);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->kbeg("part_split");
+    Part1bArgs B;
+    B.lb = lb;
+    B.lbs = lbs;
+    B.ns1 = pp.ns1;
+    const int64_t per_sg = std::max<int64_t>(1, nt / pa2.ng);
+    B.nsb = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, per_sg / 32768));
+    B.tsb = (pp.ns1 + B.nsb - 1) / B.nsb;
+    B.nsb = (pp.ns1 + B.tsb - 1) / B.tsb;
+    B.oa = oA;
+    B.o1 = o1;
+    const size_t ldsB = sizeof(Part1bLds<16>);
+    HIPCHK(hipFuncSetAttribute((const void*)k_part1b<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsB));
+    hipLaunchKernelGGL((k_part1b<16>), dim3(pa2.ng * B.nsb), dim3(256), ldsB, st, B, (const PtU4*)grecA, glkA,
+                       (PtU4*)grec, glk, (uint32_t)nt, pk_flags);
+    HIPCHK(hipGetLastError());
+    h->kend();
+  }
+}
+
 // The fused group walk (fgw.h) for one push.  Returns 1 when the push is done, 0 when a precondition failed on the
 // GPU (nothing was changed: the caller runs the sorted-walker pipeline), -1 when narrow records cannot represent the
 // push (the caller falls back to wide records).
@@ -1801,54 +1940,7 @@ static int run_fgw(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& 
     HIPCHK(hipGetLastError());
     h->kend();
   } else {
-    // two passes: supergroups of 2^lbs groups (<= 256 of them), then groups inside each supergroup
-    uint32_t lbs = 0;
-    while ((ng >> lbs) > 256u || ((ng + (1u << lbs) - 1) >> lbs) > 256u) ++lbs;
-    PartPlan pa2 = pp;
-    pa2.lb = lb + lbs;
-    pa2.ng = (kb + (1u << pa2.lb) - 1) >> pa2.lb;
-    uint32_t nbA = 0;
-    while ((1u << nbA) < pa2.ng) ++nbA;
-    pa2.nb1 = nbA;
-    const size_t nA = (size_t)pa2.ng * pp.ns1 + 1;
-    uint32_t* hA = (uint32_t*)h->ws.get("part_hA", sizeof(uint32_t) * nA, st);
-    uint32_t* oA = (uint32_t*)h->ws.get("part_oA", sizeof(uint32_t) * nA, st);
-    R* grecA = (R*)h->ws.get("grecA", sizeof(R) * nt, st);
-    uint16_t* glkA = (uint16_t*)h->ws.get("glkA", 2 * nt, st);
-    h->kbeg("part_hist");
-    HIPCHK(hipMemsetAsync(hA + nA - 1, 0, sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pa2, nt, hA, pk_flags);
-    hipLaunchKernelGGL(k_hist_wide, dim3(pp.ns1), dim3(256), 0, st, kf, kb, lb, ng, pp.seg1, pp.ns1, nt, h1, pk_flags);
-    HIPCHK(hipGetLastError());
-    scan_u32(hA, oA, nA, "part_scan_tmpA");
-    scan_u32(h1, o1, n1, "part_scan_tmp");
-    h->kend();
-    h->kbeg("part_group");
-    const size_t ldsA = sizeof(PartLds<R, PT1, uint32_t>);
-    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, true, uint32_t, uint16_t>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsA));
-    hipLaunchKernelGGL((k_part1<T, true, uint32_t, uint16_t>), dim3(pp.ns1), dim3(256), ldsA, st, pk, kf, pa2, nt, oA,
-                       grecA, glkA, pk_flags);
-    HIPCHK(hipGetLastError());
-    h->kend();
-    h->kbeg("part_split");
-    Part1bArgs B;
-    B.lb = lb;
-    B.lbs = lbs;
-    B.ns1 = pp.ns1;
-    const int64_t per_sg = std::max<int64_t>(1, nt / pa2.ng);
-    B.nsb = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, per_sg / 32768));
-    B.tsb = (pp.ns1 + B.nsb - 1) / B.nsb;
-    B.nsb = (pp.ns1 + B.tsb - 1) / B.tsb;
-    B.oa = oA;
-    B.o1 = o1;
-    const size_t ldsB = sizeof(Part1bLds<16>);
-    HIPCHK(hipFuncSetAttribute((const void*)k_part1b<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsB));
-    hipLaunchKernelGGL((k_part1b<16>), dim3(pa2.ng * B.nsb), dim3(256), ldsB, st, B, (const PtU4*)grecA, glkA,
-                       (PtU4*)grec, glk, (uint32_t)nt, pk_flags);
-    HIPCHK(hipGetLastError());
-    h->kend();
+    part1_wide<T>(h, pk, kf, kb, nt, pp, h1, o1, grec, glk, pk_flags);
   }
   uint32_t pkf = 0;
   HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -2143,9 +2235,23 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       }
     }
   }
-  const bool lds_part = d.partitioned && kb <= 65536u && h->opt.partition_sort == 0;
+  // beyond 65536 keys (C5: 1M per GPU) the LDS partition runs its first pass in two (part1_wide: narrow records only,
+  // up to 4096 groups of 256 keys) -- three counting passes in place of pack + a 3-pass onesweep sort + bounds
+  const bool wide_part = N && sizeof(R) == 16 && sizeof(T) == 4 && kb > 65536u && kb <= (4096u << 8) &&
+                         !getenv("SG_NO_WIDE_PART");
+  const bool lds_part = d.partitioned && (kb <= 65536u || wide_part) && h->opt.partition_sort == 0;
   if (lds_part) {
-    const PartPlan pp = part_plan(kb, nt);
+    PartPlan pp = part_plan(kb, nt);
+    if (kb > 65536u) {   // groups of 256 keys: pass 2 sorts by the low 8 bits
+      pp.two = 1;
+      pp.lb = 8;
+      pp.ng = (kb + 255u) >> 8;
+      pp.nb1 = 0;
+      while ((1u << pp.nb1) < pp.ng) ++pp.nb1;
+      pp.nb2 = 8;
+      pp.ts2 = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, (int64_t)8192 * pp.ng / pp.seg1));
+      pp.nj = (pp.ns1 + pp.ts2 - 1) / pp.ts2;
+    }
     KeyOf kf{bv.key, cs.key, (uint32_t)nc};
     const size_t n1 = (size_t)pp.ng * pp.ns1 + 1;
     uint32_t* h1 = (uint32_t*)h->ws.get("part_h1", sizeof(uint32_t) * n1, st);
@@ -2156,15 +2262,18 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     const size_t lds1 = sizeof(PartLds<R, PT1>), lds2 = sizeof(PartLds<RW, PT2>);
     HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
     HIPCHK(hipFuncSetAttribute((const void*)k_part2<RW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
-    h->kbeg("part_hist");
-    HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pp, nt, h1, pk_flags);
-    HIPCHK(hipGetLastError());
     size_t tb = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, tb, h1, o1, (uint32_t)0, n1, rocprim::plus<uint32_t>(), st));
-    void* tmp = h->ws.get("part_scan_tmp", tb, st);
-    HIPCHK(rocprim::exclusive_scan(tmp, tb, h1, o1, (uint32_t)0, n1, rocprim::plus<uint32_t>(), st));
-    h->kend();
+    void* tmp = nullptr;
+    if (kb <= 65536u) {
+      h->kbeg("part_hist");
+      HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
+      hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pp, nt, h1, pk_flags);
+      HIPCHK(hipGetLastError());
+      HIPCHK(rocprim::exclusive_scan(nullptr, tb, h1, o1, (uint32_t)0, n1, rocprim::plus<uint32_t>(), st));
+      tmp = h->ws.get("part_scan_tmp", tb, st);
+      HIPCHK(rocprim::exclusive_scan(tmp, tb, h1, o1, (uint32_t)0, n1, rocprim::plus<uint32_t>(), st));
+      h->kend();
+    }
     if (!pp.two) {
       h->kbeg("part_scatter");
       hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds1, st, src.pk, kf, pp, nt, o1, srec, (uint8_t*)nullptr,
@@ -2178,10 +2287,15 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       const size_t n2 = ((size_t)pp.ng << pp.lb) * pp.nj + 1;
       uint32_t* h2 = (uint32_t*)h->ws.get("part_h2", sizeof(uint32_t) * n2, st);
       uint32_t* o2 = (uint32_t*)h->ws.get("part_o2", sizeof(uint32_t) * n2, st);
-      h->kbeg("part_group");
-      hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds1, st, src.pk, kf, pp, nt, o1, grec, glk, pk_flags);
-      HIPCHK(hipGetLastError());
-      h->kend();
+      if (kb > 65536u) {
+        if constexpr (N && sizeof(R) == 16 && sizeof(T) == 4)
+          part1_wide<T>(h, src.pk, kf, kb, nt, pp, h1, o1, grec, glk, pk_flags);
+      } else {
+        h->kbeg("part_group");
+        hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds1, st, src.pk, kf, pp, nt, o1, grec, glk, pk_flags);
+        HIPCHK(hipGetLastError());
+        h->kend();
+      }
       h->kbeg("part_hist2");
       HIPCHK(hipMemsetAsync(h2 + n2 - 1, 0, sizeof(uint32_t), st));
       hipLaunchKernelGGL(k_part2_hist, dim3(pp.ng * pp.nj), dim3(256), 0, st, pp, o1, glk, h2);
@@ -2426,13 +2540,38 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
 
   // ---- 6. carry into the next push
   if (wa.carry_out) {
+    static const bool by_key = getenv("SG_CARRY_BY_KEY") != nullptr;   // (experiments: the per-key copy)
     uint32_t* coff = (uint32_t*)h->ws.get("carry_off", sizeof(uint32_t) * (K + 1), st);
-    size_t tb = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
-    void* tmp = h->ws.get("carry_scan_tmp", tb, st);
-    HIPCHK(rocprim::exclusive_scan(tmp, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t* cbits = nullptr;
+    uint32_t* cboff = nullptr;
+    uint32_t* ccount = (uint32_t*)h->ws.get("carry_count", sizeof(uint32_t), st);
+    if (by_key) {
+      size_t tb = 0;
+      HIPCHK(rocprim::exclusive_scan(nullptr, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
+      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
+      HIPCHK(rocprim::exclusive_scan(tmp, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
+      HIPCHK(hipMemcpyAsync(ccount, coff + K, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    } else {
+      h->kbeg("carry");
+      const int64_t nw = (nt + 31) / 32, nb = (nt + CARRY_BLK - 1) / CARRY_BLK;
+      cbits = (uint32_t*)h->ws.get("carry_bits", sizeof(uint32_t) * (size_t)(nb * 256), st);
+      cboff = (uint32_t*)h->ws.get("carry_boff", sizeof(uint32_t) * (size_t)(nb + 1), st);
+      uint32_t* bcnt = (uint32_t*)h->ws.get("carry_bcnt", sizeof(uint32_t) * (size_t)(nb + 1), st);
+      HIPCHK(hipMemsetAsync(cbits, 0, sizeof(uint32_t) * (size_t)(nb * 256), st));
+      hipLaunchKernelGGL((k_carry_mark<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n, cbits);
+      hipLaunchKernelGGL(k_carry_bcount, dim3((unsigned)nb), dim3(256), 0, st, nt, cbits, bcnt);
+      HIPCHK(hipMemsetAsync(bcnt + nb, 0, sizeof(uint32_t), st));
+      HIPCHK(hipGetLastError());
+      size_t tb = 0;
+      HIPCHK(rocprim::exclusive_scan(nullptr, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
+      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
+      HIPCHK(rocprim::exclusive_scan(tmp, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
+      HIPCHK(hipMemcpyAsync(ccount, cboff + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+      (void)nw;
+      h->kend();
+    }
     uint32_t ncar = 0, guard = 0;
-    HIPCHK(hipMemcpyAsync(&ncar, coff + K, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&ncar, ccount, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&guard, &wst->internal, sizeof(uint32_t), hipMemcpyDeviceToHost, st));   // record-pass guards
     HIPCHK(hipStreamSynchronize(st));
     if (guard) throw SgError(SG_EINVAL, "internal: record-pass guard tripped (" + std::to_string(guard) + ")");
@@ -2449,9 +2588,12 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     cb.key = nx.key;
     cb.flags = nx.flags;
     for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
-    if (ncar)
+    if (ncar && by_key)
       hipLaunchKernelGGL((k_carry_copy<T, N>), dim3((ncar + 255) / 256), dim3(256), 0, st, src, K, ncar, carry_q0,
                          coff, d.n_cols, widths, bv.cols, cc, cb);
+    else if (ncar)
+      hipLaunchKernelGGL(k_carry_gather, dim3((unsigned)((nt + CARRY_BLK - 1) / CARRY_BLK)), dim3(256), 0, st, v, nt,
+                         cbits, cboff, d.n_cols, widths, bv.cols, cc, cb);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
     nx.n = ncar;

@@ -358,6 +358,7 @@ struct Run {
   std::vector<int64_t> ts_base_of;
   std::vector<uint8_t> ts32_of;
   std::vector<std::vector<uint32_t>> newf_of;
+  std::vector<uint8_t> shard_tmp;            // device-dictionary route, G > 1: each row's shard (0xff: every shard)
   double t_route = 0, t_merge = 0, t_gpu[MAX_GPUS] = {};
   int64_t h2d_bytes = 0, d2h_bytes = 0;
 
@@ -469,7 +470,11 @@ void route_chunk_dev(Run& r, int64_t j) {
   auto shard = [&](int64_t i) -> int {
     return (stream && stream[i] < 0) ? -1 : (int)(sgr::mix64((uint64_t)raw[i]) % (uint64_t)G);
   };
+  // pass 1: each row's shard (0xff: a clock-only row every shard gets) and the counts per (thread slice, shard)
+  std::vector<uint8_t>& sh = r.shard_tmp;
+  if ((int64_t)sh.size() < n) sh.resize((size_t)n);
   std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(G, 0));
+  std::vector<int64_t> nbc(T, 0);
   nd.pool->parallel_for(T, [&](int t) {
     int64_t a, e;
     slice(t, a, e);
@@ -477,10 +482,12 @@ void route_chunk_dev(Run& r, int64_t j) {
     int64_t bcast = 0;
     for (int64_t i = a; i < e; ++i) {
       const int x = shard(i);
+      sh[(size_t)i] = x >= 0 ? (uint8_t)x : (uint8_t)0xff;
       if (x >= 0) ++c[x];
       else ++bcast;
     }
     for (int q = 0; q < G; ++q) c[q] += bcast;
+    nbc[t] = bcast;
   });
   std::vector<std::vector<int64_t>> off(T, std::vector<int64_t>(G, 0));
   for (int q = 0; q < G; ++q) {
@@ -494,27 +501,87 @@ void route_chunk_dev(Run& r, int64_t j) {
   const int nc = d.n_cols;
   int need[SG_MAX_COLS] = {};
   for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
+  const uint8_t* shp = sh.data();
+  // pass 2: column by column, each a tight loop over the slice's rows into the G shard streams (arrival order kept)
   nd.pool->parallel_for(T, [&](int t) {
     int64_t a, e;
     slice(t, a, e);
-    int64_t cur[MAX_GPUS];
-    for (int q = 0; q < G; ++q) cur[q] = off[t][q];
-    for (int64_t i = a; i < e; ++i) {
-      const int own = shard(i);
-      for (int q = 0; q < G; ++q) {
-        if (own >= 0 && q != own) continue;
-        NodeStage& S = nd.stage[slot][q];
-        const int64_t p = cur[q]++;
-        put_ts(r, S, j, p, r.b.ts[lo + i]);
-        S.raw.as<int64_t>()[p] = raw[i];
-        if (stream) S.stream.as<int32_t>()[p] = stream[i];
-        S.gidx.as<uint64_t>()[p] = r.b.base_index + (uint64_t)(lo + i);
-        for (int c = 0; c < nc; ++c) {
-          if (!need[c] || !r.b.cols[c]) continue;
-          if (sg_col_width(d.col_type[c]) == 8) S.col[c].as<int64_t>()[p] = ((const int64_t*)r.b.cols[c])[lo + i];
-          else S.col[c].as<int32_t>()[p] = ((const int32_t*)r.b.cols[c])[lo + i];
-          if (r.b.nulls && r.b.nulls[c]) S.nul[c].as<uint8_t>()[p] = r.b.nulls[c][lo + i];
+    if (nbc[t]) {   // a slice with clock-only rows: row by row, those rows to every shard
+      int64_t cur[MAX_GPUS];
+      for (int q = 0; q < G; ++q) cur[q] = off[t][q];
+      for (int64_t i = a; i < e; ++i) {
+        const int own = shp[i] == 0xff ? -1 : (int)shp[i];
+        for (int q = 0; q < G; ++q) {
+          if (own >= 0 && q != own) continue;
+          NodeStage& S = nd.stage[slot][q];
+          const int64_t p = cur[q]++;
+          put_ts(r, S, j, p, r.b.ts[lo + i]);
+          S.raw.as<int64_t>()[p] = raw[i];
+          if (stream) S.stream.as<int32_t>()[p] = stream[i];
+          S.gidx.as<uint64_t>()[p] = r.b.base_index + (uint64_t)(lo + i);
+          for (int c = 0; c < nc; ++c) {
+            if (!need[c] || !r.b.cols[c]) continue;
+            if (sg_col_width(d.col_type[c]) == 8) S.col[c].as<int64_t>()[p] = ((const int64_t*)r.b.cols[c])[lo + i];
+            else S.col[c].as<int32_t>()[p] = ((const int32_t*)r.b.cols[c])[lo + i];
+            if (r.b.nulls && r.b.nulls[c]) S.nul[c].as<uint8_t>()[p] = r.b.nulls[c][lo + i];
+          }
         }
+      }
+      return;
+    }
+    auto scatter = [&](auto* const* dst, auto val) {
+      int64_t cur[MAX_GPUS];
+      for (int q = 0; q < G; ++q) cur[q] = off[t][q];
+      for (int64_t i = a; i < e; ++i) {
+        const int q = shp[i];
+        dst[q][cur[q]++] = val(i);
+      }
+    };
+    const int64_t* ts = r.b.ts + lo;
+    if (r.ts32_of[j]) {
+      int32_t* dt[MAX_GPUS];
+      for (int q = 0; q < G; ++q) dt[q] = nd.stage[slot][q].ts32.as<int32_t>();
+      const int64_t tb = r.ts_base_of[j];
+      scatter(dt, [&](int64_t i) { return (int32_t)(ts[i] - tb); });
+    } else {
+      int64_t* dt[MAX_GPUS];
+      for (int q = 0; q < G; ++q) dt[q] = nd.stage[slot][q].ts.as<int64_t>();
+      scatter(dt, [&](int64_t i) { return ts[i]; });
+    }
+    {
+      int64_t* dr[MAX_GPUS];
+      for (int q = 0; q < G; ++q) dr[q] = nd.stage[slot][q].raw.as<int64_t>();
+      scatter(dr, [&](int64_t i) { return raw[i]; });
+    }
+    if (stream) {
+      int32_t* ds[MAX_GPUS];
+      for (int q = 0; q < G; ++q) ds[q] = nd.stage[slot][q].stream.as<int32_t>();
+      scatter(ds, [&](int64_t i) { return stream[i]; });
+    }
+    {
+      uint64_t* dg[MAX_GPUS];
+      for (int q = 0; q < G; ++q) dg[q] = nd.stage[slot][q].gidx.as<uint64_t>();
+      const uint64_t gb = r.b.base_index + (uint64_t)lo;
+      scatter(dg, [&](int64_t i) { return gb + (uint64_t)i; });
+    }
+    for (int c = 0; c < nc; ++c) {
+      if (!need[c] || !r.b.cols[c]) continue;
+      if (sg_col_width(d.col_type[c]) == 8) {
+        int64_t* dc[MAX_GPUS];
+        for (int q = 0; q < G; ++q) dc[q] = nd.stage[slot][q].col[c].as<int64_t>();
+        const int64_t* sc = (const int64_t*)r.b.cols[c] + lo;
+        scatter(dc, [&](int64_t i) { return sc[i]; });
+      } else {
+        int32_t* dc[MAX_GPUS];
+        for (int q = 0; q < G; ++q) dc[q] = nd.stage[slot][q].col[c].as<int32_t>();
+        const int32_t* sc = (const int32_t*)r.b.cols[c] + lo;
+        scatter(dc, [&](int64_t i) { return sc[i]; });
+      }
+      if (r.b.nulls && r.b.nulls[c]) {
+        uint8_t* dn[MAX_GPUS];
+        for (int q = 0; q < G; ++q) dn[q] = nd.stage[slot][q].nul[c].as<uint8_t>();
+        const uint8_t* sn = r.b.nulls[c] + lo;
+        scatter(dn, [&](int64_t i) { return sn[i]; });
       }
     }
   });
@@ -979,37 +1046,44 @@ void merge_chunk(Run& r, int64_t j) {
   }
   const sg_router* rt = nd.router;
   nd.pool->parallel_for(T, [&](int t) {
-    int64_t cur[MAX_GPUS], end[MAX_GPUS];
+    // per shard: rows left, ring slot of the head (wrapped by compare, not by division), the head's global trigger
+    int64_t left[MAX_GPUS], q[MAX_GPUS];
     uint64_t head[MAX_GPUS];
+    const uint64_t* trig[MAX_GPUS];
+    const uint64_t* gidx[MAX_GPUS];
+    uint64_t lbase[MAX_GPUS];
     for (int s = 0; s < G; ++s) {
-      cur[s] = cut[t][s];
-      end[s] = cut[t + 1][s];
-      head[s] = cur[s] < end[s] ? gtrig(s, cur[s]) : ~0ull;
+      const NodeRing& R = nd.ring[s];
+      left[s] = cut[t + 1][s] - cut[t][s];
+      q[s] = cut[t][s] % R.M;
+      trig[s] = R.trig.as<uint64_t>();
+      gidx[s] = nd.stage[slot][s].gidx.as<uint64_t>();
+      lbase[s] = (uint64_t)r.lbase_of[j * G + s];
+      head[s] = left[s] > 0 ? gidx[s][trig[s][q[s]] - lbase[s]] : ~0ull;
     }
+    const bool ties = w.grp;   // (a trigger on two shards: clock passes)
     auto gkey = [&](int s, int64_t p) -> int64_t {
-      const int32_t lk = nd.ring[s].key.as<int32_t>()[p % nd.ring[s].M];
+      const int32_t lk = nd.ring[s].key.as<int32_t>()[p];
       if (lk < 0) return -1;
       return nd.ddict == 1 ? (int64_t)nd.l2g[s][lk] : (int64_t)rt->l2d[s][lk];
     };
     for (int64_t o = o0[t]; o < o0[t + 1]; ++o) {
       int best = -1;
       for (int s = 0; s < G; ++s) {
-        if (cur[s] >= end[s]) continue;
+        if (left[s] <= 0) continue;
         if (best < 0 || head[s] < head[best]) { best = s; continue; }
-        if (head[s] == head[best] && w.grp) {   // same trigger on two shards: a clock pass -> (phase, key)
-          const NodeRing& A = nd.ring[s];
-          const NodeRing& B = nd.ring[best];
-          const uint32_t pa = A.grp.as<uint32_t>()[cur[s] % A.M] >> 24, pb = B.grp.as<uint32_t>()[cur[best] % B.M] >> 24;
-          if (pa < pb || (pa == pb && gkey(s, cur[s]) < gkey(best, cur[best]))) best = s;
+        if (ties && head[s] == head[best]) {   // same trigger on two shards: a clock pass -> (phase, key)
+          const uint32_t pa = nd.ring[s].grp.as<uint32_t>()[q[s]] >> 24, pb = nd.ring[best].grp.as<uint32_t>()[q[best]] >> 24;
+          if (pa < pb || (pa == pb && gkey(s, q[s]) < gkey(best, q[best]))) best = s;
         }
       }
       const int s = best;
       const NodeRing& R = nd.ring[s];
-      const int64_t p = cur[s] % R.M;
+      const int64_t p = q[s];
       if (r.out->trigger) r.out->trigger[o] = head[s];
       if (w.ts) r.out->ts[o] = R.ts.as<int64_t>()[p];
       if (w.any_fill) fill_row(r.b, nd.desc, w, r.out, o, head[s]);
-      if (r.out->key) r.out->key[o] = (int32_t)gkey(s, cur[s]);
+      if (r.out->key) r.out->key[o] = (int32_t)gkey(s, p);
       if (r.out->group) r.out->group[o] = R.grp.as<uint32_t>()[p];
       for (int c = 0; c < w.ns; ++c) {
         if (w.col[c]) {
@@ -1018,8 +1092,8 @@ void merge_chunk(Run& r, int64_t j) {
         }
         if (w.nul[c]) r.out->nulls[c][o] = R.nul[c].as<uint8_t>()[p];
       }
-      ++cur[s];
-      head[s] = cur[s] < end[s] ? gtrig(s, cur[s]) : ~0ull;
+      if (++q[s] == R.M) q[s] = 0;
+      head[s] = --left[s] > 0 ? gidx[s][trig[s][q[s]] - lbase[s]] : ~0ull;
     }
   });
   r.out_rows += total;

@@ -625,14 +625,39 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
       int ws, wop, wf;
       int64_t wc;
       if (pl.wsum && q < e && L.wait_on(ws, wop, wf, wc)) {
+        // blocks whose summary rules the term out are skipped whole; in a block that may pass, the lane reads its 8
+        // values at once and lands on the first row that passes (or moves on to the next block)
         const uint2* S = pl.wsum + (int64_t)pl.wix[ws] * pl.wnb;
-        int64_t b = q >> 3;
-        const int64_t be = (e + 7) >> 3;
-        for (int lim = 0; lim < 16 && b < be; ++lim, ++b) {
+        const uint32_t* V = (const uint32_t*)pl.val[ws];
+        const int64_t mrows = a.nc + a.n;
+        int64_t qq = q;
+        for (int lim = 0; lim < 16 && qq < e; ++lim) {
+          const int64_t b = qq >> 3;
           const uint2 mm = S[b];
-          if (pp_may_pass(mm.x, mm.y, wop, wf, wc)) break;
+          if (pp_may_pass(mm.x, mm.y, wop, wf, wc)) {
+            uint32_t x[8];
+            if ((b << 3) + 8 <= mrows) {
+              const uint4 x0 = *(const uint4*)(V + (b << 3)), x1 = *(const uint4*)(V + (b << 3) + 4);
+              x[0] = x0.x; x[1] = x0.y; x[2] = x0.z; x[3] = x0.w; x[4] = x1.x; x[5] = x1.y; x[6] = x1.z; x[7] = x1.w;
+            } else {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) x[k] = (b << 3) + k < mrows ? V[(b << 3) + k] : 0u;
+            }
+            uint32_t pm = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const bool ok = wf == 1 ? pp_cmp_i(wop, (int64_t)(int32_t)x[k], wc) : pp_cmp_f(wop, pp_f32((int64_t)x[k]), pp_f32(wc));
+              pm |= (ok ? 1u : 0u) << k;
+            }
+            pm &= ~((1u << (qq & 7)) - 1u);
+            if (pm) {
+              qq = (b << 3) + __builtin_ctz(pm);
+              break;
+            }
+          }
+          qq = (b + 1) << 3;
         }
-        if ((b << 3) > q) q = (b << 3) < e ? (b << 3) : e;
+        q = qq < e ? qq : e;
       }
       if (q >= e || src.ts(q) - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
         done = true;
