@@ -506,9 +506,13 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
     del cat, batches
     torch.cuda.empty_cache()
     ms = 1000.0 * el / steps
-    roof = roofline_of("C5", n, matches, {k: v / steps for k, v in kern.items()}, stage / steps)
-    roof["scope"] = "rank 0's share of the stream: %d events in %d pushes of <= %d rows, %d matches" % (
-        n, len(range(0, n, push_rows)), push_rows, matches)
+    # per launch (= per push): the step's kernel times and bytes over its pushes
+    pushes = max(1, len(range(0, n, push_rows)))
+    roof = roofline_of("C5", n / pushes, matches / pushes, {k: v / steps / pushes for k, v in kern.items()},
+                       stage / steps / pushes)
+    roof["scope"] = "per push (launch) of rank 0's share of the stream: %d events in %d pushes of <= %d rows, %d matches" % (
+        n, pushes, push_rows, matches)
+    roof["push_events"] = int(round(n / pushes))
     return {"workload": "C5 (BASELINE configs[4]): " + synth.QUERIES["C5"], "events": total, "keys": keys,
             "rate_events_per_ms": rate, "n_gpus": ws, "scaling": "strong", "steps": steps,
             "ms_per_step": round(ms, 3), "value": round(total / (ms * 1e-3), 1), "unit": "events/s",
@@ -676,11 +680,8 @@ def main():
 
 
 def roof_events(roof):
-    """events of the push the roofline was taken on (C5: rank 0's share of the stream, a multiple of 1e8 rows)"""
-    try:
-        return int(roof["scope"].split()[4])
-    except Exception:
-        return 0
+    """events of one push the roofline was taken on (C5: rank 0's share of the stream over its pushes)"""
+    return int(roof.get("push_events", 0))
 
 
 if __name__ == "__main__":

@@ -194,14 +194,17 @@ def test_node_c5_whole_1b_stream_ten_pushes():
     dictionary and per-key partial matches carried between pushes), every delivered row compared with the oracle
     run key-sharded over the host cores with its engines -- and so its carried state -- kept across the same ten
     pushes (parity_util.CarriedShardedOracle).  The workers fork before the first push; the rows of each push are
-    regenerated from the deterministic synth stream, so host memory stays at one push."""
+    regenerated from the deterministic synth stream, so host memory stays at one push.
+
+    The whole stream takes ~8 minutes on the box (profiles/r04/c5_whole_1b_test.log: 10 pushes, 399,303,893 matches, all
+    equal); the default suite runs its first three pushes (300M events) and SG_C5_WHOLE=1 runs all ten."""
     import os
     from parity_util import CarriedShardedOracle
     from siddhi_amd import _native as N
     cfg = "C5"
     _, n, K, R = synth.CONFIGS[cfg]
-    pushes = 10
-    per = n // pushes
+    per = n // 10
+    pushes = 10 if os.environ.get("SG_C5_WHOLE") == "1" else 3
     q = synth.QUERIES[cfg]
     oracle = CarriedShardedOracle(q, max(2, min(16, os.cpu_count() or 2)))
     nfa = __import__("siddhi_amd.lowering", fromlist=["lower"]).lower(context(q))
@@ -233,12 +236,13 @@ def test_node_c5_whole_1b_stream_ten_pushes():
             assert len(got) == len(want) > 0, (p, len(got), len(want))
             assert_same(got, want)
             total += len(got)
+            print(f"push {p}: {len(got)} matches equal the oracle's", flush=True)   # (progress: a long test)
             del got, want
         assert node.keys() == K == nxt
     finally:
         oracle.close()
         node.close()
-    assert total > 300_000_000   # (399,303,893 in the r03 whole-node bench line)
+    assert total > 36_000_000 * pushes
 
 
 @pytest.mark.timeout(300)
