@@ -41,6 +41,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <limits>
 #include <type_traits>
 #include <cstdio>
 #include <string>
@@ -2100,6 +2101,371 @@ static int run_fgw(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& 
   return 1;
 }
 
+// ---- Keyed next match (partitioned closed form, narrow 4-byte values).  A pending partial i of
+// `every A -> B[B.x OP A.x] within T` leaves e2's list only by completing or by expiring, and nothing else a later row
+// does touches it: it completes at the first later row j of its key that can complete (F_CONS, a live value) with
+// x_j OP x_i and ts_j - ts_i <= T, or never (StreamPreStateProcessor.processAndReturn :292-337 with the lazy expiry
+// of isExpired :102-113, keys' timestamps non-decreasing).  So every candidate searches forward in the key-sorted
+// records on its own -- skipping 8-record blocks whose {min, max} of completing values rules the compare out -- and
+// the matches of a trigger are its candidates in pending (= arrival) order: counts per trigger row, a scan, each
+// match placed at (trigger offset + its rank), ranks put in candidate order where a trigger completed several.  Same
+// rows, same order as the walker (the walker's monotone stack / scanned list restate the same per-partial rule).
+static const uint32_t KN_NONE = 0xffffffffu;
+template <class T>
+struct KnBlk {
+  T mn, mx;          // completing values of the block's records (empty: mn > mx)
+  int32_t ts0;       // relative time of its first record
+  uint32_t segm;     // bit o: record o starts a key segment (or lies past the end)
+};
+
+static __global__ void k_kn_segbits(uint32_t K, const uint32_t* __restrict__ seg_b, const uint32_t* __restrict__ seg_e,
+                                    uint32_t* __restrict__ bits) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const uint32_t b = seg_b[k];
+  if (seg_e[k] > b) atomicOr(&bits[b >> 5], 1u << (b & 31));
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_kn_blocks(const WRec<T, true>* __restrict__ srec, int64_t nt,
+                                                   const uint32_t* __restrict__ bits, KnBlk<T>* __restrict__ blk,
+                                                   uint32_t* __restrict__ flags) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p0 = b * 8;
+  if (p0 >= nt) return;
+  const int cnt = (int)(nt - p0 < 8 ? nt - p0 : 8);
+  uint32_t segm = (bits[p0 >> 5] >> (p0 & 31)) & 0xffu;
+  segm |= 0xffu & ~((1u << cnt) - 1u);   // (records past the end: a boundary)
+  const T hi = std::numeric_limits<T>::has_infinity ? std::numeric_limits<T>::infinity() : std::numeric_limits<T>::max();
+  T mn = hi, mx = std::numeric_limits<T>::has_infinity ? -hi : std::numeric_limits<T>::lowest();   // (empty: mn > mx)
+  int64_t prev = (p0 > 0 && !(segm & 1u)) ? srec[p0 - 1].t() : INT64_MIN;
+  bool bad = false;
+  int32_t t0 = 0;
+  for (int o = 0; o < cnt; ++o) {
+    const WRec<T, true> r = srec[p0 + o];
+    const int64_t t = r.t();
+    if (o == 0) t0 = (int32_t)t;
+    if ((segm >> o) & 1u) prev = INT64_MIN;
+    bad |= t < prev;
+    prev = t;
+    const uint32_t f = r.rowf >> 30;
+    if ((f & F_CONS) && !is_nan_val<T>(r.val)) {
+      mn = r.val < mn ? r.val : mn;
+      mx = r.val > mx ? r.val : mx;
+    }
+  }
+  KnBlk<T> o;
+  o.mn = mn;
+  o.mx = mx;
+  o.ts0 = t0;
+  o.segm = segm;
+  blk[b] = o;
+  if (bad) atomicOr(flags, 1u);
+}
+
+template <class T>
+__device__ __forceinline__ bool kn_may(int op, T mn, T mx, T x) {
+  if (mn > mx) return false;
+  switch (op) {
+    case 2: return mx > x;
+    case 3: return mx >= x;
+    case 4: return mn < x;
+    default: return mn <= x;
+  }
+}
+
+template <class T, int OP>
+__global__ void __launch_bounds__(256) k_kn_find(const WRec<T, true>* __restrict__ srec, int64_t nt,
+                                                 const KnBlk<T>* __restrict__ blk, int64_t within, int op, int64_t nc,
+                                                 uint32_t* __restrict__ mj, uint32_t* __restrict__ rank,
+                                                 uint32_t* __restrict__ cnt) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nt) return;
+  const WRec<T, true> r = srec[p];
+  uint32_t out = KN_NONE;
+  if (((r.rowf >> 30) & F_CAND) && !is_nan_val<T>(r.val)) {
+    const T x = r.val;
+    const int64_t ti = r.t();
+    int64_t b = p >> 3;
+    uint32_t o0 = (uint32_t)(p & 7) + 1u;
+    const int64_t nb = (nt + 7) >> 3;
+    while (b < nb) {
+      const KnBlk<T> B = blk[b];
+      uint32_t consider = 0xffu & ~((1u << o0) - 1u);
+      const uint32_t sm = B.segm & consider;
+      const uint32_t endo = sm ? (uint32_t)__builtin_ctz(sm) : 8u;
+      consider &= (1u << endo) - 1u;
+      if (o0 == 0 && consider && (int64_t)B.ts0 - ti > within) break;   // the block starts past `within`
+      bool stop = false;
+      if (consider && kn_may<T>(OP ? OP : op, B.mn, B.mx, x)) {
+        for (uint32_t o = 0; o < 8; ++o) {
+          if (!((consider >> o) & 1u)) continue;
+          const WRec<T, true> q = srec[b * 8 + o];
+          if (q.t() - ti > within) { stop = true; break; }
+          if (((q.rowf >> 30) & F_CONS) && !is_nan_val<T>(q.val) && cmp_sel<OP, T>(op, q.val, x)) {
+            out = (uint32_t)(b * 8 + o);
+            stop = true;
+            break;
+          }
+        }
+      }
+      if (stop || endo < 8) break;
+      ++b;
+      o0 = 0;
+    }
+  }
+  if (out != KN_NONE) {
+    const uint32_t r2 = srec[out].rowf & ROW_MASK;
+    if ((int64_t)r2 >= nc) rank[p] = atomicAdd(&cnt[r2 - nc], 1u);
+    else out = KN_NONE;   // (completed by a carried row: delivered by an earlier push)
+  }
+  mj[p] = out;
+}
+
+template <class T>
+__global__ void k_kn_place(const WRec<T, true>* __restrict__ srec, int64_t nt, const uint32_t* __restrict__ mj,
+                           const uint32_t* __restrict__ rank, const uint32_t* __restrict__ off, int64_t nc, int pay,
+                           int pfloat, MatchSink ms) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nt) return;
+  const uint32_t j = mj[p];
+  if (j == KN_NONE) return;
+  const WRec<T, true> r = srec[p];
+  const uint32_t r2 = srec[j].rowf & ROW_MASK;
+  ms.put(off[r2 - nc] + rank[p], r.rowf & ROW_MASK, r2, val_bits<T>(r.val), pay ? r.p(pfloat) : 0);
+}
+
+// a trigger that completed several partials: its matches in pending order (candidate rows ascending)
+static __global__ void k_kn_order(int64_t n, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
+                                  PtU4* __restrict__ rec) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  const uint32_t c = cnt[b];
+  if (c < 2) return;
+  PtU4* e = rec + off[b];
+  for (uint32_t i = 1; i < c; ++i) {
+    const PtU4 x = e[i];
+    uint32_t k = i;
+    while (k > 0 && e[k - 1].x > x.x) {
+      e[k] = e[k - 1];
+      --k;
+    }
+    e[k] = x;
+  }
+}
+
+template <class T>
+__global__ void k_kn_carry(Src<T, true> src, uint32_t K, const uint32_t* __restrict__ seg_b,
+                           const uint32_t* __restrict__ seg_e, int64_t within, uint32_t* __restrict__ q0s,
+                           uint32_t* __restrict__ cn) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const uint32_t sb = seg_b[k], se = seg_e[k];
+  if (se > sb) {
+    const uint32_t q0 = lb_ts(src, sb, se, src.ts(se - 1) - within);
+    q0s[k] = q0;
+    cn[k] = se - q0;
+  } else {
+    cn[k] = 0;
+  }
+}
+
+// Carry into the next push: per key the rows from carry_q0[k] on (carry_n[k] of them, the rows inside `within` of the
+// key's last row), copied out of this push's virtual rows into the other carry set.
+template <class T, bool N>
+static void carry_out_rows(SgHandle* h, EveryNextState* es, uint32_t K, int64_t nt, const Src<T, N>& src,
+                           const uint32_t* seg_b, const uint32_t* seg_e, const Virt& v, const BatchView& bv,
+                           const SgCols& cc, const uint32_t* carry_q0, const uint32_t* carry_n) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  CarrySet& cs = es->carry[es->cur];
+  (void)seg_b;
+  (void)seg_e;
+  {
+    static const bool by_key = getenv("SG_CARRY_BY_KEY") != nullptr;   // (experiments: the per-key copy)
+    uint32_t* coff = (uint32_t*)h->ws.get("carry_off", sizeof(uint32_t) * (K + 1), st);
+    uint32_t* cbits = nullptr;
+    uint32_t* cboff = nullptr;
+    uint32_t* ccount = (uint32_t*)h->ws.get("carry_count", sizeof(uint32_t), st);
+    if (by_key) {
+      size_t tb = 0;
+      HIPCHK(rocprim::exclusive_scan(nullptr, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
+      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
+      HIPCHK(rocprim::exclusive_scan(tmp, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
+      HIPCHK(hipMemcpyAsync(ccount, coff + K, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    } else {
+      h->kbeg("carry");
+      const int64_t nw = (nt + 31) / 32, nb = (nt + CARRY_BLK - 1) / CARRY_BLK;
+      cbits = (uint32_t*)h->ws.get("carry_bits", sizeof(uint32_t) * (size_t)(nb * 256), st);
+      cboff = (uint32_t*)h->ws.get("carry_boff", sizeof(uint32_t) * (size_t)(nb + 1), st);
+      uint32_t* bcnt = (uint32_t*)h->ws.get("carry_bcnt", sizeof(uint32_t) * (size_t)(nb + 1), st);
+      HIPCHK(hipMemsetAsync(cbits, 0, sizeof(uint32_t) * (size_t)(nb * 256), st));
+      hipLaunchKernelGGL((k_carry_mark<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n, cbits);
+      hipLaunchKernelGGL(k_carry_bcount, dim3((unsigned)nb), dim3(256), 0, st, nt, cbits, bcnt);
+      HIPCHK(hipMemsetAsync(bcnt + nb, 0, sizeof(uint32_t), st));
+      HIPCHK(hipGetLastError());
+      size_t tb = 0;
+      HIPCHK(rocprim::exclusive_scan(nullptr, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
+      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
+      HIPCHK(rocprim::exclusive_scan(tmp, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
+      HIPCHK(hipMemcpyAsync(ccount, cboff + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+      (void)nw;
+      h->kend();
+    }
+    uint32_t ncar = 0;
+    HIPCHK(hipMemcpyAsync(&ncar, ccount, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    CarrySet& nx = es->carry[es->cur ^ 1];
+    nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
+    int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
+    int32_t hw[SG_MAX_COLS];
+    for (int c = 0; c < SG_MAX_COLS; ++c)
+      hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
+    HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
+    CarryBufs cb;
+    memset(&cb, 0, sizeof(cb));
+    cb.ts = nx.ts;
+    cb.key = nx.key;
+    cb.flags = nx.flags;
+    for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
+    if (ncar && by_key)
+      hipLaunchKernelGGL((k_carry_copy<T, N>), dim3((ncar + 255) / 256), dim3(256), 0, st, src, K, ncar, carry_q0,
+                         coff, d.n_cols, widths, bv.cols, cc, cb);
+    else if (ncar)
+      hipLaunchKernelGGL(k_carry_gather, dim3((unsigned)((nt + CARRY_BLK - 1) / CARRY_BLK)), dim3(256), 0, st, v, nt,
+                         cbits, cboff, d.n_cols, widths, bv.cols, cc, cb);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    nx.n = ncar;
+    cs.n = 0;
+    es->cur ^= 1;
+  }
+}
+
+// The keyed next-match pipeline for one push (after the key partition).  1: done; 0: a precondition the walker
+// handles differently (payloads wider than 32 bits, a key whose timestamps go back -- the walker then decides);
+// -1: narrow records cannot represent the push (the caller retries with wide records).
+template <class T>
+static int run_keyed_next(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, int64_t nt, uint32_t K,
+                          const PushPlan& plan, const Virt& v, const SgCols& cc, const Src<T, true>& src,
+                          const uint32_t* seg_b, const uint32_t* seg_e, uint32_t* pk_flags, int op,
+                          EveryNextState* es, int b_state) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  uint32_t pkf = 0;
+  HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (pkf & PK_KEY_RANGE) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+  if (pkf & PK_INTERNAL) throw SgError(SG_EINVAL, "internal: key partition offsets out of range");
+  if (pkf & PK_TS_RANGE) return -1;
+  if (pkf & PK_PAY_RANGE) return 0;
+  const int64_t nb = (nt + 7) / 8;
+  const size_t nwords = (size_t)((nt + 31) / 32 + 1);
+  uint32_t* bits = (uint32_t*)h->ws.get("kn_bits", sizeof(uint32_t) * nwords, st);
+  KnBlk<T>* blk = (KnBlk<T>*)h->ws.get("kn_blk", sizeof(KnBlk<T>) * (size_t)nb, st);
+  uint32_t* kfl = (uint32_t*)h->ws.get("kn_flags", 2 * sizeof(uint32_t), st);
+  HIPCHK(hipMemsetAsync(bits, 0, sizeof(uint32_t) * nwords, st));
+  HIPCHK(hipMemsetAsync(kfl, 0, 2 * sizeof(uint32_t), st));
+  h->kbeg("next_blocks");
+  hipLaunchKernelGGL(k_kn_segbits, dim3((K + 255) / 256), dim3(256), 0, st, K, seg_b, seg_e, bits);
+  hipLaunchKernelGGL((k_kn_blocks<T>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src.srec, nt, bits, blk, kfl);
+  HIPCHK(hipGetLastError());
+  h->kend();
+  uint32_t order_bad = 0;
+  HIPCHK(hipMemcpyAsync(&order_bad, kfl, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (order_bad) return 0;
+  uint32_t* cnt = (uint32_t*)h->ws.get("cnt", sizeof(uint32_t) * (n + 1), st);
+  uint32_t* off = (uint32_t*)h->ws.get("off", sizeof(uint32_t) * (n + 1), st);
+  uint32_t* mj = (uint32_t*)h->ws.get("kn_mj", sizeof(uint32_t) * (size_t)nt, st);
+  uint32_t* rank = (uint32_t*)h->ws.get("kn_rank", sizeof(uint32_t) * (size_t)nt, st);
+  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
+  const dim3 g((unsigned)((nt + 255) / 256)), b256(256);
+  h->kbeg("next_search");
+  switch (op) {
+    case 2: hipLaunchKernelGGL((k_kn_find<T, 2>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
+    case 3: hipLaunchKernelGGL((k_kn_find<T, 3>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
+    case 4: hipLaunchKernelGGL((k_kn_find<T, 4>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
+    default: hipLaunchKernelGGL((k_kn_find<T, 5>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
+  }
+  HIPCHK(hipGetLastError());
+  h->kend();
+  h->kbeg("count_scan");
+  {
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+  }
+  h->kend();
+  h->mark(3);
+  uint32_t total = 0;
+  HIPCHK(hipMemcpyAsync(&total, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  h->extra_marks = 0;
+  WalkArgs wa;
+  memset(&wa, 0, sizeof(wa));
+  wa.nt = nt;
+  wa.K = K;
+  wa.partitioned = 1;
+  wa.op = op;
+  wa.base_index = bv.base_index;
+  wa.index = bv.index;
+  wa.n_select = d.n_select;
+  wa.stride = 32 + 8 * d.n_select;
+  {
+    const int rb = d.recv_of_stream[d.states[b_state].stream];
+    wa.multi = d.receivers[rb].multi;
+    wa.b_slot = 0;
+    if (wa.multi) {
+      const sg_receiver_desc& r = d.receivers[rb];
+      for (int q = 0; q < r.n; ++q)
+        if (r.pres[r.n - 1 - q] == b_state) wa.b_slot = q;   // eventSequence = reversed init order
+    }
+  }
+  MatchSink ms{nullptr, 1, 0, kfl + 1};
+  h->split_out = 1;
+  if (total) {
+    char* out = h->out.reserve(total, d.n_select, st);
+    wa.out_base = h->out.n;
+    ms.cap = total;
+    ms.rec = h->ws.get("mrec", sizeof(MRec16) * (size_t)total, st);
+    h->mark(5);
+    h->kbeg("next_place");
+    hipLaunchKernelGGL((k_kn_place<T>), g, b256, 0, st, src.srec, nt, mj, rank, off, nc, plan.pcol >= 0 ? 1 : 0,
+                       v.pfloat, ms);
+    hipLaunchKernelGGL(k_kn_order, dim3((unsigned)((n + 255) / 256)), b256, 0, st, n, cnt, off, (PtU4*)ms.rec);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->kbeg("project");
+    hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)), b256, (size_t)256 * wa.stride, st,
+                       wa, v, plan.pp, bv.cols, cc, ms, off, (int64_t)total, out);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->out.n += total;
+  } else {
+    h->mark(5);
+  }
+  h->mark(4);
+  if (!h->opt.no_carry) {
+    uint32_t* carry_q0 = (uint32_t*)h->ws.get("carry_q0", sizeof(uint32_t) * K, st);
+    uint32_t* carry_n = (uint32_t*)h->ws.get("carry_n", sizeof(uint32_t) * (K + 1), st);
+    HIPCHK(hipMemsetAsync(carry_n + K, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL((k_kn_carry<T>), dim3((K + 255) / 256), b256, 0, st, src, K, seg_b, seg_e, (int64_t)d.within,
+                       carry_q0, carry_n);
+    HIPCHK(hipGetLastError());
+    carry_out_rows<T, true>(h, es, K, nt, src, seg_b, seg_e, v, bv, cc, carry_q0, carry_n);
+  }
+  uint32_t guard = 0;
+  HIPCHK(hipMemcpyAsync(&guard, kfl + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (guard) throw SgError(SG_EINVAL, "internal: next-match placement guard tripped");
+  h->last_events = n;
+  h->last_matches = total;
+  h->last_spilled = 0;
+  return 1;
+}
+
 template <class T, bool N>
 static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan plan) {
   const sg_nfa_desc& d = h->desc;
@@ -2358,6 +2724,19 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemcpyAsync(seg_e, &seg[1], sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
   h->mark(2);
+  if constexpr (N && sizeof(T) == 4) {
+    // keyed next match (no walk units, no ring, one search per candidate): opt-in, SG_KEYED_NEXT=1.  Exact, but
+    // measured slower than the walker on C2 (search 6.3 + blocks 3.4 + place 2.3 + order 1.4 ms against 3.5 ms of
+    // units / transpose / count and record walks: one candidate's search is a chain of dependent loads and a wave
+    // waits for its longest; profiles/r04/C2_keyed_next_kernel_stats.csv)
+    const char* kn_env = getenv("SG_KEYED_NEXT");
+    const bool kn_on = kn_env && kn_env[0] == '1';
+    if (d.partitioned && !h->opt.walker_only && h->opt.ring_cap == 0 && kn_on && n > 0) {
+      const int r = run_keyed_next<T>(h, bv, n, nc, nt, K, plan, v, cc, src, seg_b, seg_e, pk_flags, op, es, b_state);
+      if (r == 1) return true;
+      if (r == -1) return false;
+    }
+  }
 
   // ---- 3. count pass + scan
   WalkArgs wa;
@@ -2540,65 +2919,11 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
 
   // ---- 6. carry into the next push
   if (wa.carry_out) {
-    static const bool by_key = getenv("SG_CARRY_BY_KEY") != nullptr;   // (experiments: the per-key copy)
-    uint32_t* coff = (uint32_t*)h->ws.get("carry_off", sizeof(uint32_t) * (K + 1), st);
-    uint32_t* cbits = nullptr;
-    uint32_t* cboff = nullptr;
-    uint32_t* ccount = (uint32_t*)h->ws.get("carry_count", sizeof(uint32_t), st);
-    if (by_key) {
-      size_t tb = 0;
-      HIPCHK(rocprim::exclusive_scan(nullptr, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
-      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
-      HIPCHK(rocprim::exclusive_scan(tmp, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
-      HIPCHK(hipMemcpyAsync(ccount, coff + K, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    } else {
-      h->kbeg("carry");
-      const int64_t nw = (nt + 31) / 32, nb = (nt + CARRY_BLK - 1) / CARRY_BLK;
-      cbits = (uint32_t*)h->ws.get("carry_bits", sizeof(uint32_t) * (size_t)(nb * 256), st);
-      cboff = (uint32_t*)h->ws.get("carry_boff", sizeof(uint32_t) * (size_t)(nb + 1), st);
-      uint32_t* bcnt = (uint32_t*)h->ws.get("carry_bcnt", sizeof(uint32_t) * (size_t)(nb + 1), st);
-      HIPCHK(hipMemsetAsync(cbits, 0, sizeof(uint32_t) * (size_t)(nb * 256), st));
-      hipLaunchKernelGGL((k_carry_mark<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n, cbits);
-      hipLaunchKernelGGL(k_carry_bcount, dim3((unsigned)nb), dim3(256), 0, st, nt, cbits, bcnt);
-      HIPCHK(hipMemsetAsync(bcnt + nb, 0, sizeof(uint32_t), st));
-      HIPCHK(hipGetLastError());
-      size_t tb = 0;
-      HIPCHK(rocprim::exclusive_scan(nullptr, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
-      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
-      HIPCHK(rocprim::exclusive_scan(tmp, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
-      HIPCHK(hipMemcpyAsync(ccount, cboff + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-      (void)nw;
-      h->kend();
-    }
-    uint32_t ncar = 0, guard = 0;
-    HIPCHK(hipMemcpyAsync(&ncar, ccount, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    uint32_t guard = 0;
     HIPCHK(hipMemcpyAsync(&guard, &wst->internal, sizeof(uint32_t), hipMemcpyDeviceToHost, st));   // record-pass guards
     HIPCHK(hipStreamSynchronize(st));
     if (guard) throw SgError(SG_EINVAL, "internal: record-pass guard tripped (" + std::to_string(guard) + ")");
-    CarrySet& nx = es->carry[es->cur ^ 1];
-    nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
-    int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
-    int32_t hw[SG_MAX_COLS];
-    for (int c = 0; c < SG_MAX_COLS; ++c)
-      hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
-    HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
-    CarryBufs cb;
-    memset(&cb, 0, sizeof(cb));
-    cb.ts = nx.ts;
-    cb.key = nx.key;
-    cb.flags = nx.flags;
-    for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
-    if (ncar && by_key)
-      hipLaunchKernelGGL((k_carry_copy<T, N>), dim3((ncar + 255) / 256), dim3(256), 0, st, src, K, ncar, carry_q0,
-                         coff, d.n_cols, widths, bv.cols, cc, cb);
-    else if (ncar)
-      hipLaunchKernelGGL(k_carry_gather, dim3((unsigned)((nt + CARRY_BLK - 1) / CARRY_BLK)), dim3(256), 0, st, v, nt,
-                         cbits, cboff, d.n_cols, widths, bv.cols, cc, cb);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(st));
-    nx.n = ncar;
-    cs.n = 0;
-    es->cur ^= 1;
+    carry_out_rows<T, N>(h, es, K, nt, src, seg_b, seg_e, v, bv, cc, carry_q0, carry_n);
   }
   h->last_events = n;
   h->last_matches = total;
