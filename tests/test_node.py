@@ -197,14 +197,14 @@ def test_node_c5_whole_1b_stream_ten_pushes():
     regenerated from the deterministic synth stream, so host memory stays at one push.
 
     The whole stream takes ~8 minutes on the box (profiles/r04/c5_whole_1b_test.log: 10 pushes, 399,303,893 matches, all
-    equal); the default suite runs its first three pushes (300M events) and SG_C5_WHOLE=1 runs all ten."""
+    equal); the default suite runs its first two pushes (200M events) and SG_C5_WHOLE=1 runs all ten."""
     import os
     from parity_util import CarriedShardedOracle
     from siddhi_amd import _native as N
     cfg = "C5"
     _, n, K, R = synth.CONFIGS[cfg]
     per = n // 10
-    pushes = 10 if os.environ.get("SG_C5_WHOLE") == "1" else 3
+    pushes = 10 if os.environ.get("SG_C5_WHOLE") == "1" else 2
     q = synth.QUERIES[cfg]
     oracle = CarriedShardedOracle(q, max(2, min(16, os.cpu_count() or 2)))
     nfa = __import__("siddhi_amd.lowering", fromlist=["lower"]).lower(context(q))
