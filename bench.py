@@ -1,30 +1,27 @@
 #!/usr/bin/env python3
-"""Benchmark: events/sec of the partitioned pattern query on MI355X (BASELINE.json metric, configs[1] = C2).
+"""Benchmark: events/sec of the partitioned pattern query on MI355X (BASELINE.json metric; its config, configs[4] = C5).
 
-Workload:
+Headline workload:
   partition with (symbol of StockStream) begin
     from every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] within 1 sec
     select e1.id as id1, e2.id as id2, e1.price as p1, e2.price as p2 insert into M; end;
-  100M synthetic events per GPU (SplitMix64 generator, siddhi_amd/synth.py), 10k keys, 1000 events/ms.
+  ONE 1B-event stream over 1M keys at 10,000 events/ms (SplitMix64 generator, siddhi_amd/synth.py).
 
-Two rates, both in the one JSON line rank 0 prints:
-  value       (task contract: inputs already resident in HBM when the timed region starts) -- a step is one
-              sg_push of the 100M-event batch through the whole HIP pipeline on a fresh state, ending with every
-              compacted match tuple projected in HBM (sg_device_records: the C-ABI's zero-copy delivery).
-  whole_node  (SURVEY.md §8d's definition, reported beside it): host raw columns -> native host router
-              (dictionary-encodes the raw symbol to first-seen dense ids, sg_router_route) -> sg_push_deliver
-              from pinned memory (chunked H2D, kernels, per-chunk GPU-transposed SoA match columns copied back into
-              pinned host memory, overlapped) -> every match tuple in host memory.  PCIe-bound; never `value`.
-Multi-GPU (one process per GPU, torchrun): weak scaling, rank r owns the disjoint key range [r*K, (r+1)*K) with
-its own stream; no data-path collective (keys never interact); times are max over ranks.
-  c5_stream   (BASELINE configs[4], beside `value`): ONE 1B-event, 1M-key C5 stream split by key hash across the
-              N ranks (strong scaling: the same stream at every N), each rank pushing its share in 100M-row batches
-              with state carried between them; value = 1e9 events / max-over-ranks time.
+value (task contract: inputs already resident in HBM when the timed region starts): the stream is split by key hash
+  across the N ranks (router.shard_of_torch: mix64(key) mod N, computed on the GPU; strong scaling -- the same stream
+  at every N, no data-path collective: keys never interact); each rank pushes its share in 100M-row
+  batches with per-key state carried between them, every match projected in HBM (sg_device_records, zero-copy).
+  A step = the whole stream; value = 1e9 events / max-over-ranks step time.
+whole_node (SURVEY.md §8d's definition, never `value`): pinned raw host rows (64-bit symbol values) -> sg_node_push
+  (native router, per-GPU chunked H2D / kernels / D2H, native merge) -> every match tuple in host memory; with the
+  PCIe rate against a measured pinned-copy peak, and on one GPU the host stages of G = 2, 4, 8 shards mapped onto it.
+configs: C2 (configs[1]), C1, C3b, C3c, C4 and PP sub-lines, one push each on one GPU, with their own rooflines.
 
-roofline: the dominant kernel of the `value` step (largest HIP-event time, recorded on the launch stream by the
-engine, sg_timing.kernel_ms) against the §8d algorithmic bytes of the whole path (16.125 B/event + 36 B/match),
-plus the predicate pass (4.125 B/event) and the end-to-end path; `traffic` comes from a rocprofv3 PMC summary of
-this same command (profiles/collect_r03.sh) and is only used when its source hash matches the tree.
+roofline (per launch = per push): the dominant kernel (largest HIP-event time, recorded on the launch stream by the
+engine, sg_timing.kernel_ms) against ITS OWN algorithmic bytes (KERNEL_BYTES), the whole path's SURVEY §8d bytes over
+the sum of the push's kernels beside it (`path`), and the predicate pass (4.125 B/event); `traffic` comes from a
+rocprofv3 PMC summary of this same command (profiles/r04/collect.sh, FETCH_SIZE x2 + WRITE_SIZE passes) and is only
+used when its kernel-source hash matches the tree.
 """
 import argparse
 import hashlib
@@ -193,14 +190,17 @@ def pmc_traffic(path, cfg, n, dominant):
     except OSError:
         return None, "no PMC summary at %s" % os.path.relpath(path, ROOT)
     if prof.get("source_hash") != source_hash(cfg):
-        return None, "stale PMC summary (source hash %s != tree %s): rerun profiles/collect_r03.sh" % (
+        return None, "stale PMC summary (source hash %s != tree %s): rerun profiles/r04/collect.sh" % (
             prof.get("source_hash"), source_hash(cfg))
     if prof.get("workload") != cfg or prof.get("events") != n:
         return None, "PMC summary is for %s/%s events" % (prof.get("workload"), prof.get("events"))
     k = prof["kernels"].get(dominant)
     dom = None if k is None else round(k["bytes_per_push"] / 1e9, 4)
-    path_tot = sum(v["bytes_per_push"] for v in prof["kernels"].values())
-    return {"dominant_GB": dom, "path_GB": round(path_tot / 1e9, 4),
+    # runtime fills / copies (hipMemset, the output buffer's growth in the warm-up step) are averaged over every
+    # push of the profiled run: reported beside the kernels' bytes, not in them
+    rt = prof["kernels"].get("runtime_fill_copy", {}).get("bytes_per_push", 0.0)
+    path_tot = sum(v["bytes_per_push"] for m, v in prof["kernels"].items() if m != "runtime_fill_copy")
+    return {"dominant_GB": dom, "path_GB": round(path_tot / 1e9, 4), "runtime_fill_copy_GB": round(rt / 1e9, 4),
             "source": os.path.relpath(path, ROOT), "collected_at_head": prof.get("git_head")}, None
 
 
@@ -210,6 +210,7 @@ def attach_traffic(roof, path, cfg, n):
         roof["traffic"] = tr["dominant_GB"]
         roof["traffic_unit"] = "GB per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)"
         roof["path_traffic_GB"] = tr["path_GB"]
+        roof["runtime_fill_copy_GB"] = tr["runtime_fill_copy_GB"]
         roof["traffic_source"] = tr["source"]
     else:
         roof["traffic_note"] = why
