@@ -1564,7 +1564,7 @@ __global__ void k_nge_blocks(Virt v, int64_t nt, T* __restrict__ best, uint8_t* 
 
 template <class T, int OP>
 __global__ void __launch_bounds__(256) k_nge(Virt v, int64_t nt, int64_t within, int op, uint32_t* __restrict__ mj,
-                                             uint32_t* __restrict__ mflag, uint32_t* __restrict__ cnt,
+                                             uint32_t* __restrict__ rank, uint32_t* __restrict__ cnt,
                                              uint32_t* __restrict__ st_flags, const T* __restrict__ best,
                                              const uint8_t* __restrict__ has) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nt; p += (int64_t)gridDim.x * blockDim.x) {
@@ -1597,32 +1597,42 @@ __global__ void __launch_bounds__(256) k_nge(Virt v, int64_t nt, int64_t within,
       }
     }
     mj[p] = j;
-    mflag[p] = j != NGE_NONE ? 1u : 0u;
-    if (j != NGE_NONE) atomicAdd(&cnt[j - v.nc], 1u);
+    if (j != NGE_NONE) rank[p] = atomicAdd(&cnt[j - v.nc], 1u);   // (rank among the trigger's matches: any order)
   }
 }
 
-static __global__ void k_nge_pairs(int64_t nt, uint32_t nc, const uint32_t* __restrict__ mj, const uint32_t* __restrict__ mpos,
-                            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+// every match to its delivery slot: the trigger's offset + the rank the search drew; then each trigger's matches in
+// pending (= arrival) order of their partials
+template <class T>
+__global__ void k_nge_place(Virt v, int64_t nt, const uint32_t* __restrict__ mj, const uint32_t* __restrict__ rank,
+                            const uint32_t* __restrict__ off, MRec* __restrict__ mrec) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nt; p += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t j = mj[p];
     if (j == NGE_NONE) continue;
-    keys[mpos[p]] = j - nc;
-    vals[mpos[p]] = (uint32_t)p;
+    MRec m;
+    m.r1 = (uint32_t)p;
+    m.r2 = j;
+    m.v1 = val_bits<T>(v_val<T>(v, (uint32_t)p, true));
+    m.p1 = v.pcol ? v_payload(v, (uint32_t)p) : 0;
+    mrec[off[j - v.nc] + rank[p]] = m;
   }
 }
 
-template <class T>
-__global__ void k_nge_mrec(Virt v, int64_t total, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
-                           MRec* __restrict__ mrec) {
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = svals[s];
-    MRec m;
-    m.r1 = p;
-    m.r2 = skeys[s] + (uint32_t)v.nc;
-    m.v1 = val_bits<T>(v_val<T>(v, p, true));
-    m.p1 = v.pcol ? v_payload(v, p) : 0;
-    mrec[s] = m;
+static __global__ void k_nge_order(int64_t n, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
+                                   MRec* __restrict__ mrec) {
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = cnt[b];
+    if (c < 2) continue;
+    MRec* e = mrec + off[b];
+    for (uint32_t i = 1; i < c; ++i) {
+      const MRec x = e[i];
+      uint32_t k = i;
+      while (k > 0 && e[k - 1].r1 > x.r1) {
+        e[k] = e[k - 1];
+        --k;
+      }
+      e[k] = x;
+    }
   }
 }
 
@@ -1665,20 +1675,18 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   const int b_state = d.shape_args[1];
   auto grid = [](int64_t m) { return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 256 * 16))); };
   uint32_t* mj = (uint32_t*)h->ws.get("nge_mj", 4 * nt, st);
-  uint32_t* mflag = (uint32_t*)h->ws.get("nge_mflag", 4 * (nt + 1), st);
-  uint32_t* mpos = (uint32_t*)h->ws.get("nge_mpos", 4 * (nt + 1), st);
+  uint32_t* rank = (uint32_t*)h->ws.get("nge_rank", 4 * nt, st);
   uint32_t* cnt = (uint32_t*)h->ws.get("cnt", sizeof(uint32_t) * (n + 1), st);
   uint32_t* off = (uint32_t*)h->ws.get("off", sizeof(uint32_t) * (n + 1), st);
   uint32_t* stf = (uint32_t*)h->ws.get("nge_flags", 8, st);
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
-  HIPCHK(hipMemsetAsync(mflag + nt, 0, 4, st));
   HIPCHK(hipMemsetAsync(stf, 0, 8, st));
   const int64_t nb = (nt + 63) >> 6;
   T* best = (T*)h->ws.get("nge_best", sizeof(T) * (nb + 1), st);
   uint8_t* has = (uint8_t*)h->ws.get("nge_has", nb + 1, st);
 #define SG_NGE_LAUNCH(OPV)                                                                                       \
   hipLaunchKernelGGL((k_nge_blocks<T, OPV>), grid(nb), dim3(256), 0, st, v, nt, best, has);                     \
-  hipLaunchKernelGGL((k_nge<T, OPV>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, mflag, cnt, stf, best, has)
+  hipLaunchKernelGGL((k_nge<T, OPV>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, rank, cnt, stf, best, has)
   h->kbeg("nge_search");
   switch (op) {
     case 2: SG_NGE_LAUNCH(2); break;
@@ -1691,35 +1699,21 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   h->kend();
   h->mark(2);
   size_t tb = 0;
-  HIPCHK(rocprim::exclusive_scan(nullptr, tb, mflag, mpos, (uint32_t)0, (size_t)nt + 1, rocprim::plus<uint32_t>(), st));
-  void* tmp = h->ws.get("nge_scan_tmp", tb, st);
-  HIPCHK(rocprim::exclusive_scan(tmp, tb, mflag, mpos, (uint32_t)0, (size_t)nt + 1, rocprim::plus<uint32_t>(), st));
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+  void* tmp = h->ws.get("scan_tmp", tb, st);
+  HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
   uint32_t hflags[2] = {0, 0};
   uint32_t total = 0;
   HIPCHK(hipMemcpyAsync(hflags, stf, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&total, mpos + nt, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&total, off + n, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (hflags[0]) throw SgError(SG_EORDER, "closed-form kernel requires non-decreasing timestamps per key");
   if (hflags[1]) return false;   // a search outgrew NGE_MAX_SCAN: the walker takes this push
-  tb = 0;
-  HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-  tmp = h->ws.get("scan_tmp", tb, st);
-  HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
   MRec* mrec = nullptr;
   if (total) {
-    uint32_t* keys = (uint32_t*)h->ws.get("nge_keys", 4 * total, st);
-    uint32_t* vals = (uint32_t*)h->ws.get("nge_vals", 4 * total, st);
-    uint32_t* skeys = (uint32_t*)h->ws.get("nge_skeys", 4 * total, st);
-    uint32_t* svals = (uint32_t*)h->ws.get("nge_svals", 4 * total, st);
-    hipLaunchKernelGGL(k_nge_pairs, grid(nt), dim3(256), 0, st, nt, (uint32_t)nc, mj, mpos, keys, vals);
-    int end_bit = 1;
-    while (end_bit < 32 && (1ull << end_bit) <= (uint64_t)n) ++end_bit;
-    tb = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, keys, skeys, vals, svals, (size_t)total, 0, end_bit, st));
-    tmp = h->ws.get("nge_sort_tmp", tb, st);
-    HIPCHK(rocprim::radix_sort_pairs(tmp, tb, keys, skeys, vals, svals, (size_t)total, 0, end_bit, st));
     mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * total, st);
-    hipLaunchKernelGGL((k_nge_mrec<T>), grid(total), dim3(256), 0, st, v, (int64_t)total, skeys, svals, mrec);
+    hipLaunchKernelGGL((k_nge_place<T>), grid(nt), dim3(256), 0, st, v, nt, mj, rank, off, mrec);
+    hipLaunchKernelGGL(k_nge_order, grid(n), dim3(256), 0, st, n, cnt, off, mrec);
     HIPCHK(hipGetLastError());
   }
   h->mark(3);
