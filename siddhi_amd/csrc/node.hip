@@ -30,6 +30,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "keydict.h"
@@ -50,6 +51,29 @@ namespace {
 
 const int NODE_RING = 3;   // host route/staging slots (chunk j reuses slot j % 3 once chunk j-3 is uploaded+merged)
 const int MAX_GPUS = 16;
+
+// non-temporal store of a 1/4/8-byte value (movnti for 4/8 bytes; a byte goes through the cache): host columns
+// written once and read next by a DMA or by the caller skip the read-for-ownership of their lines
+template <class V>
+inline void nt_store(V* p, V v) {
+  if constexpr (sizeof(V) == 4 || sizeof(V) == 8) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+// where the node uses them (SG_NODE_NT bit mask, read once): 1 the host fill of trigger-row columns, 2 the G > 1
+// scatter into shard staging, 4 the G > 1 merge's own column writes.  Default 1.  (A/B runs of the bits on one box,
+// profiles/r04/node_nt_ab.log, were inside the host stages' own run-to-run spread of up to 2x.)
+inline int nt_mode() {
+  static const int m = [] {
+    const char* e = getenv("SG_NODE_NT");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
+}
+template <int BIT, class V>
+inline void put(V* p, V v) {
+  if (nt_mode() & BIT) nt_store(p, v);
+  else *p = v;
+}
 
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -307,19 +331,19 @@ inline void fill_row(const sg_node_batch& b, const sg_nfa_desc& d, const Want& w
         nul = nd->hist_nul.empty() ? 0 : nd->hist_nul[(size_t)((int64_t)g - nd->hist_lo)];
       }
       if (out->cols[k]) {
-        if (w.width[k] == 8) ((int64_t*)out->cols[k])[o] = v;
-        else ((int32_t*)out->cols[k])[o] = (int32_t)v;
+        if (w.width[k] == 8) put<1>(&((int64_t*)out->cols[k])[o], v);
+        else put<1>(&((int32_t*)out->cols[k])[o], (int32_t)v);
       }
       if (out->nulls[k]) out->nulls[k][o] = nul;
     }
   }
-  if (w.fill_ts) out->ts[o] = b.ts[t];
+  if (w.fill_ts) put<1>(&out->ts[o], b.ts[t]);
   for (int k = 0; k < w.ns; ++k) {
     const int c = w.fill_col[k];
     if (c < 0) continue;
     if (out->cols[k]) {
-      if (w.width[k] == 8) ((int64_t*)out->cols[k])[o] = ((const int64_t*)b.cols[c])[t];
-      else ((int32_t*)out->cols[k])[o] = ((const int32_t*)b.cols[c])[t];
+      if (w.width[k] == 8) put<1>(&((int64_t*)out->cols[k])[o], ((const int64_t*)b.cols[c])[t]);
+      else put<1>(&((int32_t*)out->cols[k])[o], ((const int32_t*)b.cols[c])[t]);
     }
     if (out->nulls[k]) out->nulls[k][o] = (b.nulls && b.nulls[c]) ? b.nulls[c][t] : 0;
   }
@@ -534,7 +558,7 @@ void route_chunk_dev(Run& r, int64_t j) {
       for (int q = 0; q < G; ++q) cur[q] = off[t][q];
       for (int64_t i = a; i < e; ++i) {
         const int q = shp[i];
-        dst[q][cur[q]++] = val(i);
+        put<2>(&dst[q][cur[q]++], val(i));
       }
     };
     const int64_t* ts = r.b.ts + lo;
@@ -584,6 +608,7 @@ void route_chunk_dev(Run& r, int64_t j) {
         scatter(dn, [&](int64_t i) { return sn[i]; });
       }
     }
+    std::atomic_thread_fence(std::memory_order_seq_cst);   // (streaming stores drained before the chunk is published)
   });
 }
 
@@ -1080,21 +1105,22 @@ void merge_chunk(Run& r, int64_t j) {
       const int s = best;
       const NodeRing& R = nd.ring[s];
       const int64_t p = q[s];
-      if (r.out->trigger) r.out->trigger[o] = head[s];
-      if (w.ts) r.out->ts[o] = R.ts.as<int64_t>()[p];
+      if (r.out->trigger) put<4>(&r.out->trigger[o], head[s]);
+      if (w.ts) put<4>(&r.out->ts[o], R.ts.as<int64_t>()[p]);
       if (w.any_fill) fill_row(r.b, nd.desc, w, r.out, o, head[s]);
-      if (r.out->key) r.out->key[o] = (int32_t)gkey(s, p);
-      if (r.out->group) r.out->group[o] = R.grp.as<uint32_t>()[p];
+      if (r.out->key) put<4>(&r.out->key[o], (int32_t)gkey(s, p));
+      if (r.out->group) put<4>(&r.out->group[o], R.grp.as<uint32_t>()[p]);
       for (int c = 0; c < w.ns; ++c) {
         if (w.col[c]) {
-          if (w.width[c] == 8) ((int64_t*)r.out->cols[c])[o] = R.col[c].as<int64_t>()[p];
-          else ((int32_t*)r.out->cols[c])[o] = R.col[c].as<int32_t>()[p];
+          if (w.width[c] == 8) put<4>(&((int64_t*)r.out->cols[c])[o], R.col[c].as<int64_t>()[p]);
+          else put<4>(&((int32_t*)r.out->cols[c])[o], R.col[c].as<int32_t>()[p]);
         }
         if (w.nul[c]) r.out->nulls[c][o] = R.nul[c].as<uint8_t>()[p];
       }
       if (++q[s] == R.M) q[s] = 0;
       head[s] = --left[s] > 0 ? gidx[s][trig[s][q[s]] - lbase[s]] : ~0ull;
     }
+    std::atomic_thread_fence(std::memory_order_seq_cst);
   });
   r.out_rows += total;
 }
@@ -1126,6 +1152,7 @@ void fill_loop(Run& r) {
             }
             fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o], &nd);
           }
+          std::atomic_thread_fence(std::memory_order_seq_cst);
         });
       }
       r.publish([&] {
