@@ -566,13 +566,13 @@ __global__ void k_pp_wsum(int64_t m, PpPacked P, uint32_t slots, uint32_t fslots
 }
 
 constexpr int PP_BLOCK = 256;
-constexpr int64_t PP_WAVE_CANDS = 2048;   // start rows per wave
+constexpr int64_t PP_WAVE_CANDS = 512;    // start rows per wave (C3c sweep 128..8192: 512 and below 20.4-20.5 ms, 2048 21.5, 8192 26.0; profiles/r04/lanes_ab.log)
 template <class G>
 __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                        const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ cand,
                                                        int64_t ncand, const uint32_t* __restrict__ skey,
                                                        const uint32_t* __restrict__ sid, const uint32_t* __restrict__ end,
-                                                       PpOut o) {
+                                                       PpOut o, int64_t wave_cands) {
   // the descriptor (9.6 KB) stays in global memory (cache-resident: every lane reads the same few hundred bytes of
   // it), so LDS holds more lanes
   __shared__ SgPpRule rl;
@@ -591,8 +591,8 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   // wave never waits on its longest partial (ballot + popcount hand-out, no atomics)
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t lo = wave * PP_WAVE_CANDS;
-  const int64_t hi = lo + PP_WAVE_CANDS < ncand ? lo + PP_WAVE_CANDS : ncand;
+  const int64_t lo = wave * wave_cands;
+  const int64_t hi = lo + wave_cands < ncand ? lo + wave_cands : ncand;
   if (lo >= ncand) return;
   PpSrc src{&pl};
   PpLane<PpSrc, G> L;
@@ -1697,13 +1697,18 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   }
   h->kbeg("partial_lanes");
   if (ncand) {
-    const dim3 gl((unsigned)((ncand + PP_WAVE_CANDS * (PP_BLOCK / 64) - 1) / (PP_WAVE_CANDS * (PP_BLOCK / 64))));
+    static const int64_t wcands = [] {   // (experiments: SG_PP_WAVE_CANDS)
+      const char* e = getenv("SG_PP_WAVE_CANDS");
+      const int64_t x = e ? atoll(e) : 0;
+      return x >= 64 ? x : PP_WAVE_CANDS;
+    }();
+    const dim3 gl((unsigned)((ncand + wcands * (PP_BLOCK / 64) - 1) / (wcands * (PP_BLOCK / 64))));
     if (ps->pp_small)
       hipLaunchKernelGGL(k_pp_lanes<PpSmall>, gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand, (int64_t)ncand,
-                         skeys, sids, end, o);
+                         skeys, sids, end, o, wcands);
     else
       hipLaunchKernelGGL(k_pp_lanes<PpBig>, gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand, (int64_t)ncand,
-                         skeys, sids, end, o);
+                         skeys, sids, end, o, wcands);
   }
   HIPCHK(hipGetLastError());
   h->kend();
