@@ -1203,15 +1203,33 @@ __global__ void k_em_dest(int64_t n, const uint32_t* __restrict__ idx, uint32_t*
 }
 
 // Partial lanes: slot order is start-row order, i.e. key-ordered, so walking the slots reads the compact records and
-// the packed rows they point at nearly coalesced; each record is then written to its delivery position
-__global__ void k_em_scatter(int64_t T, const uint32_t* __restrict__ dest, const char* __restrict__ em, int32_t estride,
-                             char* __restrict__ out, int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
-                             const uint64_t* __restrict__ index, uint64_t base_index) {
+// the packed rows they point at nearly coalesced; each record is then written to its delivery position.  The block's
+// records are assembled in LDS first and written out by consecutive threads taking consecutive 8-byte words of the
+// same record, so one store instruction covers whole records instead of one word of 64 scattered ones.
+__global__ void __launch_bounds__(256) k_em_scatter(int64_t T, const uint32_t* __restrict__ dest,
+                                                    const char* __restrict__ em, int32_t estride, char* __restrict__ out,
+                                                    int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
+                                                    const uint64_t* __restrict__ index, uint64_t base_index) {
+  extern __shared__ __align__(16) char em_lds[];
+  __shared__ uint32_t dl[256];
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= T) return;
-  const uint32_t d = dest[w];
-  if (d == 0xFFFFFFFFu) return;
-  em_build((const uint32_t*)(em + (size_t)w * estride), out + (size_t)d * ostride, P, dd, index, base_index);
+  uint32_t d = 0xFFFFFFFFu;
+  if (w < T) {
+    d = dest[w];
+    if (d != 0xFFFFFFFFu)
+      em_build((const uint32_t*)(em + (size_t)w * estride), em_lds + (size_t)threadIdx.x * ostride, P, dd, index,
+               base_index);
+  }
+  dl[threadIdx.x] = d;
+  __syncthreads();
+  const int words = ostride / 8;
+  const int all = (int)blockDim.x * words;
+  for (int x = threadIdx.x; x < all; x += blockDim.x) {
+    const int rec = x / words, wd = x - rec * words;
+    const uint32_t to = dl[rec];
+    if (to == 0xFFFFFFFFu) continue;
+    ((uint64_t*)(out + (size_t)to * ostride))[wd] = ((const uint64_t*)(em_lds + (size_t)rec * ostride))[wd];
+  }
 }
 
 // carry for sequence lanes: the last H rows of every key
@@ -1272,6 +1290,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   SqPlan pl_;
   const int64_t H = ps->srule.horizon;
   pl_.R = std::max<int64_t>(64, (n + 262143) / 262144);
+  if (const char* e = getenv("SG_SQ_ROWS")) pl_.R = std::max<int64_t>(16, atoll(e));   // (experiments)
   if (h->opt.chunk_rows > 0) pl_.R = h->opt.chunk_rows;
   pl_.W = std::max<int64_t>(4 * H, 16);
   uint32_t* ncar = (uint32_t*)h->ws.get("sq_ncar", 4 * ((size_t)kb + 1), st);
@@ -1781,8 +1800,8 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     uint32_t* dest = (uint32_t*)h->ws.get("pp_dest", 4 * (size_t)(T + 1), st);
     HIPCHK(hipMemsetAsync(dest, 0xFF, 4 * (size_t)T, st));
     hipLaunchKernelGGL(k_em_dest, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, ia, dest);
-    hipLaunchKernelGGL(k_em_scatter, g2, blk, 0, st, T, dest, o.rec, o.rstride, out + (size_t)h->out.n * rstride, rstride,
-                       P, h->ddesc, bv.index, bv.base_index);
+    hipLaunchKernelGGL(k_em_scatter, g2, blk, (size_t)256 * rstride, st, T, dest, o.rec, o.rstride,
+                       out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());
     h->kend();
     h->out.n += M;
