@@ -319,7 +319,20 @@ SG_HD inline bool sg_pp_small(const SgPpRule& r, const sg_nfa_desc& d) {
   return chain <= PpSmall::CH;
 }
 
-template <class Src, class G = PpBig>
+// Every filter the lane evaluates is a list of fast compares or an event-local bit (sg_terms_fast): FAST lanes are
+// compiled without the postfix VM and the SgVal compare, which shrinks the lane kernel's code to its hot loop.
+template <class R>
+SG_HD inline bool sg_terms_fast(const R& r, int n_states) {
+  for (int s = 0; s < n_states; ++s) {
+    if ((r.local_mask >> s) & 1u) continue;   // the GPU reads these from the packed condition bits, never the VM
+    if (r.nterm[s] < 0) return false;
+    for (int i = 0; i < r.nterm[s]; ++i)
+      if (!r.term[s][i].fast) return false;
+  }
+  return true;
+}
+
+template <class Src, class G = PpBig, bool FAST = false>
 struct PpLane {
   const sg_nfa_desc* d;
   const SgPpRule* ru;
@@ -416,6 +429,21 @@ struct PpLane {
       if (b >= 0) return b != 0;
     }
     const int nt = ru->nterm[s];
+    if (FAST) {   // sg_terms_fast: every term is a fast compare
+      for (int i = 0; i < nt; ++i) {
+        const PpTerm& t = ru->term[s][i];
+        int64_t a, b;
+        int na, nb;
+        operand_bits(t.l, a, na);
+        operand_bits(t.r, b, nb);
+        if (na || nb) {
+          if (t.op != 1) return false;
+          continue;
+        }
+        if (!(t.fast == 1 ? pp_cmp_i(t.op, a, b) : pp_cmp_f(t.op, pp_f32(a), pp_f32(b)))) return false;
+      }
+      return true;
+    }
     if (nt >= 0) {
       for (int i = 0; i < nt; ++i) {
         const PpTerm& t = ru->term[s][i];

@@ -65,6 +65,7 @@ struct PartialState {
                                 // lists being unbounded, C/query/input/stream/state/StreamPreStateProcessor.java:57-58)
   int sq_small = 0;             // the query fits seq.h's small state geometry (SqSmall)
   int pp_small = 0;             // the query fits chain.h's small lane geometry (PpSmall)
+  int lanes_fast = 0;           // every filter is fast compares or event-local bits (chain.h sg_terms_fast)
   size_t sq_bytes = sizeof(SeqState);
   int64_t kst_keys = 0;
   int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
@@ -107,6 +108,15 @@ static void rows_reserve(PartialState* ps, PpRows& r, int64_t need) {
   r = nr;
 }
 
+// FAST lane kernels unless SG_LANES_NO_FAST=1 (A/B runs)
+static bool lanes_fast(const PartialState* ps) {
+  static const bool off = [] {
+    const char* e = getenv("SG_LANES_NO_FAST");
+    return e && e[0] == '1';
+  }();
+  return ps->lanes_fast && !off;
+}
+
 PartialState* sg_partial_new(const sg_nfa_desc& d) {
   SgPpRule ru = sg_pp_rule(d);
   SgSeqRule sr = sg_seq_rule(d);
@@ -125,6 +135,7 @@ PartialState* sg_partial_new(const sg_nfa_desc& d) {
     if (hipMalloc(&ps->dsrule, sizeof(SgSeqRule)) != hipSuccess) { delete ps; throw SgError(SG_EHIP, "hipMalloc rule"); }
     hipMemcpy(ps->dsrule, &ps->srule, sizeof(SgSeqRule), hipMemcpyHostToDevice);
   }
+  ps->lanes_fast = (ps->mode == 2 ? sg_terms_fast(sr, d.n_states) : sg_terms_fast(ru, d.n_states)) ? 1 : 0;
   for (int s = 0; s < d.n_states; ++s) ps->has_count |= d.states[s].kind == SG_K_COUNT;
   for (int k = 0; k < d.n_ret; ++k) {
     const int c = d.ret_col[k];
@@ -567,7 +578,7 @@ __global__ void k_pp_wsum(int64_t m, PpPacked P, uint32_t slots, uint32_t fslots
 
 constexpr int PP_BLOCK = 256;
 constexpr int64_t PP_WAVE_CANDS = 512;    // start rows per wave (C3c sweep 128..8192: 512 and below 20.4-20.5 ms, 2048 21.5, 8192 26.0; profiles/r04/lanes_ab.log)
-template <class G>
+template <class G, bool FAST = false>
 __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                        const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ cand,
                                                        int64_t ncand, const uint32_t* __restrict__ skey,
@@ -595,7 +606,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   const int64_t hi = lo + wave_cands < ncand ? lo + wave_cands : ncand;
   if (lo >= ncand) return;
   PpSrc src{&pl};
-  PpLane<PpSrc, G> L;
+  PpLane<PpSrc, G, FAST> L;
   L.d = dd;
   L.ru = &rl;
   L.src = src;
@@ -1028,7 +1039,7 @@ __device__ __forceinline__ void sq_run(Mach& m, int64_t b0, int64_t q0, int64_t 
   }
 
 // pass A: every unit from its (guessed) start state, emitting; its start and end states are kept for the check
-template <class G>
+template <class G, bool FAST = false>
 __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                       const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
                                                       SqPlan pl_, SqOut o) {
@@ -1040,7 +1051,7 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
   const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
   const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
   SeqStateT<G>& M = lanes[threadIdx.x];
-  SeqMachine<SeqSrcD, G> m;
+  SeqMachine<SeqSrcD, G, FAST> m;
   m.d = &dl;
   m.ru = &rl;
   m.src = SeqSrcD{&pl, b0};
@@ -1343,7 +1354,9 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   HIPCHK(hipMemsetAsync(o.rerun, 0, 4 * ((size_t)U + 1), st));
   if (attempt) HIPCHK(hipMemsetAsync(o.reserved, 0, 64, st));
   h->kbeg("sequence_lanes");
-  if (U && ps->sq_small) hipLaunchKernelGGL(k_sq_spec<SqSmall>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
+  if (U && ps->sq_small && lanes_fast(ps))
+    hipLaunchKernelGGL((k_sq_spec<SqSmall, true>), gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
+  else if (U && ps->sq_small) hipLaunchKernelGGL(k_sq_spec<SqSmall>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
   else if (U) hipLaunchKernelGGL(k_sq_spec<SqBig>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
   HIPCHK(hipGetLastError());
   h->kend();
@@ -1722,7 +1735,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
       return x >= 64 ? x : PP_WAVE_CANDS;
     }();
     const dim3 gl((unsigned)((ncand + wcands * (PP_BLOCK / 64) - 1) / (wcands * (PP_BLOCK / 64))));
-    if (ps->pp_small)
+    if (ps->pp_small && lanes_fast(ps))
+      hipLaunchKernelGGL((k_pp_lanes<PpSmall, true>), gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand,
+                         (int64_t)ncand, skeys, sids, end, o, wcands);
+    else if (ps->pp_small)
       hipLaunchKernelGGL(k_pp_lanes<PpSmall>, gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand, (int64_t)ncand,
                          skeys, sids, end, o, wcands);
     else

@@ -136,7 +136,7 @@ SG_HD inline bool sg_seq_small(const SgSeqRule& r, const sg_nfa_desc& d) {
 
 // Src: int64_t ts(int64_t pos); SgVal read(int64_t pos, int ret_slot, int type); int lbit(int s, int64_t pos) (-1: VM)
 // Sink: void emit(int group, int64_t pts, ...) receives the machine itself (see SeqMachine::emit)
-template <class Src, class G = SqBig>
+template <class Src, class G = SqBig, bool FAST = false>   // FAST: see chain.h sg_terms_fast
 struct SeqMachine {
   const sg_nfa_desc* d;
   const SgSeqRule* ru;
@@ -266,8 +266,23 @@ struct SeqMachine {
       const int b = src.lbit(s, cur);
       if (b >= 0) return b != 0;
     }
-    Reader rd{this, p};
     const int nt = ru->nterm[s];
+    if (FAST) {
+      for (int i = 0; i < nt; ++i) {
+        const PpTerm& t = ru->term[s][i];
+        int64_t a, b;
+        int na, nb;
+        operand_bits(p, t.l, a, na);
+        operand_bits(p, t.r, b, nb);
+        if (na || nb) {
+          if (t.op != 1) return false;
+          continue;
+        }
+        if (!(t.fast == 1 ? pp_cmp_i(t.op, a, b) : pp_cmp_f(t.op, pp_f32(a), pp_f32(b)))) return false;
+      }
+      return true;
+    }
+    Reader rd{this, p};
     if (nt >= 0) {
       for (int i = 0; i < nt; ++i) {
         const PpTerm& t = ru->term[s][i];
