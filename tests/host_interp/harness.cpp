@@ -413,6 +413,10 @@ int64_t hi_pp_steps(HiHandle* h, int64_t* lanes) { *lanes = h->pp_lanes; return 
 int64_t hi_pp_skipped(HiHandle* h) { return h->pp_skipped; }
 int hi_seq_rule(const sg_nfa_desc* d) { return sg_seq_rule(*d).ok; }
 int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
+// the lane kernels' FAST variant applies (chain.h sg_terms_fast): seq = 1 for the sequence-lane rule
+int hi_terms_fast(const sg_nfa_desc* d, int seq) {
+  return seq ? sg_terms_fast(sg_seq_rule(*d), d->n_states) : sg_terms_fast(sg_pp_rule(*d), d->n_states);
+}
 
 HiHandle* hi_open(const sg_nfa_desc* d, int P, int E, int C, int L) {
   HiHandle* h = new HiHandle();

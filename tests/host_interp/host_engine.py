@@ -44,6 +44,8 @@ def _load():
         lib.hi_pp_rule.argtypes = [P]
         lib.hi_seq_rule.restype = ct.c_int
         lib.hi_seq_rule.argtypes = [P]
+        lib.hi_terms_fast.restype = ct.c_int
+        lib.hi_terms_fast.argtypes = [P, ct.c_int]
         lib.hi_set_spec.argtypes = [P, ct.c_int64, ct.c_int64]
         lib.hi_spec_reruns.restype = ct.c_int64
         lib.hi_spec_reruns.argtypes = [P]

@@ -55,6 +55,9 @@ SEQ_SHAPES = {
                           "select e1.id as i1, e2.id as i2, e3.id as i3, e4.id as i4 insert into M; end;",
     "seq_last_ref": PART + "from every e1=S[v>40], e2=S[v>=e1.v]<1:3>, e3=S[v<e2[last].v and w>e1.w] "
                            "select e1.id as i1, e2[last].id as z, e3.id as i3 insert into M; end;",
+    # arithmetic in a cross-event filter: the postfix VM, so the general (non-FAST) sequence kernel
+    "seq_cross": PART + "from every e1=S[v>50], e2=S[v>e1.v], e3=S[v+w>e2.v+e1.w] "
+                        "select e1.id as i1, e2.id as i2, e3.id as i3 insert into M; end;",
 }
 UNPART_SEQ = ("@info(name='q') from every e1=S[v>50], e2=S[v>e1.v]<1:3>, e3=S[w<e1.w] "
               "select e1.id as i1, e2[last].id as z, e3.id as i3 insert into M;")
@@ -173,6 +176,18 @@ def test_seq_rule_covers_the_shapes():
         d = N.build_desc(L.lower(context(synth.QUERIES[cfg])))
         assert lib.hi_seq_rule(ct.byref(d)) == ok, cfg
 
+
+
+def test_fast_lane_variant_choice():
+    """The lane kernels drop the postfix VM (chain.h sg_terms_fast) only when every filter that is not event-local is
+    a list of fast compares: C3c and C3b take that variant; the shapes tests keep both variants covered on the GPU."""
+    import ctypes as ct
+    lib = _load()
+    for cfg, seq in (("C3c", 0), ("C3b", 1)):
+        assert lib.hi_terms_fast(ct.byref(N.build_desc(L.lower(context(synth.QUERIES[cfg])))), seq) == 1, cfg
+    pp = {n: lib.hi_terms_fast(ct.byref(N.build_desc(L.lower(context(HEAD + q)))), 0) for n, q in SHAPES.items()}
+    sq = {n: lib.hi_terms_fast(ct.byref(N.build_desc(L.lower(context(HEAD + q)))), 1) for n, q in SEQ_SHAPES.items()}
+    assert sorted(set(pp.values())) == [0, 1] and sorted(set(sq.values())) == [0, 1], (pp, sq)
 
 @pytest.mark.parametrize("vmax", [10, 100])
 @pytest.mark.parametrize("name", sorted(SEQ_SHAPES))
