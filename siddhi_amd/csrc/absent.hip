@@ -73,10 +73,30 @@ struct AbsCarry {
   }
 };
 
+// The Scheduler's FIFO (C/util/Scheduler.java:49, a LinkedBlockingQueue) as carried between pushes: entries not yet
+// popped, in queue order.
+struct AbsQueue {
+  int64_t n = 0, cap = 0;
+  int64_t* v = nullptr;
+  void reserve(int64_t want) {
+    if (want <= cap) return;
+    int64_t* nv = nullptr;
+    const int64_t c = std::max<int64_t>(want + want / 4, 1024);
+    if (hipMalloc(&nv, c * 8) != hipSuccess) throw SgError(SG_EHIP, "hipMalloc failed for the absence timer queue");
+    if (v) hipFree(v);
+    v = nv;
+    cap = c;
+  }
+  void release() { if (v) hipFree(v); v = nullptr; n = cap = 0; }
+};
+
 struct AbsState {
   AbsCarry carry[2];
+  AbsQueue q[2];               // timer FIFO (with carry[cur]: q[cur])
   int cur = 0;
-  int64_t* dlast = nullptr;    // device: last timestamp seen (order check across pushes)
+  int64_t lst = 0;             // AbsentStreamPreStateProcessor.lastScheduledTime (Java default 0)
+  bool seq = false;            // the state is not the closed form's: the next push runs the exact sequential pass
+  int64_t* dlast = nullptr;    // device: the playback clock (largest timestamp seen; order check across pushes)
   int64_t* dminmax = nullptr;  // device: [min, max] of compared values (as order-preserving u64)
   uint32_t* dflag = nullptr;   // device: order error
 };
@@ -229,7 +249,7 @@ template <class K>
 __global__ void k_abs_kill(AbsArgs a, const K* __restrict__ skeys, const uint32_t* __restrict__ sid,
                            const uint8_t* __restrict__ role, const uint32_t* __restrict__ nks,
                            const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
-                           uint8_t* __restrict__ dead) {
+                           uint8_t* __restrict__ dead, uint32_t* __restrict__ kc) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nt; p += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t v = sid[p];
     const uint8_t r = role[v];
@@ -243,7 +263,10 @@ __global__ void k_abs_kill(AbsArgs a, const K* __restrict__ skeys, const uint32_
     }
     if (q == NONE || skeys[q] != skeys[p]) continue;
     const uint32_t vq = sid[q];
-    if (vts(a, ts, c_dl, vq) < vts(a, ts, c_dl, v) + a.W) dead[v] = 1;
+    if (vts(a, ts, c_dl, vq) < vts(a, ts, c_dl, v) + a.W) {
+      dead[v] = 1;
+      atomicAdd(&kc[vq - a.nc], 1u);   // (the killer's FIFO entries: one per partial it kills)
+    }
   }
 }
 
@@ -254,7 +277,7 @@ template <class K>
 __global__ void __launch_bounds__(256) k_abs_kill_fast(AbsArgs a, const K* __restrict__ skeys,
                                                        const uint32_t* __restrict__ sid, K sentinel,
                                                        const int64_t* __restrict__ ts, const int64_t* __restrict__ c_dl,
-                                                       uint8_t* __restrict__ dead) {
+                                                       uint8_t* __restrict__ dead, uint32_t* __restrict__ kc) {
 #if defined(__AMDGCN_WAVEFRONT_SIZE)
   static_assert(__AMDGCN_WAVEFRONT_SIZE == 64, "k_abs_kill_fast reads lane + 1 by a 64-wide shuffle (CDNA wave64)");
 #endif
@@ -271,17 +294,21 @@ __global__ void __launch_bounds__(256) k_abs_kill_fast(AbsArgs a, const K* __res
     const K k1 = __shfl_down(kp, 1, 64);
     if (!live) continue;
     int64_t tq = 0;
+    uint32_t vk = 0;
     bool found = false;
     int64_t x = p + 1;
     if (lane < 63 && x < a.nt) {
       if (k1 != kp) continue;   // no later row with this value
-      if (v1 >= (uint32_t)a.nc) { tq = t1; found = true; }
+      if (v1 >= (uint32_t)a.nc) { tq = t1; vk = v1; found = true; }
       else ++x;                 // a carried row: search on
     }
     if (!found)
       for (; x < a.nt && skeys[x] == kp; ++x)
-        if (sid[x] >= (uint32_t)a.nc) { tq = ts[sid[x] - a.nc]; found = true; break; }
-    if (found && tq < tv + a.W) dead[v] = 1;
+        if (sid[x] >= (uint32_t)a.nc) { vk = sid[x]; tq = ts[vk - a.nc]; found = true; break; }
+    if (found && tq < tv + a.W) {
+      dead[v] = 1;
+      atomicAdd(&kc[vk - a.nc], 1u);
+    }
   }
 }
 
@@ -384,6 +411,266 @@ __global__ void k_abs_last(int64_t n, const int64_t* __restrict__ ts, int64_t* _
   if (threadIdx.x == 0 && n > 0) *dlast = ts[n - 1];
 }
 
+// ---- FIFO after a closed-form push (no timestamp went back): every entry <= the clock has been popped; the rest
+// are the carried entries above it, then per row of this push its kill entries and its creation entry (all
+// ts + W: updateLastArrivalTime and addState, AbsentStreamPreStateProcessor.java:69-101) when above the clock
+__global__ void k_abs_qcount(int64_t nq, const int64_t* __restrict__ q, int64_t n, const int64_t* __restrict__ ts,
+                             const uint8_t* __restrict__ role, int64_t nc, const uint32_t* __restrict__ kc, int64_t W,
+                             int64_t clock, uint32_t* __restrict__ m) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e <= nq + n; e += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t c = 0;
+    if (e < nq) c = q[e] > clock ? 1u : 0u;
+    else if (e < nq + n) {
+      const int64_t i = e - nq;
+      if (ts[i] + W > clock) c = kc[i] + ((role[nc + i] & R_CAND) ? 1u : 0u);
+    }
+    m[e] = c;
+  }
+}
+__global__ void k_abs_qwrite(int64_t nq, const int64_t* __restrict__ q, int64_t n, const int64_t* __restrict__ ts,
+                             int64_t W, const uint32_t* __restrict__ m, const uint32_t* __restrict__ off,
+                             int64_t* __restrict__ out) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq + n; e += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = m[e];
+    const int64_t v = e < nq ? q[e] : ts[e - nq] + W;
+    for (uint32_t k = 0; k < c; ++k) out[off[e] + k] = v;
+  }
+}
+
+// ---- exact sequential pass: a push in which some timestamp goes back, or a state the closed form cannot continue.
+// The reference's per-row sequence for `every A -> not B[x == e1.x] for W` with the playback clock and the FIFO:
+//   setCurrentTimestamp(ts): if ts >= clock, clock = ts and, while the FIFO head <= clock, a timer pass at the head
+//     value T (TimestampGeneratorImpl.java:106-125, Scheduler.java:74-86,179-214): every pending partial with
+//     ts_i + W <= T is emitted stamped T, in pending order; then lastScheduledTime = clock + W if clock > T + W, and a
+//     pass that emitted nothing with lastScheduledTime < T schedules T + W (AbsentStreamPreStateProcessor.java:140-210);
+//   a B row kills every pending partial with its value, each kill scheduling ts + W (:230-244, AbsentStreamPost-
+//     StateProcessor.java:36-56); an A row opens a partial and schedules ts + W (:77-101).
+// One lane walks the rows (the FIFO makes the order of everything global); kills find their partials through a hash
+// of the compared value, timer passes skip 64-partial blocks whose earliest deadline is later than T.
+struct SeqAbs {
+  int64_t n, nc, W;
+  const int64_t* ts;
+  const uint8_t* role;
+  const int64_t* vals;         // virtual rows (carried partials first)
+  const int64_t* c_dl;         // carried partials' deadlines
+  // FIFO in: carried entries; ring capacity qcap (power of two)
+  const int64_t* q_in;
+  int64_t nq_in, qcap;
+  int64_t* ring;
+  // partials (creation order): deadline, value, source virtual row, alive; next with the same value
+  int64_t* pd;
+  uint32_t* psrc;
+  uint8_t* palive;
+  int32_t* pnext;
+  int64_t* bmin;               // per 64 partials: earliest deadline among the alive ones (or a stale lower bound)
+  // hash of values of killable partials
+  int64_t hcap;
+  int64_t* hkey;
+  int32_t* hhead;
+  int32_t* htail;
+  uint8_t* hused;
+  // emissions in delivery order: partial, trigger row, stamp, callback group
+  uint32_t* ek;
+  uint32_t* erow;
+  int64_t* ets;
+  uint32_t* eg;
+  int64_t ecap;
+  // scalars: [0] clock, [1] lastScheduledTime, [2] emissions, [3] partials, [4] ring head, [5] ring tail,
+  // [6] flags (1 capacity), [7] closed form can continue (1)
+  int64_t* sc;
+};
+
+__device__ __forceinline__ uint64_t sa_hash(int64_t x) {
+  uint64_t z = (uint64_t)x * 0x9E3779B97F4A7C15ull;
+  return z ^ (z >> 29);
+}
+
+__global__ void k_abs_seq(SeqAbs s) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t INF = INT64_MAX;
+  int64_t clock = s.sc[0], lst = s.sc[1];
+  int64_t ne = 0, np = 0, head = 0, tail = 0;
+  bool cap_bad = false;
+  const int64_t qmask = s.qcap - 1, hmask = s.hcap - 1;
+  auto qpush = [&](int64_t v) {
+    if (tail - head >= s.qcap) { cap_bad = true; return; }
+    s.ring[tail & qmask] = v;
+    ++tail;
+  };
+  auto hslot = [&](int64_t key, bool insert) -> int64_t {
+    int64_t h = (int64_t)(sa_hash(key) & (uint64_t)hmask);
+    for (int64_t probe = 0; probe < s.hcap; ++probe, h = (h + 1) & hmask) {
+      if (!s.hused[h]) {
+        if (!insert) return -1;
+        s.hused[h] = 1;
+        s.hkey[h] = key;
+        s.hhead[h] = -1;
+        s.htail[h] = -1;
+        return h;
+      }
+      if (s.hkey[h] == key) return h;
+    }
+    cap_bad = true;
+    return -1;
+  };
+  auto add_partial = [&](int64_t d, uint32_t src, bool killable, int64_t key) {
+    const int64_t k = np++;
+    s.pd[k] = d;
+    s.psrc[k] = src;
+    s.palive[k] = 1;
+    s.pnext[k] = -1;
+    const int64_t b = k >> 6;
+    if ((k & 63) == 0) s.bmin[b] = d;
+    else if (d < s.bmin[b]) s.bmin[b] = d;
+    if (killable) {
+      const int64_t h = hslot(key, true);
+      if (h < 0) return;
+      if (s.htail[h] < 0) s.hhead[h] = (int32_t)k; else s.pnext[s.htail[h]] = (int32_t)k;
+      s.htail[h] = (int32_t)k;
+    }
+  };
+  int64_t lob = 0;   // first block that may hold an alive partial
+  uint32_t cur_row = 0xffffffffu, grp = 0;
+  auto pass = [&](int64_t T, uint32_t row) -> bool {   // one timer pass; true if it emitted
+    bool any = false;
+    const int64_t nb = (np + 63) >> 6;
+    while (lob < nb && s.bmin[lob] == INF) ++lob;
+    for (int64_t b = lob; b < nb; ++b) {
+      if (s.bmin[b] > T) continue;
+      int64_t m = INF;
+      const int64_t k1 = (b + 1) * 64 < np ? (b + 1) * 64 : np;
+      for (int64_t k = b * 64; k < k1; ++k) {
+        if (!s.palive[k]) continue;
+        if (s.pd[k] <= T) {
+          s.palive[k] = 0;
+          if (row != cur_row) { cur_row = row; grp = 0; }
+          if (ne < s.ecap) { s.ek[ne] = (uint32_t)k; s.erow[ne] = row; s.ets[ne] = T; s.eg[ne] = grp; }
+          else cap_bad = true;
+          ++ne;
+          ++grp;
+          any = true;
+        } else if (s.pd[k] < m) {
+          m = s.pd[k];
+        }
+      }
+      s.bmin[b] = m;
+    }
+    return any;
+  };
+  for (int64_t k = 0; k < s.nq_in; ++k) qpush(s.q_in[k]);
+  for (int64_t k = 0; k < s.nc; ++k) {
+    const uint8_t r = s.role[k];
+    add_partial(s.c_dl[k], (uint32_t)k, (r & R_SORT) != 0, s.vals[k]);
+  }
+  for (int64_t i = 0; i < s.n && !cap_bad; ++i) {
+    const int64_t t = s.ts[i];
+    if (t >= clock) {
+      clock = t;
+      while (head < tail && s.ring[head & qmask] <= clock && !cap_bad) {
+        const int64_t T = s.ring[head & qmask];
+        ++head;
+        const bool emitted = pass(T, (uint32_t)i);
+        if (clock > s.W + T) lst = clock + s.W;
+        if (!emitted && lst < T) {
+          lst = T + s.W;
+          qpush(lst);
+        }
+      }
+    }
+    const int64_t v = s.nc + i;
+    const uint8_t r = s.role[v];
+    if (r & R_KILL) {
+      const int64_t h = hslot(s.vals[v], false);
+      if (h >= 0) {
+        for (int32_t k = s.hhead[h]; k >= 0; k = s.pnext[k]) {
+          if (!s.palive[k]) continue;
+          s.palive[k] = 0;   // (its block's earliest deadline becomes stale: a lower bound, refreshed by the next scan)
+          lst = t + s.W;
+          qpush(lst);
+        }
+        s.hhead[h] = -1;
+        s.htail[h] = -1;
+      }
+    }
+    if (r & R_CAND) {
+      add_partial(t + s.W, (uint32_t)v, (r & R_SORT) != 0, s.vals[v]);
+      lst = t + s.W;
+      qpush(lst);
+    }
+  }
+  // can the closed form continue from here?  its FIFO must be sorted and above the clock, and lastScheduledTime at
+  // least its largest entry (then no later pass re-schedules while time moves forward)
+  bool ok = true;
+  int64_t prev = INT64_MIN;
+  for (int64_t k = head; k < tail; ++k) {
+    const int64_t x = s.ring[k & qmask];
+    if (x < prev || x <= clock || x > lst) { ok = false; break; }
+    prev = x;
+  }
+  s.sc[0] = clock;
+  s.sc[1] = lst;
+  s.sc[2] = ne;
+  s.sc[3] = np;
+  s.sc[4] = head;
+  s.sc[5] = tail;
+  s.sc[6] = cap_bad ? 1 : 0;
+  s.sc[7] = ok ? 1 : 0;
+}
+
+// FIFO ring [head, tail) -> a flat queue
+__global__ void k_abs_qflat(const int64_t* __restrict__ ring, int64_t qcap, const int64_t* __restrict__ sc,
+                            int64_t* __restrict__ out) {
+  const int64_t head = sc[4], tail = sc[5];
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tail - head; k += (int64_t)gridDim.x * blockDim.x)
+    out[k] = ring[(head + k) & (qcap - 1)];
+}
+
+// partials still alive -> carried partials (creation order); emissions -> match records
+__global__ void k_abs_seq_alive(int64_t np, const uint8_t* __restrict__ palive, uint32_t* __restrict__ flag) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= np; k += (int64_t)gridDim.x * blockDim.x)
+    flag[k] = k < np ? palive[k] : 0u;
+}
+__global__ void k_abs_seq_carry(AbsArgs a, AbsOut o, SgCols cols, const int64_t* __restrict__ ts, int64_t np,
+                                const uint32_t* __restrict__ flag, const uint32_t* __restrict__ off,
+                                const uint32_t* __restrict__ psrc, const int64_t* __restrict__ pd,
+                                const int64_t* __restrict__ vals, const uint8_t* __restrict__ role, AbsCarry cin,
+                                AbsCarry cout) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < np; k += (int64_t)gridDim.x * blockDim.x) {
+    if (!flag[k]) continue;
+    const uint32_t v = psrc[k], cs = off[k];
+    const bool carried = v < a.nc;
+    const int64_t i = (int64_t)v - a.nc;
+    uint32_t nm = carried ? cin.snul[v] : 0u;
+    cout.dl[cs] = pd[k];
+    cout.val[cs] = vals[v];
+    cout.vnul[cs] = (role[v] & R_SORT) ? 0 : 1;
+    for (int s = 0; s < o.n_select; ++s)
+      cout.sel[(int64_t)cs * o.n_select + s] = carried ? cin.sel[(int64_t)v * o.n_select + s] : abs_sel(o, cols, s, i, nm);
+    cout.snul[cs] = nm;
+  }
+}
+__global__ void k_abs_seq_write(AbsArgs a, AbsOut o, SgCols cols, int64_t ne, const uint32_t* __restrict__ ek,
+                                const uint32_t* __restrict__ erow, const int64_t* __restrict__ ets,
+                                const uint32_t* __restrict__ eg, const uint32_t* __restrict__ psrc, AbsCarry cin,
+                                char* __restrict__ out) {
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < ne; x += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = psrc[ek[x]];
+    const bool carried = v < a.nc;
+    const int64_t i = (int64_t)v - a.nc;
+    uint32_t nm = carried ? cin.snul[v] : 0u;
+    int64_t* r = (int64_t*)(out + (size_t)x * o.stride);
+    for (int s = 0; s < o.n_select; ++s) {
+      int64_t y = carried ? cin.sel[(int64_t)v * o.n_select + s] : abs_sel(o, cols, s, i, nm);
+      r[4 + s] = (nm >> s) & 1 ? 0 : y;
+    }
+    const uint32_t t = erow[x];
+    r[0] = (int64_t)(o.index ? o.index[t] : o.base_index + t);
+    r[1] = ets[x];
+    r[2] = (int64_t)((uint64_t)eg[x] << 32);
+    r[3] = (int64_t)nm;
+  }
+}
+
 AbsState* astate(SgHandle* h) {
   if (!h->state) {
     AbsState* s = new AbsState();
@@ -401,7 +688,7 @@ unsigned grid_red(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<in
 
 template <class K>
 void sort_and_kill(SgHandle* h, const AbsArgs& a, uint64_t omin, int bits, const uint8_t* role, const int64_t* vals,
-                   const int64_t* ts, const int64_t* c_dl, uint8_t* dead) {
+                   const int64_t* ts, const int64_t* c_dl, uint8_t* dead, uint32_t* kc) {
   hipStream_t st = h->stream;
   const int64_t nt = a.nt;
   K* keys = (K*)h->ws.get("abs_keys", sizeof(K) * nt, st);
@@ -425,13 +712,127 @@ void sort_and_kill(SgHandle* h, const AbsArgs& a, uint64_t omin, int bits, const
     HIPCHK(rocprim::inclusive_scan(tmp, tb, rk, nks, (size_t)nt, rocprim::minimum<uint32_t>(), st));
   }
   if (a.fast && bits < 64)   // below 64 bits the sentinel lies above every value key
-    hipLaunchKernelGGL((k_abs_kill_fast<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, sentinel, ts, c_dl, dead);
+    hipLaunchKernelGGL((k_abs_kill_fast<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, sentinel, ts, c_dl, dead,
+                       kc);
   else
-    hipLaunchKernelGGL((k_abs_kill<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, role, nks, ts, c_dl, dead);
+    hipLaunchKernelGGL((k_abs_kill<K>), dim3(grid_for(nt)), dim3(256), 0, st, a, skeys, sid, role, nks, ts, c_dl, dead, kc);
   HIPCHK(hipGetLastError());
 }
 
 }  // namespace
+
+// The exact sequential pass (k_abs_seq) for one push, from the carried state (pending partials, FIFO, lastScheduledTime,
+// clock) to the next.
+static void run_seq(SgHandle* h, AbsState* as, const AbsArgs& a, const BatchView& bv, const uint8_t* role, const int64_t* vals,
+             const AbsCarry& cin, AbsCarry& cout, const int64_t* qv, int64_t nq_in, AbsQueue& qout, int64_t clock0,
+             int64_t lst0) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  const int64_t n = a.n, nc = a.nc, P = std::max<int64_t>(nc + n, 1);
+  auto pow2 = [](int64_t x) { int64_t c = 1024; while (c < x) c <<= 1; return c; };
+  int64_t qcap = pow2(2 * (nq_in + 2 * P) + 1024);
+  const int64_t hcap = pow2(2 * P);
+  int64_t sc[8] = {};
+  SeqAbs s;
+  memset(&s, 0, sizeof(s));
+  s.n = n;
+  s.nc = nc;
+  s.W = a.W;
+  s.ts = bv.ts;
+  s.role = role;
+  s.vals = vals;
+  s.c_dl = cin.dl;
+  s.q_in = qv;
+  s.nq_in = nq_in;
+  s.pd = (int64_t*)h->ws.get("sa_pd", 8 * P, st);
+  s.psrc = (uint32_t*)h->ws.get("sa_psrc", 4 * P, st);
+  s.palive = (uint8_t*)h->ws.get("sa_palive", P, st);
+  s.pnext = (int32_t*)h->ws.get("sa_pnext", 4 * P, st);
+  s.bmin = (int64_t*)h->ws.get("sa_bmin", 8 * (P / 64 + 1), st);
+  s.hcap = hcap;
+  s.hkey = (int64_t*)h->ws.get("sa_hkey", 8 * hcap, st);
+  s.hhead = (int32_t*)h->ws.get("sa_hhead", 4 * hcap, st);
+  s.htail = (int32_t*)h->ws.get("sa_htail", 4 * hcap, st);
+  s.hused = (uint8_t*)h->ws.get("sa_hused", hcap, st);
+  s.ecap = P;
+  s.ek = (uint32_t*)h->ws.get("sa_ek", 4 * P, st);
+  s.erow = (uint32_t*)h->ws.get("sa_erow", 4 * P, st);
+  s.ets = (int64_t*)h->ws.get("sa_ets", 8 * P, st);
+  s.eg = (uint32_t*)h->ws.get("sa_eg", 4 * P, st);
+  s.sc = (int64_t*)h->ws.get("sa_sc", 64, st);
+  h->kbeg("abs_sequential");
+  for (;;) {
+    s.qcap = qcap;
+    s.ring = (int64_t*)h->ws.get("sa_ring", 8 * qcap, st);
+    HIPCHK(hipMemsetAsync(s.hused, 0, hcap, st));
+    const int64_t init[2] = {clock0, lst0};
+    HIPCHK(hipMemcpyAsync(s.sc, init, 16, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_abs_seq, dim3(1), dim3(64), 0, st, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(sc, s.sc, 64, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (!(sc[6] & 1)) break;
+    if (qcap >= ((int64_t)1 << 34)) throw SgError(SG_ECAPACITY, "absence timer queue beyond 2^34 entries");
+    qcap <<= 1;   // the timer FIFO outgrew its ring: rerun the push with a larger one (the inputs are unchanged)
+  }
+  h->kend();
+  h->mark(2);
+  const int64_t ne = sc[2], np = sc[3];
+  AbsOut o;
+  memset(&o, 0, sizeof(o));
+  o.n_select = d.n_select;
+  o.stride = 32 + 8 * d.n_select;
+  o.base_index = bv.base_index;
+  o.index = bv.index;
+  const int a_state = d.shape_args[0];
+  for (int k = 0; k < d.n_select; ++k) {
+    const int idx = d.sel_index[k];
+    o.sel_ok[k] = d.sel_state[k] == a_state && (idx == 0 || idx == -1);
+    o.sel_col[k] = d.ret_col[d.sel_ret[k]];
+    o.sel_type[k] = d.sel_type[k];
+  }
+  h->mark(3);
+  h->kbeg("abs_write");
+  char* rec = h->out.reserve(ne, d.n_select, st);
+  if (ne > 0)
+    hipLaunchKernelGGL(k_abs_seq_write, dim3(grid_for(ne)), dim3(256), 0, st, a, o, bv.cols, ne, s.ek, s.erow, s.ets, s.eg,
+                       s.psrc, cin, rec + (size_t)h->out.n * o.stride);
+  HIPCHK(hipGetLastError());
+  if (a.keep_carry) {
+    uint32_t* fl = (uint32_t*)h->ws.get("sa_flag", 4 * (np + 1), st);
+    uint32_t* fo = (uint32_t*)h->ws.get("sa_foff", 4 * (np + 1), st);
+    hipLaunchKernelGGL(k_abs_seq_alive, dim3(grid_for(np + 1)), dim3(256), 0, st, np, s.palive, fl);
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, fl, fo, 0u, (size_t)np + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("sa_scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, fl, fo, 0u, (size_t)np + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t ncar = 0;
+    HIPCHK(hipMemcpyAsync(&ncar, fo + np, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    cout.reserve(std::max<int64_t>(ncar, 1), d.n_select);
+    if (ncar)
+      hipLaunchKernelGGL(k_abs_seq_carry, dim3(grid_for(np)), dim3(256), 0, st, a, o, bv.cols, bv.ts, np, fl, fo, s.psrc,
+                         s.pd, vals, role, cin, cout);
+    const int64_t nq1 = sc[5] - sc[4];
+    qout.reserve(std::max<int64_t>(nq1, 1));
+    if (nq1) hipLaunchKernelGGL(k_abs_qflat, dim3(grid_for(nq1)), dim3(256), 0, st, s.ring, qcap, s.sc, qout.v);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(as->dlast, &sc[0], 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    cout.n = ncar;
+    qout.n = nq1;
+    as->lst = sc[1];
+    as->seq = sc[7] == 0;
+    as->cur ^= 1;
+  }
+  h->kend();
+  h->mark(4);
+  h->out.n += ne;
+  h->split_out = 0;
+  h->last_events = n;
+  h->last_matches = ne;
+  h->last_spilled = 0;
+}
 
 bool sg_every_absent_supported(const sg_nfa_desc& d) {
   const int a = d.shape_args[0], b = d.shape_args[1];
@@ -482,6 +883,8 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   uint8_t* role = (uint8_t*)h->ws.get("abs_role", nt, st);
   int64_t* vals = (int64_t*)h->ws.get("abs_vals", 8 * nt, st);
   uint8_t* dead = (uint8_t*)h->ws.get("abs_dead", nt, st);
+  uint32_t* kc = (uint32_t*)h->ws.get("abs_kc", 4 * (n + 1), st);
+  HIPCHK(hipMemsetAsync(kc, 0, 4 * (n + 1), st));
   hipLaunchKernelGGL(k_abs_init, dim3(1), dim3(64), 0, st, (unsigned long long*)as->dminmax, as->dflag);
   HIPCHK(hipMemsetAsync(dead, 0, nt, st));
   h->kbeg("abs_roles");
@@ -501,10 +904,20 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   h->mark(1);
   uint64_t mm[2] = {0, 0};
   uint32_t oflag = 0;
+  int64_t clock0 = 0;
   HIPCHK(hipMemcpyAsync(mm, as->dminmax, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&oflag, as->dflag, 4, hipMemcpyDeviceToHost, st));
+  if (!a.first_push) HIPCHK(hipMemcpyAsync(&clock0, as->dlast, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (oflag) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps");
+  AbsQueue& qin = as->q[as->cur];
+  AbsQueue& qout = as->q[as->cur ^ 1];
+  const int64_t nq_in = a.first_push ? 0 : qin.n;
+  const int64_t lst0 = a.first_push ? 0 : as->lst;
+  if (oflag || (as->seq && !a.first_push)) {
+    // a timestamp goes back (or the state is not the closed form's): the exact sequential pass
+    run_seq(h, as, a, bv, role, vals, cin, cout, qin.v, nq_in, qout, clock0, lst0);
+    return;
+  }
   // ---- 2-4. sort by value, kill
   h->kbeg("abs_sort_kill");
   if (mm[0] <= mm[1] && nt > 0) {
@@ -513,9 +926,9 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
     while (bits < 64 && (range + 1) >> bits) ++bits;
     if (range + 1 == 0) bits = 64;
     if (bits <= 32)
-      sort_and_kill<uint32_t>(h, a, mm[0], bits, role, vals, bv.ts, cin.dl, dead);
+      sort_and_kill<uint32_t>(h, a, mm[0], bits, role, vals, bv.ts, cin.dl, dead, kc);
     else
-      sort_and_kill<uint64_t>(h, a, mm[0], bits, role, vals, bv.ts, cin.dl, dead);
+      sort_and_kill<uint64_t>(h, a, mm[0], bits, role, vals, bv.ts, cin.dl, dead, kc);
   }
   h->kend();
   h->mark(2);
@@ -574,6 +987,31 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   h->mark(4);
   h->out.n += n_emit;
   if (!h->opt.no_carry) {
+    // the scheduler's FIFO above the clock (kill and creation entries of the push's last W), lastScheduledTime
+    int64_t tlast = clock0;
+    if (n > 0) HIPCHK(hipMemcpyAsync(&tlast, bv.ts + (n - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int64_t clock1 = std::max(clock0, tlast);
+    const int64_t ne_q = nq_in + n;
+    uint32_t* qm = (uint32_t*)h->ws.get("abs_qm", 4 * (ne_q + 1), st);
+    uint32_t* qo = (uint32_t*)h->ws.get("abs_qo", 4 * (ne_q + 1), st);
+    hipLaunchKernelGGL(k_abs_qcount, dim3(grid_for(ne_q + 1)), dim3(256), 0, st, nq_in, qin.v, n, bv.ts, role, a.nc, kc,
+                       a.W, clock1, qm);
+    size_t tq = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tq, qm, qo, 0u, (size_t)ne_q + 1, rocprim::plus<uint32_t>(), st));
+    void* tmpq = h->ws.get("abs_qscan_tmp", tq, st);
+    HIPCHK(rocprim::exclusive_scan(tmpq, tq, qm, qo, 0u, (size_t)ne_q + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t nq1 = 0;
+    HIPCHK(hipMemcpyAsync(&nq1, qo + ne_q, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    qout.reserve(std::max<int64_t>(nq1, 1));
+    hipLaunchKernelGGL(k_abs_qwrite, dim3(grid_for(ne_q)), dim3(256), 0, st, nq_in, qin.v, n, bv.ts, a.W, qm, qo, qout.v);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    qout.n = nq1;
+    // any value >= every queued entry acts alike: it is read only by a pass that emitted nothing (L < T), and new
+    // entries overwrite it first
+    as->lst = std::max(lst0, clock1 + a.W);
     cout.n = n_carry;
     as->cur ^= 1;
   }
@@ -586,6 +1024,9 @@ void sg_every_absent_reset(SgHandle* h) {
   if (h->state && h->state_kind == 3) {
     AbsState* as = (AbsState*)h->state;
     as->carry[0].n = as->carry[1].n = 0;
+    as->q[0].n = as->q[1].n = 0;
+    as->lst = 0;
+    as->seq = false;
   }
 }
 
@@ -594,6 +1035,8 @@ void sg_every_absent_release(SgHandle* h) {
   AbsState* as = (AbsState*)h->state;
   as->carry[0].release();
   as->carry[1].release();
+  as->q[0].release();
+  as->q[1].release();
   hipFree(as->dlast);
   hipFree(as->dminmax);
   hipFree(as->dflag);
@@ -617,6 +1060,12 @@ void sg_every_absent_snapshot(SgHandle* h, SnapW& w) {
     HIPCHK(hipStreamSynchronize(h->stream));
   }
   w.pod(last);
+  // the scheduler's FIFO, lastScheduledTime, and whether the closed form can continue
+  const int64_t nq = as ? as->q[as->cur].n : 0;
+  w.pod(nq);
+  w.pod(as ? as->lst : (int64_t)0);
+  w.pod((int32_t)(as && as->seq ? 1 : 0));
+  if (nq) w.dev(as->q[as->cur].v, nq * 8, h->stream);
   if (!n) return;
   const AbsCarry& c = as->carry[as->cur];
   w.dev(c.dl, n * 8, h->stream);
@@ -632,9 +1081,19 @@ void sg_every_absent_restore(SgHandle* h, SnapR& r) {
   const int64_t n = r.pod<int64_t>();
   if (n < 0 || n >= (1ll << 31)) throw SgError(SG_EINVAL, "snapshot: bad pending-partial count");
   const int64_t last = r.pod<int64_t>();
+  const int64_t nq = r.pod<int64_t>();
+  if (nq < 0 || nq >= (1ll << 34)) throw SgError(SG_EINVAL, "snapshot: bad timer-queue length");
+  as->lst = r.pod<int64_t>();
+  as->seq = r.pod<int32_t>() != 0;
   as->carry[0].n = as->carry[1].n = 0;
+  as->q[0].n = as->q[1].n = 0;
   HIPCHK(hipMemcpyAsync(as->dlast, &last, 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  if (nq) {
+    as->q[as->cur].reserve(nq);
+    r.dev(as->q[as->cur].v, nq * 8, h->stream);
+    as->q[as->cur].n = nq;
+  }
   if (!n) return;
   AbsCarry& c = as->carry[as->cur];
   c.reserve(n, h->desc.n_select);

@@ -83,6 +83,8 @@ struct Virt {
   const void* pcol;           // e1 payload column (one projected attribute carried in the pending list)
   const void* c_pcol;
   int32_t pw, pfloat;         // width 4/8; FLOAT bits zero-extended, integral sign-extended
+  const int32_t* stream;      // batch stream column (null: every row is stream 0)
+  int32_t s_b;                // B's stream: its rows visit e2's pending list (expiry), whatever their filters say
 };
 
 struct KeyOf {   // sort key of virtual row r (the dense partition key; -1 sorts last)
@@ -94,12 +96,21 @@ struct KeyOf {   // sort key of virtual row r (the dense partition key; -1 sorts
   }
 };
 
+// carried rows keep F_CAND / F_CONS in bits 0-1 and F_VISIT (a row of B's stream) in bit 2
+static const uint32_t F_VISIT = 4;
 __device__ __forceinline__ uint32_t v_flags(const Virt& v, uint32_t r) {
-  if (r < v.nc) return v.c_flags[r];
+  if (r < v.nc) return v.c_flags[r] & 3u;
   uint64_t b = r - v.nc;
   uint32_t f = mask_bit(v.cand_m, b);
   f |= v.cons_m ? (mask_bit(v.cons_m, b) << 1) : F_CONS;
   return f;
+}
+// Does virtual row r visit e2's pending list?  Every row of B's stream does (MultiProcessStreamReceiver.receive ->
+// StreamPreStateProcessor.processAndReturn, C/query/input/stream/state/StreamPreStateProcessor.java:292-337): its
+// `within` expiry applies whether or not the row passes a filter.
+__device__ __forceinline__ bool v_visit(const Virt& v, uint32_t r) {
+  if (r < v.nc) return (v.c_flags[r] & F_VISIT) != 0;
+  return (v.stream ? v.stream[r - v.nc] : 0) == v.s_b;
 }
 __device__ __forceinline__ int64_t v_ts(const Virt& v, uint32_t r) { return r < v.nc ? v.c_ts[r] : v.ts[r - v.nc]; }
 template <class T>
@@ -667,16 +678,26 @@ struct MatchSink {
 };
 
 struct UnitDesc {
-  uint32_t p0, p1, w, ovf;     // chunk positions [p0, p1), replay from w; ovf = 1 + HBM-list slot
+  uint32_t p0, p1, w, ovf;     // chunk positions [p0, p1), replay from w; ovf = 1 + first entry of its HBM list
 };
 
 struct WalkStats {
   uint32_t order_err;
-  uint32_t n_ovf;
-  uint32_t ovf_need;
+  uint32_t n_ovf;             // units on the HBM-list walker
+  uint32_t ovf_total;         // HBM-list entries they take (each unit: one entry per row it walks)
   uint32_t internal;          // internal consistency guards tripped (bit 1 unit range, 2 tile source, 4 count row,
-                              // 8 match slot): reported as SG_EINVAL instead of touching memory out of range
+                              // 8 match slot, 16 HBM-list space): reported as SG_EINVAL instead of touching memory
+                              // out of range
 };
+
+// an HBM list for unit u walking rows [w, p1): its first entry (the lists of a push are packed back to back)
+__device__ __forceinline__ uint32_t take_hbm_list(WalkStats* st, uint32_t w, uint32_t p1) {
+  const uint32_t need = p1 - w + 1;
+  const uint32_t o = atomicAdd(&st->ovf_total, need);
+  atomicAdd(&st->n_ovf, 1u);
+  if (o > 0xffffffffu - need) atomicOr(&st->internal, 16u);
+  return o;
+}
 
 struct LdsPlan {   // per-push layout of the walkers' LDS rings (count walk: value + time only)
   int32_t pay;     // 1: narrow payload plane
@@ -701,9 +722,15 @@ struct WalkArgs {
   int32_t n_select;
   int32_t stride;
   int64_t out_base;
-  uint32_t big_cap;           // entries per HBM list (BIG)
+  uint32_t big_total;         // entries of all HBM lists of the push (BIG)
   LdsPlan lp;                 // record walk LDS planes
   int32_t pay_in_rec;         // e1 payload rides in the (narrow) walker records
+  // Keys whose rows (carried ones included) go back in time take the exact walker (see Walker::step_exact): one
+  // unit per key on the HBM-list path.  kexact: per-key flag (null: no key does); alive / alive_n: the record pass
+  // of such a key leaves its final pending list (virtual rows, pending order) there for the carry.
+  const uint8_t* kexact;
+  uint32_t* alive;
+  uint32_t* alive_n;
 };
 
 template <class T> __device__ __forceinline__ bool is_nan_val(T) { return false; }
@@ -782,12 +809,11 @@ __device__ __forceinline__ void lds_planes(PendList<T, BIG>& L, char* lds, bool 
   L.pay64 = nullptr;
 }
 template <class T, bool BIG>
-__device__ __forceinline__ void hbm_planes(PendList<T, BIG>& L, char* big, uint32_t slot, size_t cap) {
-  char* base = big + (size_t)slot * cap * PendBytes<T>::hbm;
-  L.ts = (int64_t*)base;
-  L.pay64 = (int64_t*)(base + cap * 8);
-  L.val = (T*)(base + cap * 16);
-  L.row = (uint32_t*)(base + cap * (16 + sizeof(T)));
+__device__ __forceinline__ void hbm_planes(PendList<T, BIG>& L, char* big, uint32_t first, size_t total) {
+  L.ts = (int64_t*)big + first;
+  L.pay64 = (int64_t*)(big + total * 8) + first;
+  L.val = (T*)(big + total * 16) + first;
+  L.row = (uint32_t*)(big + total * (16 + sizeof(T))) + first;
   L.dts = nullptr;
   L.pay32 = nullptr;
 }
@@ -901,9 +927,12 @@ struct Walker {
   uint32_t head = 0, top = 0;
   TT hts = 0;                 // register copies (valid while head != top): time of the oldest partial and
   T tv = T();                 // value of the newest one -- the common step touches no LDS for either
-  TT prev_t;
+  int64_t prev_t;             // time of the previous row (the records' own time domain): the order check
   TT within;
   bool bad = false;
+  // exact mode (a key whose time goes back; HBM list only): min / max time over the list while head != top
+  bool exact = false;
+  int64_t lo_t = 0, hi_t = 0;
   bool oob = false;           // internal guard: a row outside the batch (never expected)
   bool overflow = false;
   uint32_t ew = 0xffffffffu, ebits = 0;   // count pass: emit bitmap word being built
@@ -911,11 +940,8 @@ struct Walker {
     within = BIG ? (TT)w : (TT)(w > 0x7fffffffll ? 0x7fffffffll : w);   // a wider window never expires in-unit
   }
   __device__ __forceinline__ TT rel(int64_t t) const { return BIG ? (TT)t : (TT)(t - L.base); }
-  // order check against the row before the replay window (which may lie far outside the 31-bit span)
-  __device__ __forceinline__ void init_prev(int64_t before, int64_t first) {
-    if (BIG) prev_t = (TT)before;
-    else prev_t = before > first ? (TT)0x7fffffff : (TT)0;
-  }
+  // order check against the row before the replay window
+  __device__ __forceinline__ void init_prev(int64_t before) { prev_t = before; }
   __device__ __forceinline__ TT at(uint32_t s) const {
     return BIG ? (TT)L.ts[L.ix(s)] : (TT)L.dts[L.ix(s)];
   }
@@ -940,20 +966,14 @@ struct Walker {
                                        uint32_t ofs, uint32_t* __restrict__ cnt, const MatchSink& em,
                                        bool payload, int64_t pay = 0, bool pay_ready = false) {
     const uint32_t f = rc.rowf >> 30;
+    // every row of the key takes part in the order check (a row that fails both filters still expires partials in
+    // the reference): a key whose time goes back is redone by the exact walker
+    const int64_t tabs = rc.t();
+    bad |= tabs < prev_t;
+    prev_t = tabs;
     if (!f) return false;
-#ifdef SG_EXP_STUB_STEP
-    {   // experiment: memory streaming only
-      const uint32_t r = rc.rowf & ROW_MASK;
-      top += (uint32_t)(rc.t() & 1) + (uint32_t)(rc.val > (T)0);
-      const bool e = in_chunk && ((r & 7) == 0);
-      if (!WRITE && e) cnt[r - v.nc] = top;
-      return e;
-    }
-#endif
     const T x = rc.val;
-    const TT t = rel(rc.t());
-    bad |= t < prev_t;
-    prev_t = t;
+    const TT t = rel(tabs);
     // lazy `within` expiry of the oldest partials (StreamPreStateProcessor.isExpired :102-113)
     if (head != top && t - hts > within) {
       ++head;
@@ -1021,10 +1041,82 @@ struct Walker {
     }
     return emitted;
   }
+  __device__ __forceinline__ void keep(uint32_t& wr, uint32_t s, T e, int64_t ti) {
+    if (wr != s) L.put(wr, e, ti, L.grow(s), L.gpay(s));
+    ++wr;
+    if (wr == head + 1) { lo_t = ti; hi_t = ti; } else { lo_t = ti < lo_t ? ti : lo_t; hi_t = ti > hi_t ? ti : hi_t; }
+  }
+  // The reference's list for any arrival order (HBM list only): a row of B's stream first drops every pending
+  // partial with |e1.ts - ts| > within -- on either side, not only the oldest (StreamPreStateProcessor.isExpired,
+  // C/query/input/stream/state/StreamPreStateProcessor.java:102-113) -- then a B consumer completes, in pending
+  // order, every partial its compare accepts (processAndReturn :292-337), then a candidate appends itself.
+  template <class R>
+  __device__ __forceinline__ bool step_exact(const WalkArgs& a, const Virt& v, const R& rc, bool in_chunk,
+                                             uint32_t ofs, uint32_t* __restrict__ cnt, const MatchSink& em,
+                                             bool payload) {
+    const uint32_t f = rc.rowf >> 30;
+    const uint32_t r = rc.rowf & ROW_MASK;
+    const int64_t t = rc.t();
+    const T x = rc.val;
+    const bool live = !is_nan_val<T>(x);
+    if (BIG && head != top && (t - lo_t > (int64_t)within || hi_t - t > (int64_t)within) && v_visit(v, r)) {
+      uint32_t wr = head;
+      for (uint32_t s = head; s != top; ++s) {
+        const int64_t ti = (int64_t)at(s);
+        if (t - ti > (int64_t)within || ti - t > (int64_t)within) continue;
+        keep(wr, s, L.gv(s), ti);
+      }
+      top = wr;
+    }
+    uint32_t m = 0;
+    if ((f & F_CONS) && live && head != top) {
+      const bool emit = in_chunk && (r >= v.nc);
+      uint32_t wr = head;
+      for (uint32_t s = head; s != top; ++s) {
+        const T e = L.gv(s);
+        if (cmp_sel<OP, T>(a.op, x, e)) {
+          if (WRITE && emit) em.put(ofs + m, L.grow(s), r, val_bits<T>(e), L.gpay(s));
+          ++m;
+        } else {
+          keep(wr, s, e, (int64_t)at(s));
+        }
+      }
+      top = wr;
+    }
+    const bool emitted = m && in_chunk && (r >= v.nc);
+    if (!WRITE && emitted) {
+      if (r - v.nc < (uint64_t)v.n) cnt[r - v.nc] = m;
+      else oob = true;
+    }
+    if ((f & F_CAND) && live) {
+      int64_t pv = 0;
+      if (WRITE && payload) pv = (R::has_pay && a.pay_in_rec) ? rc.p(v.pfloat) : v_payload(v, r);
+      if (head == top) { lo_t = t; hi_t = t; } else { lo_t = t < lo_t ? t : lo_t; hi_t = t > hi_t ? t : hi_t; }
+      L.put(top, x, t, r, pv);
+      ++top;
+    }
+    return emitted;
+  }
 };
 
-// One lane per unit (chunk c, key k).  WRITE=false: count pass (also fixes the unit's replay range);
-// WRITE=true: record pass.  BIG: only units that overflowed the LDS ring, with an HBM list.
+// First sorted position of key segment [sb, se) the carry keeps, for a key whose time never went back: partials
+// started more than `within` before the key's last row of B's stream were expired by it, and rows before the window
+// can change no later partial.  A key with no row of B's stream yet keeps every row from its first candidate on
+// (none of its partials has been visited, so none has expired).
+template <class T, bool N>
+__device__ __forceinline__ uint32_t carry_start(const Src<T, N>& src, const Virt& v, uint32_t sb, uint32_t se,
+                                                int64_t within) {
+  uint32_t q = se;
+  while (q > sb && !v_visit(v, src.row(q - 1))) --q;
+  if (q > sb) return lb_ts(src, sb, se, src.ts(q - 1) - within);
+  uint32_t p = sb;
+  while (p < se && !((src.at(p).rowf >> 30) & F_CAND)) ++p;
+  return p;
+}
+
+// HBM-list walker: one lane per unit whose pending list outgrew the LDS ring, whose time span does not fit the ring's
+// 31-bit times, or whose key's time goes back (exact mode: the key's whole segment in one unit).  WRITE=false: count
+// pass; WRITE=true: record pass.
 template <class T, bool N, bool WRITE, bool BIG>
 __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, const uint32_t* __restrict__ seg_b,
                                                      const uint32_t* __restrict__ seg_e, UnitDesc* __restrict__ ud,
@@ -1032,12 +1124,12 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
                                                      const MatchSink em, uint32_t* __restrict__ emap,
                                                      WalkStats* __restrict__ st, char* __restrict__ big,
                                                      uint32_t* __restrict__ carry_q0, uint32_t* __restrict__ carry_n) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+  static_assert(BIG, "the LDS-ring units run on the tiled walker (k_walk_t)");
   const uint32_t u = xcd_block(blockIdx.x, gridDim.x) * WALK_BLOCK + threadIdx.x;
   if (u >= a.n_units) return;
   const Virt& v = src.pk.v;
   const bool part = a.partitioned != 0;
-  const uint32_t c = u / a.K, k = u % a.K;
+  const uint32_t k = u % a.K;
   uint32_t sb, se;
   if (part) {
     sb = seg_b[k];
@@ -1046,43 +1138,27 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
     sb = 0;
     se = (uint32_t)a.nt;
   }
-  uint32_t p0, p1, w, ovf = 0;
-  if (!WRITE && !BIG) {
-    if (sb >= se) { ud[u] = UnitDesc{0, 0, 0, 0}; return; }
-    uint64_t lo_row = (uint64_t)c * a.R, hi_row = lo_row + a.R;
-    p0 = c == 0 ? sb : lb_row(src, sb, se, (uint32_t)(lo_row < (uint64_t)a.nt ? lo_row : a.nt), part);
-    p1 = c + 1 >= a.C ? se : lb_row(src, p0, se, (uint32_t)(hi_row < (uint64_t)a.nt ? hi_row : a.nt), part);
-    if (p0 >= p1) { ud[u] = UnitDesc{p0, p0, p0, 0}; return; }
-    w = lb_ts(src, sb, p0, src.ts(p0) - a.within);
-    ud[u] = UnitDesc{p0, p1, w, 0};
-  } else {
-    UnitDesc d = ud[u];
-    p0 = d.p0; p1 = d.p1; w = d.w; ovf = d.ovf;
-    if (p0 >= p1) return;
-    if (BIG != (ovf != 0)) return;
-  }
+  const UnitDesc d = ud[u];
+  const uint32_t p0 = d.p0, p1 = d.p1, w = d.w, ovf = d.ovf;
+  if (p0 >= p1 || ovf == 0) return;
   Walker<T, WRITE, BIG> W;
-  if (BIG) hbm_planes<T, BIG>(W.L, big, ovf - 1, a.big_cap);
-  else lds_planes<T, BIG>(W.L, lds, WRITE, a.lp);
+  hbm_planes<T, BIG>(W.L, big, ovf - 1, a.big_total);
   W.L.pzero = v.pfloat;
+  W.exact = a.kexact && a.kexact[k];
   const bool payload = v.pcol != nullptr;
   const int64_t tw = src.ts(w);
   W.L.base = tw;
-  auto mark_overflow = [&]() {
-    uint32_t slot = atomicAdd(&st->n_ovf, 1u);
-    atomicMax(&st->ovf_need, p1 - w);
-    ud[u].ovf = slot + 1;
-  };
-  if (!BIG && !WRITE) {
-    int64_t tl = src.ts(p1 - 1);
-    if (tl - tw > 0x7fffffffll || tl < tw) { mark_overflow(); return; }   // relative ts would not fit
-  }
   W.set_within(a.within);
-  W.init_prev((w > sb) ? src.ts(w - 1) : tw, tw);
+  W.init_prev((w > sb) ? src.ts(w - 1) : tw);
   // record walk: output offsets only for the positions the count pass marked as emitting
   auto off_of = [&](const WRec<T, N>& rc, uint32_t pos, uint32_t bits) -> uint32_t {
     uint32_t r = rc.rowf & ROW_MASK;
     return (bits && pos >= p0 && pos < p1 && r >= v.nc) ? off[r - v.nc] : 0u;
+  };
+  auto one = [&](const WRec<T, N>& rc, uint32_t p, uint32_t o) {
+    const bool e = W.exact ? W.step_exact(a, v, rc, p >= p0, o, cnt, em, payload)
+                           : W.step(a, v, rc, p >= p0, o, cnt, em, payload);
+    if (e && !WRITE) W.mark_emit(p, emap);
   };
   if (src.srec) {
     // key-sorted records: whole-line group loads, next group in flight while this one is walked
@@ -1108,10 +1184,8 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
       for (int i = 0; i < GT::G; ++i) {
         const uint32_t p = g + i;
         if (p < w || p >= p1) continue;
-        if (W.step(a, v, cur.rec(i), p >= p0, WRITE ? ofs[i] : 0u, cnt, em, payload) && !WRITE) W.mark_emit(p, emap);
-        if (!BIG && W.overflow) break;
+        one(cur.rec(i), p, WRITE ? ofs[i] : 0u);
       }
-      if (!BIG && W.overflow) break;
       cur = nxt;
       if (WRITE) {
 #pragma unroll
@@ -1124,24 +1198,26 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
     // unpartitioned: the rows themselves, in order
     for (uint32_t p = w; p < p1; ++p) {
       WRec<T, N> rc = src.pk(p);
-      uint32_t o = 0;
-      if (WRITE) o = off_of(rc, p, (emap[p >> 5] >> (p & 31)) & 1u);
-      if (W.step(a, v, rc, p >= p0, o, cnt, em, payload) && !WRITE) W.mark_emit(p, emap);
-      if (!BIG && W.overflow) break;
+      one(rc, p, WRITE ? off_of(rc, p, (emap[p >> 5] >> (p & 31)) & 1u) : 0u);
     }
   }
   if (!WRITE) W.flush_bits(emap);
-  if (!BIG && W.overflow) {
-    if (!WRITE) mark_overflow();
-    return;   // the HBM-list walker redoes this unit
-  }
   if (W.oob) atomicOr(&st->internal, 4u);
-  if (W.bad) atomicOr(&st->order_err, 1u);
+  if (W.bad && !W.exact) atomicOr(&st->order_err, 1u);
   if (WRITE && a.carry_out && p1 == se) {
-    // rows of this key still inside the window of its last event survive into the next push
-    uint32_t q0 = lb_ts(src, sb, se, src.ts(se - 1) - a.within);
-    carry_q0[k] = q0;
-    carry_n[k] = se - q0;
+    if (W.exact) {
+      // the key's pending list itself survives: its partials, in pending order (replaying them changes nothing --
+      // each survived every later row of the key, so none expires or completes another)
+      const uint32_t m = W.top - W.head;
+      const uint32_t o = m ? atomicAdd(a.alive_n, m) : 0u;
+      for (uint32_t s = 0; s < m; ++s) a.alive[o + s] = W.L.grow(W.head + s);
+      carry_q0[k] = se;
+      carry_n[k] = 0;
+    } else {
+      const uint32_t q0 = carry_start(src, v, sb, se, a.within);
+      carry_q0[k] = q0;
+      carry_n[k] = se - q0;
+    }
   }
 }
 
@@ -1163,7 +1239,10 @@ __global__ void __launch_bounds__(256) k_units(WalkArgs a, Src<T, N> src, const 
     uint32_t sb = seg_b[k], se = seg_e[k];
     UnitDesc d{0, 0, 0, 0};
     if (se > a.nt || sb > se) { atomicOr(&st->internal, 1u); sb = se = 0; }
-    if (sb < se) {
+    if (sb < se && a.kexact && a.kexact[k]) {
+      // a key whose time goes back: its whole segment in one exact unit (chunk 0) on the HBM-list walker
+      if (c == 0) d = UnitDesc{sb, se, sb, take_hbm_list(st, sb, se) + 1};
+    } else if (sb < se) {
       uint64_t lo_row = (uint64_t)c * a.R, hi_row = lo_row + a.R;
       uint32_t p0 = c == 0 ? sb : lb_row(src, sb, se, (uint32_t)(lo_row < (uint64_t)a.nt ? lo_row : a.nt), true);
       uint32_t p1 = c + 1 >= a.C ? se : lb_row(src, p0, se, (uint32_t)(hi_row < (uint64_t)a.nt ? hi_row : a.nt), true);
@@ -1173,9 +1252,7 @@ __global__ void __launch_bounds__(256) k_units(WalkArgs a, Src<T, N> src, const 
         d = UnitDesc{p0, p1, w, 0};
         int64_t tw = src.ts(w), tl = src.ts(p1 - 1);
         if (tl - tw > 0x7fffffffll || tl < tw) {   // relative ts would not fit: HBM-list walker
-          uint32_t slot = atomicAdd(&st->n_ovf, 1u);
-          atomicMax(&st->ovf_need, p1 - w);
-          d.ovf = slot + 1;
+          d.ovf = take_hbm_list(st, w, p1) + 1;
         } else {
           len = p1 - w;
         }
@@ -1262,7 +1339,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
   const int64_t tw = active ? src.ts(w) : 0;
   Wk.L.base = tw;
   Wk.set_within(a.within);
-  Wk.init_prev((active && w > sb) ? src.ts(w - 1) : tw, tw);
+  Wk.init_prev((active && w > sb) ? src.ts(w - 1) : tw);
   const bool payload = v.pcol != nullptr;
   const uint32_t chunk_i = active ? p0 - w : 0;   // rows before this index only rebuild the pending list
   const WRec<T, N>* tp = tile + (size_t)base * 64 + lane;
@@ -1312,17 +1389,13 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
   if (Wk.oob) atomicOr(&st->internal, 4u);
   if (!active) return;
   if (Wk.overflow) {
-    if (!WRITE) {
-      uint32_t slot = atomicAdd(&st->n_ovf, 1u);
-      atomicMax(&st->ovf_need, p1 - w);
-      ud_w[u].ovf = slot + 1;
-    }
+    if (!WRITE) ud_w[u].ovf = take_hbm_list(st, w, p1) + 1;
     return;
   }
   if (Wk.bad) atomicOr(&st->order_err, 1u);
   const uint32_t se = seg_e[k];
   if (WRITE && a.carry_out && p1 == se) {
-    uint32_t q0 = lb_ts(src, sb, se, src.ts(se - 1) - a.within);
+    const uint32_t q0 = carry_start(src, v, sb, se, a.within);
     carry_q0[k] = q0;
     carry_n[k] = se - q0;
   }
@@ -1336,35 +1409,6 @@ struct CarryBufs {
   void* col[SG_MAX_COLS];
   uint8_t* nul[SG_MAX_COLS];
 };
-
-// one thread per carried row (coalesced writes; a key's suffix is found by binary search over the key offsets,
-// so keys with long suffixes no longer serialise one lane)
-template <class T, bool N>
-__global__ void k_carry_copy(Src<T, N> src, uint32_t K, uint32_t ncar, const uint32_t* __restrict__ q0s,
-                             const uint32_t* __restrict__ offs, int n_cols, const int32_t* __restrict__ widths,
-                             SgCols bc, SgCols cc, CarryBufs dst) {
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= ncar) return;
-  uint32_t lo = 0, hi = K;   // last key k with offs[k] <= d (offs: exclusive scan of the suffix lengths)
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (offs[mid] <= d) lo = mid;
-    else hi = mid;
-  }
-  const Virt& v = src.pk.v;
-  const uint32_t r = src.row(q0s[lo] + (d - offs[lo]));
-  dst.ts[d] = v_ts(v, r);
-  dst.key[d] = r < v.nc ? v.c_key[r] : (v.key ? v.key[r - v.nc] : 0);
-  dst.flags[d] = (uint8_t)v_flags(v, r);
-  const SgCols& s = r < v.nc ? cc : bc;
-  const uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
-  for (int c = 0; c < n_cols; ++c) {
-    if (!s.col[c]) continue;
-    if (widths[c] == 8) ((int64_t*)dst.col[c])[d] = ((const int64_t*)s.col[c])[rr];
-    else ((int32_t*)dst.col[c])[d] = ((const int32_t*)s.col[c])[rr];
-    dst.nul[c][d] = s.nul[c] ? s.nul[c][rr] : 0;
-  }
-}
 
 // Carry by arrival order: a virtual row survives into the next push iff its key's last row is within `within` of it
 // (the rows lb_ts finds per key in the record walk: sorted positions [carry_q0, seg_e)).  Those positions mark their
@@ -1421,7 +1465,7 @@ static __global__ void __launch_bounds__(256) k_carry_gather(Virt v, int64_t nt,
       const uint32_t r = (uint32_t)r64;
       dst.ts[d] = v_ts(v, r);
       dst.key[d] = r < v.nc ? v.c_key[r] : (v.key ? v.key[r - v.nc] : 0);
-      dst.flags[d] = (uint8_t)v_flags(v, r);
+      dst.flags[d] = (uint8_t)(v_flags(v, r) | (v_visit(v, r) ? F_VISIT : 0u));
       const SgCols& s = r < v.nc ? cc : bc;
       const uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
       for (int c = 0; c < n_cols; ++c) {
@@ -1533,24 +1577,33 @@ static void launch_walk_t(int op, dim3 g, dim3 b, size_t lds, hipStream_t st, co
 // Unpartitioned streams: per-candidate search instead of the walker.  One key means the walker's units are
 // time chunks of a single row sequence, each replaying a whole `within` window before it: few, long,
 // latency-bound lanes (C1: 1000-row windows).  Every partial of this shape is independent:
-// partial i completes at the first later consumer j with x_j OP x_i, unless the oldest-first expiry
-// (StreamPreStateProcessor.isExpired, C/query/input/stream/state/StreamPreStateProcessor.java:102-113) drops
-// it first, i.e. iff ts_j - ts_i <= T.  So one lane per candidate scans forward (lanes of a wave read
-// neighbouring rows: coalesced), matches become (trigger j, partial i) pairs, and a stable radix sort by j
-// of the pairs compacted in i order yields the reference's delivery order (trigger, then pending order).
-// A search longer than NGE_MAX_SCAN rows sends the push to the walker (bounded work per lane).
+// partial i leaves e2's list at the first later row of B's stream that either expires it (|ts_j - ts_i| > T,
+// StreamPreStateProcessor.isExpired, C/query/input/stream/state/StreamPreStateProcessor.java:102-113 -- for any
+// arrival order, so time going back needs no special case) or, as a consumer with x_j OP x_i, completes it
+// (processAndReturn :292-337).  So one lane per candidate scans forward (lanes of a wave read neighbouring rows:
+// coalesced); matches go to their slots by per-trigger counts, and a candidate whose scan reaches the end of the
+// push is still pending: exactly those rows are carried into the next push.  A search longer than NGE_MAX_SCAN
+// rows sends the push to the walker (bounded work per lane).
 static const uint32_t NGE_MAX_SCAN = 4096;
 static const uint32_t NGE_NONE = 0xffffffffu;
 
-// per 64-row block of virtual rows: the most completing consumer value (max for > >=, min for < <=) and
-// whether the block has a live consumer at all -- lets a search skip blocks that cannot complete it
+// per 64-row block of virtual rows: the most completing consumer value (max for > >=, min for < <=), whether the
+// block has a live consumer at all, and the time range of its rows of B's stream -- a search skips a block that
+// can neither complete nor expire its partial
 template <class T, int OP>
-__global__ void k_nge_blocks(Virt v, int64_t nt, T* __restrict__ best, uint8_t* __restrict__ has) {
+__global__ void k_nge_blocks(Virt v, int64_t nt, T* __restrict__ best, uint8_t* __restrict__ has,
+                             int64_t* __restrict__ bmin, int64_t* __restrict__ bmax) {
   const int64_t nb = (nt + 63) >> 6;
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (int64_t)gridDim.x * blockDim.x) {
     T m{};
     bool any = false;
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
     for (int64_t q = b << 6, e = (q + 64 < nt ? q + 64 : nt); q < e; ++q) {
+      if (v_visit(v, (uint32_t)q)) {
+        const int64_t t = v_ts(v, (uint32_t)q);
+        lo = t < lo ? t : lo;
+        hi = t > hi ? t : hi;
+      }
       if (!(v_flags(v, (uint32_t)q) & F_CONS)) continue;
       const T x = v_val<T>(v, (uint32_t)q, false);
       if (is_nan_val<T>(x)) continue;
@@ -1559,6 +1612,8 @@ __global__ void k_nge_blocks(Virt v, int64_t nt, T* __restrict__ best, uint8_t* 
     }
     best[b] = m;
     has[b] = any ? 1 : 0;
+    bmin[b] = lo;
+    bmax[b] = hi;
   }
 }
 
@@ -1566,34 +1621,38 @@ template <class T, int OP>
 __global__ void __launch_bounds__(256) k_nge(Virt v, int64_t nt, int64_t within, int op, uint32_t* __restrict__ mj,
                                              uint32_t* __restrict__ rank, uint32_t* __restrict__ cnt,
                                              uint32_t* __restrict__ st_flags, const T* __restrict__ best,
-                                             const uint8_t* __restrict__ has) {
+                                             const uint8_t* __restrict__ has, const int64_t* __restrict__ bmin,
+                                             const int64_t* __restrict__ bmax, uint32_t* __restrict__ alive) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nt; p += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t f = v_flags(v, (uint32_t)p);
-    const int64_t tp = v_ts(v, (uint32_t)p);
-    if (p + 1 < nt && v_ts(v, (uint32_t)(p + 1)) < tp) atomicOr(&st_flags[0], 1u);   // order check
     uint32_t j = NGE_NONE;
     if (f & F_CAND) {
       const T xp = v_val<T>(v, (uint32_t)p, true);
+      const int64_t tp = v_ts(v, (uint32_t)p);
       if (!is_nan_val<T>(xp)) {
         uint32_t steps = 0;
+        bool open = true;   // still pending when the scan reaches the end of the push
         int64_t q = p + 1;
         while (q < nt) {
-          if (++steps > NGE_MAX_SCAN) { atomicOr(&st_flags[1], 1u); break; }
+          if (++steps > NGE_MAX_SCAN) { atomicOr(&st_flags[1], 1u); open = false; break; }
           if ((q & 63) == 0 && q + 64 <= nt && !(has[q >> 6] && cmp_sel<OP, T>(op, best[q >> 6], xp)) &&
-              v_ts(v, (uint32_t)(q + 63)) - tp <= within) {
-            q += 64;                                                       // nothing in this block completes i
+              bmax[q >> 6] <= tp + within && bmin[q >> 6] >= tp - within) {
+            q += 64;                                                       // nothing in this block ends i
             continue;
           }
-          if (v_ts(v, (uint32_t)q) - tp > within) break;                  // expired before q
+          const int64_t tq = v_ts(v, (uint32_t)q);
+          if ((tq - tp > within || tp - tq > within) && v_visit(v, (uint32_t)q)) { open = false; break; }   // expired
           if (v_flags(v, (uint32_t)q) & F_CONS) {
             const T xq = v_val<T>(v, (uint32_t)q, false);
             if (!is_nan_val<T>(xq) && cmp_sel<OP, T>(op, xq, xp)) {
               if (q >= v.nc) j = (uint32_t)q;                             // (carried triggers were emitted before)
+              open = false;
               break;
             }
           }
           ++q;
         }
+        if (open && alive) atomicOr(&alive[p >> 5], 1u << (p & 31));
       }
     }
     mj[p] = j;
@@ -1618,11 +1677,16 @@ __global__ void k_nge_place(Virt v, int64_t nt, const uint32_t* __restrict__ mj,
   }
 }
 
+// Each trigger's matches into pending order (ascending e1 row).  Triggers with up to NGE_ORDER_SMALL matches are
+// insertion-sorted by their own lane; larger ones (a long run of candidates completed by one row) are flagged and
+// sorted by a segmented radix sort afterwards, so no lane does quadratic work.
+static const uint32_t NGE_ORDER_SMALL = 32;
 static __global__ void k_nge_order(int64_t n, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                   MRec* __restrict__ mrec) {
+                                   MRec* __restrict__ mrec, uint32_t* __restrict__ nbig) {
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < n; b += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t c = cnt[b];
     if (c < 2) continue;
+    if (c > NGE_ORDER_SMALL) { atomicAdd(nbig, c); continue; }
     MRec* e = mrec + off[b];
     for (uint32_t i = 1; i < c; ++i) {
       const MRec x = e[i];
@@ -1636,34 +1700,20 @@ static __global__ void k_nge_order(int64_t n, const uint32_t* __restrict__ cnt, 
   }
 }
 
-// rows still inside `within` of the last row survive into the next push (one key: a suffix)
-static __global__ void k_nge_carry_start(Virt v, int64_t nt, int64_t within, uint32_t* __restrict__ q0) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const int64_t tmin = v_ts(v, (uint32_t)(nt - 1)) - within;
-  int64_t lo = 0, hi = nt;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (v_ts(v, (uint32_t)mid) < tmin) lo = mid + 1; else hi = mid;
+// large triggers: (trigger slot, e1 row) keys of their matches, then one stable radix sort orders every match
+static __global__ void k_nge_bigkeys(int64_t total, const MRec* __restrict__ mrec, const uint32_t* __restrict__ mj,
+                                     const uint32_t* __restrict__ off, int64_t nc, uint64_t* __restrict__ key,
+                                     uint32_t* __restrict__ idx) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (int64_t)gridDim.x * blockDim.x) {
+    const MRec m = mrec[s];
+    key[s] = ((uint64_t)off[m.r2 - nc] << 32) | m.r1;
+    idx[s] = (uint32_t)s;
   }
-  *q0 = (uint32_t)lo;
 }
-
-static __global__ void k_nge_carry_copy(Virt v, uint32_t q0, uint32_t ncar, int n_cols, const int32_t* __restrict__ widths,
-                                 SgCols bc, SgCols cc, CarryBufs dst) {
-  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ncar; d += gridDim.x * blockDim.x) {
-    const uint32_t r = q0 + d;
-    dst.ts[d] = v_ts(v, r);
-    dst.key[d] = 0;
-    dst.flags[d] = (uint8_t)v_flags(v, r);
-    const SgCols& s = r < v.nc ? cc : bc;
-    const uint32_t rr = r < v.nc ? r : (uint32_t)(r - v.nc);
-    for (int c = 0; c < n_cols; ++c) {
-      if (!s.col[c]) continue;
-      if (widths[c] == 8) ((int64_t*)dst.col[c])[d] = ((const int64_t*)s.col[c])[rr];
-      else ((int32_t*)dst.col[c])[d] = ((const int32_t*)s.col[c])[rr];
-      dst.nul[c][d] = s.nul[c] ? s.nul[c][rr] : 0;
-    }
-  }
+static __global__ void k_nge_permute(int64_t total, const MRec* __restrict__ src, const uint32_t* __restrict__ idx,
+                                     MRec* __restrict__ dst) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (int64_t)gridDim.x * blockDim.x)
+    dst[s] = src[idx[s]];
 }
 
 template <class T>
@@ -1678,15 +1728,22 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   uint32_t* rank = (uint32_t*)h->ws.get("nge_rank", 4 * nt, st);
   uint32_t* cnt = (uint32_t*)h->ws.get("cnt", sizeof(uint32_t) * (n + 1), st);
   uint32_t* off = (uint32_t*)h->ws.get("off", sizeof(uint32_t) * (n + 1), st);
-  uint32_t* stf = (uint32_t*)h->ws.get("nge_flags", 8, st);
+  uint32_t* stf = (uint32_t*)h->ws.get("nge_flags", 16, st);
+  const bool carry = !h->opt.no_carry && nt > 0;
+  const int64_t cnb = (nt + CARRY_BLK - 1) / CARRY_BLK;
+  uint32_t* cbits = carry ? (uint32_t*)h->ws.get("carry_bits", sizeof(uint32_t) * (size_t)(cnb * 256), st) : nullptr;
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
-  HIPCHK(hipMemsetAsync(stf, 0, 8, st));
+  HIPCHK(hipMemsetAsync(stf, 0, 16, st));
+  if (carry) HIPCHK(hipMemsetAsync(cbits, 0, sizeof(uint32_t) * (size_t)(cnb * 256), st));
   const int64_t nb = (nt + 63) >> 6;
   T* best = (T*)h->ws.get("nge_best", sizeof(T) * (nb + 1), st);
   uint8_t* has = (uint8_t*)h->ws.get("nge_has", nb + 1, st);
+  int64_t* bmin = (int64_t*)h->ws.get("nge_bmin", sizeof(int64_t) * (nb + 1), st);
+  int64_t* bmax = (int64_t*)h->ws.get("nge_bmax", sizeof(int64_t) * (nb + 1), st);
 #define SG_NGE_LAUNCH(OPV)                                                                                       \
-  hipLaunchKernelGGL((k_nge_blocks<T, OPV>), grid(nb), dim3(256), 0, st, v, nt, best, has);                     \
-  hipLaunchKernelGGL((k_nge<T, OPV>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, rank, cnt, stf, best, has)
+  hipLaunchKernelGGL((k_nge_blocks<T, OPV>), grid(nb), dim3(256), 0, st, v, nt, best, has, bmin, bmax);        \
+  hipLaunchKernelGGL((k_nge<T, OPV>), grid(nt), dim3(256), 0, st, v, nt, d.within, op, mj, rank, cnt, stf, best, has, \
+                     bmin, bmax, cbits)
   h->kbeg("nge_search");
   switch (op) {
     case 2: SG_NGE_LAUNCH(2); break;
@@ -1702,19 +1759,37 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
   void* tmp = h->ws.get("scan_tmp", tb, st);
   HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-  uint32_t hflags[2] = {0, 0};
+  uint32_t hflags[4] = {0, 0, 0, 0};
   uint32_t total = 0;
-  HIPCHK(hipMemcpyAsync(hflags, stf, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hflags, stf, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(&total, off + n, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (hflags[0]) throw SgError(SG_EORDER, "closed-form kernel requires non-decreasing timestamps per key");
   if (hflags[1]) return false;   // a search outgrew NGE_MAX_SCAN: the walker takes this push
   MRec* mrec = nullptr;
   if (total) {
     mrec = (MRec*)h->ws.get("mrec", sizeof(MRec) * total, st);
     hipLaunchKernelGGL((k_nge_place<T>), grid(nt), dim3(256), 0, st, v, nt, mj, rank, off, mrec);
-    hipLaunchKernelGGL(k_nge_order, grid(n), dim3(256), 0, st, n, cnt, off, mrec);
+    hipLaunchKernelGGL(k_nge_order, grid(n), dim3(256), 0, st, n, cnt, off, mrec, stf + 2);
     HIPCHK(hipGetLastError());
+    uint32_t nbig = 0;
+    HIPCHK(hipMemcpyAsync(&nbig, stf + 2, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (nbig) {
+      // a trigger completed more than NGE_ORDER_SMALL partials: order every match by (trigger slot, e1 row)
+      uint64_t* k1 = (uint64_t*)h->ws.get("nge_k1", 8 * (size_t)total, st);
+      uint64_t* k2 = (uint64_t*)h->ws.get("nge_k2", 8 * (size_t)total, st);
+      uint32_t* i1 = (uint32_t*)h->ws.get("nge_i1", 4 * (size_t)total, st);
+      uint32_t* i2 = (uint32_t*)h->ws.get("nge_i2", 4 * (size_t)total, st);
+      MRec* m2 = (MRec*)h->ws.get("mrec2", sizeof(MRec) * total, st);
+      hipLaunchKernelGGL(k_nge_bigkeys, grid(total), dim3(256), 0, st, (int64_t)total, mrec, mj, off, nc, k1, i1);
+      size_t sb = 0;
+      HIPCHK(rocprim::radix_sort_pairs(nullptr, sb, k1, k2, i1, i2, (size_t)total, 0, 64, st));
+      void* stmp = h->ws.get("nge_sort_tmp", sb, st);
+      HIPCHK(rocprim::radix_sort_pairs(stmp, sb, k1, k2, i1, i2, (size_t)total, 0, 64, st));
+      hipLaunchKernelGGL(k_nge_permute, grid(total), dim3(256), 0, st, (int64_t)total, mrec, i2, m2);
+      HIPCHK(hipGetLastError());
+      mrec = m2;
+    }
   }
   h->mark(3);
   h->extra_marks = 0;
@@ -1745,15 +1820,20 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   }
   h->out.n += total;
   h->mark(4);
-  // carry: the suffix inside `within` of the last row
-  CarrySet& cs = es->carry[es->cur];
-  if (!h->opt.no_carry && nt > 0) {
-    uint32_t* q0d = (uint32_t*)h->ws.get("nge_q0", 4, st);
-    hipLaunchKernelGGL(k_nge_carry_start, dim3(1), dim3(64), 0, st, v, nt, d.within, q0d);
-    uint32_t q0 = 0;
-    HIPCHK(hipMemcpyAsync(&q0, q0d, 4, hipMemcpyDeviceToHost, st));
+  // carry: the partials still pending at the end of the push
+  if (carry) {
+    CarrySet& cs = es->carry[es->cur];
+    uint32_t* cboff = (uint32_t*)h->ws.get("carry_boff", sizeof(uint32_t) * (size_t)(cnb + 1), st);
+    uint32_t* bcnt = (uint32_t*)h->ws.get("carry_bcnt", sizeof(uint32_t) * (size_t)(cnb + 1), st);
+    hipLaunchKernelGGL(k_carry_bcount, dim3((unsigned)cnb), dim3(256), 0, st, nt, cbits, bcnt);
+    HIPCHK(hipMemsetAsync(bcnt + cnb, 0, sizeof(uint32_t), st));
+    size_t cb_tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, cb_tb, bcnt, cboff, (uint32_t)0, (size_t)cnb + 1, rocprim::plus<uint32_t>(), st));
+    void* ctmp = h->ws.get("carry_scan_tmp", cb_tb, st);
+    HIPCHK(rocprim::exclusive_scan(ctmp, cb_tb, bcnt, cboff, (uint32_t)0, (size_t)cnb + 1, rocprim::plus<uint32_t>(), st));
+    uint32_t ncar = 0;
+    HIPCHK(hipMemcpyAsync(&ncar, cboff + cnb, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    const uint32_t ncar = (uint32_t)(nt - q0);
     CarrySet& nx = es->carry[es->cur ^ 1];
     nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
     int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
@@ -1761,14 +1841,15 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
     for (int c = 0; c < SG_MAX_COLS; ++c)
       hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
     HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
-    CarryBufs cb;
-    memset(&cb, 0, sizeof(cb));
-    cb.ts = nx.ts;
-    cb.key = nx.key;
-    cb.flags = nx.flags;
-    for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
+    CarryBufs cbuf;
+    memset(&cbuf, 0, sizeof(cbuf));
+    cbuf.ts = nx.ts;
+    cbuf.key = nx.key;
+    cbuf.flags = nx.flags;
+    for (int c = 0; c < d.n_cols; ++c) { cbuf.col[c] = nx.col[c]; cbuf.nul[c] = nx.nul[c]; }
     if (ncar)
-      hipLaunchKernelGGL(k_nge_carry_copy, grid(ncar), dim3(256), 0, st, v, q0, ncar, d.n_cols, widths, bv.cols, cc, cb);
+      hipLaunchKernelGGL(k_carry_gather, dim3((unsigned)cnb), dim3(256), 0, st, v, nt, cbits, cboff, d.n_cols, widths,
+                         bv.cols, cc, cbuf);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
     nx.n = ncar;
@@ -1781,25 +1862,7 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
   return true;
 }
 
-#include "fgw.h"
-
-template <class T, int KG, int CAP>
-static void launch_fgw(int op, unsigned grid, size_t lds, hipStream_t st, const FgwArgs& A, const PtU4* grec,
-                       const uint8_t* glk, const FgwSeg* segs, uint32_t* gm32, PtU4* comp, uint32_t* cst, uint32_t* cend,
-                       uint32_t* kcnt, uint32_t* kent, uint32_t* fl) {
-#define SG_FGW(OPV)                                                                                                   \
-  HIPCHK(hipFuncSetAttribute((const void*)k_fgw<T, KG, CAP, OPV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-  hipLaunchKernelGGL((k_fgw<T, KG, CAP, OPV>), dim3(grid), dim3(256), lds, st, A, grec, glk, segs, gm32, comp, cst, cend,  \
-                     kcnt, kent, fl)
-  switch (op) {
-    case 2: SG_FGW(2); break;
-    case 3: SG_FGW(3); break;
-    case 4: SG_FGW(4); break;
-    default: SG_FGW(5); break;
-  }
-#undef SG_FGW
-  HIPCHK(hipGetLastError());
-}
+#include "part_wide.h"
 
 // Pass 1 of the key partition beyond 256 key groups (up to 4096 groups of 2^pp.lb keys, e.g. C5's 1M keys): rows ->
 // narrow walker records grouped by key group, arrival order kept inside a group, in two LDS counting passes --
@@ -1871,593 +1934,77 @@ static void part1_wide(SgHandle* h, const PackFn<T, true>& pk, KeyOf kf, uint32_
   }
 }
 
-// The fused group walk (fgw.h) for one push.  Returns 1 when the push is done, 0 when a precondition failed on the
-// GPU (nothing was changed: the caller runs the sorted-walker pipeline), -1 when narrow records cannot represent the
-// push (the caller falls back to wide records).
-template <class T>
-static int run_fgw(SgHandle* h, const BatchView& bv, int64_t n, const PushPlan& plan, const Virt& v, const SgCols& cc,
-                   uint32_t kb, int cap, const WalkArgs& wa0, EveryNextState* es) {
-  typedef WRec<T, true> R;
-  static_assert(sizeof(R) == 16, "narrow record");
-  const sg_nfa_desc& d = h->desc;
-  hipStream_t st = h->stream;
-  const int64_t nc = v.nc, nt = nc + n;
-  const int KG = cap <= 16 ? 256 : (cap <= 32 ? 128 : 64);
-  uint32_t lb = 0;
-  while ((1u << lb) < (uint32_t)KG) ++lb;
-  const uint32_t ng = (kb + KG - 1) / KG;
-  // ---- plan: part1 with digit = key >> lb, segments of <= 8192 rows (projection chunks)
-  PartPlan pp;
-  memset(&pp, 0, sizeof(pp));
-  pp.K = kb;
-  pp.lb = lb;
-  pp.ng = ng;
-  pp.two = 1;
-  uint32_t nb1 = 0;
-  while ((1u << nb1) < ng) ++nb1;
-  pp.nb1 = nb1;
-  pp.nb2 = lb;
-  // (part1 segments are the projection chunks: <= 65536 rows, ~2048 of them when the batch allows)
-  // 8192-row chunks (one LDS pass in the projection) unless the (group, chunk) tables would pass 4M entries
-  const int64_t cmax = (int64_t)ng * ((nt + FGW_SUB - 1) / FGW_SUB) <= ((int64_t)4 << 20) ? FGW_SUB : FGW_CHUNK;
-  const int64_t sub = std::max<int64_t>(1, std::min<int64_t>(cmax / PT1_ROWS, nt / ((int64_t)PT1_ROWS * 2048)));
-  pp.seg1 = (uint32_t)(PT1_ROWS * sub);
-  pp.ns1 = (uint32_t)std::max<int64_t>(1, (nt + pp.seg1 - 1) / pp.seg1);
-  KeyOf kf{bv.key, es->carry[es->cur].key, (uint32_t)nc};
-  const size_t n1 = (size_t)pp.ng * pp.ns1 + 1;
-  uint32_t* pk_flags = (uint32_t*)h->ws.get("pack_flags", sizeof(uint32_t), st);
-  HIPCHK(hipMemsetAsync(pk_flags, 0, sizeof(uint32_t), st));
-  uint32_t* h1 = (uint32_t*)h->ws.get("part_h1", sizeof(uint32_t) * n1, st);
-  uint32_t* o1 = (uint32_t*)h->ws.get("part_o1", sizeof(uint32_t) * n1, st);
-  R* grec = (R*)h->ws.get("grec", sizeof(R) * nt, st);
-  uint8_t* glk = (uint8_t*)h->ws.get("glk", nt, st);
-  PackFn<T, true> pk;
-  pk.v = v;
-  size_t tb = 0;
-  void* tmp = nullptr;
-  auto scan_u32 = [&](const uint32_t* in, uint32_t* outp, size_t cnt, const char* tmpname) {
-    size_t b = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, b, in, outp, (uint32_t)0, cnt, rocprim::plus<uint32_t>(), st));
-    void* tp = h->ws.get(tmpname, b, st);
-    HIPCHK(rocprim::exclusive_scan(tp, b, in, outp, (uint32_t)0, cnt, rocprim::plus<uint32_t>(), st));
-  };
-  if (ng <= 256) {
-    const size_t lds1 = sizeof(PartLds<R, PT1>);
-    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
-    h->kbeg("part_hist");
-    HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pp, nt, h1, pk_flags);
-    HIPCHK(hipGetLastError());
-    scan_u32(h1, o1, n1, "part_scan_tmp");
-    h->kend();
-    h->kbeg("part_group");
-    hipLaunchKernelGGL((k_part1<T, true>), dim3(pp.ns1), dim3(256), lds1, st, pk, kf, pp, nt, o1, grec, glk, pk_flags);
-    HIPCHK(hipGetLastError());
-    h->kend();
-  } else {
-    part1_wide<T>(h, pk, kf, kb, nt, pp, h1, o1, grec, glk, pk_flags);
-  }
-  uint32_t pkf = 0;
-  HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (pkf & PK_KEY_RANGE) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-  if (pkf & PK_INTERNAL) throw SgError(SG_EINVAL, "internal: key partition offsets out of range");
-  if (pkf & PK_TS_RANGE) return -1;
-  if (pkf & PK_PAY_RANGE) return 0;   // (payloads wider than 32 bits: the sorted walker gathers them by row)
-  h->mark(2);
-  // ---- walk segments
-  FgwArgs A;
-  memset(&A, 0, sizeof(A));
-  A.nc = nc;
-  A.within = (int32_t)std::min<int64_t>(d.within, 0x7fffffffll);
-  A.op = wa0.op;
-  A.stack_mode = wa0.stack_mode;
-  A.K = ng * (uint32_t)KG;   // (padded: carry scratch is indexed by dense key)
-  A.lb = lb;
-  A.ng = ng;
-  A.ns1 = pp.ns1;
-  A.seg1 = pp.seg1;
-  A.cap = (uint32_t)cap;
-  A.o1 = o1;
-  // one workgroup per CU (LDS): ~2 full rounds of (group, segment) workgroups, fewer segments = less replay
-  const uint32_t nsw = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(pp.ns1, 512 / ng));
-  A.nsw = nsw;
-  A.tsw = (pp.ns1 + nsw - 1) / nsw;
-  const uint32_t nw = ng * nsw;
-  FgwSeg* segs = (FgwSeg*)h->ws.get("fgw_segs", sizeof(FgwSeg) * nw, st);
-  uint32_t* caps = (uint32_t*)h->ws.get("fgw_caps", sizeof(uint32_t) * (nw + 1), st);
-  uint32_t* cofs = (uint32_t*)h->ws.get("fgw_cofs", sizeof(uint32_t) * (nw + 1), st);
-  h->kbeg("fgw_plan");
-  HIPCHK(hipMemsetAsync(caps + nw, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_fgw_plan, dim3((nw + 255) / 256), dim3(256), 0, st, A, (const PtU4*)grec, segs, caps);
-  HIPCHK(hipGetLastError());
-  tb = 0;
-  HIPCHK(rocprim::exclusive_scan(nullptr, tb, caps, cofs, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
-  tmp = h->ws.get("fgw_scan_tmp", tb, st);
-  HIPCHK(rocprim::exclusive_scan(tmp, tb, caps, cofs, (uint32_t)0, (size_t)nw + 1, rocprim::plus<uint32_t>(), st));
-  hipLaunchKernelGGL(k_fgw_cb, dim3((nw + 255) / 256), dim3(256), 0, st, nw, cofs, segs);
-  HIPCHK(hipGetLastError());
-  uint32_t ccap = 0;
-  HIPCHK(hipMemcpyAsync(&ccap, cofs + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  h->kend();
-  uint32_t* gm32 = (uint32_t*)h->ws.get("fgw_gm32", sizeof(uint32_t) * nt, st);
-  PtU4* comp = (PtU4*)h->ws.get("fgw_comp", sizeof(PtU4) * std::max<uint32_t>(ccap, 1), st);
-  uint32_t* cst = (uint32_t*)h->ws.get("fgw_cst", sizeof(uint32_t) * n1, st);
-  uint32_t* cend = (uint32_t*)h->ws.get("fgw_cend", sizeof(uint32_t) * n1, st);
-  uint32_t* ctot = (uint32_t*)h->ws.get("fgw_ctot", sizeof(uint32_t) * (pp.ns1 + 1), st);
-  uint32_t* cbase = (uint32_t*)h->ws.get("fgw_cbase", sizeof(uint32_t) * (pp.ns1 + 1), st);
-  const bool carry = !h->opt.no_carry;
-  const size_t kslots = (size_t)nsw * A.K;
-  uint32_t* kcnt = carry ? (uint32_t*)h->ws.get("fgw_kcnt", sizeof(uint32_t) * kslots, st) : nullptr;
-  uint32_t* kent = carry ? (uint32_t*)h->ws.get("fgw_kent", sizeof(uint32_t) * kslots * (cap + 1), st) : nullptr;
-  uint32_t* fl = (uint32_t*)h->ws.get("fgw_flags", sizeof(uint32_t), st);
-  HIPCHK(hipMemsetAsync(fl, 0, sizeof(uint32_t), st));
-  if (carry) HIPCHK(hipMemsetAsync(kcnt, 0xff, sizeof(uint32_t) * kslots, st));
-  h->kbeg("fgw_walk");
-  const int op = wa0.op;
-  if (KG == 256) {
-    launch_fgw<T, 256, 16>(op, nw, sizeof(FgwLds<T, 256, 16>), st, A, (const PtU4*)grec, glk, segs, gm32, comp, cst, cend,
-                           kcnt, kent, fl);
-  } else if (KG == 128) {
-    launch_fgw<T, 128, 32>(op, nw, sizeof(FgwLds<T, 128, 32>), st, A, (const PtU4*)grec, glk, segs, gm32, comp, cst, cend,
-                           kcnt, kent, fl);
-  } else {
-    launch_fgw<T, 64, 64>(op, nw, sizeof(FgwLds<T, 64, 64>), st, A, (const PtU4*)grec, glk, segs, gm32, comp, cst, cend,
-                          kcnt, kent, fl);
-  }
-  h->kend();
-  uint32_t hfl = 0;
-  HIPCHK(hipMemcpyAsync(&hfl, fl, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (hfl & FGW_F_INTERNAL) throw SgError(SG_EINVAL, "internal: fused group walk guard tripped");
-  if (hfl) {
-    if (getenv("SG_DEBUG_FGW")) fprintf(stderr, "fused group walk declined (flags %u)\n", hfl);
-    return 0;
-  }
-  h->mark(3);
-  h->kbeg("fgw_scan");
-  hipLaunchKernelGGL(k_fgw_ctot, dim3(pp.ns1 + 1), dim3(256), 0, st, A, cst, cend, ctot);
-  HIPCHK(hipGetLastError());
-  tb = 0;
-  HIPCHK(rocprim::exclusive_scan(nullptr, tb, ctot, cbase, (uint32_t)0, (size_t)pp.ns1 + 1, rocprim::plus<uint32_t>(), st));
-  tmp = h->ws.get("fgw_scan_tmp2", tb, st);
-  HIPCHK(rocprim::exclusive_scan(tmp, tb, ctot, cbase, (uint32_t)0, (size_t)pp.ns1 + 1, rocprim::plus<uint32_t>(), st));
-  uint32_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, cbase + pp.ns1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  h->kend();
-  h->split_out = 1;
-  h->extra_marks = 0;
-  WalkArgs wa = wa0;
-  char* out = h->out.reserve(total, d.n_select, st);
-  wa.out_base = h->out.n;
-  h->mark(5);
-  if (total) {
-    h->kbeg("fgw_project");
-    const size_t ldsp = sizeof(FgwProjLds) + sizeof(uint32_t) * (3 * (size_t)ng + 1);
-    HIPCHK(hipFuncSetAttribute((const void*)k_fgw_proj<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsp));
-    uint32_t* gcur = (uint32_t*)h->ws.get("fgw_gcur", sizeof(uint32_t) * (size_t)pp.ns1 * ng, st);
-    uint32_t* gsrc = (uint32_t*)h->ws.get("fgw_gsrc", sizeof(uint32_t) * (size_t)pp.ns1 * ng, st);
-    hipLaunchKernelGGL((k_fgw_proj<T>), dim3(pp.ns1), dim3(256), ldsp, st, A, wa, v, plan.pp, bv.cols, cc, gm32,
-                       (const PtU4*)comp, cst, cbase, gcur, gsrc, out, fl);
-    HIPCHK(hipGetLastError());
-    h->kend();
-    HIPCHK(hipMemcpyAsync(&hfl, fl, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (hfl & FGW_F_INTERNAL) throw SgError(SG_EINVAL, "internal: fused group projection guard tripped");
-  }
-  h->out.n += total;
-  h->mark(4);
-  // ---- carry into the next push
-  if (carry) {
-    h->kbeg("carry");
-    const uint32_t Kp = A.K;
-    uint32_t* cn = (uint32_t*)h->ws.get("fgw_ccnt", sizeof(uint32_t) * (Kp + 1), st);
-    uint32_t* coff = (uint32_t*)h->ws.get("fgw_coff", sizeof(uint32_t) * (Kp + 1), st);
-    uint32_t* cseg = (uint32_t*)h->ws.get("fgw_cseg", sizeof(uint32_t) * (Kp + 1), st);
-    hipLaunchKernelGGL(k_fgw_carry_count, dim3((Kp + 1 + 255) / 256), dim3(256), 0, st, Kp, nsw, kcnt, cn, cseg);
-    HIPCHK(hipGetLastError());
-    tb = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cn, coff, (uint32_t)0, (size_t)Kp + 1, rocprim::plus<uint32_t>(), st));
-    tmp = h->ws.get("fgw_carry_scan_tmp", tb, st);
-    HIPCHK(rocprim::exclusive_scan(tmp, tb, cn, coff, (uint32_t)0, (size_t)Kp + 1, rocprim::plus<uint32_t>(), st));
-    uint32_t ncar = 0;
-    HIPCHK(hipMemcpyAsync(&ncar, coff + Kp, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    CarrySet& cs = es->carry[es->cur];
-    CarrySet& nx = es->carry[es->cur ^ 1];
-    nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
-    int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
-    int32_t hw[SG_MAX_COLS];
-    for (int c = 0; c < SG_MAX_COLS; ++c)
-      hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
-    HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
-    CarryBufs cb;
-    memset(&cb, 0, sizeof(cb));
-    cb.ts = nx.ts;
-    cb.key = nx.key;
-    cb.flags = nx.flags;
-    for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
-    if (ncar)
-      hipLaunchKernelGGL((k_fgw_carry_copy<T>), dim3((Kp + 255) / 256), dim3(256), 0, st, v, Kp, (uint32_t)(cap + 1), cseg,
-                         coff, kent, d.n_cols, widths, bv.cols, cc, cb);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(st));
-    nx.n = ncar;
-    cs.n = 0;
-    es->cur ^= 1;
-    h->kend();
-  }
-  h->last_events = n;
-  h->last_matches = total;
-  h->last_spilled = 0;
-  return 1;
-}
-
-// ---- Keyed next match (partitioned closed form, narrow 4-byte values).  A pending partial i of
-// `every A -> B[B.x OP A.x] within T` leaves e2's list only by completing or by expiring, and nothing else a later row
-// does touches it: it completes at the first later row j of its key that can complete (F_CONS, a live value) with
-// x_j OP x_i and ts_j - ts_i <= T, or never (StreamPreStateProcessor.processAndReturn :292-337 with the lazy expiry
-// of isExpired :102-113, keys' timestamps non-decreasing).  So every candidate searches forward in the key-sorted
-// records on its own -- skipping 8-record blocks whose {min, max} of completing values rules the compare out -- and
-// the matches of a trigger are its candidates in pending (= arrival) order: counts per trigger row, a scan, each
-// match placed at (trigger offset + its rank), ranks put in candidate order where a trigger completed several.  Same
-// rows, same order as the walker (the walker's monotone stack / scanned list restate the same per-partial rule).
-static const uint32_t KN_NONE = 0xffffffffu;
-template <class T>
-struct KnBlk {
-  T mn, mx;          // completing values of the block's records (empty: mn > mx)
-  int32_t ts0;       // relative time of its first record
-  uint32_t segm;     // bit o: record o starts a key segment (or lies past the end)
-};
-
-static __global__ void k_kn_segbits(uint32_t K, const uint32_t* __restrict__ seg_b, const uint32_t* __restrict__ seg_e,
-                                    uint32_t* __restrict__ bits) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const uint32_t b = seg_b[k];
-  if (seg_e[k] > b) atomicOr(&bits[b >> 5], 1u << (b & 31));
-}
-
-template <class T>
-__global__ void __launch_bounds__(256) k_kn_blocks(const WRec<T, true>* __restrict__ srec, int64_t nt,
-                                                   const uint32_t* __restrict__ bits, KnBlk<T>* __restrict__ blk,
-                                                   uint32_t* __restrict__ flags) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t p0 = b * 8;
-  if (p0 >= nt) return;
-  const int cnt = (int)(nt - p0 < 8 ? nt - p0 : 8);
-  uint32_t segm = (bits[p0 >> 5] >> (p0 & 31)) & 0xffu;
-  segm |= 0xffu & ~((1u << cnt) - 1u);   // (records past the end: a boundary)
-  const T hi = std::numeric_limits<T>::has_infinity ? std::numeric_limits<T>::infinity() : std::numeric_limits<T>::max();
-  T mn = hi, mx = std::numeric_limits<T>::has_infinity ? -hi : std::numeric_limits<T>::lowest();   // (empty: mn > mx)
-  int64_t prev = (p0 > 0 && !(segm & 1u)) ? srec[p0 - 1].t() : INT64_MIN;
-  bool bad = false;
-  int32_t t0 = 0;
-  for (int o = 0; o < cnt; ++o) {
-    const WRec<T, true> r = srec[p0 + o];
-    const int64_t t = r.t();
-    if (o == 0) t0 = (int32_t)t;
-    if ((segm >> o) & 1u) prev = INT64_MIN;
-    bad |= t < prev;
-    prev = t;
-    const uint32_t f = r.rowf >> 30;
-    if ((f & F_CONS) && !is_nan_val<T>(r.val)) {
-      mn = r.val < mn ? r.val : mn;
-      mx = r.val > mx ? r.val : mx;
-    }
-  }
-  KnBlk<T> o;
-  o.mn = mn;
-  o.mx = mx;
-  o.ts0 = t0;
-  o.segm = segm;
-  blk[b] = o;
-  if (bad) atomicOr(flags, 1u);
-}
-
-template <class T>
-__device__ __forceinline__ bool kn_may(int op, T mn, T mx, T x) {
-  if (mn > mx) return false;
-  switch (op) {
-    case 2: return mx > x;
-    case 3: return mx >= x;
-    case 4: return mn < x;
-    default: return mn <= x;
-  }
-}
-
-template <class T, int OP>
-__global__ void __launch_bounds__(256) k_kn_find(const WRec<T, true>* __restrict__ srec, int64_t nt,
-                                                 const KnBlk<T>* __restrict__ blk, int64_t within, int op, int64_t nc,
-                                                 uint32_t* __restrict__ mj, uint32_t* __restrict__ rank,
-                                                 uint32_t* __restrict__ cnt) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= nt) return;
-  const WRec<T, true> r = srec[p];
-  uint32_t out = KN_NONE;
-  if (((r.rowf >> 30) & F_CAND) && !is_nan_val<T>(r.val)) {
-    const T x = r.val;
-    const int64_t ti = r.t();
-    int64_t b = p >> 3;
-    uint32_t o0 = (uint32_t)(p & 7) + 1u;
-    const int64_t nb = (nt + 7) >> 3;
-    while (b < nb) {
-      const KnBlk<T> B = blk[b];
-      uint32_t consider = 0xffu & ~((1u << o0) - 1u);
-      const uint32_t sm = B.segm & consider;
-      const uint32_t endo = sm ? (uint32_t)__builtin_ctz(sm) : 8u;
-      consider &= (1u << endo) - 1u;
-      if (o0 == 0 && consider && (int64_t)B.ts0 - ti > within) break;   // the block starts past `within`
-      bool stop = false;
-      if (consider && kn_may<T>(OP ? OP : op, B.mn, B.mx, x)) {
-        for (uint32_t o = 0; o < 8; ++o) {
-          if (!((consider >> o) & 1u)) continue;
-          const WRec<T, true> q = srec[b * 8 + o];
-          if (q.t() - ti > within) { stop = true; break; }
-          if (((q.rowf >> 30) & F_CONS) && !is_nan_val<T>(q.val) && cmp_sel<OP, T>(op, q.val, x)) {
-            out = (uint32_t)(b * 8 + o);
-            stop = true;
-            break;
-          }
-        }
-      }
-      if (stop || endo < 8) break;
-      ++b;
-      o0 = 0;
-    }
-  }
-  if (out != KN_NONE) {
-    const uint32_t r2 = srec[out].rowf & ROW_MASK;
-    if ((int64_t)r2 >= nc) rank[p] = atomicAdd(&cnt[r2 - nc], 1u);
-    else out = KN_NONE;   // (completed by a carried row: delivered by an earlier push)
-  }
-  mj[p] = out;
-}
-
-template <class T>
-__global__ void k_kn_place(const WRec<T, true>* __restrict__ srec, int64_t nt, const uint32_t* __restrict__ mj,
-                           const uint32_t* __restrict__ rank, const uint32_t* __restrict__ off, int64_t nc, int pay,
-                           int pfloat, MatchSink ms) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= nt) return;
-  const uint32_t j = mj[p];
-  if (j == KN_NONE) return;
-  const WRec<T, true> r = srec[p];
-  const uint32_t r2 = srec[j].rowf & ROW_MASK;
-  ms.put(off[r2 - nc] + rank[p], r.rowf & ROW_MASK, r2, val_bits<T>(r.val), pay ? r.p(pfloat) : 0);
-}
-
-// a trigger that completed several partials: its matches in pending order (candidate rows ascending)
-static __global__ void k_kn_order(int64_t n, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                                  PtU4* __restrict__ rec) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
-  const uint32_t c = cnt[b];
-  if (c < 2) return;
-  PtU4* e = rec + off[b];
-  for (uint32_t i = 1; i < c; ++i) {
-    const PtU4 x = e[i];
-    uint32_t k = i;
-    while (k > 0 && e[k - 1].x > x.x) {
-      e[k] = e[k - 1];
-      --k;
-    }
-    e[k] = x;
-  }
-}
-
-template <class T>
-__global__ void k_kn_carry(Src<T, true> src, uint32_t K, const uint32_t* __restrict__ seg_b,
-                           const uint32_t* __restrict__ seg_e, int64_t within, uint32_t* __restrict__ q0s,
-                           uint32_t* __restrict__ cn) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const uint32_t sb = seg_b[k], se = seg_e[k];
-  if (se > sb) {
-    const uint32_t q0 = lb_ts(src, sb, se, src.ts(se - 1) - within);
-    q0s[k] = q0;
-    cn[k] = se - q0;
-  } else {
-    cn[k] = 0;
-  }
-}
-
-// Carry into the next push: per key the rows from carry_q0[k] on (carry_n[k] of them, the rows inside `within` of the
-// key's last row), copied out of this push's virtual rows into the other carry set.
+// keys whose rows (sorted positions of one key, carried rows first) go back in time
 template <class T, bool N>
-static void carry_out_rows(SgHandle* h, EveryNextState* es, uint32_t K, int64_t nt, const Src<T, N>& src,
-                           const uint32_t* seg_b, const uint32_t* seg_e, const Virt& v, const BatchView& bv,
-                           const SgCols& cc, const uint32_t* carry_q0, const uint32_t* carry_n) {
+__global__ void k_order_keys(Src<T, N> src, KeyOf kf, const uint32_t* __restrict__ seg_b, uint32_t K, int64_t nt,
+                             uint8_t* __restrict__ kx) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; p < nt; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = kf(src.row((uint32_t)p));
+    if (k < K && (uint32_t)p > seg_b[k] && src.ts((uint32_t)p) < src.ts((uint32_t)(p - 1))) kx[k] = 1;
+  }
+}
+
+// rows listed in rows[0, *n) -> carry bitmask
+static __global__ void k_carry_mark_list(const uint32_t* __restrict__ rows, const uint32_t* __restrict__ n,
+                                         uint32_t* __restrict__ bits) {
+  const uint32_t m = *n;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
+    atomicOr(&bits[rows[i] >> 5], 1u << (rows[i] & 31));
+}
+
+// The next push's carried rows, in arrival order: per key the sorted positions [carry_q0, carry_q0 + carry_n) (keys
+// on the fast path), plus the listed pending partials of keys that walked exact (alive, alive_n; may be null).
+template <class T, bool N>
+static void carry_out_rows(SgHandle* h, EveryNextState* es, uint32_t K, int64_t nt, const Src<T, N>& src, const Virt& v,
+                           const BatchView& bv, const SgCols& cc, const uint32_t* carry_q0, const uint32_t* carry_n,
+                           const uint32_t* alive, const uint32_t* alive_n) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
   CarrySet& cs = es->carry[es->cur];
-  (void)seg_b;
-  (void)seg_e;
-  {
-    static const bool by_key = getenv("SG_CARRY_BY_KEY") != nullptr;   // (experiments: the per-key copy)
-    uint32_t* coff = (uint32_t*)h->ws.get("carry_off", sizeof(uint32_t) * (K + 1), st);
-    uint32_t* cbits = nullptr;
-    uint32_t* cboff = nullptr;
-    uint32_t* ccount = (uint32_t*)h->ws.get("carry_count", sizeof(uint32_t), st);
-    if (by_key) {
-      size_t tb = 0;
-      HIPCHK(rocprim::exclusive_scan(nullptr, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
-      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
-      HIPCHK(rocprim::exclusive_scan(tmp, tb, carry_n, coff, (uint32_t)0, (size_t)K + 1, rocprim::plus<uint32_t>(), st));
-      HIPCHK(hipMemcpyAsync(ccount, coff + K, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    } else {
-      h->kbeg("carry");
-      const int64_t nw = (nt + 31) / 32, nb = (nt + CARRY_BLK - 1) / CARRY_BLK;
-      cbits = (uint32_t*)h->ws.get("carry_bits", sizeof(uint32_t) * (size_t)(nb * 256), st);
-      cboff = (uint32_t*)h->ws.get("carry_boff", sizeof(uint32_t) * (size_t)(nb + 1), st);
-      uint32_t* bcnt = (uint32_t*)h->ws.get("carry_bcnt", sizeof(uint32_t) * (size_t)(nb + 1), st);
-      HIPCHK(hipMemsetAsync(cbits, 0, sizeof(uint32_t) * (size_t)(nb * 256), st));
-      hipLaunchKernelGGL((k_carry_mark<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n, cbits);
-      hipLaunchKernelGGL(k_carry_bcount, dim3((unsigned)nb), dim3(256), 0, st, nt, cbits, bcnt);
-      HIPCHK(hipMemsetAsync(bcnt + nb, 0, sizeof(uint32_t), st));
-      HIPCHK(hipGetLastError());
-      size_t tb = 0;
-      HIPCHK(rocprim::exclusive_scan(nullptr, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
-      void* tmp = h->ws.get("carry_scan_tmp", tb, st);
-      HIPCHK(rocprim::exclusive_scan(tmp, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
-      HIPCHK(hipMemcpyAsync(ccount, cboff + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-      (void)nw;
-      h->kend();
-    }
-    uint32_t ncar = 0;
-    HIPCHK(hipMemcpyAsync(&ncar, ccount, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    CarrySet& nx = es->carry[es->cur ^ 1];
-    nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
-    int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
-    int32_t hw[SG_MAX_COLS];
-    for (int c = 0; c < SG_MAX_COLS; ++c)
-      hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
-    HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
-    CarryBufs cb;
-    memset(&cb, 0, sizeof(cb));
-    cb.ts = nx.ts;
-    cb.key = nx.key;
-    cb.flags = nx.flags;
-    for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
-    if (ncar && by_key)
-      hipLaunchKernelGGL((k_carry_copy<T, N>), dim3((ncar + 255) / 256), dim3(256), 0, st, src, K, ncar, carry_q0,
-                         coff, d.n_cols, widths, bv.cols, cc, cb);
-    else if (ncar)
-      hipLaunchKernelGGL(k_carry_gather, dim3((unsigned)((nt + CARRY_BLK - 1) / CARRY_BLK)), dim3(256), 0, st, v, nt,
-                         cbits, cboff, d.n_cols, widths, bv.cols, cc, cb);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(st));
-    nx.n = ncar;
-    cs.n = 0;
-    es->cur ^= 1;
-  }
-}
-
-// The keyed next-match pipeline for one push (after the key partition).  1: done; 0: a precondition the walker
-// handles differently (payloads wider than 32 bits, a key whose timestamps go back -- the walker then decides);
-// -1: narrow records cannot represent the push (the caller retries with wide records).
-template <class T>
-static int run_keyed_next(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, int64_t nt, uint32_t K,
-                          const PushPlan& plan, const Virt& v, const SgCols& cc, const Src<T, true>& src,
-                          const uint32_t* seg_b, const uint32_t* seg_e, uint32_t* pk_flags, int op,
-                          EveryNextState* es, int b_state) {
-  const sg_nfa_desc& d = h->desc;
-  hipStream_t st = h->stream;
-  uint32_t pkf = 0;
-  HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (pkf & PK_KEY_RANGE) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-  if (pkf & PK_INTERNAL) throw SgError(SG_EINVAL, "internal: key partition offsets out of range");
-  if (pkf & PK_TS_RANGE) return -1;
-  if (pkf & PK_PAY_RANGE) return 0;
-  const int64_t nb = (nt + 7) / 8;
-  const size_t nwords = (size_t)((nt + 31) / 32 + 1);
-  uint32_t* bits = (uint32_t*)h->ws.get("kn_bits", sizeof(uint32_t) * nwords, st);
-  KnBlk<T>* blk = (KnBlk<T>*)h->ws.get("kn_blk", sizeof(KnBlk<T>) * (size_t)nb, st);
-  uint32_t* kfl = (uint32_t*)h->ws.get("kn_flags", 2 * sizeof(uint32_t), st);
-  HIPCHK(hipMemsetAsync(bits, 0, sizeof(uint32_t) * nwords, st));
-  HIPCHK(hipMemsetAsync(kfl, 0, 2 * sizeof(uint32_t), st));
-  h->kbeg("next_blocks");
-  hipLaunchKernelGGL(k_kn_segbits, dim3((K + 255) / 256), dim3(256), 0, st, K, seg_b, seg_e, bits);
-  hipLaunchKernelGGL((k_kn_blocks<T>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, src.srec, nt, bits, blk, kfl);
+  uint32_t* ccount = (uint32_t*)h->ws.get("carry_count", sizeof(uint32_t), st);
+  h->kbeg("carry");
+  const int64_t nb = (nt + CARRY_BLK - 1) / CARRY_BLK;
+  uint32_t* cbits = (uint32_t*)h->ws.get("carry_bits", sizeof(uint32_t) * (size_t)(nb * 256), st);
+  uint32_t* cboff = (uint32_t*)h->ws.get("carry_boff", sizeof(uint32_t) * (size_t)(nb + 1), st);
+  uint32_t* bcnt = (uint32_t*)h->ws.get("carry_bcnt", sizeof(uint32_t) * (size_t)(nb + 1), st);
+  HIPCHK(hipMemsetAsync(cbits, 0, sizeof(uint32_t) * (size_t)(nb * 256), st));
+  hipLaunchKernelGGL((k_carry_mark<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n, cbits);
+  if (alive && alive_n)
+    hipLaunchKernelGGL(k_carry_mark_list, dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 4096)), dim3(256), 0, st,
+                       alive, alive_n, cbits);
+  hipLaunchKernelGGL(k_carry_bcount, dim3((unsigned)nb), dim3(256), 0, st, nt, cbits, bcnt);
+  HIPCHK(hipMemsetAsync(bcnt + nb, 0, sizeof(uint32_t), st));
   HIPCHK(hipGetLastError());
+  size_t tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
+  void* tmp = h->ws.get("carry_scan_tmp", tb, st);
+  HIPCHK(rocprim::exclusive_scan(tmp, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
+  HIPCHK(hipMemcpyAsync(ccount, cboff + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   h->kend();
-  uint32_t order_bad = 0;
-  HIPCHK(hipMemcpyAsync(&order_bad, kfl, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint32_t ncar = 0;
+  HIPCHK(hipMemcpyAsync(&ncar, ccount, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (order_bad) return 0;
-  uint32_t* cnt = (uint32_t*)h->ws.get("cnt", sizeof(uint32_t) * (n + 1), st);
-  uint32_t* off = (uint32_t*)h->ws.get("off", sizeof(uint32_t) * (n + 1), st);
-  uint32_t* mj = (uint32_t*)h->ws.get("kn_mj", sizeof(uint32_t) * (size_t)nt, st);
-  uint32_t* rank = (uint32_t*)h->ws.get("kn_rank", sizeof(uint32_t) * (size_t)nt, st);
-  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
-  const dim3 g((unsigned)((nt + 255) / 256)), b256(256);
-  h->kbeg("next_search");
-  switch (op) {
-    case 2: hipLaunchKernelGGL((k_kn_find<T, 2>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
-    case 3: hipLaunchKernelGGL((k_kn_find<T, 3>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
-    case 4: hipLaunchKernelGGL((k_kn_find<T, 4>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
-    default: hipLaunchKernelGGL((k_kn_find<T, 5>), g, b256, 0, st, src.srec, nt, blk, (int64_t)d.within, op, nc, mj, rank, cnt); break;
-  }
+  CarrySet& nx = es->carry[es->cur ^ 1];
+  nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
+  int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
+  int32_t hw[SG_MAX_COLS];
+  for (int c = 0; c < SG_MAX_COLS; ++c)
+    hw[c] = (c < d.n_cols && (d.col_type[c] == SG_T_LONG || d.col_type[c] == SG_T_DOUBLE)) ? 8 : 4;
+  HIPCHK(hipMemcpyAsync(widths, hw, sizeof(hw), hipMemcpyHostToDevice, st));
+  CarryBufs cb;
+  memset(&cb, 0, sizeof(cb));
+  cb.ts = nx.ts;
+  cb.key = nx.key;
+  cb.flags = nx.flags;
+  for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
+  if (ncar)
+    hipLaunchKernelGGL(k_carry_gather, dim3((unsigned)nb), dim3(256), 0, st, v, nt, cbits, cboff, d.n_cols, widths,
+                       bv.cols, cc, cb);
   HIPCHK(hipGetLastError());
-  h->kend();
-  h->kbeg("count_scan");
-  {
-    size_t tb = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-    void* tmp = h->ws.get("scan_tmp", tb, st);
-    HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-  }
-  h->kend();
-  h->mark(3);
-  uint32_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  h->extra_marks = 0;
-  WalkArgs wa;
-  memset(&wa, 0, sizeof(wa));
-  wa.nt = nt;
-  wa.K = K;
-  wa.partitioned = 1;
-  wa.op = op;
-  wa.base_index = bv.base_index;
-  wa.index = bv.index;
-  wa.n_select = d.n_select;
-  wa.stride = 32 + 8 * d.n_select;
-  {
-    const int rb = d.recv_of_stream[d.states[b_state].stream];
-    wa.multi = d.receivers[rb].multi;
-    wa.b_slot = 0;
-    if (wa.multi) {
-      const sg_receiver_desc& r = d.receivers[rb];
-      for (int q = 0; q < r.n; ++q)
-        if (r.pres[r.n - 1 - q] == b_state) wa.b_slot = q;   // eventSequence = reversed init order
-    }
-  }
-  MatchSink ms{nullptr, 1, 0, kfl + 1};
-  h->split_out = 1;
-  if (total) {
-    char* out = h->out.reserve(total, d.n_select, st);
-    wa.out_base = h->out.n;
-    ms.cap = total;
-    ms.rec = h->ws.get("mrec", sizeof(MRec16) * (size_t)total, st);
-    h->mark(5);
-    h->kbeg("next_place");
-    hipLaunchKernelGGL((k_kn_place<T>), g, b256, 0, st, src.srec, nt, mj, rank, off, nc, plan.pcol >= 0 ? 1 : 0,
-                       v.pfloat, ms);
-    hipLaunchKernelGGL(k_kn_order, dim3((unsigned)((n + 255) / 256)), b256, 0, st, n, cnt, off, (PtU4*)ms.rec);
-    HIPCHK(hipGetLastError());
-    h->kend();
-    h->kbeg("project");
-    hipLaunchKernelGGL((k_project<T>), dim3((unsigned)(((int64_t)total + 255) / 256)), b256, (size_t)256 * wa.stride, st,
-                       wa, v, plan.pp, bv.cols, cc, ms, off, (int64_t)total, out);
-    HIPCHK(hipGetLastError());
-    h->kend();
-    h->out.n += total;
-  } else {
-    h->mark(5);
-  }
-  h->mark(4);
-  if (!h->opt.no_carry) {
-    uint32_t* carry_q0 = (uint32_t*)h->ws.get("carry_q0", sizeof(uint32_t) * K, st);
-    uint32_t* carry_n = (uint32_t*)h->ws.get("carry_n", sizeof(uint32_t) * (K + 1), st);
-    HIPCHK(hipMemsetAsync(carry_n + K, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL((k_kn_carry<T>), dim3((K + 255) / 256), b256, 0, st, src, K, seg_b, seg_e, (int64_t)d.within,
-                       carry_q0, carry_n);
-    HIPCHK(hipGetLastError());
-    carry_out_rows<T, true>(h, es, K, nt, src, seg_b, seg_e, v, bv, cc, carry_q0, carry_n);
-  }
-  uint32_t guard = 0;
-  HIPCHK(hipMemcpyAsync(&guard, kfl + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (guard) throw SgError(SG_EINVAL, "internal: next-match placement guard tripped");
-  h->last_events = n;
-  h->last_matches = total;
-  h->last_spilled = 0;
-  return 1;
+  nx.n = ncar;
+  cs.n = 0;
+  es->cur ^= 1;
 }
 
 template <class T, bool N>
@@ -2530,6 +2077,8 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   v.c_ts = cs.ts;
   v.c_key = cs.key;
   v.c_flags = cs.flags;
+  v.stream = bv.stream;
+  v.s_b = pa.s_b;
   v.c_val_a = cs.col[val_col_a];
   v.c_val_b = cs.col[val_col_b];
   if (plan.pcol >= 0) {
@@ -2558,47 +2107,9 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   seg_b = (uint32_t*)h->ws.get("seg_b", sizeof(uint32_t) * K, st);
   seg_e = (uint32_t*)h->ws.get("seg_e", sizeof(uint32_t) * K, st);
   const dim3 pgrd((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 32));
-  // fused group walk (fgw.h): no key-sorted copy, one walk, arrival-ordered projection.  Opt-in (SG_FGW=1): measured
-  // slower than the sorted-walker pipeline on C2 (k_fgw 7.2 + k_fgw_proj 9.9 ms against 7.6 ms for the whole pipeline,
-  // profiles/r04/C2_fgw_v2_kernel_stats.csv) -- kept, parity-tested, as the base of a later attempt
-  if constexpr (N && sizeof(T) == 4) {
-    const char* fgw_env = getenv("SG_FGW");
-    const bool fgw_on = fgw_env && fgw_env[0] == '1';
-    if (d.partitioned && h->opt.partition_sort == 0 && !h->opt.walker_only && fgw_on && n > 0) {
-      int64_t tfl[2] = {0, 0};
-      HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      const int64_t win = window_rows(kb, nt, d.within, tfl[1] - tfl[0]);
-      const int cap = h->opt.ring_cap > 0 ? h->opt.ring_cap : pick_cap(win);
-      const int KG = cap <= 16 ? 256 : (cap <= 32 ? 128 : 64);
-      if (cap <= 64 && (kb + KG - 1) / KG <= 4096u) {
-        WalkArgs w0;
-        memset(&w0, 0, sizeof(w0));
-        w0.partitioned = 1;
-        w0.op = op;
-        w0.stack_mode = ((val_col_a == val_col_b) && (pa.s_a == pa.s_b) && pa.prog_b_len == 0) ? 1 : 0;
-        w0.base_index = bv.base_index;
-        w0.index = bv.index;
-        const int rbx = d.recv_of_stream[d.states[b_state].stream];
-        w0.multi = d.receivers[rbx].multi;
-        if (w0.multi) {
-          const sg_receiver_desc& r = d.receivers[rbx];
-          for (int q = 0; q < r.n; ++q)
-            if (r.pres[r.n - 1 - q] == b_state) w0.b_slot = q;   // eventSequence = reversed init order
-        }
-        w0.n_select = d.n_select;
-        w0.stride = 32 + 8 * d.n_select;
-        const int rr = run_fgw<T>(h, bv, n, plan, v, cc, kb, cap, w0, es);
-        if (rr == 1) return true;
-        if (rr == -1) return false;
-      }
-    }
-  }
   // beyond 65536 keys (C5: 1M per GPU) the LDS partition runs its first pass in two (part1_wide: narrow records only,
   // up to 4096 groups of 256 keys) -- three counting passes in place of pack + a 3-pass onesweep sort + bounds
-  const bool wide_part = N && sizeof(R) == 16 && sizeof(T) == 4 && kb > 65536u && kb <= (4096u << 8) &&
-                         !getenv("SG_NO_WIDE_PART");
+  const bool wide_part = N && sizeof(R) == 16 && sizeof(T) == 4 && kb > 65536u && kb <= (4096u << 8);
   const bool lds_part = d.partitioned && (kb <= 65536u || wide_part) && h->opt.partition_sort == 0;
   if (lds_part) {
     PartPlan pp = part_plan(kb, nt);
@@ -2718,20 +2229,6 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemcpyAsync(seg_e, &seg[1], sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
   h->mark(2);
-  if constexpr (N && sizeof(T) == 4) {
-    // keyed next match (no walk units, no ring, one search per candidate): opt-in, SG_KEYED_NEXT=1.  Exact, but
-    // measured slower than the walker on C2 (search 6.3 + blocks 3.4 + place 2.3 + order 1.4 ms against 3.5 ms of
-    // units / transpose / count and record walks: one candidate's search is a chain of dependent loads and a wave
-    // waits for its longest; profiles/r04/C2_keyed_next_kernel_stats.csv)
-    const char* kn_env = getenv("SG_KEYED_NEXT");
-    const bool kn_on = kn_env && kn_env[0] == '1';
-    if (d.partitioned && !h->opt.walker_only && h->opt.ring_cap == 0 && kn_on && n > 0) {
-      const int r = run_keyed_next<T>(h, bv, n, nc, nt, K, plan, v, cc, src, seg_b, seg_e, pk_flags, op, es, b_state);
-      if (r == 1) return true;
-      if (r == -1) return false;
-    }
-  }
-
   // ---- 3. count pass + scan
   WalkArgs wa;
   memset(&wa, 0, sizeof(wa));
@@ -2782,22 +2279,32 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   uint32_t* off = (uint32_t*)h->ws.get("off", sizeof(uint32_t) * (n + 1), st);
   uint32_t* carry_q0 = (uint32_t*)h->ws.get("carry_q0", sizeof(uint32_t) * K, st);
   uint32_t* carry_n = (uint32_t*)h->ws.get("carry_n", sizeof(uint32_t) * (K + 1), st);
-  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
   uint32_t* emap = (uint32_t*)h->ws.get("emap", sizeof(uint32_t) * (nt / 32 + 2), st);
-  HIPCHK(hipMemsetAsync(emap, 0, sizeof(uint32_t) * (nt / 32 + 2), st));
-  HIPCHK(hipMemsetAsync(wst, 0, sizeof(WalkStats), st));
-  if (wa.carry_out) HIPCHK(hipMemsetAsync(carry_n, 0, sizeof(uint32_t) * (K + 1), st));
   const dim3 wblk(WALK_BLOCK), wgrd((unsigned)((units + WALK_BLOCK - 1) / WALK_BLOCK));
   const uint32_t nw = (uint32_t)((units + 63) / 64);
   MatchSink ms{nullptr, 0, 0, &wst->internal};   // (record pass: set once the match list is allocated)
-  uint32_t* wlen = nullptr;
-  uint32_t* wrow = nullptr;
+  uint32_t* wlen = (uint32_t*)h->ws.get("wlen", sizeof(uint32_t) * (nw + 1), st);
+  uint32_t* wrow = (uint32_t*)h->ws.get("wrow", sizeof(uint32_t) * (nw + 1), st);
   R* tile = nullptr;
   uint64_t* emask = nullptr;
-  {
+  auto scan_counts = [&]() {
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+  };
+  WalkStats hs;
+  uint32_t total = 0;
+  char* big = nullptr;
+  h->extra_marks = 0;
+  // Pass 0 walks every key on the fast path, which needs each key's time not to go back.  When some key's does
+  // (its rows, carried ones included, out of time order), pass 1 redoes the count with those keys on the exact walker.
+  for (int pass = 0;; ++pass) {
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
+    HIPCHK(hipMemsetAsync(emap, 0, sizeof(uint32_t) * (nt / 32 + 2), st));
+    HIPCHK(hipMemsetAsync(wst, 0, sizeof(WalkStats), st));
+    if (wa.carry_out) HIPCHK(hipMemsetAsync(carry_n, 0, sizeof(uint32_t) * (K + 1), st));
     // lane-interleaved tiles: unit ranges -> per-wave rows -> LDS transpose of the sorted records
-    wlen = (uint32_t*)h->ws.get("wlen", sizeof(uint32_t) * (nw + 1), st);
-    wrow = (uint32_t*)h->ws.get("wrow", sizeof(uint32_t) * (nw + 1), st);
     HIPCHK(hipMemsetAsync(wlen, 0, sizeof(uint32_t) * (nw + 1), st));
     h->kbeg("units");
     hipLaunchKernelGGL((k_units<T, N>), dim3((unsigned)(nw * 64 + 255) / 256), dim3(256), 0, st, wa, src, seg_b, seg_e,
@@ -2843,41 +2350,46 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     launch_walk_t<T, N, false>(op, wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, ms,
                                emask, wst, carry_q0, carry_n);
     h->kend();
-  }
-  auto scan_counts = [&]() {
-    size_t tb = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-    void* tmp = h->ws.get("scan_tmp", tb, st);
-    HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-  };
-  h->kbeg("count_scan");
-  scan_counts();
-  h->kend();
-  h->mark(3);
-  WalkStats hs;
-  uint32_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&hs, wst, sizeof(WalkStats), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  char* big = nullptr;
-  h->extra_marks = 0;
-  if (hs.n_ovf) {
-    // units whose pending list outgrew the LDS ring: redo them with unbounded HBM lists
-    wa.big_cap = (std::max<uint32_t>(hs.ovf_need, 1) + 1) & ~1u;
-    big = (char*)h->ws.get("big_lists", (size_t)hs.n_ovf * wa.big_cap * PendBytes<T>::hbm, st);
-    h->mark(6);
-    hipLaunchKernelGGL((k_walk<T, N, false, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
-                       ms, emap, wst, big, carry_q0, carry_n);
-    HIPCHK(hipGetLastError());
+    h->kbeg("count_scan");
     scan_counts();
-    h->mark(7);
-    h->extra_marks = 1;
+    h->kend();
+    h->mark(3);
     HIPCHK(hipMemcpyAsync(&total, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&hs, wst, sizeof(WalkStats), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (hs.n_ovf) {
+      // units whose pending list outgrew the LDS ring (or that walk exact): redo them with unbounded HBM lists
+      if (hs.internal & 16u) throw SgError(SG_ECAPACITY, "HBM pending lists exceed 2^32 entries: push smaller batches");
+      wa.big_total = hs.ovf_total;
+      big = (char*)h->ws.get("big_lists", (size_t)hs.ovf_total * PendBytes<T>::hbm, st);
+      h->mark(6);
+      hipLaunchKernelGGL((k_walk<T, N, false, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
+                         ms, emap, wst, big, carry_q0, carry_n);
+      HIPCHK(hipGetLastError());
+      scan_counts();
+      h->mark(7);
+      h->extra_marks = 1;
+      HIPCHK(hipMemcpyAsync(&total, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&hs, wst, sizeof(WalkStats), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    if (hs.internal) throw SgError(SG_EINVAL, "internal: walker guard tripped (" + std::to_string(hs.internal) + ")");
+    if (!hs.order_err) break;
+    if (pass) throw SgError(SG_EINVAL, "internal: a key's time went back on the fast walker after the exact pass");
+    // keys whose time goes back (StreamPreStateProcessor.isExpired compares |e1.ts - ts| with `within`, and a playback
+    // clock that stays put still processes the row, TimestampGeneratorImpl.java:106-125): exact walker
+    uint8_t* kx = (uint8_t*)h->ws.get("kexact", K, st);
+    if (d.partitioned) {
+      HIPCHK(hipMemsetAsync(kx, 0, K, st));
+      KeyOf kf{bv.key, cs.key, (uint32_t)nc};
+      hipLaunchKernelGGL((k_order_keys<T, N>), dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 256 * 64)), dim3(256), 0,
+                         st, src, kf, seg_b, K, nt, kx);
+      HIPCHK(hipGetLastError());
+    } else {
+      HIPCHK(hipMemsetAsync(kx, 1, K, st));
+    }
+    wa.kexact = kx;
   }
-  if (hs.internal) throw SgError(SG_EINVAL, "internal: walker guard tripped (" + std::to_string(hs.internal) + ")");
-  if (hs.order_err) throw SgError(SG_EORDER, "closed-form kernel requires non-decreasing timestamps per key");
 
   // ---- 5. record pass
   char* out = nullptr;
@@ -2891,6 +2403,11 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     ms.cap = total;
     ms.rec = h->ws.get("mrec", (ms.narrow ? sizeof(MRec16) : sizeof(MRec)) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
+    if (wa.kexact && wa.carry_out) {
+      wa.alive = (uint32_t*)h->ws.get("alive_rows", sizeof(uint32_t) * (size_t)std::max<int64_t>(nt, 1), st);
+      wa.alive_n = (uint32_t*)h->ws.get("alive_n", sizeof(uint32_t), st);
+      HIPCHK(hipMemsetAsync(wa.alive_n, 0, sizeof(uint32_t), st));
+    }
     h->kbeg("walk_record");
     launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, ms,
                               emask, wst, carry_q0, carry_n);
@@ -2917,7 +2434,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemcpyAsync(&guard, &wst->internal, sizeof(uint32_t), hipMemcpyDeviceToHost, st));   // record-pass guards
     HIPCHK(hipStreamSynchronize(st));
     if (guard) throw SgError(SG_EINVAL, "internal: record-pass guard tripped (" + std::to_string(guard) + ")");
-    carry_out_rows<T, N>(h, es, K, nt, src, seg_b, seg_e, v, bv, cc, carry_q0, carry_n);
+    carry_out_rows<T, N>(h, es, K, nt, src, v, bv, cc, carry_q0, carry_n, wa.alive, wa.alive_n);
   }
   h->last_events = n;
   h->last_matches = total;

@@ -953,12 +953,15 @@ struct KeyMachine {
 // that fire on the global playback clock.  Timer semantics: InputHandler.send -> setCurrentTimestamp
 // (C/stream/input/InputHandler.java:57-65, TimestampGeneratorImpl.java:106-125) notifies every
 // Scheduler in registration order before the row is dispatched; a Scheduler fires while its FIFO head
-// <= clock (Scheduler.java:74-86,179-214).  With non-decreasing timestamps (checked by the caller) the
-// first row that fires a head value h after position `pos` is the first row with ts >= h.
+// <= clock (Scheduler.java:74-86,179-214).  The clock is the largest timestamp so far: a row whose time goes
+// back leaves it where it is and notifies no scheduler (setCurrentTimestamp returns early), but is still
+// processed.  So the first row that fires a head value h after position `pos` is the first row at or after it
+// that advances (or repeats) the clock to a value >= h.
 //
 // Rows interface:  n_own(), own_local(i) (local row index of the i-th own row), fill(local, SgRow&),
-//                  ts(local), find_ge(from_local, value) -> first local row >= from_local with ts >= value
-//                  (or n_rows), n_rows(), plus has_receiver(stream).
+//                  ts(local), clock_at(local) (the clock once the row has set it), find_ge(from_local, value) ->
+//                  first local row >= from_local that notifies the schedulers with the clock at >= value (or
+//                  n_rows), n_rows(), plus has_receiver(stream).
 //
 // emit_from: own rows before this index only rebuild state (a chunked unit's replay window, see
 // interp.hip): their matches are not emitted.
@@ -987,7 +990,7 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t em
     }
     m.silent = i < emit_from ? 1 : 0;
     if (ltim < nrows && ltim <= lev) {
-      m.now = rows.ts(ltim);
+      m.now = rows.clock_at(ltim);
       m.trigger = rows.index_of(ltim);
       m.trig_local = ltim;
       m.phase = 0;
@@ -1013,7 +1016,7 @@ SG_HD void sg_run_key(KeyMachine& m, Rows& rows, int create_at_start, int64_t em
     }
     SgRow row;
     rows.fill(lev, row);
-    m.now = row.ts;
+    m.now = rows.clock_at(lev);
     m.trigger = row.index;
     m.trig_local = lev;
     if (!m.hdr()[K_CREATED]) m.create_runtime();

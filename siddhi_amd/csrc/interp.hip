@@ -41,6 +41,7 @@ struct GeneralState {
   PartialState* pp = nullptr; // partial-lane route (partial.hip) while the query and the stream allow it
   int pp_checked = 0;
   int64_t max_ts = INT64_MIN;  // largest timestamp pushed (INT64_MAX once a timestamp went back)
+  int64_t clock = 0;           // playback clock after the last push (TimestampGeneratorImpl.lastEventTimestamp)
   int64_t grows = 0;           // capacity growths (pushes rerun with larger pools / lists / emission space)
   int cut_count = 0;           // runtimes rebuilt by time-horizon units for a query with a count state (see run_machine)
 };
@@ -116,14 +117,25 @@ struct DevRows {
   __device__ int64_t n_rows() { return n; }
   __device__ int64_t ts_at(int64_t r) { return gptr<int64_t>(ts)[r]; }
   __device__ int64_t ts_(int64_t r) { return gptr<int64_t>(ts)[r]; }
+  // playback clock (queries with absence): clk = running max of the batch's ts, clock0 = the clock before the push,
+  // nfr[n - 1 - r] = first row >= r that notifies the schedulers (ts >= the clock before it), or n
+  const int64_t* clk;
+  const uint32_t* nfr;
+  int64_t clock0;
+  __device__ int64_t clock_at(int64_t r) {
+    if (!clk) return gptr<int64_t>(ts)[r];
+    const int64_t c = gptr<int64_t>(clk)[r];
+    return c > clock0 ? c : clock0;
+  }
   __device__ int64_t find_ge(int64_t from, int64_t v) {
     int64_t lo = from, hi = n;
     while (lo < hi) {
       int64_t mid = (lo + hi) >> 1;
-      if (gptr<int64_t>(ts)[mid] < v) lo = mid + 1;
+      if (clock_at(mid) < v) lo = mid + 1;
       else hi = mid;
     }
-    return lo;
+    if (!clk || lo >= n) return lo;
+    return (int64_t)gptr<uint32_t>(nfr)[n - 1 - lo];
   }
   __device__ void fill(int64_t r, SgRow& row) {
     row.ts = gptr<int64_t>(ts)[r];
@@ -180,6 +192,9 @@ struct NfaArgs {
   const int32_t* stream;
   const uint64_t* index;
   const uint64_t* lbits[SG_MAX_STATES];   // predicate-pass condition bits per state (null: none)
+  const int64_t* clk;                     // playback clock per row and next notifying row (DevRows); null: none
+  const uint32_t* nfr;
+  int64_t clock0;
 };
 
 __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDesc* __restrict__ dd,
@@ -221,6 +236,9 @@ __global__ void __launch_bounds__(64) k_nfa(NfaArgs a, SgCols cols, const DevDes
   rows.d = dd;
   rows.base = a.base_index;
   rows.index = a.index;
+  rows.clk = a.clk;
+  rows.nfr = a.nfr;
+  rows.clock0 = a.clock0;
   sg_run_key(m, rows, !a.partitioned);
   if (m.failed) atomicCAS(fail_code, 0, m.failed);
 }
@@ -312,6 +330,9 @@ __global__ void __launch_bounds__(64) k_nfa_units(NfaArgs a, UnitArgs ua, SgCols
   rows.d = dd;
   rows.base = a.base_index;
   rows.index = a.index;
+  rows.clk = a.clk;
+  rows.nfr = a.nfr;
+  rows.clock0 = a.clock0;
   sg_run_key(m, rows, !a.partitioned, p0 - q);
   if (m.failed) atomicCAS(fail_code, 0, m.failed);
 }
@@ -388,6 +409,18 @@ __global__ void k_gather(int64_t n, const char* __restrict__ buf, int32_t stride
   const uint64_t* src = (const uint64_t*)(buf + (size_t)idx[i] * stride + 8);
   uint64_t* dst = (uint64_t*)(out + (size_t)i * ostride);
   for (int w = 0; w < ostride / 8; ++w) dst[w] = src[w];
+}
+
+// The playback clock over a push (TimestampGeneratorImpl.setCurrentTimestamp, C/util/timestamp/
+// TimestampGeneratorImpl.java:106-125): clk = running max of ts (scanned), then per row whether it notifies the
+// schedulers (ts >= the clock before it) written in reverse, so a min scan gives each row's next notifying row.
+__global__ void k_fire_rev(int64_t n, const int64_t* __restrict__ ts, const int64_t* __restrict__ clk, int64_t clock0,
+                           uint32_t* __restrict__ rev) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t before = i ? clk[i - 1] : clock0;
+  before = before > clock0 ? before : clock0;
+  rev[n - 1 - i] = ts[i] >= before ? (uint32_t)i : (uint32_t)n;
 }
 
 static GeneralState* gstate(SgHandle* h) {
@@ -582,7 +615,6 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   HIPCHK(hipStreamSynchronize(st));
   if (oerr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-  if ((oerr & 1) && has_absent) throw SgError(SG_EORDER, "absence timers need non-decreasing playback timestamps within a push");
   // time-horizon units rebuild a key's state from the rows inside `within` before them: only sound while timestamps
   // never decrease, within this push and after the earlier ones
   const bool ts_monotone = !(oerr & 1) && (n == 0 || tfl[0] >= gs->max_ts);
@@ -596,6 +628,7 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
                              "time-horizon units (open the handle with partial_lanes = -1 for such streams)");
   if (n > 0) gs->max_ts = std::max(gs->max_ts, ts_monotone ? tfl[1] : std::max(tfl[0], tfl[1]));
   if (!ts_monotone) gs->max_ts = INT64_MAX;   // from now on the order of the stream is unknown
+  int64_t next_clock = gs->clock;
   NfaArgs na;
   na.n = n;
   na.base_index = bv.base_index;
@@ -608,6 +641,31 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
   na.ts = bv.ts;
   na.stream = bv.stream;
   na.index = bv.index;
+  na.clk = nullptr;
+  na.nfr = nullptr;
+  na.clock0 = gs->clock;
+  if (has_absent && n > 0) {
+    // absence timers fire on the playback clock, which a row whose time goes back leaves where it is
+    int64_t* clk = (int64_t*)h->ws.get("g_clk", sizeof(int64_t) * n, st);
+    uint32_t* rev = (uint32_t*)h->ws.get("g_fire_rev", sizeof(uint32_t) * n, st);
+    uint32_t* nfr = (uint32_t*)h->ws.get("g_fire_next", sizeof(uint32_t) * n, st);
+    size_t tb = 0;
+    HIPCHK(rocprim::inclusive_scan(nullptr, tb, bv.ts, clk, (size_t)n, rocprim::maximum<int64_t>(), st));
+    void* tmp = h->ws.get("g_clk_tmp", tb, st);
+    HIPCHK(rocprim::inclusive_scan(tmp, tb, bv.ts, clk, (size_t)n, rocprim::maximum<int64_t>(), st));
+    hipLaunchKernelGGL(k_fire_rev, grd, blk, 0, st, n, bv.ts, clk, gs->clock, rev);
+    HIPCHK(hipGetLastError());
+    tb = 0;
+    HIPCHK(rocprim::inclusive_scan(nullptr, tb, rev, nfr, (size_t)n, rocprim::minimum<uint32_t>(), st));
+    tmp = h->ws.get("g_nfr_tmp", tb, st);
+    HIPCHK(rocprim::inclusive_scan(tmp, tb, rev, nfr, (size_t)n, rocprim::minimum<uint32_t>(), st));
+    int64_t last = 0;
+    HIPCHK(hipMemcpyAsync(&last, clk + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    na.clk = clk;
+    na.nfr = nfr;
+    next_clock = std::max(gs->clock, last);
+  }
   // ---- predicate-evaluation pass: condition bits of every state whose filter reads only the arriving event
   for (int s = 0; s < SG_MAX_STATES; ++s) na.lbits[s] = nullptr;
   {
@@ -763,6 +821,7 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
     h->out.n += (int64_t)total;
   }
   h->mark(4);
+  gs->clock = next_clock;
   h->last_events = n;
   h->last_spilled = 0;
   h->last_matches = (int64_t)total;
@@ -774,6 +833,7 @@ void sg_general_reset(SgHandle* h) {
   if (gs->arena) hipMemset(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4);
   sg_partial_reset(gs->pp);
   gs->max_ts = INT64_MIN;
+  gs->clock = 0;
   gs->cut_count = 0;
   h->key_bound_seen = 0;
 }

@@ -85,11 +85,12 @@ __device__ __forceinline__ int64_t row_key(const OnceArgs& a, int64_t r) {
 
 // pass 1: the first row of each still-waiting key that passes A's filter
 __global__ void __launch_bounds__(256) k_once_first(OnceArgs a, const uint8_t* __restrict__ phase,
-                                                    uint32_t* __restrict__ first) {
+                                                    uint32_t* __restrict__ first, uint32_t* __restrict__ err) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * blockDim.x) {
-    if (!mask_bit(a.cand_m, (uint64_t)r)) continue;
     const int64_t k = row_key(a, r);
-    if (k < 0 || k >= (int64_t)a.K || phase[k] != 0) continue;
+    if (k >= (int64_t)a.K) { atomicOr(err, 1u); continue; }   // beyond the caller's key_bound (every row checked)
+    if (!mask_bit(a.cand_m, (uint64_t)r)) continue;
+    if (k < 0 || phase[k] != 0) continue;
     if ((uint32_t)r < __hip_atomic_load(&first[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
       atomicMin(&first[k], (uint32_t)r);
   }
@@ -349,7 +350,13 @@ void sg_run_once(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(hipMemsetAsync(cnt, 0, 8, st));
   const dim3 blk(256), gk((unsigned)((kb + 255) / 256));
   h->kbeg("once_match");
-  if (n > 0) hipLaunchKernelGGL(k_once_first, dim3(grid_rows(n)), blk, 0, st, a, s.phase, first);
+  if (n > 0) {
+    hipLaunchKernelGGL(k_once_first, dim3(grid_rows(n)), blk, 0, st, a, s.phase, first, cnt + 1);
+    uint32_t kerr = 0;
+    HIPCHK(hipMemcpyAsync(&kerr, cnt + 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (kerr) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+  }
   hipLaunchKernelGGL(k_once_bind, gk, blk, 0, st, a, bv.cols, sp, s, first, lo);
   if (n > 0) hipLaunchKernelGGL(k_once_second, dim3(grid_rows(n)), blk, 0, st, a, bv.cols, s, lo, hit, expd);
   hipLaunchKernelGGL(k_once_finish, gk, blk, 0, st, a, s, lo, hit, expd, cnt, prow, pkey);

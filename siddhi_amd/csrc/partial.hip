@@ -108,14 +108,8 @@ static void rows_reserve(PartialState* ps, PpRows& r, int64_t need) {
   r = nr;
 }
 
-// FAST lane kernels unless SG_LANES_NO_FAST=1 (A/B runs)
-static bool lanes_fast(const PartialState* ps) {
-  static const bool off = [] {
-    const char* e = getenv("SG_LANES_NO_FAST");
-    return e && e[0] == '1';
-  }();
-  return ps->lanes_fast && !off;
-}
+// FAST lane kernels whenever the query's terms allow them (sg_terms_fast)
+static bool lanes_fast(const PartialState* ps) { return ps->lanes_fast; }
 
 PartialState* sg_partial_new(const sg_nfa_desc& d) {
   SgPpRule ru = sg_pp_rule(d);
@@ -1301,7 +1295,6 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   SqPlan pl_;
   const int64_t H = ps->srule.horizon;
   pl_.R = std::max<int64_t>(64, (n + 262143) / 262144);
-  if (const char* e = getenv("SG_SQ_ROWS")) pl_.R = std::max<int64_t>(16, atoll(e));   // (experiments)
   if (h->opt.chunk_rows > 0) pl_.R = h->opt.chunk_rows;
   pl_.W = std::max<int64_t>(4 * H, 16);
   uint32_t* ncar = (uint32_t*)h->ws.get("sq_ncar", 4 * ((size_t)kb + 1), st);
@@ -1337,7 +1330,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   // unchanged start states (kst) with four times the space -- the reference's lists are unbounded
   cap = n + (int64_t)SQ_CHUNK * ((int64_t)U + (int64_t)kb) + 65536;
   if (ps->sq_cap_hint > cap) cap = ps->sq_cap_hint;
-  if (const char* e = getenv("SG_SQ_MATCH_CAP")) {   // (tests start from a tiny match space to exercise the regrowth)
+  if (const char* e = getenv("SG_DEBUG_SQ_MATCH_CAP")) {   // (debug: a tiny match space exercises the regrowth)
     const int64_t v = atoll(e);
     if (v > 0) cap = std::max<int64_t>(v, SQ_CHUNK);
   }
@@ -1477,7 +1470,7 @@ static void carry_rows(SgHandle* h, PartialState* ps, const BatchView& bv, const
 // larger pushes are cut into sub-pushes by the caller (a stream without carry runs on the machine instead).
 int64_t sg_partial_max_rows(SgHandle* h, PartialState* ps) {
   if (ps->mode != 1 || h->opt.no_carry) return INT64_MAX;
-  const char* e = getenv("SG_PP_ROW_BUDGET");   // (tests lower the budget through the environment)
+  const char* e = getenv("SG_DEBUG_PP_ROW_BUDGET");   // (debug: a lower budget exercises sub-pushes)
   const int64_t v = e ? atoll(e) : 0;
   const int64_t lim = v > 0 && v < ((int64_t)1 << 27) ? v : ((int64_t)1 << 27);
   return lim - 1 - ps->rows[ps->cur].n;
@@ -1703,7 +1696,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   HIPCHK(hipMemsetAsync(o.count, 0, 16, st));
   // wait-term block summaries (chain.h PpWait): only without nulls (a null row passes `!=`), 4-byte attributes
   P.wsum = nullptr;
-  if (ps->rule.wait_slots && !P.nul && m > 0 && !getenv("SG_PP_NO_SKIP")) {
+  if (ps->rule.wait_slots && !P.nul && m > 0) {
     uint32_t slots = 0, fslots = 0;
     int nw = 0;
     for (int k = 0; k < SG_MAX_RET; ++k) P.wix[k] = -1;
@@ -1729,11 +1722,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   }
   h->kbeg("partial_lanes");
   if (ncand) {
-    static const int64_t wcands = [] {   // (experiments: SG_PP_WAVE_CANDS)
-      const char* e = getenv("SG_PP_WAVE_CANDS");
-      const int64_t x = e ? atoll(e) : 0;
-      return x >= 64 ? x : PP_WAVE_CANDS;
-    }();
+    const int64_t wcands = PP_WAVE_CANDS;
     const dim3 gl((unsigned)((ncand + wcands * (PP_BLOCK / 64) - 1) / (wcands * (PP_BLOCK / 64))));
     if (ps->pp_small && lanes_fast(ps))
       hipLaunchKernelGGL((k_pp_lanes<PpSmall, true>), gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand,
@@ -1816,6 +1805,8 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     uint32_t* dest = (uint32_t*)h->ws.get("pp_dest", 4 * (size_t)(T + 1), st);
     HIPCHK(hipMemsetAsync(dest, 0xFF, 4 * (size_t)T, st));
     hipLaunchKernelGGL(k_em_dest, dim3((unsigned)((M + 255) / 256)), blk, 0, st, M, ia, dest);
+    if ((size_t)256 * rstride > 65536)   // (up to SG_MAX_SELECT selected attributes: 256 * 288 B of LDS)
+      HIPCHK(hipFuncSetAttribute((const void*)k_em_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(256 * rstride)));
     hipLaunchKernelGGL(k_em_scatter, g2, blk, (size_t)256 * rstride, st, T, dest, o.rec, o.rstride,
                        out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());

@@ -30,6 +30,7 @@ struct HiHandle {
   std::vector<SeqStateT<SqSmall>> seq_state_s;   // (... or small, sg_seq_small)
   int64_t spec_rows = 0, spec_warm = 0, spec_reruns = 0;   // speculative units (0: one run per key)
   int64_t pp_steps = 0, pp_lanes = 0, pp_skipped = 0;      // partial lanes: rows stepped, lanes started, rows skipped
+  int64_t clock = 0;   // playback clock after the last push (TimestampGeneratorImpl.lastEventTimestamp)
 };
 
 struct HostRows {
@@ -46,10 +47,13 @@ struct HostRows {
   int stream_at(int64_t r) { return b->stream ? b->stream[r] : 0; }
   int64_t n_rows() { return b->n; }
   int64_t ts(int64_t r) { return b->ts[r]; }
+  // playback clock: clk[r] = the clock once row r has set it, nf[r] = first row >= r that notifies the schedulers
+  const std::vector<int64_t>* clk;
+  const std::vector<int64_t>* nf;
+  int64_t clock_at(int64_t r) { return (*clk)[r]; }
   int64_t find_ge(int64_t from, int64_t v) {
-    const int64_t* lo = b->ts + from;
-    const int64_t* hi = b->ts + b->n;
-    return std::lower_bound(lo, hi, v) - b->ts;
+    const int64_t lo = std::lower_bound(clk->begin() + from, clk->end(), v) - clk->begin();
+    return lo >= b->n ? b->n : (*nf)[lo];
   }
   void fill(int64_t r, SgRow& row) {
     row.ts = b->ts[r];
@@ -548,6 +552,21 @@ static int machine_push(HiHandle* h, const sg_batch* b, bool silent) {
   std::vector<char> buf(cap * stride);
   int kb = 1;
   while ((1ull << kb) <= (uint64_t)h->arenas.size()) ++kb;
+  // the playback clock over this push (TimestampGeneratorImpl.setCurrentTimestamp: a row whose time goes back does not
+  // move it and notifies nobody)
+  std::vector<int64_t> clk((size_t)n), nf((size_t)n + 1);
+  {
+    int64_t c = h->clock;
+    std::vector<char> fires((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+      fires[i] = b->ts[i] >= c;
+      c = std::max(c, b->ts[i]);
+      clk[i] = c;
+    }
+    nf[n] = n;
+    for (int64_t i = n - 1; i >= 0; --i) nf[i] = fires[i] ? i : nf[i + 1];
+    h->clock = c;
+  }
   for (size_t k = 0; k < h->arenas.size(); ++k) {
     if (h->arenas[k].empty()) {
       if (own[k].empty() && d.partitioned) continue;
@@ -563,7 +582,7 @@ static int machine_push(HiHandle* h, const sg_batch* b, bool silent) {
       m.clone = d.partitioned;
       m.sink = SgEmitSink{buf.data(), (int64_t)cap, &count, &overflow, stride, kb};
       m.base_index = b->base_index;
-      HostRows rows{b, &d, rws};
+      HostRows rows{b, &d, rws, &clk, &nf};
       sg_run_key(m, rows, !d.partitioned, emit_from);
       return m.failed;
     };

@@ -78,7 +78,7 @@ def test_machine_without_growth_still_reports_capacity():
 @pytest.mark.parametrize("cap", [16, 3000])
 def test_sequence_lanes_regrow_match_space(monkeypatch, cap):
     """Sequence lanes (C3b's route, csrc/partial.hip seq_lanes_push) start from a match space of `cap` slots
-    (SG_SQ_MATCH_CAP, a test hook): the first push and every later one outgrow it, and each is rerun from its unchanged
+    (SG_DEBUG_SQ_MATCH_CAP, a test hook): the first push and every later one outgrow it, and each is rerun from its unchanged
     start states with four times the space -- no push fails (the second push used to throw
     SG_ECAPACITY "match buffer").  Three pushes with carried state, oracle-equal."""
     from siddhi_amd._native import GpuEngine
@@ -90,5 +90,5 @@ def test_sequence_lanes_regrow_match_space(monkeypatch, cap):
     cuts = [0, 30_000, 60_000, 90_000]
     parts = [Batch(h - l, l, b.ts[l:h], b.stream[l:h], b.key[l:h], [c[l:h] for c in b.cols], [None] * 4)
              for l, h in zip(cuts[:-1], cuts[1:])]
-    monkeypatch.setenv("SG_SQ_MATCH_CAP", str(cap))
+    monkeypatch.setenv("SG_DEBUG_SQ_MATCH_CAP", str(cap))
     assert_same(run_engine(GpuEngine, q, parts), want)

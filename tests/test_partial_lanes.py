@@ -416,7 +416,7 @@ def test_gpu_pushes_beyond_the_row_budget_are_split(monkeypatch):
     """Tie components hold a combined row in 27 bits: a push whose rows (carried rows included) pass that budget runs
     as consecutive sub-pushes on the route instead of failing (budget lowered to 30k rows here), first push included."""
     from siddhi_amd._native import GpuEngine
-    monkeypatch.setenv("SG_PP_ROW_BUDGET", "30000")   # (rate 10/ms: about 10k rows inside `within 1 sec` are carried)
+    monkeypatch.setenv("SG_DEBUG_PP_ROW_BUDGET", "30000")   # (rate 10/ms: about 10k rows inside `within 1 sec` are carried)
     q = synth.QUERIES["C3c"]
     g = synth.generate("C3c", 0, 200_000, keys=500, rate=10)
     b = Batch(200_000, 0, g["ts"], np.zeros(200_000, np.int32), dense_first_seen(g["key"]),

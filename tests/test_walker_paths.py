@@ -126,21 +126,18 @@ PRICE_TIES = {"price": lambda r, n: 20 + r.integers(0, 12, n)}          # few di
 @pytest.mark.parametrize("op", [">", ">=", "<", "<="])
 @pytest.mark.parametrize("part,walker_only", [(True, False), (True, True), (False, False), (False, True)])
 def test_compare_operators(op, part, walker_only):
-    """Both partitioned (keyed next match) and unpartitioned streams run a per-candidate search by default;
-    walker_only keeps the walker covered."""
+    """Partitioned streams run the walker; unpartitioned ones the per-candidate search by default, and
+    walker_only keeps the walker covered for them."""
     app = (q_part if part else q_flat)(f"price {op} e1.price")
     b = make_batch(app, 60_000, seed=1, keys=200 if part else 1, rate=20, values=PRICE_TIES)
     check(app, [b], walker_only=walker_only)
 
 
 @pytest.mark.parametrize("op", [">", ">=", "<", "<="])
-def test_keyed_next_match_operators(op, monkeypatch):
-    """the opt-in keyed next-match pipeline (SG_KEYED_NEXT=1, engine_impl.h run_keyed_next): same rows as the oracle,
-    with ties, several pushes with carried rows"""
-    monkeypatch.setenv("SG_KEYED_NEXT", "1")
+def test_operators_multi_push_ties(op):
+    """the walker with ties across several pushes with carried rows, every operator"""
     app = q_part(f"price {op} e1.price")
     b = make_batch(app, 60_000, seed=3, keys=200, rate=20, values=PRICE_TIES)
-    check(app, [b])
     check(app, split(b, [1, 15_000, 15_001, 41_000]))
 
 
