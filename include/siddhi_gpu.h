@@ -62,7 +62,7 @@ extern "C" {
 #define SG_EHIP -2
 #define SG_ECAPACITY -3     /* a per-key pool / list capacity (sg_options) was exceeded */
 #define SG_EUNSUPPORTED -4
-#define SG_EORDER -5        /* a closed-form kernel's precondition (non-decreasing ts) failed */
+#define SG_EORDER -5        /* sg_merge_runs: a run is not ordered by trigger */
 
 /* state kinds (Pre/Post processor pairs) */
 #define SG_K_STREAM 0       /* StreamPre/PostStateProcessor */

@@ -269,19 +269,12 @@ SG_HD inline SgPpRule sg_pp_rule(const sg_nfa_desc& d) {
   return r;
 }
 
-// Carry window of the partial-lane route: per key, the rows with ts >= last ts - window survive into the next push
-// and rebuild every partial that can still match (`within` of the key's last row).  A query with a count state
-// carries one more `within` of rows (pp_regress_tol): count states never expire partials (CountPreStateProcessor.
-// processAndReturn, C/query/input/stream/state/CountPreStateProcessor.java:53-93), so a push whose time goes BACK can
-// revive a partial parked in a count state after it left `within`.  When a key's time goes back by at most the
-// tolerance below its last carried row, the per-key machine rebuilt from these rows takes over exactly: every partial
-// it lacks started before last - within - tol and stays expired for every row at or after last - tol
-// (StreamPreStateProcessor.isExpired compares |ts - e1.ts| with `within`).  A deeper regression is SG_EORDER.
-SG_HD inline int64_t pp_regress_tol(const sg_nfa_desc& d, bool has_count) { return has_count ? d.within : 0; }
-SG_HD inline int64_t pp_carry_window(const sg_nfa_desc& d, bool has_count) {
-  const int64_t tol = pp_regress_tol(d, has_count);
-  return d.within > INT64_MAX / 4 || tol > INT64_MAX / 4 ? d.within : d.within + tol;
-}
+// Carry of the partial-lane route: a lane still pending after its key's last row marks the rows it holds
+// (PpLane::witnesses) and they survive into the next push, its e1 flagged as a start; nothing else is carried.  Count
+// states never expire partials (CountPreStateProcessor.processAndReturn, C/query/input/stream/state/
+// CountPreStateProcessor.java:53-93), so a partial waiting in one stays carried however old its e1 -- a later row whose
+// time goes back can still complete it; every other state drops the partial at the first row more than `within` from
+// e1 on either side (StreamPreStateProcessor.isExpired, :102-113).
 
 // Tie key of an emission: the insertion history newest first, 31 bits per component (row << 4 | visit slot), two
 // components per word (bit 63 is always set).  Rows only need to be in arrival order within one key.
@@ -345,6 +338,7 @@ struct PpLane {
   int64_t e1_ts;
   int32_t nh;
   int32_t overflow;
+  bool wait_count;   // (set by wait_on) the partial waits in a count state: a skipped row cannot expire it
   // current row
   int32_t cur_row;
   int cur_rank;
@@ -563,13 +557,44 @@ struct PpLane {
   }
   SG_HD bool get_any(int s) { return st(s).kind == SG_K_COUNT ? A->clen[s] > 0 : A->slot[s] >= 0; }
   SG_HD bool dead() const { return (l0 | l1) == 0; }
+  // A count state still short of its minimum holds the partial: counts never expire by `within`
+  // (CountPreStateProcessor.processAndReturn, C/query/input/stream/state/CountPreStateProcessor.java:53-93), so a later
+  // row -- with time going back, one inside `within` of e1 -- can still complete it.  Every other live state is dropped
+  // by the first row of the stream more than `within` from e1 (isExpired compares |e1.ts - ts|, :102-113), and a count
+  // state past its minimum can no longer forward the partial.
+  SG_HD bool waiting_count() const {
+    const uint32_t live = l0 | l1;
+    for (int s = 0; s < G::S && s < d->n_states; ++s)
+      if (((live >> s) & 1u) && st(s).kind == SG_K_COUNT && A->clen[s] < st(s).min_count) return true;
+    return false;
+  }
+  SG_HD bool live_other() const {   // a live state that is not a count state
+    const uint32_t live = l0 | l1;
+    for (int s = 0; s < G::S && s < d->n_states; ++s)
+      if (((live >> s) & 1u) && st(s).kind != SG_K_COUNT) return true;
+    return false;
+  }
+  // rows the partial holds (e1, every bound slot, every chain event): replaying a superset of them in arrival order,
+  // within the rows that followed e1, rebuilds it exactly -- a row that changed it is among them, and any other row
+  // changed nothing the first time (the same state meets the same row again)
+  template <class F>
+  SG_HD void witnesses(F mark) const {
+    for (int s = 0; s < G::S && s < d->n_states; ++s) {
+      if (st(s).kind == SG_K_COUNT) {
+        const int32_t* c = A->chain + ru->coff[s];
+        for (int i = 0; i < A->clen[s]; ++i) mark(c[i], false);
+      } else if (A->slot[s] >= 0) {
+        mark(A->slot[s], s == ru->start);
+      }
+    }
+  }
 
   // Wait skipping.  While the partial's only live state s is a stream, count or logical state with a wait term
   // (PpWait), an arriving row that fails the term changes nothing: step() binds the row (slot or chain append), the
   // filter fails, and the binding is undone -- no post, no add_state, no emission; the flags it clears are rewritten
-  // before they are next read.  The one other effect, expiry, the caller checks on the row it lands on (a key's
-  // timestamps never decrease on this route, so a skipped row that had expired the partial means the landing row has
-  // too).  Not while the count state's successors hold the partial (step() would drop it from s) or a full chain, nor
+  // before they are next read.  The one other effect, expiry, the caller checks on the row it lands on when the key's
+  // timestamps never decrease (a skipped row that had expired the partial means the landing row has too); in a count
+  // state (wait_count) there is no expiry, and a key whose time goes back skips only there.  Not while the count state's successors hold the partial (step() would drop it from s) or a full chain, nor
   // for an `or` state whose partner has matched, nor while the fixed operand is null.  Returns whether the partial
   // waits, with the term `row.slot OP c`.
   SG_HD bool wait_on(int& slot, int& op, int& fast, int64_t& cbits) {
@@ -589,6 +614,7 @@ struct PpLane {
     int null = 0;
     operand_bits(w.other ? t.l : t.r, cbits, null);
     if (null) return false;
+    wait_count = x.kind == SG_K_COUNT;
     slot = w.slot;
     op = w.op;
     fast = w.fast;

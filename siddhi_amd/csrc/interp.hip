@@ -43,7 +43,6 @@ struct GeneralState {
   int64_t max_ts = INT64_MIN;  // largest timestamp pushed (INT64_MAX once a timestamp went back)
   int64_t clock = 0;           // playback clock after the last push (TimestampGeneratorImpl.lastEventTimestamp)
   int64_t grows = 0;           // capacity growths (pushes rerun with larger pools / lists / emission space)
-  int cut_count = 0;           // runtimes rebuilt by time-horizon units for a query with a count state (see run_machine)
 };
 
 static bool has_count_state(const sg_nfa_desc& d) {
@@ -497,15 +496,10 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
       lo += cnt;
     }
     if (lo == n) return;
-    // the stream left the route's precondition (a timestamp went back): rebuild the general machine's per-key runtimes
-    // by replaying the carried rows without emitting (they were delivered already), then continue on the machine
-    BatchView cv = sg_partial_carried_view(h, gs->pp, (int32_t)kb);
+    // the route declined a push before anything was carried (sg_partial_push, seq_lanes_push): the per-key machine
+    // takes the stream from here, exactly
+    if (sg_partial_carried(gs->pp)) throw SgError(SG_EUNSUPPORTED, "partial-lane route left with carried partials");
     sg_partial_deactivate(gs->pp);
-    if (cv.n) {
-      const int64_t delivered = h->out.n;
-      run_machine(h, cv, cv.n);
-      h->out.n = delivered;
-    }
     run_machine(h, slice_view(h->desc, bv, lo, n - lo), n - lo);
     return;
   }
@@ -618,14 +612,6 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
   // time-horizon units rebuild a key's state from the rows inside `within` before them: only sound while timestamps
   // never decrease, within this push and after the earlier ones
   const bool ts_monotone = !(oerr & 1) && (n == 0 || tfl[0] >= gs->max_ts);
-  // A unit's runtime is rebuilt from the rows inside `within` before its chunk, so a key's runtime after a cut push lacks
-  // the partials parked in a count state since before that horizon -- harmless while time never goes back (they can
-  // never complete again), but time going back would revive them (CountPreStateProcessor never expires a partial,
-  // C/query/input/stream/state/CountPreStateProcessor.java:53-93).  Handles opened with partial_lanes = -1 (streams
-  // that may go back) never cut such queries; on the others a push that goes back after a cut one is SG_EORDER.
-  if (!ts_monotone && n > 0 && gs->cut_count)
-    throw SgError(SG_EORDER, "per-key machine: time went back after a push whose count-state runtimes were rebuilt by "
-                             "time-horizon units (open the handle with partial_lanes = -1 for such streams)");
   if (n > 0) gs->max_ts = std::max(gs->max_ts, ts_monotone ? tfl[1] : std::max(tfl[0], tfl[1]));
   if (!ts_monotone) gs->max_ts = INT64_MAX;   // from now on the order of the stream is unknown
   int64_t next_clock = gs->clock;
@@ -713,9 +699,12 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
   sink.key_bits = kbits;
   // ---- unit plan: one unit per key, or (chunkable shapes) per (key, chunk of R rows)
   uint32_t R = 0;
+  // A time-horizon unit's runtime is rebuilt from the rows inside `within` before its chunk, so it lacks the partials
+  // parked in a count state since before that horizon: they never expire (CountPreStateProcessor.processAndReturn,
+  // C/query/input/stream/state/CountPreStateProcessor.java:53-93) and a later push whose time goes back can complete
+  // them -- queries with a count state are cut only by the sequence's event horizon
   const bool count_q = has_count_state(d);
-  if (rule.kind != 0 && (rule.kind == 2 || ts_monotone) && h->opt.chunk_rows >= 0 && n > 0 &&
-      !(count_q && h->opt.partial_lanes < 0)) {
+  if (rule.kind != 0 && (rule.kind == 2 || (ts_monotone && !count_q)) && h->opt.chunk_rows >= 0 && n > 0) {
     if (h->opt.chunk_rows > 0) {
       R = (uint32_t)h->opt.chunk_rows;
     } else {
@@ -735,7 +724,6 @@ static void run_machine(SgHandle* h, const BatchView& bv, int64_t n) {
     }
   }
   if (R > 0) {
-    if (count_q) gs->cut_count = 1;
     uint32_t* nch = (uint32_t*)h->ws.get("g_nch", sizeof(uint32_t) * (kb + 1), st);
     uint32_t* uoff = (uint32_t*)h->ws.get("g_uoff", sizeof(uint32_t) * (kb + 1), st);
     hipLaunchKernelGGL(k_unit_count, dim3((unsigned)((kb + 1 + 255) / 256)), blk, 0, st, (int64_t)kb, beg, end, R, nch);
@@ -834,7 +822,6 @@ void sg_general_reset(SgHandle* h) {
   sg_partial_reset(gs->pp);
   gs->max_ts = INT64_MIN;
   gs->clock = 0;
-  gs->cut_count = 0;
   h->key_bound_seen = 0;
 }
 
@@ -885,8 +872,7 @@ void sg_general_restore(SgHandle* h, SnapR& r) {
     if (!gs->pp || h->opt.partial_lanes < 0) throw SgError(SG_EINVAL, "snapshot: taken on the partial-lane route");
     sg_partial_restore(h, gs->pp, r);
     gs->max_ts = max_ts;
-    gs->cut_count = 0;
-    // the machine's per-key runtimes from before the restore (a fallback taken earlier) are stale: a later fallback
+      // the machine's per-key runtimes from before the restore (a fallback taken earlier) are stale: a later fallback
     // rebuilds them from the restored carried rows alone
     if (gs->arena) HIPCHK(hipMemsetAsync(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -894,8 +880,6 @@ void sg_general_restore(SgHandle* h, SnapR& r) {
   }
   if (gs->pp) sg_partial_deactivate(gs->pp);
   gs->max_ts = max_ts;
-  // (whether the snapshot's runtimes came from cut pushes is not recorded: assume they did, as run_machine may have)
-  gs->cut_count = has_count_state(h->desc) && h->opt.partial_lanes >= 0 && max_ts != INT64_MIN ? 1 : 0;
   const int64_t keys = r.pod<int64_t>();
   if (keys < 0 || keys > (1ll << 31)) throw SgError(SG_EINVAL, "snapshot: bad key count");
   if (gs->arena) HIPCHK(hipMemsetAsync(gs->arena, 0, (size_t)gs->keys_alloc * gs->geo.key_words * 4, st));

@@ -1,27 +1,26 @@
 // Partial lanes (chain.h): the general machine's route for patterns whose partial matches never interact
 // (sg_pp_rule: `every e1=S[local] -> ... within T` over stream / count / logical states of one stream).
 //
-// Per sg_push, with the rows carried from earlier pushes listed first ("carried rows": per key, the rows inside
-// `within` of the key's last row -- they rebuild every partial that can still match, StreamPreStateProcessor.isExpired,
-// C/query/input/stream/state/StreamPreStateProcessor.java:102-113):
+// Per sg_push, with the rows carried from earlier pushes listed first ("carried rows": the rows every partial still
+// pending holds -- its e1, its bound slots, its count chains -- with the e1 rows marked as starts; replaying them
+// rebuilds exactly those partials, whatever the order of time, chain.h PpLane::witnesses):
 //   1. k_pp_route      combined rows (carried, then the batch) -> partition key (PartitionStreamReceiver routing)
 //   2. key partition   stable radix sort of (key, combined row): each key's rows contiguous, in arrival order;
 //                      k_pp_segments: per-key bounds and the route's precondition -- a key's timestamps never decrease
 //                      (also across pushes), as for the closed forms
 //   3. predicate pass  condition bits of every event-local filter over the batch (pred.h)
-//   4. k_pp_lanes      one lane per row that starts a partial (passes the start state's filter): chain.h's PpLane runs
-//                      that partial alone over the key's following rows until it dies or leaves `within`; a match is
-//                      written with its sort key (trigger row, visit slot) and its insertion history (tie key)
+//   4. k_pp_lanes      one lane per row that starts a partial (a batch row passing the start state's filter, or a
+//                      carried start): chain.h's PpLane runs that partial alone over the key's following rows until it
+//                      dies (|ts - e1.ts| > within drops it everywhere but in a count state short of its minimum); a
+//                      match is written with its sort key (trigger row, visit slot) and its insertion history (tie key);
+//                      a partial still pending at the key's last row marks the rows it holds for the carry
 //   5. match order     stable radix sorts: tie words, then (trigger, visit slot) -> the reference's delivery order;
 //                      k_pp_gather writes the match records
-//   6. carry           per key, the rows with ts >= last ts - window become the next push's carried rows (window =
-//                      within, plus one more `within` for queries with a count state: chain.h pp_carry_window)
-// A push that breaks the ordering precondition leaves this route: the carried rows are handed back so the caller can
-// replay them through the general machine (interp.hip) and continue there.  With a count state that replay is exact only
-// for a regression of at most `within` below the key's last carried row: CountPreStateProcessor never expires a partial
-// (CountPreStateProcessor.java:53-93), so time going back further could revive a partial parked in a count state that
-// the carried rows do not hold -- such a push fails with SG_EORDER, like the closed forms (open the handle with
-// partial_lanes = -1 for streams whose timestamps may go back that far).
+//   6. carry           the marked rows, in arrival order, with their start flags
+// Time going back needs no special case: expiry compares |e1.ts - ts| with `within` in every step, a partial parked in
+// a count state (CountPreStateProcessor never expires one, CountPreStateProcessor.java:53-93) keeps walking the key's
+// rows and is carried however old it is, and a key whose time goes back skips rows only while it waits in a count
+// state.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -49,6 +48,7 @@ struct PpRows {
   int64_t n = 0, cap = 0;
   int64_t* ts = nullptr;
   int32_t* key = nullptr;
+  uint8_t* start = nullptr;     // partial lanes: the row is the e1 of a pending partial (its lane restarts there)
   void* col[SG_MAX_COLS] = {};
   uint8_t* nul[SG_MAX_COLS] = {};
 };
@@ -85,6 +85,7 @@ struct PartialState {
 static void rows_free(PpRows& r) {
   if (r.ts) hipFree(r.ts);
   if (r.key) hipFree(r.key);
+  if (r.start) hipFree(r.start);
   for (int c = 0; c < SG_MAX_COLS; ++c) {
     if (r.col[c]) hipFree(r.col[c]);
     if (r.nul[c]) hipFree(r.nul[c]);
@@ -97,7 +98,8 @@ static void rows_reserve(PartialState* ps, PpRows& r, int64_t need) {
   const int64_t cap = std::max<int64_t>(need + need / 4, 1024);
   PpRows nr;
   nr.cap = cap;
-  if (hipMalloc(&nr.ts, 8 * cap) != hipSuccess || hipMalloc(&nr.key, 4 * cap) != hipSuccess)
+  if (hipMalloc(&nr.ts, 8 * cap) != hipSuccess || hipMalloc(&nr.key, 4 * cap) != hipSuccess ||
+      hipMalloc(&nr.start, cap) != hipSuccess)
     throw SgError(SG_EHIP, "hipMalloc carried rows");
   for (int c = 0; c < SG_MAX_COLS; ++c) {
     if (!ps->used_col[c]) continue;
@@ -207,6 +209,10 @@ struct PpArgs {
   const int32_t* ckey;
   const uint64_t* lbits[SG_MAX_STATES];
   int32_t any_bits;
+  const uint8_t* cstart;      // partial lanes: carried row starts a lane
+  uint32_t* keep;             // partial lanes: per sorted position, 1 = carried into the next push
+  uint8_t* kstart;            // partial lanes: per sorted position, 1 = the carried row starts a lane
+  const uint8_t* kback;       // partial lanes: per key, its time goes back somewhere in this push (carried rows included)
 };
 
 // Key-ordered packed rows (position q = the q-th row of the key partition): what a lane reads at every step, so the
@@ -352,7 +358,7 @@ __global__ void __launch_bounds__(256) k_pp_rec(PpArgs a, SgCols bc, SgCols cc, 
         if (ok) lb |= 1u << s;
       }
       if (ra.mode == 1) {
-        rec.w[0] |= ((lb >> ra.start) & 1u) << 31;
+        rec.w[0] |= ((lb >> ra.start) & (carried ? (uint32_t)a.cstart[r] : 1u) & 1u) << 31;
         const int64_t dt = (carried ? a.cts[r] : a.bts[r]) - ra.tbase;
         if (dt != (int64_t)(int32_t)dt) atomicOr(err, 4);
         rec.w[1] = (uint32_t)(int32_t)dt;
@@ -421,11 +427,10 @@ __global__ void __launch_bounds__(256) k_pp_unpack(PpArgs a, SgCols bc, SgCols c
   }
 }
 
-// err bit 1: a key's timestamps go back somewhere; bit 8: by more than `tol` below the key's last carried row (the
-// regression the per-key machine cannot take over exactly, pp_regress_tol).  check_order 0: no check.
+// per-key bounds; check_order: kback[k] = 1 when the key's timestamps go back somewhere (carried rows included)
 __global__ void k_pp_segments(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
-                              const int64_t* __restrict__ qts, int check_order, int64_t tol, uint32_t sentinel,
-                              uint32_t* __restrict__ beg, uint32_t* __restrict__ end, int32_t* __restrict__ err) {
+                              const int64_t* __restrict__ qts, int check_order, uint32_t sentinel,
+                              uint32_t* __restrict__ beg, uint32_t* __restrict__ end, uint8_t* __restrict__ kback) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= m) return;
   const uint32_t k = skey[p];
@@ -436,28 +441,7 @@ __global__ void k_pp_segments(int64_t m, PpArgs a, const uint32_t* __restrict__ 
     return c < a.nc ? a.cts[c] : a.bts[c - a.nc];
   };
   if (p == 0 || skey[p - 1] != k) beg[k] = (uint32_t)p;
-  else if (check_order) {
-    const int64_t t1 = ts_at(p);
-    if (ts_at(p - 1) > t1) {   // (rare: searched, not precomputed)
-      int32_t f = 1;
-      if (check_order == 2) {
-        int64_t lo = 0, hi = p;   // the key's first position
-        while (lo < hi) {
-          const int64_t mid = (lo + hi) >> 1;
-          if (skey[mid] < k) lo = mid + 1; else hi = mid;
-        }
-        if ((int64_t)sid[lo] < a.nc) {   // carried rows (they come first): the key's last one
-          int64_t l2 = lo, h2 = p;
-          while (l2 < h2) {
-            const int64_t mid = (l2 + h2) >> 1;
-            if ((int64_t)sid[mid] < a.nc) l2 = mid + 1; else h2 = mid;
-          }
-          if (t1 < ts_at(l2 - 1) - tol) f |= 8;
-        }
-      }
-      atomicOr(err, f);
-    }
-  }
+  else if (check_order && ts_at(p - 1) > ts_at(p)) kback[k] = 1;
   if (p == m - 1 || skey[p + 1] != k) end[k] = (uint32_t)p + 1;
 }
 
@@ -527,7 +511,7 @@ __global__ void __launch_bounds__(256) k_pp_pack(PpArgs a, SgCols bc, SgCols cc,
       if (ok) lb |= 1u << s;
     }
     P.lb[q] = lb;
-    flag[q] = (lb >> start) & 1u;
+    flag[q] = (lb >> start) & (carried && a.cstart ? (uint32_t)a.cstart[r] : 1u) & 1u;
   }
 }
 
@@ -626,10 +610,11 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
     bool done = false;
     if (active) {
       // wait skipping: the 8-row blocks in which no row can pass the partial's wait term change nothing
-      // (PpLane::wait_on); at most 16 blocks per step, the row landed on is checked for expiry below
+      // (PpLane::wait_on); at most 16 blocks per step, the row landed on is checked for expiry below (a key whose time
+      // goes back skips only while the partial waits in a count state, which nothing expires)
       int ws, wop, wf;
       int64_t wc;
-      if (pl.wsum && q < e && L.wait_on(ws, wop, wf, wc)) {
+      if (pl.wsum && q < e && L.wait_on(ws, wop, wf, wc) && (L.wait_count || !(a.kback && a.kback[k]))) {
         // blocks whose summary rules the term out are skipped whole; in a block that may pass, the lane reads its 8
         // values at once and lands on the first row that passes (or moves on to the next block)
         const uint2* S = pl.wsum + (int64_t)pl.wix[ws] * pl.wnb;
@@ -664,7 +649,18 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
         }
         q = qq < e ? qq : e;
       }
-      if (q >= e || src.ts(q) - L.e1_ts > within) {   // expired everywhere it can still emit (sg_pp_rule)
+      int64_t dt = q < e ? src.ts(q) - L.e1_ts : 0;
+      dt = dt < 0 ? -dt : dt;
+      if (q >= e) {
+        done = true;
+        // still pending after the key's last row (and not finished: a partial completes at most once): the rows it
+        // holds are carried, its e1 marked as the start of its lane in the next push
+        if (a.keep && !emitted && !L.overflow && !L.dead() && (L.waiting_count() || L.live_other()))
+          L.witnesses([&](int32_t pos, bool st) {
+            atomicOr(&a.keep[pos], 1u);
+            if (st) a.kstart[pos] = 1;
+          });
+      } else if (dt > within && !L.waiting_count()) {   // expired everywhere it can still emit (sg_pp_rule)
         done = true;
       } else {
         const int em = L.step(q);
@@ -793,22 +789,6 @@ __global__ void k_pp_gather(int64_t n, const char* __restrict__ rec, const uint3
   for (int w = 0; w < stride / 8; ++w) t[w] = s[w];
 }
 
-// carry: keep sorted position p if ts >= ts(last row of its key) - within
-__global__ void k_pp_keep(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
-                          const uint32_t* __restrict__ end, uint32_t sentinel, int64_t within, uint32_t* __restrict__ keep) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= m) return;
-  const uint32_t k = skey[p];
-  uint32_t f = 0;
-  if (k != sentinel) {
-    const int64_t c = sid[p], cl = sid[end[k] - 1];
-    const int64_t t = c < a.nc ? a.cts[c] : a.bts[c - a.nc];
-    const int64_t tl = cl < a.nc ? a.cts[cl] : a.bts[cl - a.nc];
-    f = t >= tl - within ? 1u : 0u;
-  }
-  keep[p] = f;
-}
-
 struct PpCopyCols {
   const void* bsrc[SG_MAX_COLS];
   const uint8_t* bnul[SG_MAX_COLS];
@@ -822,7 +802,7 @@ struct PpCopyCols {
 
 __global__ void k_pp_carry(int64_t m, PpArgs a, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sid,
                            const uint32_t* __restrict__ keep, const uint32_t* __restrict__ pos, PpCopyCols cc,
-                           int64_t* __restrict__ nts, int32_t* __restrict__ nkey) {
+                           int64_t* __restrict__ nts, int32_t* __restrict__ nkey, uint8_t* __restrict__ nstart) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= m || !keep[p]) return;
   const int64_t c = sid[p];
@@ -831,6 +811,7 @@ __global__ void k_pp_carry(int64_t m, PpArgs a, const uint32_t* __restrict__ ske
   const int64_t r = carried ? c : c - a.nc;
   nts[o] = carried ? a.cts[r] : a.bts[r];
   nkey[o] = (int32_t)skey[p];
+  nstart[o] = a.kstart ? a.kstart[p] : 0;
   for (int j = 0; j < cc.ncols; ++j) {
     if (!cc.dst[j]) continue;
     const void* s = carried ? cc.csrc[j] : cc.bsrc[j];
@@ -848,27 +829,7 @@ static SgCols carried_cols(const PartialState* ps, const PpRows& r) {
   return c;
 }
 
-// A view of the carried rows as a batch (for the replay through the general machine when the route is left).
-BatchView sg_partial_carried_view(SgHandle* h, PartialState* ps, int32_t key_bound) {
-  const PpRows& r = ps->rows[ps->cur];
-  BatchView v;
-  v.n = r.n;
-  v.base_index = 0;
-  v.ts = r.ts;
-  v.key = r.key;
-  v.index = nullptr;
-  v.cols = carried_cols(ps, r);
-  v.key_bound = key_bound;
-  v.stream = nullptr;
-  const int rs = h->desc.receivers[ps->rule.recv].stream;
-  if (rs != 0 && r.n) {   // every carried row belongs to the query's stream
-    int32_t* s = (int32_t*)h->ws.get("pp_stream", 4 * r.n, h->stream);
-    std::vector<int32_t> host((size_t)r.n, rs);
-    HIPCHK(hipMemcpy(s, host.data(), 4 * r.n, hipMemcpyHostToDevice));
-    v.stream = s;
-  }
-  return v;
-}
+int64_t sg_partial_carried(const PartialState* ps) { return ps->rows[ps->cur].n; }
 
 static void sort_pairs64(SgHandle* h, const char* tag, uint64_t* k_in, uint64_t* k_out, uint32_t* v_in, uint32_t* v_out,
                          int64_t n, int end_bit) {
@@ -1367,7 +1328,6 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   fail = (int32_t)(cnt[2] & 0xffffffffu);
   if (fail != 5) break;
   const int64_t grown = std::max<int64_t>(4 * cap, (int64_t)std::min<unsigned long long>(cnt[0], (1ull << 40)) + cap);
-  if (getenv("SG_DEBUG_SEQ")) fprintf(stderr, "sequence lanes: match space %lld -> %lld\n", (long long)cap, (long long)grown);
   cap = grown;
   ps->sq_cap_hint = cap;
   }
@@ -1381,7 +1341,6 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   cnt[1] -= cnt[4];
   ps->last_reruns = (int64_t)cnt[3];
   if (fail) {
-    if (getenv("SG_DEBUG_SEQ")) fprintf(stderr, "sequence lanes failed: reason %d\n", fail);
     if (ps->seq_pushes == 0 && a.nc == 0) {   // nothing carried yet: the per-key machine can take the stream exactly
       HIPCHK(hipMemsetAsync(ps->kst, 0, ps->sq_bytes * (size_t)ps->kst_keys, st));
       return 0;
@@ -1456,7 +1415,7 @@ static void carry_rows(SgHandle* h, PartialState* ps, const BatchView& bv, const
       c2.dnul[j] = nr.nul[j];
       c2.bytes[j] = ps->col_bytes[j];
     }
-    hipLaunchKernelGGL(k_pp_carry, grd, blk, 0, st, m, a, skeys, sids, keep, pos, c2, nr.ts, nr.key);
+    hipLaunchKernelGGL(k_pp_carry, grd, blk, 0, st, m, a, skeys, sids, keep, pos, c2, nr.ts, nr.key, nr.start);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
     nr.n = nn;
@@ -1484,14 +1443,12 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   const int64_t nc = h->opt.no_carry ? 0 : cr.n;
   const int64_t m = nc + n;
   if (ps->mode == 1 && m >= ((int64_t)1 << 27)) {   // tie components hold a combined row in 27 bits
-    if (ps->has_count && nc > 0)
-      throw SgError(SG_ECAPACITY, "partial-lane route: push at most 2^27 rows at a time (carried rows included)");
+    // (the caller cuts pushes into sub-pushes of sg_partial_max_rows; the carried partials cannot leave the route)
+    if (nc > 0) throw SgError(SG_ECAPACITY, "partial-lane route: push at most 2^27 rows at a time (carried rows included)");
     return 0;
   }
-  // the route's ordering precondition (k_pp_segments): 1 detect a key's time going back, 2 also whether it went back
-  // deeper than the regression tolerance below the key's carried rows (count states with carried rows only)
-  const int order_check = ps->mode == 1 ? ((ps->has_count && nc > 0) ? 2 : 1) : 0;
-  const int64_t tol = pp_regress_tol(d, ps->has_count != 0);
+  // keys whose time goes back (k_pp_segments): their lanes skip rows only while waiting in a count state
+  const int order_check = ps->mode == 1 ? 1 : 0;
   PpArgs a;
   memset(&a, 0, sizeof(a));
   a.nc = nc;
@@ -1503,6 +1460,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   a.stream = bv.stream;
   a.bkey = bv.key;
   a.ckey = cr.key;
+  a.cstart = ps->mode == 1 && nc > 0 ? cr.start : nullptr;
   const SgCols cc = carried_cols(ps, cr);
   int end_bit = 1;
   while ((1ull << end_bit) <= (uint64_t)kb) ++end_bit;
@@ -1570,6 +1528,12 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   uint32_t* cand = (uint32_t*)h->ws.get("pp_cand", 4 * (m + 1), st);
   uint32_t* beg = (uint32_t*)h->ws.get("pp_beg", 4 * (size_t)kb, st);
   uint32_t* end = (uint32_t*)h->ws.get("pp_end", 4 * (size_t)kb, st);
+  uint8_t* kback = nullptr;
+  if (order_check) {
+    kback = (uint8_t*)h->ws.get("pp_kback", (size_t)kb, st);
+    HIPCHK(hipMemsetAsync(kback, 0, (size_t)kb, st));
+    a.kback = kback;
+  }
   bool rec_mode = ps->rec_ok && !any_nul && m > 0;
   if (rec_mode) {
     // record sort: one 16-B record per row through the key sort, unpacked into the SoA rows (no batch-wide gather)
@@ -1615,8 +1579,8 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
       HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
-      hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, P.ts, order_check, tol, sentinel, beg,
-                         end, err);
+      hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, P.ts, order_check, sentinel, beg,
+                         end, kback);
       HIPCHK(hipGetLastError());
       h->kend();
     }
@@ -1637,7 +1601,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     HIPCHK(hipMemsetAsync(beg, 0, 4 * (size_t)kb, st));
     HIPCHK(hipMemsetAsync(end, 0, 4 * (size_t)kb, st));
     if (m) hipLaunchKernelGGL(k_pp_segments, grd, blk, 0, st, m, a, skeys, sids, (const int64_t*)nullptr,
-                              order_check, tol, sentinel, beg, end, err);
+                              order_check, sentinel, beg, end, kback);
     HIPCHK(hipGetLastError());
     h->kend();
     h->kbeg("pack");
@@ -1651,13 +1615,6 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (herr & 2) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-    if ((herr & 1) && ps->mode == 1) {
-      if (herr & 8)
-        throw SgError(SG_EORDER, "partial-lane route: a key's time went back by more than `within` below its carried "
-                                 "rows while a count state may hold partials (open the handle with partial_lanes = -1 "
-                                 "for such streams)");
-      return 0;   // the per-key machine, rebuilt from the carried rows, takes over exactly
-    }
   }
   h->mark(2);
   if (ps->mode == 2) return seq_lanes_push(h, ps, bv, n, kb, a, P, skeys, sids, beg, end, sentinel);
@@ -1694,6 +1651,16 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   const int k1_bits = std::min(64, rb + 8);
   o.k1_none = k1_bits >= 64 ? ~0ull : (1ull << k1_bits) - 1;
   HIPCHK(hipMemsetAsync(o.count, 0, 16, st));
+  // the carry: lanes still pending after their key's last row mark the rows they hold (PpLane::witnesses)
+  uint32_t* keep = nullptr;
+  if (!h->opt.no_carry && m) {
+    keep = (uint32_t*)h->ws.get("pp_keep", 4 * (m + 1), st);
+    uint8_t* kst = (uint8_t*)h->ws.get("pp_kstart", (size_t)m + 1, st);
+    HIPCHK(hipMemsetAsync(keep, 0, 4 * (m + 1), st));
+    HIPCHK(hipMemsetAsync(kst, 0, (size_t)m + 1, st));
+    a.keep = keep;
+    a.kstart = kst;
+  }
   // wait-term block summaries (chain.h PpWait): only without nulls (a null row passes `!=`), 4-byte attributes
   P.wsum = nullptr;
   if (ps->rule.wait_slots && !P.nul && m > 0) {
@@ -1814,12 +1781,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     h->out.n += M;
   }
   // ---- carry
-  if (!h->opt.no_carry && m) {
-    uint32_t* keep = (uint32_t*)h->ws.get("pp_keep", 4 * (m + 1), st);
-    hipLaunchKernelGGL(k_pp_keep, grd, blk, 0, st, m, a, skeys, sids, end, sentinel,
-                       ps->mode == 1 ? pp_carry_window(d, ps->has_count) : (int64_t)d.within, keep);
-    carry_rows(h, ps, bv, a, m, skeys, sids, keep);
-  }
+  if (keep) carry_rows(h, ps, bv, a, m, skeys, sids, keep);
   h->mark(4);
   h->last_events = n;
   h->last_spilled = 0;
@@ -1827,8 +1789,8 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   return 1;
 }
 
-// Snapshot of the route's state: the carried rows (per key, the rows inside `within` of its last row -- replaying them
-// rebuilds every partial the reference still holds in StreamPreStateProcessor.pendingStateEventList /
+// Snapshot of the route's state: the carried rows (the rows pending partials hold, each flagged when a partial starts at
+// it -- replaying them rebuilds every partial the reference still holds in StreamPreStateProcessor.pendingStateEventList /
 // newAndEveryStateEventList, C/query/input/stream/state/StreamPreStateProcessor.java:352-367) and the latest timestamp.
 void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
   const PpRows& r = ps->rows[ps->cur];
@@ -1842,6 +1804,7 @@ void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
   if (!r.n) return;
   w.dev(r.ts, 8 * r.n, h->stream);
   w.dev(r.key, 4 * r.n, h->stream);
+  w.dev(r.start, r.n, h->stream);
   for (int j = 0; j < SG_MAX_COLS; ++j) {
     if (!ps->used_col[j]) continue;
     w.dev(r.col[j], (size_t)ps->col_bytes[j] * r.n, h->stream);
@@ -1877,6 +1840,7 @@ void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& rd) {
   if (n) {
     rd.dev(r.ts, 8 * n, h->stream);
     rd.dev(r.key, 4 * n, h->stream);
+    rd.dev(r.start, n, h->stream);
     for (int j = 0; j < SG_MAX_COLS; ++j) {
       if (!ps->used_col[j]) continue;
       rd.dev(r.col[j], (size_t)ps->col_bytes[j] * n, h->stream);

@@ -242,6 +242,6 @@ int sg_partial_active(const PartialState* ps);
 void sg_partial_deactivate(PartialState* ps);
 int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t n, uint32_t key_bound);
 int64_t sg_partial_max_rows(SgHandle* h, PartialState* ps);
-BatchView sg_partial_carried_view(SgHandle* h, PartialState* ps, int32_t key_bound);
+int64_t sg_partial_carried(const PartialState* ps);   // rows carried into the next push
 void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w);
 void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& r);

@@ -24,7 +24,7 @@ struct HiHandle {
   // partial lanes (chain.h, as partial.hip runs them): carried rows per push, values as retained-slot bits
   int pp = 0;
   int pp_active = 1;
-  struct CRow { int64_t ts; int32_t key; int64_t vals[SG_MAX_RET]; int32_t nullmask; };
+  struct CRow { int64_t ts; int32_t key; int64_t vals[SG_MAX_RET]; int32_t nullmask; uint8_t start; };
   std::vector<CRow> carried;
   std::vector<SeqState> seq_state;   // sequence lanes: per key (partial.hip's geometry choice: big ...)
   std::vector<SeqStateT<SqSmall>> seq_state_s;   // (... or small, sg_seq_small)
@@ -122,7 +122,7 @@ struct HostPpSrc {
   }
 };
 
-// partial-lane push (partial.hip restated on the host); returns 0 when the push breaks the route's precondition
+// partial-lane push (partial.hip restated on the host); returns -1 when a lane outgrows its arrays
 template <class G>
 static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std::vector<uint64_t>& k1,
                    std::vector<uint64_t>& th, std::vector<uint64_t>& tl) {
@@ -143,25 +143,12 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
     own[k].push_back(nc + i);
   }
   HostPpSrc src{b, &d, &h->carried, nc};
-  bool has_count = false;
-  for (int s = 0; s < d.n_states; ++s) has_count |= d.states[s].kind == SG_K_COUNT;
-  // the route's precondition: a key's timestamps never decrease (also across pushes).  A push that breaks it goes to
-  // the per-key machine rebuilt from the carried rows -- exactly, unless a count state's partial older than the carry
-  // window could be revived (a regression deeper than pp_regress_tol below the key's last carried row): SG_EORDER
-  {
-    const int64_t tol = pp_regress_tol(d, has_count);
-    bool regress = false, deep = false;
-    for (const auto& rows : own) {
-      int64_t last_car = INT64_MIN;   // the key's last carried row's ts (carried rows come first)
-      for (size_t p = 0; p < rows.size() && rows[p] < nc; ++p) last_car = src.ts(rows[p]);
-      for (size_t p = 1; p < rows.size(); ++p)
-        if (src.ts(rows[p - 1]) > src.ts(rows[p])) {
-          regress = true;
-          if (has_count && last_car != INT64_MIN && src.ts(rows[p]) < last_car - tol) deep = true;
-        }
-    }
-    if (regress) return deep ? -2 : 0;
-  }
+  // keys whose time goes back somewhere in this push, carried rows included (k_pp_segments)
+  std::vector<uint8_t> kback(own.size(), 0);
+  for (size_t k = 0; k < own.size(); ++k)
+    for (size_t p = 1; p < own[k].size(); ++p)
+      if (src.ts(own[k][p - 1]) > src.ts(own[k][p])) kback[k] = 1;
+  std::vector<uint8_t> keep((size_t)(nc + n), 0), kstart((size_t)(nc + n), 0);
   const int rstride = 32 + 8 * d.n_select;
   for (size_t k = 0; k < own.size(); ++k) {
     const auto& rows = own[k];
@@ -172,17 +159,20 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
       L.ru = &ru;
       L.src = src;
       L.A = &arr;
+      if (rows[p] < nc && !h->carried[rows[p]].start) continue;   // a carried row starts only its pending partial
       if (!L.start_ok(rows[p])) continue;
       L.start(rows[p]);
       ++h->pp_lanes;
+      bool emitted = false, finished = false;
       for (size_t q = p + 1; q < rows.size(); ++q) {
         const int64_t c = rows[q];
-        if (src.ts(c) - L.e1_ts > d.within) break;
+        const int64_t dt = src.ts(c) - L.e1_ts;
+        if ((dt > d.within || -dt > d.within) && !L.waiting_count()) { finished = true; break; }
         {   // wait skipping (chain.h PpLane::wait_on): here every row the wait term rejects is skipped, the GPU skips
-            // whole 8-row blocks that cannot pass it
+            // whole 8-row blocks that cannot pass it (on a key whose time goes back, only in a count state)
           int ws, wop, wf;
           int64_t wc;
-          if (L.wait_on(ws, wop, wf, wc)) {
+          if (L.wait_on(ws, wop, wf, wc) && (L.wait_count || !kback[k])) {
             int64_t rb;
             int rn;
             src.read_bits(c, ws, wf == 1 ? SG_T_INT : SG_T_FLOAT, rb, rn);
@@ -197,6 +187,7 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
         ++h->pp_steps;
         if (L.overflow) return -1;
         if (em >= 0 && c >= nc) {
+          emitted = true;
           const int64_t r = c - nc;
           k1.push_back(((uint64_t)r << 8) | (uint32_t)em);
           uint64_t a, z;
@@ -223,19 +214,21 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
           }
           memcpy(rec + 16, h32, 16);
         }
-        if (L.dead()) break;
+        if (L.dead()) { finished = true; break; }
       }
+      // pending after the key's last row: the rows the partial holds are carried, its e1 flagged as a start
+      if (!finished && !emitted && !L.dead() && (L.waiting_count() || L.live_other()))
+        L.witnesses([&](int64_t c, bool st) {
+          keep[(size_t)c] = 1;
+          if (st) kstart[(size_t)c] = 1;
+        });
     }
   }
-  // carry: per key, rows with ts >= last ts - window (pp_carry_window)
+  // carry: the marked rows, key by key in arrival order (k_pp_carry)
   std::vector<HiHandle::CRow> next;
-  const int64_t window = pp_carry_window(d, has_count);
   for (size_t k = 0; k < own.size(); ++k) {
-    const auto& rows = own[k];
-    if (rows.empty()) continue;
-    const int64_t last = src.ts(rows.back());
-    for (int64_t c : rows) {
-      if (src.ts(c) < last - window) continue;
+    for (int64_t c : own[k]) {
+      if (!keep[(size_t)c]) continue;
       HiHandle::CRow cr;
       memset(&cr, 0, sizeof(cr));
       cr.ts = src.ts(c);
@@ -248,6 +241,7 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
           if (null) cr.nullmask |= 1 << j;
         }
       }
+      cr.start = kstart[(size_t)c];
       next.push_back(cr);
     }
   }
@@ -469,7 +463,6 @@ int hi_push(HiHandle* h, const sg_batch* b) {
     std::vector<uint64_t> k1, th, tl;
     const int rc = sg_pp_small(sg_pp_rule(h->d), h->d) ? pp_push<PpSmall>(h, b, recs, k1, th, tl)
                                                        : pp_push<PpBig>(h, b, recs, k1, th, tl);
-    if (rc == -2) { h->err = SG_EORDER; return SG_EORDER; }
     if (rc < 0) { h->err = SG_EUNSUPPORTED; return SG_EUNSUPPORTED; }
     if (rc == 1) {
       const int rstride = 32 + 8 * h->d.n_select;

@@ -130,12 +130,12 @@ def test_500_handles_20_nodes_release_everything():
 
 
 def test_binding_loads_one_hip_runtime():
+    """CPU check of the import-order fix: loading the library first still maps exactly one libamdhip64 and one
+    libhsa-runtime64 (torch's), whatever the caller imports afterwards."""
     import importlib.util
     from siddhi_amd import _native
     if importlib.util.find_spec("torch") is None or not os.path.exists(_native.LIB_PATH):
         pytest.skip("needs torch and the built libsiddhi_gpu.so")
-    """CPU check of the import-order fix: loading the library first still maps exactly one libamdhip64 and one
-    libhsa-runtime64 (torch's), whatever the caller imports afterwards."""
     code = ("import sys; sys.path.insert(0, %r)\n"
             "from siddhi_amd import _native as N; N.load_library()\n"
             "import torch\n"

@@ -1,8 +1,8 @@
 """Partial lanes (siddhi_amd/csrc/chain.h, partial.hip): patterns whose partial matches never interact run one partial
 per lane, and the delivery order is rebuilt from each partial's insertion history.  The same chain.h code runs on the
 CPU here (tests/host_interp) against the oracle over a family of pattern shapes, value domains small enough to make
-ties, multi-push carries and a stream whose timestamps go back (the route hands its carried rows to the per-key
-machine).  GPU tests run the HIP route through the C-ABI against the oracle."""
+ties, multi-push carries and streams whose timestamps go back (per key, within and across pushes, by up to 10x
+`within`).  GPU tests run the HIP route through the C-ABI against the oracle."""
 import os
 import sys
 
@@ -134,12 +134,16 @@ def _going_back(q, back=40):
                  [np.concatenate([x, y]) for x, y in zip(a.cols, b.cols)], [None] * 4)
 
 
-@pytest.mark.parametrize("name", ["next3", "and_next", "or"])
-def test_timestamps_going_back_leave_the_route(name):
-    """A push whose timestamps go back (per key) ends the route for count-free queries: the carried rows are replayed
-    silently through the per-key machine, which then continues -- output identical to the oracle on the stream."""
+@pytest.mark.parametrize("back", [40, 400])
+@pytest.mark.parametrize("name", ["next3", "and_next", "or", "c3c", "count13", "count_or"])
+def test_timestamps_going_back(name, back):
+    """A push whose timestamps go back (per key) stays on the route: a partial expires at the first row more than
+    `within` from its e1 on either side (StreamPreStateProcessor.isExpired, :102-113), except while it waits in a count
+    state, which never expires it (CountPreStateProcessor.java:53-93) -- so a regression of 400 ms (within is 40-80 ms)
+    can complete a partial parked there long ago, and the carry keeps every partial still pending (chain.h
+    PpLane::witnesses)."""
     q = HEAD + SHAPES[name]
-    both = _going_back(q)
+    both = _going_back(q, back=back)
     assert both.ts[10_000] < both.ts[9_999]
     want = run_engine(OracleEngine, q, [both])
     got = run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(both, [10_000, 15_000]))
@@ -147,23 +151,21 @@ def test_timestamps_going_back_leave_the_route(name):
     assert_same(got, want)
 
 
-def test_timestamps_going_back_with_a_count_state():
-    """Count states never expire partials (CountPreStateProcessor.java:53-93), so time going back can revive one parked
-    in a count state after it left `within`.  The route carries one extra `within` of rows for such queries
-    (chain.h pp_carry_window): a key whose time goes back by at most `within` below its carried rows continues exactly
-    on the per-key machine rebuilt from them; a deeper regression is SG_EORDER, and the per-key machine from the start
-    (partial_lanes = -1) takes such streams."""
-    q = HEAD + SHAPES["c3c"]   # within 60 ms
-    shallow = _going_back(q, back=40)
-    assert shallow.ts[10_000] < shallow.ts[9_999]
-    want = run_engine(OracleEngine, q, [shallow])
+def _jittered(n, keys, seed, within, pushes):
+    from test_time_regression import jitter
+    b = small_batch(n, keys, 100, 4, seed=seed)
+    b.ts = jitter(b.ts, within, seed + 1, frac=0.03)
+    return split(b, [n * p // pushes for p in range(1, pushes)])
+
+
+@pytest.mark.parametrize("name", ["c3c", "count13", "count22", "next3", "and_next"])
+def test_jittered_pushes(name):
+    """rows pulled back by 1-5 ms, up to `within` and up to 10x `within`, blocks of rows shifted back, 4 pushes"""
+    q = HEAD + SHAPES[name]
+    parts = _jittered(24_000, 30, sum(name.encode()), 60, 4)
+    want = run_engine(OracleEngine, q, parts)
     assert len(want) > 0
-    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(shallow, [10_000, 15_000])), want)
-    deep = _going_back(q, back=400)
-    with pytest.raises(RuntimeError, match="-5"):
-        run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(deep, [10_000, 15_000]))
-    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=False), q, split(deep, [10_000, 15_000])),
-                run_engine(OracleEngine, q, [deep]))
+    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, parts), want)
 
 
 def test_seq_rule_covers_the_shapes():
@@ -267,27 +269,46 @@ def test_gpu_shapes_every_order_path(name, order):
 
 
 @pytest.mark.gpu
-def test_gpu_unpartitioned_and_order_fallback():
-    from siddhi_amd._native import GpuEngine, SgError
+def test_gpu_unpartitioned_and_time_going_back():
+    from siddhi_amd._native import GpuEngine
     q = HEAD + UNPART
     b = small_batch(20_000, 1, 100, 2, seed=3)
     assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(b, [7000])),
                 run_engine(OracleEngine, q, [b]))
-    q = HEAD + SHAPES["and_next"]
-    both = _going_back(q)
-    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(both, [10_000, 15_000])),
-                run_engine(OracleEngine, q, [both]))
-    q = HEAD + SHAPES["c3c"]   # count state, within 60 ms: a 40 ms regression continues exactly, 400 ms is SG_EORDER
-    shallow = _going_back(q, back=40)
-    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(shallow, [10_000, 15_000])),
-                run_engine(OracleEngine, q, [shallow]))
-    deep = _going_back(q, back=400)
-    with pytest.raises(SgError) as ei:
-        run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(deep, [10_000, 15_000]))
-    assert ei.value.code == -5
-    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=-1), q,
-                           split(deep, [10_000, 15_000])),
-                run_engine(OracleEngine, q, [deep]))
+    for name in ("and_next", "c3c"):   # c3c: a count state, within 60 ms; the regressions 40 and 400 ms
+        q = HEAD + SHAPES[name]
+        for back in (40, 400):
+            both = _going_back(q, back=back)
+            assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, split(both, [10_000, 15_000])),
+                        run_engine(OracleEngine, q, [both]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c3c", "count13", "count22", "next3", "and_next"])
+def test_gpu_jittered_pushes(name):
+    from siddhi_amd._native import GpuEngine
+    q = HEAD + SHAPES[name]
+    parts = _jittered(24_000, 30, sum(name.encode()), 60, 4)
+    want = run_engine(OracleEngine, q, parts)
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, parts), want)
+
+
+@pytest.mark.gpu
+def test_gpu_c3c_jittered():
+    """C3c's query and generator (within 1 sec, 500 keys), rows pulled back up to 10 s, three pushes, the third starting
+    2 s before the second ended"""
+    from siddhi_amd._native import GpuEngine
+    from test_time_regression import jitter
+    q = synth.QUERIES["C3c"]
+    g = synth.generate("C3c", 0, 240_000, keys=500, rate=100)
+    ts = jitter(g["ts"], 1000, 17)
+    ts[160_000:] -= 2000
+    b = Batch(240_000, 0, ts, np.zeros(240_000, np.int32), dense_first_seen(g["key"]),
+              [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
+    parts = split(b, [80_000, 160_000])
+    want = run_engine(OracleEngine, q, parts)
+    assert len(want) > 0
+    assert_same(run_engine(GpuEngine, q, parts), want)
 
 
 def _two_stream_going_back(back):
@@ -303,22 +324,19 @@ def _two_stream_going_back(back):
 
 @pytest.mark.gpu
 def test_gpu_machine_count_state_time_going_back():
-    """A two-stream count pattern (outside the lane routes: the per-key machine, cut into time-horizon units while
-    time moves forward).  A cut runtime lacks the partials parked in the count state since before the unit horizon,
-    which time going back would revive: the push that goes back is SG_EORDER on a default handle, and a handle opened
-    with partial_lanes = -1 (never cut for count states) matches the oracle."""
-    from siddhi_amd._native import GpuEngine, SgError
+    """A two-stream count pattern (outside the lane routes: the per-key machine).  Time-horizon units would lack the
+    partials parked in the count state since before the unit horizon, which time going back revives: such queries
+    are never cut by time, so a push that goes back matches the oracle on every handle."""
+    from siddhi_amd._native import GpuEngine
     q = ("define stream S (id long, symbol string, v int, w int); define stream T (id long, symbol string, v int, w int); "
          "partition with (symbol of S, symbol of T) begin @info(name='q') "
          "from every e1=S[v>50] -> e2=T[v>e1.v]<2:5> -> e3=S[v<e1.v] within 60 milliseconds "
          "select e1.id as i1, e2[0].id as a, e2[last].id as z, e3.id as i3 insert into M; end;")
     b = _two_stream_going_back(400)
     parts = split(b, [10_000, 15_000])
-    with pytest.raises(SgError) as ei:
-        run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, parts)
-    assert ei.value.code == -5
     want = run_engine(OracleEngine, q, [b])
     assert len(want) > 0
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True), q, parts), want)
     assert_same(run_engine(lambda ctx: GpuEngine(ctx, force_general=True, partial_lanes=-1), q, parts), want)
 
 
@@ -416,7 +434,7 @@ def test_gpu_pushes_beyond_the_row_budget_are_split(monkeypatch):
     """Tie components hold a combined row in 27 bits: a push whose rows (carried rows included) pass that budget runs
     as consecutive sub-pushes on the route instead of failing (budget lowered to 30k rows here), first push included."""
     from siddhi_amd._native import GpuEngine
-    monkeypatch.setenv("SG_DEBUG_PP_ROW_BUDGET", "30000")   # (rate 10/ms: about 10k rows inside `within 1 sec` are carried)
+    monkeypatch.setenv("SG_DEBUG_PP_ROW_BUDGET", "30000")   # (the carried rows of pending partials count against it)
     q = synth.QUERIES["C3c"]
     g = synth.generate("C3c", 0, 200_000, keys=500, rate=10)
     b = Batch(200_000, 0, g["ts"], np.zeros(200_000, np.int32), dense_first_seen(g["key"]),
