@@ -17,11 +17,13 @@ whole_node (SURVEY.md §8d's definition, never `value`): pinned raw host rows (6
   PCIe rate against a measured pinned-copy peak, and on one GPU the host stages of G = 2, 4, 8 shards mapped onto it.
 configs: C2 (configs[1]), C1, C3b, C3c, C4 and PP sub-lines, one push each on one GPU, with their own rooflines.
 
-roofline (per launch = per push): the dominant kernel (largest HIP-event time, recorded on the launch stream by the
-engine, sg_timing.kernel_ms) against ITS OWN algorithmic bytes (KERNEL_BYTES), the whole path's SURVEY §8d bytes over
-the sum of the push's kernels beside it (`path`), and the predicate pass (4.125 B/event); `traffic` comes from a
-rocprofv3 PMC summary of this same command (profiles/r04/collect.sh, FETCH_SIZE x2 + WRITE_SIZE passes) and is only
+roofline (per launch = per push): SURVEY §8d's algorithmic bytes of the push over the dominant kernel's average
+duration (largest HIP-event time, recorded on the launch stream by the engine, sg_timing.kernel_ms) -- the task's
+definition -- with beside it the same kernel against ITS OWN algorithmic bytes (`kernel_own`, KERNEL_BYTES), the §8d
+bytes over the sum of the push's kernels (`path`), and the predicate pass (4.125 B/event); `traffic` comes from a
+rocprofv3 PMC summary of this same command (profiles/r05/collect.sh, FETCH_SIZE x2 + WRITE_SIZE passes) and is only
 used when its kernel-source hash matches the tree.
+The JSON line ends with `whole_node` and `roofline` (the driver keeps the line's tail).
 """
 import argparse
 import hashlib
@@ -44,7 +46,7 @@ from siddhi_amd import lowering as L          # noqa: E402
 from siddhi_amd import synth                  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_DIR = os.path.join(ROOT, "profiles", "r04")
+PMC_DIR = os.path.join(ROOT, "profiles", "r05")
 
 
 def barrier():
@@ -190,7 +192,7 @@ def pmc_traffic(path, cfg, n, dominant):
     except OSError:
         return None, "no PMC summary at %s" % os.path.relpath(path, ROOT)
     if prof.get("source_hash") != source_hash(cfg):
-        return None, "stale PMC summary (source hash %s != tree %s): rerun profiles/r04/collect.sh" % (
+        return None, "stale PMC summary (source hash %s != tree %s): rerun profiles/r05/collect.sh" % (
             prof.get("source_hash"), source_hash(cfg))
     if prof.get("workload") != cfg or prof.get("events") != n:
         return None, "PMC summary is for %s/%s events" % (prof.get("workload"), prof.get("events"))
@@ -345,8 +347,9 @@ KERNEL_BYTES = {"pred": (4.125, 0.0), "part_hist": (4.0, 0.0), "part_group": (41
 
 
 def roofline_of(cfg, n, matches, kern, stage):
-    """`roofline` of one push: the dominant kernel's OWN algorithmic bytes (KERNEL_BYTES) over its HIP-event time;
-    `path` = SURVEY.md §8d whole-path bytes over the sum of the push's kernels; the predicate-evaluation pass."""
+    """`roofline` of one push: SURVEY.md §8d bytes over the dominant kernel's HIP-event time (`achieved`, `frac`);
+    `kernel_own` = the same kernel against its OWN algorithmic bytes (KERNEL_BYTES); `path` = §8d bytes over the sum
+    of the push's kernels; the predicate-evaluation pass."""
     per_ev, per_m, pred_b = PATH_BYTES[cfg]
     path_bytes = per_ev * n + per_m * matches
     dominant = max(kern, key=kern.get) if kern else None
@@ -359,11 +362,15 @@ def roofline_of(cfg, n, matches, kern, stage):
         dom_bytes = path_bytes
         dom_def = "SURVEY.md §8d whole-path bytes (%.3f B/event + %.0f B/match): no per-kernel model" % (per_ev, per_m)
     dom_gbs = dom_bytes / (t_dom * 1e-3) / 1e9 if t_dom else 0.0
+    s8_gbs = path_bytes / (t_dom * 1e-3) / 1e9 if t_dom else 0.0
     path_gbs = path_bytes / (stage[4] * 1e-3) / 1e9 if stage[4] else 0.0
-    roof = {"bound": "hbm", "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(dom_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+    roof = {"bound": "hbm", "achieved": round(s8_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(s8_gbs / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": dominant, "kernel_ms": round(t_dom, 4),
-            "algorithmic_GB_per_launch": round(dom_bytes / 1e9, 4), "bytes_definition": dom_def,
+            "algorithmic_GB_per_launch": round(path_bytes / 1e9, 4),
+            "bytes_definition": "SURVEY.md §8d: %.3f B/event + %.0f B/match over the dominant kernel's time" % (per_ev, per_m),
+            "kernel_own": {"achieved": round(dom_gbs, 1), "frac": round(dom_gbs / HBM_PEAK_GBS, 4),
+                           "algorithmic_GB": round(dom_bytes / 1e9, 4), "bytes_definition": dom_def},
             "path": {"achieved": round(path_gbs, 1), "frac": round(path_gbs / HBM_PEAK_GBS, 4),
                      "kernels_total_ms": round(float(stage[4]), 4), "algorithmic_GB": round(path_bytes / 1e9, 4),
                      "bytes_definition": "SURVEY.md §8d: %.3f B/event + %.0f B/match" % (per_ev, per_m)},
@@ -562,7 +569,7 @@ def main():
     ap.add_argument("--other-configs", default="C2,C1,C3b,C3c,C4,PP",
                     help="BASELINE configs measured beside the headline (one GPU, rank 0; '' to skip)")
     ap.add_argument("--other-steps", type=int, default=3)
-    ap.add_argument("--pmc", default="", help="rocprofv3 PMC summary of this command (default profiles/r04/<cfg>_pmc.json)")
+    ap.add_argument("--pmc", default="", help="rocprofv3 PMC summary of this command (default profiles/r05/<cfg>_pmc.json)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -671,11 +678,11 @@ def main():
         "dtype": "f32", "data": "synthetic (SplitMix64 generator, SURVEY.md §8d), inputs resident in HBM; matches "
                                "projected in HBM (zero-copy sg_device_records)",
         "config": conf,
-        "whole_node": c5w,
-        "roofline": roof,
         "cpu_baseline": cpu,
         "configs": others,
         "source_hash": source_hash(pmc_cfg),
+        "whole_node": c5w,   # (last: the driver stores the line's tail)
+        "roofline": roof,
     }
     print(json.dumps(line))
 

@@ -158,3 +158,42 @@ class CarriedShardedOracle:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+
+
+def _c4_worker(w):
+    from oracle import OracleEngine
+    b = _SHARDS["batch"]
+    S = _SHARDS["S"]
+    idcol = _SHARDS["idcol"]
+    # rows of the other ids become clock-only rows of the app's Tick stream, at their global indices
+    st = np.where((b.stream == 0) & (b.cols[idcol] % S == w), 0, _SHARDS["tick"]).astype(np.int32)
+    sb = Batch(b.n, b.base_index, b.ts, st, b.key, b.cols, b.nulls, b.index)
+    return run_engine(OracleEngine, _SHARDS["q"], [sb])
+
+
+def id_sharded_absence_oracle(query_text, batch, shards, workers, id_col=0, tick_stream=1, order_col=0):
+    """The oracle over an unpartitioned absence query `every e1=S -> not S[id==e1.id] for W` (C4's shape), sharded
+    by the id the kill compares.  Shard s keeps the S rows whose id is s mod `shards`; every other
+    row stays at its global index as a clock-only row of the app's Tick stream, so each shard's playback clock and
+    scheduler see the rows the single runtime sees (TimestampGeneratorImpl.setCurrentTimestamp, C/util/timestamp/
+    TimestampGeneratorImpl.java:106-125; Scheduler.java:179-214).  A kill involves rows of one id only
+    (AbsentStreamPreStateProcessor.processAndReturn, C/query/input/stream/state/AbsentStreamPreStateProcessor.java:
+    140-244), and an emission's trigger depends only on the clock, so the shards' emissions are the single runtime's;
+    within one trigger the scheduler's FIFO fires them in schedule order -- for a stream whose time never goes back,
+    the e1 arrival order.  Merged stably by (trigger, e1's `order_col` select value); the callback group is the rank
+    within the trigger.  Test infrastructure only."""
+    import multiprocessing as mp
+    _SHARDS.update(batch=batch, S=shards, idcol=id_col, tick=tick_stream, q=query_text)
+    try:
+        with mp.get_context("fork").Pool(workers) as pool:
+            outs = pool.map(_c4_worker, range(shards))
+    finally:
+        _SHARDS.clear()
+    fields = ("trigger", "ts", "key", "group", "vals", "vnull")
+    cat = [np.concatenate([getattr(o, f) for o in outs]) for f in fields]
+    order = np.lexsort((cat[4][:, order_col], cat[0]))
+    out = [c[order] for c in cat]
+    t = out[0]
+    first = np.searchsorted(t, t, side="left")
+    out[3] = (np.arange(len(t)) - first).astype(out[3].dtype)
+    return Outputs(*out)

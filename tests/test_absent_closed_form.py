@@ -3,7 +3,8 @@
 CPU: the numpy restatement of SURVEY.md A.8 (tests/absent_np.py) is pinned against the oracle and the
 golden fixture.  GPU: the HIP closed form (siddhi_amd/csrc/absent.hip) against the oracle on small
 streams (edge cases: nulls, filters on either side, two streams, clock-only rows, bursts that fire many
-timers at one trigger, multi-push carry) and against the numpy restatement at the full C4 size."""
+timers at one trigger, multi-push carry) and at the full C4 size (10M events) against the oracle sharded by id
+(parity_util.id_sharded_absence_oracle, itself checked against the single oracle here on the CPU)."""
 import os
 import sys
 import zlib
@@ -13,7 +14,7 @@ import pytest
 
 from absent_np import absent_every_eq
 from oracle import OracleEngine
-from parity_util import assert_same, run_engine, synth_batch
+from parity_util import assert_same, id_sharded_absence_oracle, run_engine, synth_batch
 from siddhi_amd import synth
 from siddhi_amd.runtime import Batch
 
@@ -48,6 +49,15 @@ def test_numpy_restatement_matches_oracle():
     want = run_engine(OracleEngine, synth.QUERIES["C4"], [b])
     assert len(want) > 0
     check_np(b, want)
+
+
+def test_id_sharded_oracle_matches_oracle():
+    """the id-sharded oracle (other ids' rows as clock-only Tick rows, merged by (trigger, e1.seq)) is the single
+    runtime's output -- including bursts where one row fires many timers"""
+    b = c4_batch(30_000, 2_000)
+    want = run_engine(OracleEngine, synth.QUERIES["C4"], [b])
+    assert len(want) > 0 and int(np.max(want.group)) > 0
+    assert_same(id_sharded_absence_oracle(synth.QUERIES["C4"], b, 16, 4), want)
 
 
 def test_numpy_restatement_matches_golden():
@@ -155,13 +165,19 @@ def test_gpu_absent_two_streams_and_clock_rows():
     assert_same(got, want)
 
 
+SHARD_WORKERS = 16   # (the GPU box's CPU share)
+
+
 @pytest.mark.gpu
-def test_gpu_c4_full_size_vs_numpy():
-    """BASELINE config C4 at full size (10M events, 10k ids, 1 event/ms) against the numpy restatement."""
+@pytest.mark.timeout(600)
+def test_gpu_c4_full_size():
+    """BASELINE config C4 at full size (10M events, 10k ids, 1 event/ms) against the oracle sharded by id"""
     n = synth.CONFIGS["C4"][1]
     b = c4_batch(n, synth.CONFIGS["C4"][2])
     got = run_engine(gpu(), synth.QUERIES["C4"], [b])
-    check_np(b, got)
+    want = id_sharded_absence_oracle(synth.QUERIES["C4"], b, 128, SHARD_WORKERS)
+    assert len(want) > 6_000_000
+    assert_same(got, want)
 
 
 def _no_stream(b):
@@ -169,13 +185,16 @@ def _no_stream(b):
 
 
 @pytest.mark.gpu
-def test_gpu_c4_fast_path_full_size_vs_numpy():
+@pytest.mark.timeout(600)
+def test_gpu_c4_fast_path_full_size():
     """No stream column (every row is S): the role pass reads the id column directly and the kill pass steps
-    to the next sorted row (absent.hip `fast`)."""
+    to the next sorted row (absent.hip `fast`); the id-sharded oracle at full size"""
     n = synth.CONFIGS["C4"][1]
     b = c4_batch(n, synth.CONFIGS["C4"][2], tick=False)
     got = run_engine(gpu(), synth.QUERIES["C4"], [_no_stream(b)])
-    check_np(b, got)
+    want = id_sharded_absence_oracle(synth.QUERIES["C4"], b, 128, SHARD_WORKERS)
+    assert len(want) > 6_000_000
+    assert_same(got, want)
 
 
 @pytest.mark.gpu
