@@ -329,11 +329,10 @@ typedef struct sg_node_stats {  /* of the last sg_node_push */
   int64_t shard_rows[SG_NODE_MAX_GPUS];   /* rows each GPU has received since open/reset */
 } sg_node_stats;
 /* chunk_rows 0: about 16 chunks per push (4M..25M rows each); host_threads 0: all hardware threads.
- * Closed-form queries (`every A -> B[..]`): out->ts and B-attribute columns are filled on the host from the
- * batch's trigger rows instead of being copied back from the GPU (environment SG_NODE_NO_FILL: copy them).  With one
- * GPU and the device dictionary, the e1 attribute the query only projects is not uploaded either: the GPU carries
- * each row's event index mod 2^32 instead and the host reads the attribute (opt-in: SG_NODE_TAGS=1; measured slower
- * on hosts whose memory system makes the random e1 reads dearer than the PCIe bytes they save). */
+ * With several GPUs and the device key dictionary, rows are sharded, exchanged and merged on the GPUs (each GPU uploads
+ * a contiguous slice of the batch; peer copies between GPUs); queries with playback timers route and merge on the host.
+ * One GPU, closed-form queries (`every A -> B[..]`): out->ts and B-attribute columns are filled on the host from the
+ * batch's trigger rows instead of being copied back from the GPU. */
 int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const sg_options* opt, int host_threads,
                  int64_t chunk_rows, sg_node** out);
 /* Push a batch; its matches (node delivery order) go to out rows [0, *n).  out->trigger is required; other NULL

@@ -12,32 +12,6 @@ void sg_run_every_next(SgHandle* h, const BatchView& bv, int64_t n) {
   }
 }
 
-// Largest (ref - tag) mod 2^32 over the carried rows' 32-bit column `col` (the node's row tags: global event index
-// mod 2^32), i.e. how far back the oldest row the closed form still holds lies; -1 without carried rows.
-__global__ void k_carry_lag(const uint32_t* __restrict__ tags, int64_t n, uint32_t ref, unsigned int* __restrict__ out) {
-  unsigned int m = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    m = max(m, (unsigned int)(ref - tags[i]));
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o));
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
-}
-
-int64_t sg_every_next_carry_max_lag(SgHandle* h, int col, uint32_t ref) {
-  if (!h->state || h->state_kind != 1) return -1;
-  EveryNextState* es = (EveryNextState*)h->state;
-  const CarrySet& cs = es->carry[es->cur];
-  if (cs.n == 0 || !cs.col[col]) return -1;
-  unsigned int* d = (unsigned int*)h->ws.get("carry_lag", sizeof(unsigned int), h->stream);
-  HIPCHK(hipMemsetAsync(d, 0, sizeof(unsigned int), h->stream));
-  hipLaunchKernelGGL(k_carry_lag, dim3((unsigned)std::min<int64_t>((cs.n + 255) / 256, 1024)), dim3(256), 0, h->stream,
-                     (const uint32_t*)cs.col[col], cs.n, ref, d);
-  HIPCHK(hipGetLastError());
-  unsigned int v = 0;
-  HIPCHK(hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  return (int64_t)v;
-}
-
 void sg_every_next_reset(SgHandle* h) {
   if (h->state && h->state_kind == 1) {
     EveryNextState* es = (EveryNextState*)h->state;

@@ -3,22 +3,30 @@
 // The reference runs a partitioned query in one JVM: PartitionStreamReceiver.receive looks each event's key up and
 // hands it to that key's cloned runtime (C/partition/PartitionStreamReceiver.java:80-281, PartitionRuntime.java:
 // 255-308); the matches reach QueryCallback.receive in one ordered stream (C/query/output/callback/
-// QueryCallback.java:52-85).  Here the same contract is met by a pipeline over chunks of the host batch:
+// QueryCallback.java:52-85).  Here the same contract is met by a pipeline over chunks of the host batch.
 //
+// G > 1 GPUs with the device key dictionary (every partitioned query without playback timers): the GPU-side shard
+// exchange (x_loop below).  Each GPU uploads a contiguous slice of the caller's rows, shards them on the device,
+// exchanges rows with the other GPUs (peer copies), runs its shard, sends each match to the GPU that owns its trigger's
+// slice, and that GPU merges by trigger and copies straight into the caller's columns -- the host does no per-row or
+// per-match work.
+//
+// One GPU, or queries whose playback timers need every row's clock on every shard (host key dictionary):
 //   route    host thread pool: raw partition-key values -> first-seen dense ids -> shard (GPU) + per-shard id
 //            (router.h); with G > 1 every chunk's rows are scattered, in arrival order, into per-shard pinned
-//            staging (two passes: count per shard, then place), keeping each row's global event index on the host
+//            staging (clock rows fan out to every shard), keeping each row's global event index on the host
 //   upload   one copy thread per GPU: the shard's rows of chunk j go to HBM while chunk j-1 computes
 //   compute  one thread per GPU: sg_push_view over the chunk (state carried between chunks = one stream)
 //   deliver  the same thread: the chunk's matches are transposed on the GPU into SoA columns and copied back into
 //            the shard's pinned ring while the next chunk computes
 //   merge    (G > 1) host thread pool: chunk j's shard streams merged into the node's delivery order by (global
-//            trigger, phase, global dense key) -- every trigger's matches come from its key's shard, so the merge
-//            is a k-way interleave by trigger; G = 1: the GPU delivers straight into the caller's columns.
+//            trigger, phase, global dense key) -- timer passes fan out to every shard; G = 1: the GPU delivers
+//            straight into the caller's columns.
 //
 // Every stage of chunk j overlaps the other stages of chunks j-1 and j+1 (ring depth NODE_RING on the host,
 // two device slots per GPU); no stage blocks another except through those rings.  A handle (sg_handle) is
 // single-threaded: each is only ever driven by its shard's compute thread (and its copy thread's stream).
+// Host threads come from process-wide pools (host_pool, pipeline_threads): no thread is started per node or push.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -32,6 +40,8 @@
 #include <thread>
 #include <type_traits>
 #include <vector>
+
+#include <rocprim/rocprim.hpp>
 
 #include "keydict.h"
 #include "router.h"
@@ -59,19 +69,11 @@ inline void nt_store(V* p, V v) {
   if constexpr (sizeof(V) == 4 || sizeof(V) == 8) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
-// where the node uses them (SG_NODE_NT bit mask, read once): 1 the host fill of trigger-row columns, 2 the G > 1
-// scatter into shard staging, 4 the G > 1 merge's own column writes.  Default 1.  (A/B runs of the bits on one box,
-// profiles/r04/node_nt_ab.log, were inside the host stages' own run-to-run spread of up to 2x.)
-inline int nt_mode() {
-  static const int m = [] {
-    const char* e = getenv("SG_NODE_NT");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
+// (used by the host fill of trigger-row columns; A/B runs of streaming stores in the G > 1 host scatter and merge,
+// profiles/r04/node_nt_ab.log, were inside the host stages' own run-to-run spread)
 template <int BIT, class V>
 inline void put(V* p, V v) {
-  if (nt_mode() & BIT) nt_store(p, v);
+  if (BIT == 1) nt_store(p, v);
   else *p = v;
 }
 
@@ -79,37 +81,33 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Fixed thread pool: parallel_for(n, fn) runs fn(0..n-1) on the workers and the caller and returns when all are
-// done.  Several coordinator threads may submit at once (their tasks interleave).
+// Process-wide thread pool shared by every node: parallel_for(n, fn) runs fn(0..n-1) on the workers and the caller
+// and returns when all are done.  Several coordinator threads may submit at once (their tasks interleave).  Workers
+// live as long as the process (glibc gives each new thread a malloc arena of its own, kept after the thread exits:
+// threads started per node or per push would keep adding arenas); grow() adds workers up to the largest host_threads
+// a node asked for.
 struct Pool {
   std::vector<std::thread> th;
   std::mutex mu;
   std::condition_variable cv;
   std::vector<std::function<void()>> q;
-  bool stop = false;
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i)
+  void grow(int n) {
+    std::lock_guard<std::mutex> lk(mu);
+    while ((int)th.size() < n) {
       th.emplace_back([this] {
         while (true) {
           std::function<void()> f;
           {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return stop || !q.empty(); });
-            if (stop && q.empty()) return;
+            std::unique_lock<std::mutex> lk2(mu);
+            cv.wait(lk2, [&] { return !q.empty(); });
             f = std::move(q.back());
             q.pop_back();
           }
           f();
         }
       });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      stop = true;
+      th.back().detach();
     }
-    cv.notify_all();
-    for (auto& t : th) t.join();
   }
   // Completion state of one parallel_for, shared by the submitter and every queued closure: the worker that finishes
   // the last task decrements and notifies under the mutex, and the closures own the state, so the submitter may
@@ -168,6 +166,65 @@ struct Pool {
   }
 };
 
+Pool& host_pool() {
+  static Pool* p = new Pool();   // (never destroyed: its detached workers outlive static destruction)
+  return *p;
+}
+
+// Process-wide pipeline threads: a node push runs its per-GPU loops as tasks on parked threads, starting a new thread
+// only when every one is busy -- the thread count stays at the largest number of loops that ran at once.
+struct Task {
+  std::function<void()> fn;
+  std::mutex m;
+  std::condition_variable cv;
+  bool done = false;
+  void join() {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return done; });
+  }
+};
+struct ThreadCache {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::shared_ptr<Task>> q;
+  int idle = 0;
+  std::shared_ptr<Task> run(std::function<void()> fn) {
+    auto t = std::make_shared<Task>();
+    t->fn = std::move(fn);
+    std::lock_guard<std::mutex> lk(mu);
+    q.push_back(t);
+    if ((int)q.size() > idle) {
+      std::thread([this] { loop(); }).detach();
+    } else {
+      cv.notify_one();
+    }
+    return t;
+  }
+  void loop() {
+    while (true) {
+      std::shared_ptr<Task> t;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        ++idle;
+        cv.wait(lk, [&] { return !q.empty(); });
+        --idle;
+        t = q.front();
+        q.erase(q.begin());
+      }
+      t->fn();
+      {
+        std::lock_guard<std::mutex> lk(t->m);
+        t->done = true;
+      }
+      t->cv.notify_all();
+    }
+  }
+};
+ThreadCache& pipeline_threads() {
+  static ThreadCache* c = new ThreadCache();   // (never destroyed, like host_pool)
+  return *c;
+}
+
 // Pinned host buffer (hipHostMalloc), grow-only.
 struct Pinned {
   void* p = nullptr;
@@ -186,11 +243,289 @@ struct Pinned {
   template <class T> T* as() const { return (T*)p; }
 };
 
+// =====================================================================================================================
+// GPU-side shard exchange (G > 1 with the device dictionary: every partitioned query without playback timers).
+//
+// The host only hands out contiguous row slices: GPU g uploads rows [lo + n*g/G, lo + n*(g+1)/G) of chunk j straight
+// from the caller's columns.  On the device:
+//   shard    k_xcount: each row's shard mix64(raw key) mod G (PartitionStreamReceiver.receive routes a row to its key's
+//            runtime, C/partition/PartitionStreamReceiver.java:177-221) and per-block counts per shard; one scan;
+//            k_xscatter: a stable counting scatter into a send buffer grouped by shard, arrival order kept, with each
+//            row's global event index
+//   exchange the G x G pieces go to their shard's receive slot (hipMemcpyPeerAsync when the GPUs differ, plain D2D
+//            copies when shards share a device): rows, not state -- per-key state never moves (PartitionRuntime.java:
+//            255-308 keeps one runtime per key)
+//   compute  shard s dictionary-encodes its rows (keydict.hip) and runs them with their global indices as triggers
+//   return   its matches, in delivery order, are cut by trigger slice (k_xbounds) and sent to the slice's GPU
+//   merge    GPU g merges the G runs it receives -- every trigger's matches come from its key's shard, so the merge
+//            is a placement by trigger (k_xmark + scan + k_xplace) -- and copies the merged columns straight into the
+//            caller's columns at its offset (the host adds up G match counts per chunk).
+// Host work is per chunk (counts, offsets, events), never per row or per match.  Rows of stream -1 (clock-only) are
+// dropped: without playback timers they change no runtime.
+// =====================================================================================================================
+constexpr int XB_ROWS = 2048;   // rows per block of the shard count / scatter (8 per thread)
+
+__device__ __forceinline__ uint64_t xmix64(uint64_t x) {   // (router.h sgr::mix64)
+  x += 0x9E3779B97F4A7C15ull;
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+
+struct XCols {   // one row set's device columns
+  int64_t* ts;
+  int64_t* raw;
+  int32_t* stream;
+  uint64_t* gidx;
+  void* col[SG_MAX_COLS];
+  uint8_t* nul[SG_MAX_COLS];
+};
+struct XSpec {
+  int32_t ncols;
+  int32_t width[SG_MAX_COLS];   // 0: column not moved
+  int32_t nul[SG_MAX_COLS];
+  int32_t stream;
+};
+
+__global__ void __launch_bounds__(256) k_xcount(const int64_t* __restrict__ raw, const int32_t* __restrict__ stream,
+                                                int64_t n, uint32_t G, uint8_t* __restrict__ shard,
+                                                uint32_t* __restrict__ bcnt, uint32_t nblk) {
+  __shared__ uint32_t c[MAX_GPUS];
+  const uint32_t t = threadIdx.x, b = blockIdx.x;
+  if (t < MAX_GPUS) c[t] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)b * XB_ROWS;
+#pragma unroll
+  for (int k = 0; k < XB_ROWS / 256; ++k) {
+    const int64_t i = base + k * 256 + t;
+    if (i >= n) break;
+    const bool clock = stream && stream[i] < 0;
+    const uint32_t s = clock ? 0xffu : (uint32_t)(xmix64((uint64_t)raw[i]) % G);
+    shard[i] = (uint8_t)s;
+    if (!clock) atomicAdd(&c[s], 1u);
+  }
+  __syncthreads();
+  if (t < G) bcnt[(size_t)t * nblk + b] = c[t];
+}
+
+// per shard s: the start of its rows in the send buffer (boff[s * nblk]); [G] = rows sent
+__global__ void k_xstarts(const uint32_t* __restrict__ boff, uint32_t nblk, uint32_t G, uint32_t* __restrict__ out) {
+  const uint32_t s = threadIdx.x;
+  if (s <= G) out[s] = boff[(size_t)s * nblk];
+}
+
+__global__ void __launch_bounds__(256) k_xscatter(XCols in, XCols out, XSpec sp, int64_t n, uint64_t gbase,
+                                                  const uint8_t* __restrict__ shard, const uint32_t* __restrict__ boff,
+                                                  uint32_t nblk, uint32_t G) {
+  __shared__ uint32_t cur[MAX_GPUS];
+  __shared__ uint32_t wc[4][MAX_GPUS];
+  const uint32_t t = threadIdx.x, b = blockIdx.x, w = t >> 6, lane = t & 63;
+  if (t < G) cur[t] = boff[(size_t)t * nblk + b];
+  if (t < 4 * MAX_GPUS) wc[t / MAX_GPUS][t % MAX_GPUS] = 0;
+  __syncthreads();
+  uint32_t nb = 0;
+  while ((1u << nb) < G) ++nb;
+  const int64_t base = (int64_t)b * XB_ROWS;
+  for (int k = 0; k < XB_ROWS / 256; ++k) {   // 256 rows per step, in arrival order
+    const int64_t i = base + k * 256 + t;
+    const uint32_t s = i < n ? shard[i] : 0xffu;
+    const bool keep = s != 0xffu;
+    // lanes of the wave with the same shard: rank among them and their count
+    uint64_t m = __ballot(keep);
+    for (uint32_t q = 0; q < nb; ++q) {
+      const bool bit = (s >> q) & 1u;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (keep && rank == 0) wc[w][s] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (keep) {
+      uint32_t pos = cur[s] + rank;
+      for (uint32_t q = 0; q < w; ++q) pos += wc[q][s];
+      out.ts[pos] = in.ts[i];
+      out.raw[pos] = in.raw[i];
+      out.gidx[pos] = gbase + (uint64_t)i;
+      if (sp.stream) out.stream[pos] = in.stream[i];
+      for (int c = 0; c < sp.ncols; ++c) {
+        if (sp.width[c] == 8) ((int64_t*)out.col[c])[pos] = ((const int64_t*)in.col[c])[i];
+        else if (sp.width[c] == 4) ((int32_t*)out.col[c])[pos] = ((const int32_t*)in.col[c])[i];
+        if (sp.nul[c]) out.nul[c][pos] = in.nul[c][i];
+      }
+    }
+    __syncthreads();
+    if (t < G) {
+      cur[t] += wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];
+      wc[0][t] = wc[1][t] = wc[2][t] = wc[3][t] = 0;
+    }
+    __syncthreads();
+    (void)lane;
+  }
+}
+
+struct XSlices {
+  uint64_t lo[MAX_GPUS + 1];   // global index of each slice's first row; [G] = the chunk's end
+};
+// matches of one shard (delivery order: triggers non-decreasing) -> the first match of each slice
+__global__ void k_xbounds(const uint64_t* __restrict__ trig, int64_t k, XSlices sl, uint32_t G, int64_t* __restrict__ out) {
+  const uint32_t g = threadIdx.x;
+  if (g > G) return;
+  int64_t a = 0, e = k;
+  const uint64_t x = sl.lo[g];
+  while (a < e) {
+    const int64_t mid = a + (e - a) / 2;
+    if (trig[mid] < x) a = mid + 1;
+    else e = mid;
+  }
+  out[g] = a;
+}
+
+__global__ void k_xmapkeys(int32_t* __restrict__ key, int64_t k, const int32_t* __restrict__ l2g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < k && key[i] >= 0) key[i] = l2g[key[i]];
+}
+
+__global__ void k_xgather_u64(const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx, int64_t m,
+                              uint64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) dst[i] = src[idx[i]];
+}
+
+struct XRuns {
+  int64_t off[MAX_GPUS + 1];   // run r = merge-input rows [off[r], off[r + 1])
+};
+// merge input (G runs, each ordered by trigger; a trigger's matches all in one run): per trigger row of the slice, the
+// length of its segment and where it starts
+__global__ void k_xmark(const uint64_t* __restrict__ trig, int64_t M, XRuns runs, uint32_t G, uint64_t slo,
+                        uint32_t* __restrict__ cnt, uint32_t* __restrict__ seg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  uint32_t r = 0;
+  while (r + 1 < G && runs.off[r + 1] <= i) ++r;
+  const uint64_t x = trig[i];
+  if (i > runs.off[r] && trig[i - 1] == x) return;
+  int64_t e = i + 1;
+  while (e < runs.off[r + 1] && trig[e] == x) ++e;
+  cnt[x - slo] = (uint32_t)(e - i);
+  seg[x - slo] = (uint32_t)i;
+}
+
+struct XLay {   // one SoA match layout (ColLayout offsets from a base)
+  char* base;
+  size_t off_trig, off_ts, off_key, off_grp, off_col[SG_MAX_SELECT], off_nul[SG_MAX_SELECT];
+};
+struct XWant {
+  int32_t ts, key, grp, ns;
+  int32_t width[SG_MAX_SELECT];   // 0: column not delivered
+  int32_t nul[SG_MAX_SELECT];
+};
+__device__ __forceinline__ void xcopy_row(const XLay& a, int64_t i, const XLay& b, int64_t o, const XWant& w) {
+  ((uint64_t*)(b.base + b.off_trig))[o] = ((const uint64_t*)(a.base + a.off_trig))[i];
+  if (w.ts) ((int64_t*)(b.base + b.off_ts))[o] = ((const int64_t*)(a.base + a.off_ts))[i];
+  if (w.key) ((int32_t*)(b.base + b.off_key))[o] = ((const int32_t*)(a.base + a.off_key))[i];
+  if (w.grp) ((uint32_t*)(b.base + b.off_grp))[o] = ((const uint32_t*)(a.base + a.off_grp))[i];
+  for (int c = 0; c < w.ns; ++c) {
+    if (w.width[c] == 8) ((int64_t*)(b.base + b.off_col[c]))[o] = ((const int64_t*)(a.base + a.off_col[c]))[i];
+    else if (w.width[c] == 4) ((int32_t*)(b.base + b.off_col[c]))[o] = ((const int32_t*)(a.base + a.off_col[c]))[i];
+    if (w.nul[c]) ((uint8_t*)(b.base + b.off_nul[c]))[o] = ((const uint8_t*)(a.base + a.off_nul[c]))[i];
+  }
+}
+__global__ void k_xplace(XLay in, int64_t M, uint64_t slo, const uint32_t* __restrict__ off,
+                         const uint32_t* __restrict__ seg, XLay out, XWant w) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const uint64_t t = ((const uint64_t*)(in.base + in.off_trig))[i] - slo;
+  xcopy_row(in, i, out, (int64_t)off[t] + (i - (int64_t)seg[t]), w);
+}
+
+// ---- host side of the exchange ---------------------------------------------------------------------------------
+struct XBuf {   // device buffer, grow-only (the caller makes sure no queued work still reads the old one)
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    HIPCHK(hipMalloc(&p, b ? b : 1));
+    bytes = b;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+struct XRows {   // columns of up to `cap` rows in one allocation
+  XBuf buf;
+  int64_t cap = 0;
+  XCols c;
+};
+
+void xrows_layout(XRows& r, int64_t cap, const XSpec& sp, bool gidx) {
+  cap = std::max(cap, r.cap);
+  auto sz = [&](size_t w) { return ((w * (size_t)cap + 255) / 256) * 256; };
+  size_t bytes = 2 * sz(8) + (gidx ? sz(8) : 0) + (sp.stream ? sz(4) : 0);
+  for (int c = 0; c < sp.ncols; ++c) bytes += (sp.width[c] ? sz((size_t)sp.width[c]) : 0) + (sp.nul[c] ? sz(1) : 0);
+  r.buf.ensure(bytes);
+  r.cap = cap;
+  char* q = r.buf.as<char>();
+  memset(&r.c, 0, sizeof(r.c));
+  auto take = [&](size_t w) { char* x = q; q += sz(w); return x; };
+  r.c.ts = (int64_t*)take(8);
+  r.c.raw = (int64_t*)take(8);
+  if (gidx) r.c.gidx = (uint64_t*)take(8);
+  if (sp.stream) r.c.stream = (int32_t*)take(4);
+  for (int c = 0; c < sp.ncols; ++c) {
+    if (sp.width[c]) r.c.col[c] = take((size_t)sp.width[c]);
+    if (sp.nul[c]) r.c.nul[c] = (uint8_t*)take(1);
+  }
+}
+
+struct XGpu {
+  XRows in[2], send[2];
+  XBuf shard, bcnt, boff, scan_tmp, starts, bounds, mcnt, mseg, moff, mscan_tmp, l2g, nfg;
+  XBuf min[2], mo[2];
+  int64_t min_cap[2] = {0, 0}, mo_cap[2] = {0, 0};
+  int64_t l2g_n = 0;
+  Pinned hstarts[2], hbounds, hnf;
+  hipStream_t xs = nullptr;
+  hipEvent_t ev_in[2] = {}, ev_scat[2] = {}, ev_sent[2] = {}, ev_rfree[2] = {}, ev_osent[2] = {}, ev_mfree[2] = {},
+             ev_d2h[2] = {};
+  bool init = false;
+  void release() {
+    for (int p = 0; p < 2; ++p) {
+      in[p].buf.release();
+      send[p].buf.release();
+      in[p].cap = send[p].cap = 0;
+      min[p].release();
+      mo[p].release();
+      min_cap[p] = mo_cap[p] = 0;
+    }
+    for (XBuf* b : {&shard, &bcnt, &boff, &scan_tmp, &starts, &bounds, &mcnt, &mseg, &moff, &mscan_tmp, &l2g, &nfg})
+      b->release();
+    l2g_n = 0;
+    if (xs) hipStreamDestroy(xs);
+    xs = nullptr;
+    for (hipEvent_t* e : {ev_in, ev_scat, ev_sent, ev_rfree, ev_osent, ev_mfree, ev_d2h})
+      for (int p = 0; p < 2; ++p) {
+        if (e[p]) hipEventDestroy(e[p]);
+        e[p] = nullptr;
+      }
+    init = false;
+  }
+};
+
 }  // namespace
 
 // One shard's rows of one chunk, in arrival order (host staging, G > 1).
 struct NodeStage {
-  Pinned ts, ts32, key, stream, gidx, raw;   // (ts32: the chunk's timestamps as 32-bit offsets from its minimum)   // (raw: device-dictionary mode, the key as received)
+  Pinned ts, ts32, key, stream, gidx;   // (ts32: the chunk's timestamps as 32-bit offsets from its minimum)
   Pinned col[SG_MAX_COLS], nul[SG_MAX_COLS];
 };
 
@@ -237,19 +572,8 @@ struct sg_node {
   int64_t* draw[MAX_GPUS][2] = {};   // device raw-key slots
   int64_t draw_rows = 0;
   std::vector<int32_t> l2g[MAX_GPUS];   // G > 1, device mode: shard-local id -> node-wide first-seen id
+  XGpu x[MAX_GPUS];                  // G > 1, device mode: the GPU-side shard exchange's buffers, streams, events
   int64_t g_keys = 0;
-  // Row tags (one GPU, closed form): the e1 attribute the query only projects (e.g. `e1.id`) never crosses PCIe --
-  // the GPU carries each row's event index mod 2^32 in its place (generated in HBM) and the host selector reads the
-  // attribute of the e1 row the tag names from the caller's columns, or, for rows of earlier pushes the engine still
-  // holds, from `hist` (kept at each push's end for exactly the carried rows' range).
-  int tag_col = -1;
-  int tag_cand = -1;                 // the query's tag column if it has one (tag_col: in use for this stream)
-  bool tag_sel[SG_MAX_SELECT] = {};
-  sg_nfa_desc edesc;                 // what the engine runs (the tag column as INT)
-  Pinned tagbuf;
-  int64_t hist_lo = 0, hist_n = 0;
-  std::vector<int64_t> hist;
-  std::vector<uint8_t> hist_nul;
 };
 
 namespace {
@@ -263,7 +587,6 @@ namespace {
 // them from the caller's pinned input columns by global trigger index.
 struct Want {
   bool ts, key, grp, col[SG_MAX_SELECT], nul[SG_MAX_SELECT];
-  bool tag[SG_MAX_SELECT];      // e1.<tag column>: the GPU delivers the row tag (node tagbuf), the host the value
   int ns;
   int width[SG_MAX_SELECT];
   bool fill_ts;                 // out->ts from the trigger row's ts (host)
@@ -271,13 +594,13 @@ struct Want {
   bool any_fill;
 };
 
-Want want_of(const sg_node& nd, const sg_node_batch& b, const sg_match_columns* out) {
+Want want_of(const sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, bool allow_fill) {
   Want w;
   memset(&w, 0, sizeof(w));
   const sg_nfa_desc& d = nd.desc;
   w.ns = d.n_out > 0 ? d.n_out : d.n_select;
   const bool tie = nd.G > 1 && d.shape != SG_SHAPE_EVERY_NEXT_CMP;
-  const bool closed = d.shape == SG_SHAPE_EVERY_NEXT_CMP && d.n_out == 0 && !nd.no_fill;
+  const bool closed = allow_fill && d.shape == SG_SHAPE_EVERY_NEXT_CMP && d.n_out == 0 && !nd.no_fill;
   const int b_state = d.shape_args[1];
   w.ts = out->ts != nullptr;
   w.fill_ts = closed && w.ts;
@@ -298,45 +621,15 @@ Want want_of(const sg_node& nd, const sg_node_batch& b, const sg_match_columns* 
       w.col[k] = w.nul[k] = false;
     }
   }
-  for (int k = 0; k < w.ns; ++k)
-    if (nd.tag_sel[k] && (w.col[k] || w.nul[k])) {
-      w.tag[k] = true;
-      w.col[k] = true;   // (D2H of the tag into tagbuf)
-      w.nul[k] = false;
-    }
   w.any_fill = w.fill_ts;
-  for (int k = 0; k < w.ns; ++k) w.any_fill |= w.fill_col[k] >= 0 || w.tag[k];
+  for (int k = 0; k < w.ns; ++k) w.any_fill |= w.fill_col[k] >= 0;
   return w;
 }
 
 // Host selector for the trigger-row columns of output rows [o0, o1): trig[] holds their global trigger indices.
 inline void fill_row(const sg_node_batch& b, const sg_nfa_desc& d, const Want& w, const sg_match_columns* out,
-                     int64_t o, uint64_t trig, const sg_node* nd = nullptr) {
+                     int64_t o, uint64_t trig) {
   const int64_t t = (int64_t)(trig - b.base_index);
-  if (nd && nd->tag_col >= 0) {   // e1's projected attribute through its row tag
-    const int c = nd->tag_col;
-    const int wc = sg_col_width(d.col_type[c]);
-    for (int k = 0; k < w.ns; ++k) {
-      if (!w.tag[k]) continue;
-      const uint32_t tag = nd->tagbuf.as<uint32_t>()[o];
-      const uint64_t g = trig - (uint64_t)(uint32_t)((uint32_t)trig - tag);   // e1 is at most 2^32 - 1 rows back
-      int64_t v = 0;
-      uint8_t nul = 0;
-      if (g >= b.base_index) {
-        const int64_t r = (int64_t)(g - b.base_index);
-        v = wc == 8 ? ((const int64_t*)b.cols[c])[r] : (int64_t)((const int32_t*)b.cols[c])[r];
-        nul = (b.nulls && b.nulls[c]) ? b.nulls[c][r] : 0;
-      } else if ((int64_t)g >= nd->hist_lo && (int64_t)g < nd->hist_lo + nd->hist_n) {
-        v = nd->hist[(size_t)((int64_t)g - nd->hist_lo)];
-        nul = nd->hist_nul.empty() ? 0 : nd->hist_nul[(size_t)((int64_t)g - nd->hist_lo)];
-      }
-      if (out->cols[k]) {
-        if (w.width[k] == 8) put<1>(&((int64_t*)out->cols[k])[o], v);
-        else put<1>(&((int32_t*)out->cols[k])[o], (int32_t)v);
-      }
-      if (out->nulls[k]) out->nulls[k][o] = nul;
-    }
-  }
   if (w.fill_ts) put<1>(&out->ts[o], b.ts[t]);
   for (int k = 0; k < w.ns; ++k) {
     const int c = w.fill_col[k];
@@ -375,15 +668,17 @@ struct Run {
   // per (chunk, shard): rows, key bound and local index of row 0 (fixed when the chunk is routed)
   std::vector<int64_t> rows_of, lbase_of;
   std::vector<int32_t> kb_of;
-  // device-dictionary mode, per (chunk, shard): the shard's key count before the chunk and the first rows of the
-  // keys the chunk introduced, in id order (G > 1: merged into node-wide first-seen ids)
-  std::vector<int64_t> kbase_of;
   // per chunk: timestamps travel as 32-bit offsets from ts_base_of[j] when the chunk spans less than 2^31 ms
   std::vector<int64_t> ts_base_of;
   std::vector<uint8_t> ts32_of;
-  std::vector<std::vector<uint32_t>> newf_of;
-  std::vector<uint8_t> shard_tmp;            // device-dictionary route, G > 1: each row's shard (0xff: every shard)
   double t_route = 0, t_merge = 0, t_gpu[MAX_GPUS] = {};
+  // GPU-side shard exchange (x_loop): per (chunk, GPU) send starts per shard and match bounds per slice (G + 1 each),
+  // new keys' first global rows; per GPU the chunks past each step
+  std::vector<int64_t> xst, xpc, xkbase;
+  std::vector<std::vector<uint64_t>> xnf;
+  int64_t xcounted[MAX_GPUS] = {}, xsent[MAX_GPUS] = {}, xused[MAX_GPUS] = {}, xnfp[MAX_GPUS] = {},
+          xpieced[MAX_GPUS] = {}, xmready[MAX_GPUS] = {}, xosent[MAX_GPUS] = {};
+  int64_t xids = 0;
   int64_t h2d_bytes = 0, d2h_bytes = 0;
 
   Run(sg_node& n, const sg_node_batch& bb, const sg_match_columns* o, int64_t c) : nd(n), b(bb), out(o), cap(c) {}
@@ -471,145 +766,9 @@ inline void put_ts(const Run& r, NodeStage& S, int64_t j, int64_t p, int64_t ts)
   else S.ts.as<int64_t>()[p] = ts;
 }
 
-// ---- device-dictionary mode: no key lookups on the host.  G = 1: nothing to do; G > 1: rows are scattered to
-// shard mix64(raw key) mod G (rows of stream -1 reach every shard), each GPU dictionary-encodes its own keys --
-// first-seen order inside a shard is the node's first-seen order restricted to it.
+// ---- device-dictionary mode, one GPU: no key lookups on the host (G > 1: the GPU-side shard exchange, x_loop)
 void route_chunk_dev(Run& r, int64_t j) {
-  sg_node& nd = r.nd;
-  const sg_nfa_desc& d = nd.desc;
-  const int G = nd.G;
-  const int slot = (int)(j % NODE_RING);
-  const int64_t lo = chunk_lo(r, j), hi = chunk_lo(r, j + 1), n = hi - lo;
-  if (G == 1) {
-    r.rows_of[j] = n;
-    return;
-  }
-  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, n / 65536 + 1));
-  auto slice = [&](int t, int64_t& a, int64_t& e) {
-    a = n * t / T;
-    e = n * (t + 1) / T;
-  };
-  const int32_t* stream = r.b.stream ? r.b.stream + lo : nullptr;
-  const int64_t* raw = r.b.raw_key + lo;
-  auto shard = [&](int64_t i) -> int {
-    return (stream && stream[i] < 0) ? -1 : (int)(sgr::mix64((uint64_t)raw[i]) % (uint64_t)G);
-  };
-  // pass 1: each row's shard (0xff: a clock-only row every shard gets) and the counts per (thread slice, shard)
-  std::vector<uint8_t>& sh = r.shard_tmp;
-  if ((int64_t)sh.size() < n) sh.resize((size_t)n);
-  std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(G, 0));
-  std::vector<int64_t> nbc(T, 0);
-  nd.pool->parallel_for(T, [&](int t) {
-    int64_t a, e;
-    slice(t, a, e);
-    int64_t* c = cnt[t].data();
-    int64_t bcast = 0;
-    for (int64_t i = a; i < e; ++i) {
-      const int x = shard(i);
-      sh[(size_t)i] = x >= 0 ? (uint8_t)x : (uint8_t)0xff;
-      if (x >= 0) ++c[x];
-      else ++bcast;
-    }
-    for (int q = 0; q < G; ++q) c[q] += bcast;
-    nbc[t] = bcast;
-  });
-  std::vector<std::vector<int64_t>> off(T, std::vector<int64_t>(G, 0));
-  for (int q = 0; q < G; ++q) {
-    int64_t o = 0;
-    for (int t = 0; t < T; ++t) {
-      off[t][q] = o;
-      o += cnt[t][q];
-    }
-    r.rows_of[j * G + q] = o;
-  }
-  const int nc = d.n_cols;
-  int need[SG_MAX_COLS] = {};
-  for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
-  const uint8_t* shp = sh.data();
-  // pass 2: column by column, each a tight loop over the slice's rows into the G shard streams (arrival order kept)
-  nd.pool->parallel_for(T, [&](int t) {
-    int64_t a, e;
-    slice(t, a, e);
-    if (nbc[t]) {   // a slice with clock-only rows: row by row, those rows to every shard
-      int64_t cur[MAX_GPUS];
-      for (int q = 0; q < G; ++q) cur[q] = off[t][q];
-      for (int64_t i = a; i < e; ++i) {
-        const int own = shp[i] == 0xff ? -1 : (int)shp[i];
-        for (int q = 0; q < G; ++q) {
-          if (own >= 0 && q != own) continue;
-          NodeStage& S = nd.stage[slot][q];
-          const int64_t p = cur[q]++;
-          put_ts(r, S, j, p, r.b.ts[lo + i]);
-          S.raw.as<int64_t>()[p] = raw[i];
-          if (stream) S.stream.as<int32_t>()[p] = stream[i];
-          S.gidx.as<uint64_t>()[p] = r.b.base_index + (uint64_t)(lo + i);
-          for (int c = 0; c < nc; ++c) {
-            if (!need[c] || !r.b.cols[c]) continue;
-            if (sg_col_width(d.col_type[c]) == 8) S.col[c].as<int64_t>()[p] = ((const int64_t*)r.b.cols[c])[lo + i];
-            else S.col[c].as<int32_t>()[p] = ((const int32_t*)r.b.cols[c])[lo + i];
-            if (r.b.nulls && r.b.nulls[c]) S.nul[c].as<uint8_t>()[p] = r.b.nulls[c][lo + i];
-          }
-        }
-      }
-      return;
-    }
-    auto scatter = [&](auto* const* dst, auto val) {
-      int64_t cur[MAX_GPUS];
-      for (int q = 0; q < G; ++q) cur[q] = off[t][q];
-      for (int64_t i = a; i < e; ++i) {
-        const int q = shp[i];
-        put<2>(&dst[q][cur[q]++], val(i));
-      }
-    };
-    const int64_t* ts = r.b.ts + lo;
-    if (r.ts32_of[j]) {
-      int32_t* dt[MAX_GPUS];
-      for (int q = 0; q < G; ++q) dt[q] = nd.stage[slot][q].ts32.as<int32_t>();
-      const int64_t tb = r.ts_base_of[j];
-      scatter(dt, [&](int64_t i) { return (int32_t)(ts[i] - tb); });
-    } else {
-      int64_t* dt[MAX_GPUS];
-      for (int q = 0; q < G; ++q) dt[q] = nd.stage[slot][q].ts.as<int64_t>();
-      scatter(dt, [&](int64_t i) { return ts[i]; });
-    }
-    {
-      int64_t* dr[MAX_GPUS];
-      for (int q = 0; q < G; ++q) dr[q] = nd.stage[slot][q].raw.as<int64_t>();
-      scatter(dr, [&](int64_t i) { return raw[i]; });
-    }
-    if (stream) {
-      int32_t* ds[MAX_GPUS];
-      for (int q = 0; q < G; ++q) ds[q] = nd.stage[slot][q].stream.as<int32_t>();
-      scatter(ds, [&](int64_t i) { return stream[i]; });
-    }
-    {
-      uint64_t* dg[MAX_GPUS];
-      for (int q = 0; q < G; ++q) dg[q] = nd.stage[slot][q].gidx.as<uint64_t>();
-      const uint64_t gb = r.b.base_index + (uint64_t)lo;
-      scatter(dg, [&](int64_t i) { return gb + (uint64_t)i; });
-    }
-    for (int c = 0; c < nc; ++c) {
-      if (!need[c] || !r.b.cols[c]) continue;
-      if (sg_col_width(d.col_type[c]) == 8) {
-        int64_t* dc[MAX_GPUS];
-        for (int q = 0; q < G; ++q) dc[q] = nd.stage[slot][q].col[c].as<int64_t>();
-        const int64_t* sc = (const int64_t*)r.b.cols[c] + lo;
-        scatter(dc, [&](int64_t i) { return sc[i]; });
-      } else {
-        int32_t* dc[MAX_GPUS];
-        for (int q = 0; q < G; ++q) dc[q] = nd.stage[slot][q].col[c].as<int32_t>();
-        const int32_t* sc = (const int32_t*)r.b.cols[c] + lo;
-        scatter(dc, [&](int64_t i) { return sc[i]; });
-      }
-      if (r.b.nulls && r.b.nulls[c]) {
-        uint8_t* dn[MAX_GPUS];
-        for (int q = 0; q < G; ++q) dn[q] = nd.stage[slot][q].nul[c].as<uint8_t>();
-        const uint8_t* sn = r.b.nulls[c] + lo;
-        scatter(dn, [&](int64_t i) { return sn[i]; });
-      }
-    }
-    std::atomic_thread_fence(std::memory_order_seq_cst);   // (streaming stores drained before the chunk is published)
-  });
+  r.rows_of[j] = chunk_lo(r, j + 1) - chunk_lo(r, j);
 }
 
 // ---- route (+ scatter) of chunk j into host slot j % NODE_RING --------------------------------------------------
@@ -784,7 +943,6 @@ sg_batch shard_batch(Run& r, int64_t j, int s, const void** cols, const uint8_t*
     for (int c = 0; c < d.n_cols; ++c) {
       cols[c] = (need[c] && r.b.cols[c]) ? (const char*)r.b.cols[c] + (size_t)sg_col_width(d.col_type[c]) * lo : nullptr;
       nuls[c] = (need[c] && r.b.nulls && r.b.nulls[c]) ? r.b.nulls[c] + lo : nullptr;
-      if (c == nd.tag_col) cols[c] = nuls[c] = nullptr;   // (tags are made in HBM)
       nul |= nuls[c] != nullptr;
     }
     sb.cols = cols;
@@ -827,7 +985,7 @@ void copy_loop(Run& r, int s) {
         HIPCHK(hipMemcpyAsync(nd.dts32[s][ds], t32, 4 * (size_t)sb.n, hipMemcpyHostToDevice, nd.cp[s]));
       }
       if (sb.n > 0 && nd.ddict == 1) {
-        const int64_t* rk = nd.G == 1 ? r.b.raw_key + chunk_lo(r, j) : nd.stage[j % NODE_RING][s].raw.as<int64_t>();
+        const int64_t* rk = r.b.raw_key + chunk_lo(r, j);   // (device dictionary: one GPU here)
         HIPCHK(hipMemcpyAsync(nd.draw[s][ds], rk, 8 * (size_t)sb.n, hipMemcpyHostToDevice, nd.cp[s]));
       }
       HIPCHK(hipEventRecord(nd.ev_copied[s][ds], nd.cp[s]));
@@ -844,11 +1002,6 @@ void copy_loop(Run& r, int s) {
 }
 
 // ---- per-GPU compute + deliver thread --------------------------------------------------------------------------
-__global__ void k_row_tags(uint32_t base, int64_t n, uint32_t* __restrict__ tag) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    tag[i] = base + (uint32_t)i;
-}
-
 __global__ void k_ts_widen(const int32_t* __restrict__ d, int64_t base, int64_t n, int64_t* __restrict__ ts) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     ts[i] = base + (int64_t)d[i];
@@ -916,8 +1069,8 @@ void gpu_loop(Run& r, int s) {
       dst.key = r.out->key;
       dst.grp = r.out->group;
       for (int c = 0; c < r.w.ns; ++c) {
-        dst.col[c] = r.w.tag[c] ? nd.tagbuf.p : r.out->cols[c];
-        dst.nul[c] = r.w.tag[c] ? nullptr : r.out->nulls[c];
+        dst.col[c] = r.out->cols[c];
+        dst.nul[c] = r.out->nulls[c];
       }
       dst.M = 0;
     } else {
@@ -952,29 +1105,18 @@ void gpu_loop(Run& r, int s) {
         bv.stream = sb.stream ? (const int32_t*)sp.stream : nullptr;
         bv.key = (const int32_t*)sp.key;
         bv.index = nullptr;
-        if (nd.tag_col >= 0) {   // row tags: event index mod 2^32, in place of the projected-only column
-          hipLaunchKernelGGL(k_row_tags, dim3((unsigned)std::min<int64_t>((sb.n + 255) / 256, 8192)), dim3(256), 0,
-                             h.stream, (uint32_t)(sb.base_index), sb.n, (uint32_t*)sp.col[nd.tag_col]);
-          HIPCHK(hipGetLastError());
-        }
         if (r.ts32_of[j]) {   // widen the 32-bit offsets into the slot's timestamp column
           hipLaunchKernelGGL(k_ts_widen, dim3((unsigned)std::min<int64_t>((sb.n + 255) / 256, 8192)), dim3(256), 0,
                              h.stream, (const int32_t*)nd.dts32[s][ds], r.ts_base_of[j], sb.n, (int64_t*)sp.ts);
           HIPCHK(hipGetLastError());
         }
         if (nd.ddict == 1) {   // dictionary-encode the chunk's raw keys on this GPU
-          const int64_t before = nd.kd[s].n_keys;
-          std::vector<uint32_t> nf;
-          kd_resolve(nd.kd[s], nd.draw[s][ds], bv.stream, sb.n, (int32_t*)sp.key, h.stream, nd.G > 1 ? &nf : nullptr);
+          kd_resolve(nd.kd[s], nd.draw[s][ds], bv.stream, sb.n, (int32_t*)sp.key, h.stream, nullptr);
           bv.key_bound = (int32_t)std::max<int64_t>(1, nd.kd[s].n_keys);
-          r.publish([&] {
-            r.kbase_of[j * nd.G + s] = before;
-            r.newf_of[j * nd.G + s].swap(nf);
-          });
         }
         for (int c = 0; c < nd.desc.n_cols; ++c) {
-          bv.cols.col[c] = (sb.cols[c] || c == nd.tag_col) ? sp.col[c] : nullptr;
-          bv.cols.nul[c] = (sb.nulls && sb.nulls[c] && c != nd.tag_col) ? (const uint8_t*)sp.nul[c] : nullptr;
+          bv.cols.col[c] = sb.cols[c] ? sp.col[c] : nullptr;
+          bv.cols.nul[c] = (sb.nulls && sb.nulls[c]) ? (const uint8_t*)sp.nul[c] : nullptr;
         }
         sg_push_view(h, bv, sb.n);
         k = h.out.n;
@@ -1020,24 +1162,6 @@ void merge_chunk(Run& r, int64_t j) {
     a[s] = j ? r.dlv_end[s][j - 1] : 0;
     e[s] = r.dlv_end[s][j];
     total += e[s] - a[s];
-  }
-  if (nd.ddict == 1) {
-    // node-wide first-seen ids of the keys chunk j introduced: every shard's new keys are in first-row order, so a
-    // k-way merge by global first row interleaves them
-    int64_t cur[MAX_GPUS] = {}, m[MAX_GPUS];
-    for (int s = 0; s < G; ++s) {
-      m[s] = (int64_t)r.newf_of[j * G + s].size();
-      if (m[s] > 0) nd.l2g[s].resize((size_t)(r.kbase_of[j * G + s] + m[s]));   // (kbase_of is unset without rows)
-    }
-    auto gfirst = [&](int s, int64_t q) { return nd.stage[slot][s].gidx.as<uint64_t>()[r.newf_of[j * G + s][q]]; };
-    while (true) {
-      int best = -1;
-      for (int s = 0; s < G; ++s)
-        if (cur[s] < m[s] && (best < 0 || gfirst(s, cur[s]) < gfirst(best, cur[best]))) best = s;
-      if (best < 0) break;
-      nd.l2g[best][r.kbase_of[j * G + best] + cur[best]] = (int32_t)nd.g_keys++;
-      ++cur[best];
-    }
   }
   if (r.out_rows + total > r.cap) throw SgError(SG_ECAPACITY, "node: more matches than the output capacity");
   if (total == 0) return;
@@ -1090,7 +1214,7 @@ void merge_chunk(Run& r, int64_t j) {
     auto gkey = [&](int s, int64_t p) -> int64_t {
       const int32_t lk = nd.ring[s].key.as<int32_t>()[p];
       if (lk < 0) return -1;
-      return nd.ddict == 1 ? (int64_t)nd.l2g[s][lk] : (int64_t)rt->l2d[s][lk];
+      return (int64_t)rt->l2d[s][lk];
     };
     for (int64_t o = o0[t]; o < o0[t + 1]; ++o) {
       int best = -1;
@@ -1139,18 +1263,8 @@ void fill_loop(Run& r) {
         const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, cnt / 65536 + 1));
         nd.pool->parallel_for(T, [&](int t) {
           const int64_t a = o0 + cnt * t / T, e = o0 + cnt * (t + 1) / T;
-          const int tc = nd.tag_col;
-          const bool pf = tc >= 0 && r.b.cols[tc];
-          const int wc = pf ? sg_col_width(nd.desc.col_type[tc]) : 8;
-          const uint32_t* tags = nd.tagbuf.as<uint32_t>();
-          constexpr int64_t D = 32;   // e1 rows are scattered over the last `within`: keep 32 of their lines in flight
           for (int64_t o = a; o < e; ++o) {
-            if (pf && o + D < e) {
-              const uint64_t tr = r.out->trigger[o + D];
-              const uint64_t g = tr - (uint64_t)(uint32_t)((uint32_t)tr - tags[o + D]);
-              if (g >= r.b.base_index) __builtin_prefetch((const char*)r.b.cols[tc] + (size_t)wc * (g - r.b.base_index));
-            }
-            fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o], &nd);
+            fill_row(r.b, nd.desc, r.w, r.out, o, r.out->trigger[o]);
           }
           std::atomic_thread_fence(std::memory_order_seq_cst);
         });
@@ -1184,6 +1298,491 @@ void merge_loop(Run& r) {
   });
 }
 
+// ---- GPU-side shard exchange: the per-push pipeline (G > 1, device dictionary) -----------------------------------
+bool use_xchg(const sg_node& nd) { return nd.G > 1 && nd.ddict == 1; }
+
+XSpec xspec_of(const sg_node& nd, const sg_node_batch& b) {
+  const sg_nfa_desc& d = nd.desc;
+  XSpec sp;
+  memset(&sp, 0, sizeof(sp));
+  sp.ncols = d.n_cols;
+  sp.stream = b.stream ? 1 : 0;
+  int need[SG_MAX_COLS] = {};
+  for (int k = 0; k < d.n_ret; ++k) need[d.ret_col[k]] = 1;
+  for (int c = 0; c < d.n_cols; ++c) {
+    if (!need[c] || !b.cols || !b.cols[c]) continue;
+    sp.width[c] = sg_col_width(d.col_type[c]);
+    sp.nul[c] = (b.nulls && b.nulls[c]) ? 1 : 0;
+  }
+  return sp;
+}
+
+// one slice of chunk j: rows [a, e) of the caller's batch
+void x_slice(const Run& r, int64_t j, int g, int64_t& a, int64_t& e) {
+  const int64_t lo = chunk_lo(r, j), n = chunk_lo(r, j + 1) - lo;
+  a = lo + n * g / r.nd.G;
+  e = lo + n * (g + 1) / r.nd.G;
+}
+
+void xcopy(void* dst, int ddev, const void* src, int sdev, size_t bytes, hipStream_t st) {
+  if (!bytes) return;
+  if (ddev == sdev) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemcpyPeerAsync(dst, ddev, src, sdev, bytes, st));
+}
+
+// H2D of GPU g's slice of chunk j into its ingress slot j & 1 (copy stream)
+void x_upload(Run& r, int g, int64_t j, const XSpec& sp) {
+  sg_node& nd = r.nd;
+  XGpu& X = nd.x[g];
+  const int p = (int)(j & 1);
+  int64_t a, e;
+  x_slice(r, j, g, a, e);
+  const int64_t n = e - a;
+  if (j >= 2) HIPCHK(hipStreamWaitEvent(nd.cp[g], X.ev_scat[p], 0));   // the slot's last rows were scattered
+  const XCols& c = X.in[p].c;
+  int64_t bytes = 0;
+  auto up = [&](void* dst, const void* src, size_t w) {
+    if (!n) return;
+    HIPCHK(hipMemcpyAsync(dst, (const char*)src + w * (size_t)a, w * (size_t)n, hipMemcpyHostToDevice, nd.cp[g]));
+    bytes += (int64_t)(w * (size_t)n);
+  };
+  up(c.ts, r.b.ts, 8);
+  up(c.raw, r.b.raw_key, 8);
+  if (sp.stream) up(c.stream, r.b.stream, 4);
+  for (int k = 0; k < sp.ncols; ++k) {
+    if (sp.width[k]) up(c.col[k], r.b.cols[k], (size_t)sp.width[k]);
+    if (sp.nul[k]) up(c.nul[k], r.b.nulls[k], 1);
+  }
+  HIPCHK(hipEventRecord(X.ev_in[p], nd.cp[g]));
+  std::lock_guard<std::mutex> lk(r.mu);
+  r.h2d_bytes += bytes;
+}
+
+XLay xlay(char* base, const ColLayout& L) {
+  XLay x;
+  x.base = base;
+  x.off_trig = L.off_trig;
+  x.off_ts = L.off_ts;
+  x.off_key = L.off_key;
+  x.off_grp = L.off_grp;
+  for (int k = 0; k < SG_MAX_SELECT; ++k) {
+    x.off_col[k] = k < L.ns ? L.off_col[k] : 0;
+    x.off_nul[k] = k < L.ns ? L.off_nul[k] : 0;
+  }
+  return x;
+}
+
+XWant xwant(const Want& w, const ColLayout& L) {
+  XWant x;
+  memset(&x, 0, sizeof(x));
+  x.ts = w.ts;
+  x.key = w.key;
+  x.grp = w.grp;
+  x.ns = L.ns;
+  for (int k = 0; k < L.ns; ++k) {
+    x.width[k] = w.col[k] ? L.width[k] : 0;
+    x.nul[k] = w.nul[k] ? 1 : 0;
+  }
+  return x;
+}
+
+// device buffers of every GPU for chunks of C rows (before the pipeline's threads start)
+void x_reserve(Run& r, const XSpec& sp) {
+  sg_node& nd = r.nd;
+  const int G = nd.G;
+  const int64_t C = r.C, S = C / G + 1;
+  const int64_t nblk = (S + XB_ROWS - 1) / XB_ROWS;
+  for (int g = 0; g < G; ++g) {
+    XGpu& X = nd.x[g];
+    SgHandle& h = nd.h[g]->h;
+    HIPCHK(hipSetDevice(nd.dev[g]));
+    if (!X.init) {
+      HIPCHK(hipStreamCreateWithFlags(&X.xs, hipStreamNonBlocking));
+      for (hipEvent_t* e : {X.ev_in, X.ev_scat, X.ev_sent, X.ev_rfree, X.ev_osent, X.ev_mfree, X.ev_d2h})
+        for (int p = 0; p < 2; ++p) HIPCHK(hipEventCreateWithFlags(&e[p], hipEventDisableTiming));
+      X.init = true;
+    }
+    for (int p = 0; p < 2; ++p) {
+      xrows_layout(X.in[p], S, sp, false);
+      xrows_layout(X.send[p], S, sp, true);
+    }
+    X.shard.ensure((size_t)S);
+    X.bcnt.ensure(4 * (size_t)(G * nblk + 1));
+    X.boff.ensure(4 * (size_t)(G * nblk + 1));
+    X.starts.ensure(4 * (MAX_GPUS + 1));
+    X.bounds.ensure(8 * (MAX_GPUS + 1));
+    X.mcnt.ensure(4 * (size_t)(S + 1));
+    X.mseg.ensure(4 * (size_t)(S + 1));
+    X.moff.ensure(4 * (size_t)(S + 1));
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, X.bcnt.as<uint32_t>(), X.boff.as<uint32_t>(), (uint32_t)0,
+                                   (size_t)(G * nblk + 1), rocprim::plus<uint32_t>(), h.stream));
+    X.scan_tmp.ensure(tb);
+    tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, X.mcnt.as<uint32_t>(), X.moff.as<uint32_t>(), (uint32_t)0, (size_t)(S + 1),
+                                   rocprim::plus<uint32_t>(), h.stream));
+    X.mscan_tmp.ensure(tb);
+    for (int p = 0; p < 2; ++p) X.hstarts[p].ensure(8 * (MAX_GPUS + 1));
+    X.hbounds.ensure(8 * (MAX_GPUS + 1));
+    // receive slots: a shard may get every row of a chunk
+    sg_batch sb;
+    memset(&sb, 0, sizeof(sb));
+    const void* cols[SG_MAX_COLS] = {};
+    const uint8_t* nuls[SG_MAX_COLS] = {};
+    static const char dummy[1] = {0};
+    sb.ts = (const int64_t*)dummy;
+    sb.key = (const int32_t*)dummy;
+    sb.index = (const uint64_t*)dummy;
+    sb.stream = sp.stream ? (const int32_t*)dummy : nullptr;
+    bool nul = false;
+    for (int c = 0; c < sp.ncols; ++c) {
+      cols[c] = sp.width[c] ? dummy : nullptr;
+      nuls[c] = sp.nul[c] ? (const uint8_t*)dummy : nullptr;
+      nul |= nuls[c] != nullptr;
+    }
+    sb.cols = cols;
+    sb.nulls = nul ? nuls : nullptr;
+    for (int p = 0; p < 2; ++p) nd.dslot[g][p] = sg_reserve_slot(h, &sb, C, p);
+    if (nd.draw_rows < C)
+      for (int p = 0; p < 2; ++p) {
+        if (nd.draw[g][p]) HIPCHK(hipFree(nd.draw[g][p]));
+        nd.draw[g][p] = nullptr;
+        HIPCHK(hipMalloc((void**)&nd.draw[g][p], (size_t)C * 8));
+      }
+    HIPCHK(hipStreamSynchronize(h.stream));
+    sg_egress_init(h);
+    const int64_t eb = (int64_t)sg_col_layout(h.desc, std::max<int64_t>(1, std::min<int64_t>(S, r.cap))).bytes;
+    sg_stage_reserve(h, 0, eb);
+    sg_stage_reserve(h, 1, eb);
+  }
+  nd.draw_rows = std::max(nd.draw_rows, C);
+}
+
+// merge input / output slot p of GPU g for m rows (waits for the slot's earlier users first)
+void x_merge_room(sg_node& nd, int g, int p, int64_t m, bool out_slot) {
+  XGpu& X = nd.x[g];
+  int64_t& cap = out_slot ? X.mo_cap[p] : X.min_cap[p];
+  if (m <= cap && cap > 0) return;
+  const int64_t c = std::max<int64_t>({m + m / 4, 1024, cap});
+  HIPCHK(hipEventSynchronize(out_slot ? X.ev_d2h[p] : X.ev_mfree[p]));
+  (out_slot ? X.mo[p] : X.min[p]).ensure(sg_col_layout(nd.h[g]->h.desc, c).bytes);
+  cap = c;
+}
+
+void x_loop(Run& r, int g, XSpec sp) {
+  sg_node& nd = r.nd;
+  XGpu& X = nd.x[g];
+  SgHandle& h = nd.h[g]->h;
+  const int G = nd.G;
+  const sg_nfa_desc& d = nd.desc;
+  const Want& w = r.w;
+  auto all_gt = [&](const int64_t* v, int64_t j) {
+    for (int q = 0; q < G; ++q)
+      if (v[q] <= j) return false;
+    return true;
+  };
+  r.guarded([&] {
+    HIPCHK(hipSetDevice(nd.dev[g]));
+    int64_t out_before = 0;   // matches of the chunks before this one, node-wide
+    for (int64_t j = 0; j < r.nch; ++j) {
+      const double t0 = now_ms();
+      const int p = (int)(j & 1);
+      if (j == 0) x_upload(r, g, 0, sp);
+      if (j + 1 < r.nch) x_upload(r, g, j + 1, sp);   // (slot (j + 1) & 1 held chunk j - 1, scattered already)
+      int64_t a, e;
+      x_slice(r, j, g, a, e);
+      const int64_t n = e - a;
+      const int64_t nblk = (n + XB_ROWS - 1) / XB_ROWS;
+      // ---- shard of every row, counts per (block, shard), send offsets
+      HIPCHK(hipStreamWaitEvent(h.stream, X.ev_in[p], 0));
+      uint32_t* hst = X.hstarts[p].as<uint32_t>();
+      if (n > 0) {
+        HIPCHK(hipMemsetAsync(X.bcnt.as<uint32_t>() + G * nblk, 0, 4, h.stream));
+        hipLaunchKernelGGL(k_xcount, dim3((unsigned)nblk), dim3(256), 0, h.stream, X.in[p].c.raw, X.in[p].c.stream, n,
+                           (uint32_t)G, X.shard.as<uint8_t>(), X.bcnt.as<uint32_t>(), (uint32_t)nblk);
+        HIPCHK(hipGetLastError());
+        size_t tb = X.scan_tmp.bytes;
+        HIPCHK(rocprim::exclusive_scan(X.scan_tmp.p, tb, X.bcnt.as<uint32_t>(), X.boff.as<uint32_t>(), (uint32_t)0,
+                                       (size_t)(G * nblk + 1), rocprim::plus<uint32_t>(), h.stream));
+        hipLaunchKernelGGL(k_xstarts, dim3(1), dim3(64), 0, h.stream, X.boff.as<uint32_t>(), (uint32_t)nblk, (uint32_t)G,
+                           X.starts.as<uint32_t>());
+        HIPCHK(hipMemcpyAsync(hst, X.starts.p, 4 * (size_t)(G + 1), hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipStreamSynchronize(h.stream));
+        hipLaunchKernelGGL(k_xscatter, dim3((unsigned)nblk), dim3(256), 0, h.stream, X.in[p].c, X.send[p].c, sp, n,
+                           r.b.base_index + (uint64_t)a, X.shard.as<uint8_t>(), X.boff.as<uint32_t>(), (uint32_t)nblk,
+                           (uint32_t)G);
+        HIPCHK(hipGetLastError());
+      } else {
+        for (int s = 0; s <= G; ++s) hst[s] = 0;
+      }
+      HIPCHK(hipEventRecord(X.ev_scat[p], h.stream));
+      r.publish([&] {
+        for (int s = 0; s <= G; ++s) r.xst[(size_t)(j * G + g) * (G + 1) + s] = hst[s];
+        r.xcounted[g] = j + 1;
+      });
+      // ---- rows to their shards: piece (g -> s) lands after the pieces of slices 0 .. g-1
+      if (!r.wait([&] {
+            if (!all_gt(r.xcounted, j)) return false;
+            if (j < 2) return true;
+            for (int s = 0; s < G; ++s)
+              if (r.xused[s] < j - 1) return false;   // shard s consumed chunk j - 2 from its receive slot p
+            return true;
+          }))
+        return;
+      auto cnt_of = [&](int src, int s) {
+        const int64_t* q = &r.xst[(size_t)(j * G + src) * (G + 1)];
+        return q[s + 1] - q[s];
+      };
+      HIPCHK(hipStreamWaitEvent(X.xs, X.ev_scat[p], 0));
+      for (int s = 0; s < G; ++s) {
+        const int64_t c = cnt_of(g, s);
+        if (!c) continue;
+        int64_t ro = 0;
+        for (int q = 0; q < g; ++q) ro += cnt_of(q, s);
+        const int64_t so = r.xst[(size_t)(j * G + g) * (G + 1) + s];
+        if (j >= 2) HIPCHK(hipStreamWaitEvent(X.xs, nd.x[s].ev_rfree[p], 0));
+        const SlotPtrs& rs = nd.dslot[s][p];
+        const XCols& sc = X.send[p].c;
+        const int ds = nd.dev[s], dg = nd.dev[g];
+        xcopy((int64_t*)rs.ts + ro, ds, sc.ts + so, dg, 8 * (size_t)c, X.xs);
+        xcopy(nd.draw[s][p] + ro, ds, sc.raw + so, dg, 8 * (size_t)c, X.xs);
+        xcopy((uint64_t*)rs.index + ro, ds, sc.gidx + so, dg, 8 * (size_t)c, X.xs);
+        if (sp.stream) xcopy((int32_t*)rs.stream + ro, ds, sc.stream + so, dg, 4 * (size_t)c, X.xs);
+        for (int k = 0; k < sp.ncols; ++k) {
+          if (sp.width[k])
+            xcopy((char*)rs.col[k] + (size_t)sp.width[k] * ro, ds, (const char*)sc.col[k] + (size_t)sp.width[k] * so, dg,
+                  (size_t)sp.width[k] * c, X.xs);
+          if (sp.nul[k]) xcopy((uint8_t*)rs.nul[k] + ro, ds, sc.nul[k] + so, dg, (size_t)c, X.xs);
+        }
+      }
+      HIPCHK(hipEventRecord(X.ev_sent[p], X.xs));
+      r.publish([&] { r.xsent[g] = j + 1; });
+      // ---- shard g: its rows of chunk j, arrival order, global indices as triggers
+      if (!r.wait([&] { return all_gt(r.xsent, j); })) return;
+      int64_t ns = 0;
+      for (int q = 0; q < G; ++q) {
+        ns += cnt_of(q, g);
+        HIPCHK(hipStreamWaitEvent(h.stream, nd.x[q].ev_sent[p], 0));
+      }
+      const SlotPtrs& sl = nd.dslot[g][p];
+      int64_t kbefore = nd.kd[g].n_keys, mnew = 0;
+      if (ns > 0) {
+        mnew = kd_resolve(nd.kd[g], nd.draw[g][p], sp.stream ? (const int32_t*)sl.stream : nullptr, ns,
+                          (int32_t*)sl.key, h.stream, nullptr);
+        if (w.key && mnew > 0) {   // global first rows of the new keys (node-wide first-seen ids)
+          X.nfg.ensure(8 * (size_t)mnew);
+          X.hnf.ensure(8 * (size_t)mnew);
+          hipLaunchKernelGGL(k_xgather_u64, dim3((unsigned)((mnew + 255) / 256)), dim3(256), 0, h.stream,
+                             (const uint64_t*)sl.index, nd.kd[g].sfirst, mnew, X.nfg.as<uint64_t>());
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipMemcpyAsync(X.hnf.p, X.nfg.p, 8 * (size_t)mnew, hipMemcpyDeviceToHost, h.stream));
+          HIPCHK(hipStreamSynchronize(h.stream));
+        }
+        BatchView bv;
+        memset(&bv, 0, sizeof(bv));
+        bv.n = ns;
+        bv.base_index = 0;
+        bv.key_bound = (int32_t)std::max<int64_t>(1, nd.kd[g].n_keys);
+        bv.ts = (const int64_t*)sl.ts;
+        bv.stream = sp.stream ? (const int32_t*)sl.stream : nullptr;
+        bv.key = (const int32_t*)sl.key;
+        bv.index = (const uint64_t*)sl.index;
+        for (int k = 0; k < sp.ncols; ++k) {
+          bv.cols.col[k] = sp.width[k] ? sl.col[k] : nullptr;
+          bv.cols.nul[k] = sp.nul[k] ? (const uint8_t*)sl.nul[k] : nullptr;
+        }
+        sg_push_view(h, bv, ns);
+      }
+      HIPCHK(hipEventRecord(X.ev_rfree[p], h.stream));
+      r.publish([&] {
+        r.xused[g] = j + 1;
+        nd.local_rows[g] += ns;
+        if (w.key) {
+          r.xnf[(size_t)(j * G + g)].assign(X.hnf.as<uint64_t>(), X.hnf.as<uint64_t>() + (mnew > 0 ? mnew : 0));
+          r.xkbase[(size_t)(j * G + g)] = kbefore;
+          r.xnfp[g] = j + 1;
+        }
+      });
+      // ---- node-wide first-seen key ids (only when the caller wants keys): the shards' new keys interleaved by
+      // their first global row; GPU 0's thread assigns them for everyone
+      if (w.key) {
+        if (g == 0) {
+          if (!r.wait([&] { return all_gt(r.xnfp, j); })) return;
+          int64_t cur[MAX_GPUS] = {}, m[MAX_GPUS];
+          for (int s = 0; s < G; ++s) {
+            m[s] = (int64_t)r.xnf[(size_t)(j * G + s)].size();
+            if (m[s] > 0) nd.l2g[s].resize((size_t)(r.xkbase[(size_t)(j * G + s)] + m[s]));
+          }
+          while (true) {
+            int best = -1;
+            for (int s = 0; s < G; ++s)
+              if (cur[s] < m[s] && (best < 0 || r.xnf[(size_t)(j * G + s)][cur[s]] < r.xnf[(size_t)(j * G + best)][cur[best]]))
+                best = s;
+            if (best < 0) break;
+            nd.l2g[best][(size_t)(r.xkbase[(size_t)(j * G + best)] + cur[best])] = (int32_t)nd.g_keys++;
+            ++cur[best];
+          }
+          r.publish([&] { r.xids = j + 1; });
+        }
+        if (!r.wait([&] { return r.xids > j; })) return;
+        const int64_t nk = (int64_t)nd.l2g[g].size();
+        if (nk > X.l2g_n) {
+          if ((size_t)nk * 4 > X.l2g.bytes) {
+            HIPCHK(hipStreamSynchronize(h.stream));
+            XBuf nb;
+            nb.ensure((size_t)(nk + nk / 2 + 1024) * 4);
+            if (X.l2g_n) HIPCHK(hipMemcpy(nb.p, X.l2g.p, 4 * (size_t)X.l2g_n, hipMemcpyDeviceToDevice));
+            X.l2g.release();
+            X.l2g = nb;
+            nb.p = nullptr;
+          }
+          HIPCHK(hipMemcpyAsync(X.l2g.as<int32_t>() + X.l2g_n, nd.l2g[g].data() + X.l2g_n, 4 * (size_t)(nk - X.l2g_n),
+                                hipMemcpyHostToDevice, h.stream));
+          HIPCHK(hipStreamSynchronize(h.stream));
+          X.l2g_n = nk;
+        }
+      }
+      // ---- its matches -> SoA columns in egress slot p, cut by trigger slice
+      const int64_t k = h.out.n;
+      ColLayout L = sg_col_layout(d, std::max<int64_t>(k, 1));
+      int64_t* hb = X.hbounds.as<int64_t>();
+      if (k > 0) {
+        sg_stage_reserve(h, p, (int64_t)L.bytes);
+        HIPCHK(hipStreamWaitEvent(h.stream, h.eg.done[p], 0));
+        sg_launch_to_columns(k, h.out.rec, h.out.stride, L, h.eg.stage[p], h.stream);
+        h.out.n = 0;
+        if (w.key)
+          hipLaunchKernelGGL(k_xmapkeys, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, h.stream,
+                             (int32_t*)(h.eg.stage[p] + L.off_key), k, X.l2g.as<int32_t>());
+        XSlices xs;
+        for (int q = 0; q <= G; ++q) {
+          int64_t qa, qe;
+          x_slice(r, j, q < G ? q : G - 1, qa, qe);
+          xs.lo[q] = r.b.base_index + (uint64_t)(q < G ? qa : qe);
+        }
+        hipLaunchKernelGGL(k_xbounds, dim3(1), dim3(64), 0, h.stream, (const uint64_t*)(h.eg.stage[p] + L.off_trig), k, xs,
+                           (uint32_t)G, X.bounds.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(hb, X.bounds.p, 8 * (size_t)(G + 1), hipMemcpyDeviceToHost, h.stream));
+        HIPCHK(hipEventRecord(h.eg.ready[p], h.stream));
+        HIPCHK(hipStreamSynchronize(h.stream));
+      } else {
+        for (int q = 0; q <= G; ++q) hb[q] = 0;
+      }
+      r.publish([&] {
+        for (int q = 0; q <= G; ++q) r.xpc[(size_t)(j * G + g) * (G + 1) + q] = hb[q];
+        r.xpieced[g] = j + 1;
+      });
+      auto piece = [&](int s, int q) {
+        const int64_t* b2 = &r.xpc[(size_t)(j * G + s) * (G + 1)];
+        return b2[q + 1] - b2[q];
+      };
+      // ---- slice owner g: room for the matches of its triggers
+      if (!r.wait([&] { return all_gt(r.xpieced, j); })) return;
+      int64_t mg = 0, chunk_total = 0, before_g = 0;
+      for (int s = 0; s < G; ++s) mg += piece(s, g);
+      for (int q = 0; q < G; ++q)
+        for (int s = 0; s < G; ++s) {
+          chunk_total += piece(s, q);
+          if (q < g) before_g += piece(s, q);
+        }
+      if (out_before + chunk_total > r.cap) throw SgError(SG_ECAPACITY, "node: more matches than the output capacity");
+      if (mg > 0) x_merge_room(nd, g, p, mg, false);
+      r.publish([&] { r.xmready[g] = j + 1; });
+      // ---- shard g: piece (g -> q) into owner q's merge input after the pieces of shards 0 .. g-1
+      if (!r.wait([&] { return all_gt(r.xmready, j); })) return;
+      if (k > 0) {
+        HIPCHK(hipStreamWaitEvent(X.xs, h.eg.ready[p], 0));
+        for (int q = 0; q < G; ++q) {
+          const int64_t c = piece(g, q);
+          if (!c) continue;
+          int64_t ro = 0;
+          for (int s = 0; s < g; ++s) ro += piece(s, q);
+          XGpu& Q = nd.x[q];
+          if (j >= 2) HIPCHK(hipStreamWaitEvent(X.xs, Q.ev_mfree[p], 0));   // owner q merged chunk j - 2
+          const ColLayout Lq = sg_col_layout(d, Q.min_cap[p]);
+          char* dst = Q.min[p].as<char>();
+          const char* src = h.eg.stage[p];
+          const int64_t sr = r.xpc[(size_t)(j * G + g) * (G + 1) + q];
+          const int dq = nd.dev[q], dg = nd.dev[g];
+          auto col = [&](size_t doff, size_t soff, size_t wd) {
+            xcopy(dst + doff + wd * (size_t)ro, dq, src + soff + wd * (size_t)sr, dg, wd * (size_t)c, X.xs);
+          };
+          col(Lq.off_trig, L.off_trig, 8);
+          if (w.ts) col(Lq.off_ts, L.off_ts, 8);
+          if (w.key) col(Lq.off_key, L.off_key, 4);
+          if (w.grp) col(Lq.off_grp, L.off_grp, 4);
+          for (int c2 = 0; c2 < L.ns; ++c2) {
+            if (w.col[c2]) col(Lq.off_col[c2], L.off_col[c2], (size_t)L.width[c2]);
+            if (w.nul[c2]) col(Lq.off_nul[c2], L.off_nul[c2], 1);
+          }
+        }
+        HIPCHK(hipEventRecord(h.eg.done[p], X.xs));
+      }
+      HIPCHK(hipEventRecord(X.ev_osent[p], X.xs));
+      r.publish([&] { r.xosent[g] = j + 1; });
+      // ---- owner g: merge the G runs by trigger, then straight into the caller's columns
+      if (!r.wait([&] { return all_gt(r.xosent, j); })) return;
+      for (int q = 0; q < G; ++q) HIPCHK(hipStreamWaitEvent(h.stream, nd.x[q].ev_osent[p], 0));
+      const int64_t o0 = out_before + before_g;
+      if (mg > 0) {
+        x_merge_room(nd, g, p, mg, true);
+        int64_t sa, se;
+        x_slice(r, j, g, sa, se);
+        const int64_t nsl = se - sa;
+        const uint64_t slo = r.b.base_index + (uint64_t)sa;
+        XRuns runs;
+        runs.off[0] = 0;
+        for (int s = 0; s < G; ++s) runs.off[s + 1] = runs.off[s] + piece(s, g);
+        HIPCHK(hipMemsetAsync(X.mcnt.p, 0, 4 * (size_t)(nsl + 1), h.stream));
+        const ColLayout Li = sg_col_layout(d, X.min_cap[p]), Lo = sg_col_layout(d, X.mo_cap[p]);
+        const XLay li = xlay(X.min[p].as<char>(), Li), lo = xlay(X.mo[p].as<char>(), Lo);
+        hipLaunchKernelGGL(k_xmark, dim3((unsigned)((mg + 255) / 256)), dim3(256), 0, h.stream,
+                           (const uint64_t*)(li.base + li.off_trig), mg, runs, (uint32_t)G, slo, X.mcnt.as<uint32_t>(),
+                           X.mseg.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+        size_t tb = X.mscan_tmp.bytes;
+        HIPCHK(rocprim::exclusive_scan(X.mscan_tmp.p, tb, X.mcnt.as<uint32_t>(), X.moff.as<uint32_t>(), (uint32_t)0,
+                                       (size_t)(nsl + 1), rocprim::plus<uint32_t>(), h.stream));
+        HIPCHK(hipStreamWaitEvent(h.stream, X.ev_d2h[p], 0));   // the output slot's last copies are done
+        hipLaunchKernelGGL(k_xplace, dim3((unsigned)((mg + 255) / 256)), dim3(256), 0, h.stream, li, mg, slo,
+                           X.moff.as<uint32_t>(), X.mseg.as<uint32_t>(), lo, xwant(w, Lo));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(X.ev_mfree[p], h.stream));
+        HIPCHK(hipStreamWaitEvent(h.eg.d2h, X.ev_mfree[p], 0));
+        int64_t bytes = 0;
+        auto down = [&](void* dst, size_t off, size_t wd) {
+          if (!dst) return;
+          HIPCHK(hipMemcpyAsync((char*)dst + wd * (size_t)o0, lo.base + off, wd * (size_t)mg, hipMemcpyDeviceToHost,
+                                h.eg.d2h));
+          bytes += (int64_t)(wd * (size_t)mg);
+        };
+        down(r.out->trigger, Lo.off_trig, 8);
+        if (w.ts) down(r.out->ts, Lo.off_ts, 8);
+        if (w.key) down(r.out->key, Lo.off_key, 4);
+        if (w.grp) down(r.out->group, Lo.off_grp, 4);
+        for (int c2 = 0; c2 < Lo.ns; ++c2) {
+          if (w.col[c2]) down(r.out->cols[c2], Lo.off_col[c2], (size_t)Lo.width[c2]);
+          if (w.nul[c2]) down(r.out->nulls[c2], Lo.off_nul[c2], 1);
+        }
+        HIPCHK(hipEventRecord(X.ev_d2h[p], h.eg.d2h));
+        std::lock_guard<std::mutex> lk(r.mu);
+        r.d2h_bytes += bytes;
+      } else {
+        HIPCHK(hipEventRecord(X.ev_mfree[p], h.stream));
+      }
+      out_before += chunk_total;
+      r.publish([&] {
+        r.t_gpu[g] += now_ms() - t0;
+        if (g == 0) r.out_rows = out_before;
+      });
+    }
+    HIPCHK(hipStreamSynchronize(h.stream));
+    HIPCHK(hipStreamSynchronize(X.xs));
+    HIPCHK(hipStreamSynchronize(h.eg.d2h));
+  });
+}
+
 void reserve_all(Run& r) {
   sg_node& nd = r.nd;
   const sg_nfa_desc& d = nd.desc;
@@ -1203,7 +1802,6 @@ void reserve_all(Run& r) {
         S.key.ensure((size_t)C * 4);
         S.gidx.ensure((size_t)C * 8);
         S.ts32.ensure((size_t)C * 4);
-        if (nd.ddict == 1) S.raw.ensure((size_t)C * 8);
         if (r.b.stream || need_clocks(d)) S.stream.ensure((size_t)C * 4);
         for (int c = 0; c < d.n_cols; ++c) {
           if (!need[c] || !r.b.cols[c]) continue;
@@ -1255,7 +1853,6 @@ void reserve_all(Run& r) {
     sg_stage_reserve(h, 1, eb);
   }
   if (nd.ddict == 1) nd.draw_rows = std::max(nd.draw_rows, C);
-  if (nd.tag_col >= 0) nd.tagbuf.ensure((size_t)std::max<int64_t>(r.cap, 1) * 4);
   nd.dts32_rows = std::max(nd.dts32_rows, C);
   // shard rings: room for two chunks' worth of matches per shard beyond the share of the output capacity
   if (nd.G > 1) {
@@ -1275,54 +1872,18 @@ void reserve_all(Run& r) {
   }
 }
 
-void keep_history(sg_node& nd, const sg_node_batch& b);
-
-// Switch the row tags on or off for a new stream: the GPU handles are reopened with the tag column as INT (or as the
-// query declares it).
-void set_tags(sg_node& nd, bool on) {
-  if ((nd.tag_col >= 0) == on) return;
-  const sg_nfa_desc* dd = &nd.desc;
-  nd.edesc = nd.desc;
-  for (int k = 0; k < SG_MAX_SELECT; ++k) nd.tag_sel[k] = false;
-  if (on) {
-    const int c = nd.tag_cand;
-    nd.edesc.col_type[c] = SG_T_INT;
-    for (int k = 0; k < nd.desc.n_ret; ++k)
-      if (nd.desc.ret_col[k] == c) nd.edesc.ret_type[k] = SG_T_INT;
-    for (int k = 0; k < nd.desc.n_select; ++k)
-      if (nd.desc.ret_col[nd.desc.sel_ret[k]] == c) {
-        nd.edesc.sel_type[k] = SG_T_INT;
-        nd.tag_sel[k] = nd.desc.sel_state[k] == nd.desc.shape_args[0];
-      }
-    dd = &nd.edesc;
-  }
-  for (int s = 0; s < nd.G; ++s) {
-    HIPCHK(hipSetDevice(nd.dev[s]));
-    if (nd.h[s]) sg_close(nd.h[s]);
-    nd.h[s] = nullptr;
-    const int rc = sg_open(nd.dev[s], dd, &nd.opt, &nd.h[s]);
-    if (rc != SG_OK) throw SgError(rc, "node: reopening the GPU handle failed");
-  }
-  nd.tag_col = on ? nd.tag_cand : -1;
-  nd.hist_n = 0;
-}
-
 // Auto key dictionary: keys are encoded on the GPUs whenever the query allows it (partitioned, no playback clocks).
 // Measured on C2 (100M events, 10k keys, one GPU, profiles/r03/whole_node_*_dict.log): the host router's lookups were
 // the pipeline's bound (route 50 ms of 58.7 ms per push) even with a cache-resident table, while raw 8-byte keys cost
 // only 0.4 GB more H2D (route 13 ms, 48.8 ms per push); with 1M keys (C5) the host table is DRAM-bound as well.
 void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, int64_t cap, int64_t* n_out) {
-  if (nd.ddict < 0) {   // the first push of a stream fixes where keys are encoded, and whether rows carry tags
+  if (nd.ddict < 0) {   // the first push of a stream fixes where keys are encoded
     const bool dev_ok = nd.desc.partitioned && !need_clocks(nd.desc);
     nd.ddict = (dev_ok && nd.key_dict_mode != 1) ? 1 : 0;
-    // tags save PCIe bytes at the price of host selector work (random e1 reads): opt-in, SG_NODE_TAGS=1
-    const char* e = getenv("SG_NODE_TAGS");
-    const bool want = nd.tag_cand >= 0 && e && e[0] == '1';   // (measured: the host's e1 gathers cost more than
-                                                               // the PCIe bytes they save on this pool's hosts)
-    set_tags(nd, want);
   }
   Run r(nd, b, out, cap);
-  r.w = want_of(nd, b, out);
+  const bool xchg = use_xchg(nd);
+  r.w = want_of(nd, b, out, !xchg);
   // default chunks: ~16 per push (short pipeline fill and drain), 4M..25M rows each
   r.C = nd.chunk_rows > 0 ? nd.chunk_rows
                           : std::max<int64_t>(1, std::min<int64_t>(b.n, std::max<int64_t>((int64_t)4 << 20,
@@ -1333,22 +1894,31 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
   r.rows_of.assign((size_t)(r.nch * nd.G), 0);
   r.lbase_of.assign((size_t)(r.nch * nd.G), 0);
   r.kb_of.assign((size_t)(r.nch * nd.G), 1);
-  r.kbase_of.assign((size_t)(r.nch * nd.G), 0);
   r.ts_base_of.assign((size_t)r.nch, 0);
   r.ts32_of.assign((size_t)r.nch, 0);
-  r.newf_of.assign((size_t)(r.nch * nd.G), std::vector<uint32_t>());
   const double t0 = now_ms();
+  std::vector<std::shared_ptr<Task>> th;
+  ThreadCache& tc = pipeline_threads();
+  double t1 = 0;
+  if (xchg) {   // GPU-side shard exchange: one loop per GPU, no host route or merge
+    const int G = nd.G;
+    const XSpec sp = xspec_of(nd, b);
+    r.xst.assign((size_t)(r.nch * G * (G + 1)), 0);
+    r.xpc.assign((size_t)(r.nch * G * (G + 1)), 0);
+    r.xkbase.assign((size_t)(r.nch * G), 0);
+    r.xnf.assign((size_t)(r.nch * G), std::vector<uint64_t>());
+    x_reserve(r, sp);
+    t1 = now_ms();
+    for (int s = 0; s < G; ++s) th.push_back(tc.run([&r, s, sp] { x_loop(r, s, sp); }));
+  } else {
   reserve_all(r);
-  const double t_res = now_ms() - t0;
-  // local index bases of each shard's rows per chunk are fixed as chunks are routed
-  std::vector<std::thread> th;
+  t1 = now_ms();
   for (int s = 0; s < nd.G; ++s) {
-    th.emplace_back(copy_loop, std::ref(r), s);
-    th.emplace_back(gpu_loop, std::ref(r), s);
+    th.push_back(tc.run([&r, s] { copy_loop(r, s); }));
+    th.push_back(tc.run([&r, s] { gpu_loop(r, s); }));
   }
-  if (nd.G > 1) th.emplace_back(merge_loop, std::ref(r));
-  else if (r.w.any_fill) th.emplace_back(fill_loop, std::ref(r));
-  const double t1 = now_ms();
+  if (nd.G > 1) th.push_back(tc.run([&r] { merge_loop(r); }));
+  else if (r.w.any_fill) th.push_back(tc.run([&r] { fill_loop(r); }));
   r.guarded([&] {
     for (int64_t j = 0; j < r.nch; ++j) {
       // slot j % NODE_RING is free once chunk j - NODE_RING is uploaded everywhere (and merged: its gidx)
@@ -1371,7 +1941,9 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
       });
     }
   });
-  for (auto& t : th) t.join();
+  }
+  const double t_res = t1 - t0;
+  for (auto& t : th) t->join();
   for (int s = 0; s < nd.G; ++s) {
     hipSetDevice(nd.dev[s]);
     hipStreamSynchronize(nd.h[s]->h.stream);
@@ -1382,7 +1954,6 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
     nd.broken = true;
     throw SgError(r.fail_code, r.fail_msg);
   }
-  if (nd.tag_col >= 0) keep_history(nd, b);
   const double t2 = now_ms();
   sg_node_stats& st = nd.st;
   st.total_ms = t2 - t1;
@@ -1403,6 +1974,7 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
 void close_node(sg_node* nd) {
   for (int s = 0; s < nd->G; ++s) {
     hipSetDevice(nd->dev[s]);
+    nd->x[s].release();
     kd_free(nd->kd[s]);
     for (int k = 0; k < 2; ++k) {
       if (nd->draw[s][k]) hipFree(nd->draw[s][k]);
@@ -1416,89 +1988,7 @@ void close_node(sg_node* nd) {
     }
   }
   if (nd->router) sg_router_close(nd->router);
-  delete nd->pool;
   delete nd;
-}
-
-// The tag column of a closed-form query: the one batch column e1 contributes to the select besides the compared value
-// (LONG / INT), read by no predicate -- or -1.
-int tag_column(const sg_nfa_desc& d) {
-  if (d.shape != SG_SHAPE_EVERY_NEXT_CMP || d.n_out != 0) return -1;
-  const int a_state = d.shape_args[0];
-  const int val_a = d.ret_col[d.shape_args[4]], val_b = d.ret_col[d.shape_args[3]];
-  int c = -1;
-  for (int k = 0; k < d.n_select; ++k) {
-    if (d.sel_state[k] != a_state) continue;
-    const int col = d.ret_col[d.sel_ret[k]];
-    if (col == val_a) continue;
-    if (d.sel_index[k] != 0 && d.sel_index[k] != -1) return -1;
-    if (c >= 0 && c != col) return -1;
-    c = col;
-  }
-  if (c < 0 || c == val_b || (d.col_type[c] != SG_T_LONG && d.col_type[c] != SG_T_INT)) return -1;
-  auto reads = [&](int off, int len) {   // does a postfix program read column c?
-    for (int pc = off; pc < off + len;) {
-      const int64_t op = d.code[pc];
-      if (op == SG_OP_VAR) {
-        if (d.ret_col[d.code[pc + 3]] == c) return true;
-        pc += 5;
-      } else if (op == SG_OP_CONST || op == SG_OP_CMP || op == SG_OP_MATH) {
-        pc += 3;
-      } else {
-        pc += 1;
-      }
-    }
-    return false;
-  };
-  for (int s = 0; s < d.n_states; ++s)
-    if (reads(d.states[s].prog_off, d.states[s].prog_len)) return -1;
-  if (reads(d.shape_prog_off, d.shape_prog_len)) return -1;
-  return c;
-}
-
-// After a push: keep the tag column's values of the rows the engine still carries (the only earlier rows a later
-// match can name as e1): [push_end - lag, push_end) from the caller's columns and the previous history.
-void keep_history(sg_node& nd, const sg_node_batch& b) {
-  const int c = nd.tag_col;
-  const int64_t end = (int64_t)(b.base_index + (uint64_t)b.n);
-  HIPCHK(hipSetDevice(nd.dev[0]));
-  const int64_t lag = sg_every_next_carry_max_lag(&nd.h[0]->h, c, (uint32_t)end);
-  if (lag <= 0) {
-    nd.hist_n = 0;
-    return;
-  }
-  const int64_t lo = end - lag;
-  std::vector<int64_t> h((size_t)lag);
-  std::vector<uint8_t> hn;
-  const bool nul = (b.nulls && b.nulls[c]) || !nd.hist_nul.empty();
-  if (nul) hn.assign((size_t)lag, 0);
-  const int wc = sg_col_width(nd.desc.col_type[c]);
-  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(nd.threads, lag / 65536 + 1));
-  bool miss = false;
-  nd.pool->parallel_for(T, [&](int t) {
-    const int64_t a = lo + lag * t / T, e = lo + lag * (t + 1) / T;
-    for (int64_t g = a; g < e; ++g) {
-      int64_t v = 0;
-      uint8_t u = 0;
-      if (g >= (int64_t)b.base_index) {
-        const int64_t r = g - (int64_t)b.base_index;
-        v = wc == 8 ? ((const int64_t*)b.cols[c])[r] : (int64_t)((const int32_t*)b.cols[c])[r];
-        u = (b.nulls && b.nulls[c]) ? b.nulls[c][r] : 0;
-      } else if (g >= nd.hist_lo && g < nd.hist_lo + nd.hist_n) {
-        v = nd.hist[(size_t)(g - nd.hist_lo)];
-        u = nd.hist_nul.empty() ? 0 : nd.hist_nul[(size_t)(g - nd.hist_lo)];
-      } else {
-        miss = true;
-      }
-      h[(size_t)(g - lo)] = v;
-      if (nul) hn[(size_t)(g - lo)] = u;
-    }
-  });
-  if (miss) throw SgError(SG_EINVAL, "internal: a carried row is older than the node's tag history");
-  nd.hist.swap(h);
-  nd.hist_nul.swap(hn);
-  nd.hist_lo = lo;
-  nd.hist_n = lag;
 }
 
 }  // namespace
@@ -1519,10 +2009,8 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
   nd->opt.ingress_rows = -1;  // (the node does its own chunking)
   nd->threads = host_threads ? host_threads : (int)std::max(1u, std::thread::hardware_concurrency());
   nd->chunk_rows = chunk_rows;
-  nd->no_fill = getenv("SG_NODE_NO_FILL") != nullptr;
-  nd->no_ts32 = getenv("SG_NODE_NO_TS32") != nullptr;
-  nd->edesc = nd->desc;
-  nd->tag_cand = (n_gpus == 1 && !nd->no_fill) ? tag_column(nd->desc) : -1;
+  nd->no_fill = getenv("SG_DEBUG_NODE_NO_FILL") != nullptr;   // (test hooks)
+  nd->no_ts32 = getenv("SG_DEBUG_NODE_NO_TS32") != nullptr;
   memset(&nd->st, 0, sizeof(nd->st));
   int rc = SG_OK;
   for (int s = 0; s < n_gpus && rc == SG_OK; ++s) {
@@ -1545,7 +2033,18 @@ int sg_node_open(int n_gpus, const int* devices, const sg_nfa_desc* nfa, const s
       }
   }
   if (rc == SG_OK) rc = sg_router_open(n_gpus, nd->threads, &nd->router);
-  if (rc == SG_OK) nd->pool = new Pool(std::max(0, nd->threads - 1));
+  for (int a = 0; a < n_gpus && rc == SG_OK; ++a)   // peer copies of the shard exchange (xGMI) where devices differ
+    for (int b = 0; b < n_gpus; ++b) {
+      if (nd->dev[a] == nd->dev[b]) continue;
+      int ok = 0;
+      if (hipDeviceCanAccessPeer(&ok, nd->dev[a], nd->dev[b]) == hipSuccess && ok && hipSetDevice(nd->dev[a]) == hipSuccess)
+        (void)hipDeviceEnablePeerAccess(nd->dev[b], 0);   // (already enabled is fine; hipMemcpyPeerAsync works either way)
+      (void)hipGetLastError();
+    }
+  if (rc == SG_OK) {
+    nd->pool = &host_pool();
+    nd->pool->grow(std::max(0, nd->threads - 1));
+  }
   if (rc != SG_OK) {
     std::string e = nd->err;
     close_node(nd);
@@ -1597,9 +2096,6 @@ int sg_node_reset(sg_node* nd) {
   }
   nd->g_keys = 0;
   nd->ddict = -1;
-  nd->hist_n = 0;
-  nd->hist.clear();
-  nd->hist_nul.clear();
   if (nd->router) sg_router_close(nd->router);
   nd->router = nullptr;
   const int x = sg_router_open(nd->G, nd->threads, &nd->router);

@@ -219,7 +219,6 @@ void sg_every_next_f64(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_i32(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_i64(SgHandle* h, const BatchView& bv, int64_t n);
 void sg_every_next_reset(SgHandle* h);
-int64_t sg_every_next_carry_max_lag(SgHandle* h, int col, uint32_t ref);
 void sg_every_next_release(SgHandle* h);
 void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n);
 // SG_SHAPE_NEXT_CMP_ONCE (once.hip): state_kind 4

@@ -164,9 +164,9 @@ def test_node_partitioned_absence_clock_fanout(gpus):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("gpus", [1, 2])
 def test_node_ships_every_column_when_fill_is_off(gpus, monkeypatch):
-    """SG_NODE_NO_FILL: the closed form's trigger-row columns (ts, e2.*) come back from the GPU instead of being
-    filled on the host from the batch -- both deliveries are the same rows."""
-    monkeypatch.setenv("SG_NODE_NO_FILL", "1")
+    """SG_DEBUG_NODE_NO_FILL (a test hook): the closed form's trigger-row columns (ts, e2.*) come back from the GPU
+    instead of being filled on the host from the batch -- both deliveries are the same rows."""
+    monkeypatch.setenv("SG_DEBUG_NODE_NO_FILL", "1")
     cfg = "C2"
     b = synth_batch(cfg, 0, 150_000, keys=600, rate=100)
     want = _want(synth.QUERIES[cfg], b)
@@ -249,9 +249,10 @@ def test_node_c5_whole_1b_stream_ten_pushes():
 @pytest.mark.parametrize("ts32", [True, False])
 def test_node_timestamp_offsets_and_wide_chunks(ts32, monkeypatch):
     """Chunk timestamps travel as 32-bit offsets from the chunk's minimum; a chunk spanning 2^31 ms or more (here a
-    35-day gap in the middle of the stream) ships them as 8 bytes.  SG_NODE_NO_TS32 forces 8 bytes everywhere."""
+    35-day gap in the middle of the stream) ships them as 8 bytes.  SG_DEBUG_NODE_NO_TS32 (a test hook) forces 8 bytes
+    everywhere.  (With two GPUs the rows travel as they are: the shard exchange uploads 8-byte timestamps.)"""
     if not ts32:
-        monkeypatch.setenv("SG_NODE_NO_TS32", "1")
+        monkeypatch.setenv("SG_DEBUG_NODE_NO_TS32", "1")
     cfg = "C2"
     b = synth_batch(cfg, 0, 200_000, keys=700, rate=100)
     b.ts = b.ts.copy()
@@ -263,13 +264,10 @@ def test_node_timestamp_offsets_and_wide_chunks(ts32, monkeypatch):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("tags", [True, False])
-def test_node_row_tags_reach_back_across_pushes(tags, monkeypatch):
-    """One GPU, closed form: `e1.id` (projected only) travels as the row's event index mod 2^32 and the host reads the
-    id of the e1 row it names -- from the caller's columns, or for rows of earlier pushes the engine still carries,
-    from the node's history.  Key X is quiet from row 1000 to row 80000 (10..800 ms), so its early rows are carried
-    through four pushes and complete matches in the fifth.  SG_NODE_TAGS=0 ships the column instead."""
-    monkeypatch.setenv("SG_NODE_TAGS", "1" if tags else "0")
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_node_carried_rows_reach_back_across_pushes(gpus):
+    """Key X is quiet from row 1000 to row 80000 (10..800 ms), so its early rows are carried through four pushes and
+    complete matches in the fifth: e1's columns come from the carried rows, on one GPU and through the exchange."""
     cfg = "C2"
     b = synth_batch(cfg, 0, 160_000, keys=600, rate=100)
     b.key = b.key.copy()
@@ -279,6 +277,23 @@ def test_node_row_tags_reach_back_across_pushes(tags, monkeypatch):
     b.cols[1] = b.key
     want = _want(synth.QUERIES[cfg], b)
     assert np.any((want.trigger >= 80_000) & (want.vals[:, 0] < 1000))   # e1 rows from the first push, matched in the fifth
-    got, _ = run_node(synth.QUERIES[cfg], _split(b, [0, 20_000, 40_000, 60_000, 80_000, 160_000]), 1, 30_000,
+    got, _ = run_node(synth.QUERIES[cfg], _split(b, [0, 20_000, 40_000, 60_000, 80_000, 160_000]), gpus, 30_000,
                       synth.raw_symbols)
     assert_same(got, want)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus", [2, 3, 4, 8])
+def test_node_shard_exchange(gpus):
+    """The GPU-side shard exchange with G shards on cuda:0: slices of uneven size, chunks whose slices send no row to
+    some shard (few keys), a two-stream partitioned query (PP), and the host's per-chunk work only: route_ms and
+    merge_ms stay at zero."""
+    for cfg, n, keys, rate, chunk in (("C2", 150_000, 5, 100, 17_001), ("PP", 120_000, 300, 100, 25_000),
+                                      ("C3c", 100_000, 200, 100, 33_333)):
+        b = synth_batch(cfg, 0, n, keys=keys, rate=rate)
+        want = _want(synth.QUERIES[cfg], b)
+        assert len(want) > 0
+        got, st = run_node(synth.QUERIES[cfg], [b], gpus, chunk, synth.raw_symbols, key_dict=2)
+        assert_same(got, want)
+        assert st["route_ms"] == 0 and st["merge_ms"] == 0
+        assert sum(st["shard_rows"][:gpus]) == n
