@@ -677,7 +677,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
             o.jp[w] = (uint32_t)q;
             const uint32_t off = (uint32_t)(q - p0);
             maxoff = off > maxoff ? off : maxoff;
-            uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);   // compact: positions (k_em_out)
+            uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);   // compact: positions (k_em_scatter)
             em32[0] = (uint32_t)q;
             em32[1] = (uint32_t)c;
             em32[2] = k;
@@ -945,7 +945,7 @@ struct SqEmit {   // match writer of the emitting pass
     ++nemit;
     o.k1[w] = ((uint64_t)r << 16) | seq++;
     o.runit[w] = unit;
-    // positions only: k_em_out turns them into the match record once the matches are in delivery order (one thread
+    // positions only: k_em_scatter turns them into the match record, in slot order, once the delivery order is known (one thread
     // per match instead of dependent reads in the lane's critical path)
     uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);
     const int64_t pp = mm.dec(mm.M->P[p].pts);
@@ -1143,25 +1143,6 @@ __device__ __forceinline__ void em_build(const uint32_t* __restrict__ e, char* r
   h2[1] = (uint64_t)nm;
 }
 
-// Match records in delivery order (QuerySelector.processNoGroupBy + SelectiveStateEventPopulator,
-// C/query/selector/QuerySelector.java:125-163), gathering the compact records by the sorted order idx: each block's
-// records are assembled in LDS and leave as one contiguous copy (sequence lanes: their rows are read lazily anyway)
-__global__ void k_em_out(int64_t n, const uint32_t* __restrict__ idx, const char* __restrict__ em, int32_t estride,
-                         char* __restrict__ out, int32_t ostride, PpPacked P, const DevDesc* __restrict__ dd,
-                         const uint64_t* __restrict__ index, uint64_t base_index) {
-  extern __shared__ __align__(16) char em_lds[];
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t i = i0 + threadIdx.x;
-  const int64_t nb = n - i0 < (int64_t)blockDim.x ? n - i0 : (int64_t)blockDim.x;
-  if (i < n) em_build((const uint32_t*)(em + (size_t)idx[i] * estride), em_lds + (size_t)threadIdx.x * ostride, P, dd,
-                      index, base_index);
-  __syncthreads();
-  const uint2* src = (const uint2*)em_lds;   // records are 8-byte multiples, the output only 8-byte aligned
-  uint2* dst = (uint2*)(out + (size_t)i0 * ostride);
-  const int64_t words = nb * ostride / 8;
-  for (int64_t w = threadIdx.x; w < words; w += blockDim.x) dst[w] = src[w];
-}
-
 // delivery position of every slot (slots without a match keep ~0)
 __global__ void k_em_dest(int64_t n, const uint32_t* __restrict__ idx, uint32_t* __restrict__ dest) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1246,7 +1227,7 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   o.count = o.reserved + 1;
   o.fail = (int32_t*)(o.reserved + 2);
   o.cap = cap;
-  o.rstride = 20 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
+  o.rstride = 20 + 4 * nsel;   // compact match records (k_em_scatter writes the rstride-byte ones)
   int rb = 1;
   while ((1ll << rb) < n + 1) ++rb;
   const int k1_bits = std::min(64, rb + 16);
@@ -1362,7 +1343,14 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
     void* tmp = h->ws.get("sq_sorttmp", tb, st);
     HIPCHK(rocprim::radix_sort_pairs(tmp, tb, o.k1, kb2, ia, ib, (size_t)R, 0, k1_bits, st));
     char* out = h->out.reserve(total, nsel, st);
-    hipLaunchKernelGGL(k_em_out, dim3((unsigned)((total + 255) / 256)), blk, 256 * rstride, st, total, ib, o.rec, o.rstride,
+    // records built in slot order (a lane's slots hold one key's matches: the compact records and the packed rows they
+    // name are read nearly in order) and scattered to their delivery positions (k_em_scatter), as the partial lanes do
+    uint32_t* dest = (uint32_t*)h->ws.get("sq_dest", 4 * (size_t)(R + 1), st);
+    HIPCHK(hipMemsetAsync(dest, 0xFF, 4 * (size_t)R, st));
+    hipLaunchKernelGGL(k_em_dest, dim3((unsigned)((total + 255) / 256)), blk, 0, st, total, ib, dest);
+    if ((size_t)256 * rstride > 65536)
+      HIPCHK(hipFuncSetAttribute((const void*)k_em_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(256 * rstride)));
+    hipLaunchKernelGGL(k_em_scatter, g2, blk, (size_t)256 * rstride, st, R, dest, o.rec, o.rstride,
                        out + (size_t)h->out.n * rstride, rstride, P, h->ddesc, bv.index, bv.base_index);
     HIPCHK(hipGetLastError());
     h->kend();
@@ -1645,7 +1633,7 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   o.maxoff = (uint32_t*)(o.count + 1);
   o.jp = (uint32_t*)h->ws.get("pp_jp", 4 * cap, st);
   o.fail = err + 1;
-  o.rstride = 20 + 4 * nsel;   // compact match records (k_em_out writes the rstride-byte ones)
+  o.rstride = 20 + 4 * nsel;   // compact match records (k_em_scatter writes the rstride-byte ones)
   int rb = 1;
   while ((1ll << rb) < n + 1) ++rb;
   const int k1_bits = std::min(64, rb + 8);

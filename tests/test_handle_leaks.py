@@ -6,10 +6,13 @@ libsiddhi_gpu.so was loaded before torch the dynamic linker mapped /opt/rocm's c
 `_one_hip_runtime` now binds the library to torch's runtime).  These tests open and close 500 handles over every
 engine route and 20 node pipelines in a FRESH process (so the import order is the library's own, not the test
 runner's), check that file descriptors, threads, device memory and host address space return to their baseline, and
-only then let torch initialise HIP lazily.  The baseline is taken after ONE handle per route and one node per
-pipeline (one GPU; two shards through the GPU-side exchange), under the process's own malloc settings: node
-pipelines run on process-wide threads (node.hip host_pool / pipeline_threads), so no per-push thread adds a malloc
-arena.  Reference seam: the per-key runtimes a partition clones and drops (C/partition/PartitionRuntime.java:255-308)
+only then let torch initialise HIP lazily.  Node pipelines run on process-wide threads (node.hip host_pool /
+pipeline_threads), so no per-push thread adds a malloc arena, and the child runs under the process's own malloc
+settings.  The baseline is taken after one handle per route and one node per pipeline (one GPU; two shards through
+the GPU-side exchange) on each of the process's hardware queues: the HIP runtime keeps, per queue, the scratch of the
+largest private segment a kernel has used on it (k_pred's postfix-VM stack, 400 B per lane: ~200 MiB at full
+occupancy; measured per step in profiles/r05/leak_probe2.log) and its pageable-copy staging, and a new stream lands on
+the next queue (GPU_MAX_HW_QUEUES, 4 here).  Reference seam: the per-key runtimes a partition clones and drops (C/partition/PartitionRuntime.java:255-308)
 -- a drop-in engine must survive any number of them."""
 import json
 import os
@@ -76,10 +79,13 @@ def one_node(G):
     del sink
     return got
 
-# warm-up: one handle per route and one node per pipeline (lazy runtime threads, code objects, allocator pools)
-counts = {c: one_handle(c) for c, *_ in ROUTES}
-node_matches = {G: one_node(G) for G in (1, 2)}
-assert node_matches[1] == node_matches[2]
+# warm-up: one handle per route and one node per pipeline on every hardware queue (lazy runtime threads, code
+# objects, per-queue scratch and staging)
+QUEUES = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+for q in range(QUEUES):
+    counts = {c: one_handle(c) for c, *_ in ROUTES}
+    node_matches = {G: one_node(G) for G in (1, 2)}
+    assert node_matches[1] == node_matches[2]
 base = snap()
 n_handles = 0
 while n_handles < HANDLES:
