@@ -275,6 +275,7 @@ class Handle:
     """Thin RAII wrapper of one sg_handle."""
 
     def __init__(self, desc: sg_nfa_desc, device: int = 0, options: sg_options = None):
+        self._pid = os.getpid()
         self.lib = load_library()
         self.h = ct.c_void_p()
         self.desc = desc
@@ -366,6 +367,8 @@ class Handle:
             self.h = None
 
     def __del__(self):
+        if getattr(self, "_pid", os.getpid()) != os.getpid():
+            return   # (a forked child's copy: the parent owns the native object)
         try:
             self.close()
         except Exception:
@@ -415,6 +418,7 @@ class Router:
     """The native host partition router (sg_router_*): dense first-seen key ids, shard and per-shard dense ids."""
 
     def __init__(self, n_shards: int = 1, threads: int = 0):
+        self._pid = os.getpid()
         self.lib = load_library()
         self.r = ct.c_void_p()
         rc = self.lib.sg_router_open(n_shards, threads, ct.byref(self.r))
@@ -439,6 +443,8 @@ class Router:
             self.r = None
 
     def __del__(self):
+        if getattr(self, "_pid", os.getpid()) != os.getpid():
+            return   # (a forked child's copy: the parent owns the native object)
         try:
             self.close()
         except Exception:
@@ -469,6 +475,7 @@ class Node:
 
     def __init__(self, desc: sg_nfa_desc, n_gpus: int = 1, devices=None, options: sg_options = None,
                  threads: int = 16, chunk_rows: int = 0):
+        self._pid = os.getpid()
         self.lib = load_library()
         self.n = ct.c_void_p()
         self.desc = desc
@@ -515,6 +522,8 @@ class Node:
             self.n = None
 
     def __del__(self):
+        if getattr(self, "_pid", os.getpid()) != os.getpid():
+            return   # (a forked child's copy: the parent owns the native object)
         try:
             self.close()
         except Exception:
@@ -536,6 +545,7 @@ class PinnedArray:
     """A numpy array over pinned host memory from sg_host_alloc (freed with the object)."""
 
     def __init__(self, n: int, dtype):
+        self._pid = os.getpid()
         self.lib = load_library()
         self.p = ct.c_void_p()
         dt = np.dtype(dtype)
@@ -546,6 +556,8 @@ class PinnedArray:
         self.array = np.frombuffer(buf, dtype=dt, count=n)
 
     def __del__(self):
+        if getattr(self, "_pid", os.getpid()) != os.getpid():
+            return   # (a forked child's copy: the parent owns the pinned memory)
         if getattr(self, "p", None) and self.p.value:
             self.array = None
             self.lib.sg_host_free(self.p)
