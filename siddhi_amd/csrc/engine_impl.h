@@ -34,8 +34,9 @@
 //   5. k_walk<WRITE> replays the units and writes one AoS match record (32 + 8*n_select bytes) per match.
 //   Units whose pending list outgrows the LDS ring (or whose time span exceeds 2^31 ms) are redone by the
 //   same walker with an unbounded HBM-resident list (k_walk<BIG>), so capacity never changes results.
-//   6. carry (multi-push streams): per key the rows still inside the window of its last event survive into
-//                   the next push, prepended as virtual rows [0, nc) that are replayed but never emit.
+//   6. carry (multi-push streams): per key its final pending list -- the reference's whole state for the key
+//                   (the `every` start state holds nothing) -- survives into the next push as candidate-only virtual
+//                   rows [0, nc), replayed (re-appended in pending order) but never emitting.
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -726,11 +727,19 @@ struct WalkArgs {
   LdsPlan lp;                 // record walk LDS planes
   int32_t pay_in_rec;         // e1 payload rides in the (narrow) walker records
   // Keys whose rows (carried ones included) go back in time take the exact walker (see Walker::step_exact): one
-  // unit per key on the HBM-list path.  kexact: per-key flag (null: no key does); alive / alive_n: the record pass
-  // of such a key leaves its final pending list (virtual rows, pending order) there for the carry.
+  // unit per key on the HBM-list path.  kexact: per-key flag (null: no key does).
   const uint8_t* kexact;
+  // Carry: the record pass of each key's last unit leaves the key's final pending list -- as virtual rows (alive,
+  // alive_n: HBM lists, and LDS rings that keep e1's row) or as the entries' own time / value / payload (cv: LDS rings
+  // without a row plane; the select needs no other e1 attribute then)
   uint32_t* alive;
   uint32_t* alive_n;
+  int64_t* cv_ts;
+  int32_t* cv_key;
+  int64_t* cv_val;
+  int64_t* cv_pay;
+  uint32_t* cv_n;
+  uint32_t cv_cap;
 };
 
 template <class T> __device__ __forceinline__ bool is_nan_val(T) { return false; }
@@ -1099,21 +1108,6 @@ struct Walker {
   }
 };
 
-// First sorted position of key segment [sb, se) the carry keeps, for a key whose time never went back: partials
-// started more than `within` before the key's last row of B's stream were expired by it, and rows before the window
-// can change no later partial.  A key with no row of B's stream yet keeps every row from its first candidate on
-// (none of its partials has been visited, so none has expired).
-template <class T, bool N>
-__device__ __forceinline__ uint32_t carry_start(const Src<T, N>& src, const Virt& v, uint32_t sb, uint32_t se,
-                                                int64_t within) {
-  uint32_t q = se;
-  while (q > sb && !v_visit(v, src.row(q - 1))) --q;
-  if (q > sb) return lb_ts(src, sb, se, src.ts(q - 1) - within);
-  uint32_t p = sb;
-  while (p < se && !((src.at(p).rowf >> 30) & F_CAND)) ++p;
-  return p;
-}
-
 // HBM-list walker: one lane per unit whose pending list outgrew the LDS ring, whose time span does not fit the ring's
 // 31-bit times, or whose key's time goes back (exact mode: the key's whole segment in one unit).  WRITE=false: count
 // pass; WRITE=true: record pass.
@@ -1122,8 +1116,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
                                                      const uint32_t* __restrict__ seg_e, UnitDesc* __restrict__ ud,
                                                      uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
                                                      const MatchSink em, uint32_t* __restrict__ emap,
-                                                     WalkStats* __restrict__ st, char* __restrict__ big,
-                                                     uint32_t* __restrict__ carry_q0, uint32_t* __restrict__ carry_n) {
+                                                     WalkStats* __restrict__ st, char* __restrict__ big) {
   static_assert(BIG, "the LDS-ring units run on the tiled walker (k_walk_t)");
   const uint32_t u = xcd_block(blockIdx.x, gridDim.x) * WALK_BLOCK + threadIdx.x;
   if (u >= a.n_units) return;
@@ -1205,19 +1198,12 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk(WalkArgs a, Src<T, N> src, 
   if (W.oob) atomicOr(&st->internal, 4u);
   if (W.bad && !W.exact) atomicOr(&st->order_err, 1u);
   if (WRITE && a.carry_out && p1 == se) {
-    if (W.exact) {
-      // the key's pending list itself survives: its partials, in pending order (replaying them changes nothing --
-      // each survived every later row of the key, so none expires or completes another)
-      const uint32_t m = W.top - W.head;
-      const uint32_t o = m ? atomicAdd(a.alive_n, m) : 0u;
-      for (uint32_t s = 0; s < m; ++s) a.alive[o + s] = W.L.grow(W.head + s);
-      carry_q0[k] = se;
-      carry_n[k] = 0;
-    } else {
-      const uint32_t q0 = carry_start(src, v, sb, se, a.within);
-      carry_q0[k] = q0;
-      carry_n[k] = se - q0;
-    }
+    // the key's pending list survives: its partials as rows, in pending order (replaying them as candidates rebuilds
+    // the list -- a carried row neither expires nor completes anything)
+    const uint32_t m = W.top - W.head;
+    const uint32_t o = m ? atomicAdd(a.alive_n, m) : 0u;
+    if ((uint64_t)o + m > (uint64_t)a.nt) atomicOr(&st->internal, 32u);
+    else for (uint32_t s = 0; s < m; ++s) a.alive[o + s] = W.L.grow(W.head + s);
   }
 }
 
@@ -1310,8 +1296,10 @@ __global__ void __launch_bounds__(256) k_transpose(const WRec<T, N>* __restrict_
 }
 
 // walker over tiles (partitioned, LDS list).  All 64 lanes step through rows together.
+// (launch bounds: the record walk's LDS ring (12 B per entry, 16 entries per lane) fits three blocks per CU -- three
+// waves per SIMD -- which its registers must allow too: at 2 waves per SIMD C2's record walk took 3.2 ms, at 3 1.6 ms)
 template <class T, bool N, int OP, bool WRITE>
-__global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src, const uint32_t* __restrict__ seg_b,
+__global__ void __launch_bounds__(WALK_BLOCK, WRITE ? 3 : 5) k_walk_t(WalkArgs a, Src<T, N> src, const uint32_t* __restrict__ seg_b,
                                                        const uint32_t* __restrict__ seg_e,
                                                        const UnitDesc* __restrict__ ud,
                                                        const uint32_t* __restrict__ wlen,
@@ -1319,8 +1307,7 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
                                                        const WRec<T, N>* __restrict__ tile, uint32_t* __restrict__ cnt,
                                                        const uint32_t* __restrict__ off, const MatchSink em,
                                                        uint64_t* __restrict__ emask, WalkStats* __restrict__ st,
-                                                       UnitDesc* __restrict__ ud_w, uint32_t* __restrict__ carry_q0,
-                                                       uint32_t* __restrict__ carry_n) {
+                                                       UnitDesc* __restrict__ ud_w) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const uint32_t u = xcd_block(blockIdx.x, gridDim.x) * WALK_BLOCK + threadIdx.x;
   const uint32_t W = __builtin_amdgcn_readfirstlane(u >> 6), lane = threadIdx.x & 63;
@@ -1345,26 +1332,24 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
   const WRec<T, N>* tp = tile + (size_t)base * 64 + lane;
   WRec<T, N> ba[PF], bb[PF];
   uint32_t oa[PF], ob[PF];
-  int64_t qa[PF], qb[PF];   // e1 payload of candidate rows, fetched a batch ahead
   auto load_rows = [&](WRec<T, N>* buf, uint32_t i0) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) buf[j] = (i0 + j < rows) ? tp[(size_t)(i0 + j) * 64] : WRec<T, N>{};
   };
-  auto gather_offs = [&](const WRec<T, N>* buf, uint32_t i0, uint32_t* ofs, int64_t* pq) {   // rows the count pass marked
+  auto gather_offs = [&](const WRec<T, N>* buf, uint32_t i0, uint32_t* ofs) {   // rows the count pass marked
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const uint64_t mj = (i0 + j < rows) ? emask[base + i0 + j] : 0ull;
       const uint32_t r = buf[j].rowf & ROW_MASK;
       ofs[j] = ((mj >> lane) & 1ull) ? off[r - v.nc] : 0u;
-      pq[j] = (payload && !a.pay_in_rec && (buf[j].rowf >> 30) & F_CAND) ? v_payload(v, r) : 0;
     }
   };
-  auto process = [&](const WRec<T, N>* buf, uint32_t i0, const uint32_t* ofs, const int64_t* pq) {
+  auto process = [&](const WRec<T, N>* buf, uint32_t i0, const uint32_t* ofs) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       bool e = false;
       if (active && i0 + j < len && !Wk.overflow)
-        e = Wk.step(a, v, buf[j], i0 + j >= chunk_i, WRITE ? ofs[j] : 0u, cnt, em, payload, WRITE ? pq[j] : 0, true);
+        e = Wk.step(a, v, buf[j], i0 + j >= chunk_i, WRITE ? ofs[j] : 0u, cnt, em, payload);
       if (!WRITE) {
         const uint64_t b = __ballot(e);
         if (lane == 0) emask[base + i0 + j] = b;
@@ -1375,29 +1360,52 @@ __global__ void __launch_bounds__(WALK_BLOCK) k_walk_t(WalkArgs a, Src<T, N> src
   // stores of the last batch are complete, so the branchy walk of a batch never waits on memory -- without it
   // the compiler drains every outstanding access (including the prefetch) inside each step.
   load_rows(ba, 0);
-  if (WRITE) gather_offs(ba, 0, oa, qa);
+  if (WRITE) gather_offs(ba, 0, oa);
   for (uint32_t i = 0; i < rows; i += 2 * PF) {   // rows is a multiple of TROWS = 2 * PF
     __builtin_amdgcn_s_waitcnt(0);
     load_rows(bb, i + PF);
-    if (WRITE) gather_offs(bb, i + PF, ob, qb);
-    process(ba, i, oa, qa);
+    if (WRITE) gather_offs(bb, i + PF, ob);
+    process(ba, i, oa);
     __builtin_amdgcn_s_waitcnt(0);
     load_rows(ba, i + 2 * PF);
-    if (WRITE) gather_offs(ba, i + 2 * PF, oa, qa);
-    process(bb, i + PF, ob, qb);
+    if (WRITE) gather_offs(ba, i + 2 * PF, oa);
+    process(bb, i + PF, ob);
   }
   if (Wk.oob) atomicOr(&st->internal, 4u);
-  if (!active) return;
-  if (Wk.overflow) {
-    if (!WRITE) ud_w[u].ovf = take_hbm_list(st, w, p1) + 1;
+  if (active && Wk.overflow && !WRITE) ud_w[u].ovf = take_hbm_list(st, w, p1) + 1;
+  if (active && !Wk.overflow && Wk.bad) atomicOr(&st->order_err, 1u);
+  if (!WRITE || !a.carry_out) return;
+  // the key's last unit: its final pending list is the carry -- slots reserved once per wave (every lane of the wave
+  // is still here), not by one atomic per key on a single counter
+  const uint32_t m = (active && !Wk.overflow && p1 == seg_e[k]) ? Wk.top - Wk.head : 0u;
+  uint32_t incl = m;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if ((int)lane >= o) incl += y;
+  }
+  const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+  if (!tot) return;
+  const bool by_row = Wk.L.row != nullptr;
+  uint32_t cbase = 0;
+  if (lane == 63) cbase = atomicAdd(by_row ? a.alive_n : a.cv_n, tot);
+  cbase = (uint32_t)__shfl((int)cbase, 63);
+  const uint32_t o = cbase + incl - m;
+  if ((uint64_t)cbase + tot > (by_row ? (uint64_t)a.nt : (uint64_t)a.cv_cap)) {
+    if (lane == 63) atomicOr(&st->internal, 32u);
     return;
   }
-  if (Wk.bad) atomicOr(&st->order_err, 1u);
-  const uint32_t se = seg_e[k];
-  if (WRITE && a.carry_out && p1 == se) {
-    const uint32_t q0 = carry_start(src, v, sb, se, a.within);
-    carry_q0[k] = q0;
-    carry_n[k] = se - q0;
+  if (by_row) {
+    for (uint32_t s = 0; s < m; ++s) a.alive[o + s] = Wk.L.grow(Wk.head + s);
+  } else {
+    const int64_t t0 = N ? v_ts(v, 0) : 0;   // (narrow records keep times relative to the push's first row)
+    for (uint32_t s = 0; s < m; ++s) {
+      const uint32_t q = Wk.head + s;
+      a.cv_ts[o + s] = t0 + Wk.L.gts(q);
+      a.cv_key[o + s] = (int32_t)k;
+      a.cv_val[o + s] = val_bits<T>(Wk.L.gv(q));
+      a.cv_pay[o + s] = Wk.L.gpay(q);
+    }
   }
 }
 
@@ -1410,24 +1418,9 @@ struct CarryBufs {
   uint8_t* nul[SG_MAX_COLS];
 };
 
-// Carry by arrival order: a virtual row survives into the next push iff its key's last row is within `within` of it
-// (the rows lb_ts finds per key in the record walk: sorted positions [carry_q0, seg_e)).  Those positions mark their
-// arrival rows in a bitmask (one lane per key), a count per 8192-row block and a scan place every survivor, and the
-// survivors are copied in arrival order -- reads of the row columns are near-coalesced (the survivors are mostly the
-// push's last `within` of rows) instead of one random gather per column per row; per-key order stays arrival order,
-// which is all the next push's stable key partition needs.
-template <class T, bool N>
-__global__ void k_carry_mark(Src<T, N> src, uint32_t K, const uint32_t* __restrict__ q0s,
-                             const uint32_t* __restrict__ cn, uint32_t* __restrict__ bits) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const uint32_t q0 = q0s[k], c = cn[k];
-  for (uint32_t i = 0; i < c; ++i) {
-    const uint32_t r = src.row(q0 + i);
-    atomicOr(&bits[r >> 5], 1u << (r & 31));
-  }
-}
-
+// Carry of rows (HBM-list keys, and LDS rings that keep e1's row): the listed rows mark a bitmask, a count per
+// 8192-row block and a scan place every survivor, and the survivors are copied in arrival order (per-key order stays
+// arrival order = pending order, which is all the next push's stable key partition needs).
 static const int CARRY_BLK = 8192;   // rows per block of the survivor count (256 bitmask words)
 
 static __global__ void __launch_bounds__(256) k_carry_bcount(int64_t nt, const uint32_t* __restrict__ bits,
@@ -1554,13 +1547,13 @@ template <class T, bool N, bool WRITE>
 static void launch_walk_t(int op, dim3 g, dim3 b, size_t lds, hipStream_t st, const WalkArgs& wa, const Src<T, N>& src,
                           const uint32_t* seg_b, const uint32_t* seg_e, UnitDesc* ud, const uint32_t* wlen,
                           const uint32_t* wrow, const WRec<T, N>* tile, uint32_t* cnt, const uint32_t* off, const MatchSink& ms,
-                          uint64_t* emask, WalkStats* wst, uint32_t* carry_q0, uint32_t* carry_n) {
+                          uint64_t* emask, WalkStats* wst) {
 #define SG_WALK_T(OPV)                                                                                          \
   if (lds > 65536)                                                                                              \
     HIPCHK(hipFuncSetAttribute((const void*)k_walk_t<T, N, OPV, WRITE>,                                        \
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                          \
   hipLaunchKernelGGL((k_walk_t<T, N, OPV, WRITE>), g, b, lds, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, \
-                     ms, emask, wst, ud, carry_q0, carry_n)
+                     ms, emask, wst, ud)
   switch (op) {
     case 2: SG_WALK_T(2); break;
     case 3: SG_WALK_T(3); break;
@@ -1944,7 +1937,7 @@ __global__ void k_order_keys(Src<T, N> src, KeyOf kf, const uint32_t* __restrict
   }
 }
 
-// rows listed in rows[0, *n) -> carry bitmask
+// rows listed in rows[0, *n) -> carry bitmask (the pending partials of every key the rows list)
 static __global__ void k_carry_mark_list(const uint32_t* __restrict__ rows, const uint32_t* __restrict__ n,
                                          uint32_t* __restrict__ bits) {
   const uint32_t m = *n;
@@ -1952,26 +1945,48 @@ static __global__ void k_carry_mark_list(const uint32_t* __restrict__ rows, cons
     atomicOr(&bits[rows[i] >> 5], 1u << (rows[i] & 31));
 }
 
-// The next push's carried rows, in arrival order: per key the sorted positions [carry_q0, carry_q0 + carry_n) (keys
-// on the fast path), plus the listed pending partials of keys that walked exact (alive, alive_n; may be null).
+// pending entries kept as values (LDS rings without a row plane) -> carried candidate rows [base, base + n): time,
+// key, the compared value and e1's payload attribute; every other column of such a row is never read (no select
+// gathers an e1 attribute by row when the ring has no row plane, and a carried row is never a B row)
+template <class T>
+__global__ void k_carry_vals(uint32_t n, const int64_t* __restrict__ cts, const int32_t* __restrict__ ckey,
+                             const int64_t* __restrict__ cval, const int64_t* __restrict__ cpay, int val_col, int pay_col,
+                             int pay_w, int n_cols, uint32_t base, CarryBufs dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t d = base + i;
+  dst.ts[d] = cts[i];
+  dst.key[d] = ckey[i];
+  dst.flags[d] = (uint8_t)F_CAND;
+  const uint64_t vb = (uint64_t)cval[i];
+  T x;
+  if constexpr (sizeof(T) == 4) { const uint32_t w = (uint32_t)vb; __builtin_memcpy(&x, &w, 4); }
+  else __builtin_memcpy(&x, &vb, 8);
+  ((T*)dst.col[val_col])[d] = x;
+  if (pay_col >= 0) {
+    if (pay_w == 8) ((int64_t*)dst.col[pay_col])[d] = cpay[i];
+    else ((int32_t*)dst.col[pay_col])[d] = (int32_t)cpay[i];
+  }
+  for (int c = 0; c < n_cols; ++c) dst.nul[c][d] = 0;
+}
+
+// The next push's carried rows: every key's final pending list -- listed rows (alive) copied in arrival order, then
+// the entries kept as values (cv) appended.  Per key one of the two; per key pending order.
 template <class T, bool N>
-static void carry_out_rows(SgHandle* h, EveryNextState* es, uint32_t K, int64_t nt, const Src<T, N>& src, const Virt& v,
-                           const BatchView& bv, const SgCols& cc, const uint32_t* carry_q0, const uint32_t* carry_n,
-                           const uint32_t* alive, const uint32_t* alive_n) {
+static void carry_out_rows(SgHandle* h, EveryNextState* es, int64_t nt, const Virt& v, const BatchView& bv,
+                           const SgCols& cc, const WalkArgs& wa, int val_col, int pay_col, int pay_w) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
   CarrySet& cs = es->carry[es->cur];
-  uint32_t* ccount = (uint32_t*)h->ws.get("carry_count", sizeof(uint32_t), st);
+  uint32_t* ccount = (uint32_t*)h->ws.get("carry_count", sizeof(uint32_t) * 2, st);
   h->kbeg("carry");
   const int64_t nb = (nt + CARRY_BLK - 1) / CARRY_BLK;
   uint32_t* cbits = (uint32_t*)h->ws.get("carry_bits", sizeof(uint32_t) * (size_t)(nb * 256), st);
   uint32_t* cboff = (uint32_t*)h->ws.get("carry_boff", sizeof(uint32_t) * (size_t)(nb + 1), st);
   uint32_t* bcnt = (uint32_t*)h->ws.get("carry_bcnt", sizeof(uint32_t) * (size_t)(nb + 1), st);
   HIPCHK(hipMemsetAsync(cbits, 0, sizeof(uint32_t) * (size_t)(nb * 256), st));
-  hipLaunchKernelGGL((k_carry_mark<T, N>), dim3((K + 255) / 256), dim3(256), 0, st, src, K, carry_q0, carry_n, cbits);
-  if (alive && alive_n)
-    hipLaunchKernelGGL(k_carry_mark_list, dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 4096)), dim3(256), 0, st,
-                       alive, alive_n, cbits);
+  hipLaunchKernelGGL(k_carry_mark_list, dim3((unsigned)std::min<int64_t>((nt + 255) / 256, 4096)), dim3(256), 0, st,
+                     wa.alive, wa.alive_n, cbits);
   hipLaunchKernelGGL(k_carry_bcount, dim3((unsigned)nb), dim3(256), 0, st, nt, cbits, bcnt);
   HIPCHK(hipMemsetAsync(bcnt + nb, 0, sizeof(uint32_t), st));
   HIPCHK(hipGetLastError());
@@ -1980,12 +1995,14 @@ static void carry_out_rows(SgHandle* h, EveryNextState* es, uint32_t K, int64_t 
   void* tmp = h->ws.get("carry_scan_tmp", tb, st);
   HIPCHK(rocprim::exclusive_scan(tmp, tb, bcnt, cboff, (uint32_t)0, (size_t)nb + 1, rocprim::plus<uint32_t>(), st));
   HIPCHK(hipMemcpyAsync(ccount, cboff + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(ccount + 1, wa.cv_n, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   h->kend();
-  uint32_t ncar = 0;
-  HIPCHK(hipMemcpyAsync(&ncar, ccount, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint32_t hc[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(hc, ccount, sizeof(hc), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const uint32_t nrow = hc[0], nval = hc[1];
   CarrySet& nx = es->carry[es->cur ^ 1];
-  nx.ensure(std::max<int64_t>(ncar, 1), d.n_cols, d.col_type);
+  nx.ensure(std::max<int64_t>((int64_t)nrow + nval, 1), d.n_cols, d.col_type);
   int32_t* widths = (int32_t*)h->ws.get("col_widths", sizeof(int32_t) * SG_MAX_COLS, st);
   int32_t hw[SG_MAX_COLS];
   for (int c = 0; c < SG_MAX_COLS; ++c)
@@ -1997,12 +2014,19 @@ static void carry_out_rows(SgHandle* h, EveryNextState* es, uint32_t K, int64_t 
   cb.key = nx.key;
   cb.flags = nx.flags;
   for (int c = 0; c < d.n_cols; ++c) { cb.col[c] = nx.col[c]; cb.nul[c] = nx.nul[c]; }
-  if (ncar)
+  if (nrow)
     hipLaunchKernelGGL(k_carry_gather, dim3((unsigned)nb), dim3(256), 0, st, v, nt, cbits, cboff, d.n_cols, widths,
                        bv.cols, cc, cb);
+  if (nval) {
+    for (int c = 0; c < d.n_cols; ++c)   // (columns the value entries do not set: deterministic snapshots)
+      if (c != val_col && c != pay_col)
+        HIPCHK(hipMemsetAsync((char*)nx.col[c] + (size_t)hw[c] * nrow, 0, (size_t)hw[c] * nval, st));
+    hipLaunchKernelGGL(k_carry_vals<T>, dim3((nval + 255) / 256), dim3(256), 0, st, nval, wa.cv_ts, wa.cv_key, wa.cv_val,
+                       wa.cv_pay, val_col, pay_col, pay_w, d.n_cols, nrow, cb);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
-  nx.n = ncar;
+  nx.n = (int64_t)nrow + nval;
   cs.n = 0;
   es->cur ^= 1;
 }
@@ -2277,8 +2301,6 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
   WalkStats* wst = (WalkStats*)h->ws.get("walkstats", sizeof(WalkStats), st);
   uint32_t* cnt = (uint32_t*)h->ws.get("cnt", sizeof(uint32_t) * (n + 1), st);
   uint32_t* off = (uint32_t*)h->ws.get("off", sizeof(uint32_t) * (n + 1), st);
-  uint32_t* carry_q0 = (uint32_t*)h->ws.get("carry_q0", sizeof(uint32_t) * K, st);
-  uint32_t* carry_n = (uint32_t*)h->ws.get("carry_n", sizeof(uint32_t) * (K + 1), st);
   uint32_t* emap = (uint32_t*)h->ws.get("emap", sizeof(uint32_t) * (nt / 32 + 2), st);
   const dim3 wblk(WALK_BLOCK), wgrd((unsigned)((units + WALK_BLOCK - 1) / WALK_BLOCK));
   const uint32_t nw = (uint32_t)((units + 63) / 64);
@@ -2303,7 +2325,6 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n + 1), st));
     HIPCHK(hipMemsetAsync(emap, 0, sizeof(uint32_t) * (nt / 32 + 2), st));
     HIPCHK(hipMemsetAsync(wst, 0, sizeof(WalkStats), st));
-    if (wa.carry_out) HIPCHK(hipMemsetAsync(carry_n, 0, sizeof(uint32_t) * (K + 1), st));
     // lane-interleaved tiles: unit ranges -> per-wave rows -> LDS transpose of the sorted records
     HIPCHK(hipMemsetAsync(wlen, 0, sizeof(uint32_t) * (nw + 1), st));
     h->kbeg("units");
@@ -2348,7 +2369,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     }
     h->kbeg("walk_count");
     launch_walk_t<T, N, false>(op, wgrd, wblk, lds_count, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, ms,
-                               emask, wst, carry_q0, carry_n);
+                               emask, wst);
     h->kend();
     h->kbeg("count_scan");
     scan_counts();
@@ -2364,7 +2385,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       big = (char*)h->ws.get("big_lists", (size_t)hs.ovf_total * PendBytes<T>::hbm, st);
       h->mark(6);
       hipLaunchKernelGGL((k_walk<T, N, false, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off,
-                         ms, emap, wst, big, carry_q0, carry_n);
+                         ms, emap, wst, big);
       HIPCHK(hipGetLastError());
       scan_counts();
       h->mark(7);
@@ -2403,18 +2424,24 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     ms.cap = total;
     ms.rec = h->ws.get("mrec", (ms.narrow ? sizeof(MRec16) : sizeof(MRec)) * std::max<uint32_t>(total, 1), st);
     h->mark(5);
-    if (wa.kexact && wa.carry_out) {
+    if (wa.carry_out) {   // each key's final pending list (k_walk / k_walk_t, record pass)
       wa.alive = (uint32_t*)h->ws.get("alive_rows", sizeof(uint32_t) * (size_t)std::max<int64_t>(nt, 1), st);
-      wa.alive_n = (uint32_t*)h->ws.get("alive_n", sizeof(uint32_t), st);
-      HIPCHK(hipMemsetAsync(wa.alive_n, 0, sizeof(uint32_t), st));
+      wa.alive_n = (uint32_t*)h->ws.get("alive_n", sizeof(uint32_t) * 2, st);
+      wa.cv_n = wa.alive_n + 1;
+      HIPCHK(hipMemsetAsync(wa.alive_n, 0, sizeof(uint32_t) * 2, st));
+      wa.cv_cap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)K * wa.lp.cap));
+      wa.cv_ts = (int64_t*)h->ws.get("cv_ts", sizeof(int64_t) * (size_t)wa.cv_cap, st);
+      wa.cv_val = (int64_t*)h->ws.get("cv_val", sizeof(int64_t) * (size_t)wa.cv_cap, st);
+      wa.cv_pay = (int64_t*)h->ws.get("cv_pay", sizeof(int64_t) * (size_t)wa.cv_cap, st);
+      wa.cv_key = (int32_t*)h->ws.get("cv_key", sizeof(int32_t) * (size_t)wa.cv_cap, st);
     }
     h->kbeg("walk_record");
     launch_walk_t<T, N, true>(op, wgrd, wblk, lds_write, st, wa, src, seg_b, seg_e, ud, wlen, wrow, tile, cnt, off, ms,
-                              emask, wst, carry_q0, carry_n);
+                              emask, wst);
     h->kend();
     if (hs.n_ovf) {
       hipLaunchKernelGGL((k_walk<T, N, true, true>), wgrd, wblk, 0, st, wa, src, seg_b, seg_e, ud, cnt, off, ms,
-                         emap, wst, big, carry_q0, carry_n);
+                         emap, wst, big);
       HIPCHK(hipGetLastError());
     }
     if (total) {
@@ -2434,7 +2461,7 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
     HIPCHK(hipMemcpyAsync(&guard, &wst->internal, sizeof(uint32_t), hipMemcpyDeviceToHost, st));   // record-pass guards
     HIPCHK(hipStreamSynchronize(st));
     if (guard) throw SgError(SG_EINVAL, "internal: record-pass guard tripped (" + std::to_string(guard) + ")");
-    carry_out_rows<T, N>(h, es, K, nt, src, v, bv, cc, carry_q0, carry_n, wa.alive, wa.alive_n);
+    carry_out_rows<T, N>(h, es, nt, v, bv, cc, wa, val_col_a, v.pcol ? plan.pcol : -1, v.pw);
   }
   h->last_events = n;
   h->last_matches = total;
