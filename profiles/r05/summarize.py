@@ -32,7 +32,7 @@ MARKS = [   # kernel name pattern -> engine mark (siddhi_amd/csrc: h->kbeg names
     (r"k_walk<[^>]*false, true>", "walk_count"), (r"k_walk<[^>]*true, true>", "walk_record"),
     (r"k_project\b", "project"), (r"k_carry_copy\b|k_nge_carry", "carry"), (r"k_nge_blocks|k_nge\b", "nge_search"),
     (r"k_route\b", "route"), (r"k_segments\b", "key_sort"), (r"k_nfa_units|k_unit_", "nfa_units"),
-    (r"k_nfa\b", "nfa_keys"), (r"k_sortkeys|k_gather\b", "match_order"), (r"k_abs_rows|k_abs_init", "abs_roles"),
+    (r"k_nfa\b", "nfa_keys"), (r"k_sortkeys|k_gather\b|k_em_", "match_order"), (r"k_abs_rows|k_abs_init", "abs_roles"),
     (r"k_abs_keys|k_abs_rkill|k_abs_kill", "abs_sort_kill"), (r"k_abs_decide", "abs_decide_scan"),
     (r"k_abs_slot|k_abs_heads|k_abs_write|k_abs_last", "abs_write"),
     (r"scan|lookback", "scans"), (r"radix_sort|histogram", "key_sort"),
