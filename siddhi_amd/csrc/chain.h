@@ -325,7 +325,42 @@ SG_HD inline bool sg_terms_fast(const R& r, int n_states) {
   return true;
 }
 
-template <class Src, class G = PpBig, bool FAST = false>
+// State table of one query family known at compile time (kinds, successors, logical pairs, visit order): the lane's
+// loops over the states unroll and their kind branches fold -- the interpreter's scalar control flow is what bounds
+// the lane kernel.  Counts, windows and filters stay run-time values.  PpShapeAny reads the descriptor.
+struct PpShapeAny {
+  static constexpr bool known = false;
+  static constexpr int n = 0;
+  static constexpr int8_t kind[1] = {0}, next[1] = {0}, partner[1] = {0}, ltype[1] = {0}, sel[1] = {0}, pres[1] = {0};
+};
+// `every e1=S[..] -> e2=S[..]<m:n> -> e3=S[..] and e4=S[..]` (C3c's family: one stream, a count state feeding an
+// `and` pair whose members both select)
+struct PpShapeC3 {
+  static constexpr bool known = true;
+  static constexpr int n = 4;
+  static constexpr int8_t kind[4] = {SG_K_STREAM, SG_K_COUNT, SG_K_LOGICAL, SG_K_LOGICAL};
+  static constexpr int8_t next[4] = {1, 3, -1, -1};
+  static constexpr int8_t partner[4] = {-1, -1, 3, 2};
+  static constexpr int8_t ltype[4] = {0, 0, 0, 0};
+  static constexpr int8_t sel[4] = {0, 0, 1, 1};
+  static constexpr int8_t pres[4] = {0, 1, 2, 3};   // the receiver's processors (visited in reverse)
+};
+template <class SH>
+SG_HD inline bool sg_pp_shape_is(const sg_nfa_desc& d, const SgPpRule& r) {
+  if (!SH::known || !r.ok || d.n_states != SH::n || r.start != 0) return false;
+  const sg_receiver_desc& rv = d.receivers[r.recv];
+  if (rv.n != SH::n) return false;
+  for (int s = 0; s < SH::n; ++s) {
+    const sg_state_desc& x = d.states[s];
+    if (x.kind != SH::kind[s] || x.next_state != SH::next[s] || x.partner != SH::partner[s] ||
+        (x.kind == SG_K_LOGICAL && x.logical_type != SH::ltype[s]) || (x.has_selector != 0) != (SH::sel[s] != 0) ||
+        rv.pres[s] != SH::pres[s])
+      return false;
+  }
+  return true;
+}
+
+template <class Src, class G = PpBig, bool FAST = false, class SH = PpShapeAny>
 struct PpLane {
   const sg_nfa_desc* d;
   const SgPpRule* ru;
@@ -345,30 +380,41 @@ struct PpLane {
 
   SG_HD const sg_state_desc& st(int s) const { return d->states[s]; }
   SG_HD static uint32_t bit(int s) { return 1u << s; }
+  // the state table, from the compile-time shape when there is one
+  static constexpr int NS = SH::known ? SH::n : G::S;   // states the loops cover
+  SG_HD int nstates() const { if constexpr (SH::known) return SH::n; else return d->n_states; }
+  SG_HD int kind_of(int s) const { if constexpr (SH::known) return SH::kind[s]; else return st(s).kind; }
+  SG_HD int next_of(int s) const { if constexpr (SH::known) return SH::next[s]; else return st(s).next_state; }
+  SG_HD int partner_of(int s) const { if constexpr (SH::known) return SH::partner[s]; else return st(s).partner; }
+  SG_HD int ltype_of(int s) const { if constexpr (SH::known) return SH::ltype[s]; else return st(s).logical_type; }
+  SG_HD bool sel_of(int s) const { if constexpr (SH::known) return SH::sel[s] != 0; else return st(s).has_selector != 0; }
+  SG_HD int start_of() const { if constexpr (SH::known) return 0; else return ru->start; }
 
   // does the start state's armed partial accept this row (its filter, evaluated with e1 bound to the row)?
   SG_HD bool start_ok(int32_t row) {
-    for (int s = 0; s < G::S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
-    A->slot[ru->start] = (int32_t)row;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
+    A->slot[start_of()] = (int32_t)row;
     cur_row = row;
-    return filter(ru->start);
+    return filter(start_of());
   }
   SG_HD void start(int32_t row) {   // the armed start partial takes e1 = row (process_and_return of the start state)
-    for (int s = 0; s < G::S; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) { A->slot[s] = -1; A->clen[s] = 0; }
     l0 = l1 = 0;
     f_changed = f_returned = f_success = 0;
     nh = 0;
     overflow = 0;
     cur_row = row;
-    cur_rank = ru->visit_rank[ru->start];
-    A->slot[ru->start] = (int32_t)row;
+    cur_rank = ru->visit_rank[start_of()];
+    A->slot[start_of()] = (int32_t)row;
     e1_ts = src.ts(row);
-    stream_post(ru->start);   // the `every` clone it also makes stays behind in the start state's lists
+    stream_post(start_of());   // the `every` clone it also makes stays behind in the start state's lists
   }
 
   // ---- event access (KeyMachine::get_event): row of (state, index in chain) or -1
   SG_HD int32_t get_event(int s, int idx) {
-    if (st(s).kind != SG_K_COUNT) {
+    if (kind_of(s) != SG_K_COUNT) {
       if (A->slot[s] < 0) return -1;
       return (idx == 0 || idx == -1) ? A->slot[s] : -1;
     }
@@ -384,7 +430,7 @@ struct PpLane {
     return c[k];
   }
   SG_HD int64_t slot_ts(int s) {
-    int32_t r = st(s).kind == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
+    int32_t r = kind_of(s) == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
     return src.ts(r);
   }
   struct Reader {
@@ -466,12 +512,11 @@ struct PpLane {
 
   // ---- posts
   SG_HD void stream_post(int s) {
-    const sg_state_desc& x = st(s);
     f_changed |= bit(s);
-    pts_pos = st(s).kind == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
+    pts_pos = kind_of(s) == SG_K_COUNT ? (A->clen[s] ? A->chain[ru->coff[s]] : -1) : A->slot[s];
     pts = slot_ts(s);
-    if (x.has_selector) f_returned |= bit(s);
-    if (x.next_state >= 0) add_state(x.next_state);
+    if (sel_of(s)) f_returned |= bit(s);
+    if (next_of(s) >= 0) add_state(next_of(s));
   }
   SG_HD void count_post(int s) {
     const sg_state_desc& x = st(s);
@@ -480,25 +525,23 @@ struct PpLane {
     pts_pos = A->chain[ru->coff[s] + n - 1];
     pts = src.ts(pts_pos);
     if (n >= x.min_count) {
-      if (n == x.min_count && x.next_state >= 0) add_state(x.next_state);   // count_min_reached (no selector)
+      if (n == x.min_count && next_of(s) >= 0) add_state(next_of(s));   // count_min_reached (no selector)
       if (n == x.max_count) f_changed |= bit(s);
     }
   }
   SG_HD void logical_post(int s) {
-    const sg_state_desc& x = st(s);
-    if (x.logical_type == 0) {
-      if (A->slot[x.partner] >= 0) stream_post(s);
+    if (ltype_of(s) == 0) {
+      if (A->slot[partner_of(s)] >= 0) stream_post(s);
       else f_changed |= bit(s);
     } else {
       stream_post(s);
     }
   }
   SG_HD void add_state(int s) {
-    const sg_state_desc& x = st(s);
     if (nh < PP_MAX_HIST) A->hist[nh++] = pp_tkey(cur_row, cur_rank);
     else overflow = 1;
     l1 |= bit(s);
-    if (x.kind == SG_K_LOGICAL) l1 |= bit(x.partner);
+    if (kind_of(s) == SG_K_LOGICAL) l1 |= bit(partner_of(s));
   }
   SG_HD bool is_expired(int64_t t) {
     int64_t dt = e1_ts - t;
@@ -508,54 +551,62 @@ struct PpLane {
 
   // ---- one row: updateState of every state, then the states in visit order (KeyMachine::receive)
   // Returns the visit slot that emitted (one emission per row at most: the partial leaves the emitting state), or -1.
+  // visit k of the row: state s (returns false when the partial overflowed its arrays)
+  SG_HD bool visit(int k, int s, int64_t t, int& emitted) {
+    if (!(l0 & bit(s)) || s == start_of()) return true;
+    cur_rank = k;
+    bool remove = false;
+    if (kind_of(s) == SG_K_COUNT) {
+      if ((s + 1 < nstates() && get_any(s + 1)) || (s + 2 < nstates() && get_any(s + 2))) {
+        l0 &= ~bit(s);
+        return true;
+      }
+      if (A->clen[s] >= st(s).max_count) { overflow = 1; return false; }
+      A->chain[ru->coff[s] + A->clen[s]++] = (int32_t)cur_row;
+      f_success &= ~bit(s);
+      f_changed &= ~bit(s);
+      if (filter(s)) count_post(s);
+      if (f_changed & bit(s)) remove = true;
+      if (!(f_success & bit(s))) --A->clen[s];
+    } else {
+      if (is_expired(t)) { l0 &= ~bit(s); return true; }
+      if (kind_of(s) == SG_K_LOGICAL && ltype_of(s) == 1 && A->slot[partner_of(s)] >= 0) { l0 &= ~bit(s); return true; }
+      A->slot[s] = cur_row;
+      f_changed &= ~bit(s);
+      if (filter(s)) {
+        if (kind_of(s) == SG_K_LOGICAL) logical_post(s);
+        else stream_post(s);
+      }
+      if (f_returned & bit(s)) {
+        f_returned &= ~bit(s);
+        if (emitted < 0) emitted = k;
+        else overflow = 1;
+      }
+      if (f_changed & bit(s)) remove = true;
+      else A->slot[s] = -1;
+    }
+    if (remove) l0 &= ~bit(s);
+    return true;
+  }
   SG_HD int step(int32_t row) {
     cur_row = row;
-    const sg_receiver_desc& rv = d->receivers[ru->recv];
     const uint32_t moved = l1;
     l0 |= moved;
     l1 = 0;
     const int64_t t = src.ts(row);
     int emitted = -1;
-    for (int k = 0; k < rv.n; ++k) {
-      const int s = rv.pres[rv.n - 1 - k];
-      if (!(l0 & bit(s)) || s == ru->start) continue;
-      cur_rank = k;
-      const sg_state_desc& x = st(s);
-      bool remove = false;
-      if (x.kind == SG_K_COUNT) {
-        if ((s + 1 < d->n_states && get_any(s + 1)) || (s + 2 < d->n_states && get_any(s + 2))) {
-          l0 &= ~bit(s);
-          continue;
-        }
-        if (A->clen[s] >= st(s).max_count) { overflow = 1; return -1; }
-        A->chain[ru->coff[s] + A->clen[s]++] = (int32_t)row;
-        f_success &= ~bit(s);
-        f_changed &= ~bit(s);
-        if (filter(s)) count_post(s);
-        if (f_changed & bit(s)) remove = true;
-        if (!(f_success & bit(s))) --A->clen[s];
-      } else {
-        if (is_expired(t)) { l0 &= ~bit(s); continue; }
-        if (x.kind == SG_K_LOGICAL && x.logical_type == 1 && A->slot[x.partner] >= 0) { l0 &= ~bit(s); continue; }
-        A->slot[s] = (int32_t)row;
-        f_changed &= ~bit(s);
-        if (filter(s)) {
-          if (x.kind == SG_K_LOGICAL) logical_post(s);
-          else stream_post(s);
-        }
-        if (f_returned & bit(s)) {
-          f_returned &= ~bit(s);
-          if (emitted < 0) emitted = k;
-          else overflow = 1;
-        }
-        if (f_changed & bit(s)) remove = true;
-        else A->slot[s] = -1;
-      }
-      if (remove) l0 &= ~bit(s);
+    if constexpr (SH::known) {
+#pragma unroll
+      for (int k = 0; k < SH::n; ++k)
+        if (!visit(k, SH::pres[SH::n - 1 - k], t, emitted)) return -1;
+    } else {
+      const sg_receiver_desc& rv = d->receivers[ru->recv];
+      for (int k = 0; k < rv.n; ++k)
+        if (!visit(k, rv.pres[rv.n - 1 - k], t, emitted)) return -1;
     }
     return emitted;
   }
-  SG_HD bool get_any(int s) { return st(s).kind == SG_K_COUNT ? A->clen[s] > 0 : A->slot[s] >= 0; }
+  SG_HD bool get_any(int s) { return kind_of(s) == SG_K_COUNT ? A->clen[s] > 0 : A->slot[s] >= 0; }
   SG_HD bool dead() const { return (l0 | l1) == 0; }
   // A count state still short of its minimum holds the partial: counts never expire by `within`
   // (CountPreStateProcessor.processAndReturn, C/query/input/stream/state/CountPreStateProcessor.java:53-93), so a later
@@ -564,14 +615,16 @@ struct PpLane {
   // state past its minimum can no longer forward the partial.
   SG_HD bool waiting_count() const {
     const uint32_t live = l0 | l1;
-    for (int s = 0; s < G::S && s < d->n_states; ++s)
-      if (((live >> s) & 1u) && st(s).kind == SG_K_COUNT && A->clen[s] < st(s).min_count) return true;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (s < nstates() && ((live >> s) & 1u) && kind_of(s) == SG_K_COUNT && A->clen[s] < st(s).min_count) return true;
     return false;
   }
   SG_HD bool live_other() const {   // a live state that is not a count state
     const uint32_t live = l0 | l1;
-    for (int s = 0; s < G::S && s < d->n_states; ++s)
-      if (((live >> s) & 1u) && st(s).kind != SG_K_COUNT) return true;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (s < nstates() && ((live >> s) & 1u) && kind_of(s) != SG_K_COUNT) return true;
     return false;
   }
   // rows the partial holds (e1, every bound slot, every chain event): replaying a superset of them in arrival order,
@@ -579,12 +632,12 @@ struct PpLane {
   // changed nothing the first time (the same state meets the same row again)
   template <class F>
   SG_HD void witnesses(F mark) const {
-    for (int s = 0; s < G::S && s < d->n_states; ++s) {
-      if (st(s).kind == SG_K_COUNT) {
+    for (int s = 0; s < NS && s < nstates(); ++s) {
+      if (kind_of(s) == SG_K_COUNT) {
         const int32_t* c = A->chain + ru->coff[s];
         for (int i = 0; i < A->clen[s]; ++i) mark(c[i], false);
       } else if (A->slot[s] >= 0) {
-        mark(A->slot[s], s == ru->start);
+        mark(A->slot[s], s == start_of());
       }
     }
   }
@@ -601,12 +654,12 @@ struct PpLane {
     if (l1 != 0 || l0 == 0 || (l0 & (l0 - 1u)) != 0) return false;
     int s = 0;
     while (!((l0 >> s) & 1u)) ++s;
-    if (s == ru->start || !ru->wait[s].ok) return false;
-    const sg_state_desc& x = st(s);
-    if (x.kind == SG_K_COUNT) {
-      if ((s + 1 < d->n_states && get_any(s + 1)) || (s + 2 < d->n_states && get_any(s + 2))) return false;
-      if (A->clen[s] >= x.max_count) return false;
-    } else if (x.kind == SG_K_LOGICAL && x.logical_type == 1 && A->slot[x.partner] >= 0) {
+    if (s == start_of() || !ru->wait[s].ok) return false;
+    const int kd = kind_of(s);
+    if (kd == SG_K_COUNT) {
+      if ((s + 1 < nstates() && get_any(s + 1)) || (s + 2 < nstates() && get_any(s + 2))) return false;
+      if (A->clen[s] >= st(s).max_count) return false;
+    } else if (kd == SG_K_LOGICAL && ltype_of(s) == 1 && A->slot[partner_of(s)] >= 0) {
       return false;
     }
     const PpWait& w = ru->wait[s];
@@ -614,7 +667,7 @@ struct PpLane {
     int null = 0;
     operand_bits(w.other ? t.l : t.r, cbits, null);
     if (null) return false;
-    wait_count = x.kind == SG_K_COUNT;
+    wait_count = kd == SG_K_COUNT;
     slot = w.slot;
     op = w.op;
     fast = w.fast;

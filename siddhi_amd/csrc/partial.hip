@@ -66,6 +66,7 @@ struct PartialState {
   int sq_small = 0;             // the query fits seq.h's small state geometry (SqSmall)
   int pp_small = 0;             // the query fits chain.h's small lane geometry (PpSmall)
   int lanes_fast = 0;           // every filter is fast compares or event-local bits (chain.h sg_terms_fast)
+  int shape_c3 = 0;             // the state table is C3c's family (chain.h PpShapeC3): the specialised lane kernel
   size_t sq_bytes = sizeof(SeqState);
   int64_t kst_keys = 0;
   int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
@@ -132,6 +133,7 @@ PartialState* sg_partial_new(const sg_nfa_desc& d) {
     hipMemcpy(ps->dsrule, &ps->srule, sizeof(SgSeqRule), hipMemcpyHostToDevice);
   }
   ps->lanes_fast = (ps->mode == 2 ? sg_terms_fast(sr, d.n_states) : sg_terms_fast(ru, d.n_states)) ? 1 : 0;
+  ps->shape_c3 = (ps->mode == 1 && sg_pp_shape_is<PpShapeC3>(d, ru)) ? 1 : 0;
   for (int s = 0; s < d.n_states; ++s) ps->has_count |= d.states[s].kind == SG_K_COUNT;
   for (int k = 0; k < d.n_ret; ++k) {
     const int c = d.ret_col[k];
@@ -556,7 +558,7 @@ __global__ void k_pp_wsum(int64_t m, PpPacked P, uint32_t slots, uint32_t fslots
 
 constexpr int PP_BLOCK = 256;
 constexpr int64_t PP_WAVE_CANDS = 512;    // start rows per wave (C3c sweep 128..8192: 512 and below 20.4-20.5 ms, 2048 21.5, 8192 26.0; profiles/r04/lanes_ab.log)
-template <class G, bool FAST = false>
+template <class G, bool FAST = false, class SH = PpShapeAny>
 __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                        const SgPpRule* __restrict__ rug, const uint32_t* __restrict__ cand,
                                                        int64_t ncand, const uint32_t* __restrict__ skey,
@@ -584,7 +586,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   const int64_t hi = lo + wave_cands < ncand ? lo + wave_cands : ncand;
   if (lo >= ncand) return;
   PpSrc src{&pl};
-  PpLane<PpSrc, G, FAST> L;
+  PpLane<PpSrc, G, FAST, SH> L;
   L.d = dd;
   L.ru = &rl;
   L.src = src;
@@ -595,6 +597,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
   bool active = i < hi;
   int64_t q = 0, e = 0, p0 = 0;
   uint32_t k = 0;
+  bool back = false;   // the key's time goes back in this push: skip rows only while waiting in a count state
   if (active) {
     const int64_t p = cand[i];
     k = skey[p];
@@ -602,6 +605,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
     q = p + 1;
     p0 = p;
     e = end[k];
+    back = a.kback && a.kback[k];
   }
   const uint64_t lt = (1ull << lane) - 1ull;
   bool emitted = false;
@@ -614,7 +618,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
       // goes back skips only while the partial waits in a count state, which nothing expires)
       int ws, wop, wf;
       int64_t wc;
-      if (pl.wsum && q < e && L.wait_on(ws, wop, wf, wc) && (L.wait_count || !(a.kback && a.kback[k]))) {
+      if (pl.wsum && q < e && L.wait_on(ws, wop, wf, wc) && (L.wait_count || !back)) {
         // blocks whose summary rules the term out are skipped whole; in a block that may pass, the lane reads its 8
         // values at once and lands on the first row that passes (or moves on to the next block)
         const uint2* S = pl.wsum + (int64_t)pl.wix[ws] * pl.wnb;
@@ -660,7 +664,10 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
             atomicOr(&a.keep[pos], 1u);
             if (st) a.kstart[pos] = 1;
           });
-      } else if (dt > within && !L.waiting_count()) {   // expired everywhere it can still emit (sg_pp_rule)
+      } else if (dt > within && (!(a.keep || back) || !L.waiting_count())) {
+        // expired everywhere it can still emit (sg_pp_rule).  A partial waiting in a count state never expires
+        // (CountPreStateProcessor.java:53-93) and walks on -- but only a later row back inside `within` of e1 could
+        // complete it: with no push after this one (no carry) and a key whose time never goes back here, none can
         done = true;
       } else {
         const int em = L.step(q);
@@ -705,6 +712,7 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
           q = p + 1;
           p0 = p;
           e = end[k];
+          back = a.kback && a.kback[k];
         }
       }
       nxt += __popcll(dm);
@@ -1679,7 +1687,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   if (ncand) {
     const int64_t wcands = PP_WAVE_CANDS;
     const dim3 gl((unsigned)((ncand + wcands * (PP_BLOCK / 64) - 1) / (wcands * (PP_BLOCK / 64))));
-    if (ps->pp_small && lanes_fast(ps))
+    if (ps->pp_small && lanes_fast(ps) && ps->shape_c3)
+      hipLaunchKernelGGL((k_pp_lanes<PpSmall, true, PpShapeC3>), gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule,
+                         cand, (int64_t)ncand, skeys, sids, end, o, wcands);
+    else if (ps->pp_small && lanes_fast(ps))
       hipLaunchKernelGGL((k_pp_lanes<PpSmall, true>), gl, dim3(PP_BLOCK), 0, st, a, P, h->ddesc, ps->drule, cand,
                          (int64_t)ncand, skeys, sids, end, o, wcands);
     else if (ps->pp_small)

@@ -123,7 +123,7 @@ struct HostPpSrc {
 };
 
 // partial-lane push (partial.hip restated on the host); returns -1 when a lane outgrows its arrays
-template <class G>
+template <class G, class SH = PpShapeAny>
 static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std::vector<uint64_t>& k1,
                    std::vector<uint64_t>& th, std::vector<uint64_t>& tl) {
   const sg_nfa_desc& d = h->d;
@@ -153,7 +153,7 @@ static int pp_push(HiHandle* h, const sg_batch* b, std::vector<char>& recs, std:
   for (size_t k = 0; k < own.size(); ++k) {
     const auto& rows = own[k];
     for (size_t p = 0; p < rows.size(); ++p) {
-      PpLane<HostPpSrc, G> L;
+      PpLane<HostPpSrc, G, false, SH> L;   // (SH: the compile-time state table when the query has one, as on the GPU)
       PpArraysT<G> arr;
       L.d = &d;
       L.ru = &ru;
@@ -411,6 +411,7 @@ int64_t hi_pp_steps(HiHandle* h, int64_t* lanes) { *lanes = h->pp_lanes; return 
 int64_t hi_pp_skipped(HiHandle* h) { return h->pp_skipped; }
 int hi_seq_rule(const sg_nfa_desc* d) { return sg_seq_rule(*d).ok; }
 int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
+int hi_pp_shape_c3(const sg_nfa_desc* d) { return sg_pp_shape_is<PpShapeC3>(*d, sg_pp_rule(*d)) ? 1 : 0; }
 // the lane kernels' FAST variant applies (chain.h sg_terms_fast): seq = 1 for the sequence-lane rule
 int hi_terms_fast(const sg_nfa_desc* d, int seq) {
   return seq ? sg_terms_fast(sg_seq_rule(*d), d->n_states) : sg_terms_fast(sg_pp_rule(*d), d->n_states);
@@ -461,8 +462,10 @@ int hi_push(HiHandle* h, const sg_batch* b) {
    if (sg_pp_rule(h->d).ok) {
     std::vector<char> recs;
     std::vector<uint64_t> k1, th, tl;
-    const int rc = sg_pp_small(sg_pp_rule(h->d), h->d) ? pp_push<PpSmall>(h, b, recs, k1, th, tl)
-                                                       : pp_push<PpBig>(h, b, recs, k1, th, tl);
+    const SgPpRule pr = sg_pp_rule(h->d);
+    const int rc = !sg_pp_small(pr, h->d)                  ? pp_push<PpBig>(h, b, recs, k1, th, tl)
+                   : sg_pp_shape_is<PpShapeC3>(h->d, pr) ? pp_push<PpSmall, PpShapeC3>(h, b, recs, k1, th, tl)
+                                                          : pp_push<PpSmall>(h, b, recs, k1, th, tl);
     if (rc < 0) { h->err = SG_EUNSUPPORTED; return SG_EUNSUPPORTED; }
     if (rc == 1) {
       const int rstride = 32 + 8 * h->d.n_select;

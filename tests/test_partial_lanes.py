@@ -180,6 +180,18 @@ def test_seq_rule_covers_the_shapes():
 
 
 
+def test_shape_specialised_lane_choice():
+    """The lane specialised to C3c's state table (chain.h PpShapeC3: unrolled state loops, folded kind branches) is
+    taken by C3c and by the c3c shape here (another window and value domain), by nothing else; the host harness runs
+    the same specialisation, so every c3c-shape test above checks it against the oracle."""
+    import ctypes as ct
+    lib = _load()
+    got = {n: lib.hi_pp_shape_c3(ct.byref(N.build_desc(L.lower(context(HEAD + q))))) for n, q in SHAPES.items()}
+    assert got == {n: int(n == "c3c") for n in SHAPES}, got
+    for cfg, ok in (("C3c", 1), ("C3b", 0), ("C2", 0)):
+        assert lib.hi_pp_shape_c3(ct.byref(N.build_desc(L.lower(context(synth.QUERIES[cfg]))))) == ok, cfg
+
+
 def test_fast_lane_variant_choice():
     """The lane kernels drop the postfix VM (chain.h sg_terms_fast) only when every filter that is not event-local is
     a list of fast compares: C3c and C3b take that variant; the shapes tests keep both variants covered on the GPU."""
