@@ -306,6 +306,23 @@ def test_gpu_jittered_pushes(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("jit", [False, True], ids=["monotone", "jittered"])
+def test_gpu_c3c_single_push_no_carry(jit):
+    """One push with no carry (the bench's per-step stream): a partial waiting in the count state stops at the window
+    when nothing after the push can revive it -- only on keys whose time never goes back in the push"""
+    from siddhi_amd._native import GpuEngine
+    from test_time_regression import jitter
+    q = synth.QUERIES["C3c"]
+    g = synth.generate("C3c", 0, 200_000, keys=500, rate=100)
+    ts = jitter(g["ts"], 1000, 23) if jit else g["ts"]
+    b = Batch(200_000, 0, ts, np.zeros(200_000, np.int32), dense_first_seen(g["key"]),
+              [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
+    want = run_engine(OracleEngine, q, [b])
+    assert len(want) > 0
+    assert_same(run_engine(lambda ctx: GpuEngine(ctx, no_carry=True), q, [b]), want)
+
+
+@pytest.mark.gpu
 def test_gpu_c3c_jittered():
     """C3c's query and generator (within 1 sec, 500 keys), rows pulled back up to 10 s, three pushes, the third starting
     2 s before the second ended"""
