@@ -140,6 +140,7 @@ struct WRec {   // wide
   uint32_t rowf;
   T val;
   static constexpr bool has_pay = false;
+  static constexpr bool narrow = false;
   __host__ __device__ int64_t t() const { return ts; }
   __host__ __device__ int64_t p(int) const { return 0; }
 };
@@ -150,6 +151,7 @@ struct WRec<T, true, 4> {   // narrow, 4-byte value: room for a 32-bit payload
   T val;
   int32_t pay;
   static constexpr bool has_pay = true;
+  static constexpr bool narrow = true;
   __host__ __device__ int64_t t() const { return dts; }
   __host__ __device__ int64_t p(int pzero) const { return pzero ? (int64_t)(uint32_t)pay : (int64_t)pay; }
 };
@@ -159,6 +161,7 @@ struct WRec<T, true, 8> {   // narrow, 8-byte value
   uint32_t rowf;
   T val;
   static constexpr bool has_pay = false;
+  static constexpr bool narrow = true;
   __host__ __device__ int64_t t() const { return dts; }
   __host__ __device__ int64_t p(int) const { return 0; }
 };
@@ -937,6 +940,7 @@ struct Walker {
   TT hts = 0;                 // register copies (valid while head != top): time of the oldest partial and
   T tv = T();                 // value of the newest one -- the common step touches no LDS for either
   int64_t prev_t;             // time of the previous row (the records' own time domain): the order check
+  int32_t prev32;             // (narrow records: their 32-bit times, compared as such)
   TT within;
   bool bad = false;
   // exact mode (a key whose time goes back; HBM list only): min / max time over the list while head != top
@@ -950,7 +954,10 @@ struct Walker {
   }
   __device__ __forceinline__ TT rel(int64_t t) const { return BIG ? (TT)t : (TT)(t - L.base); }
   // order check against the row before the replay window
-  __device__ __forceinline__ void init_prev(int64_t before) { prev_t = before; }
+  __device__ __forceinline__ void init_prev(int64_t before) {
+    prev_t = before;
+    prev32 = (int32_t)(before < INT32_MIN ? INT32_MIN : (before > INT32_MAX ? INT32_MAX : before));
+  }
   __device__ __forceinline__ TT at(uint32_t s) const {
     return BIG ? (TT)L.ts[L.ix(s)] : (TT)L.dts[L.ix(s)];
   }
@@ -978,8 +985,13 @@ struct Walker {
     // every row of the key takes part in the order check (a row that fails both filters still expires partials in
     // the reference): a key whose time goes back is redone by the exact walker
     const int64_t tabs = rc.t();
-    bad |= tabs < prev_t;
-    prev_t = tabs;
+    if constexpr (R::narrow) {   // (a narrow record's time is a 32-bit offset: one 32-bit compare)
+      bad |= rc.dts < prev32;
+      prev32 = rc.dts;
+    } else {
+      bad |= tabs < prev_t;
+      prev_t = tabs;
+    }
     if (!f) return false;
     const T x = rc.val;
     const TT t = rel(tabs);
