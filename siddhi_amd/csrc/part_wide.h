@@ -16,10 +16,18 @@ static __global__ void __launch_bounds__(256) k_hist_wide(KeyOf kf, uint32_t K, 
   __syncthreads();
   const int64_t r0 = (int64_t)j * seg1, r1 = min(nt, r0 + seg1);
   uint32_t bad = 0;
-  for (int64_t r = r0 + t; r < r1; r += 256) {
-    const uint32_t k = kf((uint32_t)r);
-    if (k < K) atomicAdd(&cnt[k >> lb], 1u);
-    else if (k != 0xffffffffu) bad |= PK_KEY_RANGE;
+  for (int64_t rb = r0; rb < r1; rb += 256 * 8) {   // eight rows per thread in flight
+    uint32_t k[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int64_t r = rb + s * 256 + t;
+      k[s] = r < r1 ? kf((uint32_t)r) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (k[s] < K) atomicAdd(&cnt[k[s] >> lb], 1u);
+      else if (k[s] != 0xffffffffu) bad |= PK_KEY_RANGE;
+    }
   }
   __syncthreads();
   for (uint32_t g = t; g < ng; g += 256) h[(size_t)g * ns1 + j] = cnt[g];
