@@ -67,6 +67,7 @@ struct PartialState {
   int pp_small = 0;             // the query fits chain.h's small lane geometry (PpSmall)
   int lanes_fast = 0;           // every filter is fast compares or event-local bits (chain.h sg_terms_fast)
   int shape_c3 = 0;             // the state table is C3c's family (chain.h PpShapeC3): the specialised lane kernel
+  int shape_c3b = 0;            // the state table is C3b's family (seq.h SqShapeC3b): the specialised sequence lanes
   size_t sq_bytes = sizeof(SeqState);
   int64_t kst_keys = 0;
   int64_t seq_pushes = 0;       // pushes that left state behind (after the first, the route cannot be left exactly)
@@ -134,6 +135,7 @@ PartialState* sg_partial_new(const sg_nfa_desc& d) {
   }
   ps->lanes_fast = (ps->mode == 2 ? sg_terms_fast(sr, d.n_states) : sg_terms_fast(ru, d.n_states)) ? 1 : 0;
   ps->shape_c3 = (ps->mode == 1 && sg_pp_shape_is<PpShapeC3>(d, ru)) ? 1 : 0;
+  ps->shape_c3b = (ps->mode == 2 && sg_sq_shape_is<SqShapeC3b>(d, sr)) ? 1 : 0;
   for (int s = 0; s < d.n_states; ++s) ps->has_count |= d.states[s].kind == SG_K_COUNT;
   for (int k = 0; k < d.n_ret; ++k) {
     const int c = d.ret_col[k];
@@ -935,15 +937,17 @@ __device__ __forceinline__ void sq_zero(T* dst) {
   for (uint32_t i = 0; i < sizeof(T) / 4; ++i) d[i] = 0;
 }
 
-struct SqEmit {   // match writer of the emitting pass
+struct SqEmit {   // match writer of the emitting pass (off: the warm-up, same code so the machine is inlined once)
+  bool on;
   const PpArgs* a;
   const DevDesc* dd;
   const uint32_t* sid;
   SqOut o;
-  int64_t slot, slot_end, r;
+  int64_t slot, slot_end;
   uint32_t key, seq, nemit, unit;
   template <class Mach>
   __device__ void operator()(Mach& mm, int p, int grp) {
+    if (!on) return;
     if (slot == slot_end) {
       slot = (int64_t)atomicAdd(o.reserved, (unsigned long long)SQ_CHUNK);
       slot_end = slot + SQ_CHUNK;
@@ -951,13 +955,15 @@ struct SqEmit {   // match writer of the emitting pass
     }
     const int64_t w = slot++;
     ++nemit;
+    const int64_t q = mm.src.base + mm.cur;   // the trigger row's sorted position; its batch row through sid
+    const int64_t r = (int64_t)sid[q] - a->nc;
     o.k1[w] = ((uint64_t)r << 16) | seq++;
     o.runit[w] = unit;
     // positions only: k_em_scatter turns them into the match record, in slot order, once the delivery order is known (one thread
     // per match instead of dependent reads in the lane's critical path)
     uint32_t* em32 = (uint32_t*)(o.rec + (size_t)w * (size_t)o.rstride);
     const int64_t pp = mm.dec(mm.M->P[p].pts);
-    em32[0] = (uint32_t)(mm.src.base + mm.cur);
+    em32[0] = (uint32_t)q;
     em32[1] = (uint32_t)(r + a->nc);
     em32[2] = key;
     em32[3] = (1u << 24) | (uint32_t)grp;
@@ -968,18 +974,12 @@ struct SqEmit {   // match writer of the emitting pass
     }
   }
 };
-struct SqNoEmit {
-  template <class Mach>
-  __device__ void operator()(Mach&, int, int) {}
-};
 
 // rows [q0, q1) of a key whose positions start at b0; emit != null: the emitting pass
 template <class E, class Mach>
-__device__ __forceinline__ void sq_run(Mach& m, int64_t b0, int64_t q0, int64_t q1, E& emit,
-                                       const uint32_t* __restrict__ sid, int64_t nc, int64_t* rcur, uint32_t* seq) {
+__device__ __forceinline__ void sq_run(Mach& m, int64_t b0, int64_t q0, int64_t q1, E& emit, uint32_t* seq) {
   m.begin();
   for (int64_t q = q0; q < q1 && !m.failed; ++q) {
-    if (rcur) *rcur = (int64_t)sid[q] - nc;
     if (seq) *seq = 0;
     m.receive(q - b0, emit);
   }
@@ -1002,7 +1002,7 @@ __device__ __forceinline__ void sq_run(Mach& m, int64_t b0, int64_t q0, int64_t 
   }
 
 // pass A: every unit from its (guessed) start state, emitting; its start and end states are kept for the check
-template <class G, bool FAST = false>
+template <class G, bool FAST = false, class SH = SqShapeAny>
 __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, const DevDesc* __restrict__ ddg,
                                                       const SgSeqRule* __restrict__ rug, const uint32_t* __restrict__ sid,
                                                       SqPlan pl_, SqOut o) {
@@ -1014,22 +1014,21 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
   const int64_t b0 = pl_.beg[k], e0 = pl_.end[k];
   const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
   SeqStateT<G>& M = lanes[threadIdx.x];
-  SeqMachine<SeqSrcD, G, FAST> m;
+  SeqMachine<SeqSrcD, G, FAST, SH> m;
   m.d = &dl;
   m.ru = &rl;
   m.src = SeqSrcD{&pl, b0};
   m.M = &M;
   m.cur = 0;
-  SqNoEmit ne;
+  int64_t q0 = s0;
   if (c == 0) {
     sq_copy(&M, (const SeqStateT<G>*)pl_.kst + k);
   } else {
     sq_zero(&M);
-    const int64_t w0 = s0 - pl_.W > b0 ? s0 - pl_.W : b0;
-    sq_run(m, b0, w0, s0, ne, sid, a.nc, nullptr, nullptr);
+    q0 = s0 - pl_.W > b0 ? s0 - pl_.W : b0;
   }
-  sq_copy((SeqStateT<G>*)pl_.ust + u, &M);
   SqEmit em;
+  em.on = false;
   em.a = &a;
   em.dd = &dl;
   em.sid = sid;
@@ -1038,9 +1037,22 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_spec(PpArgs a, PpPacked P, cons
   em.key = k;
   em.nemit = 0;
   em.seq = 0;
-  em.r = 0;
   em.unit = (uint32_t)u;
-  sq_run(m, b0, s0, s1, em, sid, a.nc, &em.r, &em.seq);
+  // one loop over the warm-up rows [q0, s0) (emitter off) and the unit's rows [s0, s1): one inlined machine
+  bool started = false;
+  m.begin();
+  for (int64_t q = q0; q < s1 && !m.failed; ++q) {
+    if (q == s0) {
+      m.finish();
+      sq_copy((SeqStateT<G>*)pl_.ust + u, &M);
+      started = true;
+      em.on = true;
+    }
+    em.seq = 0;
+    m.receive(q - b0, em);
+  }
+  m.finish();
+  if (!started) sq_copy((SeqStateT<G>*)pl_.ust + u, &M);   // (a warm-up that failed: the push is rerun elsewhere)
   for (int64_t q = em.slot; q < em.slot_end && q < o.cap; ++q) o.k1[q] = o.k1_none;
   if (em.nemit) atomicAdd(o.count, (unsigned long long)em.nemit);
   if (m.failed) atomicCAS(o.fail, 0, m.failed);
@@ -1078,7 +1090,7 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const
   em.key = (uint32_t)k;
   em.nemit = 0;
   em.seq = 0;
-  em.r = 0;
+  em.on = true;
   uint32_t reruns = 0;
   for (uint32_t u = u0 + 1; u < u1; ++u) {
     if (sg_seq_equiv(((const SeqStateT<G>*)pl_.ust)[u], ((const SeqStateT<G>*)pl_.uen)[u - 1], dl, rl)) continue;
@@ -1088,7 +1100,7 @@ __global__ void __launch_bounds__(SQ_BLOCK) k_sq_fix(PpArgs a, PpPacked P, const
     const int64_t c = u - u0;
     const int64_t s0 = b0 + pl_.ncar[k] + c * pl_.R, s1 = s0 + pl_.R < e0 ? s0 + pl_.R : e0;
     sq_copy(&M, (const SeqStateT<G>*)pl_.uen + (u - 1));
-    sq_run(m, b0, s0, s1, em, sid, a.nc, &em.r, &em.seq);
+    sq_run(m, b0, s0, s1, em, &em.seq);
     if (m.failed) { atomicCAS(o.fail, 0, m.failed); return; }
     sq_copy((SeqStateT<G>*)pl_.uen + u, &M);
   }
@@ -1244,6 +1256,11 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   // ---- unit plan
   SqPlan pl_;
   const int64_t H = ps->srule.horizon;
+  // the speculative pass's kernel variant
+  const void* spec_fn = ps->sq_small && lanes_fast(ps) && ps->shape_c3b ? (const void*)k_sq_spec<SqSmall, true, SqShapeC3b>
+                        : ps->sq_small && lanes_fast(ps)                ? (const void*)k_sq_spec<SqSmall, true>
+                        : ps->sq_small                                  ? (const void*)k_sq_spec<SqSmall>
+                                                                        : (const void*)k_sq_spec<SqBig>;
   pl_.R = std::max<int64_t>(64, (n + 262143) / 262144);
   if (h->opt.chunk_rows > 0) pl_.R = h->opt.chunk_rows;
   pl_.W = std::max<int64_t>(4 * H, 16);
@@ -1297,10 +1314,14 @@ static int seq_lanes_push(SgHandle* h, PartialState* ps, const BatchView& bv, in
   HIPCHK(hipMemsetAsync(o.rerun, 0, 4 * ((size_t)U + 1), st));
   if (attempt) HIPCHK(hipMemsetAsync(o.reserved, 0, 64, st));
   h->kbeg("sequence_lanes");
-  if (U && ps->sq_small && lanes_fast(ps))
-    hipLaunchKernelGGL((k_sq_spec<SqSmall, true>), gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
-  else if (U && ps->sq_small) hipLaunchKernelGGL(k_sq_spec<SqSmall>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
-  else if (U) hipLaunchKernelGGL(k_sq_spec<SqBig>, gu, dim3(SQ_BLOCK), 0, st, a, P, h->ddesc, ps->dsrule, sids, pl_, o);
+  if (U) {
+    const DevDesc* dd_ = h->ddesc;
+    const SgSeqRule* ru_ = ps->dsrule;
+    PpArgs a_ = a;
+    PpPacked P_ = P;
+    void* args[] = {&a_, &P_, &dd_, &ru_, &sids, &pl_, &o};
+    HIPCHK(hipLaunchKernel(spec_fn, gu, dim3(SQ_BLOCK), args, 0, st));
+  }
   HIPCHK(hipGetLastError());
   h->kend();
   h->kbeg("sequence_fix");
@@ -1566,10 +1587,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
       rec_mode = false;
       HIPCHK(hipMemsetAsync(err, 0, 8, st));
     } else {
-      if (ps->mode == 2) {   // sequence lanes read timestamps and the other slots only for matches: lazily
-        P.ts = nullptr;
-        for (int k = 0; k < d.n_ret; ++k) if (ps->hot[k] < 0) P.val[k] = nullptr;
-      }
+      // the lanes read only the record's hot slots (every slot a non-local filter reads); the others are read for
+      // matches only, lazily at record build.  Sequence lanes read timestamps only for matches as well.
+      if (ps->mode == 2) P.ts = nullptr;
+      for (int k = 0; k < d.n_ret; ++k) if (ps->hot[k] < 0) P.val[k] = nullptr;
       h->kbeg("pack");
       hipLaunchKernelGGL(k_pp_unpack, grs, blk, 0, st, a, bv.cols, cc, h->ddesc, ra, skeys, srecs, P, sids, flag);
       HIPCHK(hipGetLastError());

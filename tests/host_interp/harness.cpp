@@ -262,7 +262,7 @@ struct HostSeqSrc {
   }
 };
 
-template <class G>
+template <class G, class SH = SqShapeAny>
 static int seq_push(HiHandle* h, std::vector<SeqStateT<G>>& states, const sg_batch* b, std::vector<char>& recs,
                     std::vector<uint64_t>& k1) {
   const sg_nfa_desc& d = h->d;
@@ -294,7 +294,7 @@ static int seq_push(HiHandle* h, std::vector<SeqStateT<G>>& states, const sg_bat
     const int64_t nk = (int64_t)rows.size();
     if (!nk) continue;
     SeqStateT<G>& st = next_state[k];
-    SeqMachine<HostSeqSrc, G> m;
+    SeqMachine<HostSeqSrc, G, false, SH> m;
     m.d = &d;
     m.ru = &ru;
     m.src = HostSeqSrc{src, &rows};
@@ -304,7 +304,7 @@ static int seq_push(HiHandle* h, std::vector<SeqStateT<G>>& states, const sg_bat
     if (ncar[k] == 0) { memset(&st, 0, sizeof(st)); next_state[k] = st; }   // a key without state starts zeroed
     uint32_t seq = 0;
     int64_t crow = -1;
-    auto emit = [&](SeqMachine<HostSeqSrc, G>& mm, int p, int grp) {
+    auto emit = [&](SeqMachine<HostSeqSrc, G, false, SH>& mm, int p, int grp) {
       const int64_t r = crow;
       k1.push_back(((uint64_t)r << 16) | seq++);
       const size_t o = recs.size();
@@ -328,7 +328,7 @@ static int seq_push(HiHandle* h, std::vector<SeqStateT<G>>& states, const sg_bat
       }
       memcpy(rec + 16, h32, 16);
     };
-    auto noemit = [&](SeqMachine<HostSeqSrc, G>&, int, int) {};
+    auto noemit = [&](SeqMachine<HostSeqSrc, G, false, SH>&, int, int) {};
     // run rows [a, b) from the state in `st` (the machine's M), emitting or not
     auto run = [&](int64_t a, int64_t b2, bool emitting) {
       m.begin();
@@ -412,6 +412,7 @@ int64_t hi_pp_skipped(HiHandle* h) { return h->pp_skipped; }
 int hi_seq_rule(const sg_nfa_desc* d) { return sg_seq_rule(*d).ok; }
 int hi_pp_rule(const sg_nfa_desc* d) { return sg_pp_rule(*d).ok; }
 int hi_pp_shape_c3(const sg_nfa_desc* d) { return sg_pp_shape_is<PpShapeC3>(*d, sg_pp_rule(*d)) ? 1 : 0; }
+int hi_sq_shape_c3b(const sg_nfa_desc* d) { return sg_sq_shape_is<SqShapeC3b>(*d, sg_seq_rule(*d)) ? 1 : 0; }
 // the lane kernels' FAST variant applies (chain.h sg_terms_fast): seq = 1 for the sequence-lane rule
 int hi_terms_fast(const sg_nfa_desc* d, int seq) {
   return seq ? sg_terms_fast(sg_seq_rule(*d), d->n_states) : sg_terms_fast(sg_pp_rule(*d), d->n_states);
@@ -444,7 +445,10 @@ int hi_push(HiHandle* h, const sg_batch* b) {
     const std::vector<SeqState> before_st = h->seq_state;
     const std::vector<SeqStateT<SqSmall>> before_s = h->seq_state_s;
     const bool small = sg_seq_small(sg_seq_rule(h->d), h->d);
-    if (small ? seq_push(h, h->seq_state_s, b, recs, k1) : seq_push(h, h->seq_state, b, recs, k1)) {
+    // (partial.hip's kernel choice: the specialised machine for C3b's family in the small geometry)
+    const bool c3b = small && sg_sq_shape_is<SqShapeC3b>(h->d, sg_seq_rule(h->d));
+    if (c3b ? seq_push<SqSmall, SqShapeC3b>(h, h->seq_state_s, b, recs, k1)
+            : small ? seq_push(h, h->seq_state_s, b, recs, k1) : seq_push(h, h->seq_state, b, recs, k1)) {
       const int rstride = 32 + 8 * h->d.n_select;
       std::vector<size_t> idx(k1.size());
       for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;

@@ -44,6 +44,8 @@ def _load():
         lib.hi_pp_rule.argtypes = [P]
         lib.hi_pp_shape_c3.restype = ct.c_int
         lib.hi_pp_shape_c3.argtypes = [P]
+        lib.hi_sq_shape_c3b.restype = ct.c_int
+        lib.hi_sq_shape_c3b.argtypes = [P]
         lib.hi_seq_rule.restype = ct.c_int
         lib.hi_seq_rule.argtypes = [P]
         lib.hi_terms_fast.restype = ct.c_int

@@ -192,6 +192,18 @@ def test_shape_specialised_lane_choice():
         assert lib.hi_pp_shape_c3(ct.byref(N.build_desc(L.lower(context(synth.QUERIES[cfg]))))) == ok, cfg
 
 
+def test_sequence_shape_specialised_choice():
+    """The sequence machine specialised to C3b's state table (seq.h SqShapeC3b) is taken by C3b and by seq_c3b here
+    (other counts and thresholds), by nothing else; the host harness runs the same specialisation, so every seq_c3b
+    test checks it against the oracle."""
+    import ctypes as ct
+    lib = _load()
+    got = {n: lib.hi_sq_shape_c3b(ct.byref(N.build_desc(L.lower(context(HEAD + q))))) for n, q in SEQ_SHAPES.items()}
+    assert got == {n: int(n == "seq_c3b") for n in SEQ_SHAPES}, got
+    for cfg, ok in (("C3b", 1), ("C3c", 0), ("C2", 0)):
+        assert lib.hi_sq_shape_c3b(ct.byref(N.build_desc(L.lower(context(synth.QUERIES[cfg]))))) == ok, cfg
+
+
 def test_fast_lane_variant_choice():
     """The lane kernels drop the postfix VM (chain.h sg_terms_fast) only when every filter that is not event-local is
     a list of fast compares: C3c and C3b take that variant; the shapes tests keep both variants covered on the GPU."""
