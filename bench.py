@@ -545,6 +545,68 @@ def pcie_peak(dev, mib=1024, reps=5):
     return (mib << 20) / best / 1e9
 
 
+TORCHRUN_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
+                "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+
+
+def whole_node_block(args, ws, local, dev):
+    """SURVEY.md §8d whole-node rate: the 1B-event C5 stream from pinned host memory through sg_node_push"""
+    c5w = None
+    try:
+        thr = args.node_threads or max(16, min(16 * ws, len(os.sched_getaffinity(0))))
+        devs = [int(x) for x in args.c5_node_devices.split(",")] if args.c5_node_devices else list(range(ws))
+        c5w = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
+                         synth.CONFIGS["C5"][3], devs, args.c5_node_steps, thr, 0)
+        pk = pcie_peak(dev)
+        h2d_rate = c5w["h2d_GB"] / (c5w["ms_per_step"] * 1e-3)
+        c5w["pcie"] = {"h2d_GBs": round(h2d_rate, 1), "peak_h2d_GBs": round(pk, 1),
+                       "pcie_frac": round(h2d_rate / pk / max(1, len(devs)), 4),
+                       "peak_definition": "one 1 GiB pinned -> HBM copy on this box (best of 5), per GPU"}
+        shards = [int(x) for x in args.node_shards.split(",") if x] if (len(devs) == 1 and args.node_shards) else []
+        if shards:
+            table = [{"G": 1, "ms_per_step": c5w["ms_per_step"], "route_ms": c5w["route_ms"],
+                      "merge_ms": c5w["merge_ms"], "h2d_GB": c5w["h2d_GB"], "d2h_GB": c5w["d2h_GB"],
+                      "gpu_busy_ms": c5w["gpu_busy_ms"]}]
+            for G in shards:
+                r = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
+                               synth.CONFIGS["C5"][3], [devs[0]] * G, 1, thr, 0)
+                table.append({"G": G, "ms_per_step": r["ms_per_step"], "route_ms": r["route_ms"],
+                              "merge_ms": r["merge_ms"], "h2d_GB": r["h2d_GB"], "d2h_GB": r["d2h_GB"],
+                              "gpu_busy_ms": r["gpu_busy_ms"], "shard_rows": r["shard_rows"]})
+            c5w["node_shards_on_one_gpu"] = {
+                "host_threads": thr, "rows": table,
+                "note": "G shards (one sg_handle each) mapped onto device 0: route_ms / merge_ms are the host "
+                        "stages a G-GPU node runs (scatter to per-shard pinned staging, k-way merge), with "
+                        "this box's %d host threads; GPU time is serialised on one device" % thr}
+    except Exception as e:   # report, never fake
+        c5w = {"error": str(e)}
+    return c5w
+
+
+def whole_node_child(args, ws):
+    """the whole-node measurement in a child process (a fresh interpreter, not an exec of this one): rank 0 of an
+    N-GPU job drives every GPU of the node from it, and a fault on that path costs only this entry"""
+    devs = args.c5_node_devices or ",".join(str(g) for g in range(ws))
+    thr = args.node_threads or max(16, min(16 * ws, len(os.sched_getaffinity(0))))
+    cmd = [sys.executable, os.path.abspath(__file__), "--node-only", "--c5-node-steps", str(args.c5_node_steps),
+           "--c5-node-devices", devs, "--node-threads", str(thr), "--node-shards", args.node_shards if ws == 1 else ""]
+    if args.c5_events:
+        cmd += ["--c5-events", str(args.c5_events)]
+    env = {k: v for k, v in os.environ.items() if k not in TORCHRUN_ENV and not k.startswith("TORCHELASTIC")}
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "whole-node child timed out (900 s)"}
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"whole-node child exit {p.returncode}: {p.stderr[-800:]}"}
+    c5w = json.loads(lines[-1])["whole_node"]
+    if isinstance(c5w, dict):
+        c5w["process"] = "child"
+    return c5w
+
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -570,7 +632,14 @@ def main():
                     help="BASELINE configs measured beside the headline (one GPU, rank 0; '' to skip)")
     ap.add_argument("--other-steps", type=int, default=3)
     ap.add_argument("--pmc", default="", help="rocprofv3 PMC summary of this command (default profiles/r05/<cfg>_pmc.json)")
+    ap.add_argument("--node-child", type=int, default=-1,
+                    help="run the whole-node pipeline in a child process (-1: when N > 1, so a fault on the multi-GPU "
+                         "exchange path cannot take the headline line with it)")
+    ap.add_argument("--node-only", action="store_true", help=argparse.SUPPRESS)   # (the child's mode)
     args = ap.parse_args()
+    if args.node_only:
+        print(json.dumps({"whole_node": whole_node_block(args, 1, 0, torch.device("cuda", 0))}))
+        return
 
     ws, rank, local = dist_env()
     torch.cuda.set_device(local)
@@ -612,34 +681,8 @@ def main():
     c5w = None
     if args.c5_node_steps > 0:
         if rank == 0:
-            try:
-                thr = args.node_threads or max(16, min(16 * ws, len(os.sched_getaffinity(0))))
-                devs = [int(x) for x in args.c5_node_devices.split(",")] if args.c5_node_devices else list(range(ws))
-                c5w = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
-                                 synth.CONFIGS["C5"][3], devs, args.c5_node_steps, thr, 0)
-                pk = pcie_peak(dev)
-                h2d_rate = c5w["h2d_GB"] / (c5w["ms_per_step"] * 1e-3)
-                c5w["pcie"] = {"h2d_GBs": round(h2d_rate, 1), "peak_h2d_GBs": round(pk, 1),
-                               "pcie_frac": round(h2d_rate / pk / max(1, len(devs)), 4),
-                               "peak_definition": "one 1 GiB pinned -> HBM copy on this box (best of 5), per GPU"}
-                shards = [int(x) for x in args.node_shards.split(",") if x] if (ws == 1 and args.node_shards) else []
-                if shards:
-                    table = [{"G": 1, "ms_per_step": c5w["ms_per_step"], "route_ms": c5w["route_ms"],
-                              "merge_ms": c5w["merge_ms"], "h2d_GB": c5w["h2d_GB"], "d2h_GB": c5w["d2h_GB"],
-                              "gpu_busy_ms": c5w["gpu_busy_ms"]}]
-                    for G in shards:
-                        r = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
-                                       synth.CONFIGS["C5"][3], [local] * G, 1, thr, 0)
-                        table.append({"G": G, "ms_per_step": r["ms_per_step"], "route_ms": r["route_ms"],
-                                      "merge_ms": r["merge_ms"], "h2d_GB": r["h2d_GB"], "d2h_GB": r["d2h_GB"],
-                                      "gpu_busy_ms": r["gpu_busy_ms"], "shard_rows": r["shard_rows"]})
-                    c5w["node_shards_on_one_gpu"] = {
-                        "host_threads": thr, "rows": table,
-                        "note": "G shards (one sg_handle each) mapped onto device 0: route_ms / merge_ms are the host "
-                                "stages a G-GPU node runs (scatter to per-shard pinned staging, k-way merge), with "
-                                "this box's %d host threads; GPU time is serialised on one device" % thr}
-            except Exception as e:   # report, never fake
-                c5w = {"error": str(e)}
+            child = args.node_child if args.node_child >= 0 else int(ws > 1)
+            c5w = whole_node_child(args, ws) if child else whole_node_block(args, ws, local, dev)
         barrier()
     if rank != 0:
         return
