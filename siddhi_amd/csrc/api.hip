@@ -793,7 +793,7 @@ int sg_close(sg_handle* hh) {
 }
 
 // ---- snapshot / restore -------------------------------------------------------------------------
-static const char SNAP_MAGIC[8] = {'S', 'G', 'S', 'N', 'A', 'P', '0', '2'};
+static const char SNAP_MAGIC[8] = {'S', 'G', 'S', 'N', 'A', 'P', '0', '3'};   // 03: sequence-lane state layout recorded
 
 // Fingerprint of everything the persisted state's meaning depends on: the lowered query and the engine
 // route (closed form or general machine).  Field-wise, so struct padding never enters it.

@@ -1816,6 +1816,7 @@ void sg_partial_snapshot(SgHandle* h, PartialState* ps, SnapW& w) {
   const PpRows& r = ps->rows[ps->cur];
   w.pod((int32_t)ps->mode);
   if (ps->mode == 2) {   // sequence lanes: the per-key machine states as well (seq.h SeqState, positions over the rows)
+    w.pod((int64_t)ps->sq_bytes);   // (the state layout: a snapshot restores only into the same geometry)
     w.pod(ps->kst_keys);
     w.pod(ps->seq_pushes);
     if (ps->kst_keys) w.dev(ps->kst, ps->sq_bytes * (size_t)ps->kst_keys, h->stream);
@@ -1837,6 +1838,7 @@ void sg_partial_restore(SgHandle* h, PartialState* ps, SnapR& rd) {
   ps->nulls_seen = 1;   // the restored rows may hold nulls
   if (rd.pod<int32_t>() != ps->mode) throw SgError(SG_EINVAL, "snapshot: lane route differs");
   if (ps->mode == 2) {
+    if (rd.pod<int64_t>() != (int64_t)ps->sq_bytes) throw SgError(SG_EINVAL, "snapshot: sequence state layout differs");
     const int64_t keys = rd.pod<int64_t>();
     const int64_t pushes = rd.pod<int64_t>();
     if (keys < 0 || keys > ((int64_t)1 << 31)) throw SgError(SG_EINVAL, "snapshot: bad sequence state count");
