@@ -9,8 +9,8 @@ Headline workload:
 
 value (task contract: inputs already resident in HBM when the timed region starts): the stream is split by key hash
   across the N ranks (router.shard_of_torch: mix64(key) mod N, computed on the GPU; strong scaling -- the same stream
-  at every N, no data-path collective: keys never interact); each rank pushes its share in 100M-row
-  batches with per-key state carried between them, every match projected in HBM (sg_device_records, zero-copy).
+  at every N, no data-path collective: keys never interact); each rank pushes its share in 500M-row
+  batches (tests/test_push_size.py: records identical to 100M-row pushes) with per-key state carried between them, every match projected in HBM (sg_device_records, zero-copy).
   A step = the whole stream; value = 1e9 events / max-over-ranks step time.
 whole_node (SURVEY.md §8d's definition, never `value`): pinned raw host rows (64-bit symbol values) -> sg_node_push
   (native router, per-GPU chunked H2D / kernels / D2H, native merge) -> every match tuple in host memory; with the
@@ -620,7 +620,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16, help="processes for the key-sharded CPU baseline")
     ap.add_argument("--c5-events", type=int, default=0, help="events of the C5 stream (default 1e9)")
-    ap.add_argument("--c5-push-rows", type=int, default=100_000_000)
+    ap.add_argument("--c5-push-rows", type=int, default=500_000_000)
     ap.add_argument("--c5-node-steps", type=int, default=2,
                     help="steps of the 1B-event C5 stream through the node pipeline, rank 0 driving every GPU (0: skip)")
     ap.add_argument("--c5-node-devices", default="", help="devices of the whole-node pipeline (default: one per rank)")
@@ -654,7 +654,7 @@ def main():
 
     if cfg == "C5":
         # ---- value: the metric's config, inputs resident in HBM: ONE 1B-event, 1M-key stream sharded by key hash
-        # over the ranks (strong scaling), pushed in 100M-row batches with carried state
+        # over the ranks (strong scaling), pushed in 500M-row batches with carried state
         head = c5_stream(rank, ws, dev, args.steps, args.warmup, args.c5_events, args.c5_push_rows)
         value, ms_step = head["value"], head["ms_per_step"]
         roof = head.pop("roofline")
