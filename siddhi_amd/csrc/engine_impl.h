@@ -1421,6 +1421,8 @@ __global__ void __launch_bounds__(WALK_BLOCK, WRITE ? 3 : 5) k_walk_t(WalkArgs a
   }
 }
 
+#include "gwalk.h"
+
 // carry copy: one lane per key copies its surviving suffix (virtual rows) into the new carry buffers
 struct CarryBufs {
   int64_t* ts;
@@ -2043,8 +2045,193 @@ static void carry_out_rows(SgHandle* h, EveryNextState* es, int64_t nt, const Vi
   es->cur ^= 1;
 }
 
+// The group walker (gwalk.h) for a push whose partition ran pass 1 in two (more than 65,536 keys): returns 1 when it
+// delivered the push, 2 when the push needs wide records (the caller returns false), 0 when it declines -- nothing
+// was delivered and no state changed, so the caller reruns the push on the tiled path.
+struct GwPlan {
+  bool ok = false;
+  int cap = 0;
+  GwSel sel;
+};
+template <class T>
+static GwPlan gw_plan(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, uint32_t kb, const PushPlan& plan,
+                      int val_col_a, int val_col_b, bool same_col, int prog_b_len) {
+  const sg_nfa_desc& d = h->desc;
+  GwPlan g;
+  memset(&g.sel, 0, sizeof(g.sel));
+  if (!d.partitioned || !same_col || plan.e1_row || d.n_select > SG_MAX_SELECT) return g;
+  (void)val_col_b;
+  (void)prog_b_len;
+  for (int c = 0; c < d.n_cols; ++c)
+    if (bv.cols.nul[c]) return g;
+  for (int s = 0; s < d.n_select; ++s) {
+    const int src = plan.pp.src[s], kind = plan.pp.kind[s];
+    int code = -1;
+    if (kind == 2) code = 4;
+    else if (kind == 0 && src == 0) code = 0;
+    else if (kind == 1) code = src ? 2 : 1;
+    else if (kind == 3 && src == 1 && plan.pcol >= 0 && plan.pp.col[s] == plan.pcol) code = 3;
+    if (code < 0) return g;
+    g.sel.code[s] = code;
+  }
+  // ring capacity as the tiled walker picks it (rows per key per window from the push's time span)
+  int64_t tfl[2] = {0, 0};
+  hipStream_t st = h->stream;
+  HIPCHK(hipMemcpyAsync(&tfl[0], bv.ts, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const int64_t win = window_rows(kb, nc + n, d.within, tfl[1] - tfl[0]);
+  int cap = h->opt.ring_cap > 0 ? h->opt.ring_cap : pick_cap(win);
+  if (cap > 32 || cap < 2 || (cap & (cap - 1))) return g;
+  g.cap = cap;
+  g.sel.n_select = d.n_select;
+  g.sel.stride = 32 + 8 * d.n_select;
+  g.sel.vfloat = std::is_same<T, float>::value ? 1 : 0;
+  g.ok = true;
+  return g;
+}
+
+template <class T, int OP>
+static void launch_gwalk(const GwArgs& ga, uint32_t ng, hipStream_t st) {
+  constexpr int PT = 16;   // 4096-row chunks
+  const size_t lds = sizeof(GwLds<PT>) + (size_t)ga.cap * 256 * (sizeof(T) + 8);
+  HIPCHK(hipFuncSetAttribute((const void*)k_gwalk<T, OP, PT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_gwalk<T, OP, PT>), dim3(ng), dim3(256), lds, st, ga);
+  HIPCHK(hipGetLastError());
+}
+
+template <class T>
+static int run_group_walk(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, uint32_t kb, const PartPlan& pp,
+                          const uint32_t* o1, const WRec<T, true>* grec, const uint8_t* glk, uint32_t* pk_flags,
+                          const GwPlan& gp, const PushPlan& plan, const Virt& v, const SgCols& cc, int op, int stack_mode,
+                          int val_col_a, EveryNextState* es) {
+  const sg_nfa_desc& d = h->desc;
+  hipStream_t st = h->stream;
+  const int64_t nt = nc + n;
+  const uint32_t ng = (kb + 255) >> 8;
+  // per-key rows -> each key's first row in the group domain (its match-area region starts at 3x that)
+  uint32_t* kcnt = (uint32_t*)h->ws.get("gw_kcnt", sizeof(uint32_t) * ((size_t)kb + 1), st);
+  uint32_t* kbase = (uint32_t*)h->ws.get("gw_kbase", sizeof(uint32_t) * ((size_t)kb + 1), st);
+  h->kbeg("gw_count");
+  HIPCHK(hipMemsetAsync(kcnt, 0, sizeof(uint32_t) * ((size_t)kb + 1), st));
+  hipLaunchKernelGGL(k_gw_count, dim3(ng), dim3(256), 0, st, o1, pp.ns1, kb, glk, kcnt);
+  HIPCHK(hipGetLastError());
+  {
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, kcnt, kbase, (uint32_t)0, (size_t)kb + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("gw_kscan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, kcnt, kbase, (uint32_t)0, (size_t)kb + 1, rocprim::plus<uint32_t>(), st));
+  }
+  h->kend();
+  uint32_t pkf = 0;
+  int64_t t0 = 0;   // narrow records' time origin: the push's first virtual row
+  HIPCHK(hipMemcpyAsync(&pkf, pk_flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&t0, nc ? v.c_ts : v.ts, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (pkf & PK_KEY_RANGE) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+  if (pkf & PK_INTERNAL) throw SgError(SG_EINVAL, "internal: key partition offsets out of range");
+  if (pkf & PK_TS_RANGE) return 2;
+  if (pkf & PK_PAY_RANGE) return 0;   // a payload wider than 32 bits: the tiled path gathers e1 by row
+  h->mark(2);
+
+  GwArgs ga;
+  memset(&ga, 0, sizeof(ga));
+  ga.n = n;
+  ga.nc = nc;
+  ga.within = d.within;
+  ga.t0 = t0;
+  ga.K = kb;
+  ga.ns1 = pp.ns1;
+  ga.stack_mode = stack_mode;
+  ga.cap = gp.cap;
+  ga.chunk = 4096;
+  ga.carry_out = h->opt.no_carry ? 0 : 1;
+  ga.pzero = v.pfloat;
+  ga.o1 = o1;
+  ga.grec = (const PtU4*)grec;
+  ga.glk = glk;
+  ga.kbase = kbase;
+  ga.trig = (uint64_t*)h->ws.get("gw_trig", sizeof(uint64_t) * ((size_t)n + 1), st);
+  ga.area = (uint64_t*)h->ws.get("gw_area", sizeof(uint64_t) * 3 * (size_t)std::max<int64_t>(nt, 1), st);
+  uint32_t* gflags = (uint32_t*)h->ws.get("gw_flags", sizeof(uint32_t) * 2, st);
+  ga.flags = gflags;
+  ga.cv_n = gflags + 1;
+  ga.cv_cap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)kb * gp.cap));
+  ga.cv_ts = (int64_t*)h->ws.get("cv_ts", sizeof(int64_t) * (size_t)ga.cv_cap, st);
+  ga.cv_val = (int64_t*)h->ws.get("cv_val", sizeof(int64_t) * (size_t)ga.cv_cap, st);
+  ga.cv_pay = (int64_t*)h->ws.get("cv_pay", sizeof(int64_t) * (size_t)ga.cv_cap, st);
+  ga.cv_key = (int32_t*)h->ws.get("cv_key", sizeof(int32_t) * (size_t)ga.cv_cap, st);
+  HIPCHK(hipMemsetAsync(gflags, 0, sizeof(uint32_t) * 2, st));
+  HIPCHK(hipMemsetAsync(ga.trig, 0, sizeof(uint64_t) * ((size_t)n + 1), st));
+  h->kbeg("group_walk");
+  switch (op) {
+    case 2: launch_gwalk<T, 2>(ga, ng, st); break;
+    case 3: launch_gwalk<T, 3>(ga, ng, st); break;
+    case 4: launch_gwalk<T, 4>(ga, ng, st); break;
+    default: launch_gwalk<T, 5>(ga, ng, st); break;
+  }
+  h->kend();
+  uint32_t* off = (uint32_t*)h->ws.get("gw_off", sizeof(uint32_t) * ((size_t)n + 1), st);
+  h->kbeg("count_scan");
+  {
+    auto cnt_it = rocprim::make_transform_iterator(ga.trig, GwTrigCount());
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt_it, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+    void* tmp = h->ws.get("gw_scan_tmp", tb, st);
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt_it, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
+  }
+  h->kend();
+  h->mark(3);
+  uint32_t hf[2] = {0, 0}, total = 0;
+  HIPCHK(hipMemcpyAsync(hf, gflags, sizeof(hf), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&total, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (hf[0] & GW_INTERNAL) throw SgError(SG_EINVAL, "internal: group walker guard tripped");
+  if (hf[0]) return 0;   // a key whose time goes back, or a pending list beyond the LDS ring: the tiled path
+  h->split_out = 1;
+  h->mark(5);
+  if (total) {
+    char* out = h->out.reserve(total, d.n_select, st);
+    GwSel sel = gp.sel;
+    int rb = d.recv_of_stream[d.states[d.shape_args[1]].stream];
+    sel.multi = d.receivers[rb].multi;
+    sel.b_slot = 0;
+    if (sel.multi) {
+      const sg_receiver_desc& r = d.receivers[rb];
+      for (int q = 0; q < r.n; ++q)
+        if (r.pres[r.n - 1 - q] == d.shape_args[1]) sel.b_slot = q;
+    }
+    sel.pzero = v.pfloat;
+    h->kbeg("project");
+    hipLaunchKernelGGL(k_gproject, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, ga.t0, bv.base_index,
+                       bv.index, (const uint64_t*)ga.trig, (const uint32_t*)off, (const uint64_t*)ga.area, sel,
+                       (int64_t)h->out.n, out);
+    HIPCHK(hipGetLastError());
+    h->kend();
+    h->out.n += total;
+  }
+  h->mark(4);
+  if (ga.carry_out) {
+    WalkArgs wa;
+    memset(&wa, 0, sizeof(wa));
+    wa.alive = (uint32_t*)h->ws.get("alive_rows", sizeof(uint32_t), st);
+    wa.alive_n = (uint32_t*)h->ws.get("gw_alive_n", sizeof(uint32_t), st);
+    HIPCHK(hipMemsetAsync(wa.alive_n, 0, sizeof(uint32_t), st));
+    wa.cv_n = ga.cv_n;
+    wa.cv_ts = ga.cv_ts;
+    wa.cv_key = ga.cv_key;
+    wa.cv_val = ga.cv_val;
+    wa.cv_pay = ga.cv_pay;
+    carry_out_rows<T, true>(h, es, nt, v, bv, cc, wa, val_col_a, v.pcol ? plan.pcol : -1, v.pw);
+  }
+  h->last_events = n;
+  h->last_matches = total;
+  h->last_spilled = 0;
+  return 1;
+}
+
 template <class T, bool N>
-static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan plan) {
+static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan plan, bool allow_group = true) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
   const int* sa = d.shape_args;
@@ -2195,8 +2382,20 @@ static bool run_every_next(SgHandle* h, const BatchView& bv, int64_t n, PushPlan
       uint32_t* h2 = (uint32_t*)h->ws.get("part_h2", sizeof(uint32_t) * n2, st);
       uint32_t* o2 = (uint32_t*)h->ws.get("part_o2", sizeof(uint32_t) * n2, st);
       if (kb > 65536u) {
-        if constexpr (N && sizeof(R) == 16 && sizeof(T) == 4)
+        if constexpr (N && sizeof(R) == 16 && sizeof(T) == 4) {
+          // many keys: the group walker (gwalk.h) when the query and the push allow it, else the tiled path below
+          GwPlan gp;
+          const bool same = (val_col_a == val_col_b) && (pa.s_a == pa.s_b);
+          if (allow_group) gp = gw_plan<T>(h, bv, n, nc, kb, plan, val_col_a, val_col_b, same, pa.prog_b_len);
           part1_wide<T>(h, src.pk, kf, kb, nt, pp, h1, o1, grec, glk, pk_flags);
+          if (gp.ok) {
+            const int rc = run_group_walk<T>(h, bv, n, nc, kb, pp, o1, grec, glk, pk_flags, gp, plan, v, cc, op,
+                                             (same && pa.prog_b_len == 0) ? 1 : 0, val_col_a, es);
+            if (rc == 1) return true;
+            if (rc == 2) return false;
+            return run_every_next<T, N>(h, bv, n, plan, false);
+          }
+        }
       } else {
         h->kbeg("part_group");
         hipLaunchKernelGGL((k_part1<T, N>), dim3(pp.ns1), dim3(256), lds1, st, src.pk, kf, pp, nt, o1, grec, glk, pk_flags);

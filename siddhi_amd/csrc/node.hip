@@ -1033,10 +1033,17 @@ void deliver(Run& r, SgHandle& h, const Dst& dst, int64_t pos, int64_t k, int es
   h.out.n = 0;   // all consumed (the next push writes after the transpose in stream order)
   HIPCHK(hipStreamWaitEvent(h.eg.d2h, h.eg.ready[es], 0));
   int64_t bytes = 0;
+  // every D2H destination range checked on the host before it is issued: G = 1 rows [pos, pos + k) of the caller's
+  // columns (capacity r.cap), G > 1 rows of the shard's ring of M rows (at most two pieces, each inside the ring)
+  if (pos < 0 || k < 0 || (dst.M == 0 && pos + k > r.cap) || (dst.M > 0 && k > dst.M))
+    throw SgError(SG_EINVAL, "internal: node delivery range [" + std::to_string(pos) + ", " + std::to_string(pos + k) +
+                                 ") outside its destination");
   auto cp = [&](void* base, size_t off, size_t width) {
     if (!base) return;
     const int64_t p = dst.M ? pos % dst.M : pos;
     const int64_t first = dst.M ? std::min<int64_t>(k, dst.M - p) : k;
+    if (p < 0 || first < 0 || (dst.M > 0 && (p + first > dst.M || k - first > dst.M)))
+      throw SgError(SG_EINVAL, "internal: node ring delivery piece outside the ring");
     HIPCHK(hipMemcpyAsync((char*)base + width * (size_t)p, st + off, width * (size_t)first, hipMemcpyDeviceToHost, h.eg.d2h));
     if (first < k)
       HIPCHK(hipMemcpyAsync(base, st + off + width * (size_t)first, width * (size_t)(k - first), hipMemcpyDeviceToHost,
@@ -1751,6 +1758,9 @@ void x_loop(Run& r, int g, XSpec sp) {
         HIPCHK(hipEventRecord(X.ev_mfree[p], h.stream));
         HIPCHK(hipStreamWaitEvent(h.eg.d2h, X.ev_mfree[p], 0));
         int64_t bytes = 0;
+        if (o0 < 0 || o0 + mg > r.cap)
+          throw SgError(SG_EINVAL, "internal: exchange delivery rows [" + std::to_string(o0) + ", " +
+                                       std::to_string(o0 + mg) + ") beyond the output capacity");
         auto down = [&](void* dst, size_t off, size_t wd) {
           if (!dst) return;
           HIPCHK(hipMemcpyAsync((char*)dst + wd * (size_t)o0, lo.base + off, wd * (size_t)mg, hipMemcpyDeviceToHost,
@@ -1949,6 +1959,7 @@ void run_push(sg_node& nd, const sg_node_batch& b, const sg_match_columns* out, 
     hipStreamSynchronize(nd.h[s]->h.stream);
     hipStreamSynchronize(nd.cp[s]);
     if (nd.h[s]->h.eg.d2h) hipStreamSynchronize(nd.h[s]->h.eg.d2h);
+    if (xchg && nd.x[s].xs) hipStreamSynchronize(nd.x[s].xs);   // (a failed exchange loop skips its own syncs)
   }
   if (r.failed) {
     nd.broken = true;

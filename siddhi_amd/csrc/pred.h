@@ -40,6 +40,7 @@ struct RowReader {
   __device__ SgVal read(int, int, int slot, int type) { return sg_read_col(*c, ret_col[slot], type, row); }
 };
 
+template <class Stack>
 __device__ __forceinline__ bool eval_row(const PredArgs& a, const SgCols& cols, const DevDesc* dd, int64_t i,
                                          bool side_b) {
   int s = a.stream ? a.stream[i] : 0;
@@ -48,13 +49,17 @@ __device__ __forceinline__ bool eval_row(const PredArgs& a, const SgCols& cols, 
   int vc = side_b ? a.val_col_b : a.val_col_a;   // (-1: no compared-value column, the program decides on nulls)
   if (vc >= 0 && cols.nul[vc] && cols.nul[vc][i]) return false;
   RowReader rd{&cols, dd->ret_col, i};
-  return side_b ? sg_eval(dd->code + a.prog_b_off, a.prog_b_len, rd)
-                : sg_eval(dd->code + a.prog_a_off, a.prog_a_len, rd);
+  return side_b ? sg_eval<RowReader, Stack>(dd->code + a.prog_b_off, a.prog_b_len, rd)
+                : sg_eval<RowReader, Stack>(dd->code + a.prog_a_off, a.prog_a_len, rd);
 }
 
-// general: any program, scalar loads (rows 4l+s of the tile)
-static __global__ void __launch_bounds__(256) k_pred(PredArgs a, SgCols cols, const DevDesc* __restrict__ dd,
+// general: any program, scalar loads (rows 4l+s of the tile).  The VM's operand stack is D register slots, D the
+// programs' depth rounded up (sg_prog_depth, checked on the host): no private segment, so no per-queue scratch the
+// runtime keeps after the kernel.
+template <int D>
+__global__ void __launch_bounds__(256) k_pred(PredArgs a, SgCols cols, const DevDesc* __restrict__ dd,
                                               uint64_t* __restrict__ cand_m, uint64_t* __restrict__ cons_m) {
+  typedef SgRegStack<D> Stack;
   const int lane = threadIdx.x & 63;
   const int64_t ntiles = (a.n + 255) >> 8;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -65,8 +70,8 @@ static __global__ void __launch_bounds__(256) k_pred(PredArgs a, SgCols cols, co
       int64_t i = g * 256 + lane * 4 + s;
       bool ca = false, co = false;
       if (i < a.n) {
-        ca = eval_row(a, cols, dd, i, false);
-        if (!a.cons_all) co = eval_row(a, cols, dd, i, true);
+        ca = eval_row<Stack>(a, cols, dd, i, false);
+        if (!a.cons_all) co = eval_row<Stack>(a, cols, dd, i, true);
       }
       uint64_t ma = __ballot(ca);
       uint64_t mb = __ballot(co);
@@ -305,7 +310,13 @@ static void launch_pred(const sg_nfa_desc& d, const PredArgs& pa, const int32_t*
     int64_t w2 = std::min<int64_t>(ntiles, 256 * 16);
     PredArgs ga = pa;
     ga.stream = stream;
-    hipLaunchKernelGGL(k_pred, dim3((unsigned)std::max<int64_t>(1, (w2 + 3) / 4)), blk, 0, st, ga, cols, ddesc, cand_m,
-                       cons_m);
+    int depth = sg_prog_depth(d.code + pa.prog_a_off, pa.prog_a_len);
+    if (!pa.cons_all) depth = std::max(depth, sg_prog_depth(d.code + pa.prog_b_off, pa.prog_b_len));
+    const dim3 grd((unsigned)std::max<int64_t>(1, (w2 + 3) / 4));
+    if (depth <= 2) hipLaunchKernelGGL(k_pred<2>, grd, blk, 0, st, ga, cols, ddesc, cand_m, cons_m);
+    else if (depth <= 4) hipLaunchKernelGGL(k_pred<4>, grd, blk, 0, st, ga, cols, ddesc, cand_m, cons_m);
+    else if (depth <= 8) hipLaunchKernelGGL(k_pred<8>, grd, blk, 0, st, ga, cols, ddesc, cand_m, cons_m);
+    else if (depth <= SG_VM_STACK) hipLaunchKernelGGL(k_pred<SG_VM_STACK>, grd, blk, 0, st, ga, cols, ddesc, cand_m, cons_m);
+    else throw SgError(SG_EUNSUPPORTED, "predicate program deeper than the VM stack");
   }
 }

@@ -199,71 +199,107 @@ __device__ __forceinline__ SgVal sg_math(int op, int rt, const SgVal& l, const S
 
 // Postfix VM. `Reader` supplies VAR operands: SgVal read(int state, int index_in_chain, int ret_slot, int type).
 // Booleans are kept tri-state in SgVal (i = 0/1, null) so `not` of null is true (NotConditionExpressionExecutor).
+// The operand stack is a private array indexed at run time (the compiler places it in scratch), or -- when the
+// caller knows the program's depth (sg_prog_depth) -- D register slots addressed through unrolled selects, so the
+// kernel has no private segment (k_pred).
 #define SG_VM_STACK 16
-template <class Reader>
+template <int D>
+struct SgArrStack {
+  SgVal s[D];
+  __host__ __device__ __forceinline__ SgVal get(int i) const { return s[i]; }
+  __host__ __device__ __forceinline__ void set(int i, const SgVal& v) { s[i] = v; }
+};
+#if defined(__clang__)   // (ext_vector_type; the g++ host harness never instantiates it)
+template <int D>
+struct SgRegStack {   // one register vector per field: run-time indices become register moves, not scratch
+  typedef int64_t VI __attribute__((ext_vector_type(D)));
+  typedef double VD __attribute__((ext_vector_type(D)));
+  typedef int32_t VT __attribute__((ext_vector_type(D)));
+  VI i;
+  VD d;
+  VT tn;   // type | null << 16
+  __host__ __device__ __forceinline__ SgVal get(int k) const {
+    SgVal v;
+    v.i = i[k];
+    v.d = d[k];
+    const int32_t x = tn[k];
+    v.type = x & 0xffff;
+    v.null = x >> 16;
+    return v;
+  }
+  __host__ __device__ __forceinline__ void set(int k, const SgVal& v) {
+    i[k] = v.i;
+    d[k] = v.d;
+    tn[k] = (v.type & 0xffff) | (v.null << 16);
+  }
+};
+#endif
+template <class Reader, class Stack = SgArrStack<SG_VM_STACK>>
 __device__ __forceinline__ bool sg_run(const int64_t* code, int len, Reader& rd, SgVal& top) {
-  SgVal st[SG_VM_STACK];
+  Stack st;
   int sp = 0;
   int pc = 0;
   while (pc < len) {
     int op = (int)code[pc];
     switch (op) {
       case SG_OP_VAR: {
-        st[sp++] = rd.read((int)code[pc + 1], (int)code[pc + 2], (int)code[pc + 3], (int)code[pc + 4]);
+        st.set(sp++, rd.read((int)code[pc + 1], (int)code[pc + 2], (int)code[pc + 3], (int)code[pc + 4]));
         pc += 5;
         break;
       }
       case SG_OP_CONST: {
-        st[sp++] = sg_val_from_bits(code[pc + 2], (int)code[pc + 1], 0);
+        st.set(sp++, sg_val_from_bits(code[pc + 2], (int)code[pc + 1], 0));
         pc += 3;
         break;
       }
       case SG_OP_CMP: {
-        SgVal r = st[--sp];
-        SgVal l = st[--sp];
+        SgVal r = st.get(--sp);
+        SgVal l = st.get(--sp);
         SgVal o;
         o.type = SG_T_BOOL;
         o.null = 0;
         o.d = 0;
         o.i = sg_cmp((int)code[pc + 1], (int)code[pc + 2], l, r) ? 1 : 0;
-        st[sp++] = o;
+        st.set(sp++, o);
         pc += 3;
         break;
       }
       case SG_OP_AND:
       case SG_OP_OR: {
-        SgVal r = st[--sp];
-        SgVal l = st[--sp];
+        SgVal r = st.get(--sp);
+        SgVal l = st.get(--sp);
         bool lt = !l.null && l.i, rt = !r.null && r.i;
         SgVal o;
         o.type = SG_T_BOOL;
         o.null = 0;
         o.d = 0;
         o.i = (op == SG_OP_AND) ? (lt && rt) : (lt || rt);
-        st[sp++] = o;
+        st.set(sp++, o);
         pc += 1;
         break;
       }
       case SG_OP_NOT: {
-        SgVal x = st[sp - 1];
-        st[sp - 1].i = !(!x.null && x.i);
-        st[sp - 1].null = 0;
-        st[sp - 1].type = SG_T_BOOL;
+        SgVal x = st.get(sp - 1);
+        x.i = !(!x.null && x.i);
+        x.null = 0;
+        x.type = SG_T_BOOL;
+        st.set(sp - 1, x);
         pc += 1;
         break;
       }
       case SG_OP_ISNULL: {
-        SgVal x = st[sp - 1];
-        st[sp - 1].i = x.null ? 1 : 0;
-        st[sp - 1].null = 0;
-        st[sp - 1].type = SG_T_BOOL;
+        SgVal x = st.get(sp - 1);
+        x.i = x.null ? 1 : 0;
+        x.null = 0;
+        x.type = SG_T_BOOL;
+        st.set(sp - 1, x);
         pc += 1;
         break;
       }
       case SG_OP_MATH: {
-        SgVal r = st[--sp];
-        SgVal l = st[--sp];
-        st[sp++] = sg_math((int)code[pc + 1], (int)code[pc + 2], l, r);
+        SgVal r = st.get(--sp);
+        SgVal l = st.get(--sp);
+        st.set(sp++, sg_math((int)code[pc + 1], (int)code[pc + 2], l, r));
         pc += 3;
         break;
       }
@@ -272,14 +308,31 @@ __device__ __forceinline__ bool sg_run(const int64_t* code, int len, Reader& rd,
     }
   }
   if (sp <= 0) return false;
-  top = st[sp - 1];
+  top = st.get(sp - 1);
   return true;
 }
 
-template <class Reader>
+template <class Reader, class Stack = SgArrStack<SG_VM_STACK>>
 __device__ __forceinline__ bool sg_eval(const int64_t* code, int len, Reader& rd) {
   if (len <= 0) return true;
   SgVal top;
-  if (!sg_run(code, len, rd, top)) return false;
+  if (!sg_run<Reader, Stack>(code, len, rd, top)) return false;
   return !top.null && top.i != 0;
+}
+
+// Largest operand-stack depth of a postfix program (host side; 1 << 30 for an unknown opcode).
+static inline int sg_prog_depth(const int64_t* code, int len) {
+  int sp = 0, mx = 0, pc = 0;
+  while (pc < len) {
+    switch ((int)code[pc]) {
+      case SG_OP_VAR: ++sp; pc += 5; break;
+      case SG_OP_CONST: ++sp; pc += 3; break;
+      case SG_OP_CMP: case SG_OP_MATH: --sp; pc += 3; break;
+      case SG_OP_AND: case SG_OP_OR: --sp; pc += 1; break;
+      case SG_OP_NOT: case SG_OP_ISNULL: pc += 1; break;
+      default: return 1 << 30;
+    }
+    mx = sp > mx ? sp : mx;
+  }
+  return mx;
 }
