@@ -478,9 +478,11 @@ def c5_stream(rank, ws, dev, steps, warmup, total, push_rows):
     for lo in range(0, n, push_rows):
         hi = min(n, lo + push_rows)
         cp = [cat["id"].data_ptr() + 8 * lo, cat["key"].data_ptr() + 4 * lo, cat["price"].data_ptr() + 4 * lo]
+        # (one rank keeps every row: its rows' global indices are base_index + row, so the batch needs no index column;
+        #  with N ranks each rank's rows are a subsequence and carry their global indices)
         batches.append(N.make_batch(hi - lo, int(cat["gidx"][lo].item()), cat["ts"].data_ptr() + 8 * lo, 0,
                                     cat["key"].data_ptr() + 4 * lo, cp, [0, 0, 0], 1, key_bound, keep,
-                                    index=cat["gidx"].data_ptr() + 8 * lo))
+                                    index=cat["gidx"].data_ptr() + 8 * lo if ws > 1 else 0))
     stream = torch.cuda.current_stream()
     h.check(h.lib.sg_set_stream(h.h, stream.cuda_stream))
     stage = np.zeros(5)

@@ -47,7 +47,7 @@ extern "C" {
 
 /* Checked on every sg_nfa_desc and written into every snapshot.  3: sg_options.no_grow; the general route's
    snapshots carry SgGeo with off_scratch (version-2 snapshots and bindings are refused). */
-#define SG_ABI_VERSION 3
+#define SG_ABI_VERSION 4
 
 #define SG_MAX_STATES 16
 #define SG_MAX_STREAMS 16
@@ -181,6 +181,14 @@ typedef struct sg_options {
   int32_t no_grow;          /* general machine: 1 = a push that runs out of a key's pool / list / timer capacity or of
                                emission space fails with SG_ECAPACITY instead of being rolled back and rerun with 4x the
                                capacity (testing) */
+  int32_t bounded_lateness; /* partial lanes: 1 = the caller guarantees that no row arrives more than max_lateness_ms
+                               behind the largest timestamp pushed so far; a pending partial whose e1 lies further than
+                               `within` before that bound can then never emit (every state it could still reach expires
+                               it or needs a row inside `within` of e1), so it is not carried into the next push.
+                               0 (default) = no bound: every pending partial is carried, as the reference keeps it
+                               (CountPreStateProcessor never expires a count-waiting partial, CountPreStateProcessor.java:
+                               53-93), and a stream of such partials grows the carry without bound */
+  int64_t max_lateness_ms;  /* the bound when bounded_lateness = 1 (>= 0) */
 } sg_options;
 
 /* One SoA batch of input rows in arrival order.  Column c holds the typed values of (stream,attr)

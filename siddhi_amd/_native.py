@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SIDDHI_GPU_LIB") or os.path.join(HERE, "libsiddhi_gpu.so")   # override: experiments
 
 SG_MAX_STATES, SG_MAX_STREAMS, SG_MAX_SELECT, SG_MAX_RET, SG_MAX_COLS, SG_MAX_CODE = 16, 16, 32, 16, 64, 512
-SG_ABI_VERSION = 3
+SG_ABI_VERSION = 4
 
 SYMBOLS = ["sg_open", "sg_push", "sg_advance_time", "sg_pending", "sg_poll", "sg_device_records", "sg_discard",
            "sg_flush", "sg_reset", "sg_set_stream", "sg_get_timing", "sg_close", "sg_last_error", "sg_version",
@@ -62,7 +62,8 @@ class sg_options(ct.Structure):
     _fields_ = [("max_batch", I64), ("pool_partials", I32), ("pool_events", I32), ("pool_chain", I32),
                 ("list_cap", I32), ("force_general", I32), ("no_carry", I32), ("ring_cap", I32),
                 ("chunk_rows", I32), ("walker_only", I32), ("ingress_rows", I32),
-                ("partition_sort", I32), ("partial_lanes", I32), ("no_grow", I32)]
+                ("partition_sort", I32), ("partial_lanes", I32), ("no_grow", I32), ("bounded_lateness", I32),
+                ("max_lateness_ms", I64)]
 
 
 class sg_batch(ct.Structure):
@@ -580,7 +581,8 @@ class GpuEngine:
 
     def __init__(self, ctx: L.QueryContext, device: int = 0, force_general: bool = False, pool: int = 0,
                  no_carry: bool = False, ring_cap: int = 0, chunk_rows: int = 0, walker_only: bool = False,
-                 ingress_rows: int = 0, partition_sort: int = 0, partial_lanes: int = 0, no_grow: bool = False):
+                 ingress_rows: int = 0, partition_sort: int = 0, partial_lanes: int = 0, no_grow: bool = False,
+                 max_lateness_ms: int = -1):
         self.ctx = ctx
         self.nfa = L.lower(ctx)
         self.desc = build_desc(self.nfa)
@@ -594,6 +596,9 @@ class GpuEngine:
         opts.partition_sort = partition_sort
         opts.partial_lanes = partial_lanes
         opts.no_grow = 1 if no_grow else 0
+        if max_lateness_ms >= 0:   # (sg_options.bounded_lateness: pending partials that can never emit are not carried)
+            opts.bounded_lateness = 1
+            opts.max_lateness_ms = max_lateness_ms
         if pool:
             opts.pool_partials = opts.pool_events = opts.pool_chain = opts.list_cap = pool
         self.handle = Handle(self.desc, device, opts)

@@ -706,6 +706,7 @@ int sg_reset(sg_handle* hh) {
     HIPCHK(hipStreamSynchronize(h.stream));
     h.out.n = 0;
     h.pushes = 0;
+    h.ts_max_seen = INT64_MIN;
     h.bump_gen();
     sg_every_next_reset(&h);
     sg_every_absent_reset(&h);

@@ -1907,8 +1907,8 @@ static void part1_wide(SgHandle* h, const PackFn<T, true>& pk, KeyOf kf, uint32_
     h->kbeg("part_hist");
     HIPCHK(hipMemsetAsync(hA + nA - 1, 0, sizeof(uint32_t), st));
     HIPCHK(hipMemsetAsync(h1 + n1 - 1, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_part1_hist, dim3(pp.ns1), dim3(256), 0, st, kf, pa2, nt, hA, pk_flags);
-    hipLaunchKernelGGL(k_hist_wide, dim3(pp.ns1), dim3(256), 0, st, kf, kb, lb, ng, pp.seg1, pp.ns1, nt, h1, pk_flags);
+    hipLaunchKernelGGL(k_hist_wide, dim3(pp.ns1), dim3(256), 0, st, kf, kb, lb, ng, pp.seg1, pp.ns1, nt, h1, lbs, pa2.ng, hA,
+                       pk_flags);
     HIPCHK(hipGetLastError());
     scan_u32(hA, oA, nA, "part_scan_tmpA");
     scan_u32(h1, o1, n1, "part_scan_tmp");
@@ -2081,7 +2081,10 @@ static GwPlan gw_plan(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, u
   HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int64_t win = window_rows(kb, nc + n, d.within, tfl[1] - tfl[0]);
-  int cap = h->opt.ring_cap > 0 ? h->opt.ring_cap : pick_cap(win);
+  // a ring that outgrows its list is walked again on an unbounded HBM list (k_gw_redo), so the ring is sized for
+  // occupancy: 8 entries (a monotone stack over ~10 rows holds ~3) keep three workgroups per CU
+  const char* e = getenv("SG_DEBUG_GW_CAP");   // (test hook)
+  int cap = h->opt.ring_cap > 0 ? h->opt.ring_cap : (e ? atoi(e) : std::min(8, pick_cap(win)));
   if (cap > 32 || cap < 2 || (cap & (cap - 1))) return g;
   g.cap = cap;
   g.sel.n_select = d.n_select;
@@ -2091,13 +2094,31 @@ static GwPlan gw_plan(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, u
   return g;
 }
 
+template <class T, int OP, int PT, bool STACK>
+static void launch_gwalk_pt(const GwArgs& ga, uint32_t ng, hipStream_t st) {
+  const size_t lds = sizeof(GwLds<PT>) + (size_t)ga.cap * 256 * (sizeof(T) + 8);
+  HIPCHK(hipFuncSetAttribute((const void*)k_gwalk<T, OP, PT, STACK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_gwalk<T, OP, PT, STACK>), dim3(ng), dim3(256), lds, st, ga);
+  HIPCHK(hipGetLastError());
+}
+template <class T, int OP>
+static void launch_gw_redo(const GwArgs& ga, uint32_t nk, uint32_t* rows, T* hv, int32_t* ht, int32_t* hp, hipStream_t st) {
+  if (ga.stack_mode) hipLaunchKernelGGL((k_gw_redo<T, OP, true>), dim3(nk), dim3(256), 0, st, ga, rows, hv, ht, hp);
+  else hipLaunchKernelGGL((k_gw_redo<T, OP, false>), dim3(nk), dim3(256), 0, st, ga, rows, hv, ht, hp);
+  HIPCHK(hipGetLastError());
+}
 template <class T, int OP>
 static void launch_gwalk(const GwArgs& ga, uint32_t ng, hipStream_t st) {
-  constexpr int PT = 16;   // 4096-row chunks
-  const size_t lds = sizeof(GwLds<PT>) + (size_t)ga.cap * 256 * (sizeof(T) + 8);
-  HIPCHK(hipFuncSetAttribute((const void*)k_gwalk<T, OP, PT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((k_gwalk<T, OP, PT>), dim3(ng), dim3(256), lds, st, ga);
-  HIPCHK(hipGetLastError());
+  const char* e = getenv("SG_DEBUG_GW_PT");   // (test hook: rows per thread per LDS chunk)
+  const int pt = e ? atoi(e) : 8;
+  if (ga.stack_mode) {
+    if (pt == 4) launch_gwalk_pt<T, OP, 4, true>(ga, ng, st);
+    else if (pt == 12) launch_gwalk_pt<T, OP, 12, true>(ga, ng, st);
+    else if (pt == 10) launch_gwalk_pt<T, OP, 10, true>(ga, ng, st);
+    else launch_gwalk_pt<T, OP, 8, true>(ga, ng, st);
+  } else {
+    launch_gwalk_pt<T, OP, 8, false>(ga, ng, st);
+  }
 }
 
 template <class T>
@@ -2153,15 +2174,21 @@ static int run_group_walk(SgHandle* h, const BatchView& bv, int64_t n, int64_t n
   ga.kbase = kbase;
   ga.trig = (uint64_t*)h->ws.get("gw_trig", sizeof(uint64_t) * ((size_t)n + 1), st);
   ga.area = (uint64_t*)h->ws.get("gw_area", sizeof(uint64_t) * 3 * (size_t)std::max<int64_t>(nt, 1), st);
-  uint32_t* gflags = (uint32_t*)h->ws.get("gw_flags", sizeof(uint32_t) * 2, st);
+  uint32_t* gflags = (uint32_t*)h->ws.get("gw_flags", sizeof(uint32_t) * 4, st);
   ga.flags = gflags;
   ga.cv_n = gflags + 1;
-  ga.cv_cap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)kb * gp.cap));
+  ga.ovf_n = gflags + 2;
+  ga.ovf_cap = std::min<uint32_t>(kb, 1u << 16);
+  ga.ovf_keys = (uint32_t*)h->ws.get("gw_ovf_keys", sizeof(uint32_t) * ga.ovf_cap, st);
+  ga.match_n = gflags + 3;
+  // carry: at most `cap` entries per key from the LDS rings, and a redone key's whole list -- room for 4M of those
+  // (more sends the push to the tiled path)
+  ga.cv_cap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)kb * gp.cap + (1 << 22)));
   ga.cv_ts = (int64_t*)h->ws.get("cv_ts", sizeof(int64_t) * (size_t)ga.cv_cap, st);
   ga.cv_val = (int64_t*)h->ws.get("cv_val", sizeof(int64_t) * (size_t)ga.cv_cap, st);
   ga.cv_pay = (int64_t*)h->ws.get("cv_pay", sizeof(int64_t) * (size_t)ga.cv_cap, st);
   ga.cv_key = (int32_t*)h->ws.get("cv_key", sizeof(int32_t) * (size_t)ga.cv_cap, st);
-  HIPCHK(hipMemsetAsync(gflags, 0, sizeof(uint32_t) * 2, st));
+  HIPCHK(hipMemsetAsync(gflags, 0, sizeof(uint32_t) * 4, st));
   HIPCHK(hipMemsetAsync(ga.trig, 0, sizeof(uint64_t) * ((size_t)n + 1), st));
   h->kbeg("group_walk");
   switch (op) {
@@ -2171,23 +2198,34 @@ static int run_group_walk(SgHandle* h, const BatchView& bv, int64_t n, int64_t n
     default: launch_gwalk<T, 5>(ga, ng, st); break;
   }
   h->kend();
-  uint32_t* off = (uint32_t*)h->ws.get("gw_off", sizeof(uint32_t) * ((size_t)n + 1), st);
-  h->kbeg("count_scan");
-  {
-    auto cnt_it = rocprim::make_transform_iterator(ga.trig, GwTrigCount());
-    size_t tb = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt_it, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-    void* tmp = h->ws.get("gw_scan_tmp", tb, st);
-    HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt_it, off, (uint32_t)0, (size_t)n + 1, rocprim::plus<uint32_t>(), st));
-  }
-  h->kend();
-  h->mark(3);
-  uint32_t hf[2] = {0, 0}, total = 0;
+  uint32_t hf[4] = {0, 0, 0, 0}, total = 0;
   HIPCHK(hipMemcpyAsync(hf, gflags, sizeof(hf), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&total, off + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (hf[0] & GW_INTERNAL) throw SgError(SG_EINVAL, "internal: group walker guard tripped");
-  if (hf[0]) return 0;   // a key whose time goes back, or a pending list beyond the LDS ring: the tiled path
+  if (hf[0]) return 0;   // a key whose time goes back (or more ring overflows than the list holds): the tiled path
+  if (hf[2]) {
+    // keys whose pending list outgrew the LDS ring: each walked again with an unbounded HBM list
+    h->kbeg("gw_redo");
+    uint32_t* rrows = (uint32_t*)h->ws.get("gw_redo_rows", sizeof(uint32_t) * (size_t)nt, st);
+    char* rl = (char*)h->ws.get("gw_redo_list", (sizeof(T) + 8) * (size_t)nt, st);
+    T* hv = (T*)rl;
+    int32_t* ht = (int32_t*)(rl + sizeof(T) * (size_t)nt);
+    int32_t* hp = ht + nt;
+    switch (op) {
+      case 2: launch_gw_redo<T, 2>(ga, hf[2], rrows, hv, ht, hp, st); break;
+      case 3: launch_gw_redo<T, 3>(ga, hf[2], rrows, hv, ht, hp, st); break;
+      case 4: launch_gw_redo<T, 4>(ga, hf[2], rrows, hv, ht, hp, st); break;
+      default: launch_gw_redo<T, 5>(ga, hf[2], rrows, hv, ht, hp, st); break;
+    }
+    h->kend();
+    HIPCHK(hipMemcpyAsync(hf, gflags, sizeof(hf), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (hf[0] & GW_INTERNAL) throw SgError(SG_EINVAL, "internal: group walker redo guard tripped");
+    if (hf[0]) return 0;
+  }
+  h->last_spilled = hf[2];
+  total = hf[3];   // matches, counted by the walkers
+  h->mark(3);
   h->split_out = 1;
   h->mark(5);
   if (total) {
@@ -2202,12 +2240,34 @@ static int run_group_walk(SgHandle* h, const BatchView& bv, int64_t n, int64_t n
         if (r.pres[r.n - 1 - q] == d.shape_args[1]) sel.b_slot = q;
     }
     sel.pzero = v.pfloat;
+    // per-tile match counts -> tile bases (scan) -> output records per tile (block scan inside the tile)
+    const int64_t ntile = (n + 256 * GW_SCAN_R - 1) / (256 * GW_SCAN_R);
+    uint32_t* tcount = (uint32_t*)h->ws.get("gw_tcount", sizeof(uint32_t) * ((size_t)ntile + 1), st);
+    uint32_t* tbase = (uint32_t*)h->ws.get("gw_tbase", sizeof(uint32_t) * ((size_t)ntile + 1), st);
+    h->kbeg("count_scan");
+    HIPCHK(hipMemsetAsync(tcount + ntile, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_gtile_count, dim3((unsigned)ntile), dim3(256), 0, st, n, (const uint64_t*)ga.trig, tcount);
+    HIPCHK(hipGetLastError());
+    {
+      size_t tb = 0;
+      HIPCHK(rocprim::exclusive_scan(nullptr, tb, tcount, tbase, (uint32_t)0, (size_t)ntile + 1, rocprim::plus<uint32_t>(), st));
+      void* tmp = h->ws.get("gw_tscan_tmp", tb, st);
+      HIPCHK(rocprim::exclusive_scan(tmp, tb, tcount, tbase, (uint32_t)0, (size_t)ntile + 1, rocprim::plus<uint32_t>(), st));
+    }
+    h->kend();
+    uint32_t tsum = 0;
+    HIPCHK(hipMemcpyAsync(&tsum, tbase + ntile, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     h->kbeg("project");
-    hipLaunchKernelGGL(k_gproject, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, ga.t0, bv.base_index,
-                       bv.index, (const uint64_t*)ga.trig, (const uint32_t*)off, (const uint64_t*)ga.area, sel,
-                       (int64_t)h->out.n, out);
+    const size_t plds = (size_t)GW_PROJ_S * sel.stride;
+    if (plds > 65536)
+      HIPCHK(hipFuncSetAttribute((const void*)k_gscan_project, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
+    hipLaunchKernelGGL(k_gscan_project, dim3((unsigned)ntile), dim3(256), plds, st, n, ga.t0, bv.base_index, bv.index,
+                       (const uint64_t*)ga.trig, (const uint64_t*)ga.area, sel, (int64_t)h->out.n, out,
+                       (const uint32_t*)tbase);
     HIPCHK(hipGetLastError());
     h->kend();
+    HIPCHK(hipStreamSynchronize(st));
+    if (tsum != total) throw SgError(SG_EINVAL, "internal: group walker match count mismatch");
     h->out.n += total;
   }
   h->mark(4);
@@ -2226,7 +2286,6 @@ static int run_group_walk(SgHandle* h, const BatchView& bv, int64_t n, int64_t n
   }
   h->last_events = n;
   h->last_matches = total;
-  h->last_spilled = 0;
   return 1;
 }
 

@@ -48,9 +48,13 @@ struct GwArgs {
   int64_t* cv_pay;
   uint32_t* cv_n;
   uint32_t cv_cap;
-  uint32_t* flags;            // GW_ORDER | GW_OVERFLOW | GW_INTERNAL
+  uint32_t* flags;            // GW_ORDER | GW_OVERFLOW | GW_INTERNAL | GW_CARRY_FULL
+  uint32_t* ovf_keys;         // keys whose pending list outgrew the LDS ring (walked again by k_gw_redo)
+  uint32_t* ovf_n;
+  uint32_t ovf_cap;
+  uint32_t* match_n;          // matches of the push (the projection's output size)
 };
-static const uint32_t GW_ORDER = 1, GW_OVERFLOW = 2, GW_INTERNAL = 4;
+static const uint32_t GW_ORDER = 1, GW_OVERFLOW = 2, GW_INTERNAL = 4, GW_CARRY_FULL = 8;
 
 // per-key rows of every group (LDS counters over the group's in-group keys)
 static __global__ void __launch_bounds__(256) k_gw_count(const uint32_t* __restrict__ o1, uint32_t ns1, uint32_t K,
@@ -75,29 +79,167 @@ struct GwLds {
   uint32_t wsum[4];
 };
 
-template <class T, int OP, int PT>
+// Pending list of one key: an LDS ring of `cap` entries per lane (lane-strided planes: conflict-free), or -- for a key
+// whose list outgrew the ring (k_gw_redo) -- unbounded HBM planes over the key's own rows.
+template <class T>
+struct GwLdsRing {
+  T* v;
+  int32_t* t;
+  int32_t* p;
+  uint32_t cmask, lane;
+  __device__ __forceinline__ uint32_t ix(uint32_t s) const { return (s & cmask) * 256 + lane; }
+  __device__ __forceinline__ bool full(uint32_t head, uint32_t top) const { return top - head == cmask + 1; }
+};
+template <class T>
+struct GwHbmRing {
+  T* v;
+  int32_t* t;
+  int32_t* p;
+  __device__ __forceinline__ uint32_t ix(uint32_t s) const { return s; }
+  __device__ __forceinline__ bool full(uint32_t, uint32_t) const { return false; }
+};
+
+// One key's walk state and step (the reference's per-event processing of e2's pending list, see the file header).
+template <class T, int OP, bool STACK, class RING>
+struct GwLane {
+  RING R;
+  uint32_t head = 0, top = 0;
+  int32_t hts = 0, prev = INT32_MIN;
+  T tv = T();
+  bool bad = false;
+  uint64_t cur = 0;   // next free unit of the key's match-area region
+  uint32_t k = 0;
+  uint32_t nm = 0;    // matches delivered
+  // `within` compares in 32 bits: a key's times never go back on this path (such a push is redone on the tiled
+  // path), so dts - hts is a non-negative difference of two 32-bit offsets and fits an unsigned 32-bit word
+  uint32_t wi = 0;
+  // returns false when the row would overflow the ring: the lane stops and k_gw_redo walks the whole key again
+  __device__ __forceinline__ bool step(const GwArgs& a, const PtU4& q) {
+    const int32_t dts = (int32_t)q.x;
+    const uint32_t rowf = q.y;
+    T x;
+    const uint32_t xb = q.z;
+    __builtin_memcpy(&x, &xb, sizeof(T));
+    const int32_t pay = (int32_t)q.w;
+    const uint32_t f = rowf >> 30;
+    bad |= dts < prev;   // every row of the key takes part in the order check
+    prev = dts;
+    if (!f) return true;
+    const bool live = !is_nan_val<T>(x);
+    // lazy `within` expiry of the oldest partials (isExpired :102-113)
+    if (head != top && (uint32_t)(dts - hts) > wi) {
+      ++head;
+      while (head != top) {
+        hts = R.t[R.ix(head)];
+        if ((uint32_t)(dts - hts) <= wi) break;
+        ++head;
+      }
+    }
+    const uint32_t r = rowf & ROW_MASK;
+    uint32_t m = 0;
+    if ((f & F_CONS) && live) {
+      const bool emit = r >= (uint32_t)a.nc;   // a carried row completes nothing it did not complete before
+      const uint64_t hdr = cur;
+      if constexpr (STACK) {
+        // monotone stack: the completed partials are exactly a suffix, delivered oldest first
+        if (top != head && cmp_op<T>(OP, x, tv)) {
+          --top;
+          ++m;
+          while (top != head) {
+            tv = R.v[R.ix(top - 1)];
+            if (!cmp_op<T>(OP, x, tv)) break;
+            --top;
+            ++m;
+          }
+        }
+        if (emit && m) {
+          for (uint32_t e = 0; e < m; ++e) {
+            const uint32_t s = R.ix(top + e);
+            a.area[hdr + 2 + e] = (uint64_t)(uint32_t)val_bits<T>(R.v[s]) | ((uint64_t)(uint32_t)R.p[s] << 32);
+          }
+        }
+      } else {
+        uint32_t wr = head;
+        for (uint32_t s = head; s != top; ++s) {
+          const uint32_t si = R.ix(s);
+          const T e = R.v[si];
+          if (cmp_op<T>(OP, x, e)) {
+            if (emit) a.area[hdr + 2 + m] = (uint64_t)(uint32_t)val_bits<T>(e) | ((uint64_t)(uint32_t)R.p[si] << 32);
+            ++m;
+          } else {
+            if (wr != s) {
+              const uint32_t wx = R.ix(wr);
+              R.v[wx] = e;
+              R.t[wx] = R.t[si];
+              R.p[wx] = R.p[si];
+            }
+            ++wr;
+          }
+        }
+        top = wr;
+        if (head != top) {
+          hts = R.t[R.ix(head)];
+          tv = R.v[R.ix(top - 1)];
+        }
+      }
+      if (emit && m) {
+        const uint64_t b = r - (uint32_t)a.nc;
+        a.area[hdr] = (uint64_t)(uint32_t)dts | ((uint64_t)k << 32);
+        a.area[hdr + 1] = (uint64_t)(uint32_t)val_bits<T>(x) | ((uint64_t)(uint32_t)pay << 32);
+        a.trig[b] = hdr | ((uint64_t)m << 32);
+        cur = hdr + 2 + m;
+        nm += m;
+      }
+    }
+    if ((f & F_CAND) && live) {
+      if (R.full(head, top)) return false;
+      const uint32_t s = R.ix(top);
+      R.v[s] = x;
+      R.t[s] = dts;
+      R.p[s] = pay;
+      if (top == head) hts = dts;
+      tv = x;
+      ++top;
+    }
+    return true;
+  }
+  // the key's final pending list as carried value rows
+  __device__ __forceinline__ void carry(const GwArgs& a, uint32_t o) const {
+    for (uint32_t e = 0; e < top - head; ++e) {
+      const uint32_t s = R.ix(head + e);
+      a.cv_ts[o + e] = a.t0 + (int64_t)R.t[s];
+      a.cv_key[o + e] = (int32_t)k;
+      a.cv_val[o + e] = val_bits<T>(R.v[s]);
+      a.cv_pay[o + e] = a.pzero ? (int64_t)(uint32_t)R.p[s] : (int64_t)R.p[s];
+    }
+  }
+};
+
+template <class T, int OP, int PT, bool STACK>
 __global__ void __launch_bounds__(256, 1) k_gwalk(GwArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   GwLds<PT>& L = *(GwLds<PT>*)lds_raw;
-  const uint32_t cap = (uint32_t)a.cap, cmask = cap - 1;
-  T* rv = (T*)(lds_raw + sizeof(GwLds<PT>));            // ring planes [cap][256]: value, time, payload
-  int32_t* rt = (int32_t*)(rv + (size_t)cap * 256);
-  int32_t* rp = rt + (size_t)cap * 256;
+  const uint32_t cap = (uint32_t)a.cap;
   const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t g = xcd_block(blockIdx.x, gridDim.x);
   const uint32_t k = (g << 8) + t;
   const bool active = k < a.K;
   const uint32_t lo = a.o1[(size_t)g * a.ns1], hi = a.o1[(size_t)(g + 1) * a.ns1];
-  auto ix = [&](uint32_t s) { return (s & cmask) * 256 + t; };
-  // lane state: ring [head, top) -- oldest first; register copies of the oldest time and the newest value
-  uint32_t head = 0, top = 0;
-  int32_t hts = 0, prev = INT32_MIN;
-  T tv = T();
-  bool bad = false, ovf = false;
-  uint64_t cur = active ? 3ull * a.kbase[k] : 0ull;   // next free unit of the key's match-area region
+  GwLane<T, OP, STACK, GwLdsRing<T>> W;
+  W.R.v = (T*)(lds_raw + sizeof(GwLds<PT>));            // ring planes [cap][256]: value, time, payload
+  W.R.t = (int32_t*)(W.R.v + (size_t)cap * 256);
+  W.R.p = W.R.t + (size_t)cap * 256;
+  W.R.cmask = cap - 1;
+  W.R.lane = t;
+  W.k = k;
+  W.wi = a.within > 0xffffffffll ? 0xffffffffu : (uint32_t)a.within;
+  W.cur = active ? 3ull * a.kbase[k] : 0ull;
+  bool ovf = false;
   const uint32_t ROWS = 256 * PT;
   PtU4 rc[PT], rn[PT];
   uint32_t tg[PT], tn[PT];
+  // (the loads only issue here: nothing reads the registers before the next chunk's sort, so the next chunk's loads
+  // stay in flight during this chunk's walk; rows past the group's end re-read its last row and are masked at use)
   auto load = [&](uint32_t base, PtU4* r, uint32_t* d) {
     const uint32_t rows = min(ROWS, hi - base);
 #pragma unroll
@@ -105,12 +247,17 @@ __global__ void __launch_bounds__(256, 1) k_gwalk(GwArgs a) {
       const uint32_t i = w * (PT * 64) + s * 64 + lane;
       const uint32_t p = base + (i < rows ? i : rows - 1);
       r[s] = __builtin_nontemporal_load(a.grec + p);
-      const uint32_t kk = a.glk[p];
-      d[s] = i < rows ? kk : 0xffffffffu;
+      d[s] = a.glk[p];
     }
   };
   if (lo < hi) load(lo, rc, tg);
   for (uint32_t base = lo; base < hi; base += ROWS) {
+    {
+      const uint32_t rows = min(ROWS, hi - base);
+#pragma unroll
+      for (int s = 0; s < PT; ++s)
+        if (w * (PT * 64) + s * 64 + lane >= rows) tg[s] = 0xffffffffu;
+    }
     // stable counting sort of the chunk by in-group key (wave ballots rank equal keys in arrival order)
 #pragma unroll
     for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
@@ -147,105 +294,30 @@ __global__ void __launch_bounds__(256, 1) k_gwalk(GwArgs a) {
     __syncthreads();
     // walk: lane t's rows of this chunk, in arrival order
     const uint32_t i0 = L.ls[t], i1 = i0 + L.tot[t];
-    for (uint32_t i = i0; i < i1 && active && !ovf; ++i) {
-      const PtU4 q = L.stage[i];
-      const int32_t dts = (int32_t)q.x;
-      const uint32_t rowf = q.y;
-      T x;
-      const uint32_t xb = q.z;
-      __builtin_memcpy(&x, &xb, sizeof(T));
-      const int32_t pay = (int32_t)q.w;
-      const uint32_t f = rowf >> 30;
-      bad |= dts < prev;   // every row of the key takes part in the order check
-      prev = dts;
-      if (!f) continue;
-      // lazy `within` expiry of the oldest partials (isExpired :102-113)
-      if (head != top && (int64_t)dts - (int64_t)hts > a.within) {
-        ++head;
-        while (head != top) {
-          hts = rt[ix(head)];
-          if ((int64_t)dts - (int64_t)hts <= a.within) break;
-          ++head;
-        }
-      }
-      const uint32_t r = rowf & ROW_MASK;
-      const bool live = !is_nan_val<T>(x);
-      uint32_t m = 0;
-      if ((f & F_CONS) && live) {
-        const bool emit = r >= (uint32_t)a.nc;   // a carried row completes nothing it did not complete before
-        const uint64_t hdr = cur;
-        if (a.stack_mode) {
-          // monotone stack: the completed partials are exactly a suffix, delivered oldest first
-          if (top != head && cmp_op<T>(OP, x, tv)) {
-            --top;
-            ++m;
-            while (top != head) {
-              tv = rv[ix(top - 1)];
-              if (!cmp_op<T>(OP, x, tv)) break;
-              --top;
-              ++m;
-            }
-          }
-          if (emit && m) {
-            for (uint32_t e = 0; e < m; ++e) {
-              const uint32_t s = ix(top + e);
-              a.area[hdr + 2 + e] = (uint64_t)(uint32_t)val_bits<T>(rv[s]) | ((uint64_t)(uint32_t)rp[s] << 32);
-            }
-          }
-        } else {
-          uint32_t wr = head;
-          for (uint32_t s = head; s != top; ++s) {
-            const uint32_t si = ix(s);
-            const T e = rv[si];
-            if (cmp_op<T>(OP, x, e)) {
-              if (emit) a.area[hdr + 2 + m] = (uint64_t)(uint32_t)val_bits<T>(e) | ((uint64_t)(uint32_t)rp[si] << 32);
-              ++m;
-            } else {
-              if (wr != s) {
-                const uint32_t wi = ix(wr);
-                rv[wi] = e;
-                rt[wi] = rt[si];
-                rp[wi] = rp[si];
-              }
-              ++wr;
-            }
-          }
-          top = wr;
-          if (head != top) {
-            hts = rt[ix(head)];
-            tv = rv[ix(top - 1)];
-          }
-        }
-        if (emit && m) {
-          const uint64_t b = r - (uint32_t)a.nc;
-          a.area[hdr] = (uint64_t)(uint32_t)dts | ((uint64_t)k << 32);
-          a.area[hdr + 1] = (uint64_t)(uint32_t)val_bits<T>(x) | ((uint64_t)(uint32_t)pay << 32);
-          a.trig[b] = hdr | ((uint64_t)m << 32);
-          cur = hdr + 2 + m;
-        }
-      }
-      if ((f & F_CAND) && live) {
-        if (top - head == cap) { ovf = true; break; }
-        const uint32_t s = ix(top);
-        rv[s] = x;
-        rt[s] = dts;
-        rp[s] = pay;
-        if (top == head) hts = dts;
-        tv = x;
-        ++top;
-      }
-    }
+    for (uint32_t i = i0; i < i1 && active && !ovf; ++i)
+      if (!W.step(a, L.stage[i])) ovf = true;
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < PT; ++s) { rc[s] = rn[s]; tg[s] = tn[s]; }
   }
-  uint32_t fl = (bad ? GW_ORDER : 0u) | (ovf ? GW_OVERFLOW : 0u);
+  uint32_t fl = W.bad ? GW_ORDER : 0u;
   // (3 units per row bound the key's region: a header per trigger row, one unit per completed candidate row)
-  if (active && cur > 3ull * a.kbase[k + 1]) fl |= GW_INTERNAL;
+  if (active && W.cur > 3ull * a.kbase[k + 1]) fl |= GW_INTERNAL;
+  if (ovf) {   // the key's list outgrew the ring: the whole key again on an HBM list (k_gw_redo)
+    const uint32_t o = atomicAdd(a.ovf_n, 1u);
+    if (o < a.ovf_cap) a.ovf_keys[o] = k;
+    else fl |= GW_OVERFLOW;
+  }
   if (fl) atomicOr(a.flags, fl);
+  {
+    uint32_t c = (active && !ovf) ? W.nm : 0u;   // (a redone key counts its matches in k_gw_redo)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    if (lane == 0 && c) atomicAdd(a.match_n, c);
+  }
   if (!a.carry_out) return;
   // the key's final pending list is the carry: slots reserved once per wave
-  const uint32_t m = (active && !ovf) ? top - head : 0u;
+  const uint32_t m = (active && !ovf) ? W.top - W.head : 0u;
   uint32_t incl = m;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -258,60 +330,176 @@ __global__ void __launch_bounds__(256, 1) k_gwalk(GwArgs a) {
   if (lane == 63) cb = atomicAdd(a.cv_n, tot);
   cb = (uint32_t)__shfl((int)cb, 63);
   if ((uint64_t)cb + tot > (uint64_t)a.cv_cap) {
-    if (lane == 63) atomicOr(a.flags, GW_INTERNAL);
+    if (lane == 63) atomicOr(a.flags, GW_CARRY_FULL);
     return;
   }
-  const uint32_t o = cb + incl - m;
-  for (uint32_t e = 0; e < m; ++e) {
-    const uint32_t s = ix(head + e);
-    a.cv_ts[o + e] = a.t0 + (int64_t)rt[s];
-    a.cv_key[o + e] = (int32_t)k;
-    a.cv_val[o + e] = val_bits<T>(rv[s]);
-    a.cv_pay[o + e] = a.pzero ? (int64_t)(uint32_t)rp[s] : (int64_t)rp[s];
-  }
+  if (m) W.carry(a, cb + incl - m);
 }
 
-// Output records in delivery order: one thread per batch row (trigger order = arrival order); a trigger's matches
-// are read from its header in the match area and written at its scanned output slot, in pending order.
+// A key whose pending list outgrew the LDS ring, walked again from its first row with an unbounded list: one
+// workgroup per such key gathers the key's rows from its group (arrival order kept) into the key's slice of `rows`,
+// then one lane walks them with the list in HBM planes over the key's rows, rewriting the key's match-area region,
+// its trigger words and its carry from the start (same walk, same rows: the same words the first walk wrote up to
+// the overflow, then the rest).
+template <class T, int OP, bool STACK>
+__global__ void __launch_bounds__(256) k_gw_redo(GwArgs a, uint32_t* __restrict__ rows, T* __restrict__ hv,
+                                                 int32_t* __restrict__ ht, int32_t* __restrict__ hp) {
+  __shared__ uint32_t wc[4], base_s;
+  const uint32_t k = a.ovf_keys[blockIdx.x];
+  const uint32_t g = k >> 8, d = k & 255u, t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t lo = a.o1[(size_t)g * a.ns1], hi = a.o1[(size_t)(g + 1) * a.ns1];
+  const uint32_t kb = a.kbase[k], ke = a.kbase[k + 1];
+  if (t == 0) base_s = 0;
+  __syncthreads();
+  for (uint32_t p0 = lo; p0 < hi; p0 += 256) {
+    const uint32_t p = p0 + t;
+    const bool mine = p < hi && a.glk[p] == d;
+    const uint64_t bm = __ballot(mine);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    if (lane == 0) wc[w] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    uint32_t before = base_s;
+    for (uint32_t q = 0; q < w; ++q) before += wc[q];
+    if (mine && kb + before + below < ke) rows[kb + before + below] = p;
+    __syncthreads();
+    if (t == 0) base_s += wc[0] + wc[1] + wc[2] + wc[3];
+    __syncthreads();
+  }
+  if (t != 0) return;
+  if (kb + base_s != ke) { atomicOr(a.flags, GW_INTERNAL); return; }
+  GwLane<T, OP, STACK, GwHbmRing<T>> W;
+  W.R.v = hv + kb;
+  W.R.t = ht + kb;
+  W.R.p = hp + kb;
+  W.k = k;
+  W.wi = a.within > 0xffffffffll ? 0xffffffffu : (uint32_t)a.within;
+  W.cur = 3ull * kb;
+  for (uint32_t i = kb; i < ke; ++i) W.step(a, a.grec[rows[i]]);
+  uint32_t fl = W.bad ? GW_ORDER : 0u;
+  if (W.cur > 3ull * ke) fl |= GW_INTERNAL;
+  if (fl) atomicOr(a.flags, fl);
+  if (W.nm) atomicAdd(a.match_n, W.nm);
+  if (!a.carry_out) return;
+  const uint32_t m = W.top - W.head;
+  if (!m) return;
+  const uint32_t o = atomicAdd(a.cv_n, m);
+  if ((uint64_t)o + m > (uint64_t)a.cv_cap) { atomicOr(a.flags, GW_CARRY_FULL); return; }
+  W.carry(a, o);
+}
+
+// Output records in delivery order: one thread per batch row (trigger order = arrival order).  A trigger's matches
+// are read from its header in the match area (one 16-byte header + 8 bytes per match, contiguous) and assembled in
+// LDS at their position inside the block's output range, which is then stored contiguously (whole lines, 16-byte
+// stores by consecutive threads); a block whose rows deliver more than GW_PROJ_S records does it in rounds.
 struct GwSel {
   int32_t n_select, stride, multi, b_slot, pzero, vfloat;
   int32_t code[SG_MAX_SELECT];   // 0 e1 payload, 1 e1 value, 2 e2 value, 3 e2 payload, 4 null
 };
-static __global__ void __launch_bounds__(256) k_gproject(int64_t n, int64_t t0, uint64_t base_index,
-                                                         const uint64_t* __restrict__ index,
-                                                         const uint64_t* __restrict__ trig, const uint32_t* __restrict__ off,
-                                                         const uint64_t* __restrict__ area, GwSel sel, int64_t out_base,
-                                                         char* __restrict__ out) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
-  const uint64_t tw = trig[b];
-  const uint32_t m = (uint32_t)(tw >> 32);
-  if (!m) return;
-  const uint64_t u = (uint32_t)tw;
-  const uint64_t h0 = area[u], h1 = area[u + 1];
-  const int64_t ts = t0 + (int64_t)(int32_t)(uint32_t)h0;
-  const uint32_t key = (uint32_t)(h0 >> 32);
-  auto wid = [&](uint32_t bits, bool zero) { return zero ? (int64_t)bits : (int64_t)(int32_t)bits; };
-  const int64_t v2 = wid((uint32_t)h1, sel.vfloat), p2 = wid((uint32_t)(h1 >> 32), sel.pzero);
-  const uint64_t tg = index ? index[b] : base_index + (uint64_t)b;
-  const uint32_t o = off[b];
-  uint32_t nm = 0;
-  for (int s = 0; s < sel.n_select; ++s) nm |= (sel.code[s] == 4) ? 1u << s : 0u;
-  for (uint32_t q = 0; q < m; ++q) {
-    const uint64_t e = area[u + 2 + q];
-    const int64_t v1 = wid((uint32_t)e, sel.vfloat), p1 = wid((uint32_t)(e >> 32), sel.pzero);
-    int64_t* r = (int64_t*)(out + (size_t)(out_base + o + q) * sel.stride);
-    r[0] = (int64_t)tg;
-    r[1] = ts;
-    r[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (sel.multi ? (uint32_t)sel.b_slot : (0x800000u | q))) << 32));
-    r[3] = (int64_t)nm;
-    for (int s = 0; s < sel.n_select; ++s) {
-      const int c = sel.code[s];
-      r[4 + s] = c == 0 ? p1 : c == 1 ? v1 : c == 2 ? v2 : c == 3 ? p2 : 0;
+static const int GW_PROJ_S = 512;   // records staged per round
+static const int GW_SCAN_R = 4;     // trigger words per thread (1024 rows per tile)
+
+// matches per 1024-row tile of trigger words (the projection's tile bases come from a scan over these)
+static __global__ void __launch_bounds__(256) k_gtile_count(int64_t n, const uint64_t* __restrict__ trig,
+                                                            uint32_t* __restrict__ tcount) {
+  __shared__ uint32_t red[4];
+  const int64_t r0 = (int64_t)blockIdx.x * (256 * GW_SCAN_R);
+  uint32_t c = 0;
+#pragma unroll
+  for (int s = 0; s < GW_SCAN_R; ++s) {
+    const int64_t r = r0 + s * 256 + threadIdx.x;
+    if (r < n) c += (uint32_t)(__builtin_nontemporal_load(trig + r) >> 32);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tcount[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Output records: one workgroup per 1024-row tile (4 consecutive rows per thread), its first output slot from the
+// scanned tile counts, each row's from a block scan; the tile's records are assembled in LDS in slot order and stored
+// contiguously (GW_PROJ_S records per round).
+static __global__ void __launch_bounds__(256) k_gscan_project(int64_t n, int64_t t0, uint64_t base_index,
+                                                              const uint64_t* __restrict__ index,
+                                                              const uint64_t* __restrict__ trig,
+                                                              const uint64_t* __restrict__ area, GwSel sel,
+                                                              int64_t out_base, char* __restrict__ out,
+                                                              const uint32_t* __restrict__ tbase) {
+  extern __shared__ __attribute__((aligned(16))) char stage[];
+  __shared__ uint32_t wsum[4];
+  const uint32_t t = threadIdx.x;
+  const uint32_t tile = blockIdx.x;
+  const int64_t r0 = (int64_t)tile * (256 * GW_SCAN_R) + (int64_t)t * GW_SCAN_R;
+  uint64_t tw[GW_SCAN_R];
+  if (r0 + GW_SCAN_R <= n) {
+    typedef uint64_t U2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int s = 0; s < GW_SCAN_R; s += 2) {
+      const U2 x = __builtin_nontemporal_load((const U2*)(trig + r0 + s));
+      tw[s] = x.x;
+      tw[s + 1] = x.y;
     }
+  } else {
+#pragma unroll
+    for (int s = 0; s < GW_SCAN_R; ++s) tw[s] = r0 + s < n ? trig[r0 + s] : 0ull;
+  }
+  uint32_t sum = 0;
+#pragma unroll
+  for (int s = 0; s < GW_SCAN_R; ++s) sum += (uint32_t)(tw[s] >> 32);
+  const uint32_t excl = block_excl_scan256(sum, wsum);
+  const uint32_t pre = tbase[tile];
+  const uint32_t o_lo = pre, o_hi = pre + (wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  auto wid = [&](uint32_t bits, bool zero) { return zero ? (int64_t)bits : (int64_t)(int32_t)bits; };
+  uint32_t nmask = 0;
+  for (int s = 0; s < sel.n_select; ++s) nmask |= (sel.code[s] == 4) ? 1u << s : 0u;
+  // every trigger's header and index in flight at once (random reads), before any record is built
+  uint64_t h0[GW_SCAN_R], h1[GW_SCAN_R], tg[GW_SCAN_R];
+#pragma unroll
+  for (int s = 0; s < GW_SCAN_R; ++s) {
+    const uint64_t u = (uint32_t)tw[s];
+    const bool any = (tw[s] >> 32) != 0;
+    h0[s] = any ? area[u] : 0ull;
+    h1[s] = any ? area[u + 1] : 0ull;
+    tg[s] = (any && index) ? index[r0 + s] : base_index + (uint64_t)(r0 + s);
+  }
+  typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+  for (uint32_t sub = o_lo; sub < o_hi; sub += GW_PROJ_S) {
+    const uint32_t se = (o_hi - sub < (uint32_t)GW_PROJ_S) ? o_hi : sub + GW_PROJ_S;
+    uint32_t o = pre + excl;
+#pragma unroll
+    for (int s = 0; s < GW_SCAN_R; ++s) {
+      const uint32_t m = (uint32_t)(tw[s] >> 32);
+      if (m && o < se && o + m > sub) {
+        const uint64_t u = (uint32_t)tw[s];
+        const int64_t ts = t0 + (int64_t)(int32_t)(uint32_t)h0[s];
+        const uint32_t key = (uint32_t)(h0[s] >> 32);
+        const int64_t v2 = wid((uint32_t)h1[s], sel.vfloat), p2 = wid((uint32_t)(h1[s] >> 32), sel.pzero);
+        const uint32_t qa = o < sub ? sub - o : 0u, qe = (o + m > se) ? se - o : m;
+        for (uint32_t q = qa; q < qe; ++q) {
+          const uint64_t e = area[u + 2 + q];
+          const int64_t v1 = wid((uint32_t)e, sel.vfloat), p1 = wid((uint32_t)(e >> 32), sel.pzero);
+          int64_t* r = (int64_t*)(stage + (size_t)(o + q - sub) * sel.stride);
+          r[0] = (int64_t)tg[s];
+          r[1] = ts;
+          r[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (sel.multi ? (uint32_t)sel.b_slot : (0x800000u | q))) << 32));
+          r[3] = (int64_t)nmask;
+          for (int c = 0; c < sel.n_select; ++c) {
+            const int code = sel.code[c];
+            r[4 + c] = code == 0 ? p1 : code == 1 ? v1 : code == 2 ? v2 : code == 3 ? p2 : 0;
+          }
+        }
+      }
+      o += m;
+    }
+    __syncthreads();
+    const size_t bytes = (size_t)(se - sub) * sel.stride;
+    char* dst = out + (size_t)(out_base + sub) * sel.stride;
+    if ((((uintptr_t)dst) & 15) == 0) {
+      for (size_t x = (size_t)t * 16; x < bytes; x += 256 * 16) *(U4*)(dst + x) = *(const U4*)(stage + x);
+    } else {
+      for (size_t x = (size_t)t * 8; x < bytes; x += 256 * 8) *(uint64_t*)(dst + x) = *(const uint64_t*)(stage + x);
+    }
+    __syncthreads();
   }
 }
 
-struct GwTrigCount {
-  __host__ __device__ uint32_t operator()(uint64_t x) const { return (uint32_t)(x >> 32); }
-};

@@ -6,9 +6,11 @@
 // (k_part1 with 32-bit staged keys and 16-bit in-supergroup keys); pass 1b splits each supergroup into its groups,
 // arrival order kept, straight into the group-domain positions of the per-(group, segment) histogram (o1).
 
-// per part1 segment j: rows of each group g -> h[g * ns1 + j] (up to 4096 groups, LDS counters)
+// per part1 segment j: rows of each group g -> h[g * ns1 + j] (up to 4096 groups, LDS counters), and of each
+// supergroup (2^lbs consecutive groups) -> ha[sg * ns1 + j] from the same counters (one pass over the keys)
 static __global__ void __launch_bounds__(256) k_hist_wide(KeyOf kf, uint32_t K, uint32_t lb, uint32_t ng, uint32_t seg1,
                                                           uint32_t ns1, int64_t nt, uint32_t* __restrict__ h,
+                                                          uint32_t lbs, uint32_t nsg, uint32_t* __restrict__ ha,
                                                           uint32_t* __restrict__ flags) {
   __shared__ uint32_t cnt[4096];
   const uint32_t j = blockIdx.x, t = threadIdx.x;
@@ -31,6 +33,11 @@ static __global__ void __launch_bounds__(256) k_hist_wide(KeyOf kf, uint32_t K, 
   }
   __syncthreads();
   for (uint32_t g = t; g < ng; g += 256) h[(size_t)g * ns1 + j] = cnt[g];
+  for (uint32_t sg = t; sg < nsg; sg += 256) {
+    uint32_t c = 0;
+    for (uint32_t g = sg << lbs; g < ((sg + 1) << lbs) && g < ng; ++g) c += cnt[g];
+    ha[(size_t)sg * ns1 + j] = c;
+  }
   if (bad) atomicOr(flags, bad);
 }
 

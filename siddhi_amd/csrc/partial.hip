@@ -217,6 +217,8 @@ struct PpArgs {
   uint32_t* keep;             // partial lanes: per sorted position, 1 = carried into the next push
   uint8_t* kstart;            // partial lanes: per sorted position, 1 = the carried row starts a lane
   const uint8_t* kback;       // partial lanes: per key, its time goes back somewhere in this push (carried rows included)
+  int64_t drop_before;        // partial lanes: a pending partial whose e1 is older than this is not carried
+                              // (sg_options.bounded_lateness; INT64_MIN = carry every pending partial)
 };
 
 // Key-ordered packed rows (position q = the q-th row of the key partition): what a lane reads at every step, so the
@@ -661,7 +663,8 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
         done = true;
         // still pending after the key's last row (and not finished: a partial completes at most once): the rows it
         // holds are carried, its e1 marked as the start of its lane in the next push
-        if (a.keep && !emitted && !L.overflow && !L.dead() && (L.waiting_count() || L.live_other()))
+        if (a.keep && !emitted && !L.overflow && !L.dead() && (L.waiting_count() || L.live_other()) &&
+            L.e1_ts >= a.drop_before)
           L.witnesses([&](int32_t pos, bool st) {
             atomicOr(&a.keep[pos], 1u);
             if (st) a.kstart[pos] = 1;
@@ -1478,6 +1481,24 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   a.bkey = bv.key;
   a.ckey = cr.key;
   a.cstart = ps->mode == 1 && nc > 0 ? cr.start : nullptr;
+  a.drop_before = INT64_MIN;
+  if (h->opt.bounded_lateness && n > 0 && d.within >= 0) {
+    // the largest timestamp so far; every later row is at most max_lateness_ms behind it, so a partial whose e1 is
+    // more than `within` before (that - max_lateness_ms) never sees a row it could emit at again
+    int64_t* dmax = (int64_t*)h->ws.get("pp_tsmax", sizeof(int64_t), st);
+    size_t tb = 0;
+    HIPCHK(rocprim::reduce(nullptr, tb, bv.ts, dmax, INT64_MIN, (size_t)n, rocprim::maximum<int64_t>(), st));
+    void* tmp = h->ws.get("pp_tsmax_tmp", tb, st);
+    HIPCHK(rocprim::reduce(tmp, tb, bv.ts, dmax, INT64_MIN, (size_t)n, rocprim::maximum<int64_t>(), st));
+    int64_t hm = INT64_MIN;
+    HIPCHK(hipMemcpyAsync(&hm, dmax, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    h->ts_max_seen = std::max(h->ts_max_seen, hm);
+    const int64_t lat = std::max<int64_t>(0, h->opt.max_lateness_ms);
+    const int64_t w = std::max<int64_t>(0, d.within);
+    if (h->ts_max_seen > INT64_MIN / 2 && w < (int64_t)1 << 60 && lat < (int64_t)1 << 60)
+      a.drop_before = h->ts_max_seen - lat - w;
+  }
   const SgCols cc = carried_cols(ps, cr);
   int end_bit = 1;
   while ((1ull << end_bit) <= (uint64_t)kb) ++end_bit;

@@ -112,6 +112,7 @@ struct SgHandle {
   std::vector<char> snap_cache;   // blob of the last size query (sg_snapshot), valid while gen == snap_gen
   uint64_t snap_gen = ~0ull;
   uint32_t key_bound_seen = 0;
+  int64_t ts_max_seen = INT64_MIN;   // largest timestamp pushed so far (sg_options.bounded_lateness)
   void* state = nullptr;      // per-shape persistent state (interp / absent)
   int state_kind = 0;         // 1 every->next closed form, 2 general machine, 3 absence closed form, 4 once closed form
   int split_out = 0;          // 1: output stage timed from ev[5] (host work between ev[3] and ev[5])

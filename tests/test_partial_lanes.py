@@ -14,7 +14,7 @@ from parity_util import assert_same, context, dense_first_seen, run_engine
 from siddhi_amd import _native as N
 from siddhi_amd import lowering as L
 from siddhi_amd import synth
-from siddhi_amd.runtime import Batch
+from siddhi_amd.runtime import Batch, Outputs
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "host_interp"))
 from host_engine import HostInterpEngine, _load  # noqa: E402
@@ -482,3 +482,51 @@ def test_gpu_pushes_beyond_the_row_budget_are_split(monkeypatch):
               [g["id"], g["key"], g["v"], g["w"]], [None] * 4)
     want = run_engine(OracleEngine, q, [b])
     assert_same(run_engine(GpuEngine, q, split(b, [100_000, 100_007])), want)
+
+
+def _stuck_stream(pushes, per, keys, seed):
+    """C3c's query on rows whose e1 candidates are mostly v = 999: no later row has v > 999, so each waits in the count
+    state e2<2:5> forever (CountPreStateProcessor never expires it) -- plus v = 600 candidates that do complete."""
+    rng = np.random.default_rng(seed)
+    n = pushes * per
+    v = rng.integers(0, 400, n).astype(np.int32)
+    u = rng.random(n)
+    v[u < 0.01] = 999
+    v[(u >= 0.01) & (u < 0.06)] = 600
+    v[(u >= 0.06) & (u < 0.11)] = 700
+    w = rng.integers(0, 1000, n).astype(np.int32)
+    ts = (np.int64(1_700_000_000_000) + np.arange(n, dtype=np.int64) // 20).astype(np.int64)   # 20 rows per ms
+    key = rng.integers(0, keys, n).astype(np.int32)
+    b = Batch(n, 0, ts, np.zeros(n, np.int32), dense_first_seen(key), [np.arange(n, dtype=np.int64), key, v, w],
+              [None] * 4)
+    return split(b, [per * k for k in range(1, pushes)])
+
+
+@pytest.mark.gpu
+def test_gpu_bounded_lateness_keeps_the_carry_flat():
+    """sg_options.bounded_lateness: with no row arriving behind the largest timestamp so far
+    (max_lateness_ms = 0), a partial whose e1 is more than `within` before the clock can never emit, so it is not
+    carried -- the output is the oracle's, and the carry (snapshot size) stays flat over 12 pushes while without the
+    bound it grows with every push (each stuck count-waiting partial is carried forever, as the reference keeps it)."""
+    from siddhi_amd._native import GpuEngine
+    q = synth.QUERIES["C3c"]
+    parts = _stuck_stream(12, 40_000, 100, seed=5)
+    want = run_engine(OracleEngine, q, parts)
+    assert len(want) > 100
+
+    def run(**kw):
+        eng = GpuEngine(context(q), **kw)
+        outs, sizes = [], []
+        for p in parts:
+            eng.push(p)
+            outs.append(eng.fetch())
+            sizes.append(len(eng.snapshot()))
+        eng.close()
+        return Outputs(*[np.concatenate([getattr(o, f) for o in outs]) for f in
+                         ("trigger", "ts", "key", "group", "vals", "vnull")]), sizes
+    got, flat = run(max_lateness_ms=0)
+    assert_same(got, want)
+    got2, grow = run()
+    assert_same(got2, want)
+    assert flat[-1] <= 1.3 * flat[3], flat
+    assert grow[-1] >= 2 * grow[3], grow
