@@ -46,7 +46,7 @@ from siddhi_amd import lowering as L          # noqa: E402
 from siddhi_amd import synth                  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_DIR = os.path.join(ROOT, "profiles", "r05")
+PMC_DIR = os.path.join(ROOT, "profiles", "r06")
 
 
 def barrier():
@@ -331,16 +331,21 @@ PATH_BYTES = {"C1": (12.125, 36.0, 4.125), "C2": (16.125, 36.0, 4.125), "C5": (1
 #   pred         price 4 read + condition bit 0.125 written
 #   part_hist    key 4 read
 #   part_group   ts 8 + key 4 + price 4 + id 8 + bit 0.125 read; record 16 + in-group key 1 written
-#   fgw_walk     record 16 + in-group key 1 read, count word 4 written; 16 B compact record per match written
-#   fgw_project  count word 4 read; per match: compact record 16 read, trigger's ts 8 + key 4 + id 8 + price 4
-#                read, 64 B record written
-#   (sorted-walker pipeline, used when the fused walk declines a push)
+#   part_split   record 16 + supergroup key 2 read, record 16 + in-group key 1 written
+#   gw_count     in-group key 1 read
+#   group_walk   record 16 + in-group key 1 read; per match 8 B entry + per trigger (~1.3 matches) 16 B header and an
+#                8 B trigger word written: ~26 B per match
+#   gw_tiles     trigger word 8 read
+#   gw_project   trigger word 8 read; per match its 8 B entry + the trigger's 16 B header (~12 per match) read, 64 B
+#                record written
+#   (sorted-walker pipeline: fewer than 65,536 keys (C2), or a push the group walker declines)
 #   part_key     record 16 + key 1 read, record 16 written;  units/tile_transpose  record 16 read + 16 written
 #   walk_count   record 16 read, count 4 written per match;   walk_record  record 16 read, 16 B per match written
 #   project      16 B intermediate + 24 B trigger row read, 64 B record written per match
 #   key_sort     rocPRIM onesweep over 16-B records + 4-B keys, 3 passes (C5's 1M keys), read + write
 KERNEL_BYTES = {"pred": (4.125, 0.0), "part_hist": (4.0, 0.0), "part_group": (41.125, 0.0),
-                "fgw_walk": (21.0, 16.0), "fgw_project": (4.0, 104.0), "part_key": (33.0, 0.0),
+                "group_walk": (17.0, 26.0), "gw_project": (8.0, 84.0), "gw_tiles": (8.0, 0.0), "gw_count": (1.0, 0.0),
+                "part_key": (33.0, 0.0),
                 "tile_transpose": (32.0, 0.0), "walk_count": (16.0, 4.0), "walk_record": (16.0, 16.0),
                 "project": (0.0, 104.0), "key_sort": (40.0, 0.0), "pack": (44.125, 0.0), "part_split": (35.0, 0.0),
                 "nge_search": (12.125, 8.0), "once_match": (16.125, 0.0)}
@@ -434,6 +439,61 @@ def measure_push(cfg, rank, n, keys, rate, dev, steps, warmup, sync_ranks=False)
     torch.cuda.empty_cache()
     return {"elapsed": elapsed, "stage": stage / steps, "kern": {k: v / steps for k, v in kern.items()},
             "matches": matches, "spilled": spilled}
+
+
+def stream_line(cfg, dev, steps, warmup, pushes=2, lateness=-1):
+    """A config as a stream (VERDICT r05 "next" 6): its 100M events pushed in `pushes` consecutive batches with every
+    key's pending partials carried between them (no_carry = 0) -- the streaming cost, which for count-waiting partial
+    lanes includes walking to the key's end (a count state never expires a partial, CountPreStateProcessor.java:53-93).
+    lateness >= 0 sets sg_options.bounded_lateness (the caller's bound on rows arriving behind the clock; the synthetic
+    stream is monotone), under which such a partial stops at `within` + lateness of e1."""
+    _, n_cfg, keys, rate = synth.CONFIGS[synth._base(cfg)]
+    n = min(n_cfg, 100_000_000)
+    g, key, cols = synth_columns(cfg, 0, n, keys, rate, dev)
+    torch.cuda.synchronize()
+    h, nfa = make_handle(cfg, no_carry=0)
+    if lateness >= 0:
+        h.opts.bounded_lateness = 1
+        h.opts.max_lateness_ms = lateness
+        h.close()
+        h = N.Handle(h.desc, device=torch.cuda.current_device(), options=h.opts)
+    keep, batches = [], []
+    per = (n + pushes - 1) // pushes
+    for lo in range(0, n, per):
+        hi = min(n, lo + per)
+        batches.append(N.make_batch(hi - lo, lo, g["ts"].data_ptr() + 8 * lo, 0, key.data_ptr() + 4 * lo,
+                                    [c.data_ptr() + c.element_size() * lo for c in cols], [0] * len(cols), 1, keys, keep))
+    h.check(h.lib.sg_set_stream(h.h, torch.cuda.current_stream().cuda_stream))
+    kern, matches = {}, 0
+
+    def step(record=False):
+        nonlocal matches
+        h.reset()
+        matches = 0
+        for b in batches:
+            h.push(b)
+            t = h.timing()
+            matches += t.matches
+            if record:
+                for name, ms in t.kernels():
+                    kern[name] = kern.get(name, 0.0) + ms
+            h.discard()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    ms = 1000.0 * (time.perf_counter() - t0) / steps
+    h.close()
+    del g, key, cols, batches
+    torch.cuda.empty_cache()
+    return {"workload": f"{cfg} as a stream of {pushes} pushes, state carried" +
+                        (f", bounded lateness {lateness} ms" if lateness >= 0 else ""),
+            "events": n, "pushes": pushes, "matches": int(matches), "steps": steps, "ms_per_stream": round(ms, 3),
+            "value": round(n / (ms * 1e-3), 1), "unit": "events/s",
+            "kernels_ms_per_stream": {k: round(v / steps, 3) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])[:8]}}
 
 
 CPU_SAMPLE = {"PP": 12_000_000, "PPe": 12_000_000, "C1": 1_000_000, "C2": 12_000_000, "C3b": 6_000_000, "C3c": 3_000_000, "C4": 60_000, "C5": 3_000_000}
@@ -633,6 +693,8 @@ def main():
     ap.add_argument("--other-configs", default="C2,C1,C3b,C3c,C4,PP",
                     help="BASELINE configs measured beside the headline (one GPU, rank 0; '' to skip)")
     ap.add_argument("--other-steps", type=int, default=3)
+    ap.add_argument("--stream-configs", default="C3c,C3c+bounded",
+                    help="sub-lines pushed as 2-push streams with state carried (+bounded: bounded lateness 0 ms)")
     ap.add_argument("--pmc", default="", help="rocprofv3 PMC summary of this command (default profiles/r05/<cfg>_pmc.json)")
     ap.add_argument("--node-child", type=int, default=-1,
                     help="run the whole-node pipeline in a child process (-1: when N > 1, so a fault on the multi-GPU "
@@ -716,6 +778,16 @@ def main():
                 others[oc] = config_line(oc, dev, args.other_steps, 1, not args.no_cpu)
             except Exception as e:   # report, never fake
                 others[oc] = {"error": str(e)}
+    if args.stream_configs:
+        for sc in [c for c in args.stream_configs.split(",") if c]:
+            lat = -1
+            name = sc
+            if sc.endswith("+bounded"):
+                sc, lat = sc[:-len("+bounded")], 0
+            try:
+                others[name + "_stream"] = stream_line(sc, dev, args.other_steps, 1, lateness=lat)
+            except Exception as e:   # report, never fake
+                others[name + "_stream"] = {"error": str(e)}
     line = {
         "metric": "events/sec (whole node) for partitioned pattern query at 1/2/4/8 GPUs; % HBM peak",
         "value": round(value, 1), "unit": "events/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,

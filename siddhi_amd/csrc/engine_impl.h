@@ -415,13 +415,14 @@ static __global__ void __launch_bounds__(256) k_part1_hist(KeyOf kf, PartPlan pp
 
 // pass-1 scatter: records of segment j, grouped (two passes) or final (one pass).  TG holds a staged record's key
 // (32 bits beyond 65536 keys), LK its in-group key.
-template <class T, bool N, class TG = uint16_t, class LK = uint8_t>
+template <class T, bool N, class TG = uint16_t, class LK = uint8_t, int P = PT1>
 __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPlan pp, int64_t nt,
                                                const uint32_t* __restrict__ o1, WRec<T, N>* __restrict__ orec,
                                                LK* __restrict__ olk, uint32_t* __restrict__ flags) {
   typedef WRec<T, N> R;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  PartLds<R, PT1, TG>& L = *(PartLds<R, PT1, TG>*)lds_raw;
+  PartLds<R, P, TG>& L = *(PartLds<R, P, TG>*)lds_raw;
+  constexpr uint32_t PROWS = 256 * P;
   const uint32_t j = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t lmask = (1u << pp.lb) - 1u;
   if (t < pp.ng) L.run[t] = o1[(size_t)t * pp.ns1 + j];
@@ -430,13 +431,13 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
   uint32_t bad = 0;
   // the sub-tile's loads, all issued before the first use (one memory latency per sub-tile)
   auto load = [&](int64_t base, uint32_t* tg, R* rc) {
-    const uint32_t rows = (uint32_t)((re - base < PT1_ROWS) ? re - base : PT1_ROWS);
+    const uint32_t rows = (uint32_t)((re - base < PROWS) ? re - base : PROWS);
     if (base >= (int64_t)pk.v.nc) {
       // batch rows only: branch-free loads (rows past the end re-read the last row and are dropped)
       const uint32_t b0 = (uint32_t)(base - pk.v.nc), last = rows - 1;
 #pragma unroll
-      for (int s = 0; s < PT1; ++s) {
-        const uint32_t i = w * (PT1 * 64) + s * 64 + lane;
+      for (int s = 0; s < P; ++s) {
+        const uint32_t i = w * (P * 64) + s * 64 + lane;
         const uint32_t b = b0 + (i < rows ? i : last);
         const uint32_t k = (uint32_t)pk.v.key[b];
         uint32_t bd = 0;
@@ -446,8 +447,8 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
       }
     } else {
 #pragma unroll
-      for (int s = 0; s < PT1; ++s) {
-        const uint32_t i = w * (PT1 * 64) + s * 64 + lane;
+      for (int s = 0; s < P; ++s) {
+        const uint32_t i = w * (P * 64) + s * 64 + lane;
         const uint32_t r = (uint32_t)(base + i);
         const uint32_t k = i < rows ? kf(r) : 0xffffffffu;
         tg[s] = k < pp.K ? k : 0xffffffffu;
@@ -465,20 +466,20 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
       }
     }
   };
-  uint32_t tg[PT1], tn[PT1];
-  R rc[PT1], rn[PT1];
+  uint32_t tg[P], tn[P];
+  R rc[P], rn[P];
   if (rb < re) load(rb, tg, rc);
-  for (int64_t base = rb; base < re; base += PT1_ROWS) {
+  for (int64_t base = rb; base < re; base += PROWS) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) L.cw[q][t] = 0;
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < PT1; ++s)
+    for (int s = 0; s < P; ++s)
       if (tg[s] != 0xffffffffu) atomicAdd(&L.cw[w][tg[s] >> pp.lb], 1u);
     __syncthreads();
     const uint32_t staged = part_cursors(L);
 #pragma unroll
-    for (int s = 0; s < PT1; ++s) {
+    for (int s = 0; s < P; ++s) {
       const bool valid = tg[s] != 0xffffffffu;
       const uint32_t d = valid ? tg[s] >> pp.lb : 0u;
       uint32_t rank, cnt;
@@ -490,7 +491,7 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
         L.tag[slot] = (TG)tg[s];
       }
     }
-    if (base + PT1_ROWS < re) load(base + PT1_ROWS, tn, rn);   // next sub-tile in flight during the write-out
+    if (base + PROWS < re) load(base + PROWS, tn, rn);   // next sub-tile in flight during the write-out
     __syncthreads();
     for (uint32_t q = t; q < staged; q += 256) {
       const uint32_t k = L.tag[q], d = k >> pp.lb;
@@ -502,7 +503,7 @@ __global__ void __launch_bounds__(256) k_part1(PackFn<T, N> pk, KeyOf kf, PartPl
     __syncthreads();
     L.run[t] += L.tot[t];
 #pragma unroll
-    for (int s = 0; s < PT1; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
+    for (int s = 0; s < P; ++s) { tg[s] = tn[s]; rc[s] = rn[s]; }
   }
   if (bad) atomicOr(flags, bad);
 }
@@ -1914,11 +1915,20 @@ static void part1_wide(SgHandle* h, const PackFn<T, true>& pk, KeyOf kf, uint32_
     scan_u32(h1, o1, n1, "part_scan_tmp");
     h->kend();
     h->kbeg("part_group");
-    const size_t ldsA = sizeof(PartLds<R, PT1, uint32_t>);
-    HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, true, uint32_t, uint16_t>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsA));
-    hipLaunchKernelGGL((k_part1<T, true, uint32_t, uint16_t>), dim3(pp.ns1), dim3(256), ldsA, st, pk, kf, pa2, nt, oA,
-                       grecA, glkA, pk_flags);
+    // (rows per thread per LDS sub-tile of this 256-digit pass: SG_DEBUG_P1_PT test hook)
+    const char* pe = getenv("SG_DEBUG_P1_PT");
+    const int p1 = pe ? atoi(pe) : 8;   // (C5: 8.1 -> 7.3 ms per 500M-row push against 4, profiles/r06/ab_p1.sh)
+    auto launch_a = [&](auto pt) {
+      constexpr int P = decltype(pt)::value;
+      const size_t ldsA = sizeof(PartLds<R, P, uint32_t>);
+      HIPCHK(hipFuncSetAttribute((const void*)k_part1<T, true, uint32_t, uint16_t, P>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsA));
+      hipLaunchKernelGGL((k_part1<T, true, uint32_t, uint16_t, P>), dim3(pp.ns1), dim3(256), ldsA, st, pk, kf, pa2, nt, oA,
+                         grecA, glkA, pk_flags);
+    };
+    if (p1 == 8) launch_a(std::integral_constant<int, 8>());
+    else if (p1 == 16) launch_a(std::integral_constant<int, 16>());
+    else launch_a(std::integral_constant<int, PT1>());
     HIPCHK(hipGetLastError());
     h->kend();
     h->kbeg("part_split");
@@ -2081,10 +2091,10 @@ static GwPlan gw_plan(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, u
   HIPCHK(hipMemcpyAsync(&tfl[1], bv.ts + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int64_t win = window_rows(kb, nc + n, d.within, tfl[1] - tfl[0]);
-  // a ring that outgrows its list is walked again on an unbounded HBM list (k_gw_redo), so the ring is sized for
-  // occupancy: 8 entries (a monotone stack over ~10 rows holds ~3) keep three workgroups per CU
+  // the ring as the tiled walker sizes it (a key whose list outgrows it is walked again on an unbounded list by
+  // k_gw_redo); the LDS chunk shrinks as the ring grows so two workgroups share a CU (launch_gwalk)
   const char* e = getenv("SG_DEBUG_GW_CAP");   // (test hook)
-  int cap = h->opt.ring_cap > 0 ? h->opt.ring_cap : (e ? atoi(e) : std::min(8, pick_cap(win)));
+  int cap = h->opt.ring_cap > 0 ? h->opt.ring_cap : (e ? atoi(e) : pick_cap(win));
   if (cap > 32 || cap < 2 || (cap & (cap - 1))) return g;
   g.cap = cap;
   g.sel.n_select = d.n_select;
@@ -2109,12 +2119,15 @@ static void launch_gw_redo(const GwArgs& ga, uint32_t nk, uint32_t* rows, T* hv,
 }
 template <class T, int OP>
 static void launch_gwalk(const GwArgs& ga, uint32_t ng, hipStream_t st) {
-  const char* e = getenv("SG_DEBUG_GW_PT");   // (test hook: rows per thread per LDS chunk)
-  const int pt = e ? atoi(e) : 8;
+  // rows per thread per LDS chunk: the largest that leaves room for two workgroups per CU beside the ring (measured on
+  // C5, profiles/r06/ab_gw.sh: 8 with an 8-entry ring, 6 with 16; with 32 one workgroup per CU whatever the chunk)
+  const char* e = getenv("SG_DEBUG_GW_PT");   // (test hook)
+  const int pt = e ? atoi(e) : (ga.cap <= 8 ? 8 : ga.cap <= 16 ? 6 : 4);
   if (ga.stack_mode) {
     if (pt == 4) launch_gwalk_pt<T, OP, 4, true>(ga, ng, st);
     else if (pt == 12) launch_gwalk_pt<T, OP, 12, true>(ga, ng, st);
     else if (pt == 10) launch_gwalk_pt<T, OP, 10, true>(ga, ng, st);
+    else if (pt == 6) launch_gwalk_pt<T, OP, 6, true>(ga, ng, st);
     else launch_gwalk_pt<T, OP, 8, true>(ga, ng, st);
   } else {
     launch_gwalk_pt<T, OP, 8, false>(ga, ng, st);
@@ -2241,12 +2254,13 @@ static int run_group_walk(SgHandle* h, const BatchView& bv, int64_t n, int64_t n
     }
     sel.pzero = v.pfloat;
     // per-tile match counts -> tile bases (scan) -> output records per tile (block scan inside the tile)
-    const int64_t ntile = (n + 256 * GW_SCAN_R - 1) / (256 * GW_SCAN_R);
+    const int64_t ntile = (n + GW_TILE - 1) / GW_TILE;
     uint32_t* tcount = (uint32_t*)h->ws.get("gw_tcount", sizeof(uint32_t) * ((size_t)ntile + 1), st);
     uint32_t* tbase = (uint32_t*)h->ws.get("gw_tbase", sizeof(uint32_t) * ((size_t)ntile + 1), st);
-    h->kbeg("count_scan");
+    h->kbeg("gw_tiles");
     HIPCHK(hipMemsetAsync(tcount + ntile, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_gtile_count, dim3((unsigned)ntile), dim3(256), 0, st, n, (const uint64_t*)ga.trig, tcount);
+    hipLaunchKernelGGL(k_gtile_count, dim3((unsigned)((ntile + 7) / 8)), dim3(256), 0, st, n, (const uint64_t*)ga.trig, tcount,
+                       ntile);
     HIPCHK(hipGetLastError());
     {
       size_t tb = 0;
@@ -2257,7 +2271,7 @@ static int run_group_walk(SgHandle* h, const BatchView& bv, int64_t n, int64_t n
     h->kend();
     uint32_t tsum = 0;
     HIPCHK(hipMemcpyAsync(&tsum, tbase + ntile, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    h->kbeg("project");
+    h->kbeg("gw_project");
     const size_t plds = (size_t)GW_PROJ_S * sel.stride;
     if (plds > 65536)
       HIPCHK(hipFuncSetAttribute((const void*)k_gscan_project, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));

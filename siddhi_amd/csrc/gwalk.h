@@ -338,13 +338,18 @@ __global__ void __launch_bounds__(256, 1) k_gwalk(GwArgs a) {
 
 // A key whose pending list outgrew the LDS ring, walked again from its first row with an unbounded list: one
 // workgroup per such key gathers the key's rows from its group (arrival order kept) into the key's slice of `rows`,
-// then one lane walks them with the list in HBM planes over the key's rows, rewriting the key's match-area region,
+// then one lane walks them (staged in LDS with the list when the key has at most GW_REDO_LDS rows, else from HBM with
+// the list in HBM planes over the key's rows), rewriting the key's match-area region,
 // its trigger words and its carry from the start (same walk, same rows: the same words the first walk wrote up to
 // the overflow, then the rest).
+static const uint32_t GW_REDO_LDS = 2048;   // rows of a redone key walked from LDS
 template <class T, int OP, bool STACK>
 __global__ void __launch_bounds__(256) k_gw_redo(GwArgs a, uint32_t* __restrict__ rows, T* __restrict__ hv,
                                                  int32_t* __restrict__ ht, int32_t* __restrict__ hp) {
   __shared__ uint32_t wc[4], base_s;
+  __shared__ PtU4 red_stage[GW_REDO_LDS];
+  __shared__ T red_v[GW_REDO_LDS];
+  __shared__ int32_t red_t[GW_REDO_LDS], red_p[GW_REDO_LDS];
   const uint32_t k = a.ovf_keys[blockIdx.x];
   const uint32_t g = k >> 8, d = k & 255u, t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t lo = a.o1[(size_t)g * a.ns1], hi = a.o1[(size_t)(g + 1) * a.ns1];
@@ -365,16 +370,28 @@ __global__ void __launch_bounds__(256) k_gw_redo(GwArgs a, uint32_t* __restrict_
     if (t == 0) base_s += wc[0] + wc[1] + wc[2] + wc[3];
     __syncthreads();
   }
+  const uint32_t nk = ke - kb;
+  const bool in_lds = nk <= GW_REDO_LDS;   // (C5's keys: ~500 rows) records and list in LDS, else both in HBM
+  if (in_lds)
+    for (uint32_t i = t; i < nk; i += 256) red_stage[i] = a.grec[rows[kb + i]];
+  __syncthreads();
   if (t != 0) return;
   if (kb + base_s != ke) { atomicOr(a.flags, GW_INTERNAL); return; }
   GwLane<T, OP, STACK, GwHbmRing<T>> W;
-  W.R.v = hv + kb;
-  W.R.t = ht + kb;
-  W.R.p = hp + kb;
+  if (in_lds) {
+    W.R.v = red_v;
+    W.R.t = red_t;
+    W.R.p = red_p;
+  } else {
+    W.R.v = hv + kb;
+    W.R.t = ht + kb;
+    W.R.p = hp + kb;
+  }
   W.k = k;
   W.wi = a.within > 0xffffffffll ? 0xffffffffu : (uint32_t)a.within;
   W.cur = 3ull * kb;
-  for (uint32_t i = kb; i < ke; ++i) W.step(a, a.grec[rows[i]]);
+  if (in_lds) for (uint32_t i = 0; i < nk; ++i) W.step(a, red_stage[i]);
+  else for (uint32_t i = kb; i < ke; ++i) W.step(a, a.grec[rows[i]]);
   uint32_t fl = W.bad ? GW_ORDER : 0u;
   if (W.cur > 3ull * ke) fl |= GW_INTERNAL;
   if (fl) atomicOr(a.flags, fl);
@@ -395,30 +412,33 @@ struct GwSel {
   int32_t n_select, stride, multi, b_slot, pzero, vfloat;
   int32_t code[SG_MAX_SELECT];   // 0 e1 payload, 1 e1 value, 2 e2 value, 3 e2 payload, 4 null
 };
-static const int GW_PROJ_S = 512;   // records staged per round
-static const int GW_SCAN_R = 4;     // trigger words per thread (1024 rows per tile)
+static const int GW_PROJ_S = 256;   // records staged per round
+static const int GW_TILE = 256;     // rows per projection tile (one per thread)
 
-// matches per 1024-row tile of trigger words (the projection's tile bases come from a scan over these)
+// matches per 256-row tile of trigger words, eight tiles per workgroup (the projection's tile bases come from a scan
+// over these)
 static __global__ void __launch_bounds__(256) k_gtile_count(int64_t n, const uint64_t* __restrict__ trig,
-                                                            uint32_t* __restrict__ tcount) {
-  __shared__ uint32_t red[4];
-  const int64_t r0 = (int64_t)blockIdx.x * (256 * GW_SCAN_R);
-  uint32_t c = 0;
+                                                            uint32_t* __restrict__ tcount, int64_t ntile) {
+  __shared__ uint32_t red[8][4];
+  const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
 #pragma unroll
-  for (int s = 0; s < GW_SCAN_R; ++s) {
-    const int64_t r = r0 + s * 256 + threadIdx.x;
-    if (r < n) c += (uint32_t)(__builtin_nontemporal_load(trig + r) >> 32);
+  for (int s = 0; s < 8; ++s) {
+    const int64_t r = ((int64_t)blockIdx.x * 8 + s) * GW_TILE + t;
+    uint32_t c = r < n ? (uint32_t)(__builtin_nontemporal_load(trig + r) >> 32) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    if (lane == 0) red[s][w] = c;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) tcount[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (t < 8) {
+    const int64_t tile = (int64_t)blockIdx.x * 8 + t;
+    if (tile < ntile) tcount[tile] = red[t][0] + red[t][1] + red[t][2] + red[t][3];
+  }
 }
 
-// Output records: one workgroup per 1024-row tile (4 consecutive rows per thread), its first output slot from the
-// scanned tile counts, each row's from a block scan; the tile's records are assembled in LDS in slot order and stored
-// contiguously (GW_PROJ_S records per round).
+// Output records: one workgroup per 256-row tile (one row per thread: every trigger's header read is in flight at
+// once), its first output slot from the scanned tile counts and each row's from a block scan; the tile's records are
+// assembled in LDS in slot order and stored contiguously (GW_PROJ_S records per round).
 static __global__ void __launch_bounds__(256) k_gscan_project(int64_t n, int64_t t0, uint64_t base_index,
                                                               const uint64_t* __restrict__ index,
                                                               const uint64_t* __restrict__ trig,
@@ -428,68 +448,44 @@ static __global__ void __launch_bounds__(256) k_gscan_project(int64_t n, int64_t
   extern __shared__ __attribute__((aligned(16))) char stage[];
   __shared__ uint32_t wsum[4];
   const uint32_t t = threadIdx.x;
-  const uint32_t tile = blockIdx.x;
-  const int64_t r0 = (int64_t)tile * (256 * GW_SCAN_R) + (int64_t)t * GW_SCAN_R;
-  uint64_t tw[GW_SCAN_R];
-  if (r0 + GW_SCAN_R <= n) {
-    typedef uint64_t U2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int s = 0; s < GW_SCAN_R; s += 2) {
-      const U2 x = __builtin_nontemporal_load((const U2*)(trig + r0 + s));
-      tw[s] = x.x;
-      tw[s + 1] = x.y;
-    }
-  } else {
-#pragma unroll
-    for (int s = 0; s < GW_SCAN_R; ++s) tw[s] = r0 + s < n ? trig[r0 + s] : 0ull;
+  const int64_t b = (int64_t)blockIdx.x * GW_TILE + t;
+  const uint64_t tw = b < n ? __builtin_nontemporal_load(trig + b) : 0ull;
+  const uint32_t m = (uint32_t)(tw >> 32);
+  const uint64_t u = (uint32_t)tw;
+  uint64_t h0 = 0, h1 = 0, tg = 0;
+  if (m) {
+    h0 = area[u];
+    h1 = area[u + 1];
+    tg = index ? index[b] : base_index + (uint64_t)b;
   }
-  uint32_t sum = 0;
-#pragma unroll
-  for (int s = 0; s < GW_SCAN_R; ++s) sum += (uint32_t)(tw[s] >> 32);
-  const uint32_t excl = block_excl_scan256(sum, wsum);
-  const uint32_t pre = tbase[tile];
+  const uint32_t excl = block_excl_scan256(m, wsum);
+  const uint32_t pre = tbase[blockIdx.x];
   const uint32_t o_lo = pre, o_hi = pre + (wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  const uint32_t o = pre + excl;
   auto wid = [&](uint32_t bits, bool zero) { return zero ? (int64_t)bits : (int64_t)(int32_t)bits; };
   uint32_t nmask = 0;
   for (int s = 0; s < sel.n_select; ++s) nmask |= (sel.code[s] == 4) ? 1u << s : 0u;
-  // every trigger's header and index in flight at once (random reads), before any record is built
-  uint64_t h0[GW_SCAN_R], h1[GW_SCAN_R], tg[GW_SCAN_R];
-#pragma unroll
-  for (int s = 0; s < GW_SCAN_R; ++s) {
-    const uint64_t u = (uint32_t)tw[s];
-    const bool any = (tw[s] >> 32) != 0;
-    h0[s] = any ? area[u] : 0ull;
-    h1[s] = any ? area[u + 1] : 0ull;
-    tg[s] = (any && index) ? index[r0 + s] : base_index + (uint64_t)(r0 + s);
-  }
+  const int64_t ts = t0 + (int64_t)(int32_t)(uint32_t)h0;
+  const uint32_t key = (uint32_t)(h0 >> 32);
+  const int64_t v2 = wid((uint32_t)h1, sel.vfloat), p2 = wid((uint32_t)(h1 >> 32), sel.pzero);
   typedef uint32_t U4 __attribute__((ext_vector_type(4)));
   for (uint32_t sub = o_lo; sub < o_hi; sub += GW_PROJ_S) {
     const uint32_t se = (o_hi - sub < (uint32_t)GW_PROJ_S) ? o_hi : sub + GW_PROJ_S;
-    uint32_t o = pre + excl;
-#pragma unroll
-    for (int s = 0; s < GW_SCAN_R; ++s) {
-      const uint32_t m = (uint32_t)(tw[s] >> 32);
-      if (m && o < se && o + m > sub) {
-        const uint64_t u = (uint32_t)tw[s];
-        const int64_t ts = t0 + (int64_t)(int32_t)(uint32_t)h0[s];
-        const uint32_t key = (uint32_t)(h0[s] >> 32);
-        const int64_t v2 = wid((uint32_t)h1[s], sel.vfloat), p2 = wid((uint32_t)(h1[s] >> 32), sel.pzero);
-        const uint32_t qa = o < sub ? sub - o : 0u, qe = (o + m > se) ? se - o : m;
-        for (uint32_t q = qa; q < qe; ++q) {
-          const uint64_t e = area[u + 2 + q];
-          const int64_t v1 = wid((uint32_t)e, sel.vfloat), p1 = wid((uint32_t)(e >> 32), sel.pzero);
-          int64_t* r = (int64_t*)(stage + (size_t)(o + q - sub) * sel.stride);
-          r[0] = (int64_t)tg[s];
-          r[1] = ts;
-          r[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (sel.multi ? (uint32_t)sel.b_slot : (0x800000u | q))) << 32));
-          r[3] = (int64_t)nmask;
-          for (int c = 0; c < sel.n_select; ++c) {
-            const int code = sel.code[c];
-            r[4 + c] = code == 0 ? p1 : code == 1 ? v1 : code == 2 ? v2 : code == 3 ? p2 : 0;
-          }
+    if (m && o < se && o + m > sub) {
+      const uint32_t qa = o < sub ? sub - o : 0u, qe = (o + m > se) ? se - o : m;
+      for (uint32_t q = qa; q < qe; ++q) {
+        const uint64_t e = area[u + 2 + q];
+        const int64_t v1 = wid((uint32_t)e, sel.vfloat), p1 = wid((uint32_t)(e >> 32), sel.pzero);
+        int64_t* r = (int64_t*)(stage + (size_t)(o + q - sub) * sel.stride);
+        r[0] = (int64_t)tg;
+        r[1] = ts;
+        r[2] = (int64_t)((uint64_t)key | ((uint64_t)((1u << 24) | (sel.multi ? (uint32_t)sel.b_slot : (0x800000u | q))) << 32));
+        r[3] = (int64_t)nmask;
+        for (int c = 0; c < sel.n_select; ++c) {
+          const int code = sel.code[c];
+          r[4 + c] = code == 0 ? p1 : code == 1 ? v1 : code == 2 ? v2 : code == 3 ? p2 : 0;
         }
       }
-      o += m;
     }
     __syncthreads();
     const size_t bytes = (size_t)(se - sub) * sel.stride;

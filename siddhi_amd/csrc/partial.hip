@@ -219,6 +219,8 @@ struct PpArgs {
   const uint8_t* kback;       // partial lanes: per key, its time goes back somewhere in this push (carried rows included)
   int64_t drop_before;        // partial lanes: a pending partial whose e1 is older than this is not carried
                               // (sg_options.bounded_lateness; INT64_MIN = carry every pending partial)
+  int64_t dead_after;         // partial lanes: a partial at a row more than this after e1 is dead (within + lateness;
+                              // INT64_MAX without bounded_lateness)
 };
 
 // Key-ordered packed rows (position q = the q-th row of the key partition): what a lane reads at every step, so the
@@ -657,9 +659,13 @@ __global__ void __launch_bounds__(PP_BLOCK, G::S <= 4 ? 8 : 4) k_pp_lanes(PpArgs
         }
         q = qq < e ? qq : e;
       }
-      int64_t dt = q < e ? src.ts(q) - L.e1_ts : 0;
-      dt = dt < 0 ? -dt : dt;
-      if (q >= e) {
+      const int64_t sdt = q < e ? src.ts(q) - L.e1_ts : 0;
+      const int64_t dt = sdt < 0 ? -sdt : sdt;
+      if (q < e && sdt > a.dead_after) {
+        // bounded lateness: the clock is at least this row's time, so no later row can lie inside `within` of e1 --
+        // the partial never emits again, in this push or a later one (not carried)
+        done = true;
+      } else if (q >= e) {
         done = true;
         // still pending after the key's last row (and not finished: a partial completes at most once): the rows it
         // holds are carried, its e1 marked as the start of its lane in the next push
@@ -1482,7 +1488,13 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
   a.ckey = cr.key;
   a.cstart = ps->mode == 1 && nc > 0 ? cr.start : nullptr;
   a.drop_before = INT64_MIN;
-  if (h->opt.bounded_lateness && n > 0 && d.within >= 0) {
+  a.dead_after = INT64_MAX;
+  // (only when every state a partial can emit from expires it by `within`: a count state never does, so a query whose
+  // count state is a final one keeps every partial)
+  bool lat_ok = h->opt.bounded_lateness && n > 0 && d.within >= 0;
+  for (int s = 0; s < d.n_states; ++s)
+    if (d.states[s].kind == SG_K_COUNT && d.states[s].has_selector) lat_ok = false;
+  if (lat_ok) {
     // the largest timestamp so far; every later row is at most max_lateness_ms behind it, so a partial whose e1 is
     // more than `within` before (that - max_lateness_ms) never sees a row it could emit at again
     int64_t* dmax = (int64_t*)h->ws.get("pp_tsmax", sizeof(int64_t), st);
@@ -1496,8 +1508,10 @@ int sg_partial_push(SgHandle* h, PartialState* ps, const BatchView& bv, int64_t 
     h->ts_max_seen = std::max(h->ts_max_seen, hm);
     const int64_t lat = std::max<int64_t>(0, h->opt.max_lateness_ms);
     const int64_t w = std::max<int64_t>(0, d.within);
-    if (h->ts_max_seen > INT64_MIN / 2 && w < (int64_t)1 << 60 && lat < (int64_t)1 << 60)
+    if (h->ts_max_seen > INT64_MIN / 2 && w < (int64_t)1 << 60 && lat < (int64_t)1 << 60) {
       a.drop_before = h->ts_max_seen - lat - w;
+      a.dead_after = w + lat;
+    }
   }
   const SgCols cc = carried_cols(ps, cr);
   int end_bit = 1;
