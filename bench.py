@@ -630,19 +630,49 @@ def whole_node_block(args, ws, local, dev):
                       "merge_ms": c5w["merge_ms"], "h2d_GB": c5w["h2d_GB"], "d2h_GB": c5w["d2h_GB"],
                       "gpu_busy_ms": c5w["gpu_busy_ms"]}]
             for G in shards:
-                r = node_whole("C5", args.c5_events or synth.CONFIGS["C5"][1], synth.CONFIGS["C5"][2],
-                               synth.CONFIGS["C5"][3], [devs[0]] * G, 1, thr, 0)
+                # each G in a child process given 4 x G hardware queues -- what a G-GPU node gives this pipeline
+                # (the HIP runtime's 4 per device): the exchange's per-shard compute, H2D, D2H and peer-copy streams
+                # then keep queues of their own, as they do with one shard per GPU (at 4 queues for G shards on one
+                # device the copies of different shards serialise behind each other's kernels: profiles/r06/
+                # ab_node_queues.sh, G = 2: 905 ms at 4 queues, 728 at 8, 609 at 16)
+                r = node_child(args, G, thr)
+                if "error" in r:
+                    table.append({"G": G, "error": r["error"]})
+                    continue
                 table.append({"G": G, "ms_per_step": r["ms_per_step"], "route_ms": r["route_ms"],
                               "merge_ms": r["merge_ms"], "h2d_GB": r["h2d_GB"], "d2h_GB": r["d2h_GB"],
-                              "gpu_busy_ms": r["gpu_busy_ms"], "shard_rows": r["shard_rows"]})
+                              "gpu_busy_ms": r["gpu_busy_ms"], "shard_rows": r["shard_rows"],
+                              "hw_queues": r.get("hw_queues")})
             c5w["node_shards_on_one_gpu"] = {
                 "host_threads": thr, "rows": table,
-                "note": "G shards (one sg_handle each) mapped onto device 0: route_ms / merge_ms are the host "
-                        "stages a G-GPU node runs (scatter to per-shard pinned staging, k-way merge), with "
-                        "this box's %d host threads; GPU time is serialised on one device" % thr}
+                "note": "G shards (one sg_handle each) mapped onto device 0, each G in a child process with 4 x G HIP "
+                        "hardware queues (a G-GPU node's per-device 4): route_ms / merge_ms are the host stages a "
+                        "G-GPU node runs, with this box's %d host threads; GPU time and the one PCIe link are "
+                        "shared by the G shards" % thr}
     except Exception as e:   # report, never fake
         c5w = {"error": str(e)}
     return c5w
+
+
+def node_child(args, G, thr):
+    """the whole-node pipeline with G shards on device 0, one step, in a child process with 4 x G hardware queues"""
+    cmd = [sys.executable, os.path.abspath(__file__), "--node-only", "--c5-node-steps", "1",
+           "--c5-node-devices", ",".join(["0"] * G), "--node-threads", str(thr), "--node-shards", ""]
+    if args.c5_events:
+        cmd += ["--c5-events", str(args.c5_events)]
+    env = {k: v for k, v in os.environ.items() if k not in TORCHRUN_ENV and not k.startswith("TORCHELASTIC")}
+    env["GPU_MAX_HW_QUEUES"] = str(min(32, 4 * G))
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "shards child timed out (900 s)"}
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"shards child exit {p.returncode}: {p.stderr[-800:]}"}
+    r = json.loads(lines[-1])["whole_node"]
+    if isinstance(r, dict):
+        r["hw_queues"] = int(env["GPU_MAX_HW_QUEUES"])
+    return r
 
 
 def whole_node_child(args, ws):

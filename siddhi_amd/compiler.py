@@ -178,6 +178,9 @@ class StreamDefinition:
 class Partition:
     keys: List[Tuple[str, str]]    # (stream id, attribute name)  value partition `attr of S`
     queries: List[Query]
+    # range partition `c1 as 'l1' or c2 as 'l2' ... of S`: per stream, its (condition, label) list in written order
+    # (PartitionParser -> RangePartitionExecutor, C/partition/executor/RangePartitionExecutor.java:38-43)
+    ranges: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -351,12 +354,30 @@ class _Parser:
         self.eat("partition")
         self.eat("with")
         self.eat("(")
-        keys = []
+        keys, ranges = [], {}
         while True:
-            attr = self.ident()
-            self.eat("of")
-            sid = self.ident()
-            keys.append((sid, attr))
+            if self.peek().kind == "id" and self.peek(1).text == "of":   # value partition `attr of S`
+                attr = self.ident()
+                self.eat("of")
+                sid = self.ident()
+                keys.append((sid, attr))
+            else:   # range partition `cond as 'label' (or cond as 'label')* of S` (a condition with `or` is parenthesised)
+                rl = []
+                while True:
+                    cond = self.and_expr()
+                    self.eat("as")
+                    t = self.peek()
+                    if t.kind != "str":
+                        raise SiddhiParserException("range partition: a string label after `as`")
+                    self.i += 1
+                    rl.append((cond, t.text[1:-1]))
+                    if not self.accept("or"):
+                        break
+                self.eat("of")
+                sid = self.ident()
+                if sid in ranges or any(k[0] == sid for k in keys):
+                    raise SiddhiParserException(f"stream {sid} partitioned twice")
+                ranges[sid] = rl
             if self.accept(")"):
                 break
             self.eat(",")
@@ -373,7 +394,7 @@ class _Parser:
             queries.append(self.query(info))
             info = None
         self.eat("end")
-        return Partition(keys, queries)
+        return Partition(keys, queries, ranges)
 
     def query(self, name) -> Query:
         self.eat("from")

@@ -42,6 +42,8 @@ class QueryContext:
     key_attr: List[int]                # per stream index: partition key attribute index or -1
     strings: Dict[str, int]            # global string dictionary (shared, grows at runtime)
     names: Dict[str, int] = field(default_factory=dict)
+    # per stream index: the range partition's (condition, label) list in written order, or None
+    key_ranges: List[Optional[list]] = field(default_factory=list)
 
     def name_id(self, s: str) -> int:
         if s not in self.names:
@@ -68,7 +70,46 @@ def make_context(app: C.SiddhiApp, query: C.Query, partition: Optional[C.Partiti
             if ai < 0:
                 raise LoweringError(f"partition attribute {attr} not in {sid}")
             key_attr[sids.index(sid)] = ai
-    return QueryContext(app, query, sids, partition is not None, key_attr, strings)
+    key_ranges = [None] * len(sids)
+    if partition is not None:
+        for sid, rl in partition.ranges.items():
+            if sid not in app.streams:
+                raise LoweringError(f"range partition of undefined stream {sid}")
+            for cond, _ in rl:
+                _check_range_cond(app.streams[sid], cond)
+            key_ranges[sids.index(sid)] = rl
+    ctx = QueryContext(app, query, sids, partition is not None, key_attr, strings)
+    ctx.key_ranges = key_ranges
+    return ctx
+
+
+def _check_range_cond(d: C.StreamDefinition, e):
+    """A range partition's condition reads the partitioned stream's own attributes (RangePartitionExecutor runs it
+    on the arriving event, C/partition/executor/RangePartitionExecutor.java:38-43): compares, and / or / not and
+    `is null` over attributes and constants (what the host router evaluates)."""
+    if isinstance(e, (C.And, C.Or)):
+        _check_range_cond(d, e.left)
+        _check_range_cond(d, e.right)
+    elif isinstance(e, (C.Not, C.IsNull)):
+        _check_range_cond(d, e.expr)
+    elif isinstance(e, C.Compare):
+        ts = []
+        for x in (e.left, e.right):
+            if isinstance(x, C.Var):
+                if x.stream_ref not in (None, d.id) or x.index is not None or d.attr_index(x.attr) < 0:
+                    raise LoweringError(f"range partition condition: {x.attr} is not an attribute of {d.id}")
+                ts.append(d.attr_type(x.attr))
+            elif isinstance(x, C.Const):
+                ts.append(x.type)
+            else:
+                raise LoweringError("range partition condition: compares of attributes and constants only")
+        # ExpressionParser.parseCompare: STRING and BOOL compare only with their own type, and only by == / !=
+        if any(t in ("STRING", "BOOL") for t in ts) and (ts[0] != ts[1] or e.op not in ("==", "!=")):
+            raise LoweringError(f"range partition condition: cannot compare {ts[0]} {e.op} {ts[1]}")
+    elif isinstance(e, C.Var) and d.attr_type(e.attr) == "BOOL":
+        pass
+    else:
+        raise LoweringError("range partition condition must be a boolean expression")
 
 
 # ------------------------------------------------------------------------------ oracle image

@@ -204,19 +204,122 @@ def _broadcast(b: "Batch", bcast: np.ndarray, keys_before: int) -> "Batch":
                  [None if x is None else x[idx] for x in b.nulls], index=index)
 
 
+def _range_value(e, d: C.StreamDefinition, cols: dict, nulls: dict, strings: dict, n: int):
+    """(values, type, null mask) of a range condition operand over n rows of stream d"""
+    if isinstance(e, C.Const):
+        if e.type == "STRING":
+            return np.full(n, strings.get(e.value, -1), np.int64), "STRING", np.zeros(n, bool)
+        if e.type == "BOOL":
+            return np.full(n, 1 if e.value else 0, np.int64), "BOOL", np.zeros(n, bool)
+        return np.full(n, e.value, _NP[e.type]), e.type, np.zeros(n, bool)
+    t = d.attr_type(e.attr)
+    nul = nulls.get(e.attr)
+    return cols[e.attr], t, (nul.astype(bool) if nul is not None else np.zeros(n, bool))
+
+
+def _range_mask(e, d: C.StreamDefinition, cols: dict, nulls: dict, strings: dict, n: int) -> np.ndarray:
+    """RangePartitionExecutor's condition (C/partition/executor/RangePartitionExecutor.java:38-43) over n rows, with
+    the compare executors' rules: a null operand makes a compare false and `!=` true (CompareConditionExpression
+    Executor.java:39-43, NotEqualCompareConditionExpressionExecutor.java:37); numbers compare in the wider of the
+    two types (INT / LONG as LONG, with a FLOAT as FLOAT, with a DOUBLE as DOUBLE: Java binary promotion)."""
+    if isinstance(e, C.And):
+        return _range_mask(e.left, d, cols, nulls, strings, n) & _range_mask(e.right, d, cols, nulls, strings, n)
+    if isinstance(e, C.Or):
+        return _range_mask(e.left, d, cols, nulls, strings, n) | _range_mask(e.right, d, cols, nulls, strings, n)
+    if isinstance(e, C.Not):
+        return ~_range_mask(e.expr, d, cols, nulls, strings, n)
+    if isinstance(e, C.IsNull):
+        return _range_value(e.expr, d, cols, nulls, strings, n)[2]
+    if isinstance(e, C.Var):   # a BOOL attribute
+        v, _, nul = _range_value(e, d, cols, nulls, strings, n)
+        return (v != 0) & ~nul
+    lv, lt, ln = _range_value(e.left, d, cols, nulls, strings, n)
+    rv, rt, rn = _range_value(e.right, d, cols, nulls, strings, n)
+    if (lt in ("STRING", "BOOL") or rt in ("STRING", "BOOL")) and (lt != rt or e.op not in ("==", "!=")):
+        raise SiddhiAppCreationException(f"range partition: cannot compare {lt} {e.op} {rt}")
+    if "DOUBLE" in (lt, rt):
+        lv, rv = lv.astype(np.float64), rv.astype(np.float64)
+    elif "FLOAT" in (lt, rt):
+        lv, rv = lv.astype(np.float32), rv.astype(np.float32)
+    else:
+        lv, rv = lv.astype(np.int64), rv.astype(np.int64)
+    r = {"==": np.equal, "!=": np.not_equal, ">": np.greater, ">=": np.greater_equal, "<": np.less,
+         "<=": np.less_equal}[e.op](lv, rv)
+    anynull = ln | rn
+    return (r | anynull) if e.op == "!=" else (r & ~anynull)
+
+
+def _range_route(b: "Batch", stream: np.ndarray, masks: dict, key_of_label, clock: bool = False) -> "Batch":
+    """PartitionStreamReceiver with range executors (C/partition/PartitionStreamReceiver.java:94-100,110-125 for
+    a single event; send() drops a null key, :270-275): a row of a range-partitioned stream goes to the partition of
+    EVERY range whose condition holds, in the written range order, and to none if no range holds; rows of other
+    streams keep their key.  Each copy keeps the row's event index, so an event's matches come out per range in
+    range order (the engines order the copies of one trigger by their position).  masks: stream index -> (labels,
+    bool[n_ranges, n]) over this batch's rows.  clock: a row that holds no range still moves the playback clock
+    (InputHandler.send sets the time before the junction sees the event, C/stream/input/InputHandler.java:57-65), so
+    it stays as one clock-only row (stream -1, the heartbeat form)."""
+    n = b.n
+    reps = np.ones(n, np.int64)
+    none = np.zeros(n, bool)
+    for s, (labels, m) in masks.items():
+        rows = stream == s
+        reps[rows] = m[:, rows].sum(axis=0)
+        none |= rows & (reps == 0)
+    if clock:
+        reps[none] = 1
+    idx = np.repeat(np.arange(n, dtype=np.int64), reps)
+    key = b.key[idx].copy()
+    starts = np.cumsum(reps) - reps
+    within = np.arange(len(idx), dtype=np.int64) - np.repeat(starts, reps)
+    all_labels = []          # every range stream's labels, one code each
+    code = np.full(len(idx), -1, np.int64)
+    for s, (labels, m) in masks.items():
+        sel = (stream[idx] == s) & ~none[idx]
+        if not sel.any():
+            continue
+        base = len(all_labels)
+        all_labels += list(labels)
+        # the k-th copy of a row is its k-th holding range (written order)
+        rank = np.cumsum(m, axis=0) - 1                        # per range: its rank among the row's holding ranges
+        rows, wk = idx[sel], within[sel]
+        hit = np.zeros(len(rows), np.int64)
+        for ri in range(m.shape[0]):
+            hit = np.where(m[ri, rows] & (rank[ri, rows] == wk), ri, hit)
+        code[sel] = base + hit
+    ranged = code >= 0
+    if ranged.any():
+        # dense ids in first-seen order over the copies, which are in (row, range) order
+        u, first = np.unique(code[ranged], return_index=True)
+        ids = np.empty(len(u), np.int32)
+        for j in np.argsort(first, kind="stable"):
+            ids[j] = key_of_label(all_labels[int(u[j])])
+        key[ranged] = ids[np.searchsorted(u, code[ranged])]
+    st = b.stream[idx].copy()
+    if clock and none.any():
+        ck = none[idx]
+        st[ck] = -1
+        key[ck] = -1
+    index = (np.uint64(b.base_index) + idx.astype(np.uint64)) if b.index is None else b.index[idx]
+    return Batch(len(idx), b.base_index, b.ts[idx], st, key, [c[idx] for c in b.cols],
+                 [None if x is None else x[idx] for x in b.nulls], index=index)
+
+
 class _QueryRuntime:
     def __init__(self, app_rt: "SiddhiAppRuntime", query: C.Query, partition: Optional[C.Partition],
                  engine_factory):
         self.app_rt = app_rt
         self.query = query
         self.partition = partition
-        self.ctx = L.make_context(app_rt.app, query, partition, app_rt.strings)
+        try:
+            self.ctx = L.make_context(app_rt.app, query, partition, app_rt.strings)
+        except L.LoweringError as x:
+            raise SiddhiAppCreationException(str(x)) from x
         # streams read inside the partition without a partition key: broadcast to every instance
         self.global_streams = set()
         if partition is not None:
             reads = _query_streams(query)
             self.global_streams = {i for i, sid in enumerate(self.ctx.stream_ids)
-                                   if sid in reads and self.ctx.key_attr[i] < 0}
+                                   if sid in reads and self.ctx.key_attr[i] < 0 and self.ctx.key_ranges[i] is None}
         self.sel_types = [self._select_type(oa.expr) for oa in query.select]
         # the query is checked (types, references) when the app is created, whichever engine runs it
         # (SiddhiAppRuntime creation -> ExpressionParser throws SiddhiAppCreationException, C/util/parser/
@@ -455,11 +558,35 @@ class SiddhiAppRuntime:
             else:
                 key = np.zeros(n, np.int32) if not q.ctx.partitioned else np.full(n, -1, np.int32)
             b = Batch(n, base, ts, stream_col, key, allcols, nulls)
+            if q.ctx.partitioned and q.ctx.key_ranges[stream] is not None:
+                b = self._route_ranges(qi, q, b, stream_col)
             if stream in q.global_streams:
                 b = _broadcast(b, np.ones(n, bool), len(self.key_dicts[qi]))
             if b.n:
                 q.engine.push(b)
             self._deliver(q, q.engine.fetch())
+
+    def _route_ranges(self, qi: int, q: "_QueryRuntime", b: "Batch", stream: np.ndarray) -> "Batch":
+        """the batch's rows of range-partitioned streams, one copy per holding range (_range_route)"""
+        kd = self.key_dicts[qi]
+
+        def key_of_label(label):
+            i = kd.get(label)
+            if i is None:
+                i = len(kd)
+                kd[label] = i
+            return i
+        masks = {}
+        for s, rl in enumerate(q.ctx.key_ranges):
+            if rl is None or not (stream == s).any():
+                continue
+            d = self.app.streams[self.stream_ids[s]]
+            cb = self._col_base(s)
+            cols = {name: b.cols[cb + a] for a, (name, _) in enumerate(d.attrs)}
+            nulls = {name: b.nulls[cb + a] for a, (name, _) in enumerate(d.attrs) if b.nulls[cb + a] is not None}
+            m = np.stack([_range_mask(c, d, cols, nulls, self.strings, b.n) for c, _ in rl])
+            masks[s] = ([lab for _, lab in rl], m)
+        return _range_route(b, stream, masks, key_of_label, clock=bool(self.app.playback)) if masks else b
 
     def _col_base(self, stream: int) -> int:
         return sum(len(self.app.streams[sid].attrs) for sid in self.stream_ids[:stream])
@@ -547,6 +674,10 @@ class SiddhiAppRuntime:
             else:
                 key[:] = 0
             b = Batch(n, base, ts, stream, key, cols, nulls)
+            if q.ctx.partitioned and any(r is not None for r in q.ctx.key_ranges):
+                b = self._route_ranges(qi, q, b, stream)
+                if q.global_streams:
+                    bcast = np.isin(b.stream, list(q.global_streams))
             if bcast is not None and bcast.any():
                 b = _broadcast(b, bcast, keys_before)
             if b.n:
