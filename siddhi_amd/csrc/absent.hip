@@ -98,7 +98,7 @@ struct AbsState {
   bool seq = false;            // the state is not the closed form's: the next push runs the exact sequential pass
   int64_t* dlast = nullptr;    // device: the playback clock (largest timestamp seen; order check across pushes)
   int64_t* dminmax = nullptr;  // device: [min, max] of compared values (as order-preserving u64)
-  uint32_t* dflag = nullptr;   // device: order error
+  uint32_t* dflag = nullptr;   // device: the push's first row whose time goes back (0xffffffff: none)
 };
 
 struct AbsArgs {
@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(256) k_abs_rows(AbsArgs a, SgCols cols, const 
         if (ca) r |= R_CAND;
         if (ki && !sv.null) r |= R_KILL;   // `==` with a null operand is false
       }
-      if ((i > 0 && ts[i - 1] > ts[i]) || (i == 0 && !a.first_push && ts[0] < *dlast)) atomicOr(oflag, 1u);
+      if ((i > 0 && ts[i - 1] > ts[i]) || (i == 0 && !a.first_push && ts[0] < *dlast)) atomicMin(oflag, (uint32_t)i);
     }
     role[v] = (uint8_t)r;
     vals[v] = x;
@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(256) k_abs_rows_fast(AbsArgs a, const V* __res
                                                        unsigned long long* __restrict__ minmax,
                                                        const int64_t* __restrict__ dlast, uint32_t* __restrict__ oflag) {
   uint64_t lo = ~0ull, hi = 0;
-  bool bad = false;
+  uint32_t late = 0xffffffffu;   // first row whose time goes back
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < a.nt; v += (int64_t)gridDim.x * blockDim.x) {
     uint32_t r;
     int64_t x = 0;
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(256) k_abs_rows_fast(AbsArgs a, const V* __res
       x = (int64_t)col[i];
       r = R_CAND | R_KILL | R_SORT;
       const int64_t t = ts[i];
-      bad |= (i > 0 && ts[i - 1] > t) || (i == 0 && !a.first_push && t < *dlast);
+      if (((i > 0 && ts[i - 1] > t) || (i == 0 && !a.first_push && t < *dlast)) && (uint32_t)i < late) late = (uint32_t)i;
     }
     role[v] = (uint8_t)r;
     vals[v] = x;
@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(256) k_abs_rows_fast(AbsArgs a, const V* __res
       hi = o > hi ? o : hi;
     }
   }
-  if (bad) atomicOr(oflag, 1u);
+  if (late != 0xffffffffu) atomicMin(oflag, late);
   block_minmax(lo, hi, minmax);
 }
 
@@ -403,7 +403,7 @@ __global__ void k_abs_init(unsigned long long* __restrict__ minmax, uint32_t* __
   if (threadIdx.x == 0) {
     minmax[0] = ~0ull;
     minmax[1] = 0ull;
-    *oflag = 0;
+    *oflag = 0xffffffffu;   // first row whose time goes back (none)
   }
 }
 
@@ -445,10 +445,15 @@ __global__ void k_abs_qwrite(int64_t nq, const int64_t* __restrict__ q, int64_t 
 //     pass that emitted nothing with lastScheduledTime < T schedules T + W (AbsentStreamPreStateProcessor.java:140-210);
 //   a B row kills every pending partial with its value, each kill scheduling ts + W (:230-244, AbsentStreamPost-
 //     StateProcessor.java:36-56); an A row opens a partial and schedules ts + W (:77-101).
-// One lane walks the rows (the FIFO makes the order of everything global); kills find their partials through a hash
-// of the compared value, timer passes skip 64-partial blocks whose earliest deadline is later than T.
+// One wave walks the rows in lockstep (the FIFO makes the order of everything global): the per-row work (clock, FIFO,
+// kills through a hash of the compared value, new partials) is the same on every lane; a timer pass is shared -- the
+// lanes test 64 blocks' earliest deadlines at once and then one block's 64 partials at once, emitting in creation
+// order by ballot.  After `min_rows` rows the pass may stop at a row boundary once the state is the closed form's
+// again (FIFO sorted, above the clock, below lastScheduledTime; checked every 1024 rows): the caller runs the rest of
+// the push through the closed form.
 struct SeqAbs {
   int64_t n, nc, W;
+  int64_t min_rows;            // stop early only after this many rows (<= 0: never; walk every row)
   const int64_t* ts;
   const uint8_t* role;
   const int64_t* vals;         // virtual rows (carried partials first)
@@ -476,7 +481,7 @@ struct SeqAbs {
   uint32_t* eg;
   int64_t ecap;
   // scalars: [0] clock, [1] lastScheduledTime, [2] emissions, [3] partials, [4] ring head, [5] ring tail,
-  // [6] flags (1 capacity), [7] closed form can continue (1)
+  // [6] flags (1 capacity), [7] closed form can continue (1), [8] rows walked
   int64_t* sc;
 };
 
@@ -485,13 +490,26 @@ __device__ __forceinline__ uint64_t sa_hash(int64_t x) {
   return z ^ (z >> 29);
 }
 
-__global__ void k_abs_seq(SeqAbs s) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ __forceinline__ int64_t sa_wave_min(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t y = __shfl_xor(v, o);
+    v = y < v ? y : v;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(64) k_abs_seq(SeqAbs s) {
+  if (blockIdx.x != 0) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   const int64_t INF = INT64_MAX;
   int64_t clock = s.sc[0], lst = s.sc[1];
   int64_t ne = 0, np = 0, head = 0, tail = 0;
   bool cap_bad = false;
   const int64_t qmask = s.qcap - 1, hmask = s.hcap - 1;
+  // (every lane runs the uniform work with the same values: the stores repeat the same word, and each lane reads
+  // back only what it stored itself)
   auto qpush = [&](int64_t v) {
     if (tail - head >= s.qcap) { cap_bad = true; return; }
     s.ring[tail & qmask] = v;
@@ -534,35 +552,65 @@ __global__ void k_abs_seq(SeqAbs s) {
   auto pass = [&](int64_t T, uint32_t row) -> bool {   // one timer pass; true if it emitted
     bool any = false;
     const int64_t nb = (np + 63) >> 6;
-    while (lob < nb && s.bmin[lob] == INF) ++lob;
-    for (int64_t b = lob; b < nb; ++b) {
-      if (s.bmin[b] > T) continue;
-      int64_t m = INF;
-      const int64_t k1 = (b + 1) * 64 < np ? (b + 1) * 64 : np;
-      for (int64_t k = b * 64; k < k1; ++k) {
-        if (!s.palive[k]) continue;
-        if (s.pd[k] <= T) {
-          s.palive[k] = 0;
+    for (;;) {   // skip the leading blocks with nothing alive
+      const int64_t b = lob + lane;
+      const uint64_t live = __ballot(!(b < nb && s.bmin[b] == INF));
+      if (live) { lob += __builtin_ctzll(live); break; }
+      lob += 64;
+    }
+    for (int64_t b0 = lob; b0 < nb; b0 += 64) {
+      const int64_t b = b0 + lane;
+      uint64_t cm = __ballot(b < nb && s.bmin[b] <= T);
+      while (cm) {
+        const int64_t bb = b0 + __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const int64_t k = bb * 64 + lane;
+        const bool al = k < np && s.palive[k];
+        const int64_t d = al ? s.pd[k] : INF;
+        const bool em = al && d <= T;
+        const uint64_t emm = __ballot(em);
+        const int64_t rest = sa_wave_min(em ? INF : d);
+        if (emm) {
           if (row != cur_row) { cur_row = row; grp = 0; }
-          if (ne < s.ecap) { s.ek[ne] = (uint32_t)k; s.erow[ne] = row; s.ets[ne] = T; s.eg[ne] = grp; }
-          else cap_bad = true;
-          ++ne;
-          ++grp;
+          const uint32_t below = (uint32_t)__popcll(emm & lt), cnt = (uint32_t)__popcll(emm);
+          if (em) {
+            s.palive[k] = 0;
+            const int64_t slot = ne + below;
+            if (slot < s.ecap) { s.ek[slot] = (uint32_t)k; s.erow[slot] = row; s.ets[slot] = T; s.eg[slot] = grp + below; }
+          }
+          if (ne + cnt > s.ecap) cap_bad = true;
+          ne += cnt;
+          grp += cnt;
           any = true;
-        } else if (s.pd[k] < m) {
-          m = s.pd[k];
+          __threadfence_block();   // (a later kill reads these flags on every lane)
         }
+        s.bmin[bb] = rest;
       }
-      s.bmin[b] = m;
     }
     return any;
+  };
+  auto fifo_ok = [&]() -> bool {   // the closed form can continue from this state
+    for (int64_t k0 = head; k0 < tail; k0 += 64) {
+      const int64_t k = k0 + lane;
+      bool bad = false;
+      if (k < tail) {
+        const int64_t x = s.ring[k & qmask];
+        const int64_t prev = k > head ? s.ring[(k - 1) & qmask] : INT64_MIN;
+        bad = x < prev || x <= clock || x > lst;
+      }
+      if (__ballot(bad)) return false;
+    }
+    return true;
   };
   for (int64_t k = 0; k < s.nq_in; ++k) qpush(s.q_in[k]);
   for (int64_t k = 0; k < s.nc; ++k) {
     const uint8_t r = s.role[k];
     add_partial(s.c_dl[k], (uint32_t)k, (r & R_SORT) != 0, s.vals[k]);
   }
-  for (int64_t i = 0; i < s.n && !cap_bad; ++i) {
+  int64_t i = 0;
+  bool ok = false;
+  for (; i < s.n && !cap_bad; ++i) {
+    if (s.min_rows > 0 && i >= s.min_rows && (i & 1023) == 0 && fifo_ok()) { ok = true; break; }
     const int64_t t = s.ts[i];
     if (t >= clock) {
       clock = t;
@@ -600,21 +648,18 @@ __global__ void k_abs_seq(SeqAbs s) {
   }
   // can the closed form continue from here?  its FIFO must be sorted and above the clock, and lastScheduledTime at
   // least its largest entry (then no later pass re-schedules while time moves forward)
-  bool ok = true;
-  int64_t prev = INT64_MIN;
-  for (int64_t k = head; k < tail; ++k) {
-    const int64_t x = s.ring[k & qmask];
-    if (x < prev || x <= clock || x > lst) { ok = false; break; }
-    prev = x;
+  if (!ok) ok = fifo_ok();
+  if (lane == 0) {
+    s.sc[0] = clock;
+    s.sc[1] = lst;
+    s.sc[2] = ne;
+    s.sc[3] = np;
+    s.sc[4] = head;
+    s.sc[5] = tail;
+    s.sc[6] = cap_bad ? 1 : 0;
+    s.sc[7] = ok ? 1 : 0;
+    s.sc[8] = i;
   }
-  s.sc[0] = clock;
-  s.sc[1] = lst;
-  s.sc[2] = ne;
-  s.sc[3] = np;
-  s.sc[4] = head;
-  s.sc[5] = tail;
-  s.sc[6] = cap_bad ? 1 : 0;
-  s.sc[7] = ok ? 1 : 0;
 }
 
 // FIFO ring [head, tail) -> a flat queue
@@ -683,6 +728,7 @@ AbsState* astate(SgHandle* h) {
   return (AbsState*)h->state;
 }
 
+static const int64_t SEQ_MIN_ROWS = 1024;   // rows the sequential pass walks before it may hand back to the closed form
 unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 256 * 16)); }
 unsigned grid_red(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)); }
 
@@ -721,21 +767,23 @@ void sort_and_kill(SgHandle* h, const AbsArgs& a, uint64_t omin, int bits, const
 
 }  // namespace
 
-// The exact sequential pass (k_abs_seq) for one push, from the carried state (pending partials, FIFO, lastScheduledTime,
-// clock) to the next.
-static void run_seq(SgHandle* h, AbsState* as, const AbsArgs& a, const BatchView& bv, const uint8_t* role, const int64_t* vals,
-             const AbsCarry& cin, AbsCarry& cout, const int64_t* qv, int64_t nq_in, AbsQueue& qout, int64_t clock0,
-             int64_t lst0) {
+// The exact sequential pass (k_abs_seq) over rows [0, m) of a segment, from the carried state (pending partials, FIFO,
+// lastScheduledTime, clock) to the next; m = every row, or (min_rows > 0) the first row boundary after min_rows rows
+// where the closed form can take over again.  Returns m.
+static int64_t run_seq(SgHandle* h, AbsState* as, const AbsArgs& a, const BatchView& bv, const uint8_t* role,
+                       const int64_t* vals, const AbsCarry& cin, AbsCarry& cout, const int64_t* qv, int64_t nq_in,
+                       AbsQueue& qout, int64_t clock0, int64_t lst0, int64_t min_rows) {
   const sg_nfa_desc& d = h->desc;
   hipStream_t st = h->stream;
   const int64_t n = a.n, nc = a.nc, P = std::max<int64_t>(nc + n, 1);
   auto pow2 = [](int64_t x) { int64_t c = 1024; while (c < x) c <<= 1; return c; };
   int64_t qcap = pow2(2 * (nq_in + 2 * P) + 1024);
   const int64_t hcap = pow2(2 * P);
-  int64_t sc[8] = {};
+  int64_t sc[9] = {};
   SeqAbs s;
   memset(&s, 0, sizeof(s));
   s.n = n;
+  s.min_rows = min_rows;
   s.nc = nc;
   s.W = a.W;
   s.ts = bv.ts;
@@ -759,7 +807,7 @@ static void run_seq(SgHandle* h, AbsState* as, const AbsArgs& a, const BatchView
   s.erow = (uint32_t*)h->ws.get("sa_erow", 4 * P, st);
   s.ets = (int64_t*)h->ws.get("sa_ets", 8 * P, st);
   s.eg = (uint32_t*)h->ws.get("sa_eg", 4 * P, st);
-  s.sc = (int64_t*)h->ws.get("sa_sc", 64, st);
+  s.sc = (int64_t*)h->ws.get("sa_sc", 128, st);
   h->kbeg("abs_sequential");
   for (;;) {
     s.qcap = qcap;
@@ -767,9 +815,9 @@ static void run_seq(SgHandle* h, AbsState* as, const AbsArgs& a, const BatchView
     HIPCHK(hipMemsetAsync(s.hused, 0, hcap, st));
     const int64_t init[2] = {clock0, lst0};
     HIPCHK(hipMemcpyAsync(s.sc, init, 16, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_abs_seq, dim3(1), dim3(64), 0, st, s);
+    hipLaunchKernelGGL(k_abs_seq, dim3(1), dim3(64), 0, st, s);   // (one wave)
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(sc, s.sc, 64, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(sc, s.sc, sizeof(sc), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (!(sc[6] & 1)) break;
     if (qcap >= ((int64_t)1 << 34)) throw SgError(SG_ECAPACITY, "absence timer queue beyond 2^34 entries");
@@ -829,9 +877,7 @@ static void run_seq(SgHandle* h, AbsState* as, const AbsArgs& a, const BatchView
   h->mark(4);
   h->out.n += ne;
   h->split_out = 0;
-  h->last_events = n;
-  h->last_matches = ne;
-  h->last_spilled = 0;
+  return sc[8];
 }
 
 bool sg_every_absent_supported(const sg_nfa_desc& d) {
@@ -843,12 +889,13 @@ bool sg_every_absent_supported(const sg_nfa_desc& d) {
   return d.col_type[ca] == d.col_type[cb];
 }
 
-void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
+// One segment of a push: rows [0, m) of bv, m returned.  The closed form takes the rows up to the first one whose time
+// goes back (all of them when none does); from such a row -- or from the segment's start when the carried state is
+// not the closed form's -- the exact sequential pass takes over until the state is the closed form's again.
+// first: the stream's first rows (no clock, FIFO or lastScheduledTime before them); carry_in: the carried partials
+// are the segment's virtual rows; keep: write the carried state for what follows.
+static int64_t absent_segment(SgHandle* h, const BatchView& bv, int64_t n, bool first, bool carry_in, bool keep) {
   const sg_nfa_desc& d = h->desc;
-  if (!sg_every_absent_supported(d)) {
-    sg_run_general(h, bv, n);
-    return;
-  }
   hipStream_t st = h->stream;
   AbsState* as = astate(h);
   AbsCarry& cin = as->carry[as->cur];
@@ -857,7 +904,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   AbsArgs a;
   memset(&a, 0, sizeof(a));
   a.n = n;
-  a.nc = h->opt.no_carry ? 0 : cin.n;
+  a.nc = carry_in ? cin.n : 0;
   a.nt = a.nc + n;
   if (a.nt >= (1ll << 31)) throw SgError(SG_EINVAL, "batch plus pending partials exceed 2^31");
   a.W = d.states[b_state].waiting_time;
@@ -871,8 +918,8 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   a.prog_b_off = d.shape_prog_off;
   a.prog_b_len = d.shape_prog_len;
   a.has_stream = bv.stream ? 1 : 0;
-  a.first_push = h->pushes == 0 || h->opt.no_carry ? 1 : 0;
-  a.keep_carry = h->opt.no_carry ? 0 : 1;
+  a.first_push = first ? 1 : 0;
+  a.keep_carry = keep ? 1 : 0;
   a.fast = (a.s_a == 0 && a.s_b == 0 && a.col_a == a.col_b && !bv.stream && a.prog_a_len == 0 && a.prog_b_len == 0 &&
             !bv.cols.nul[a.col_a] && (a.type == SG_T_LONG || a.type == SG_T_INT || a.type == SG_T_STRING)) ? 1 : 0;
   const int64_t nt = a.nt;
@@ -913,10 +960,15 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   AbsQueue& qout = as->q[as->cur ^ 1];
   const int64_t nq_in = a.first_push ? 0 : qin.n;
   const int64_t lst0 = a.first_push ? 0 : as->lst;
-  if (oflag || (as->seq && !a.first_push)) {
-    // a timestamp goes back (or the state is not the closed form's): the exact sequential pass
-    run_seq(h, as, a, bv, role, vals, cin, cout, qin.v, nq_in, qout, clock0, lst0);
-    return;
+  const bool seq_state = as->seq && !a.first_push;
+  if (oflag != 0xffffffffu || seq_state) {
+    const int64_t p = seq_state ? 0 : (int64_t)oflag;
+    // the rows before the first late one are in order: the closed form takes them, carrying its state to the rest
+    if (p > 0) return absent_segment(h, sg_slice_view(d, bv, 0, p), p, first, carry_in, true);
+    // from a row whose time goes back (or a state the closed form cannot continue): the exact sequential pass, kept
+    // only as long as that state lasts
+    a.keep_carry = 1;
+    return run_seq(h, as, a, bv, role, vals, cin, cout, qin.v, nq_in, qout, clock0, lst0, SEQ_MIN_ROWS);
   }
   // ---- 2-4. sort by value, kill
   h->kbeg("abs_sort_kill");
@@ -965,7 +1017,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   }
   char* rec = h->out.reserve(n_emit, d.n_select, st);
   char* dst = rec + (size_t)h->out.n * o.stride;
-  if (!h->opt.no_carry) cout.reserve(n_carry, d.n_select);
+  if (a.keep_carry) cout.reserve(n_carry, d.n_select);
   uint32_t* slot_trig = (uint32_t*)h->ws.get("abs_slot_trig", 4 * (n_emit + 1), st);
   uint32_t* first_slot = (uint32_t*)h->ws.get("abs_first_slot", 4 * (n_emit + 1), st);
   h->kbeg("abs_write");
@@ -986,7 +1038,7 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
   h->kend();
   h->mark(4);
   h->out.n += n_emit;
-  if (!h->opt.no_carry) {
+  if (a.keep_carry) {
     // the scheduler's FIFO above the clock (kill and creation entries of the push's last W), lastScheduledTime
     int64_t tlast = clock0;
     if (n > 0) HIPCHK(hipMemcpyAsync(&tlast, bv.ts + (n - 1), 8, hipMemcpyDeviceToHost, st));
@@ -1013,10 +1065,27 @@ void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
     // entries overwrite it first
     as->lst = std::max(lst0, clock1 + a.W);
     cout.n = n_carry;
+    as->seq = false;
     as->cur ^= 1;
   }
+  return n;
+}
+
+void sg_run_every_absent(SgHandle* h, const BatchView& bv, int64_t n) {
+  const sg_nfa_desc& d = h->desc;
+  if (!sg_every_absent_supported(d)) {
+    sg_run_general(h, bv, n);
+    return;
+  }
+  const int64_t out0 = h->out.n;
+  const bool fresh = h->pushes == 0 || h->opt.no_carry;
+  int64_t lo = 0;
+  do {   // segments: closed form, then the sequential pass from a late row until the closed form can resume, ...
+    lo += absent_segment(h, sg_slice_view(d, bv, lo, n - lo), n - lo, lo == 0 && fresh,
+                         lo > 0 || !h->opt.no_carry, !h->opt.no_carry);
+  } while (lo < n);
   h->last_events = n;
-  h->last_matches = n_emit;
+  h->last_matches = h->out.n - out0;
   h->last_spilled = 0;
 }
 

@@ -462,7 +462,7 @@ static uint32_t general_key_bound(SgHandle* h, const BatchView& bv, int64_t n) {
 static void run_machine(SgHandle* h, const BatchView& bv, int64_t n);
 
 // rows [lo, lo + cnt) of a device batch view
-static BatchView slice_view(const sg_nfa_desc& d, const BatchView& bv, int64_t lo, int64_t cnt) {
+BatchView sg_slice_view(const sg_nfa_desc& d, const BatchView& bv, int64_t lo, int64_t cnt) {
   if (lo == 0 && cnt == bv.n) return bv;
   BatchView v = bv;
   v.n = cnt;
@@ -492,7 +492,7 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
       const int64_t room = sg_partial_max_rows(h, gs->pp);
       if (room < 1) throw SgError(SG_ECAPACITY, "partial-lane route: carried rows alone exceed the row budget");
       const int64_t cnt = std::min(n - lo, room);
-      if (!sg_partial_push(h, gs->pp, slice_view(h->desc, bv, lo, cnt), cnt, kb)) break;
+      if (!sg_partial_push(h, gs->pp, sg_slice_view(h->desc, bv, lo, cnt), cnt, kb)) break;
       lo += cnt;
     }
     if (lo == n) return;
@@ -500,7 +500,7 @@ void sg_run_general(SgHandle* h, const BatchView& bv, int64_t n) {
     // takes the stream from here, exactly
     if (sg_partial_carried(gs->pp)) throw SgError(SG_EUNSUPPORTED, "partial-lane route left with carried partials");
     sg_partial_deactivate(gs->pp);
-    run_machine(h, slice_view(h->desc, bv, lo, n - lo), n - lo);
+    run_machine(h, sg_slice_view(h->desc, bv, lo, n - lo), n - lo);
     return;
   }
   run_machine(h, bv, n);

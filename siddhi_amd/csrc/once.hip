@@ -103,11 +103,14 @@ struct SelPlan {
 };
 
 // keys: bind the e1 found in this push (its attributes are kept: a later push's match projects them); lo[k] = first
-// row that may complete the key's partial (NONE: none in this push)
+// row that may complete the key's partial (NONE: none in this push).  A push with a key beyond key_bound (*err, from
+// k_once_first) changes no key's state: every key gets lo = NONE, so the later passes do nothing, and the host raises
+// the error with the push's one end-of-push readback.
 __global__ void k_once_bind(OnceArgs a, SgCols bc, SelPlan sp, OnceState s, const uint32_t* __restrict__ first,
-                            uint32_t* __restrict__ lo) {
+                            uint32_t* __restrict__ lo, const uint32_t* __restrict__ err) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (int64_t)a.K) return;
+  if (*err) { lo[k] = NONE; return; }
   const uint8_t ph = s.phase[k];
   if (ph == 1) { lo[k] = 0; return; }
   if (ph != 0 || first[k] == NONE) { lo[k] = NONE; return; }
@@ -350,21 +353,17 @@ void sg_run_once(SgHandle* h, const BatchView& bv, int64_t n) {
   HIPCHK(hipMemsetAsync(cnt, 0, 8, st));
   const dim3 blk(256), gk((unsigned)((kb + 255) / 256));
   h->kbeg("once_match");
-  if (n > 0) {
-    hipLaunchKernelGGL(k_once_first, dim3(grid_rows(n)), blk, 0, st, a, s.phase, first, cnt + 1);
-    uint32_t kerr = 0;
-    HIPCHK(hipMemcpyAsync(&kerr, cnt + 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (kerr) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
-  }
-  hipLaunchKernelGGL(k_once_bind, gk, blk, 0, st, a, bv.cols, sp, s, first, lo);
+  if (n > 0) hipLaunchKernelGGL(k_once_first, dim3(grid_rows(n)), blk, 0, st, a, s.phase, first, cnt + 1);
+  hipLaunchKernelGGL(k_once_bind, gk, blk, 0, st, a, bv.cols, sp, s, first, lo, cnt + 1);
   if (n > 0) hipLaunchKernelGGL(k_once_second, dim3(grid_rows(n)), blk, 0, st, a, bv.cols, s, lo, hit, expd);
   hipLaunchKernelGGL(k_once_finish, gk, blk, 0, st, a, s, lo, hit, expd, cnt, prow, pkey);
   HIPCHK(hipGetLastError());
   h->kend();
-  uint32_t m = 0;
-  HIPCHK(hipMemcpyAsync(&m, cnt, 4, hipMemcpyDeviceToHost, st));
+  uint32_t hc[2] = {0, 0};   // matches, key-range error
+  HIPCHK(hipMemcpyAsync(hc, cnt, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (hc[1]) throw SgError(SG_EINVAL, "a partition key id is >= the batch's key_bound");
+  const uint32_t m = hc[0];
   h->mark(2);
   h->mark(3);
   if (m) {

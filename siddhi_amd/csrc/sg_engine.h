@@ -208,6 +208,7 @@ SlotPtrs sg_reserve_slot(SgHandle& h, const sg_batch* b, int64_t rows, int slot)
 BatchView sg_upload_to(const sg_nfa_desc& d, const SlotPtrs& p, const sg_batch* b, int64_t lo, int64_t cnt,
                        hipStream_t st);
 void sg_push_view(SgHandle& h, BatchView& bv, int64_t n);   // one push of rows in HBM (engine route + select)
+BatchView sg_slice_view(const sg_nfa_desc& d, const BatchView& bv, int64_t lo, int64_t cnt);   // rows [lo, lo + cnt)
 ColLayout sg_col_layout(const sg_nfa_desc& d, int64_t cap);
 // egress staging slot `slot` of h holds at least `bytes` (grows after the slot's last copy has read it; api.hip)
 void sg_stage_reserve(SgHandle& h, int slot, int64_t bytes);

@@ -78,3 +78,40 @@ def test_no_carry_handles_are_not_split():
     want = run_engine(OracleEngine, q, [b])
     got = run_engine(lambda ctx: GpuEngine(ctx, ingress_rows=10_000, no_carry=True), q, [b])
     assert_same(got, want)
+
+
+@pytest.mark.timeout(120)
+def test_once_key_beyond_key_bound_is_einval_and_changes_no_state():
+    """The once closed form (a non-`every` two-state pattern, csrc/once.hip) checks every row's key against the
+    batch's key_bound on the device and reports it with the push's end-of-push readback (no blocking
+    read in the middle of the push).  A push with such a key raises SG_EINVAL and leaves every key's runtime as it
+    was: the next, valid push binds its own e1 rows, none of the failed push's."""
+    from siddhi_amd import _native as N
+    from siddhi_amd import compiler as C
+    from siddhi_amd import lowering as L
+    q = ("define stream S (id long, symbol string, price float); partition with (symbol of S) begin @info(name='q') "
+         "from e1=S[price>20] -> e2=S[price>e1.price] select e1.id as a, e2.id as b insert into M; end;")
+    app = C.parse(q)
+    p = app.partitions[0]
+    h = N.Handle(N.build_desc(L.lower(L.make_context(app, p.queries[0], p, {}))), device=0)
+
+    def push(ids, keys, prices, key_bound):
+        keep = [ids, keys, prices]
+        ts = np.arange(len(ids), dtype=np.int64)
+        keep.append(ts)
+        b = N.make_batch(len(ids), int(ids[0]), ts.ctypes.data, 0, keys.ctypes.data,
+                         [ids.ctypes.data, keys.ctypes.data, prices.ctypes.data], [0, 0, 0], 0, key_bound, keep)
+        h.push(b)
+
+    try:
+        with pytest.raises(N.SgError) as ei:
+            push(np.array([100, 101, 102, 103], np.int64), np.array([0, 1, 7, 1], np.int32),
+                 np.array([25, 30, 40, 50], np.float32), 2)
+        assert ei.value.code == -1
+        assert h.pending() == 0
+        push(np.array([0, 1, 2, 3], np.int64), np.array([0, 1, 0, 1], np.int32),
+             np.array([21, 35, 22, 36], np.float32), 2)
+        tr, _, ky, _, vals, _ = h.poll(2)
+        assert sorted(map(tuple, vals.tolist())) == [(0, 2), (1, 3)]
+    finally:
+        h.close()

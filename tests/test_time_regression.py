@@ -167,3 +167,38 @@ def test_absence_closed_form_resumes():
     bs = [Batch(hi - lo, lo, ts[lo:hi], st[lo:hi], np.zeros(hi - lo, np.int32), [c[lo:hi] for c in cols], [None] * 3)
           for lo, hi in zip(cuts[:-1], cuts[1:])]
     check(synth.QUERIES["C4"], bs, L.SHAPE_EVERY_ABSENT_EQ)
+
+
+def _c4_late(n, ids, late_at, back_ms, pushes, seed=0):
+    """C4 rows at 1 row/ms with single rows pulled `back_ms` back at the positions `late_at` (and a block of 50
+    rows pulled back after the last position), a final Tick row, split into `pushes`"""
+    b = synth_batch("C4", 0, n, keys=ids, rate=1)
+    ts = b.ts.copy()
+    for p in late_at:
+        ts[p] -= back_ms
+    q = late_at[-1] + 3000
+    ts[q:q + 50] -= back_ms // 2
+    ts = np.append(ts, ts.max() + 5001)
+    st = np.append(b.stream, np.int32(1)).astype(np.int32)
+    cols = [np.append(b.cols[0], 0), np.append(b.cols[1], 0), np.append(b.cols[2], 0).astype(np.int32)]
+    m = n + 1
+    cuts = [m * p // pushes for p in range(pushes + 1)]
+    return [Batch(hi - lo, lo, ts[lo:hi], st[lo:hi], np.zeros(hi - lo, np.int32), [c[lo:hi] for c in cols], [None] * 3)
+            for lo, hi in zip(cuts[:-1], cuts[1:])]
+
+
+@pytest.mark.timeout(300)
+def test_absence_late_rows_inside_large_pushes():
+    """a late row used to send the whole push (and the pushes after it) through the one-lane sequential
+    pass.  Now the closed form takes the rows before it, the sequential pass (one wave) runs from it until the FIFO is
+    the closed form's again, and the closed form resumes inside the same push -- several times per push here (single
+    rows 2 s back, one 50-row block, a late row right at a push's start), row for row against the oracle"""
+    bs = _c4_late(120_000, 6000, [7_000, 31_000, 31_500, 60_000, 90_000], 2000, 2)
+    check(synth.QUERIES["C4"], bs, L.SHAPE_EVERY_ABSENT_EQ)
+
+
+@pytest.mark.timeout(300)
+def test_absence_late_rows_no_carry_single_push():
+    """the same stream as one no-carry push (end-of-stream mode): the segments still carry their state to each other"""
+    bs = _c4_late(100_000, 6000, [5_000, 40_000, 40_001, 70_000], 1500, 1)
+    check(synth.QUERIES["C4"], bs, L.SHAPE_EVERY_ABSENT_EQ, no_carry=True)
