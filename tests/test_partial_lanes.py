@@ -530,3 +530,49 @@ def test_gpu_bounded_lateness_keeps_the_carry_flat():
     assert_same(got2, want)
     assert flat[-1] <= 1.3 * flat[3], flat
     assert grow[-1] >= 2 * grow[3], grow
+
+
+def _rising_runs(n, keys, seed):
+    """C3b rows whose per-key v climbs in runs longer than e2's max count (5) and drops now and then, w constant but
+    for rare low values: every key keeps partials with e2 at each count 1..5 and the `e3 or e4` pair pending"""
+    rng = np.random.default_rng(seed)
+    key = rng.integers(0, keys, n)
+    cur = np.full(keys, 501)
+    v = np.empty(n, np.int32)
+    w = np.full(n, 50, np.int32)
+    for i in range(n):
+        k = key[i]
+        if rng.random() < 0.06:
+            cur[k] = 501 + int(rng.integers(0, 200))   # a drop: e3 (v < e1.v) for the partials started above it
+        else:
+            cur[k] += int(rng.integers(1, 4))
+        v[i] = cur[k]
+        if rng.random() < 0.03:
+            w[i] = 10                                   # e4 (w < e1.w)
+    ts = (synth.T0 + np.arange(n) // 4).astype(np.int64)
+    k32 = dense_first_seen(key.astype(np.int64)).astype(np.int32)
+    return Batch(n, 0, ts, np.zeros(n, np.int32), k32, [np.arange(n, dtype=np.int64), k32, v, w], [None] * 4)
+
+
+def test_seq_pool_at_its_bound_host():
+    """the small sequence geometry sizes its pool to elements + 1 (4 partials for C3b), on the argument
+    that each newAndEvery list holds at most one partial in SEQUENCE mode.  Rising runs keep every key's count state
+    at its maximum with the `or` pair pending the whole time; the host harness runs the same lane code (seq.h) and
+    must equal the oracle without a capacity error, across pushes."""
+    import ctypes as ct
+    q = synth.QUERIES["C3b"]
+    assert _load().hi_seq_rule(ct.byref(N.build_desc(L.lower(context(q))))) == 1
+    b = _rising_runs(24_000, 12, 3)
+    want = run_engine(OracleEngine, q, [b])
+    assert len(want) > 1000
+    assert_same(run_engine(lambda ctx: HostInterpEngine(ctx, pp=True), q, split(b, [5000, 5001, 17_000])), want)
+
+
+@pytest.mark.gpu
+def test_gpu_seq_pool_at_its_bound():
+    from siddhi_amd._native import GpuEngine
+    q = synth.QUERIES["C3b"]
+    b = _rising_runs(60_000, 40, 4)
+    want = run_engine(OracleEngine, q, [b])
+    assert len(want) > 1000
+    assert_same(run_engine(GpuEngine, q, split(b, [20_000, 20_001, 41_000])), want)
