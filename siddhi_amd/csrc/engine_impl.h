@@ -1640,25 +1640,42 @@ __global__ void __launch_bounds__(256) k_nge(Virt v, int64_t nt, int64_t within,
       if (!is_nan_val<T>(xp)) {
         uint32_t steps = 0;
         bool open = true;   // still pending when the scan reaches the end of the push
+        bool done = false;
         int64_t q = p + 1;
-        while (q < nt) {
-          if (++steps > NGE_MAX_SCAN) { atomicOr(&st_flags[1], 1u); open = false; break; }
+        while (q < nt && !done) {
           if ((q & 63) == 0 && q + 64 <= nt && !(has[q >> 6] && cmp_sel<OP, T>(op, best[q >> 6], xp)) &&
               bmax[q >> 6] <= tp + within && bmin[q >> 6] >= tp - within) {
+            if (++steps > NGE_MAX_SCAN) { atomicOr(&st_flags[1], 1u); open = false; break; }
             q += 64;                                                       // nothing in this block ends i
             continue;
           }
-          const int64_t tq = v_ts(v, (uint32_t)q);
-          if ((tq - tp > within || tp - tq > within) && v_visit(v, (uint32_t)q)) { open = false; break; }   // expired
-          if (v_flags(v, (uint32_t)q) & F_CONS) {
-            const T xq = v_val<T>(v, (uint32_t)q, false);
-            if (!is_nan_val<T>(xq) && cmp_sel<OP, T>(op, xq, xp)) {
-              if (q >= v.nc) j = (uint32_t)q;                             // (carried triggers were emitted before)
+          // the rows up to the next multiple of 8: every load issued before the first test (one memory latency per
+          // eight rows instead of one per row; most searches end within a few rows)
+          const int64_t ge = ((q & ~(int64_t)7) + 8) < nt ? (q & ~(int64_t)7) + 8 : nt;
+          int64_t tq[8];
+          uint32_t fq[8];
+          bool vq[8];
+          T xq[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int64_t r = q + u < ge ? q + u : ge - 1;
+            tq[u] = v_ts(v, (uint32_t)r);
+            fq[u] = v_flags(v, (uint32_t)r);
+            vq[u] = v_visit(v, (uint32_t)r);
+            xq[u] = v_val<T>(v, (uint32_t)r, false);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (done || q + u >= ge) continue;
+            if (++steps > NGE_MAX_SCAN) { atomicOr(&st_flags[1], 1u); open = false; done = true; continue; }
+            if ((tq[u] - tp > within || tp - tq[u] > within) && vq[u]) { open = false; done = true; continue; }   // expired
+            if ((fq[u] & F_CONS) && !is_nan_val<T>(xq[u]) && cmp_sel<OP, T>(op, xq[u], xp)) {
+              if (q + u >= v.nc) j = (uint32_t)(q + u);                    // (carried triggers were emitted before)
               open = false;
-              break;
+              done = true;
             }
           }
-          ++q;
+          q = ge;
         }
         if (open && alive) atomicOr(&alive[p >> 5], 1u << (p & 31));
       }
@@ -1874,7 +1891,7 @@ static bool run_nge(SgHandle* h, const BatchView& bv, int64_t n, int64_t nc, con
 
 // Pass 1 of the key partition beyond 256 key groups (up to 4096 groups of 2^pp.lb keys, e.g. C5's 1M keys): rows ->
 // narrow walker records grouped by key group, arrival order kept inside a group, in two LDS counting passes --
-// supergroups of 2^lbs groups (<= 256 of them, k_part1 with 32-bit staged keys), then the groups inside each
+// supergroups of 2^lbs groups (<= 64 of them, k_part1 with 32-bit staged keys), then the groups inside each
 // supergroup (k_part1b) straight into the group positions o1[g * ns1 + j] of the per-(group, segment) histogram.
 // Output: grec, glk (in-group key), o1.
 template <class T>
@@ -1891,9 +1908,11 @@ static void part1_wide(SgHandle* h, const PackFn<T, true>& pk, KeyOf kf, uint32_
     HIPCHK(rocprim::exclusive_scan(tp, b, in, outp, (uint32_t)0, cnt, rocprim::plus<uint32_t>(), st));
   };
   {
-    // two passes: supergroups of 2^lbs groups (<= 256 of them), then groups inside each supergroup
+    // two passes: supergroups of 2^lbs groups (<= 64 of them), then groups inside each supergroup.  (C5, 4096 groups,
+    // per 500M-row push: 256 supergroups part_group 7.7 + part_split 3.8 ms; 64 supergroups 6.0 + 4.2 ms -- pass 1's
+    // runs per supergroup are 4x longer; 32 supergroups 5.8 + 4.7 ms; profiles/r06/ab_lbs.sh)
     uint32_t lbs = 0;
-    while ((ng >> lbs) > 256u || ((ng + (1u << lbs) - 1) >> lbs) > 256u) ++lbs;
+    while (((ng + (1u << lbs) - 1) >> lbs) > 64u && lbs < 8) ++lbs;
     PartPlan pa2 = pp;
     pa2.lb = lb + lbs;
     pa2.ng = (kb + (1u << pa2.lb) - 1) >> pa2.lb;
