@@ -655,13 +655,17 @@ def whole_node_block(args, ws, local, dev):
 
 
 def node_child(args, G, thr):
-    """the whole-node pipeline with G shards on device 0, one step, in a child process with 4 x G hardware queues"""
+    """the whole-node pipeline with G shards on device 0, one step, in a child process with min(24, 8 G) hardware
+    queues up to G = 4, else 8 (a real node gives each GPU its own queues; on one device, per 1B events
+    (profiles/r06/ab_node_queues.sh): G = 2 609 ms at 16 queues (905 at 4), G = 4 644 ms at 24 / 748 at 16 / 890 at 8,
+    G = 8 1036 ms at 8 / 1358 at 16 / 2508 at 24 / 2642 at 32 -- its 32 streams oversubscribe the device's queues);
+    SG_NODE_CHILD_QUEUES overrides it"""
     cmd = [sys.executable, os.path.abspath(__file__), "--node-only", "--c5-node-steps", "1",
            "--c5-node-devices", ",".join(["0"] * G), "--node-threads", str(thr), "--node-shards", ""]
     if args.c5_events:
         cmd += ["--c5-events", str(args.c5_events)]
     env = {k: v for k, v in os.environ.items() if k not in TORCHRUN_ENV and not k.startswith("TORCHELASTIC")}
-    env["GPU_MAX_HW_QUEUES"] = str(min(32, 4 * G))
+    env["GPU_MAX_HW_QUEUES"] = os.environ.get("SG_NODE_CHILD_QUEUES", str(min(24, 8 * G) if G <= 4 else 8))
     try:
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
     except subprocess.TimeoutExpired:
