@@ -192,3 +192,44 @@ def test_gpu_range_partition_column_path_equals_oracle():
     want = run(OracleEngine, text, cols=cols)
     assert len(want) > 1000
     assert run(GpuEngine, text, cols=cols) == want
+
+
+ABSENT_APP = ("@app:playback define stream S (id long, price float); "
+              "partition with (price>=50 as 'hi' or price<10 as 'lo' of S) begin @info(name='q') "
+              "from every e1=S -> not S[id==e1.id] for 1 sec select e1.id as id insert into M; end;")
+
+
+def _absent_run(engine, rows):
+    rt = SiddhiManager(engine=engine).createSiddhiAppRuntime(ABSENT_APP)
+    got = []
+
+    class CB(QueryCallback):
+        def receive(self, ts, ins, rem):
+            got.extend((ts, tuple(e.data)) for e in ins)
+
+    rt.addCallback("q", CB())
+    h = rt.getInputHandler("S")
+    for t, r in rows:
+        h.send(t, list(r))
+    rt.flush()
+    rt.shutdown()
+    return got
+
+
+def test_row_in_no_range_still_moves_the_playback_clock():
+    """InputHandler.send sets the app's time before the partition receiver drops a row no range holds
+    (C/stream/input/InputHandler.java:57-65): rows at 500 and 1600 in no range fire the 'hi' instance's timer"""
+    assert _absent_run(OracleEngine, [(0, (1, 60.0)), (500, (2, 30.0)), (1600, (3, 30.0))]) == [(1000, (1,))]
+
+
+@pytest.mark.gpu
+def test_gpu_range_partition_absence_with_clock_rows():
+    from siddhi_amd._native import GpuEngine
+    rng = np.random.default_rng(11)
+    rows, t = [], 0
+    for i in range(4000):
+        t += int(rng.integers(0, 300))
+        rows.append((t, (int(rng.integers(0, 50)), float(rng.choice([5.0, 30.0, 70.0])))))
+    want = _absent_run(OracleEngine, rows)
+    assert len(want) > 100
+    assert _absent_run(GpuEngine, rows) == want
