@@ -509,10 +509,13 @@ __global__ void __launch_bounds__(64) k_abs_seq(SeqAbs s) {
   bool cap_bad = false;
   const int64_t qmask = s.qcap - 1, hmask = s.hcap - 1;
   // (every lane runs the uniform work with the same values: the stores repeat the same word, and each lane reads
-  // back only what it stored itself)
+  // back only what it stored itself.  Values the wave keeps in registers instead of re-reading: the FIFO head `qh`,
+  // the last partial block's earliest deadline `lbm`, the next row's inputs.)
+  int64_t qh = INF;   // ring[head] while head < tail
   auto qpush = [&](int64_t v) {
     if (tail - head >= s.qcap) { cap_bad = true; return; }
     s.ring[tail & qmask] = v;
+    if (tail == head) qh = v;
     ++tail;
   };
   auto hslot = [&](int64_t key, bool insert) -> int64_t {
@@ -531,19 +534,28 @@ __global__ void __launch_bounds__(64) k_abs_seq(SeqAbs s) {
     cap_bad = true;
     return -1;
   };
-  auto add_partial = [&](int64_t d, uint32_t src, bool killable, int64_t key) {
+  int64_t lbb = -1, lbm = INF;   // the last partial block and its earliest deadline (as stored in bmin)
+  // h_known >= 0: the value's hash slot, found by this row's kill, whose list the kill just emptied
+  auto add_partial = [&](int64_t d, uint32_t src, bool killable, int64_t key, int64_t h_known) {
     const int64_t k = np++;
     s.pd[k] = d;
     s.psrc[k] = src;
     s.palive[k] = 1;
     s.pnext[k] = -1;
     const int64_t b = k >> 6;
-    if ((k & 63) == 0) s.bmin[b] = d;
-    else if (d < s.bmin[b]) s.bmin[b] = d;
+    if (b != lbb) { lbb = b; lbm = d; }
+    else if (d < lbm) lbm = d;
+    s.bmin[b] = lbm;
     if (killable) {
+      if (h_known >= 0) {
+        s.hhead[h_known] = (int32_t)k;
+        s.htail[h_known] = (int32_t)k;
+        return;
+      }
       const int64_t h = hslot(key, true);
       if (h < 0) return;
-      if (s.htail[h] < 0) s.hhead[h] = (int32_t)k; else s.pnext[s.htail[h]] = (int32_t)k;
+      const int32_t tl = s.htail[h];
+      if (tl < 0) s.hhead[h] = (int32_t)k; else s.pnext[tl] = (int32_t)k;
       s.htail[h] = (int32_t)k;
     }
   };
@@ -552,39 +564,50 @@ __global__ void __launch_bounds__(64) k_abs_seq(SeqAbs s) {
   auto pass = [&](int64_t T, uint32_t row) -> bool {   // one timer pass; true if it emitted
     bool any = false;
     const int64_t nb = (np + 63) >> 6;
-    for (;;) {   // skip the leading blocks with nothing alive
-      const int64_t b = lob + lane;
-      const uint64_t live = __ballot(!(b < nb && s.bmin[b] == INF));
-      if (live) { lob += __builtin_ctzll(live); break; }
-      lob += 64;
-    }
-    for (int64_t b0 = lob; b0 < nb; b0 += 64) {
-      const int64_t b = b0 + lane;
-      uint64_t cm = __ballot(b < nb && s.bmin[b] <= T);
-      while (cm) {
-        const int64_t bb = b0 + __builtin_ctzll(cm);
-        cm &= cm - 1;
-        const int64_t k = bb * 64 + lane;
-        const bool al = k < np && s.palive[k];
-        const int64_t d = al ? s.pd[k] : INF;
-        const bool em = al && d <= T;
-        const uint64_t emm = __ballot(em);
-        const int64_t rest = sa_wave_min(em ? INF : d);
-        if (emm) {
-          if (row != cur_row) { cur_row = row; grp = 0; }
-          const uint32_t below = (uint32_t)__popcll(emm & lt), cnt = (uint32_t)__popcll(emm);
-          if (em) {
-            s.palive[k] = 0;
-            const int64_t slot = ne + below;
-            if (slot < s.ecap) { s.ek[slot] = (uint32_t)k; s.erow[slot] = row; s.ets[slot] = T; s.eg[slot] = grp + below; }
-          }
-          if (ne + cnt > s.ecap) cap_bad = true;
-          ne += cnt;
-          grp += cnt;
-          any = true;
-          __threadfence_block();   // (a later kill reads these flags on every lane)
+    bool lead = true;   // still skipping leading blocks with nothing alive
+    for (int64_t b0 = lob; b0 < nb; b0 += 256) {
+      int64_t bm[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {   // 256 blocks' earliest deadlines per memory round trip
+        const int64_t b = b0 + 64 * u + lane;
+        bm[u] = b < nb ? s.bmin[b] : INF;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t bu = b0 + 64 * u;
+        if (bu >= nb) break;
+        if (lead) {
+          const uint64_t live = __ballot(!(bu + lane < nb && bm[u] == INF));
+          if (live) { lob = bu + __builtin_ctzll(live); lead = false; }
+          else lob = bu + 64;
         }
-        s.bmin[bb] = rest;
+        uint64_t cm = __ballot(bu + lane < nb && bm[u] <= T);
+        while (cm) {
+          const int64_t bb = bu + __builtin_ctzll(cm);
+          cm &= cm - 1;
+          const int64_t k = bb * 64 + lane;
+          const bool al = k < np && s.palive[k];
+          const int64_t d = al ? s.pd[k] : INF;
+          const bool em = al && d <= T;
+          const uint64_t emm = __ballot(em);
+          const int64_t rest = sa_wave_min(em ? INF : d);
+          if (emm) {
+            if (row != cur_row) { cur_row = row; grp = 0; }
+            const uint32_t below = (uint32_t)__popcll(emm & lt), cnt = (uint32_t)__popcll(emm);
+            if (em) {
+              s.palive[k] = 0;
+              const int64_t slot = ne + below;
+              if (slot < s.ecap) { s.ek[slot] = (uint32_t)k; s.erow[slot] = row; s.ets[slot] = T; s.eg[slot] = grp + below; }
+            }
+            if (ne + cnt > s.ecap) cap_bad = true;
+            ne += cnt;
+            grp += cnt;
+            any = true;
+            __threadfence_block();   // (a later kill reads these flags on every lane)
+          }
+          s.bmin[bb] = rest;
+          if (bb == lbb) lbm = rest;
+        }
       }
     }
     return any;
@@ -605,18 +628,26 @@ __global__ void __launch_bounds__(64) k_abs_seq(SeqAbs s) {
   for (int64_t k = 0; k < s.nq_in; ++k) qpush(s.q_in[k]);
   for (int64_t k = 0; k < s.nc; ++k) {
     const uint8_t r = s.role[k];
-    add_partial(s.c_dl[k], (uint32_t)k, (r & R_SORT) != 0, s.vals[k]);
+    add_partial(s.c_dl[k], (uint32_t)k, (r & R_SORT) != 0, s.vals[k], -1);
   }
   int64_t i = 0;
   bool ok = false;
+  // row i's inputs, loaded one row ahead (the inputs are never written here)
+  int64_t tn = 0, xn = 0;
+  uint8_t rn = 0;
+  if (s.n > 0) { tn = s.ts[0]; rn = s.role[s.nc]; xn = s.vals[s.nc]; }
   for (; i < s.n && !cap_bad; ++i) {
     if (s.min_rows > 0 && i >= s.min_rows && (i & 1023) == 0 && fifo_ok()) { ok = true; break; }
-    const int64_t t = s.ts[i];
+    const int64_t t = tn;
+    const uint8_t r = rn;
+    const int64_t x = xn;
+    if (i + 1 < s.n) { tn = s.ts[i + 1]; rn = s.role[s.nc + i + 1]; xn = s.vals[s.nc + i + 1]; }
     if (t >= clock) {
       clock = t;
-      while (head < tail && s.ring[head & qmask] <= clock && !cap_bad) {
-        const int64_t T = s.ring[head & qmask];
+      while (head < tail && qh <= clock && !cap_bad) {
+        const int64_t T = qh;
         ++head;
+        qh = head < tail ? s.ring[head & qmask] : INF;
         const bool emitted = pass(T, (uint32_t)i);
         if (clock > s.W + T) lst = clock + s.W;
         if (!emitted && lst < T) {
@@ -626,9 +657,9 @@ __global__ void __launch_bounds__(64) k_abs_seq(SeqAbs s) {
       }
     }
     const int64_t v = s.nc + i;
-    const uint8_t r = s.role[v];
+    int64_t h_known = -1;
     if (r & R_KILL) {
-      const int64_t h = hslot(s.vals[v], false);
+      const int64_t h = hslot(x, false);
       if (h >= 0) {
         for (int32_t k = s.hhead[h]; k >= 0; k = s.pnext[k]) {
           if (!s.palive[k]) continue;
@@ -638,10 +669,12 @@ __global__ void __launch_bounds__(64) k_abs_seq(SeqAbs s) {
         }
         s.hhead[h] = -1;
         s.htail[h] = -1;
+        h_known = h;
       }
     }
     if (r & R_CAND) {
-      add_partial(t + s.W, (uint32_t)v, (r & R_SORT) != 0, s.vals[v]);
+      // (a row's kill and candidate read the same value: one compared value per row, sg_every_absent_supported)
+      add_partial(t + s.W, (uint32_t)v, (r & R_SORT) != 0, x, h_known);
       lst = t + s.W;
       qpush(lst);
     }
