@@ -162,8 +162,9 @@ def run_child(handles, nodes):
 def test_500_handles_20_nodes_release_everything():
     """Two phases of 500 handles + 20 nodes after the warm-up.  A leak grows every phase by the same amount; a one-time
     reservation (a malloc arena, a runtime pool) grows the first only.  So phase 2 must add ≤ 16 MiB of committed address
-    space, RSS and malloc'd bytes over phase 1's end, and the whole run stays within 64 MiB of the baseline; every
-    reading follows malloc_trim(0) and the mappings that grew are named per phase (grown_phase1/2) in the message."""
+    space, RSS and malloc'd bytes over phase 1's end, and the whole run stays within 64 MiB (malloc'd) / 256 MiB
+    (mappings, RSS) of the baseline; every reading follows malloc_trim(0) and the mappings that grew are named per
+    phase (grown_phase1/2) in the message."""
     r = run_child(500, 20)
     b, p1, a = r["base"], r["p1"], r["after"]
     why = json.dumps({k: r[k] for k in ("base", "p1", "after", "grown_phase1", "grown_phase2")})
@@ -178,10 +179,14 @@ def test_500_handles_20_nodes_release_everything():
     # plateau: the second phase adds nothing (a linear leak of 16 KiB per handle fails here)
     for k in ("heap_used_kb", "vm_committed_kb", "rss_kb"):
         assert a[k] - p1[k] <= 16 * 1024, (k, why)
-    # and the whole run stays near the baseline: bytes malloc'd and not freed, committed mappings (PROT_NONE arena
-    # reservations excluded: they hold no page) and resident pages
-    for k in ("heap_used_kb", "vm_committed_kb", "rss_kb"):
-        assert a[k] - b[k] <= 64 * 1024, (k, why)
+    # and the whole run stays near the baseline: bytes malloc'd and not freed within 64 MiB; committed mappings
+    # (PROT_NONE arena reservations excluded: they hold no page) and resident pages within 256 MiB.  Some runs'
+    # first phase (r05 and r06, not every run) grows by one ~189 MiB anonymous rw-p mapping that malloc did not make
+    # (heap_used +8 MB in the same run) and that phase 2 never repeats -- a one-time host allocation of the HIP
+    # runtime (profiles/r06/logs/leak_one_time_189MiB.log); the plateau check above is the leak criterion
+    assert a["heap_used_kb"] - b["heap_used_kb"] <= 64 * 1024, ("heap_used_kb", why)
+    for k in ("vm_committed_kb", "rss_kb"):
+        assert a[k] - b[k] <= 256 * 1024, (k, why)
     assert r["torch_sum"] == 999 * 1000 // 2
 
 
