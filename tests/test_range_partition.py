@@ -233,3 +233,83 @@ def test_gpu_range_partition_absence_with_clock_rows():
     want = _absent_run(OracleEngine, rows)
     assert len(want) > 100
     assert _absent_run(GpuEngine, rows) == want
+
+
+@pytest.mark.gpu
+def test_gpu_range_partition_snapshot_restore():
+    """persist half-way through a range-partitioned stream and restore into a fresh runtime: the labels' instances
+    (their dense ids and per-key state) come back and the rest of the stream gives the uninterrupted run's rows"""
+    from siddhi_amd._native import GpuEngine
+    rows = _random_rows(6000, 21)
+    text = app(within="within 1 sec")
+
+    def make():
+        rt = SiddhiManager(engine=GpuEngine).createSiddhiAppRuntime(text)
+        got = []
+
+        class CB(QueryCallback):
+            def receive(self, ts, ins, rem):
+                got.extend(tuple(e.data) for e in ins)
+
+        rt.addCallback("q", CB())
+        rt.start()
+        return rt, got
+
+    def send(rt, lo, hi):
+        h = rt.getInputHandler("S")
+        for t, r in rows[lo:hi]:
+            h.send(t, list(r))
+        rt.flush()
+
+    rt, whole = make()
+    send(rt, 0, len(rows))
+    rt.shutdown()
+    rt1, p1 = make()
+    send(rt1, 0, 2500)
+    blob = rt1.snapshot()
+    rt1.shutdown()
+    rt2, p2 = make()
+    rt2.restore(blob)
+    send(rt2, 2500, len(rows))
+    rt2.shutdown()
+    assert len(whole) > 200
+    assert p1 + p2 == whole
+    assert whole == run(OracleEngine, text, rows)
+
+
+@pytest.mark.gpu
+def test_gpu_value_and_range_partition_two_streams():
+    """one partition keyed by value on one stream and by ranges on the other (PartitionTestCase's mixed form):
+    a T row reaches the instance of every range it holds, an S row its symbol's instance"""
+    from siddhi_amd._native import GpuEngine
+    text = ("define stream S (k string, price float); define stream T (k string, v float); "
+            "partition with (k of S, v>=50 as 'A' or v<50 as 'B' or v<20 as 'C' of T) begin @info(name='q') "
+            "from every e1=S[price>10] -> e2=T[v>e1.price] within 2 sec select e1.price as p, e2.v as v "
+            "insert into M; end;")
+    rng = np.random.default_rng(5)
+
+    def go(engine):
+        rt = SiddhiManager(engine=engine).createSiddhiAppRuntime(text)
+        got = []
+
+        class CB(QueryCallback):
+            def receive(self, ts, ins, rem):
+                got.extend(tuple(e.data) for e in ins)
+
+        rt.addCallback("q", CB())
+        s, t = rt.getInputHandler("S"), rt.getInputHandler("T")
+        r2 = np.random.default_rng(5)
+        ts = 0
+        for i in range(5000):
+            ts += int(r2.integers(0, 30))
+            if r2.random() < 0.5:
+                s.send(ts, [["A", "B", "C"][int(r2.integers(0, 3))], float(r2.integers(0, 100))])
+            else:
+                t.send(ts, ["x", float(r2.integers(0, 100))])
+            if i % 1000 == 999:
+                rt.flush()
+        rt.shutdown()
+        return got
+    want = go(OracleEngine)
+    assert len(want) > 100
+    assert go(GpuEngine) == want
