@@ -93,3 +93,20 @@ def test_select_e2_value_only_and_constants():
     """selects of e2's compared value and e1's payload only"""
     b = batch()
     same(query(select="e2.price as p2, e1.id as i1"), [b])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("typ", ["double", "long", "int"])
+def test_compared_value_types(typ):
+    """the walker's other instantiations: the compared attribute as DOUBLE, LONG and INT (integer prices: ties)"""
+    b = batch()
+    price = b.cols[2]
+    if typ == "double":
+        b.cols[2] = price.astype(np.float64) + 1e-9 * (np.arange(b.n) % 7)
+    else:
+        b.cols[2] = np.round(price).astype(np.int64 if typ == "long" else np.int32)
+    q = ("define stream StockStream (id long, symbol string, price " + typ + "); "
+         "partition with (symbol of StockStream) begin @info(name='q') "
+         "from every e1=StockStream[price>20] -> e2=StockStream[price > e1.price] within 1 sec "
+         "select e1.id as id1, e2.id as id2, e1.price as p1, e2.price as p2 insert into M; end;")
+    same(q, pieces(b, [900_000]))
